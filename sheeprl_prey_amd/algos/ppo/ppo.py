@@ -1,0 +1,257 @@
+"""PPO, coupled (reference: ``sheeprl/algos/ppo/ppo.py:32-459``).
+
+Every rank runs ``env.num_envs`` envs, fills a device-resident rollout buffer, computes GAE
+with the HIP reverse-scan kernel, optionally all-gathers the rollouts (``buffer.share_data``),
+and runs ``update_epochs`` x minibatch SGD; gradients are averaged with one RCCL all-reduce of
+the optimiser's flat slab per step.
+"""
+from __future__ import annotations
+
+import copy
+import os
+from typing import Any, Dict
+
+import numpy as np
+import torch
+
+from sheeprl_prey_amd.algos.common import (
+    PolynomialLR,
+    action_info,
+    build_envs,
+    check_obs_keys,
+    episode_stats,
+    load_resume,
+    log_throughput,
+    setup_logger,
+    warn_log_ckpt_every,
+)
+from sheeprl_prey_amd.algos.ppo.agent import PPOAgent
+from sheeprl_prey_amd.algos.ppo.loss import entropy_loss, policy_loss, value_loss
+from sheeprl_prey_amd.algos.ppo.utils import test
+from sheeprl_prey_amd.data.buffers import ReplayBuffer
+from sheeprl_prey_amd.data.tensordict import TensorDict
+from sheeprl_prey_amd.parallel.flat_optim import build_optimizer
+from sheeprl_prey_amd.utils.metric import MeanMetric, MetricAggregator
+from sheeprl_prey_amd.utils.registry import register_algorithm
+from sheeprl_prey_amd.utils.timer import timer
+from sheeprl_prey_amd.utils.utils import gae, normalize_tensor, polynomial_decay
+
+
+def shard_indices(n: int, runner, shuffle: bool, seed: int, epoch: int) -> torch.Tensor:
+    """DistributedSampler semantics: a seeded permutation, padded to a multiple of world, strided."""
+    g = torch.Generator().manual_seed(seed + epoch)
+    idx = torch.randperm(n, generator=g) if shuffle else torch.arange(n)
+    ws, rk = runner.world_size, runner.global_rank
+    total = ((n + ws - 1) // ws) * ws
+    if total > n:
+        idx = torch.cat([idx, idx[: total - n]])
+    return idx[rk:total:ws]
+
+
+def train(runner, agent, optimizer, data: TensorDict, aggregator: MetricAggregator, cfg: Dict[str, Any]) -> None:
+    n = data.shape[0]
+    obs_keys = list(cfg.mlp_keys.encoder) + list(cfg.cnn_keys.encoder)
+    for epoch in range(cfg.algo.update_epochs):
+        if cfg.buffer.share_data and runner.world_size > 1:
+            idx = shard_indices(n, runner, True, cfg.seed, epoch)
+        else:
+            idx = torch.randperm(n)
+        idx = idx.to(data["rewards"].device)
+        for start in range(0, len(idx), cfg.per_rank_batch_size):
+            batch = data[idx[start : start + cfg.per_rank_batch_size]]
+            obs = {k: batch[k] / 255 - 0.5 if k in cfg.cnn_keys.encoder else batch[k] for k in obs_keys}
+            _, logprobs, entropy, new_values = agent(obs, torch.split(batch["actions"], agent.actions_dim, dim=-1))
+            adv = batch["advantages"]
+            if cfg.algo.normalize_advantages:
+                adv = normalize_tensor(adv)
+            pg_loss = policy_loss(logprobs, batch["logprobs"], adv, cfg.algo.clip_coef, cfg.algo.loss_reduction)
+            v_loss = value_loss(new_values, batch["values"], batch["returns"], cfg.algo.clip_coef, cfg.algo.clip_vloss,
+                                cfg.algo.loss_reduction)
+            ent_loss = entropy_loss(entropy, cfg.algo.loss_reduction)
+            loss = pg_loss + cfg.algo.vf_coef * v_loss + cfg.algo.ent_coef * ent_loss
+            optimizer.zero_grad(set_to_none=True)
+            runner.backward(loss, optimizer)
+            if cfg.algo.max_grad_norm > 0.0:
+                runner.clip_gradients(agent, optimizer, max_norm=cfg.algo.max_grad_norm)
+            optimizer.step()
+            aggregator.update("Loss/policy_loss", pg_loss.detach())
+            aggregator.update("Loss/value_loss", v_loss.detach())
+            aggregator.update("Loss/entropy_loss", ent_loss.detach())
+
+
+@register_algorithm()
+def main(runner, cfg: Dict[str, Any]):
+    cfg, state = load_resume(runner, cfg)
+    initial_ent_coef = copy.deepcopy(cfg.algo.ent_coef)
+    initial_clip_coef = copy.deepcopy(cfg.algo.clip_coef)
+    device = runner.device
+    rank, world_size = runner.global_rank, runner.world_size
+    runner.seed_everything(cfg.seed + rank)
+
+    logger, log_dir = setup_logger(runner, cfg)
+    envs = build_envs(runner, cfg, log_dir)
+    observation_space = envs.single_observation_space
+    check_obs_keys(cfg, observation_space)
+    runner.print("Encoder CNN keys:", cfg.cnn_keys.encoder)
+    runner.print("Encoder MLP keys:", cfg.mlp_keys.encoder)
+    obs_keys = list(cfg.cnn_keys.encoder) + list(cfg.mlp_keys.encoder)
+    is_continuous, _, actions_dim = action_info(envs.single_action_space)
+
+    agent = PPOAgent(actions_dim, observation_space, cfg.algo.encoder, cfg.algo.actor, cfg.algo.critic,
+                     cfg.cnn_keys.encoder, cfg.mlp_keys.encoder, cfg.env.screen_size, cfg.distribution, is_continuous)
+    if state:
+        agent.load_state_dict(state["agent"])
+    agent = runner.setup_module(agent)
+    optimizer = build_optimizer(cfg.algo.optimizer, agent.parameters())
+    if state:
+        optimizer.load_state_dict(state["optimizer"])
+
+    aggregator = MetricAggregator({
+        "Rewards/rew_avg": MeanMetric(sync_on_compute=cfg.metric.sync_on_compute),
+        "Game/ep_len_avg": MeanMetric(sync_on_compute=cfg.metric.sync_on_compute),
+        "Loss/value_loss": MeanMetric(sync_on_compute=cfg.metric.sync_on_compute),
+        "Loss/policy_loss": MeanMetric(sync_on_compute=cfg.metric.sync_on_compute),
+        "Loss/entropy_loss": MeanMetric(sync_on_compute=cfg.metric.sync_on_compute),
+    })
+
+    if cfg.buffer.size < cfg.algo.rollout_steps:
+        raise ValueError(f"The size of the buffer ({cfg.buffer.size}) cannot be lower than the rollout steps ({cfg.algo.rollout_steps})")
+    rb = ReplayBuffer(cfg.buffer.size, cfg.env.num_envs, device=device, memmap=cfg.buffer.memmap and device.type == "cpu",
+                      memmap_dir=os.path.join(log_dir, "memmap_buffer", f"rank_{rank}"), obs_keys=obs_keys)
+    step_data = TensorDict({}, batch_size=[cfg.env.num_envs], device=device)
+
+    last_train = 0
+    train_step = 0
+    start_step = state["update"] // world_size if state else 1
+    policy_step = state["update"] * cfg.env.num_envs * cfg.algo.rollout_steps if state else 0
+    last_log = state["last_log"] if state else 0
+    last_checkpoint = state["last_checkpoint"] if state else 0
+    policy_steps_per_update = int(cfg.env.num_envs * cfg.algo.rollout_steps * world_size)
+    num_updates = cfg.total_steps // policy_steps_per_update if not cfg.dry_run else 1
+    warn_log_ckpt_every(cfg, policy_steps_per_update)
+
+    scheduler = None
+    if cfg.algo.anneal_lr:
+        scheduler = PolynomialLR(optimizer, total_iters=num_updates, power=1.0)
+        if state and state.get("scheduler"):
+            scheduler.load_state_dict(state["scheduler"])
+
+    o = envs.reset(seed=cfg.seed)[0]
+    next_obs = {}
+    for k in obs_keys:
+        t = torch.as_tensor(o[k]).to(device)
+        if k in cfg.cnn_keys.encoder:
+            t = t.view(cfg.env.num_envs, -1, *t.shape[-2:])
+        else:
+            t = t.float()
+        step_data[k] = t
+        next_obs[k] = t
+
+    for update in range(start_step, num_updates + 1):
+        for _ in range(cfg.algo.rollout_steps):
+            policy_step += cfg.env.num_envs * world_size
+            with timer("Time/env_interaction_time"):
+                with torch.no_grad():
+                    nobs = {k: next_obs[k] / 255 - 0.5 if k in cfg.cnn_keys.encoder else next_obs[k] for k in obs_keys}
+                    actions, logprobs, _, values = agent(nobs)
+                    if is_continuous:
+                        real_actions = torch.cat(actions, -1).cpu().numpy()
+                    else:
+                        real_actions = np.stack([a.argmax(dim=-1).cpu().numpy() for a in actions], axis=-1)
+                    actions = torch.cat(actions, -1)
+                o, rewards, dones, truncated, info = envs.step(real_actions.reshape(envs.action_space.shape))
+                truncated_envs = np.nonzero(truncated)[0]
+                if len(truncated_envs) > 0:
+                    # bootstrap truncated episodes with V(final_observation)
+                    real_next = {}
+                    for k in obs_keys:
+                        vals = np.stack([np.asarray(info["final_observation"][e][k]) for e in truncated_envs])
+                        tv = torch.as_tensor(vals, dtype=torch.float32, device=device)
+                        if k in cfg.cnn_keys.encoder:
+                            tv = tv.view(len(truncated_envs), -1, *tv.shape[-2:]) / 255.0 - 0.5
+                        real_next[k] = tv
+                    with torch.no_grad():
+                        v = agent.get_value(real_next).cpu().numpy()
+                    rewards[truncated_envs] += v.reshape(rewards[truncated_envs].shape)
+                dones = np.logical_or(dones, truncated)
+                dones = torch.as_tensor(dones, dtype=torch.float32, device=device).view(cfg.env.num_envs, -1)
+                rewards = torch.as_tensor(rewards, dtype=torch.float32, device=device).view(cfg.env.num_envs, -1)
+
+            step_data["dones"] = dones
+            step_data["values"] = values
+            step_data["actions"] = actions
+            step_data["logprobs"] = logprobs
+            step_data["rewards"] = rewards
+            step_data["returns"] = torch.zeros_like(rewards)
+            step_data["advantages"] = torch.zeros_like(rewards)
+            rb.add(step_data.unsqueeze(0))
+
+            next_obs = {}
+            for k in obs_keys:
+                if k in cfg.cnn_keys.encoder:
+                    t = torch.as_tensor(o[k], device=device)
+                    t = t.view(cfg.env.num_envs, -1, *t.shape[-2:])
+                else:
+                    t = torch.as_tensor(o[k], device=device, dtype=torch.float32)
+                step_data[k] = t
+                next_obs[k] = t
+
+            for i, ep_rew, ep_len in episode_stats(info):
+                aggregator.update("Rewards/rew_avg", ep_rew)
+                aggregator.update("Game/ep_len_avg", ep_len)
+                runner.print(f"Rank-0: policy_step={policy_step}, reward_env_{i}={ep_rew[-1]}")
+
+        with torch.no_grad():
+            nobs = {k: next_obs[k] / 255 - 0.5 if k in cfg.cnn_keys.encoder else next_obs[k] for k in obs_keys}
+            next_values = agent.get_value(nobs)
+            returns, advantages = gae(rb["rewards"], rb["values"], rb["dones"], next_values, cfg.algo.rollout_steps,
+                                      cfg.algo.gamma, cfg.algo.gae_lambda)
+            rb["returns"] = returns.float()
+            rb["advantages"] = advantages.float()
+
+        local_data = rb.buffer.view(-1)
+        if cfg.buffer.share_data and world_size > 1:
+            gathered = runner.all_gather(local_data.to_dict())
+            n = next(iter(gathered.values())).shape[0] * local_data.shape[0]
+            local_data = TensorDict({k: v.reshape(n, *v.shape[2:]) for k, v in gathered.items()}, batch_size=[n])
+        with timer("Time/train_time"):
+            train(runner, agent, optimizer, local_data, aggregator, cfg)
+        train_step += world_size
+
+        if cfg.algo.anneal_lr:
+            runner.log("Info/learning_rate", scheduler.get_last_lr()[0], policy_step)
+            scheduler.step()
+        else:
+            runner.log("Info/learning_rate", cfg.algo.optimizer.lr, policy_step)
+        runner.log("Info/clip_coef", cfg.algo.clip_coef, policy_step)
+        if cfg.algo.anneal_clip_coef:
+            cfg.algo.clip_coef = polynomial_decay(update, initial=initial_clip_coef, final=0.0, max_decay_steps=num_updates)
+        runner.log("Info/ent_coef", cfg.algo.ent_coef, policy_step)
+        if cfg.algo.anneal_ent_coef:
+            cfg.algo.ent_coef = polynomial_decay(update, initial=initial_ent_coef, final=0.0, max_decay_steps=num_updates)
+
+        if policy_step - last_log >= cfg.metric.log_every or update == num_updates or cfg.dry_run:
+            runner.log_dict(aggregator.compute(), policy_step)
+            aggregator.reset()
+            log_throughput(runner, timer.compute(), policy_step, last_log, train_step, last_train, cfg.env.action_repeat)
+            timer.reset()
+            last_log = policy_step
+            last_train = train_step
+
+        if (cfg.checkpoint.every > 0 and policy_step - last_checkpoint >= cfg.checkpoint.every) or cfg.dry_run or update == num_updates:
+            last_checkpoint = policy_step
+            ckpt_state = {
+                "agent": agent.state_dict(),
+                "optimizer": optimizer.state_dict(),
+                "scheduler": scheduler.state_dict() if scheduler is not None else None,
+                "update": update * world_size,
+                "batch_size": cfg.per_rank_batch_size * world_size,
+                "last_log": last_log,
+                "last_checkpoint": last_checkpoint,
+            }
+            ckpt_path = os.path.join(log_dir, f"checkpoint/ckpt_{policy_step}_{rank}.ckpt")
+            runner.call("on_checkpoint_coupled", ckpt_path=ckpt_path, state=ckpt_state)
+
+    envs.close()
+    if runner.is_global_zero:
+        test(agent, runner, cfg, log_dir)

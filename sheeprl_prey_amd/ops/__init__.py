@@ -1,0 +1,357 @@
+"""Fused ops: HIP kernels on GPU tensors, eager PyTorch on CPU tensors.
+
+GPU tensors ALWAYS go through the compiled extension ``sheeprl_prey_amd/ops/_C*.so``
+(built in-tree by ``python setup.py build_ext --inplace`` / ``__graft_entry__.build``); if it is
+missing on a GPU box the op raises instead of silently falling back.  ``set_fused(False)``
+explicitly routes GPU tensors through the eager reference (for A/B measurements only).
+"""
+from __future__ import annotations
+
+import importlib
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from sheeprl_prey_amd.ops import reference as ref
+from sheeprl_prey_amd.ops.reference import ACTS
+
+_C = None
+_LOAD_ERROR: Optional[BaseException] = None
+_FUSED = True
+
+
+def _ext():
+    global _C, _LOAD_ERROR
+    if _C is None and _LOAD_ERROR is None:
+        try:
+            _C = importlib.import_module("sheeprl_prey_amd.ops._C")
+        except BaseException as e:  # noqa: BLE001
+            _LOAD_ERROR = e
+    if _C is None:
+        raise RuntimeError(
+            "sheeprl_prey_amd HIP extension is not built/loadable "
+            f"({_LOAD_ERROR!r}). Run `python setup.py build_ext --inplace` (PYTORCH_ROCM_ARCH=gfx950)."
+        )
+    return _C
+
+
+def native_available() -> bool:
+    try:
+        _ext()
+        return True
+    except RuntimeError:
+        return False
+
+
+def set_fused(flag: bool) -> None:
+    global _FUSED
+    _FUSED = bool(flag)
+
+
+def fused_enabled() -> bool:
+    return _FUSED
+
+
+def _native(t: Tensor) -> bool:
+    if t.is_cuda and _FUSED:
+        _ext()  # loud failure if missing
+        return True
+    return False
+
+
+def _act_code(act: str) -> int:
+    a = (act or "none").lower()
+    if a not in ACTS:
+        raise ValueError(f"unsupported fused activation {act}")
+    return ACTS[a]
+
+
+# =============================================================== LayerNorm + activation
+class _LNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, act):
+        shape = x.shape
+        x2 = x.contiguous().view(-1, shape[-1])
+        y, mean, rstd = _ext().ln_act_fwd(x2, weight, bias, eps, act)
+        ctx.save_for_backward(x2, weight, bias, mean, rstd)
+        ctx.act, ctx.shape = act, shape
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, bias, mean, rstd = ctx.saved_tensors
+        dx, dg, db = _ext().ln_act_bwd(x2, dy.contiguous().view_as(x2), weight, bias, mean, rstd, ctx.act)
+        return dx.view(ctx.shape), (dg if weight is not None else None), (db if bias is not None else None), None, None
+
+
+def ln_act(x: Tensor, weight: Optional[Tensor], bias: Optional[Tensor], eps: float = 1e-5, act: str = "none") -> Tensor:
+    """``act(LayerNorm(x))`` over the last dim."""
+    if _native(x) and x.dtype == torch.float32 and x.shape[-1] <= 12288:
+        return _LNAct.apply(x, weight, bias, float(eps), _act_code(act))
+    return ref.ln_act(x, weight, bias, eps, act)
+
+
+class _LNActNCHW(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, act):
+        x = x.contiguous()
+        y, mean, rstd = _ext().ln_nchw_fwd(x, weight, bias, eps, act)
+        ctx.save_for_backward(x, weight, bias, mean, rstd)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, bias, mean, rstd = ctx.saved_tensors
+        dx, dg, db = _ext().ln_nchw_bwd(x, dy.contiguous(), weight, bias, mean, rstd, ctx.act)
+        return dx, (dg if weight is not None else None), (db if bias is not None else None), None, None
+
+
+def ln_act_nchw(x: Tensor, weight: Optional[Tensor], bias: Optional[Tensor], eps: float = 1e-5, act: str = "none") -> Tensor:
+    """``act(LayerNorm over C)`` of an NCHW tensor, without the NHWC round trip."""
+    if _native(x) and x.dtype == torch.float32 and x.dim() == 4:
+        return _LNActNCHW.apply(x, weight, bias, float(eps), _act_code(act))
+    return ref.ln_act_nchw(x, weight, bias, eps, act)
+
+
+# =============================================================== LayerNorm-GRU epilogue
+class _LNGRU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, h, weight, bias, eps):
+        H = h.shape[-1]
+        x2 = x.contiguous().view(-1, 3 * H)
+        h2 = h.contiguous().view(-1, H)
+        hn, mean, rstd = _ext().ln_gru_fwd(x2, h2, weight, bias, eps)
+        ctx.save_for_backward(x2, h2, weight, bias, mean, rstd)
+        ctx.xshape, ctx.hshape = x.shape, h.shape
+        return hn.view(h.shape)
+
+    @staticmethod
+    def backward(ctx, dhn):
+        x2, h2, weight, bias, mean, rstd = ctx.saved_tensors
+        dx, dh, dg, db = _ext().ln_gru_bwd(x2, h2, weight, bias, mean, rstd, dhn.contiguous().view_as(h2))
+        return dx.view(ctx.xshape), dh.view(ctx.hshape), dg, db, None
+
+
+def ln_gru(x: Tensor, h: Tensor, weight: Tensor, bias: Tensor, eps: float = 1e-5) -> Tensor:
+    """GRU gates of ``LayerNormGRUCell`` applied to the projected input ``x = [h, in] @ W``."""
+    if _native(x) and x.dtype == torch.float32 and h.shape[-1] <= 4096:
+        return _LNGRU.apply(x, h, weight, bias, float(eps))
+    return ref.ln_gru(x, h, weight, bias, eps)
+
+
+# =============================================================== unimix + straight-through sampling
+class _UnimixSample(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, uniform, classes, alpha, sample):
+        l2 = logits.contiguous()
+        mixed, st = _ext().unimix_sample_fwd(l2, uniform if sample else None, classes, alpha)
+        ctx.save_for_backward(l2)
+        ctx.classes, ctx.alpha, ctx.sample = classes, alpha, sample
+        if not sample:
+            ctx.mark_non_differentiable(st)
+        return mixed, st
+
+    @staticmethod
+    def backward(ctx, g_mixed, g_st):
+        (l2,) = ctx.saved_tensors
+        gm = g_mixed.contiguous() if g_mixed is not None else None
+        gs = g_st.contiguous() if (g_st is not None and ctx.sample) else None
+        if gm is None and gs is None:
+            return torch.zeros_like(l2), None, None, None, None
+        dl = _ext().unimix_sample_bwd(l2, gm, gs, ctx.classes, ctx.alpha)
+        return dl, None, None, None, None
+
+
+def unimix_sample(
+    logits: Tensor, classes: int, unimix: float = 0.01, sample: bool = True, uniform: Optional[Tensor] = None
+) -> Tuple[Tensor, Tensor]:
+    """(mixed logits, one-hot sample with straight-through grads | mode one-hot).
+
+    ``logits[..., G*C]`` holds G categoricals of ``classes`` classes each."""
+    if _native(logits) and logits.dtype == torch.float32 and classes <= 64:
+        if sample and uniform is None:
+            uniform = torch.rand(logits.numel() // classes, device=logits.device)
+        return _UnimixSample.apply(logits, uniform, int(classes), float(unimix), bool(sample))
+    return ref.unimix_sample(logits, classes, unimix, uniform=uniform, sample=sample)
+
+
+# =============================================================== two-hot
+_BINS = {}
+
+
+def twohot_bins(num_bins: int, low: float = -20.0, high: float = 20.0, device=None) -> Tensor:
+    key = (num_bins, low, high, str(device))
+    if key not in _BINS:
+        _BINS[key] = torch.linspace(low, high, num_bins, device=device)
+    return _BINS[key]
+
+
+class _TwoHotNLL(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, bins):
+        K = logits.shape[-1]
+        l2 = logits.contiguous().view(-1, K)
+        y = target.detach().contiguous().view(-1).float()
+        loss = _ext().twohot_nll_fwd(l2, y, bins)
+        ctx.save_for_backward(l2, y, bins)
+        ctx.shape = logits.shape
+        return loss.view(logits.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, gl):
+        l2, y, bins = ctx.saved_tensors
+        dl = _ext().twohot_nll_bwd(l2, y, bins, gl.contiguous().view(-1))
+        return dl.view(ctx.shape), None, None
+
+
+def twohot_nll(logits: Tensor, target: Tensor, low: float = -20.0, high: float = 20.0) -> Tensor:
+    """``-TwoHotEncodingDistribution(logits, dims=1).log_prob(target)`` with target [..., 1] or [...]."""
+    if target.dim() == logits.dim():
+        target = target.squeeze(-1)
+    bins = twohot_bins(logits.shape[-1], low, high, device=logits.device)
+    if _native(logits) and logits.dtype == torch.float32 and logits.shape[-1] <= 512:
+        return _TwoHotNLL.apply(logits, target, bins)
+    return ref.twohot_nll(logits, target, bins)
+
+
+class _TwoHotMean(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, bins):
+        K = logits.shape[-1]
+        l2 = logits.contiguous().view(-1, K)
+        out, s = _ext().twohot_mean_fwd(l2, bins)
+        ctx.save_for_backward(l2, bins, s)
+        ctx.shape = logits.shape
+        return out.view(*logits.shape[:-1], 1)
+
+    @staticmethod
+    def backward(ctx, g):
+        l2, bins, s = ctx.saved_tensors
+        dl = _ext().twohot_mean_bwd(l2, bins, s, g.contiguous().view(-1))
+        return dl.view(ctx.shape), None
+
+
+def twohot_mean(logits: Tensor, low: float = -20.0, high: float = 20.0) -> Tensor:
+    """``TwoHotEncodingDistribution(logits, dims=1).mean`` -> [..., 1]."""
+    bins = twohot_bins(logits.shape[-1], low, high, device=logits.device)
+    if _native(logits) and logits.dtype == torch.float32 and logits.shape[-1] <= 512:
+        return _TwoHotMean.apply(logits, bins)
+    return ref.twohot_mean(logits, bins).unsqueeze(-1)
+
+
+# =============================================================== KL balancing
+class _KLBalance(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, post, prior, groups, classes, dyn, rep, free):
+        a = post.contiguous()
+        b = prior.contiguous()
+        kl, loss = _ext().kl_fwd(a, b, groups, classes, dyn, rep, free)
+        ctx.save_for_backward(a, b, kl)
+        ctx.cfg = (groups, classes, dyn, rep, free)
+        ctx.mark_non_differentiable(kl)
+        shape = post.shape[:-1] if post.shape[-1] == groups * classes else post.shape[:-2]
+        ctx.shape = post.shape
+        return loss.view(shape), kl.view(shape)
+
+    @staticmethod
+    def backward(ctx, gl, _gkl):
+        a, b, kl = ctx.saved_tensors
+        groups, classes, dyn, rep, free = ctx.cfg
+        da, db = _ext().kl_bwd(a, b, kl, gl.contiguous().view(-1), groups, classes, dyn, rep, free)
+        return da.view(ctx.shape), db.view(ctx.shape), None, None, None, None, None
+
+
+def kl_balance(
+    post_logits: Tensor, prior_logits: Tensor, groups: int, classes: int, dyn: float = 0.5, rep: float = 0.1,
+    free_nats: float = 1.0,
+) -> Tuple[Tensor, Tensor]:
+    """DreamerV3 KL loss per row: ``dyn*max(KL(sg(post)||prior),free) + rep*max(KL(post||sg(prior)),free)``.
+    Returns (loss, kl)."""
+    if _native(post_logits) and post_logits.dtype == torch.float32 and classes <= 64:
+        return _KLBalance.apply(post_logits, prior_logits, int(groups), int(classes), float(dyn), float(rep), float(free_nats))
+    return ref.kl_balance(post_logits, prior_logits, groups, classes, dyn, rep, free_nats)
+
+
+# =============================================================== scans
+class _Lambda(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, r, v, c, lam):
+        r2, v2, c2 = r.contiguous(), v.contiguous(), c.contiguous()
+        out = _ext().lambda_fwd(r2, v2, c2, lam)
+        ctx.save_for_backward(v2, c2, out)
+        ctx.lam = lam
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        v2, c2, out = ctx.saved_tensors
+        dr, dv, dc = _ext().lambda_bwd(v2, c2, out, g.contiguous(), ctx.lam)
+        return dr, dv, dc, None
+
+
+def lambda_returns(rewards: Tensor, values: Tensor, continues: Tensor, lmbda: float = 0.95) -> Tensor:
+    """DreamerV3 lambda-values over [H, ...] (reference ``dreamer_v3/utils.py:44-55``)."""
+    if _native(rewards) and rewards.dtype == torch.float32:
+        return _Lambda.apply(rewards, values, continues, float(lmbda))
+    return ref.lambda_returns(rewards, values, continues, lmbda)
+
+
+@torch.no_grad()
+def gae_scan(rewards: Tensor, values: Tensor, dones: Tensor, next_value: Tensor, gamma: float, lam: float):
+    """(returns, advantages) for a [T, N, 1] rollout."""
+    if _native(rewards):
+        ret, adv = _ext().gae(
+            rewards.float().contiguous(), values.float().contiguous(), dones.float().contiguous(),
+            next_value.float().contiguous().view(-1), float(gamma), float(lam),
+        )
+        return ret, adv
+    return ref.gae(rewards, values, dones, next_value, gamma, lam)
+
+
+# =============================================================== flat optimiser
+def flat_grad_norm(grad: Tensor, scalars: Tensor, max_norm: float) -> Tensor:
+    if _native(grad):
+        return _ext().flat_grad_norm(grad, scalars, float(max_norm))
+    norm = torch.linalg.vector_norm(grad)
+    coef = torch.ones((), device=grad.device)
+    if 0 < max_norm < float("inf"):
+        coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+    scalars[0] += 1
+    scalars[1] = coef
+    scalars[2] = norm
+    return norm
+
+
+def flat_advance(scalars: Tensor) -> None:
+    if _native(scalars):
+        _ext().flat_advance(scalars)
+        return
+    scalars[0] += 1
+    scalars[1] = 1.0
+
+
+def flat_adam(p, g, m, v, scalars, lr, b1, b2, eps, wd, decoupled) -> None:
+    if _native(p):
+        _ext().flat_adam(p, g, m, v, scalars, lr, b1, b2, eps, wd, bool(decoupled))
+        return
+    t = float(scalars[0].item())
+    coef = scalars[1]
+    grad = g * coef
+    if decoupled:
+        p.mul_(1 - lr * wd)
+    elif wd:
+        grad = grad.add(p, alpha=wd)
+    m.lerp_(grad, 1 - b1)
+    v.mul_(b2).addcmul_(grad, grad, value=1 - b2)
+    bc1 = 1 - b1**t
+    bc2s = (1 - b2**t) ** 0.5
+    denom = (v.sqrt() / bc2s).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / bc1)
+
+
+__all__ = [
+    "ln_act", "ln_act_nchw", "ln_gru", "unimix_sample", "twohot_nll", "twohot_mean", "twohot_bins", "kl_balance",
+    "lambda_returns", "gae_scan", "flat_grad_norm", "flat_advance", "flat_adam", "native_available", "set_fused",
+]

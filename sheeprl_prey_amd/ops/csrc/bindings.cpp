@@ -1,0 +1,360 @@
+// Torch bindings for the sheeprl_prey_amd HIP kernels.  Kernels live in *.hip files that only
+// include <hip/hip_runtime.h>; this file owns shape checks, allocation and the current stream.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <hip/hip_runtime.h>
+
+// ---- launchers (defined in the .hip translation units)
+void launch_flat_grad_norm(const float*, int64_t, float*, int, float*, float*, float, hipStream_t);
+void launch_flat_advance(float*, hipStream_t);
+void launch_flat_adam(float*, const float*, float*, float*, const float*, int64_t, float, float, float, float, float, int,
+                      hipStream_t);
+bool launch_ln_act_fwd(const float*, const float*, const float*, float*, float*, float*, int, int, float, int, hipStream_t);
+int ln_act_bwd_grid(int);
+bool launch_ln_act_bwd(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
+                       float*, float*, float*, int, int, int, hipStream_t);
+void launch_ln_nchw_fwd(const float*, const float*, const float*, float*, float*, float*, int, int, int, float, int,
+                        hipStream_t);
+int ln_nchw_splits(int, int);
+void launch_ln_nchw_bwd(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
+                        float*, float*, float*, int, int, int, int, hipStream_t);
+bool launch_ln_gru_fwd(const float*, const float*, const float*, const float*, float*, float*, float*, int, int, float,
+                       hipStream_t);
+int ln_gru_bwd_grid(int);
+bool launch_ln_gru_bwd(const float*, const float*, const float*, const float*, const float*, const float*, const float*,
+                       float*, float*, float*, float*, float*, float*, int, int, hipStream_t);
+bool launch_unimix_sample_fwd(const float*, const float*, float*, float*, int, int, float, hipStream_t);
+bool launch_unimix_sample_bwd(const float*, const float*, const float*, float*, int, int, float, hipStream_t);
+bool launch_twohot_nll_fwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
+bool launch_twohot_nll_bwd(const float*, const float*, const float*, const float*, float*, int, int, hipStream_t);
+bool launch_twohot_mean_fwd(const float*, const float*, float*, float*, int, int, hipStream_t);
+bool launch_twohot_mean_bwd(const float*, const float*, const float*, const float*, float*, int, int, hipStream_t);
+bool launch_kl_fwd(const float*, const float*, float*, float*, int, int, int, float, float, float, hipStream_t);
+bool launch_kl_bwd(const float*, const float*, const float*, const float*, float*, float*, int, int, int, float, float, float,
+                   hipStream_t);
+void launch_lambda_fwd(const float*, const float*, const float*, float*, int, int, float, hipStream_t);
+void launch_lambda_bwd(const float*, const float*, const float*, const float*, float*, float*, float*, int, int, float,
+                       hipStream_t);
+void launch_gae(const float*, const float*, const float*, const float*, float*, float*, int, int, float, float, hipStream_t);
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_f32(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+const float* opt_ptr(const c10::optional<torch::Tensor>& t) {
+  return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr;
+}
+
+// ------------------------------------------------------------------ optimiser
+torch::Tensor flat_grad_norm(torch::Tensor g, torch::Tensor scalars, double max_norm) {
+  check_f32(g, "grad");
+  check_f32(scalars, "scalars");
+  TORCH_CHECK(g.numel() % 4 == 0, "flat grad numel must be a multiple of 4");
+  const int np = 2048;
+  auto partial = torch::empty({np}, g.options());
+  auto out = torch::empty({}, g.options());
+  launch_flat_grad_norm(g.data_ptr<float>(), g.numel(), partial.data_ptr<float>(), np, scalars.data_ptr<float>(),
+                        out.data_ptr<float>(), (float)max_norm, cur_stream());
+  return out;
+}
+
+void flat_advance(torch::Tensor scalars) {
+  check_f32(scalars, "scalars");
+  launch_flat_advance(scalars.data_ptr<float>(), cur_stream());
+}
+
+void flat_adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, torch::Tensor scalars, double lr,
+               double b1, double b2, double eps, double wd, bool decoupled) {
+  for (auto* t : {&p, &g, &m, &v, &scalars}) check_f32(*t, "adam buffer");
+  TORCH_CHECK(p.numel() == g.numel() && p.numel() == m.numel() && p.numel() == v.numel(), "adam: size mismatch");
+  TORCH_CHECK(p.numel() % 4 == 0, "adam: numel must be a multiple of 4");
+  launch_flat_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                   scalars.data_ptr<float>(), p.numel(), (float)lr, (float)b1, (float)b2, (float)eps, (float)wd,
+                   decoupled ? 1 : 0, cur_stream());
+}
+
+// ------------------------------------------------------------------ LayerNorm + act
+std::vector<torch::Tensor> ln_act_fwd(torch::Tensor x, c10::optional<torch::Tensor> gamma,
+                                      c10::optional<torch::Tensor> beta, double eps, int64_t act) {
+  check_f32(x, "x");
+  const int N = x.size(-1);
+  const int M = x.numel() / N;
+  auto y = torch::empty_like(x);
+  auto mean = torch::empty({M}, x.options());
+  auto rstd = torch::empty({M}, x.options());
+  bool ok = launch_ln_act_fwd(x.data_ptr<float>(), opt_ptr(gamma), opt_ptr(beta), y.data_ptr<float>(),
+                              mean.data_ptr<float>(), rstd.data_ptr<float>(), M, N, (float)eps, (int)act, cur_stream());
+  TORCH_CHECK(ok, "ln_act_fwd: unsupported feature size ", N);
+  return {y, mean, rstd};
+}
+
+std::vector<torch::Tensor> ln_act_bwd(torch::Tensor x, torch::Tensor dy, c10::optional<torch::Tensor> gamma,
+                                      c10::optional<torch::Tensor> beta, torch::Tensor mean, torch::Tensor rstd,
+                                      int64_t act) {
+  check_f32(x, "x");
+  check_f32(dy, "dy");
+  const int N = x.size(-1);
+  const int M = x.numel() / N;
+  auto dx = torch::empty_like(x);
+  bool affine = gamma.has_value() && gamma->defined();
+  torch::Tensor pdg, pdb, dg, db;
+  const int grid = ln_act_bwd_grid(M);
+  if (affine) {
+    pdg = torch::empty({grid, N}, x.options());
+    pdb = torch::empty({grid, N}, x.options());
+    dg = torch::empty({N}, x.options());
+    db = torch::empty({N}, x.options());
+  }
+  bool ok = launch_ln_act_bwd(x.data_ptr<float>(), dy.data_ptr<float>(), opt_ptr(gamma), opt_ptr(beta),
+                              mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr<float>(),
+                              affine ? pdg.data_ptr<float>() : nullptr, affine ? pdb.data_ptr<float>() : nullptr,
+                              affine ? dg.data_ptr<float>() : nullptr, affine ? db.data_ptr<float>() : nullptr, M, N,
+                              (int)act, cur_stream());
+  TORCH_CHECK(ok, "ln_act_bwd: unsupported feature size ", N);
+  return {dx, dg, db};
+}
+
+std::vector<torch::Tensor> ln_nchw_fwd(torch::Tensor x, c10::optional<torch::Tensor> gamma,
+                                       c10::optional<torch::Tensor> beta, double eps, int64_t act) {
+  check_f32(x, "x");
+  TORCH_CHECK(x.dim() == 4, "ln_nchw expects NCHW");
+  const int B = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  auto y = torch::empty_like(x);
+  auto mean = torch::empty({B * HW}, x.options());
+  auto rstd = torch::empty({B * HW}, x.options());
+  launch_ln_nchw_fwd(x.data_ptr<float>(), opt_ptr(gamma), opt_ptr(beta), y.data_ptr<float>(), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), B, C, HW, (float)eps, (int)act, cur_stream());
+  return {y, mean, rstd};
+}
+
+std::vector<torch::Tensor> ln_nchw_bwd(torch::Tensor x, torch::Tensor dy, c10::optional<torch::Tensor> gamma,
+                                       c10::optional<torch::Tensor> beta, torch::Tensor mean, torch::Tensor rstd,
+                                       int64_t act) {
+  check_f32(x, "x");
+  check_f32(dy, "dy");
+  const int B = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  auto dx = torch::empty_like(x);
+  bool affine = gamma.has_value() && gamma->defined();
+  torch::Tensor pdg, pdb, dg, db;
+  if (affine) {
+    const int S = ln_nchw_splits(B, HW);
+    pdg = torch::empty({S, C}, x.options());
+    pdb = torch::empty({S, C}, x.options());
+    dg = torch::empty({C}, x.options());
+    db = torch::empty({C}, x.options());
+  }
+  launch_ln_nchw_bwd(x.data_ptr<float>(), dy.data_ptr<float>(), opt_ptr(gamma), opt_ptr(beta), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), dx.data_ptr<float>(), affine ? pdg.data_ptr<float>() : nullptr,
+                     affine ? pdb.data_ptr<float>() : nullptr, affine ? dg.data_ptr<float>() : nullptr,
+                     affine ? db.data_ptr<float>() : nullptr, B, C, HW, (int)act, cur_stream());
+  return {dx, dg, db};
+}
+
+// ------------------------------------------------------------------ LN-GRU
+std::vector<torch::Tensor> ln_gru_fwd(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::Tensor beta,
+                                      double eps) {
+  check_f32(x, "x");
+  check_f32(h, "h");
+  check_f32(gamma, "gamma");
+  check_f32(beta, "beta");
+  const int H = h.size(-1);
+  const int M = h.numel() / H;
+  TORCH_CHECK(x.size(-1) == 3 * H && x.numel() == (int64_t)M * 3 * H, "ln_gru: x must be [M, 3H]");
+  auto hn = torch::empty_like(h);
+  auto mean = torch::empty({M}, x.options());
+  auto rstd = torch::empty({M}, x.options());
+  bool ok = launch_ln_gru_fwd(x.data_ptr<float>(), h.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                              hn.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), M, H, (float)eps,
+                              cur_stream());
+  TORCH_CHECK(ok, "ln_gru_fwd: unsupported hidden size ", H);
+  return {hn, mean, rstd};
+}
+
+std::vector<torch::Tensor> ln_gru_bwd(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::Tensor beta,
+                                      torch::Tensor mean, torch::Tensor rstd, torch::Tensor dhn) {
+  check_f32(dhn, "dhn");
+  const int H = h.size(-1);
+  const int M = h.numel() / H;
+  auto dx = torch::empty_like(x);
+  auto dh = torch::empty_like(h);
+  const int grid = ln_gru_bwd_grid(M);
+  auto pdg = torch::empty({grid, 3 * H}, x.options());
+  auto pdb = torch::empty({grid, 3 * H}, x.options());
+  auto dg = torch::empty({3 * H}, x.options());
+  auto db = torch::empty({3 * H}, x.options());
+  bool ok = launch_ln_gru_bwd(x.data_ptr<float>(), h.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                              mean.data_ptr<float>(), rstd.data_ptr<float>(), dhn.data_ptr<float>(), dx.data_ptr<float>(),
+                              dh.data_ptr<float>(), pdg.data_ptr<float>(), pdb.data_ptr<float>(), dg.data_ptr<float>(),
+                              db.data_ptr<float>(), M, H, cur_stream());
+  TORCH_CHECK(ok, "ln_gru_bwd: unsupported hidden size ", H);
+  return {dx, dh, dg, db};
+}
+
+// ------------------------------------------------------------------ distributions
+std::vector<torch::Tensor> unimix_sample_fwd(torch::Tensor logits, c10::optional<torch::Tensor> uniform, int64_t C,
+                                             double alpha) {
+  check_f32(logits, "logits");
+  const int R = logits.numel() / C;
+  if (uniform.has_value() && uniform->defined()) {
+    check_f32(*uniform, "uniform");
+    TORCH_CHECK(uniform->numel() == R, "uniform must have one value per categorical");
+  }
+  auto mixed = torch::empty_like(logits);
+  auto sample = torch::empty_like(logits);
+  bool ok = launch_unimix_sample_fwd(logits.data_ptr<float>(), opt_ptr(uniform), mixed.data_ptr<float>(),
+                                     sample.data_ptr<float>(), R, (int)C, (float)alpha, cur_stream());
+  TORCH_CHECK(ok, "unimix_sample: too many classes ", C);
+  return {mixed, sample};
+}
+
+torch::Tensor unimix_sample_bwd(torch::Tensor logits, c10::optional<torch::Tensor> g_mixed,
+                                c10::optional<torch::Tensor> g_sample, int64_t C, double alpha) {
+  const int R = logits.numel() / C;
+  auto dl = torch::empty_like(logits);
+  bool ok = launch_unimix_sample_bwd(logits.data_ptr<float>(), opt_ptr(g_mixed), opt_ptr(g_sample), dl.data_ptr<float>(),
+                                     R, (int)C, (float)alpha, cur_stream());
+  TORCH_CHECK(ok, "unimix_sample_bwd: too many classes ", C);
+  return dl;
+}
+
+torch::Tensor twohot_nll_fwd(torch::Tensor logits, torch::Tensor y, torch::Tensor bins) {
+  check_f32(logits, "logits");
+  check_f32(y, "y");
+  check_f32(bins, "bins");
+  const int K = logits.size(-1);
+  const int R = logits.numel() / K;
+  TORCH_CHECK(y.numel() == R && bins.numel() == K, "twohot_nll: shape mismatch");
+  auto loss = torch::empty({R}, logits.options());
+  bool ok = launch_twohot_nll_fwd(logits.data_ptr<float>(), y.data_ptr<float>(), bins.data_ptr<float>(),
+                                  loss.data_ptr<float>(), R, K, cur_stream());
+  TORCH_CHECK(ok, "twohot: too many bins ", K);
+  return loss;
+}
+
+torch::Tensor twohot_nll_bwd(torch::Tensor logits, torch::Tensor y, torch::Tensor bins, torch::Tensor gl) {
+  check_f32(gl, "grad");
+  const int K = logits.size(-1);
+  const int R = logits.numel() / K;
+  auto dl = torch::empty_like(logits);
+  bool ok = launch_twohot_nll_bwd(logits.data_ptr<float>(), y.data_ptr<float>(), bins.data_ptr<float>(),
+                                  gl.data_ptr<float>(), dl.data_ptr<float>(), R, K, cur_stream());
+  TORCH_CHECK(ok, "twohot: too many bins ", K);
+  return dl;
+}
+
+std::vector<torch::Tensor> twohot_mean_fwd(torch::Tensor logits, torch::Tensor bins) {
+  check_f32(logits, "logits");
+  check_f32(bins, "bins");
+  const int K = logits.size(-1);
+  const int R = logits.numel() / K;
+  auto out = torch::empty({R}, logits.options());
+  auto s = torch::empty({R}, logits.options());
+  bool ok = launch_twohot_mean_fwd(logits.data_ptr<float>(), bins.data_ptr<float>(), out.data_ptr<float>(),
+                                   s.data_ptr<float>(), R, K, cur_stream());
+  TORCH_CHECK(ok, "twohot: too many bins ", K);
+  return {out, s};
+}
+
+torch::Tensor twohot_mean_bwd(torch::Tensor logits, torch::Tensor bins, torch::Tensor s, torch::Tensor gout) {
+  check_f32(gout, "grad");
+  const int K = logits.size(-1);
+  const int R = logits.numel() / K;
+  auto dl = torch::empty_like(logits);
+  bool ok = launch_twohot_mean_bwd(logits.data_ptr<float>(), bins.data_ptr<float>(), s.data_ptr<float>(),
+                                   gout.data_ptr<float>(), dl.data_ptr<float>(), R, K, cur_stream());
+  TORCH_CHECK(ok, "twohot: too many bins ", K);
+  return dl;
+}
+
+std::vector<torch::Tensor> kl_fwd(torch::Tensor a, torch::Tensor b, int64_t G, int64_t C, double dyn, double rep,
+                                  double free_nats) {
+  check_f32(a, "post_logits");
+  check_f32(b, "prior_logits");
+  TORCH_CHECK(a.numel() == b.numel(), "kl: shape mismatch");
+  const int R = a.numel() / (G * C);
+  auto kl = torch::empty({R}, a.options());
+  auto loss = torch::empty({R}, a.options());
+  bool ok = launch_kl_fwd(a.data_ptr<float>(), b.data_ptr<float>(), kl.data_ptr<float>(), loss.data_ptr<float>(), R,
+                          (int)G, (int)C, (float)dyn, (float)rep, (float)free_nats, cur_stream());
+  TORCH_CHECK(ok, "kl: too many classes ", C);
+  return {kl, loss};
+}
+
+std::vector<torch::Tensor> kl_bwd(torch::Tensor a, torch::Tensor b, torch::Tensor kl, torch::Tensor gl, int64_t G,
+                                  int64_t C, double dyn, double rep, double free_nats) {
+  check_f32(gl, "grad");
+  const int R = a.numel() / (G * C);
+  auto da = torch::empty_like(a);
+  auto db = torch::empty_like(b);
+  bool ok = launch_kl_bwd(a.data_ptr<float>(), b.data_ptr<float>(), kl.data_ptr<float>(), gl.data_ptr<float>(),
+                          da.data_ptr<float>(), db.data_ptr<float>(), R, (int)G, (int)C, (float)dyn, (float)rep,
+                          (float)free_nats, cur_stream());
+  TORCH_CHECK(ok, "kl: too many classes ", C);
+  return {da, db};
+}
+
+// ------------------------------------------------------------------ scans
+torch::Tensor lambda_fwd(torch::Tensor r, torch::Tensor v, torch::Tensor c, double lam) {
+  for (auto* t : {&r, &v, &c}) check_f32(*t, "lambda input");
+  const int H = r.size(0);
+  const int M = r.numel() / H;
+  auto out = torch::empty_like(r);
+  launch_lambda_fwd(r.data_ptr<float>(), v.data_ptr<float>(), c.data_ptr<float>(), out.data_ptr<float>(), H, M, (float)lam,
+                    cur_stream());
+  return out;
+}
+
+std::vector<torch::Tensor> lambda_bwd(torch::Tensor v, torch::Tensor c, torch::Tensor ret, torch::Tensor g, double lam) {
+  check_f32(g, "grad");
+  const int H = v.size(0);
+  const int M = v.numel() / H;
+  auto dr = torch::empty_like(v), dv = torch::empty_like(v), dc = torch::empty_like(v);
+  launch_lambda_bwd(v.data_ptr<float>(), c.data_ptr<float>(), ret.data_ptr<float>(), g.data_ptr<float>(),
+                    dr.data_ptr<float>(), dv.data_ptr<float>(), dc.data_ptr<float>(), H, M, (float)lam, cur_stream());
+  return {dr, dv, dc};
+}
+
+std::vector<torch::Tensor> gae(torch::Tensor rew, torch::Tensor val, torch::Tensor done, torch::Tensor next_value,
+                               double gamma, double lam) {
+  for (auto* t : {&rew, &val, &done, &next_value}) check_f32(*t, "gae input");
+  const int T = rew.size(0);
+  const int N = rew.numel() / T;
+  TORCH_CHECK(next_value.numel() == N, "gae: next_value must have one value per env");
+  auto ret = torch::empty_like(rew), adv = torch::empty_like(rew);
+  launch_gae(rew.data_ptr<float>(), val.data_ptr<float>(), done.data_ptr<float>(), next_value.data_ptr<float>(),
+             ret.data_ptr<float>(), adv.data_ptr<float>(), T, N, (float)gamma, (float)lam, cur_stream());
+  return {ret, adv};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "sheeprl_prey_amd HIP kernels (gfx950)";
+  m.def("flat_grad_norm", &flat_grad_norm);
+  m.def("flat_advance", &flat_advance);
+  m.def("flat_adam", &flat_adam);
+  m.def("ln_act_fwd", &ln_act_fwd);
+  m.def("ln_act_bwd", &ln_act_bwd);
+  m.def("ln_nchw_fwd", &ln_nchw_fwd);
+  m.def("ln_nchw_bwd", &ln_nchw_bwd);
+  m.def("ln_gru_fwd", &ln_gru_fwd);
+  m.def("ln_gru_bwd", &ln_gru_bwd);
+  m.def("unimix_sample_fwd", &unimix_sample_fwd);
+  m.def("unimix_sample_bwd", &unimix_sample_bwd);
+  m.def("twohot_nll_fwd", &twohot_nll_fwd);
+  m.def("twohot_nll_bwd", &twohot_nll_bwd);
+  m.def("twohot_mean_fwd", &twohot_mean_fwd);
+  m.def("twohot_mean_bwd", &twohot_mean_bwd);
+  m.def("kl_fwd", &kl_fwd);
+  m.def("kl_bwd", &kl_bwd);
+  m.def("lambda_fwd", &lambda_fwd);
+  m.def("lambda_bwd", &lambda_bwd);
+  m.def("gae", &gae);
+}

@@ -1,0 +1,417 @@
+// Distribution-head kernels for the world-model / actor-critic losses (fp32):
+//  * unimix + straight-through one-hot sampling (reference RSSM._uniform_mix + compute_stochastic_state,
+//    dreamer_v3/agent.py:390-437; OneHotCategoricalStraightThrough, utils/distribution.py:380-393)
+//  * two-hot symlog NLL and two-hot mean (TwoHotEncodingDistribution, utils/distribution.py:224-270)
+//  * categorical KL summed over groups (dreamer_v3/loss.py:65-110)
+// Categorical rows are mapped onto aligned lane segments of W = next_pow2(C) <= 64 lanes, so a
+// wave64 processes 64/W groups at once and every reduction is a segmented xor-shuffle.
+#include "common.h"
+
+namespace srl {
+
+__device__ __forceinline__ float seg_prefix_sum(float v, int width, int lane_in_seg) {
+  for (int o = 1; o < width; o <<= 1) {
+    float t = __shfl_up(v, o, width);
+    if (lane_in_seg >= o) v += t;
+  }
+  return v;
+}
+
+// argmax (first index on ties) over a segment
+__device__ __forceinline__ int seg_argmax(float v, int idx, int width) {
+  for (int o = width >> 1; o > 0; o >>= 1) {
+    float ov = __shfl_xor(v, o, SRL_WAVE);
+    int oi = __shfl_xor(idx, o, SRL_WAVE);
+    if (ov > v || (ov == v && oi < idx)) {
+      v = ov;
+      idx = oi;
+    }
+  }
+  return idx;
+}
+
+#define FEPS 1.1920928955078125e-07f
+
+// One segment = one categorical of C classes.  uniform == nullptr -> mode (argmax).
+__global__ void __launch_bounds__(256) unimix_sample_fwd_kernel(const float* __restrict__ logits,
+                                                                const float* __restrict__ uniform,
+                                                                float* __restrict__ mixed, float* __restrict__ sample,
+                                                                int R, int C, int W, float alpha) {
+  const int lane = threadIdx.x & 63;
+  const int seg_per_wave = 64 / W;
+  const int gwave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int r = gwave * seg_per_wave + lane / W;
+  const int k = lane % W;
+  const bool row_ok = r < R;
+  const bool valid = row_ok && k < C;
+  const int64_t off = (int64_t)r * C + k;
+  float l = valid ? logits[off] : -INFINITY;
+  float m = l;
+  if (alpha > 0.f) {
+    float mx = seg_max(l, W);
+    float e = valid ? __expf(l - mx) : 0.f;
+    float s = seg_sum(e, W);
+    float q = e / s;
+    float pm = (1.f - alpha) * q + alpha / C;
+    pm = fminf(fmaxf(pm, FEPS), 1.f - FEPS);
+    m = valid ? logf(pm) : -INFINITY;
+  }
+  // probabilities of Categorical(logits=m)
+  float mx2 = seg_max(m, W);
+  float e2 = valid ? __expf(m - mx2) : 0.f;
+  float s2 = seg_sum(e2, W);
+  float p = e2 / s2;
+  int pick;
+  if (uniform != nullptr) {
+    float cdf = seg_prefix_sum(p, W, k);
+    float u = row_ok ? uniform[r] : 0.f;
+    float below = (valid && cdf < u * seg_max(cdf, W)) ? 1.f : 0.f;
+    pick = (int)seg_sum(below, W);
+    if (pick > C - 1) pick = C - 1;
+  } else {
+    pick = seg_argmax(valid ? p : -1.f, k, W);
+  }
+  if (valid) {
+    mixed[off] = m;
+    sample[off] = (k == pick) ? 1.f : 0.f;
+  }
+}
+
+// d(loss)/d(logits) given g_mixed (may be null) and g_sample (straight-through path, may be null)
+__global__ void __launch_bounds__(256) unimix_sample_bwd_kernel(const float* __restrict__ logits,
+                                                                const float* __restrict__ g_mixed,
+                                                                const float* __restrict__ g_sample,
+                                                                float* __restrict__ dlogits, int R, int C, int W,
+                                                                float alpha) {
+  const int lane = threadIdx.x & 63;
+  const int seg_per_wave = 64 / W;
+  const int gwave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int r = gwave * seg_per_wave + lane / W;
+  const int k = lane % W;
+  const bool valid = r < R && k < C;
+  const int64_t off = (int64_t)r * C + k;
+  float l = valid ? logits[off] : -INFINITY;
+  float q = 0.f, pm = 0.f, m = l;
+  bool clamped = false;
+  if (alpha > 0.f) {
+    float mx = seg_max(l, W);
+    float e = valid ? __expf(l - mx) : 0.f;
+    float s = seg_sum(e, W);
+    q = e / s;
+    pm = (1.f - alpha) * q + alpha / C;
+    clamped = pm <= FEPS || pm >= 1.f - FEPS;
+    m = valid ? logf(fminf(fmaxf(pm, FEPS), 1.f - FEPS)) : -INFINITY;
+  }
+  float gm = (valid && g_mixed) ? g_mixed[off] : 0.f;
+  if (g_sample) {
+    float mx2 = seg_max(m, W);
+    float e2 = valid ? __expf(m - mx2) : 0.f;
+    float p = e2 / seg_sum(e2, W);
+    float gs = valid ? g_sample[off] : 0.f;
+    float dot = seg_sum(p * gs, W);
+    gm += p * (gs - dot);
+  }
+  float dl;
+  if (alpha > 0.f) {
+    float w = (valid && !clamped) ? (1.f - alpha) * gm / pm : 0.f;
+    float dot = seg_sum(q * w, W);
+    dl = q * (w - dot);
+  } else {
+    dl = gm;
+  }
+  if (valid) dlogits[off] = dl;
+}
+
+// ---------------------------------------------------------------- two-hot (one wave per row)
+template <int MAXK>
+__global__ void __launch_bounds__(256) twohot_nll_fwd_kernel(const float* __restrict__ logits, const float* __restrict__ y,
+                                                             const float* __restrict__ bins, float* __restrict__ loss,
+                                                             int R, int K) {
+  const int lane = threadIdx.x & 63;
+  const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;
+  const float* lr = logits + (int64_t)r * K;
+  float yv = y[r];
+  float x = copysignf(log1pf(fabsf(yv)), yv);
+  float lv[MAXK], bv[MAXK];
+  float mx = -INFINITY;
+  int cle = 0, cgt = 0;
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) {
+    int k = lane + 64 * i;
+    bool ok = k < K;
+    lv[i] = ok ? lr[k] : -INFINITY;
+    bv[i] = ok ? bins[k] : 0.f;
+    mx = fmaxf(mx, lv[i]);
+    cle += (ok && bv[i] <= x) ? 1 : 0;
+    cgt += (ok && bv[i] > x) ? 1 : 0;
+  }
+  mx = wave_max(mx);
+  float se = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) se += (lane + 64 * i < K) ? __expf(lv[i] - mx) : 0.f;
+  const float lse = mx + logf(wave_sum(se));
+  int below = (int)wave_sum((float)cle) - 1;
+  int above = K - (int)wave_sum((float)cgt);
+  below = below < 0 ? 0 : (below > K - 1 ? K - 1 : below);
+  above = above < 0 ? 0 : (above > K - 1 ? K - 1 : above);
+  const float bb = bins[below], ba = bins[above];
+  const bool eq = below == above;
+  const float db = eq ? 1.f : fabsf(bb - x), da = eq ? 1.f : fabsf(ba - x);
+  const float tot = db + da;
+  const float wb = da / tot, wa = db / tot;
+  if (lane == 0) {
+    float lpb = lr[below] - lse, lpa = lr[above] - lse;
+    loss[r] = -(wb * lpb + wa * lpa);
+  }
+}
+
+template <int MAXK>
+__global__ void __launch_bounds__(256) twohot_nll_bwd_kernel(const float* __restrict__ logits, const float* __restrict__ y,
+                                                             const float* __restrict__ bins, const float* __restrict__ gl,
+                                                             float* __restrict__ dlogits, int R, int K) {
+  const int lane = threadIdx.x & 63;
+  const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;
+  const float* lr = logits + (int64_t)r * K;
+  float yv = y[r];
+  float x = copysignf(log1pf(fabsf(yv)), yv);
+  float lv[MAXK];
+  float mx = -INFINITY;
+  int cle = 0, cgt = 0;
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) {
+    int k = lane + 64 * i;
+    bool ok = k < K;
+    lv[i] = ok ? lr[k] : -INFINITY;
+    float b = ok ? bins[k] : 0.f;
+    mx = fmaxf(mx, lv[i]);
+    cle += (ok && b <= x) ? 1 : 0;
+    cgt += (ok && b > x) ? 1 : 0;
+  }
+  mx = wave_max(mx);
+  float se = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) se += (lane + 64 * i < K) ? __expf(lv[i] - mx) : 0.f;
+  se = wave_sum(se);
+  int below = (int)wave_sum((float)cle) - 1;
+  int above = K - (int)wave_sum((float)cgt);
+  below = below < 0 ? 0 : (below > K - 1 ? K - 1 : below);
+  above = above < 0 ? 0 : (above > K - 1 ? K - 1 : above);
+  const float bb = bins[below], ba = bins[above];
+  const bool eq = below == above;
+  const float db = eq ? 1.f : fabsf(bb - x), da = eq ? 1.f : fabsf(ba - x);
+  const float tot = db + da;
+  const float wb = da / tot, wa = db / tot;
+  const float g = gl[r];
+  float* dr = dlogits + (int64_t)r * K;
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) {
+    int k = lane + 64 * i;
+    if (k < K) {
+      float t = (k == below ? wb : 0.f) + (k == above ? wa : 0.f);
+      dr[k] = g * (__expf(lv[i] - mx) / se - t);
+    }
+  }
+}
+
+// out[r] = symexp(sum_k softmax(l)_k * bins_k); also stores s = sum p*b for the backward
+template <int MAXK>
+__global__ void __launch_bounds__(256) twohot_mean_fwd_kernel(const float* __restrict__ logits,
+                                                              const float* __restrict__ bins, float* __restrict__ out,
+                                                              float* __restrict__ s_out, int R, int K) {
+  const int lane = threadIdx.x & 63;
+  const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;
+  const float* lr = logits + (int64_t)r * K;
+  float lv[MAXK];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) {
+    int k = lane + 64 * i;
+    lv[i] = k < K ? lr[k] : -INFINITY;
+    mx = fmaxf(mx, lv[i]);
+  }
+  mx = wave_max(mx);
+  float se = 0.f, sb = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) {
+    int k = lane + 64 * i;
+    if (k < K) {
+      float e = __expf(lv[i] - mx);
+      se += e;
+      sb += e * bins[k];
+    }
+  }
+  se = wave_sum(se);
+  sb = wave_sum(sb);
+  if (lane == 0) {
+    float s = sb / se;
+    s_out[r] = s;
+    out[r] = copysignf(expm1f(fabsf(s)), s);
+  }
+}
+
+template <int MAXK>
+__global__ void __launch_bounds__(256) twohot_mean_bwd_kernel(const float* __restrict__ logits,
+                                                              const float* __restrict__ bins, const float* __restrict__ s_in,
+                                                              const float* __restrict__ gout, float* __restrict__ dlogits,
+                                                              int R, int K) {
+  const int lane = threadIdx.x & 63;
+  const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;
+  const float* lr = logits + (int64_t)r * K;
+  float lv[MAXK];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) {
+    int k = lane + 64 * i;
+    lv[i] = k < K ? lr[k] : -INFINITY;
+    mx = fmaxf(mx, lv[i]);
+  }
+  mx = wave_max(mx);
+  float se = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) se += (lane + 64 * i < K) ? __expf(lv[i] - mx) : 0.f;
+  se = wave_sum(se);
+  const float s = s_in[r];
+  const float g = gout[r] * __expf(fabsf(s));
+  float* dr = dlogits + (int64_t)r * K;
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) {
+    int k = lane + 64 * i;
+    if (k < K) dr[k] = g * (__expf(lv[i] - mx) / se) * (bins[k] - s);
+  }
+}
+
+// ---------------------------------------------------------------- categorical KL(post || prior)
+// one block per row; row holds G groups of C classes; loss = (dyn + rep) * max(kl, free)
+__global__ void __launch_bounds__(256) kl_fwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                     float* __restrict__ kl_out, float* __restrict__ loss_out, int R, int G,
+                                                     int C, int W, float dyn, float rep, float free_nats) {
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int spw = 64 / W;
+  const int k = lane % W;
+  const int r = blockIdx.x;
+  float acc = 0.f;
+  for (int g0 = 0; g0 < G; g0 += 4 * spw) {
+    const int g = g0 + wid * spw + lane / W;
+    const bool valid = g < G && k < C;
+    const int64_t off = ((int64_t)r * G + g) * C + k;
+    float av = valid ? a[off] : -INFINITY, bv = valid ? b[off] : -INFINITY;
+    float ma = seg_max(av, W), mb = seg_max(bv, W);
+    float ea = valid ? __expf(av - ma) : 0.f, eb = valid ? __expf(bv - mb) : 0.f;
+    float la = logf(seg_sum(ea, W)) + ma, lb = logf(seg_sum(eb, W)) + mb;
+    float lpa = av - la, lpb = bv - lb;
+    float p = valid ? __expf(lpa) : 0.f;
+    acc += valid ? p * (lpa - lpb) : 0.f;
+  }
+  float kl = block_sum<4>(acc, red);
+  if (threadIdx.x == 0) {
+    kl_out[r] = kl;
+    loss_out[r] = (dyn + rep) * fmaxf(kl, free_nats);
+  }
+}
+
+__global__ void __launch_bounds__(256) kl_bwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                     const float* __restrict__ kl_in, const float* __restrict__ gl,
+                                                     float* __restrict__ da, float* __restrict__ db, int R, int G, int C,
+                                                     int W, float dyn, float rep, float free_nats) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int spw = 64 / W;
+  const int k = lane % W;
+  const int r = blockIdx.x;
+  const bool active = kl_in[r] > free_nats;
+  const float g = active ? gl[r] : 0.f;
+  for (int g0 = 0; g0 < G; g0 += 4 * spw) {
+    const int grp = g0 + wid * spw + lane / W;
+    const bool valid = grp < G && k < C;
+    const int64_t off = ((int64_t)r * G + grp) * C + k;
+    float av = valid ? a[off] : -INFINITY, bv = valid ? b[off] : -INFINITY;
+    float ma = seg_max(av, W), mb = seg_max(bv, W);
+    float ea = valid ? __expf(av - ma) : 0.f, eb = valid ? __expf(bv - mb) : 0.f;
+    float sa = seg_sum(ea, W), sb = seg_sum(eb, W);
+    float lpa = av - (logf(sa) + ma), lpb = bv - (logf(sb) + mb);
+    float p = ea / sa, q = eb / sb;
+    float klg = seg_sum(valid ? p * (lpa - lpb) : 0.f, W);
+    if (valid) {
+      da[off] = rep * g * p * ((lpa - lpb) - klg);
+      db[off] = dyn * g * (q - p);
+    }
+  }
+}
+
+}  // namespace srl
+
+using namespace srl;
+
+static int next_pow2(int c) {
+  int w = 1;
+  while (w < c) w <<= 1;
+  return w;
+}
+
+bool launch_unimix_sample_fwd(const float* logits, const float* uniform, float* mixed, float* sample, int R, int C,
+                              float alpha, hipStream_t st) {
+  if (C > 64) return false;
+  int W = next_pow2(C);
+  int segs_per_block = 4 * (64 / W);
+  hipLaunchKernelGGL(unimix_sample_fwd_kernel, dim3(cdiv(R, segs_per_block)), dim3(256), 0, st, logits, uniform, mixed,
+                     sample, R, C, W, alpha);
+  return true;
+}
+
+bool launch_unimix_sample_bwd(const float* logits, const float* g_mixed, const float* g_sample, float* dlogits, int R,
+                              int C, float alpha, hipStream_t st) {
+  if (C > 64) return false;
+  int W = next_pow2(C);
+  int segs_per_block = 4 * (64 / W);
+  hipLaunchKernelGGL(unimix_sample_bwd_kernel, dim3(cdiv(R, segs_per_block)), dim3(256), 0, st, logits, g_mixed, g_sample,
+                     dlogits, R, C, W, alpha);
+  return true;
+}
+
+#define TH_DISPATCH(KERNEL, ...)                                                                       \
+  do {                                                                                                 \
+    dim3 g(cdiv(R, 4)), b(256);                                                                        \
+    if (K <= 64) hipLaunchKernelGGL(KERNEL<1>, g, b, 0, st, __VA_ARGS__);                              \
+    else if (K <= 128) hipLaunchKernelGGL(KERNEL<2>, g, b, 0, st, __VA_ARGS__);                        \
+    else if (K <= 256) hipLaunchKernelGGL(KERNEL<4>, g, b, 0, st, __VA_ARGS__);                        \
+    else if (K <= 512) hipLaunchKernelGGL(KERNEL<8>, g, b, 0, st, __VA_ARGS__);                        \
+    else return false;                                                                                 \
+  } while (0)
+
+bool launch_twohot_nll_fwd(const float* logits, const float* y, const float* bins, float* loss, int R, int K,
+                           hipStream_t st) {
+  TH_DISPATCH(twohot_nll_fwd_kernel, logits, y, bins, loss, R, K);
+  return true;
+}
+bool launch_twohot_nll_bwd(const float* logits, const float* y, const float* bins, const float* gl, float* dlogits, int R,
+                           int K, hipStream_t st) {
+  TH_DISPATCH(twohot_nll_bwd_kernel, logits, y, bins, gl, dlogits, R, K);
+  return true;
+}
+bool launch_twohot_mean_fwd(const float* logits, const float* bins, float* out, float* s, int R, int K, hipStream_t st) {
+  TH_DISPATCH(twohot_mean_fwd_kernel, logits, bins, out, s, R, K);
+  return true;
+}
+bool launch_twohot_mean_bwd(const float* logits, const float* bins, const float* s, const float* gout, float* dlogits,
+                            int R, int K, hipStream_t st) {
+  TH_DISPATCH(twohot_mean_bwd_kernel, logits, bins, s, gout, dlogits, R, K);
+  return true;
+}
+
+bool launch_kl_fwd(const float* a, const float* b, float* kl, float* loss, int R, int G, int C, float dyn, float rep,
+                   float free_nats, hipStream_t st) {
+  if (C > 64) return false;
+  hipLaunchKernelGGL(kl_fwd_kernel, dim3(R), dim3(256), 0, st, a, b, kl, loss, R, G, C, next_pow2(C), dyn, rep, free_nats);
+  return true;
+}
+bool launch_kl_bwd(const float* a, const float* b, const float* kl, const float* gl, float* da, float* db, int R, int G,
+                   int C, float dyn, float rep, float free_nats, hipStream_t st) {
+  if (C > 64) return false;
+  hipLaunchKernelGGL(kl_bwd_kernel, dim3(R), dim3(256), 0, st, a, b, kl, gl, da, db, R, G, C, next_pow2(C), dyn, rep,
+                     free_nats);
+  return true;
+}

@@ -1,0 +1,197 @@
+#include "hip/hip_runtime.h"
+// LayerNorm-GRU cell epilogue (reference: LayerNormGRUCell, sheeprl/models/models.py:362-402):
+//   x = [h, in] @ W            (GEMM, done by the caller)
+//   z = LN(x) * gamma + beta   over 3H
+//   r = sig(z_r); c = tanh(r * z_c); u = sig(z_u - 1); h' = u * c + (1 - u) * h
+// One block per row; thread t owns hidden units t, t+T, ... and reads their r/c/u columns,
+// so every load is coalesced.  Backward recomputes z from (x, mean, rstd).
+#include "common.h"
+
+namespace srl {
+
+template <int MAXH>
+__global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict__ x, const float* __restrict__ h,
+                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                         float* __restrict__ hn, float* __restrict__ mean_out,
+                                                         float* __restrict__ rstd_out, int M, int H, float eps) {
+  __shared__ float red[4];
+  const int T = 256, N = 3 * H;
+  for (int row = blockIdx.x; row < M; row += gridDim.x) {
+    const float* xr = x + (int64_t)row * N;
+    float v[3][MAXH];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXH; ++k) {
+      int j = threadIdx.x + k * T;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        v[g][k] = j < H ? xr[g * H + j] : 0.f;
+        s += v[g][k];
+      }
+    }
+    const float mu = block_sum<4>(s, red) / N;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXH; ++k) {
+      int j = threadIdx.x + k * T;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        float d = j < H ? v[g][k] - mu : 0.f;
+        q += d * d;
+      }
+    }
+    const float rs = rsqrtf(block_sum<4>(q, red) / N + eps);
+#pragma unroll
+    for (int k = 0; k < MAXH; ++k) {
+      int j = threadIdx.x + k * T;
+      if (j < H) {
+        float zr = (v[0][k] - mu) * rs * gamma[j] + beta[j];
+        float zc = (v[1][k] - mu) * rs * gamma[H + j] + beta[H + j];
+        float zu = (v[2][k] - mu) * rs * gamma[2 * H + j] + beta[2 * H + j];
+        float r = sigmoidf_(zr);
+        float c = tanhf(r * zc);
+        float u = sigmoidf_(zu - 1.f);
+        float hp = h[(int64_t)row * H + j];
+        hn[(int64_t)row * H + j] = u * c + (1.f - u) * hp;
+      }
+    }
+    if (threadIdx.x == 0) {
+      mean_out[row] = mu;
+      rstd_out[row] = rs;
+    }
+  }
+}
+
+template <int MAXH>
+__global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict__ x, const float* __restrict__ h,
+                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                         const float* __restrict__ dhn, float* __restrict__ dx,
+                                                         float* __restrict__ dh, float* __restrict__ pdg,
+                                                         float* __restrict__ pdb, int M, int H) {
+  __shared__ float red[4];
+  const int T = 256, N = 3 * H;
+  float ag[3][MAXH], ab[3][MAXH];
+#pragma unroll
+  for (int k = 0; k < MAXH; ++k)
+#pragma unroll
+    for (int g = 0; g < 3; ++g) ag[g][k] = ab[g][k] = 0.f;
+  for (int row = blockIdx.x; row < M; row += gridDim.x) {
+    const float* xr = x + (int64_t)row * N;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[3][MAXH], dxh[3][MAXH];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXH; ++k) {
+      int j = threadIdx.x + k * T;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) xh[g][k] = dxh[g][k] = 0.f;
+      if (j < H) {
+        float hr = (xr[j] - mu) * rs, hc = (xr[H + j] - mu) * rs, hu = (xr[2 * H + j] - mu) * rs;
+        float gr = gamma[j], gc = gamma[H + j], gu = gamma[2 * H + j];
+        float zr = hr * gr + beta[j], zc = hc * gc + beta[H + j], zu = hu * gu + beta[2 * H + j];
+        float r = sigmoidf_(zr);
+        float c = tanhf(r * zc);
+        float u = sigmoidf_(zu - 1.f);
+        float hp = h[(int64_t)row * H + j];
+        float g_out = dhn[(int64_t)row * H + j];
+        dh[(int64_t)row * H + j] = g_out * (1.f - u);
+        float du = g_out * (c - hp);
+        float dc = g_out * u;
+        float dzu = du * u * (1.f - u);
+        float da = dc * (1.f - c * c);
+        float dzc = da * r;
+        float dr = da * zc;
+        float dzr = dr * r * (1.f - r);
+        ag[0][k] += dzr * hr; ag[1][k] += dzc * hc; ag[2][k] += dzu * hu;
+        ab[0][k] += dzr; ab[1][k] += dzc; ab[2][k] += dzu;
+        xh[0][k] = hr; xh[1][k] = hc; xh[2][k] = hu;
+        dxh[0][k] = dzr * gr; dxh[1][k] = dzc * gc; dxh[2][k] = dzu * gu;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+          s1 += dxh[g][k];
+          s2 += dxh[g][k] * xh[g][k];
+        }
+      }
+    }
+    const float m1 = block_sum<4>(s1, red) / N;
+    const float m2 = block_sum<4>(s2, red) / N;
+    float* dxr = dx + (int64_t)row * N;
+#pragma unroll
+    for (int k = 0; k < MAXH; ++k) {
+      int j = threadIdx.x + k * T;
+      if (j < H) {
+#pragma unroll
+        for (int g = 0; g < 3; ++g) dxr[g * H + j] = rs * (dxh[g][k] - m1 - xh[g][k] * m2);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < MAXH; ++k) {
+    int j = threadIdx.x + k * T;
+    if (j < H) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        pdg[(int64_t)blockIdx.x * N + g * H + j] = ag[g][k];
+        pdb[(int64_t)blockIdx.x * N + g * H + j] = ab[g][k];
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) colsum2_gru_kernel(const float* __restrict__ pa, const float* __restrict__ pb,
+                                                          float* __restrict__ oa, float* __restrict__ ob, int rows, int N) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float a = 0.f, b = 0.f;
+  for (int r = 0; r < rows; ++r) {
+    a += pa[(int64_t)r * N + n];
+    b += pb[(int64_t)r * N + n];
+  }
+  oa[n] = a;
+  ob[n] = b;
+}
+
+}  // namespace srl
+
+using namespace srl;
+
+static int gru_maxh(int H) {
+  if (H <= 512) return 2;
+  if (H <= 1024) return 4;
+  if (H <= 2048) return 8;
+  if (H <= 4096) return 16;
+  return 0;
+}
+
+bool launch_ln_gru_fwd(const float* x, const float* h, const float* gamma, const float* beta, float* hn, float* mean,
+                       float* rstd, int M, int H, float eps, hipStream_t st) {
+  int mh = gru_maxh(H);
+  dim3 g(M), b(256);
+  switch (mh) {
+    case 2: hipLaunchKernelGGL(ln_gru_fwd_kernel<2>, g, b, 0, st, x, h, gamma, beta, hn, mean, rstd, M, H, eps); return true;
+    case 4: hipLaunchKernelGGL(ln_gru_fwd_kernel<4>, g, b, 0, st, x, h, gamma, beta, hn, mean, rstd, M, H, eps); return true;
+    case 8: hipLaunchKernelGGL(ln_gru_fwd_kernel<8>, g, b, 0, st, x, h, gamma, beta, hn, mean, rstd, M, H, eps); return true;
+    case 16: hipLaunchKernelGGL(ln_gru_fwd_kernel<16>, g, b, 0, st, x, h, gamma, beta, hn, mean, rstd, M, H, eps); return true;
+    default: return false;
+  }
+}
+
+int ln_gru_bwd_grid(int M) { return M < 256 ? M : 256; }
+
+bool launch_ln_gru_bwd(const float* x, const float* h, const float* gamma, const float* beta, const float* mean,
+                       const float* rstd, const float* dhn, float* dx, float* dh, float* pdg, float* pdb, float* dgamma,
+                       float* dbeta, int M, int H, hipStream_t st) {
+  int mh = gru_maxh(H);
+  int grid = ln_gru_bwd_grid(M);
+  dim3 g(grid), b(256);
+  switch (mh) {
+    case 2: hipLaunchKernelGGL(ln_gru_bwd_kernel<2>, g, b, 0, st, x, h, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
+    case 4: hipLaunchKernelGGL(ln_gru_bwd_kernel<4>, g, b, 0, st, x, h, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
+    case 8: hipLaunchKernelGGL(ln_gru_bwd_kernel<8>, g, b, 0, st, x, h, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
+    case 16: hipLaunchKernelGGL(ln_gru_bwd_kernel<16>, g, b, 0, st, x, h, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
+    default: return false;
+  }
+  hipLaunchKernelGGL(colsum2_gru_kernel, dim3(cdiv(3 * H, 256)), dim3(256), 0, st, pdg, pdb, dgamma, dbeta, grid, 3 * H);
+  return true;
+}

@@ -1,0 +1,397 @@
+"""The distributed runner: one process per GPU, RCCL over xGMI (gloo on CPU).
+
+Replaces Lightning Fabric in the reference (``sheeprl/cli.py:83-84``, ``fabric.launch``,
+``setup_module``, ``backward``, ``clip_gradients``, ``all_gather``, ``all_reduce``, ``barrier``,
+``save``/``load``, ``log``/``log_dict``, ``call``).  Design choices for MI355X:
+
+* no DDP wrapper per sub-module: every optimiser owns ONE flat fp32 gradient slab
+  (:class:`~sheeprl_prey_amd.parallel.flat_optim.FlatOptimizer`), reduced by one RCCL
+  all-reduce (or a few large buckets) per backward instead of 9 DDP instances;
+* global-norm clipping and the Adam update run as two fused HIP kernels on that slab;
+* launch: torchrun env (``RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*``) or local spawn of
+  ``devices`` processes (the multi-process CPU tests use gloo).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import pickle
+import random
+import socket
+from contextlib import closing
+from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+from torch import Tensor
+
+
+def _free_port() -> int:
+    with closing(socket.socket(socket.AF_INET, socket.SOCK_STREAM)) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _resolve_accelerator(accelerator: str) -> str:
+    acc = os.environ.get("LT_ACCELERATOR", accelerator) or "cpu"
+    acc = str(acc).lower()
+    if acc in ("gpu", "cuda", "rocm", "hip"):
+        return "cuda"
+    if acc == "auto":
+        return "cuda" if torch.cuda.is_available() else "cpu"
+    return "cpu"
+
+
+def _resolve_devices(devices: Any, accelerator: str) -> int:
+    dev = os.environ.get("LT_DEVICES", devices)
+    if isinstance(dev, str):
+        if dev in ("auto", "-1"):
+            if "WORLD_SIZE" in os.environ:
+                return int(os.environ["LOCAL_WORLD_SIZE"]) if "LOCAL_WORLD_SIZE" in os.environ else int(os.environ["WORLD_SIZE"])
+            return max(torch.cuda.device_count(), 1) if accelerator == "cuda" else 1
+        dev = int(dev)
+    if isinstance(dev, (list, tuple)):
+        return len(dev)
+    if dev is None or int(dev) <= 0:
+        # `devices: 0` in ddp presets means "all visible"
+        return max(torch.cuda.device_count(), 1) if accelerator == "cuda" else 1
+    return int(dev)
+
+
+def _spawn_entry(local_rank: int, world_size: int, port: int, fn, cfg, runner_kwargs) -> None:
+    os.environ["RANK"] = str(local_rank)
+    os.environ["LOCAL_RANK"] = str(local_rank)
+    os.environ["WORLD_SIZE"] = str(world_size)
+    os.environ["LOCAL_WORLD_SIZE"] = str(world_size)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    runner = Runner(**runner_kwargs)
+    runner._init_distributed()
+    try:
+        fn(runner, cfg)
+    finally:
+        runner.teardown()
+
+
+class Runner:
+    """Process/device/collective layer used by every algorithm."""
+
+    def __init__(
+        self,
+        devices: Any = 1,
+        num_nodes: int = 1,
+        strategy: str = "auto",
+        accelerator: str = "cpu",
+        precision: str = "32-true",
+        callbacks: Optional[Sequence[Any]] = None,
+        loggers: Optional[Sequence[Any]] = None,
+        cuda_graphs: bool = False,
+        fused_ops: bool = True,
+        bucket_mb: int = 32,
+        process_group=None,
+        **_unused,
+    ) -> None:
+        self.accelerator = _resolve_accelerator(accelerator)
+        if self.accelerator == "cuda" and not torch.cuda.is_available():
+            self.accelerator = "cpu"
+        self.devices = _resolve_devices(devices, self.accelerator)
+        self.num_nodes = int(num_nodes)
+        self.strategy = strategy
+        self.precision = precision
+        self.callbacks = list(callbacks or [])
+        self._loggers = list(loggers or [])
+        self.cuda_graphs = bool(cuda_graphs) and self.accelerator == "cuda"
+        self.fused_ops = bool(fused_ops)
+        self.bucket_mb = int(bucket_mb)
+        self._kwargs = dict(
+            devices=devices, num_nodes=num_nodes, strategy=strategy, accelerator=accelerator,
+            precision=precision, callbacks=callbacks, cuda_graphs=cuda_graphs, fused_ops=fused_ops, bucket_mb=bucket_mb,
+        )
+        self.group = process_group  # None == WORLD
+        if str(strategy).lower() in ("fsdp",):
+            raise ValueError("FSDP is not supported: SheepRL-style RL models are replicated (data parallel only)")
+
+    # ------------------------------------------------------------------ topology
+    @property
+    def world_size(self) -> int:
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_world_size(self.group)
+        return 1
+
+    @property
+    def global_rank(self) -> int:
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(self.group) if self.group is not None else dist.get_rank()
+        return 0
+
+    @property
+    def local_rank(self) -> int:
+        return int(os.environ.get("LOCAL_RANK", 0))
+
+    @property
+    def node_rank(self) -> int:
+        return int(os.environ.get("GROUP_RANK", 0))
+
+    @property
+    def is_global_zero(self) -> bool:
+        return self.global_rank == 0
+
+    @property
+    def device(self) -> torch.device:
+        if self.accelerator == "cuda":
+            n = torch.cuda.device_count()
+            return torch.device("cuda", self.local_rank % max(n, 1))
+        return torch.device("cpu")
+
+    @property
+    def backend(self) -> str:
+        # On ROCm the "nccl" backend string IS RCCL.
+        return "nccl" if self.accelerator == "cuda" else "gloo"
+
+    @property
+    def logger(self):
+        return self._loggers[0] if self._loggers else None
+
+    @property
+    def loggers(self):
+        return self._loggers
+
+    # ------------------------------------------------------------------ launch
+    def _init_distributed(self) -> None:
+        ws = int(os.environ.get("WORLD_SIZE", "1"))
+        if self.accelerator == "cuda":
+            torch.cuda.set_device(self.device)
+        if ws > 1 and not dist.is_initialized():
+            kwargs = dict(backend=self.backend, timeout=datetime.timedelta(minutes=30))
+            if self.accelerator == "cuda":
+                kwargs["device_id"] = self.device
+            dist.init_process_group(**kwargs)
+
+    def launch(self, fn: Callable[["Runner", Any], Any], cfg: Any) -> Any:
+        """Run ``fn(runner, cfg)`` on every rank."""
+        already = "WORLD_SIZE" in os.environ and int(os.environ.get("WORLD_SIZE", "1")) > 1
+        if already or self.devices * self.num_nodes <= 1:
+            if already or dist.is_initialized():
+                self._init_distributed()
+            elif self.accelerator == "cuda":
+                torch.cuda.set_device(self.device)
+            return fn(self, cfg)
+        import torch.multiprocessing as mp
+
+        port = _free_port()
+        mp.start_processes(
+            _spawn_entry,
+            args=(self.devices, port, fn, cfg, self._kwargs),
+            nprocs=self.devices,
+            join=True,
+            start_method="spawn",
+        )
+        return None
+
+    def teardown(self) -> None:
+        for lg in self._loggers:
+            try:
+                lg.finalize("success")
+            except Exception:
+                pass
+        if dist.is_available() and dist.is_initialized():
+            try:
+                dist.barrier()
+            except Exception:
+                pass
+            dist.destroy_process_group()
+
+    # ------------------------------------------------------------------ utils
+    def seed_everything(self, seed: int) -> int:
+        random.seed(seed)
+        np.random.seed(seed % (2**32))
+        torch.manual_seed(seed)
+        if torch.cuda.is_available():
+            torch.cuda.manual_seed_all(seed)
+        return seed
+
+    def print(self, *args, **kwargs) -> None:
+        if self.is_global_zero:
+            print(*args, **kwargs, flush=True)
+
+    def to_device(self, x):
+        if isinstance(x, Tensor):
+            return x.to(self.device, non_blocking=True)
+        if isinstance(x, dict):
+            return {k: self.to_device(v) for k, v in x.items()}
+        return x
+
+    def setup_module(self, module: nn.Module) -> nn.Module:
+        """Move to device and make every rank start from rank 0's weights."""
+        module = module.to(self.device)
+        if self.world_size > 1:
+            with torch.no_grad():
+                tensors = [p.data for p in module.parameters()] + [b for b in module.buffers()]
+                if tensors:
+                    flat = torch.cat([t.reshape(-1).float() for t in tensors])
+                    dist.broadcast(flat, src=self._global_src(0), group=self.group)
+                    off = 0
+                    for t in tensors:
+                        n = t.numel()
+                        t.copy_(flat[off : off + n].view_as(t).to(t.dtype))
+                        off += n
+        return module
+
+    def setup_optimizers(self, *optimizers):
+        return optimizers[0] if len(optimizers) == 1 else optimizers
+
+    def _global_src(self, src: int) -> int:
+        if self.group is None:
+            return src
+        return dist.get_global_rank(self.group, src)
+
+    # ------------------------------------------------------------------ grads
+    def backward(self, loss: Tensor, optimizer=None, **kwargs) -> None:
+        """``loss.backward()`` then average the optimiser's flat gradient slab across ranks."""
+        loss.backward(**kwargs)
+        if optimizer is not None:
+            self.sync_gradients(optimizer)
+
+    def sync_gradients(self, optimizer) -> None:
+        if self.world_size <= 1:
+            return
+        from sheeprl_prey_amd.parallel.flat_optim import FlatOptimizer
+
+        if isinstance(optimizer, FlatOptimizer):
+            optimizer.all_reduce_grads(self.group, self.world_size, bucket_mb=self.bucket_mb)
+            return
+        grads = [p.grad for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
+        if not grads:
+            return
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat, group=self.group)
+        flat.div_(self.world_size)
+        off = 0
+        for g in grads:
+            n = g.numel()
+            g.copy_(flat[off : off + n].view_as(g))
+            off += n
+
+    def clip_gradients(
+        self,
+        module: Optional[nn.Module] = None,
+        optimizer=None,
+        max_norm: float = 1.0,
+        norm_type: float = 2.0,
+        error_if_nonfinite: bool = False,
+    ) -> Tensor:
+        """Global-norm clip.  On a flat slab: one fused norm kernel; the scaling is folded into
+        the next optimiser step (no host sync).  Returns the pre-clip norm (device tensor)."""
+        from sheeprl_prey_amd.parallel.flat_optim import FlatOptimizer
+
+        if isinstance(optimizer, FlatOptimizer):
+            return optimizer.clip_grad_norm_(max_norm)
+        params = [p for p in (module.parameters() if module is not None else []) if p.grad is not None]
+        return torch.nn.utils.clip_grad_norm_(params, max_norm, norm_type=norm_type, error_if_nonfinite=error_if_nonfinite)
+
+    # ------------------------------------------------------------------ collectives
+    def barrier(self, *_args, **_kw) -> None:
+        if self.world_size > 1:
+            if self.backend == "nccl":
+                dist.barrier(group=self.group, device_ids=[self.device.index])
+            else:
+                dist.barrier(group=self.group)
+
+    def all_reduce(self, x: Tensor, reduce_op: str = "mean", group=None) -> Tensor:
+        group = group if group is not None else self.group
+        if self.world_size <= 1:
+            return x
+        x = x.clone()
+        dist.all_reduce(x, group=group)
+        if reduce_op in ("mean", "avg"):
+            x = x / dist.get_world_size(group)
+        return x
+
+    def all_gather(self, data: Union[Tensor, Dict[str, Tensor]], group=None, sync_grads: bool = False):
+        """Gather tensors (or dicts of tensors) into a new leading [world] dim."""
+        group = group if group is not None else self.group
+        if isinstance(data, dict):
+            return {k: self.all_gather(v, group=group) for k, v in data.items()}
+        if self.world_size <= 1:
+            return data.unsqueeze(0)
+        ws = dist.get_world_size(group)
+        t = data.contiguous()
+        if self.backend == "gloo" and t.is_cuda:
+            t = t.cpu()
+        if t.is_cuda:
+            out = torch.empty((ws,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+            dist.all_gather_into_tensor(out, t, group=group)
+        else:
+            parts = [torch.empty_like(t) for _ in range(ws)]
+            dist.all_gather(parts, t, group=group)
+            out = torch.stack(parts)
+        return out.to(data.device)
+
+    def broadcast(self, x: Tensor, src: int = 0, group=None) -> Tensor:
+        group = group if group is not None else self.group
+        if self.world_size > 1:
+            dist.broadcast(x, src=src if group is None else dist.get_global_rank(group, src), group=group)
+        return x
+
+    def broadcast_object(self, obj: Any, src: int = 0, group=None) -> Any:
+        group = group if group is not None else self.group
+        if self.world_size <= 1:
+            return obj
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=src if group is None else dist.get_global_rank(group, src), group=group)
+        return lst[0]
+
+    def gather_object(self, obj: Any, dst: int = 0, group=None) -> Optional[List[Any]]:
+        group = group if group is not None else self.group
+        if self.world_size <= 1:
+            return [obj]
+        out = [None] * dist.get_world_size(group) if self.global_rank == dst else None
+        if self.backend == "nccl":
+            # object collectives over RCCL would pickle into device tensors: use a gloo side group
+            group = self.cpu_group(group)
+        dist.gather_object(obj, out, dst=dst, group=group)
+        return out
+
+    _cpu_groups: Dict[Any, Any] = {}
+
+    def cpu_group(self, group=None):
+        key = id(group)
+        if key not in Runner._cpu_groups:
+            ranks = None if group is None else dist.get_process_group_ranks(group)
+            Runner._cpu_groups[key] = dist.new_group(ranks=ranks, backend="gloo")
+        return Runner._cpu_groups[key]
+
+    # ------------------------------------------------------------------ io / logging
+    def save(self, path: str, state: Dict[str, Any]) -> None:
+        if self.is_global_zero:
+            os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+            tmp = path + ".tmp"
+            torch.save(state, tmp)
+            os.replace(tmp, path)
+        self.barrier()
+
+    def load(self, path: str, map_location: Any = "cpu") -> Dict[str, Any]:
+        return torch.load(path, map_location=map_location, weights_only=True)
+
+    def log(self, name: str, value: Any, step: int) -> None:
+        if self.is_global_zero:
+            for lg in self._loggers:
+                lg.log_metrics({name: float(value)}, step)
+
+    def log_dict(self, metrics: Dict[str, Any], step: int) -> None:
+        if self.is_global_zero and metrics:
+            for lg in self._loggers:
+                lg.log_metrics(metrics, step)
+
+    def call(self, hook: str, **kwargs) -> None:
+        for cb in self.callbacks:
+            fn = getattr(cb, hook, None)
+            if fn is not None:
+                fn(runner=self, **kwargs)
+
+    def send_object_to_player(self, obj: Any, group) -> None:
+        """Trainer rank 1 -> player rank 0 over the {0,1} group (decoupled checkpoints)."""
+        lst = [obj]
+        dist.broadcast_object_list(lst, src=1, group=group)
