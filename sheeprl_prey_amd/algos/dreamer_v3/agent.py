@@ -1,0 +1,591 @@
+"""DreamerV3 agent (reference: ``sheeprl/algos/dreamer_v3/agent.py:28-1068``).
+
+Module structure and ``state_dict`` keys follow the reference (so checkpoints line up), but the
+hot paths are re-shaped for MI355X:
+
+* every ``Linear -> LayerNorm -> SiLU`` runs LN+SiLU as one fused HIP kernel, and the channel
+  LayerNorm of the conv stacks runs directly on NCHW (no permute copies);
+* the GRU epilogue (LN over 3H + gates) is one fused kernel;
+* unimix + straight-through one-hot sampling is one fused kernel per categorical block;
+* ``RSSM.scan_dynamic`` runs the T-step posterior scan with the step-invariant GEMM work hoisted
+  out of the loop: the embedding half of the representation layer ([T*B, 4096] x [4096, 512]) and
+  the action half of the recurrent input layer are computed for all T in one large GEMM each, so
+  the sequential loop only carries the h/z-dependent small-M GEMMs.
+"""
+from __future__ import annotations
+
+import copy
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import Tensor, nn
+from torch.distributions import Distribution, Independent, Normal, TanhTransform, TransformedDistribution
+
+from sheeprl_prey_amd import ops
+from sheeprl_prey_amd.config.instantiate import get_class
+from sheeprl_prey_amd.models.models import CNN, MLP, DeCNN, LayerNormGRUCell, MultiDecoder, MultiEncoder
+from sheeprl_prey_amd.models.world_model import WorldModel
+from sheeprl_prey_amd.utils.distribution import (
+    OneHotCategoricalStraightThroughValidateArgs,
+    OneHotCategoricalValidateArgs,
+    TruncatedNormal,
+)
+from sheeprl_prey_amd.utils.model import LayerNormChannelLast, ModuleType, cnn_forward
+from sheeprl_prey_amd.utils.utils import symlog
+
+
+def _act(name):
+    return get_class(name) if isinstance(name, str) else name
+
+
+# ------------------------------------------------------------------ Hafner initialisation
+def init_weights(m: nn.Module) -> None:
+    """Truncated-normal fan-avg init (reference ``dreamer_v3/utils.py:162-187``)."""
+    if isinstance(m, nn.Linear):
+        denoms = (m.in_features + m.out_features) / 2.0
+        std = np.sqrt(1.0 / denoms) / 0.87962566103423978
+        nn.init.trunc_normal_(m.weight.data, mean=0.0, std=std, a=-2.0 * std, b=2.0 * std)
+        if m.bias is not None:
+            m.bias.data.fill_(0.0)
+    elif isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)):
+        space = m.kernel_size[0] * m.kernel_size[1]
+        denoms = (space * m.in_channels + space * m.out_channels) / 2.0
+        std = np.sqrt(1.0 / denoms) / 0.87962566103423978
+        nn.init.trunc_normal_(m.weight.data, mean=0.0, std=std, a=-2.0, b=2.0)
+        if m.bias is not None:
+            m.bias.data.fill_(0.0)
+    elif isinstance(m, nn.LayerNorm):
+        if m.weight is not None:
+            m.weight.data.fill_(1.0)
+        if m.bias is not None:
+            m.bias.data.fill_(0.0)
+
+
+def uniform_init_weights(given_scale: float):
+    """Uniform init of output heads (reference ``dreamer_v3/utils.py:190-207``)."""
+
+    def f(m: nn.Module) -> None:
+        if isinstance(m, nn.Linear):
+            denoms = (m.in_features + m.out_features) / 2.0
+            limit = np.sqrt(3 * given_scale / denoms)
+            nn.init.uniform_(m.weight.data, a=-limit, b=limit)
+            if m.bias is not None:
+                m.bias.data.fill_(0.0)
+        elif isinstance(m, nn.LayerNorm):
+            if m.weight is not None:
+                m.weight.data.fill_(1.0)
+            if m.bias is not None:
+                m.bias.data.fill_(0.0)
+
+    return f
+
+
+# ------------------------------------------------------------------ encoders / decoders
+class CNNEncoder(nn.Module):
+    """``stages`` x (Conv k4 s2 p1 -> channel LN(eps 1e-3) -> SiLU), channels [1,2,4,8]*mult."""
+
+    def __init__(self, keys: Sequence[str], input_channels: Sequence[int], image_size: Tuple[int, int],
+                 channels_multiplier: int, layer_norm: bool = True, activation: ModuleType = nn.SiLU, stages: int = 4) -> None:
+        super().__init__()
+        self.keys = keys
+        self.input_dim = (sum(input_channels), *image_size)
+        self.model = nn.Sequential(
+            CNN(
+                input_channels=self.input_dim[0],
+                hidden_channels=[(2**i) * channels_multiplier for i in range(stages)],
+                cnn_layer=nn.Conv2d,
+                layer_args={"kernel_size": 4, "stride": 2, "padding": 1, "bias": not layer_norm},
+                activation=activation,
+                norm_layer=[LayerNormChannelLast for _ in range(stages)] if layer_norm else None,
+                norm_args=[{"normalized_shape": (2**i) * channels_multiplier, "eps": 1e-3} for i in range(stages)]
+                if layer_norm else None,
+            ),
+            nn.Flatten(-3, -1),
+        )
+        with torch.no_grad():
+            self.output_dim = self.model(torch.zeros(1, *self.input_dim)).shape[-1]
+
+    def forward(self, obs: Dict[str, Tensor]) -> Tensor:
+        x = torch.cat([obs[k] for k in self.keys], -3)
+        return cnn_forward(self.model, x, x.shape[-3:], (-1,))
+
+
+class MLPEncoder(nn.Module):
+    def __init__(self, keys: Sequence[str], input_dims: Sequence[int], mlp_layers: int = 4, dense_units: int = 512,
+                 layer_norm: bool = True, activation: ModuleType = nn.SiLU, symlog_inputs: bool = True) -> None:
+        super().__init__()
+        self.keys = keys
+        self.input_dim = sum(input_dims)
+        self.model = MLP(
+            self.input_dim, None, [dense_units] * mlp_layers, activation=activation, layer_args={"bias": not layer_norm},
+            norm_layer=[nn.LayerNorm for _ in range(mlp_layers)] if layer_norm else None,
+            norm_args=[{"normalized_shape": dense_units, "eps": 1e-3} for _ in range(mlp_layers)] if layer_norm else None,
+        )
+        self.output_dim = dense_units
+        self.symlog_inputs = symlog_inputs
+
+    def forward(self, obs: Dict[str, Tensor]) -> Tensor:
+        x = torch.cat([symlog(obs[k]) if self.symlog_inputs else obs[k] for k in self.keys], -1)
+        return self.model(x)
+
+
+class CNNDecoder(nn.Module):
+    """Linear(latent -> 8*mult*4*4) -> (stages-1) x (ConvT k4 s2 p1 -> LN -> SiLU) -> ConvT -> +0.5."""
+
+    def __init__(self, keys: Sequence[str], output_channels: Sequence[int], channels_multiplier: int,
+                 latent_state_size: int, cnn_encoder_output_dim: int, image_size: Tuple[int, int],
+                 activation: ModuleType = nn.SiLU, layer_norm: bool = True, stages: int = 4) -> None:
+        super().__init__()
+        self.keys = keys
+        self.output_channels = output_channels
+        self.cnn_encoder_output_dim = cnn_encoder_output_dim
+        self.image_size = image_size
+        self.output_dim = (sum(output_channels), *image_size)
+        self.model = nn.Sequential(
+            nn.Linear(latent_state_size, cnn_encoder_output_dim),
+            nn.Unflatten(1, (-1, 4, 4)),
+            DeCNN(
+                input_channels=(2 ** (stages - 1)) * channels_multiplier,
+                hidden_channels=[(2**i) * channels_multiplier for i in reversed(range(stages - 1))] + [self.output_dim[0]],
+                cnn_layer=nn.ConvTranspose2d,
+                layer_args=[{"kernel_size": 4, "stride": 2, "padding": 1, "bias": not layer_norm} for _ in range(stages - 1)]
+                + [{"kernel_size": 4, "stride": 2, "padding": 1}],
+                activation=[activation for _ in range(stages - 1)] + [None],
+                norm_layer=([LayerNormChannelLast for _ in range(stages - 1)] + [None]) if layer_norm else None,
+                norm_args=([{"normalized_shape": (2 ** (stages - i - 2)) * channels_multiplier, "eps": 1e-3}
+                            for i in range(stages - 1)] + [None]) if layer_norm else None,
+            ),
+        )
+
+    def forward(self, latent_states: Tensor) -> Dict[str, Tensor]:
+        out = cnn_forward(self.model, latent_states, (latent_states.shape[-1],), self.output_dim) + 0.5
+        return {k: o for k, o in zip(self.keys, torch.split(out, self.output_channels, -3))}
+
+
+class MLPDecoder(nn.Module):
+    def __init__(self, keys: Sequence[str], output_dims: Sequence[int], latent_state_size: int, mlp_layers: int = 4,
+                 dense_units: int = 512, activation: ModuleType = nn.SiLU, layer_norm: bool = True) -> None:
+        super().__init__()
+        self.output_dims = output_dims
+        self.keys = keys
+        self.model = MLP(
+            latent_state_size, None, [dense_units] * mlp_layers, activation=activation, layer_args={"bias": not layer_norm},
+            norm_layer=[nn.LayerNorm for _ in range(mlp_layers)] if layer_norm else None,
+            norm_args=[{"normalized_shape": dense_units, "eps": 1e-3} for _ in range(mlp_layers)] if layer_norm else None,
+        )
+        self.heads = nn.ModuleList([nn.Linear(dense_units, d) for d in self.output_dims])
+
+    def forward(self, latent_states: Tensor) -> Dict[str, Tensor]:
+        x = self.model(latent_states)
+        return {k: h(x) for k, h in zip(self.keys, self.heads)}
+
+
+# ------------------------------------------------------------------ recurrent model / RSSM
+class RecurrentModel(nn.Module):
+    """Linear(no bias) -> LN(1e-3) -> SiLU -> LayerNormGRUCell (reference ``agent.py:260-309``)."""
+
+    def __init__(self, input_size: int, recurrent_state_size: int, dense_units: int, activation_fn: ModuleType = nn.SiLU,
+                 layer_norm: bool = True) -> None:
+        super().__init__()
+        self.mlp = MLP(
+            input_dims=input_size, output_dim=None, hidden_sizes=[dense_units], activation=activation_fn,
+            layer_args={"bias": not layer_norm},
+            norm_layer=[nn.LayerNorm] if layer_norm else None,
+            norm_args=[{"normalized_shape": dense_units, "eps": 1e-3}] if layer_norm else None,
+        )
+        self.rnn = LayerNormGRUCell(dense_units, recurrent_state_size, bias=False, batch_first=False, layer_norm=True)
+
+    def forward(self, input: Tensor, recurrent_state: Tensor) -> Tensor:
+        return self.rnn(self.mlp(input), recurrent_state)
+
+
+def _lin(mlp: MLP, i: int) -> nn.Linear:
+    return mlp.model[i]
+
+
+class RSSM(nn.Module):
+    """Discrete RSSM with unimix categoricals (reference ``agent.py:312-455``)."""
+
+    def __init__(self, recurrent_model: nn.Module, representation_model: nn.Module, transition_model: nn.Module,
+                 distribution_cfg: Dict[str, Any], discrete: int = 32, unimix: float = 0.01) -> None:
+        super().__init__()
+        self.recurrent_model = recurrent_model
+        self.representation_model = representation_model
+        self.transition_model = transition_model
+        self.discrete = discrete
+        self.unimix = unimix
+        self.distribution_cfg = distribution_cfg
+
+    # ---- reference-semantics single steps (player / tests) ----------------------------
+    def dynamic(self, posterior: Tensor, recurrent_state: Tensor, action: Tensor, embedded_obs: Tensor, is_first: Tensor):
+        action = (1 - is_first) * action
+        recurrent_state = (1 - is_first) * recurrent_state + is_first * torch.tanh(torch.zeros_like(recurrent_state))
+        posterior = posterior.view(*posterior.shape[:-2], -1)
+        posterior = (1 - is_first) * posterior + is_first * self._transition(recurrent_state, sample_state=False)[1].view_as(posterior)
+        recurrent_state = self.recurrent_model(torch.cat((posterior, action), -1), recurrent_state)
+        prior_logits, prior = self._transition(recurrent_state)
+        posterior_logits, posterior = self._representation(recurrent_state, embedded_obs)
+        return recurrent_state, posterior, prior, posterior_logits, prior_logits
+
+    def _uniform_mix(self, logits: Tensor) -> Tensor:
+        return ops.reference.unimix_logits(logits, self.discrete, self.unimix)
+
+    def _sample(self, logits: Tensor, sample: bool = True) -> Tuple[Tensor, Tensor]:
+        mixed, st = ops.unimix_sample(logits, self.discrete, self.unimix, sample=sample)
+        return mixed, st.view(*st.shape[:-1], -1, self.discrete)
+
+    def _representation(self, recurrent_state: Tensor, embedded_obs: Tensor) -> Tuple[Tensor, Tensor]:
+        return self._sample(self.representation_model(torch.cat((recurrent_state, embedded_obs), -1)))
+
+    def _transition(self, recurrent_out: Tensor, sample_state: bool = True) -> Tuple[Tensor, Tensor]:
+        return self._sample(self.transition_model(recurrent_out), sample=sample_state)
+
+    def imagination(self, prior: Tensor, recurrent_state: Tensor, actions: Tensor) -> Tuple[Tensor, Tensor]:
+        recurrent_state = self.recurrent_model(torch.cat((prior, actions), -1), recurrent_state)
+        _, imagined_prior = self._transition(recurrent_state)
+        return imagined_prior, recurrent_state
+
+    # ---- MI355X scan: T-step posterior rollout with hoisted GEMMs --------------------
+    def _mlp_head(self, mlp: MLP, x_pre: Tensor) -> Tensor:
+        """Finish an ``MLP(hidden=[h], out=o)`` whose first Linear output is ``x_pre``."""
+        seq = mlp.model
+        x = x_pre
+        for m in list(seq)[1:]:
+            x = m(x)
+        return x
+
+    def scan_dynamic(self, embedded_obs: Tensor, actions: Tensor, is_first: Tensor, uniform: Optional[Tensor] = None):
+        """Posterior scan over ``T`` (reference loop: ``dreamer_v3.py:122-129``).
+
+        embedded_obs [T, B, E], actions [T, B, A] (already shifted), is_first [T, B, 1].
+        Returns recurrent_states [T,B,H], posteriors [T,B,S,D], posteriors_logits [T,B,S*D],
+        priors_logits [T,B,S*D]."""
+        T, B = embedded_obs.shape[:2]
+        rec_mlp = self.recurrent_model.mlp
+        gru = self.recurrent_model.rnn
+        rep, trans = self.representation_model, self.transition_model
+        H = gru.hidden_size
+        stoch = trans.model[-1].out_features
+        rec_lin = _lin(rec_mlp, 0)
+        Wz = rec_lin.weight[:, :stoch]
+        Wa = rec_lin.weight[:, stoch:]
+        rep_lin = _lin(rep, 0)
+        Wh_rep = rep_lin.weight[:, :H]
+        We_rep = rep_lin.weight[:, H:]
+        # hoisted: action half of the recurrent input layer and embedding half of the representation layer
+        act_masked = (1 - is_first) * actions
+        a_proj = F.linear(act_masked, Wa)  # [T, B, dense]
+        if rec_lin.bias is not None:
+            a_proj = a_proj + rec_lin.bias
+        e_proj = F.linear(embedded_obs, We_rep, rep_lin.bias)  # [T, B, hidden]
+        # initial state: h0 = tanh(0) = 0, z0 = mode of the transition from h0
+        h0 = torch.zeros(1, H, device=embedded_obs.device, dtype=embedded_obs.dtype)
+        z0 = self._transition(h0, sample_state=False)[1].reshape(1, -1)
+        h = torch.zeros(B, H, device=embedded_obs.device, dtype=embedded_obs.dtype)
+        z = torch.zeros(B, stoch, device=embedded_obs.device, dtype=embedded_obs.dtype)
+        if uniform is None:
+            uniform = torch.rand(T, B, stoch // self.discrete, device=embedded_obs.device)
+        hs, posts, post_logits, prior_logits = [], [], [], []
+        for t in range(T):
+            first = is_first[t]
+            h = (1 - first) * h
+            z = (1 - first) * z + first * z0
+            x = torch.addmm(a_proj[t], z, Wz.t())
+            feat = self._mlp_head(rec_mlp, x)
+            h = gru.gates(gru.project(feat, h), h)
+            pl = self._uniform_mix_fused(trans(h))
+            rep_pre = torch.addmm(e_proj[t], h, Wh_rep.t())
+            ql, zs = ops.unimix_sample(self._mlp_head(rep, rep_pre), self.discrete, self.unimix, sample=True,
+                                       uniform=uniform[t])
+            z = zs
+            hs.append(h)
+            posts.append(zs)
+            post_logits.append(ql)
+            prior_logits.append(pl)
+        recurrent_states = torch.stack(hs)
+        posteriors = torch.stack(posts).view(T, B, -1, self.discrete)
+        return recurrent_states, posteriors, torch.stack(post_logits), torch.stack(prior_logits)
+
+    def _uniform_mix_fused(self, logits: Tensor) -> Tensor:
+        """Unimix logits only (no sampling) - the prior in the posterior scan is never sampled."""
+        if ops._native(logits) and self.discrete <= 64:
+            mixed, _ = ops.unimix_sample(logits, self.discrete, self.unimix, sample=False)
+            return mixed
+        return ops.reference.unimix_logits(logits, self.discrete, self.unimix)
+
+
+# ------------------------------------------------------------------ actor
+class Actor(nn.Module):
+    """Actor MLP + heads (reference ``agent.py:602-747``): discrete -> unimix one-hot categorical
+    with straight-through samples; continuous -> trunc_normal / normal / tanh_normal."""
+
+    def __init__(self, latent_state_size: int, actions_dim: Sequence[int], is_continuous: bool,
+                 distribution_cfg: Dict[str, Any], init_std: float = 0.0, min_std: float = 0.1, dense_units: int = 1024,
+                 activation: ModuleType = nn.SiLU, mlp_layers: int = 5, layer_norm: bool = True, unimix: float = 0.01) -> None:
+        super().__init__()
+        self.distribution_cfg = distribution_cfg
+        dist = str(distribution_cfg.get("type", "auto")).lower()
+        if dist not in ("auto", "normal", "tanh_normal", "discrete", "trunc_normal"):
+            raise ValueError(
+                "The distribution must be on of: `auto`, `discrete`, `normal`, `tanh_normal` and `trunc_normal`. "
+                f"Found: {dist}"
+            )
+        if dist == "discrete" and is_continuous:
+            raise ValueError("You have choose a discrete distribution but `is_continuous` is true")
+        if dist == "auto":
+            dist = "trunc_normal" if is_continuous else "discrete"
+        self.distribution = dist
+        self.model = MLP(
+            input_dims=latent_state_size, output_dim=None, hidden_sizes=[dense_units] * mlp_layers, activation=activation,
+            flatten_dim=None, layer_args={"bias": not layer_norm},
+            norm_layer=[nn.LayerNorm for _ in range(mlp_layers)] if layer_norm else None,
+            norm_args=[{"normalized_shape": dense_units, "eps": 1e-3} for _ in range(mlp_layers)] if layer_norm else None,
+        )
+        if is_continuous:
+            self.mlp_heads = nn.ModuleList([nn.Linear(dense_units, int(np.sum(actions_dim)) * 2)])
+        else:
+            self.mlp_heads = nn.ModuleList([nn.Linear(dense_units, a) for a in actions_dim])
+        self.actions_dim = actions_dim
+        self.is_continuous = is_continuous
+        self.init_std = torch.tensor(init_std)
+        self.min_std = min_std
+        self._unimix = unimix
+
+    def _continuous_dist(self, pre: Tensor) -> Distribution:
+        va = self.distribution_cfg.get("validate_args", False)
+        mean, std = torch.chunk(pre, 2, -1)
+        if self.distribution == "tanh_normal":
+            mean = 5 * torch.tanh(mean / 5)
+            std = F.softplus(std + self.init_std) + self.min_std
+            return Independent(TransformedDistribution(Normal(mean, std), TanhTransform(), validate_args=va), 1, validate_args=va)
+        if self.distribution == "normal":
+            return Independent(Normal(mean, std, validate_args=va), 1, validate_args=va)
+        std = 2 * torch.sigmoid((std + self.init_std) / 2) + self.min_std
+        return Independent(TruncatedNormal(torch.tanh(mean), std, -1, 1, validate_args=va), 1, validate_args=va)
+
+    def forward(self, state: Tensor, is_training: bool = True, mask: Optional[Dict[str, np.ndarray]] = None):
+        out = self.model(state)
+        pre_dist = [head(out) for head in self.mlp_heads]
+        va = self.distribution_cfg.get("validate_args", False)
+        if self.is_continuous:
+            d = self._continuous_dist(pre_dist[0])
+            if is_training:
+                actions = d.rsample()
+            else:
+                sample = d.sample((100,))
+                log_prob = d.log_prob(sample)
+                actions = sample[log_prob.argmax(0)].view(1, 1, -1)
+            return (actions,), (d,)
+        actions, dists = [], []
+        for logits in pre_dist:
+            C = logits.shape[-1]
+            mixed, st = ops.unimix_sample(logits, C, self._unimix, sample=is_training)
+            dists.append(OneHotCategoricalStraightThroughValidateArgs(logits=mixed, validate_args=va))
+            actions.append(st)
+        return tuple(actions), tuple(dists)
+
+    def _uniform_mix(self, logits: Tensor) -> Tensor:
+        return ops.reference.unimix_logits(logits, logits.shape[-1], self._unimix)
+
+
+class MinedojoActor(Actor):
+    """Actor with MineDojo action masks (reference ``agent.py:750-828``)."""
+
+    def forward(self, state: Tensor, is_training: bool = True, mask: Optional[Dict[str, np.ndarray]] = None):
+        out = self.model(state)
+        logits_list = [head(out) for head in self.mlp_heads]
+        va = self.distribution_cfg.get("validate_args", False)
+        actions, dists = [], []
+        functional_action = None
+        for i, logits in enumerate(logits_list):
+            if mask is not None:
+                if i == 0:
+                    logits[torch.logical_not(mask["mask_action_type"].expand_as(logits))] = -torch.inf
+                elif i == 1:
+                    m = mask["mask_craft_smelt"].expand_as(logits)
+                    craft = (functional_action == 15).unsqueeze(-1)
+                    logits = torch.where(craft & torch.logical_not(m), torch.full_like(logits, -torch.inf), logits)
+                elif i == 2:
+                    me = mask["mask_destroy"].expand_as(logits)
+                    mp = mask["mask_equip/place"].expand_as(logits)
+                    fa = functional_action.unsqueeze(-1)
+                    bad = ((fa == 16) | (fa == 17)) & torch.logical_not(mp) | (fa == 18) & torch.logical_not(me)
+                    logits = torch.where(bad, torch.full_like(logits, -torch.inf), logits)
+            d = OneHotCategoricalStraightThroughValidateArgs(logits=logits, validate_args=va)
+            dists.append(d)
+            actions.append(d.rsample() if is_training else d.mode)
+            if functional_action is None:
+                functional_action = actions[0].argmax(dim=-1)
+        return tuple(actions), tuple(dists)
+
+
+# ------------------------------------------------------------------ player
+class PlayerDV3(nn.Module):
+    """Env-interaction model: keeps (h, z, a) per env on the device (reference ``agent.py:458-599``)."""
+
+    def __init__(self, encoder: nn.Module, rssm: RSSM, actor: nn.Module, actions_dim: Sequence[int], expl_amount: float,
+                 num_envs: int, stochastic_size: int, recurrent_state_size: int, device="cpu", discrete_size: int = 32) -> None:
+        super().__init__()
+        self.encoder = encoder
+        self.rssm = rssm
+        self.actor = actor
+        self.device = device
+        self.expl_amount = expl_amount
+        self.actions_dim = actions_dim
+        self.stochastic_size = stochastic_size
+        self.discrete_size = discrete_size
+        self.recurrent_state_size = recurrent_state_size
+        self.num_envs = num_envs
+
+    @torch.no_grad()
+    def init_states(self, reset_envs: Optional[Sequence[int]] = None) -> None:
+        if reset_envs is None or len(reset_envs) == 0:
+            self.actions = torch.zeros(1, self.num_envs, int(np.sum(self.actions_dim)), device=self.device)
+            self.recurrent_state = torch.tanh(torch.zeros(1, self.num_envs, self.recurrent_state_size, device=self.device))
+            self.stochastic_state = self.rssm._transition(self.recurrent_state, sample_state=False)[1].reshape(1, self.num_envs, -1)
+        else:
+            idx = torch.as_tensor(list(reset_envs), device=self.device)
+            self.actions[:, idx] = 0
+            self.recurrent_state[:, idx] = torch.tanh(torch.zeros_like(self.recurrent_state[:, idx]))
+            self.stochastic_state[:, idx] = self.rssm._transition(self.recurrent_state[:, idx], sample_state=False)[1].reshape(
+                1, len(reset_envs), -1)
+
+    def get_exploration_action(self, obs: Dict[str, Tensor], is_continuous: bool, mask=None) -> Tuple[Tensor, ...]:
+        actions = self.get_greedy_action(obs, mask=mask)
+        if is_continuous:
+            self.actions = torch.cat(actions, -1)
+            if self.expl_amount > 0.0:
+                self.actions = torch.clip(Normal(self.actions, self.expl_amount).sample(), -1, 1)
+            expl = [self.actions]
+        else:
+            expl = []
+            for act in actions:
+                if self.expl_amount > 0.0:
+                    rnd = F.one_hot(torch.randint(0, act.shape[-1], act.shape[:-1], device=act.device), act.shape[-1]).to(act)
+                    act = torch.where(torch.rand(act.shape[:1], device=self.device).view(-1, *([1] * (act.dim() - 1))) < self.expl_amount, rnd, act)
+                expl.append(act)
+            self.actions = torch.cat(expl, -1)
+        return tuple(expl)
+
+    def get_greedy_action(self, obs: Dict[str, Tensor], is_training: bool = True, mask=None) -> Sequence[Tensor]:
+        embedded_obs = self.encoder(obs)
+        self.recurrent_state = self.rssm.recurrent_model(torch.cat((self.stochastic_state, self.actions), -1), self.recurrent_state)
+        _, self.stochastic_state = self.rssm._representation(self.recurrent_state, embedded_obs)
+        self.stochastic_state = self.stochastic_state.view(*self.stochastic_state.shape[:-2], self.stochastic_size * self.discrete_size)
+        actions, _ = self.actor(torch.cat((self.stochastic_state, self.recurrent_state), -1), is_training, mask)
+        self.actions = torch.cat(actions, -1)
+        return actions
+
+
+# ------------------------------------------------------------------ factory
+def build_models(runner, actions_dim: Sequence[int], is_continuous: bool, cfg: Dict[str, Any], obs_space,
+                 world_model_state=None, actor_state=None, critic_state=None, target_critic_state=None):
+    """Build world model, actor, critic, target critic (reference ``agent.py:831-1068``)."""
+    wm_cfg = cfg.algo.world_model
+    actor_cfg = cfg.algo.actor
+    critic_cfg = cfg.algo.critic
+    recurrent_state_size = wm_cfg.recurrent_model.recurrent_state_size
+    stochastic_size = wm_cfg.stochastic_size * wm_cfg.discrete_size
+    latent_state_size = stochastic_size + recurrent_state_size
+    cnn_stages = int(np.log2(cfg.env.screen_size) - np.log2(4))
+    cnn_keys_enc = list(cfg.cnn_keys.encoder or [])
+    mlp_keys_enc = list(cfg.mlp_keys.encoder or [])
+    cnn_encoder = (
+        CNNEncoder(keys=cnn_keys_enc, input_channels=[int(np.prod(obs_space[k].shape[:-2])) for k in cnn_keys_enc],
+                   image_size=obs_space[cnn_keys_enc[0]].shape[-2:],
+                   channels_multiplier=wm_cfg.encoder.cnn_channels_multiplier, layer_norm=wm_cfg.encoder.layer_norm,
+                   activation=_act(wm_cfg.encoder.cnn_act), stages=cnn_stages)
+        if cnn_keys_enc else None
+    )
+    mlp_encoder = (
+        MLPEncoder(keys=mlp_keys_enc, input_dims=[obs_space[k].shape[0] for k in mlp_keys_enc],
+                   mlp_layers=wm_cfg.encoder.mlp_layers, dense_units=wm_cfg.encoder.dense_units,
+                   activation=_act(wm_cfg.encoder.dense_act), layer_norm=wm_cfg.encoder.layer_norm)
+        if mlp_keys_enc else None
+    )
+    encoder = MultiEncoder(cnn_encoder, mlp_encoder)
+    rm_cfg = dict(wm_cfg.recurrent_model)
+    recurrent_model = RecurrentModel(input_size=int(sum(actions_dim) + stochastic_size),
+                                     recurrent_state_size=rm_cfg["recurrent_state_size"], dense_units=rm_cfg["dense_units"],
+                                     layer_norm=rm_cfg.get("layer_norm", True))
+    rep_cfg, tr_cfg = wm_cfg.representation_model, wm_cfg.transition_model
+    representation_model = MLP(
+        input_dims=recurrent_state_size + encoder.cnn_output_dim + encoder.mlp_output_dim, output_dim=stochastic_size,
+        hidden_sizes=[rep_cfg.hidden_size], activation=_act(rep_cfg.dense_act), flatten_dim=None,
+        norm_layer=[nn.LayerNorm] if rep_cfg.layer_norm else None,
+        norm_args=[{"normalized_shape": rep_cfg.hidden_size}] if rep_cfg.layer_norm else None,
+    )
+    transition_model = MLP(
+        input_dims=recurrent_state_size, output_dim=stochastic_size, hidden_sizes=[tr_cfg.hidden_size],
+        activation=_act(tr_cfg.dense_act), flatten_dim=None,
+        norm_layer=[nn.LayerNorm] if tr_cfg.layer_norm else None,
+        norm_args=[{"normalized_shape": tr_cfg.hidden_size}] if tr_cfg.layer_norm else None,
+    )
+    rssm = RSSM(recurrent_model.apply(init_weights), representation_model.apply(init_weights),
+                transition_model.apply(init_weights), cfg.distribution, discrete=wm_cfg.discrete_size, unimix=cfg.algo.unimix)
+    cnn_keys_dec = list(cfg.cnn_keys.decoder or [])
+    mlp_keys_dec = list(cfg.mlp_keys.decoder or [])
+    cnn_decoder = (
+        CNNDecoder(keys=cnn_keys_dec, output_channels=[int(np.prod(obs_space[k].shape[:-2])) for k in cnn_keys_dec],
+                   channels_multiplier=wm_cfg.observation_model.cnn_channels_multiplier, latent_state_size=latent_state_size,
+                   cnn_encoder_output_dim=cnn_encoder.output_dim, image_size=obs_space[cnn_keys_dec[0]].shape[-2:],
+                   activation=_act(wm_cfg.observation_model.cnn_act), layer_norm=wm_cfg.observation_model.layer_norm,
+                   stages=cnn_stages)
+        if cnn_keys_dec else None
+    )
+    mlp_decoder = (
+        MLPDecoder(keys=mlp_keys_dec, output_dims=[obs_space[k].shape[0] for k in mlp_keys_dec],
+                   latent_state_size=latent_state_size, mlp_layers=wm_cfg.observation_model.mlp_layers,
+                   dense_units=wm_cfg.observation_model.dense_units, activation=_act(wm_cfg.observation_model.dense_act),
+                   layer_norm=wm_cfg.observation_model.layer_norm)
+        if mlp_keys_dec else None
+    )
+    observation_model = MultiDecoder(cnn_decoder, mlp_decoder)
+
+    def head(out_dim, c):
+        n = c.mlp_layers
+        return MLP(input_dims=latent_state_size, output_dim=out_dim, hidden_sizes=[c.dense_units] * n,
+                   activation=_act(c.dense_act), flatten_dim=None,
+                   norm_layer=[nn.LayerNorm for _ in range(n)] if c.layer_norm else None,
+                   norm_args=[{"normalized_shape": c.dense_units} for _ in range(n)] if c.layer_norm else None)
+
+    reward_model = head(wm_cfg.reward_model.bins, wm_cfg.reward_model)
+    continue_model = head(1, wm_cfg.discount_model)
+    world_model = WorldModel(encoder.apply(init_weights), rssm, observation_model.apply(init_weights),
+                             reward_model.apply(init_weights), continue_model.apply(init_weights))
+    actor_cls = get_class(cfg.algo.actor.cls)
+    actor = actor_cls(latent_state_size=latent_state_size, actions_dim=actions_dim, is_continuous=is_continuous,
+                      init_std=actor_cfg.init_std, min_std=actor_cfg.min_std, dense_units=actor_cfg.dense_units,
+                      activation=_act(actor_cfg.dense_act), mlp_layers=actor_cfg.mlp_layers,
+                      distribution_cfg=cfg.distribution, layer_norm=actor_cfg.layer_norm, unimix=cfg.algo.unimix)
+    critic = head(critic_cfg.bins, critic_cfg)
+    actor.apply(init_weights)
+    critic.apply(init_weights)
+    if cfg.algo.hafner_initialization:
+        actor.mlp_heads.apply(uniform_init_weights(1.0))
+        critic.model[-1].apply(uniform_init_weights(0.0))
+        rssm.transition_model.model[-1].apply(uniform_init_weights(1.0))
+        rssm.representation_model.model[-1].apply(uniform_init_weights(1.0))
+        world_model.reward_model.model[-1].apply(uniform_init_weights(0.0))
+        world_model.continue_model.model[-1].apply(uniform_init_weights(1.0))
+        if mlp_decoder is not None:
+            mlp_decoder.heads.apply(uniform_init_weights(1.0))
+        if cnn_decoder is not None:
+            cnn_decoder.model[-1].model[-1].apply(uniform_init_weights(1.0))
+    if world_model_state:
+        world_model.load_state_dict(world_model_state)
+    if actor_state:
+        actor.load_state_dict(actor_state)
+    if critic_state:
+        critic.load_state_dict(critic_state)
+    world_model = runner.setup_module(world_model)
+    actor = runner.setup_module(actor)
+    critic = runner.setup_module(critic)
+    target_critic = copy.deepcopy(critic)
+    if target_critic_state:
+        target_critic.load_state_dict(target_critic_state)
+    for p in target_critic.parameters():
+        p.requires_grad_(False)
+    return world_model, actor, critic, target_critic

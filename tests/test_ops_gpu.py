@@ -1,0 +1,194 @@
+"""Numerics of every HIP kernel against the fp32 eager reference (forward and backward)."""
+import pytest
+import torch
+
+from sheeprl_prey_amd import ops
+from sheeprl_prey_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _grads(fn, *inputs):
+    ins = [x.detach().clone().requires_grad_(x.is_floating_point()) for x in inputs]
+    out = fn(*ins)
+    if isinstance(out, tuple):
+        out = out[0]
+    gen = torch.Generator(device=out.device).manual_seed(1234)
+    g = torch.randn(out.shape, device=out.device, generator=gen)
+    (out * g).sum().backward()
+    return out.detach(), [x.grad for x in ins if x.requires_grad]
+
+
+def _close(a, b, rtol=1e-4, atol=1e-5):
+    torch.testing.assert_close(a, b, rtol=rtol, atol=atol)
+
+
+def test_extension_loaded():
+    assert ops.native_available()
+    assert "_C" in ops._ext().__file__
+
+
+@pytest.mark.parametrize("N", [8, 64, 512, 1000, 1536, 4096, 12288])
+@pytest.mark.parametrize("act", ["none", "silu", "elu", "relu", "tanh"])
+def test_ln_act(N, act):
+    torch.manual_seed(0)
+    x = torch.randn(37, N, device=DEV) * 3 + 1
+    w = torch.randn(N, device=DEV)
+    b = torch.randn(N, device=DEV)
+    torch.manual_seed(1)
+    y1, g1 = _grads(lambda x, w, b: ops.ln_act(x, w, b, 1e-3, act), x, w, b)
+    torch.manual_seed(1)
+    y2, g2 = _grads(lambda x, w, b: ref.ln_act(x, w, b, 1e-3, act), x, w, b)
+    _close(y1, y2)
+    for a, c in zip(g1, g2):
+        _close(a, c, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("shape", [(4, 32, 32, 32), (3, 7, 5, 9), (2, 256, 4, 4)])
+def test_ln_act_nchw(shape):
+    torch.manual_seed(0)
+    x = torch.randn(*shape, device=DEV)
+    w = torch.randn(shape[1], device=DEV)
+    b = torch.randn(shape[1], device=DEV)
+    torch.manual_seed(1)
+    y1, g1 = _grads(lambda x, w, b: ops.ln_act_nchw(x, w, b, 1e-3, "silu"), x, w, b)
+    torch.manual_seed(1)
+    y2, g2 = _grads(lambda x, w, b: ref.ln_act_nchw(x, w, b, 1e-3, "silu"), x, w, b)
+    _close(y1, y2)
+    for a, c in zip(g1, g2):
+        _close(a, c, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("H", [8, 200, 512, 1024, 4096])
+def test_ln_gru(H):
+    torch.manual_seed(0)
+    x = torch.randn(19, 3 * H, device=DEV)
+    h = torch.randn(19, H, device=DEV)
+    w = torch.randn(3 * H, device=DEV)
+    b = torch.randn(3 * H, device=DEV)
+    torch.manual_seed(1)
+    y1, g1 = _grads(lambda *a: ops.ln_gru(*a, 1e-5), x, h, w, b)
+    torch.manual_seed(1)
+    y2, g2 = _grads(lambda *a: ref.ln_gru(*a, 1e-5), x, h, w, b)
+    _close(y1, y2)
+    for a, c in zip(g1, g2):
+        _close(a, c, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("C,G", [(32, 32), (9, 1), (18, 1), (2, 3), (64, 2)])
+@pytest.mark.parametrize("alpha", [0.0, 0.01])
+def test_unimix_sample(C, G, alpha):
+    torch.manual_seed(0)
+    logits = torch.randn(50, G * C, device=DEV) * 2
+    u = torch.rand(50 * G, device=DEV)
+    m1, s1 = ops.unimix_sample(logits, C, alpha, sample=True, uniform=u)
+    m2, s2 = ref.unimix_sample(logits, C, alpha, uniform=u, sample=True)
+    _close(m1, m2, rtol=1e-4, atol=1e-5)
+    assert torch.equal(s1.detach().view(-1, C).argmax(-1), s2.detach().view(-1, C).argmax(-1))
+    _close(s1.detach(), s2.detach(), rtol=0, atol=1e-6)
+    # gradients through both outputs (KL path + straight-through path)
+    lg1 = logits.clone().requires_grad_()
+    lg2 = logits.clone().requires_grad_()
+    gm = torch.randn_like(logits)
+    gs = torch.randn_like(logits)
+    a1, b1 = ops.unimix_sample(lg1, C, alpha, sample=True, uniform=u)
+    ((a1 * gm).sum() + (b1 * gs).sum()).backward()
+    a2, b2 = ref.unimix_sample(lg2, C, alpha, uniform=u, sample=True)
+    ((a2 * gm).sum() + (b2 * gs).sum()).backward()
+    _close(lg1.grad, lg2.grad, rtol=1e-3, atol=1e-4)
+    # mode
+    _, mode = ops.unimix_sample(logits, C, alpha, sample=False)
+    _, mode_ref = ref.unimix_sample(logits, C, alpha, sample=False)
+    assert torch.equal(mode.view(-1, C).argmax(-1), mode_ref.view(-1, C).argmax(-1))
+
+
+def test_unimix_sample_distribution():
+    torch.manual_seed(0)
+    logits = torch.tensor([[0.0, 1.0, 2.0, -1.0]], device=DEV).repeat(200000, 1)
+    _, s = ops.unimix_sample(logits, 4, 0.01, sample=True)
+    freq = s.mean(0)
+    p = ref.unimix_logits(logits[:1], 4, 0.01).softmax(-1)[0]
+    _close(freq, p, rtol=0, atol=5e-3)
+
+
+@pytest.mark.parametrize("K", [255, 41, 64, 300])
+def test_twohot(K):
+    torch.manual_seed(0)
+    logits = torch.randn(333, K, device=DEV)
+    y = torch.randn(333, device=DEV) * 50
+    y[:5] = torch.tensor([0.0, 1e9, -1e9, 3.0, -0.5], device=DEV)
+    bins = ops.twohot_bins(K, device=DEV)
+    l1, g1 = _grads(lambda l: ops.twohot_nll(l, y), logits)
+    l2, g2 = _grads(lambda l: ref.twohot_nll(l, y, bins), logits)
+    _close(l1, l2, rtol=1e-4, atol=1e-4)
+    _close(g1[0], g2[0], rtol=1e-3, atol=1e-4)
+    m1, h1 = _grads(lambda l: ops.twohot_mean(l), logits)
+    m2, h2 = _grads(lambda l: ref.twohot_mean(l, bins).unsqueeze(-1), logits)
+    _close(m1, m2, rtol=1e-3, atol=1e-4)
+    _close(h1[0], h2[0], rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("G,C", [(32, 32), (4, 8), (30, 1 + 1)])
+def test_kl_balance(G, C):
+    torch.manual_seed(0)
+    a = torch.randn(77, G * C, device=DEV)
+    b = torch.randn(77, G * C, device=DEV)
+    a[:3] = b[:3]  # below free nats -> zero grads
+    l1, g1 = _grads(lambda a, b: ops.kl_balance(a, b, G, C, 0.5, 0.1, 1.0), a, b)
+    l2, g2 = _grads(lambda a, b: ref.kl_balance(a, b, G, C, 0.5, 0.1, 1.0), a, b)
+    _close(l1, l2, rtol=1e-4, atol=1e-4)
+    for x, y in zip(g1, g2):
+        _close(x, y, rtol=1e-3, atol=1e-5)
+
+
+def test_lambda_returns():
+    torch.manual_seed(0)
+    r = torch.randn(15, 1024, 1, device=DEV)
+    v = torch.randn(15, 1024, 1, device=DEV)
+    c = torch.rand(15, 1024, 1, device=DEV)
+    y1, g1 = _grads(lambda r, v, c: ops.lambda_returns(r, v, c, 0.95), r, v, c)
+    y2, g2 = _grads(lambda r, v, c: ref.lambda_returns(r, v, c, 0.95), r, v, c)
+    _close(y1, y2)
+    for a, b in zip(g1, g2):
+        _close(a, b, rtol=1e-4, atol=1e-5)
+
+
+def test_gae():
+    torch.manual_seed(0)
+    r = torch.randn(128, 8, 1, device=DEV)
+    v = torch.randn(128, 8, 1, device=DEV)
+    d = (torch.rand(128, 8, 1, device=DEV) < 0.05).float()
+    nv = torch.randn(8, 1, device=DEV)
+    ret1, adv1 = ops.gae_scan(r, v, d, nv, 0.99, 0.95)
+    ret2, adv2 = ref.gae(r.cpu(), v.cpu(), d.cpu(), nv.cpu(), 0.99, 0.95)
+    _close(ret1.cpu(), ret2)
+    _close(adv1.cpu(), adv2)
+
+
+@pytest.mark.parametrize("wd,decoupled,clip", [(0.0, False, 0.0), (0.01, False, 1.0), (0.01, True, 0.5)])
+def test_flat_adam_matches_torch(wd, decoupled, clip):
+    import copy
+
+    from sheeprl_prey_amd.parallel.flat_optim import FlatAdam
+
+    torch.manual_seed(0)
+    m1 = torch.nn.Sequential(torch.nn.Linear(33, 65), torch.nn.Tanh(), torch.nn.Linear(65, 7)).to(DEV)
+    m2 = copy.deepcopy(m1)
+    cls = torch.optim.AdamW if decoupled else torch.optim.Adam
+    o1 = cls(m1.parameters(), lr=1e-2, eps=1e-5, weight_decay=wd)
+    o2 = FlatAdam(m2.parameters(), lr=1e-2, eps=1e-5, weight_decay=wd, decoupled=decoupled)
+    for _ in range(6):
+        x = torch.randn(16, 33, device=DEV)
+        for m, o in ((m1, o1), (m2, o2)):
+            o.zero_grad()
+            m(x).pow(2).mean().backward()
+            if clip:
+                if o is o1:
+                    torch.nn.utils.clip_grad_norm_(m.parameters(), clip)
+                else:
+                    o.clip_grad_norm_(clip)
+            o.step()
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        _close(a, b, rtol=1e-5, atol=1e-6)
