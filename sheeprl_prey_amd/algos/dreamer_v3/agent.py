@@ -263,6 +263,16 @@ class RSSM(nn.Module):
         Returns recurrent_states [T,B,H], posteriors [T,B,S,D], posteriors_logits [T,B,S*D],
         priors_logits [T,B,S*D]."""
         T, B = embedded_obs.shape[:2]
+        if ops._native(embedded_obs) and getattr(self, "fused_scan", True):
+            from sheeprl_prey_amd.ops.rssm import fused_scan, fused_scan_supported
+
+            if fused_scan_supported(self):
+                H = self.recurrent_model.rnn.hidden_size
+                h0 = torch.zeros(1, H, device=embedded_obs.device, dtype=embedded_obs.dtype)
+                with torch.no_grad():
+                    z0 = self._transition(h0, sample_state=False)[1].reshape(-1)
+                hs, post, post_logits, prior_logits = fused_scan(self, embedded_obs, actions, is_first, z0, uniform)
+                return hs, post.view(T, B, -1, self.discrete), post_logits, prior_logits
         rec_mlp = self.recurrent_model.mlp
         gru = self.recurrent_model.rnn
         rep, trans = self.representation_model, self.transition_model

@@ -10,19 +10,25 @@ void launch_flat_grad_norm(const float*, int64_t, float*, int, float*, float*, f
 void launch_flat_advance(float*, hipStream_t);
 void launch_flat_adam(float*, const float*, float*, float*, const float*, int64_t, float, float, float, float, float, int,
                       hipStream_t);
-bool launch_ln_act_fwd(const float*, const float*, const float*, float*, float*, float*, int, int, float, int, hipStream_t);
-int ln_act_bwd_grid(int);
-bool launch_ln_act_bwd(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
-                       float*, float*, float*, int, int, int, hipStream_t);
+bool launch_ln_act_fwd(const float*, int, float*, int, const float*, const float*, float*, float*, int, int, int, float, int,
+                       hipStream_t);
+int ln_bwd_grid(int, int, int);
+bool launch_ln_act_bwd(const float*, int, const float*, int, float*, int, const float*, const float*, const float*,
+                       const float*, float*, float*, float*, float*, int, int, int, int, hipStream_t);
+void launch_colsum2(const float*, const float*, float*, float*, int, int, int, hipStream_t);
+void launch_rssm_mask_fwd(const float*, int, const float*, const float*, const float*, float*, int, float*, int, int, int,
+                          hipStream_t);
+void launch_rssm_mask_bwd(const float*, int, const float*, int, const float*, const float*, float*, float*, int, int, int,
+                          hipStream_t);
 void launch_ln_nchw_fwd(const float*, const float*, const float*, float*, float*, float*, int, int, int, float, int,
                         hipStream_t);
 int ln_nchw_splits(int, int);
 void launch_ln_nchw_bwd(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
                         float*, float*, float*, int, int, int, int, hipStream_t);
-bool launch_ln_gru_fwd(const float*, const float*, const float*, const float*, float*, float*, float*, int, int, float,
+bool launch_ln_gru_fwd(const float*, const float*, int, const float*, const float*, float*, float*, float*, int, int, float,
                        hipStream_t);
 int ln_gru_bwd_grid(int);
-bool launch_ln_gru_bwd(const float*, const float*, const float*, const float*, const float*, const float*, const float*,
+bool launch_ln_gru_bwd(const float*, const float*, int, const float*, const float*, const float*, const float*, const float*,
                        float*, float*, float*, float*, float*, float*, int, int, hipStream_t);
 bool launch_unimix_sample_fwd(const float*, const float*, float*, float*, int, int, float, hipStream_t);
 bool launch_unimix_sample_bwd(const float*, const float*, const float*, float*, int, int, float, hipStream_t);
@@ -89,8 +95,8 @@ std::vector<torch::Tensor> ln_act_fwd(torch::Tensor x, c10::optional<torch::Tens
   auto y = torch::empty_like(x);
   auto mean = torch::empty({M}, x.options());
   auto rstd = torch::empty({M}, x.options());
-  bool ok = launch_ln_act_fwd(x.data_ptr<float>(), opt_ptr(gamma), opt_ptr(beta), y.data_ptr<float>(),
-                              mean.data_ptr<float>(), rstd.data_ptr<float>(), M, N, (float)eps, (int)act, cur_stream());
+  bool ok = launch_ln_act_fwd(x.data_ptr<float>(), N, y.data_ptr<float>(), N, opt_ptr(gamma), opt_ptr(beta),
+                              mean.data_ptr<float>(), rstd.data_ptr<float>(), M, N, 1, (float)eps, (int)act, cur_stream());
   TORCH_CHECK(ok, "ln_act_fwd: unsupported feature size ", N);
   return {y, mean, rstd};
 }
@@ -105,17 +111,17 @@ std::vector<torch::Tensor> ln_act_bwd(torch::Tensor x, torch::Tensor dy, c10::op
   auto dx = torch::empty_like(x);
   bool affine = gamma.has_value() && gamma->defined();
   torch::Tensor pdg, pdb, dg, db;
-  const int grid = ln_act_bwd_grid(M);
+  const int grid = ln_bwd_grid(M, N, 1);
   if (affine) {
     pdg = torch::empty({grid, N}, x.options());
     pdb = torch::empty({grid, N}, x.options());
     dg = torch::empty({N}, x.options());
     db = torch::empty({N}, x.options());
   }
-  bool ok = launch_ln_act_bwd(x.data_ptr<float>(), dy.data_ptr<float>(), opt_ptr(gamma), opt_ptr(beta),
-                              mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr<float>(),
+  bool ok = launch_ln_act_bwd(x.data_ptr<float>(), N, dy.data_ptr<float>(), N, dx.data_ptr<float>(), N, opt_ptr(gamma),
+                              opt_ptr(beta), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                               affine ? pdg.data_ptr<float>() : nullptr, affine ? pdb.data_ptr<float>() : nullptr,
-                              affine ? dg.data_ptr<float>() : nullptr, affine ? db.data_ptr<float>() : nullptr, M, N,
+                              affine ? dg.data_ptr<float>() : nullptr, affine ? db.data_ptr<float>() : nullptr, M, N, 1,
                               (int)act, cur_stream());
   TORCH_CHECK(ok, "ln_act_bwd: unsupported feature size ", N);
   return {dx, dg, db};
@@ -170,7 +176,7 @@ std::vector<torch::Tensor> ln_gru_fwd(torch::Tensor x, torch::Tensor h, torch::T
   auto hn = torch::empty_like(h);
   auto mean = torch::empty({M}, x.options());
   auto rstd = torch::empty({M}, x.options());
-  bool ok = launch_ln_gru_fwd(x.data_ptr<float>(), h.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+  bool ok = launch_ln_gru_fwd(x.data_ptr<float>(), h.data_ptr<float>(), H, gamma.data_ptr<float>(), beta.data_ptr<float>(),
                               hn.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(), M, H, (float)eps,
                               cur_stream());
   TORCH_CHECK(ok, "ln_gru_fwd: unsupported hidden size ", H);
@@ -189,7 +195,7 @@ std::vector<torch::Tensor> ln_gru_bwd(torch::Tensor x, torch::Tensor h, torch::T
   auto pdb = torch::empty({grid, 3 * H}, x.options());
   auto dg = torch::empty({3 * H}, x.options());
   auto db = torch::empty({3 * H}, x.options());
-  bool ok = launch_ln_gru_bwd(x.data_ptr<float>(), h.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+  bool ok = launch_ln_gru_bwd(x.data_ptr<float>(), h.data_ptr<float>(), H, gamma.data_ptr<float>(), beta.data_ptr<float>(),
                               mean.data_ptr<float>(), rstd.data_ptr<float>(), dhn.data_ptr<float>(), dx.data_ptr<float>(),
                               dh.data_ptr<float>(), pdg.data_ptr<float>(), pdb.data_ptr<float>(), dg.data_ptr<float>(),
                               db.data_ptr<float>(), M, H, cur_stream());
@@ -333,6 +339,81 @@ std::vector<torch::Tensor> gae(torch::Tensor rew, torch::Tensor val, torch::Tens
   return {ret, adv};
 }
 
+
+// ------------------------------------------------------------------ low-level entry points (RSSM scan)
+// Pointers come from (possibly offset) views; strides are explicit so outputs can land in slices
+// of persistent buffers.  No allocation happens here (hipGraph-friendly).
+const float* fp(const torch::Tensor& t) { return t.defined() ? t.data_ptr<float>() : nullptr; }
+float* mp(const torch::Tensor& t) { return t.defined() ? t.data_ptr<float>() : nullptr; }
+const float* ofp(const c10::optional<torch::Tensor>& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
+float* omp(const c10::optional<torch::Tensor>& t) { return t.has_value() && t->defined() ? t->data_ptr<float>() : nullptr; }
+
+void ln_act_fwd_into(torch::Tensor x, int64_t ldx, torch::Tensor y, int64_t ldy, c10::optional<torch::Tensor> gamma,
+                     c10::optional<torch::Tensor> beta, torch::Tensor mean, torch::Tensor rstd, int64_t M, int64_t N,
+                     int64_t G, double eps, int64_t act) {
+  TORCH_CHECK(x.is_cuda() && y.is_cuda(), "ln_act_fwd_into: GPU tensors required");
+  bool ok = launch_ln_act_fwd(fp(x), ldx, mp(y), ldy, ofp(gamma), ofp(beta), mp(mean), mp(rstd), M, N, G, (float)eps,
+                              (int)act, cur_stream());
+  TORCH_CHECK(ok, "ln_act_fwd_into: unsupported N/G ", N, "/", G);
+}
+
+void ln_act_bwd_into(torch::Tensor x, int64_t ldx, torch::Tensor dy, int64_t lddy, torch::Tensor dx, int64_t lddx,
+                     c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, torch::Tensor mean,
+                     torch::Tensor rstd, c10::optional<torch::Tensor> pdg, c10::optional<torch::Tensor> pdb,
+                     c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, int64_t M, int64_t N,
+                     int64_t G, int64_t act) {
+  bool ok = launch_ln_act_bwd(fp(x), ldx, fp(dy), lddy, mp(dx), lddx, ofp(gamma), ofp(beta), fp(mean), fp(rstd), omp(pdg),
+                              omp(pdb), omp(dgamma), omp(dbeta), M, N, G, (int)act, cur_stream());
+  TORCH_CHECK(ok, "ln_act_bwd_into: unsupported N/G ", N, "/", G);
+}
+
+int64_t ln_bwd_grid_py(int64_t M, int64_t N, int64_t G) { return ln_bwd_grid(M, N, G); }
+int64_t ln_gru_bwd_grid_py(int64_t M) { return ln_gru_bwd_grid(M); }
+
+void ln_gru_fwd_into(torch::Tensor x, torch::Tensor h, int64_t ldh, torch::Tensor gamma, torch::Tensor beta,
+                     torch::Tensor hn, torch::Tensor mean, torch::Tensor rstd, int64_t M, int64_t H, double eps) {
+  bool ok = launch_ln_gru_fwd(fp(x), fp(h), ldh, fp(gamma), fp(beta), mp(hn), mp(mean), mp(rstd), M, H, (float)eps,
+                              cur_stream());
+  TORCH_CHECK(ok, "ln_gru_fwd_into: unsupported H ", H);
+}
+
+void ln_gru_bwd_into(torch::Tensor x, torch::Tensor h, int64_t ldh, torch::Tensor gamma, torch::Tensor beta,
+                     torch::Tensor mean, torch::Tensor rstd, torch::Tensor dhn, torch::Tensor dx, torch::Tensor dh,
+                     torch::Tensor pdg, torch::Tensor pdb, c10::optional<torch::Tensor> dgamma,
+                     c10::optional<torch::Tensor> dbeta, int64_t M, int64_t H) {
+  bool ok = launch_ln_gru_bwd(fp(x), fp(h), ldh, fp(gamma), fp(beta), fp(mean), fp(rstd), fp(dhn), mp(dx), mp(dh), mp(pdg),
+                              mp(pdb), omp(dgamma), omp(dbeta), M, H, cur_stream());
+  TORCH_CHECK(ok, "ln_gru_bwd_into: unsupported H ", H);
+}
+
+void colsum2(torch::Tensor pa, torch::Tensor pb, torch::Tensor oa, torch::Tensor ob, int64_t rows, int64_t N, int64_t G) {
+  launch_colsum2(fp(pa), fp(pb), mp(oa), mp(ob), rows, N, G, cur_stream());
+}
+
+void rssm_mask_fwd(c10::optional<torch::Tensor> h, int64_t ldh_in, c10::optional<torch::Tensor> z, torch::Tensor first,
+                   torch::Tensor z0, torch::Tensor hout, int64_t ldh_out, torch::Tensor zout, int64_t B, int64_t H, int64_t S) {
+  launch_rssm_mask_fwd(ofp(h), ldh_in, ofp(z), fp(first), fp(z0), mp(hout), ldh_out, mp(zout), B, H, S, cur_stream());
+}
+
+void rssm_mask_bwd(torch::Tensor dha, int64_t ldha, torch::Tensor dhb, int64_t ldhb, torch::Tensor dz, torch::Tensor first,
+                   torch::Tensor dh_acc, torch::Tensor dz_acc, int64_t B, int64_t H, int64_t S) {
+  launch_rssm_mask_bwd(fp(dha), ldha, fp(dhb), ldhb, fp(dz), fp(first), mp(dh_acc), mp(dz_acc), B, H, S, cur_stream());
+}
+
+void unimix_sample_fwd_into(torch::Tensor logits, c10::optional<torch::Tensor> uniform, torch::Tensor mixed,
+                            torch::Tensor sample, int64_t C, double alpha) {
+  const int R = logits.numel() / C;
+  bool ok = launch_unimix_sample_fwd(fp(logits), ofp(uniform), mp(mixed), mp(sample), R, (int)C, (float)alpha, cur_stream());
+  TORCH_CHECK(ok, "unimix_sample_fwd_into: too many classes ", C);
+}
+
+void unimix_sample_bwd_into(torch::Tensor logits, c10::optional<torch::Tensor> g_mixed, c10::optional<torch::Tensor> g_sample,
+                            torch::Tensor dl, int64_t C, double alpha) {
+  const int R = logits.numel() / C;
+  bool ok = launch_unimix_sample_bwd(fp(logits), ofp(g_mixed), ofp(g_sample), mp(dl), R, (int)C, (float)alpha, cur_stream());
+  TORCH_CHECK(ok, "unimix_sample_bwd_into: too many classes ", C);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -357,4 +438,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lambda_fwd", &lambda_fwd);
   m.def("lambda_bwd", &lambda_bwd);
   m.def("gae", &gae);
+  m.def("ln_act_fwd_into", &ln_act_fwd_into);
+  m.def("ln_act_bwd_into", &ln_act_bwd_into);
+  m.def("ln_bwd_grid", &ln_bwd_grid_py);
+  m.def("ln_gru_bwd_grid", &ln_gru_bwd_grid_py);
+  m.def("ln_gru_fwd_into", &ln_gru_fwd_into);
+  m.def("ln_gru_bwd_into", &ln_gru_bwd_into);
+  m.def("colsum2", &colsum2);
+  m.def("rssm_mask_fwd", &rssm_mask_fwd);
+  m.def("rssm_mask_bwd", &rssm_mask_bwd);
+  m.def("unimix_sample_fwd_into", &unimix_sample_fwd_into);
+  m.def("unimix_sample_bwd_into", &unimix_sample_bwd_into);
 }

@@ -9,7 +9,7 @@
 namespace srl {
 
 template <int MAXH>
-__global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict__ x, const float* __restrict__ h,
+__global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict__ x, const float* __restrict__ h, int ldh,
                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
                                                          float* __restrict__ hn, float* __restrict__ mean_out,
                                                          float* __restrict__ rstd_out, int M, int H, float eps) {
@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict
         float r = sigmoidf_(zr);
         float c = tanhf(r * zc);
         float u = sigmoidf_(zu - 1.f);
-        float hp = h[(int64_t)row * H + j];
+        float hp = h[(int64_t)row * ldh + j];
         hn[(int64_t)row * H + j] = u * c + (1.f - u) * hp;
       }
     }
@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict
 }
 
 template <int MAXH>
-__global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict__ x, const float* __restrict__ h,
+__global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict__ x, const float* __restrict__ h, int ldh,
                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
                                                          const float* __restrict__ dhn, float* __restrict__ dx,
@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict
         float r = sigmoidf_(zr);
         float c = tanhf(r * zc);
         float u = sigmoidf_(zu - 1.f);
-        float hp = h[(int64_t)row * H + j];
+        float hp = h[(int64_t)row * ldh + j];
         float g_out = dhn[(int64_t)row * H + j];
         dh[(int64_t)row * H + j] = g_out * (1.f - u);
         float du = g_out * (c - hp);
@@ -138,19 +138,6 @@ __global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict
   }
 }
 
-__global__ void __launch_bounds__(256) colsum2_gru_kernel(const float* __restrict__ pa, const float* __restrict__ pb,
-                                                          float* __restrict__ oa, float* __restrict__ ob, int rows, int N) {
-  int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float a = 0.f, b = 0.f;
-  for (int r = 0; r < rows; ++r) {
-    a += pa[(int64_t)r * N + n];
-    b += pb[(int64_t)r * N + n];
-  }
-  oa[n] = a;
-  ob[n] = b;
-}
-
 }  // namespace srl
 
 using namespace srl;
@@ -163,34 +150,37 @@ static int gru_maxh(int H) {
   return 0;
 }
 
-bool launch_ln_gru_fwd(const float* x, const float* h, const float* gamma, const float* beta, float* hn, float* mean,
-                       float* rstd, int M, int H, float eps, hipStream_t st) {
+bool launch_ln_gru_fwd(const float* x, const float* h, int ldh, const float* gamma, const float* beta, float* hn,
+                       float* mean, float* rstd, int M, int H, float eps, hipStream_t st) {
   int mh = gru_maxh(H);
-  dim3 g(M), b(256);
+  dim3 g(M < 8192 ? M : 8192), b(256);
   switch (mh) {
-    case 2: hipLaunchKernelGGL(ln_gru_fwd_kernel<2>, g, b, 0, st, x, h, gamma, beta, hn, mean, rstd, M, H, eps); return true;
-    case 4: hipLaunchKernelGGL(ln_gru_fwd_kernel<4>, g, b, 0, st, x, h, gamma, beta, hn, mean, rstd, M, H, eps); return true;
-    case 8: hipLaunchKernelGGL(ln_gru_fwd_kernel<8>, g, b, 0, st, x, h, gamma, beta, hn, mean, rstd, M, H, eps); return true;
-    case 16: hipLaunchKernelGGL(ln_gru_fwd_kernel<16>, g, b, 0, st, x, h, gamma, beta, hn, mean, rstd, M, H, eps); return true;
+    case 2: hipLaunchKernelGGL(ln_gru_fwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps); return true;
+    case 4: hipLaunchKernelGGL(ln_gru_fwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps); return true;
+    case 8: hipLaunchKernelGGL(ln_gru_fwd_kernel<8>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps); return true;
+    case 16: hipLaunchKernelGGL(ln_gru_fwd_kernel<16>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps); return true;
     default: return false;
   }
 }
 
 int ln_gru_bwd_grid(int M) { return M < 256 ? M : 256; }
 
-bool launch_ln_gru_bwd(const float* x, const float* h, const float* gamma, const float* beta, const float* mean,
+void launch_colsum2(const float* pa, const float* pb, float* oa, float* ob, int rows, int N, int G, hipStream_t st);
+
+// pdg/pdb: [grid, 3H] partial rows; reduced into dgamma/dbeta when those are non-null.
+bool launch_ln_gru_bwd(const float* x, const float* h, int ldh, const float* gamma, const float* beta, const float* mean,
                        const float* rstd, const float* dhn, float* dx, float* dh, float* pdg, float* pdb, float* dgamma,
                        float* dbeta, int M, int H, hipStream_t st) {
   int mh = gru_maxh(H);
   int grid = ln_gru_bwd_grid(M);
   dim3 g(grid), b(256);
   switch (mh) {
-    case 2: hipLaunchKernelGGL(ln_gru_bwd_kernel<2>, g, b, 0, st, x, h, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
-    case 4: hipLaunchKernelGGL(ln_gru_bwd_kernel<4>, g, b, 0, st, x, h, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
-    case 8: hipLaunchKernelGGL(ln_gru_bwd_kernel<8>, g, b, 0, st, x, h, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
-    case 16: hipLaunchKernelGGL(ln_gru_bwd_kernel<16>, g, b, 0, st, x, h, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
+    case 2: hipLaunchKernelGGL(ln_gru_bwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
+    case 4: hipLaunchKernelGGL(ln_gru_bwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
+    case 8: hipLaunchKernelGGL(ln_gru_bwd_kernel<8>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
+    case 16: hipLaunchKernelGGL(ln_gru_bwd_kernel<16>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
     default: return false;
   }
-  hipLaunchKernelGGL(colsum2_gru_kernel, dim3(cdiv(3 * H, 256)), dim3(256), 0, st, pdg, pdb, dgamma, dbeta, grid, 3 * H);
+  if (dgamma) launch_colsum2(pdg, pdb, dgamma, dbeta, grid, 3 * H, 1, st);
   return true;
 }

@@ -1,46 +1,177 @@
 #include "hip/hip_runtime.h"
 // Fused LayerNorm + activation kernels (fp32).
-//  * row-major:  y[m, :] = act(gamma * (x - mu) * rstd + beta)   (nn.Linear -> LayerNorm -> act)
+//  * row-major:  y[r, :] = act(gamma * (x - mu) * rstd + beta)   (nn.Linear -> LayerNorm -> act)
+//    - arbitrary input/output row strides (the RSSM scan writes straight into a concat buffer)
+//    - "grouped" mode: M = Bn*G input rows ordered (b, g) with per-group gamma/beta, written
+//      group-major (g, b) so the next per-group GEMM reads contiguous operands
 //  * NCHW:       normalise over C at every pixel directly in NCHW (the reference permutes to
 //                NHWC and back around nn.LayerNorm: LayerNormChannelLast, utils/model.py:225-235;
 //                here consecutive threads own consecutive pixels, so the C-strided reads coalesce).
-// Backward recomputes x_hat from the saved (mu, rstd); dgamma/dbeta are reduced
-// deterministically: per-block partial rows, then a column-sum kernel.
+// Rows with N <= 2048 are processed one wave per row, 4 waves per block; wider rows use the whole
+// 256-thread block per row.  Backward recomputes x_hat from the saved (mu, rstd); dgamma/dbeta are
+// reduced deterministically (per-block partial rows -> column sums), optionally into per-call
+// "slots" so a time loop can defer the reduction to one kernel after the loop.
 #include "common.h"
 
 namespace srl {
 
-template <int NW, int MAXV>
-__global__ void __launch_bounds__(64 * NW) ln_act_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
-                                                             const float* __restrict__ beta, float* __restrict__ y,
-                                                             float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                             int M, int N, float eps, int act) {
-  __shared__ float red[NW];
-  const int T = 64 * NW;
-  for (int row = blockIdx.x; row < M; row += gridDim.x) {
-    const float* xr = x + (int64_t)row * N;
+// ------------------------------------------------------------------ wave-per-row (N <= 64*MAXV)
+template <int MAXV>
+__global__ void __launch_bounds__(256) ln_wave_fwd_kernel(const float* __restrict__ x, int ldx, float* __restrict__ y,
+                                                          int ldy, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* __restrict__ mean_out,
+                                                          float* __restrict__ rstd_out, int M, int N, int G, float eps,
+                                                          int act) {
+  const int lane = threadIdx.x & 63;
+  const int nwaves = gridDim.x * 4;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int Bn = M / G;
+  const int g = gw % G;
+  const float* gam = gamma ? gamma + (int64_t)g * N : nullptr;
+  const float* bet = beta ? beta + (int64_t)g * N : nullptr;
+  for (int b = gw / G; b < Bn; b += nwaves / G) {
+    const int r = b * G + g;
+    const float* xr = x + (int64_t)r * ldx;
     float v[MAXV];
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      int idx = threadIdx.x + k * T;
+      int idx = lane + 64 * k;
       v[k] = idx < N ? xr[idx] : 0.f;
       s += v[k];
     }
-    const float mu = block_sum<NW>(s, red) / N;
+    const float mu = wave_sum(s) / N;
     float q = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      int idx = threadIdx.x + k * T;
+      int idx = lane + 64 * k;
       float d = idx < N ? v[k] - mu : 0.f;
       q += d * d;
     }
-    const float var = block_sum<NW>(q, red) / N;
-    const float rs = rsqrtf(var + eps);
-    float* yr = y + (int64_t)row * N;
+    const float rs = rsqrtf(wave_sum(q) / N + eps);
+    const int ro = (G == 1) ? r : g * Bn + b;
+    float* yr = y + (int64_t)ro * ldy;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      int idx = threadIdx.x + k * T;
+      int idx = lane + 64 * k;
+      if (idx < N) {
+        float z = (v[k] - mu) * rs;
+        if (gam) z = z * gam[idx] + bet[idx];
+        yr[idx] = act_fwd(z, act);
+      }
+    }
+    if (lane == 0) {
+      mean_out[r] = mu;
+      rstd_out[r] = rs;
+    }
+  }
+}
+
+template <int MAXV>
+__global__ void __launch_bounds__(256) ln_wave_bwd_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ dy,
+                                                          int lddy, float* __restrict__ dx, int lddx,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                          float* __restrict__ pdg, float* __restrict__ pdb, int M, int N,
+                                                          int G, int act) {
+  __shared__ float red_g[4][64 * MAXV];
+  __shared__ float red_b[4][64 * MAXV];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nwaves = gridDim.x * 4;
+  const int gw = blockIdx.x * 4 + w;
+  const int Bn = M / G;
+  const int g = gw % G;
+  const float* gam = gamma ? gamma + (int64_t)g * N : nullptr;
+  const float* bet = beta ? beta + (int64_t)g * N : nullptr;
+  float ag[MAXV], ab[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) ag[k] = ab[k] = 0.f;
+  for (int b = gw / G; b < Bn; b += nwaves / G) {
+    const int r = b * G + g;
+    const int ro = (G == 1) ? r : g * Bn + b;
+    const float* xr = x + (int64_t)r * ldx;
+    const float* dyr = dy + (int64_t)ro * lddy;
+    const float mu = mean[r], rs = rstd[r];
+    float xh[MAXV], dxh[MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      int idx = lane + 64 * k;
+      xh[k] = dxh[k] = 0.f;
+      if (idx < N) {
+        float h = (xr[idx] - mu) * rs;
+        float gg = gam ? gam[idx] : 1.f;
+        float z = gam ? h * gg + bet[idx] : h;
+        float dz = dyr[idx] * act_grad(z, act);
+        ag[k] += dz * h;
+        ab[k] += dz;
+        xh[k] = h;
+        dxh[k] = dz * gg;
+        s1 += dxh[k];
+        s2 += dxh[k] * h;
+      }
+    }
+    const float m1 = wave_sum(s1) / N;
+    const float m2 = wave_sum(s2) / N;
+    float* dxr = dx + (int64_t)r * lddx;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      int idx = lane + 64 * k;
+      if (idx < N) dxr[idx] = rs * (dxh[k] - m1 - xh[k] * m2);
+    }
+  }
+  if (pdg) {
+    // block partial per group: waves w with (w % G) == g'
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      red_g[w][lane + 64 * k] = ag[k];
+      red_b[w][lane + 64 * k] = ab[k];
+    }
+    __syncthreads();
+    for (int gg = 0; gg < G; ++gg) {
+      for (int idx = threadIdx.x; idx < N; idx += 256) {
+        float a = 0.f, bb = 0.f;
+        for (int ww = gg; ww < 4; ww += G) {
+          a += red_g[ww][idx];
+          bb += red_b[ww][idx];
+        }
+        pdg[((int64_t)blockIdx.x * G + gg) * N + idx] = a;
+        pdb[((int64_t)blockIdx.x * G + gg) * N + idx] = bb;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ block-per-row (wide rows, G == 1)
+template <int MAXV>
+__global__ void __launch_bounds__(256) ln_block_fwd_kernel(const float* __restrict__ x, int ldx, float* __restrict__ y,
+                                                           int ldy, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float* __restrict__ mean_out,
+                                                           float* __restrict__ rstd_out, int M, int N, float eps, int act) {
+  __shared__ float red[4];
+  for (int row = blockIdx.x; row < M; row += gridDim.x) {
+    const float* xr = x + (int64_t)row * ldx;
+    float v[MAXV];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      int idx = threadIdx.x + k * 256;
+      v[k] = idx < N ? xr[idx] : 0.f;
+      s += v[k];
+    }
+    const float mu = block_sum<4>(s, red) / N;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      int idx = threadIdx.x + k * 256;
+      float d = idx < N ? v[k] - mu : 0.f;
+      q += d * d;
+    }
+    const float rs = rsqrtf(block_sum<4>(q, red) / N + eps);
+    float* yr = y + (int64_t)row * ldy;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      int idx = threadIdx.x + k * 256;
       if (idx < N) {
         float z = (v[k] - mu) * rs;
         if (gamma) z = z * gamma[idx] + beta[idx];
@@ -54,54 +185,53 @@ __global__ void __launch_bounds__(64 * NW) ln_act_fwd_kernel(const float* __rest
   }
 }
 
-template <int NW, int MAXV>
-__global__ void __launch_bounds__(64 * NW) ln_act_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                                             const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                             const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                             float* __restrict__ dx, float* __restrict__ pdg,
-                                                             float* __restrict__ pdb, int M, int N, int act) {
-  __shared__ float red[NW];
-  const int T = 64 * NW;
+template <int MAXV>
+__global__ void __launch_bounds__(256) ln_block_bwd_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ dy,
+                                                           int lddy, float* __restrict__ dx, int lddx,
+                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                           float* __restrict__ pdg, float* __restrict__ pdb, int M, int N,
+                                                           int act) {
+  __shared__ float red[4];
   float ag[MAXV], ab[MAXV];
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) ag[k] = ab[k] = 0.f;
   for (int row = blockIdx.x; row < M; row += gridDim.x) {
-    const float* xr = x + (int64_t)row * N;
-    const float* dyr = dy + (int64_t)row * N;
+    const float* xr = x + (int64_t)row * ldx;
+    const float* dyr = dy + (int64_t)row * lddy;
     const float mu = mean[row], rs = rstd[row];
     float xh[MAXV], dxh[MAXV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      int idx = threadIdx.x + k * T;
-      xh[k] = 0.f;
-      dxh[k] = 0.f;
+      int idx = threadIdx.x + k * 256;
+      xh[k] = dxh[k] = 0.f;
       if (idx < N) {
         float h = (xr[idx] - mu) * rs;
-        float g = gamma ? gamma[idx] : 1.f;
-        float z = gamma ? h * g + beta[idx] : h;
+        float gg = gamma ? gamma[idx] : 1.f;
+        float z = gamma ? h * gg + beta[idx] : h;
         float dz = dyr[idx] * act_grad(z, act);
         ag[k] += dz * h;
         ab[k] += dz;
         xh[k] = h;
-        dxh[k] = dz * g;
+        dxh[k] = dz * gg;
         s1 += dxh[k];
         s2 += dxh[k] * h;
       }
     }
-    const float m1 = block_sum<NW>(s1, red) / N;
-    const float m2 = block_sum<NW>(s2, red) / N;
-    float* dxr = dx + (int64_t)row * N;
+    const float m1 = block_sum<4>(s1, red) / N;
+    const float m2 = block_sum<4>(s2, red) / N;
+    float* dxr = dx + (int64_t)row * lddx;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      int idx = threadIdx.x + k * T;
+      int idx = threadIdx.x + k * 256;
       if (idx < N) dxr[idx] = rs * (dxh[k] - m1 - xh[k] * m2);
     }
   }
   if (pdg) {
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      int idx = threadIdx.x + k * T;
+      int idx = threadIdx.x + k * 256;
       if (idx < N) {
         pdg[(int64_t)blockIdx.x * N + idx] = ag[k];
         pdb[(int64_t)blockIdx.x * N + idx] = ab[k];
@@ -110,18 +240,29 @@ __global__ void __launch_bounds__(64 * NW) ln_act_bwd_kernel(const float* __rest
   }
 }
 
-// out_a[n] = sum_b pa[b, n]; out_b likewise (deterministic order)
+// out_a[g*N + n] = sum_{p : p % G == g} pa[p, n]  (deterministic; 4 row-slices per 64 columns)
 __global__ void __launch_bounds__(256) colsum2_kernel(const float* __restrict__ pa, const float* __restrict__ pb,
-                                                      float* __restrict__ oa, float* __restrict__ ob, int rows, int N) {
-  int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
+                                                      float* __restrict__ oa, float* __restrict__ ob, int rows, int N,
+                                                      int G) {
+  __shared__ float sa[4][64], sb[4][64];
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int slice = threadIdx.x >> 6;
+  const int g = blockIdx.y;
   float a = 0.f, b = 0.f;
-  for (int r = 0; r < rows; ++r) {
-    a += pa[(int64_t)r * N + n];
-    b += pb[(int64_t)r * N + n];
+  if (n < N) {
+    for (int p = g + slice * G; p < rows; p += 4 * G) {
+      a += pa[(int64_t)p * N + n];
+      b += pb[(int64_t)p * N + n];
+    }
   }
-  oa[n] = a;
-  ob[n] = b;
+  sa[slice][threadIdx.x & 63] = a;
+  sb[slice][threadIdx.x & 63] = b;
+  __syncthreads();
+  if (slice == 0 && n < N) {
+    int c = threadIdx.x & 63;
+    oa[(int64_t)g * N + n] = sa[0][c] + sa[1][c] + sa[2][c] + sa[3][c];
+    ob[(int64_t)g * N + n] = sb[0][c] + sb[1][c] + sb[2][c] + sb[3][c];
+  }
 }
 
 // ---------------------------------------------------------------- NCHW (normalise over C)
@@ -214,46 +355,82 @@ __global__ void __launch_bounds__(256) ln_nchw_dgb_kernel(const float* __restric
 
 using namespace srl;
 
-#define LN_DISPATCH(NW, MAXV, KERNEL, ...) \
-  hipLaunchKernelGGL((KERNEL<NW, MAXV>), dim3(grid), dim3(64 * NW), 0, st, __VA_ARGS__)
-
-// Picks (waves per row, values per thread).  Returns false if N is unsupported.
-static bool ln_config(int N, int& nw, int& maxv) {
-  if (N <= 256) { nw = 1; maxv = 4; }
-  else if (N <= 512) { nw = 1; maxv = 8; }
-  else if (N <= 1024) { nw = 2; maxv = 8; }
-  else if (N <= 2048) { nw = 4; maxv = 8; }
-  else if (N <= 4096) { nw = 4; maxv = 16; }
-  else if (N <= 12288) { nw = 4; maxv = 48; }
+// ---------------------------------------------------------------- launch configuration (shared with bindings)
+// mode 0: wave-per-row with MAXV = 64*k; mode 1: block-per-row.  Returns false if unsupported.
+static bool ln_mode(int N, int G, int& mode, int& maxv) {
+  if (N <= 256) { mode = 0; maxv = 4; }
+  else if (N <= 512) { mode = 0; maxv = 8; }
+  else if (N <= 1024) { mode = 0; maxv = 16; }
+  else if (N <= 2048) { mode = 0; maxv = 32; }
+  else if (G != 1) return false;
+  else if (N <= 4096) { mode = 1; maxv = 16; }
+  else if (N <= 12288) { mode = 1; maxv = 48; }
   else return false;
   return true;
 }
 
-bool launch_ln_act_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd, int M,
-                       int N, float eps, int act, hipStream_t st) {
-  int nw, maxv;
-  if (!ln_config(N, nw, maxv)) return false;
-  int grid = M;
-#define F(NW_, MV_) if (nw == NW_ && maxv == MV_) { LN_DISPATCH(NW_, MV_, ln_act_fwd_kernel, x, gamma, beta, y, mean, rstd, M, N, eps, act); return true; }
-  F(1, 4) F(1, 8) F(2, 8) F(4, 8) F(4, 16) F(4, 48)
+// Number of blocks (== partial rows per group) the backward uses for M rows.
+int ln_bwd_grid(int M, int N, int G) {
+  int mode, maxv;
+  if (!ln_mode(N, G, mode, maxv)) return 0;
+  if (mode == 0) {
+    int waves = M;                      // one wave per row
+    int g = cdiv(waves, 4);
+    if (g > 256) g = 256;
+    if (g < 1) g = 1;
+    if (G > 1 && (g * 4) % G) g += 1;   // nwaves must be a multiple of G
+    return g;
+  }
+  return M < 512 ? M : 512;
+}
+
+bool launch_ln_act_fwd(const float* x, int ldx, float* y, int ldy, const float* gamma, const float* beta, float* mean,
+                       float* rstd, int M, int N, int G, float eps, int act, hipStream_t st) {
+  int mode, maxv;
+  if (!ln_mode(N, G, mode, maxv)) return false;
+  if (mode == 0) {
+    int grid = cdiv(M, 4);
+    if (grid > 4096) grid = 4096;
+    if (G > 1 && (grid * 4) % G) grid += 1;
+#define F(MV) if (maxv == MV) { hipLaunchKernelGGL(ln_wave_fwd_kernel<MV>, dim3(grid), dim3(256), 0, st, x, ldx, y, ldy, gamma, beta, mean, rstd, M, N, G, eps, act); return true; }
+    F(4) F(8) F(16) F(32)
 #undef F
+  } else {
+    int grid = M < 8192 ? M : 8192;
+#define F(MV) if (maxv == MV) { hipLaunchKernelGGL(ln_block_fwd_kernel<MV>, dim3(grid), dim3(256), 0, st, x, ldx, y, ldy, gamma, beta, mean, rstd, M, N, eps, act); return true; }
+    F(16) F(48)
+#undef F
+  }
   return false;
 }
 
-int ln_act_bwd_grid(int M) { return M < 512 ? M : 512; }
+void launch_colsum2(const float* pa, const float* pb, float* oa, float* ob, int rows, int N, int G, hipStream_t st) {
+  hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(N, 64), G), dim3(256), 0, st, pa, pb, oa, ob, rows, N, G);
+}
 
-bool launch_ln_act_bwd(const float* x, const float* dy, const float* gamma, const float* beta, const float* mean,
-                       const float* rstd, float* dx, float* pdg, float* pdb, float* dgamma, float* dbeta, int M, int N,
-                       int act, hipStream_t st) {
-  int nw, maxv;
-  if (!ln_config(N, nw, maxv)) return false;
-  int grid = ln_act_bwd_grid(M);
-#define F(NW_, MV_) if (nw == NW_ && maxv == MV_) { LN_DISPATCH(NW_, MV_, ln_act_bwd_kernel, x, dy, gamma, beta, mean, rstd, dx, pdg, pdb, M, N, act); goto reduce; }
-  F(1, 4) F(1, 8) F(2, 8) F(4, 8) F(4, 16) F(4, 48)
+// pdg/pdb: [grid*G, N] partial rows (required if gamma != null).  If dgamma != null the partials
+// are reduced into dgamma/dbeta [G, N] right away; otherwise the caller reduces them later.
+bool launch_ln_act_bwd(const float* x, int ldx, const float* dy, int lddy, float* dx, int lddx, const float* gamma,
+                       const float* beta, const float* mean, const float* rstd, float* pdg, float* pdb, float* dgamma,
+                       float* dbeta, int M, int N, int G, int act, hipStream_t st) {
+  int mode, maxv;
+  if (!ln_mode(N, G, mode, maxv)) return false;
+  const int grid = ln_bwd_grid(M, N, G);
+  float* pg = gamma ? pdg : nullptr;
+  float* pb = gamma ? pdb : nullptr;
+  if (mode == 0) {
+#define F(MV) if (maxv == MV) { hipLaunchKernelGGL(ln_wave_bwd_kernel<MV>, dim3(grid), dim3(256), 0, st, x, ldx, dy, lddy, dx, lddx, gamma, beta, mean, rstd, pg, pb, M, N, G, act); goto reduce; }
+    F(4) F(8) F(16) F(32)
 #undef F
-  return false;
+    return false;
+  } else {
+#define F(MV) if (maxv == MV) { hipLaunchKernelGGL(ln_block_bwd_kernel<MV>, dim3(grid), dim3(256), 0, st, x, ldx, dy, lddy, dx, lddx, gamma, beta, mean, rstd, pg, pb, M, N, act); goto reduce; }
+    F(16) F(48)
+#undef F
+    return false;
+  }
 reduce:
-  if (dgamma) hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(N, 256)), dim3(256), 0, st, pdg, pdb, dgamma, dbeta, grid, N);
+  if (gamma && dgamma) launch_colsum2(pdg, pdb, dgamma, dbeta, grid * G, N, G, st);
   return true;
 }
 
@@ -281,6 +458,6 @@ void launch_ln_nchw_bwd(const float* x, const float* dy, const float* gamma, con
     int S = ln_nchw_splits(B, HW);
     hipLaunchKernelGGL(ln_nchw_dgb_kernel, dim3(C, S), dim3(256), 0, st, x, dy, gamma, beta, mean, rstd, pdg, pdb, B, C, HW,
                        act);
-    hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(C, 256)), dim3(256), 0, st, pdg, pdb, dgamma, dbeta, S, C);
+    launch_colsum2(pdg, pdb, dgamma, dbeta, S, C, 1, st);
   }
 }

@@ -1,0 +1,208 @@
+"""Fused DreamerV3 posterior scan (forward + BPTT) for GPU tensors.
+
+The reference runs ``rssm.dynamic`` T=64 times under autograd (``dreamer_v3.py:122-129``): every
+step re-records ~20 kernels, and the backward adds a small-M weight-gradient GEMM plus a gradient
+accumulation add per weight per step.  Here one autograd node owns the whole scan:
+
+forward, per step (9 launches):
+  mask(h,z | is_first) -> x = z'Wz^T + a_proj[t] -> LN+SiLU (written into the [h', feat] buffer)
+  -> gx = [h', feat] Wg^T -> LN-GRU gates -> u = h [Wt1; Wr1]^T + P[t] (prior|posterior first layers
+  as ONE GEMM) -> grouped LN+SiLU (two parameter sets, group-major output) -> two second-layer GEMMs as
+  one batched GEMM -> unimix + straight-through sample for prior and posterior in one kernel.
+backward, per step (9 launches): the adjoint chain only (activation gradients);
+after the loop every weight gradient is ONE large GEMM over the stacked T*B rows and every LayerNorm
+parameter gradient ONE column reduction over per-step partial slots.
+
+The step-invariant work (action half of the recurrent input layer, embedding half of the posterior
+layer) is hoisted by the caller (``RSSM.scan_dynamic``) and enters as ``a_proj`` / ``P`` inputs, so
+autograd handles their (large, efficient) GEMM backward.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+from torch import Tensor
+
+from sheeprl_prey_amd.ops.reference import ACTS
+
+
+class RSSMScanFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a_proj, P, is_first, uniform, z0, Wz, ln1_w, ln1_b, Wg, lng_w, lng_b, W1, ln2_w, ln2_b, W2, b2, meta):
+        from sheeprl_prey_amd.ops import _ext
+
+        C = _ext()
+        T, B, D = a_proj.shape
+        S = Wz.shape[1]
+        H = lng_w.shape[0] // 3
+        hid = W1.shape[0] // 2
+        disc, alpha, eps1, epsg, eps2, act1, act2 = meta
+        dev, f32 = a_proj.device, torch.float32
+        HD = H + D
+        first = is_first.reshape(T, B).contiguous()
+        cat = torch.empty(T, B, HD, device=dev, dtype=f32)
+        zm = torch.empty(T, B, S, device=dev, dtype=f32)
+        xr = torch.empty(T, B, D, device=dev, dtype=f32)
+        m1 = torch.empty(T, B, device=dev, dtype=f32)
+        r1 = torch.empty(T, B, device=dev, dtype=f32)
+        gx = torch.empty(T, B, 3 * H, device=dev, dtype=f32)
+        mg = torch.empty(T, B, device=dev, dtype=f32)
+        rg = torch.empty(T, B, device=dev, dtype=f32)
+        hs = torch.empty(T, B, H, device=dev, dtype=f32)
+        u = torch.empty(T, B, 2 * hid, device=dev, dtype=f32)
+        v = torch.empty(T, 2, B, hid, device=dev, dtype=f32)
+        m2 = torch.empty(T, 2 * B, device=dev, dtype=f32)
+        r2 = torch.empty(T, 2 * B, device=dev, dtype=f32)
+        logits = torch.empty(T, 2, B, S, device=dev, dtype=f32)
+        mixed = torch.empty(T, 2, B, S, device=dev, dtype=f32)
+        samples = torch.empty(T, 2, B, S, device=dev, dtype=f32)
+        Wz_t, Wg_t, W1_t, W2_t = Wz.t(), Wg.t(), W1.t(), W2.transpose(1, 2)
+        h_prev = None
+        z_prev = None
+        for t in range(T):
+            C.rssm_mask_fwd(h_prev, H, z_prev, first[t], z0, cat[t], HD, zm[t], B, H, S)
+            torch.addmm(a_proj[t], zm[t], Wz_t, out=xr[t])
+            C.ln_act_fwd_into(xr[t], D, cat[t, :, H:], HD, ln1_w, ln1_b, m1[t], r1[t], B, D, 1, eps1, act1)
+            torch.mm(cat[t], Wg_t, out=gx[t])
+            C.ln_gru_fwd_into(gx[t], cat[t], HD, lng_w, lng_b, hs[t], mg[t], rg[t], B, H, epsg)
+            torch.addmm(P[t], hs[t], W1_t, out=u[t])
+            C.ln_act_fwd_into(u[t], hid, v[t], hid, ln2_w, ln2_b, m2[t], r2[t], 2 * B, hid, 2, eps2, act2)
+            torch.baddbmm(b2, v[t], W2_t, out=logits[t])
+            C.unimix_sample_fwd_into(logits[t], uniform[t], mixed[t], samples[t], disc, alpha)
+            h_prev = hs[t]
+            z_prev = samples[t, 1]
+        ctx.save_for_backward(first, Wz, ln1_w, ln1_b, Wg, lng_w, lng_b, W1, ln2_w, ln2_b, W2,
+                              cat, zm, xr, m1, r1, gx, mg, rg, hs, u, v, m2, r2, logits)
+        ctx.meta = meta
+        ctx.dims = (T, B, D, S, H, hid)
+        post = samples[:, 1].contiguous()
+        return hs, post, mixed[:, 1].contiguous(), mixed[:, 0].contiguous()
+
+    @staticmethod
+    def backward(ctx, d_hs, d_post, d_post_mixed, d_prior_mixed):
+        from sheeprl_prey_amd.ops import _ext
+
+        C = _ext()
+        (first, Wz, ln1_w, ln1_b, Wg, lng_w, lng_b, W1, ln2_w, ln2_b, W2,
+         cat, zm, xr, m1, r1, gx, mg, rg, hs, u, v, m2, r2, logits) = ctx.saved_tensors
+        disc, alpha, eps1, epsg, eps2, act1, act2 = ctx.meta
+        T, B, D, S, H, hid = ctx.dims
+        dev, f32 = hs.device, torch.float32
+        HD = H + D
+        DH = d_hs.clone() if d_hs is not None else torch.zeros(T, B, H, device=dev, dtype=f32)
+        DH = DH.contiguous()
+        dsamp = torch.zeros(T, 2, B, S, device=dev, dtype=f32)
+        if d_post is not None:
+            dsamp[:, 1].copy_(d_post)
+        dmixed = torch.zeros(T, 2, B, S, device=dev, dtype=f32)
+        if d_prior_mixed is not None:
+            dmixed[:, 0].copy_(d_prior_mixed)
+        if d_post_mixed is not None:
+            dmixed[:, 1].copy_(d_post_mixed)
+        dlog = torch.empty(T, 2, B, S, device=dev, dtype=f32)
+        dv = torch.empty(T, 2, B, hid, device=dev, dtype=f32)
+        du = torch.empty(T, B, 2 * hid, device=dev, dtype=f32)
+        dgx = torch.empty(T, B, 3 * H, device=dev, dtype=f32)
+        dx = torch.empty(T, B, D, device=dev, dtype=f32)
+        dcat = torch.empty(B, HD, device=dev, dtype=f32)
+        dhp = torch.empty(B, H, device=dev, dtype=f32)
+        dzp = torch.empty(B, S, device=dev, dtype=f32)
+        g1 = C.ln_bwd_grid(B, D, 1)
+        g2 = C.ln_bwd_grid(2 * B, hid, 2)
+        gg = C.ln_gru_bwd_grid(B)
+        p1g = torch.empty(T, g1, D, device=dev, dtype=f32)
+        p1b = torch.empty_like(p1g)
+        p2g = torch.empty(T, g2 * 2, hid, device=dev, dtype=f32)
+        p2b = torch.empty_like(p2g)
+        pgg = torch.empty(T, gg, 3 * H, device=dev, dtype=f32)
+        pgb = torch.empty_like(pgg)
+        for t in range(T - 1, -1, -1):
+            C.unimix_sample_bwd_into(logits[t], dmixed[t], dsamp[t], dlog[t], disc, alpha)
+            torch.bmm(dlog[t], W2, out=dv[t])
+            C.ln_act_bwd_into(u[t], hid, dv[t], hid, du[t], hid, ln2_w, ln2_b, m2[t], r2[t], p2g[t], p2b[t], None, None,
+                              2 * B, hid, 2, act2)
+            DH[t].addmm_(du[t], W1)
+            C.ln_gru_bwd_into(gx[t], cat[t], HD, lng_w, lng_b, mg[t], rg[t], DH[t], dgx[t], dhp, pgg[t], pgb[t], None, None,
+                              B, H)
+            torch.mm(dgx[t], Wg, out=dcat)
+            C.ln_act_bwd_into(xr[t], D, dcat[:, H:], HD, dx[t], D, ln1_w, ln1_b, m1[t], r1[t], p1g[t], p1b[t], None, None,
+                              B, D, 1, act1)
+            if t > 0:
+                torch.mm(dx[t], Wz, out=dzp)
+                C.rssm_mask_bwd(dhp, H, dcat, HD, dzp, first[t], DH[t - 1], dsamp[t - 1, 1], B, H, S)
+        TB = T * B
+        # ---- batched weight gradients: one GEMM / one reduction each
+        dWz = dx.reshape(TB, D).t().mm(zm.reshape(TB, S))
+        dWg = dgx.reshape(TB, 3 * H).t().mm(cat.reshape(TB, HD))
+        dW1 = du.reshape(TB, 2 * hid).t().mm(hs.reshape(TB, H))
+        dlog_g = dlog.transpose(0, 1).reshape(2, TB, S)
+        v_g = v.transpose(0, 1).reshape(2, TB, hid)
+        dW2 = torch.bmm(dlog_g.transpose(1, 2), v_g)
+        db2 = dlog_g.sum(1, keepdim=True)
+        dln1_w = torch.empty_like(ln1_w)
+        dln1_b = torch.empty_like(ln1_b)
+        C.colsum2(p1g, p1b, dln1_w, dln1_b, T * g1, D, 1)
+        dlng_w = torch.empty_like(lng_w)
+        dlng_b = torch.empty_like(lng_b)
+        C.colsum2(pgg, pgb, dlng_w, dlng_b, T * gg, 3 * H, 1)
+        dln2_w = torch.empty_like(ln2_w)
+        dln2_b = torch.empty_like(ln2_b)
+        C.colsum2(p2g, p2b, dln2_w, dln2_b, T * g2 * 2, hid, 2)
+        return (dx, du, None, None, None, dWz, dln1_w, dln1_b, dWg, dlng_w, dlng_b, dW1, dln2_w, dln2_b, dW2, db2, None)
+
+
+def fused_scan_supported(rssm) -> bool:
+    """The fused scan covers the DreamerV3 RSSM layout: LN+act MLPs, LN-GRU, equal prior/posterior widths."""
+    import torch.nn as nn
+
+    from sheeprl_prey_amd.utils.model import LayerNorm
+
+    try:
+        rec = rssm.recurrent_model.mlp.model
+        tr = rssm.transition_model.model
+        rep = rssm.representation_model.model
+        gru = rssm.recurrent_model.rnn
+    except AttributeError:
+        return False
+    ok = (
+        len(rec) == 3 and isinstance(rec[1], LayerNorm) and rec[1].act in ACTS and rec[0].bias is None
+        and len(tr) == 4 and isinstance(tr[1], LayerNorm) and len(rep) == 4 and isinstance(rep[1], LayerNorm)
+        and tr[1].act == rep[1].act and tr[1].eps == rep[1].eps
+        and tr[0].out_features == rep[0].out_features and tr[0].bias is not None and rep[0].bias is not None
+        and isinstance(gru.layer_norm, nn.LayerNorm) and gru.linear.bias is None
+        and rssm.discrete <= 64 and gru.hidden_size <= 4096 and rec[0].out_features <= 2048 and tr[0].out_features <= 2048
+    )
+    return bool(ok)
+
+
+def fused_scan(rssm, embedded_obs: Tensor, actions: Tensor, is_first: Tensor, z0: Tensor,
+               uniform: Tensor = None) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """Returns recurrent_states [T,B,H], posteriors [T,B,S], posteriors_logits [T,B,S], priors_logits [T,B,S]."""
+    T, B = embedded_obs.shape[:2]
+    rec = rssm.recurrent_model.mlp.model
+    gru = rssm.recurrent_model.rnn
+    tr = rssm.transition_model.model
+    rep = rssm.representation_model.model
+    H = gru.hidden_size
+    S = tr[3].out_features
+    rec_lin = rec[0]
+    Wz = rec_lin.weight[:, :S]
+    Wa = rec_lin.weight[:, S:]
+    a_proj = torch.nn.functional.linear((1 - is_first) * actions, Wa)
+    We = rep[0].weight[:, H:]
+    e_proj = torch.nn.functional.linear(embedded_obs, We, rep[0].bias)
+    hid = tr[0].out_features
+    P = torch.cat((tr[0].bias.expand(T, B, hid), e_proj), -1)
+    W1 = torch.cat((tr[0].weight, rep[0].weight[:, :H]), 0)
+    ln2_w = torch.stack((tr[1].weight, rep[1].weight))
+    ln2_b = torch.stack((tr[1].bias, rep[1].bias))
+    W2 = torch.stack((tr[3].weight, rep[3].weight))
+    b2 = torch.stack((tr[3].bias, rep[3].bias)).unsqueeze(1)
+    if uniform is None:
+        uniform = torch.rand(T, 2 * B * (S // rssm.discrete), device=embedded_obs.device)
+    meta = (rssm.discrete, float(rssm.unimix), float(rec[1].eps), float(gru.layer_norm.eps), float(tr[1].eps),
+            ACTS[rec[1].act], ACTS[tr[1].act])
+    return RSSMScanFn.apply(a_proj.contiguous(), P.contiguous(), is_first.contiguous(), uniform, z0.reshape(-1).contiguous(),
+                            Wz, rec[1].weight, rec[1].bias, gru.linear.weight, gru.layer_norm.weight, gru.layer_norm.bias,
+                            W1, ln2_w, ln2_b, W2, b2, meta)

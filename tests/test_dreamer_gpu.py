@@ -66,3 +66,43 @@ def test_dv3_graph_matches_eager_losses():
     torch.manual_seed(11)
     lb = float(b.train_step(data)["Loss/observation_loss"])
     assert abs(la - lb) / abs(la) < 1e-4
+
+
+@pytest.mark.parametrize("H,D,hid,B,T", [(64, 64, 64, 4, 16), (512, 512, 512, 16, 8), (96, 80, 48, 3, 5)])
+def test_fused_rssm_scan_matches_python_scan(H, D, hid, B, T):
+    """The fused scan (9+9 launches/step, batched weight grads) vs the python step loop, same noise."""
+    import copy
+
+    from sheeprl_prey_amd.algos.dreamer_v3.agent import RSSM, RecurrentModel, init_weights
+    from sheeprl_prey_amd.models.models import MLP
+
+    torch.manual_seed(0)
+    S, A, E = 32 * 32, 6, 200
+    rec = RecurrentModel(S + A, H, D)
+    rep = MLP(H + E, S, [hid], activation=torch.nn.SiLU, norm_layer=[torch.nn.LayerNorm], norm_args=[{"normalized_shape": hid}])
+    tr = MLP(H, S, [hid], activation=torch.nn.SiLU, norm_layer=[torch.nn.LayerNorm], norm_args=[{"normalized_shape": hid}])
+    rssm = RSSM(rec.apply(init_weights), rep.apply(init_weights), tr.apply(init_weights), {"validate_args": False}).cuda()
+    for p in rssm.parameters():  # non-trivial LN affine params
+        if p.dim() == 1:
+            p.data.add_(0.1 * torch.randn_like(p))
+    rssm_ref = copy.deepcopy(rssm)
+    rssm_ref.fused_scan = False
+    emb = torch.randn(T, B, E, device="cuda")
+    act = torch.nn.functional.one_hot(torch.randint(0, A, (T, B), device="cuda"), A).float()
+    first = (torch.rand(T, B, 1, device="cuda") < 0.2).float()
+    first[0] = 1
+    uni = torch.rand(T, 2 * B * 32, device="cuda")
+    # python scan consumes one uniform per posterior categorical: feed it the posterior half
+    uni_post = uni.view(T, 2, B * 32)[:, 1].reshape(T, B, 32)
+    e1, e2 = emb.clone().requires_grad_(), emb.clone().requires_grad_()
+    out1 = rssm.scan_dynamic(e1, act, first, uniform=uni)
+    out2 = rssm_ref.scan_dynamic(e2, act, first, uniform=uni_post)
+    names = ["h", "post", "post_logits", "prior_logits"]
+    for n, a, b in zip(names, out1, out2):
+        torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-4, msg=lambda m: f"{n}: {m}")
+    gs = [torch.randn_like(o) for o in out1]
+    sum((o * g).sum() for o, g in zip(out1, gs)).backward()
+    sum((o * g).sum() for o, g in zip(out2, gs)).backward()
+    torch.testing.assert_close(e1.grad, e2.grad, rtol=2e-3, atol=2e-3)
+    for (n, p1), p2 in zip(rssm.named_parameters(), rssm_ref.parameters()):
+        torch.testing.assert_close(p1.grad, p2.grad, rtol=3e-3, atol=3e-3, msg=lambda m: f"{n}: {m}")
