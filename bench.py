@@ -159,6 +159,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if args.profile_steps:
+        torch.cuda._sleep(1000)  # marker kernel: scripts/trace_window.py aggregates the dispatches after it
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = one_step()

@@ -1,0 +1,33 @@
+"""Aggregate a rocprofv3 kernel-trace CSV over the timed window only (after the last marker
+kernel launched by ``bench.py --profile-steps``), dropping MIOpen find/tuning noise from warm-up.
+
+usage: python scripts/trace_window.py <kernel_trace.csv> <timed_steps> [top]"""
+import collections
+import csv
+import sys
+
+
+def main(path, steps, top=40):
+    rows = list(csv.DictReader(open(path)))
+    key_s, key_e = "Start_Timestamp", "End_Timestamp"
+    rows.sort(key=lambda r: int(r[key_s]))
+    idx = max(i for i, r in enumerate(rows) if "sleep" in r["Kernel_Name"].lower() or "spin" in r["Kernel_Name"].lower())
+    win = rows[idx + 1 :]
+    t0, t1 = int(win[0][key_s]), int(win[-1][key_e])
+    agg = collections.defaultdict(lambda: [0, 0])
+    for r in win:
+        d = int(r[key_e]) - int(r[key_s])
+        a = agg[r["Kernel_Name"]]
+        a[0] += d
+        a[1] += 1
+    busy = sum(a[0] for a in agg.values())
+    n = sum(a[1] for a in agg.values())
+    print(f"timed window: {steps} steps, wall {(t1 - t0) / 1e6:.2f} ms ({(t1 - t0) / 1e6 / steps:.2f} ms/step), "
+          f"kernel busy {busy / 1e6:.2f} ms ({busy / 1e6 / steps:.2f} ms/step), {n / steps:.0f} dispatches/step\n")
+    print("| ms/step | calls/step | avg us | % busy | kernel |\n|---:|---:|---:|---:|---|")
+    for name, (d, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:top]:
+        print(f"| {d / 1e6 / steps:.3f} | {c / steps:.1f} | {d / c / 1e3:.1f} | {100 * d / busy:.1f} | `{name[:95]}` |")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]) if len(sys.argv) > 3 else 40)

@@ -77,8 +77,21 @@ def _entropy_categorical(logits: Tensor) -> Tensor:
 
 
 class DreamerV3Trainer:
+    """One DreamerV3 gradient step as five phases separated by the collectives they need:
+
+    ``wm`` (world-model fwd/bwd) | all-reduce(wm grads) | ``imagine`` (wm step, imagination, lambda) |
+    all-gather(lambda) | ``actor`` (Moments, actor fwd/bwd) | all-reduce(actor grads) | ``critic`` (actor
+    step, critic fwd/bwd) | all-reduce(critic grads) | ``final`` (critic step).
+
+    Execution: one hipGraph for the whole step on a single rank; on N ranks (discrete actions) one
+    hipGraph per phase with the RCCL collectives issued eagerly between replays (collectives stay
+    out of captured graphs); otherwise eager."""
+
+    PHASES = ("wm", "imagine", "actor", "critic", "final")
+
     def __init__(self, runner, cfg, world_model, actor, critic, target_critic, world_optimizer, actor_optimizer,
-                 critic_optimizer, moments: Moments, is_continuous: bool, actions_dim: Sequence[int]):
+                 critic_optimizer, moments: Moments, is_continuous: bool, actions_dim: Sequence[int],
+                 force_segmented: bool = False):
         self.runner, self.cfg = runner, cfg
         self.world_model, self.actor, self.critic, self.target_critic = world_model, actor, critic, target_critic
         self.world_optimizer, self.actor_optimizer, self.critic_optimizer = world_optimizer, actor_optimizer, critic_optimizer
@@ -86,8 +99,25 @@ class DreamerV3Trainer:
         self.is_continuous = is_continuous
         self.actions_dim = list(actions_dim)
         self.target_flat = flatten_like(target_critic, critic_optimizer)
-        use_graph = bool(runner.cuda_graphs) and runner.world_size == 1
-        self.graphed = GraphedStep(self._train_core, warmup=2, enabled=use_graph, name="dreamer_v3_train")
+        self._st: Dict[str, Any] = {}
+        self._gather_buf = None
+        ws = runner.world_size
+        graphs = bool(runner.cuda_graphs)
+        self.segmented = graphs and (force_segmented or (ws > 1 and not is_continuous))
+        single = graphs and ws == 1 and not self.segmented
+        self.graphed = GraphedStep(self._full_step, warmup=2, enabled=single, name="dreamer_v3_train")
+        if self.segmented:
+            from sheeprl_prey_amd.parallel.graphs import SegmentedGraph
+
+            self.seg = SegmentedGraph(
+                [self._phase_wm, self._phase_imagine, self._phase_actor, self._phase_critic, self._phase_final],
+                [self._coll_wm, self._coll_lambda, self._coll_actor, self._coll_critic],
+                warmup=2,
+            )
+
+    @property
+    def uses_graphs(self) -> bool:
+        return bool(self.graphed.enabled or self.segmented)
 
     @torch.no_grad()
     def update_target(self, tau: float) -> None:
@@ -95,26 +125,68 @@ class DreamerV3Trainer:
         self.target_flat.lerp_(self.critic_optimizer.flat_param, float(tau))
 
     def train_step(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        if self.segmented:
+            return self.seg(data)
         return self.graphed(data)
 
-    # ------------------------------------------------------------------ the step
-    def _train_core(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:
-        cfg, runner = self.cfg, self.runner
-        wm, actor, critic = self.world_model, self.actor, self.critic
+    def _full_step(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        self._phase_wm(data)
+        self._coll_wm()
+        self._phase_imagine(data)
+        self._coll_lambda()
+        self._phase_actor(data)
+        self._coll_actor()
+        self._phase_critic(data)
+        self._coll_critic()
+        return self._phase_final(data)
+
+    # ------------------------------------------------------------------ collectives (eager)
+    # ``dry=True``: bind buffers only (called between phase captures, no communication)
+    def _coll_wm(self, dry: bool = False) -> None:
+        if not dry:
+            self.runner.sync_gradients(self.world_optimizer)
+
+    def _coll_actor(self, dry: bool = False) -> None:
+        if not dry:
+            self.runner.sync_gradients(self.actor_optimizer)
+
+    def _coll_critic(self, dry: bool = False) -> None:
+        if not dry:
+            self.runner.sync_gradients(self.critic_optimizer)
+
+    def _coll_lambda(self, dry: bool = False) -> None:
+        lam = self._st["lambda_values"]
+        ws = self.runner.world_size
+        if ws <= 1:
+            self._st["gathered"] = lam
+            return
+        import torch.distributed as dist
+
+        if self._gather_buf is None or self._gather_buf.shape[1:] != lam.shape:
+            self._gather_buf = torch.empty((ws,) + tuple(lam.shape), device=lam.device, dtype=lam.dtype)
+        self._st["gathered"] = self._gather_buf
+        if dry:
+            return
+        if lam.is_cuda:
+            dist.all_gather_into_tensor(self._gather_buf, lam.detach().contiguous(), group=self.runner.group)
+        else:
+            dist.all_gather(list(self._gather_buf.unbind(0)), lam.detach().contiguous(), group=self.runner.group)
+        self._st["gathered"] = self._gather_buf
+
+    # ------------------------------------------------------------------ phases
+    def _phase_wm(self, data: Dict[str, Tensor]) -> None:
+        cfg = self.cfg
+        wm = self.world_model
+        st = self._st
         T, B = data["rewards"].shape[:2]
         wm_cfg = cfg.algo.world_model
         stoch, disc = wm_cfg.stochastic_size, wm_cfg.discrete_size
-        S = stoch * disc
-        H = wm_cfg.recurrent_model.recurrent_state_size
         out: Dict[str, Tensor] = {}
-
         batch_obs = {k: data[k] / 255.0 for k in cfg.cnn_keys.encoder}
         batch_obs.update({k: data[k] for k in cfg.mlp_keys.encoder})
         is_first = data["is_first"].clone()
         is_first[0] = 1.0
         batch_actions = torch.cat((torch.zeros_like(data["actions"][:1]), data["actions"][:-1]), dim=0)
-
-        # ---------------- dynamic learning
         embedded_obs = wm.encoder(batch_obs)
         recurrent_states, posteriors, posteriors_logits, priors_logits = wm.rssm.scan_dynamic(
             embedded_obs, batch_actions, is_first)
@@ -138,11 +210,7 @@ class DreamerV3Trainer:
             continue_logits, continue_targets, wm_cfg.continue_scale_factor,
         )
         self.world_optimizer.zero_grad(set_to_none=True)
-        runner.backward(rec_loss, self.world_optimizer)
-        wm_grads = runner.clip_gradients(wm, self.world_optimizer, max_norm=wm_cfg.clip_gradients) \
-            if wm_cfg.clip_gradients is not None and wm_cfg.clip_gradients > 0 else torch.zeros((), device=rec_loss.device)
-        self.world_optimizer.step()
-        out["Grads/world_model"] = wm_grads.detach()
+        rec_loss.backward()
         out["Loss/world_model_loss"] = rec_loss.detach()
         out["Loss/observation_loss"] = observation_loss.detach()
         out["Loss/reward_loss"] = reward_loss.detach()
@@ -154,26 +222,38 @@ class DreamerV3Trainer:
             ql = priors_logits.detach().view(T, B, stoch, disc)
             out["State/post_entropy"] = _entropy_categorical(pl).sum(-1).mean()
             out["State/prior_entropy"] = _entropy_categorical(ql).sum(-1).mean()
+        st["out"] = out
+        st["posteriors"] = posteriors.detach()
+        st["recurrent_states"] = recurrent_states.detach()
 
-        # ---------------- behaviour learning (imagination)
-        horizon = cfg.algo.horizon
+    def _phase_imagine(self, data: Dict[str, Tensor]) -> None:
+        cfg, st = self.cfg, self._st
+        wm, actor, critic = self.world_model, self.actor, self.critic
+        wm_cfg = cfg.algo.world_model
+        S = wm_cfg.stochastic_size * wm_cfg.discrete_size
+        H = wm_cfg.recurrent_model.recurrent_state_size
+        clip = wm_cfg.clip_gradients
+        if clip is not None and clip > 0:
+            st["out"]["Grads/world_model"] = self.runner.clip_gradients(wm, self.world_optimizer, max_norm=clip).detach()
+        else:
+            st["out"]["Grads/world_model"] = torch.zeros((), device=data["rewards"].device)
+        self.world_optimizer.step()
         grad_ctx = torch.enable_grad() if self.is_continuous else torch.no_grad()
         with grad_ctx:
-            prior = posteriors.detach().reshape(-1, S)
-            h = recurrent_states.detach().reshape(-1, H)
+            prior = st["posteriors"].reshape(-1, S)
+            h = st["recurrent_states"].reshape(-1, H)
             latent = torch.cat((prior, h), -1)
             trajectories: List[Tensor] = [latent]
             actions = torch.cat(actor(latent.detach())[0], dim=-1)
             imagined_actions: List[Tensor] = [actions]
-            for _ in range(horizon):
+            for _ in range(cfg.algo.horizon):
                 prior, h = wm.rssm.imagination(prior, h, actions)
                 prior = prior.reshape(-1, S)
                 latent = torch.cat((prior, h), -1)
                 trajectories.append(latent)
                 actions = torch.cat(actor(latent.detach())[0], dim=-1)
                 imagined_actions.append(actions)
-            imagined_trajectories = torch.stack(trajectories)  # [H+1, B*T, L]
-            imagined_actions_t = torch.stack(imagined_actions)
+            imagined_trajectories = torch.stack(trajectories)
             predicted_values = ops.twohot_mean(critic(imagined_trajectories))
             predicted_rewards = ops.twohot_mean(wm.reward_model(imagined_trajectories))
             continues = (wm.continue_model(imagined_trajectories) > 0).to(predicted_values.dtype)
@@ -182,54 +262,65 @@ class DreamerV3Trainer:
             lambda_values = compute_lambda_values(predicted_rewards[1:], predicted_values[1:],
                                                   continues[1:] * cfg.algo.gamma, lmbda=cfg.algo.lmbda)
         with torch.no_grad():
-            discount = torch.cumprod(continues * cfg.algo.gamma, dim=0) / cfg.algo.gamma
+            st["discount"] = torch.cumprod(continues * cfg.algo.gamma, dim=0) / cfg.algo.gamma
+        st["imagined_trajectories"] = imagined_trajectories
+        st["imagined_actions"] = torch.stack(imagined_actions)
+        st["predicted_values"] = predicted_values
+        st["lambda_values"] = lambda_values
 
-        # ---------------- actor
+    def _phase_actor(self, data: Dict[str, Tensor]) -> None:
+        cfg, st = self.cfg, self._st
         self.actor_optimizer.zero_grad(set_to_none=True)
-        policies = actor(imagined_trajectories.detach())[1]
-        baseline = predicted_values[:-1]
-        offset, invscale = self.moments(lambda_values)
-        normed_lambda = (lambda_values - offset) / invscale
-        normed_baseline = (baseline - offset) / invscale
-        advantage = normed_lambda - normed_baseline
+        policies = self.actor(st["imagined_trajectories"].detach())[1]
+        lambda_values = st["lambda_values"]
+        baseline = st["predicted_values"][:-1]
+        offset, invscale = self.moments.update(st["gathered"])
+        advantage = (lambda_values - offset) / invscale - (baseline - offset) / invscale
         if self.is_continuous:
             objective = advantage
         else:
             objective = torch.stack(
                 [p.log_prob(a.detach()).unsqueeze(-1)[:-1]
-                 for p, a in zip(policies, torch.split(imagined_actions_t, self.actions_dim, dim=-1))], dim=-1,
+                 for p, a in zip(policies, torch.split(st["imagined_actions"], self.actions_dim, dim=-1))], dim=-1,
             ).sum(dim=-1) * advantage.detach()
         try:
             entropy = cfg.algo.actor.ent_coef * torch.stack([p.entropy() for p in policies], -1).sum(dim=-1)
         except NotImplementedError:
             entropy = torch.zeros_like(objective[..., 0])
-        policy_loss = -torch.mean(discount[:-1].detach() * (objective + entropy.unsqueeze(-1)[:-1]))
-        runner.backward(policy_loss, self.actor_optimizer)
-        actor_grads = runner.clip_gradients(actor, self.actor_optimizer, max_norm=cfg.algo.actor.clip_gradients) \
-            if cfg.algo.actor.clip_gradients is not None and cfg.algo.actor.clip_gradients > 0 else torch.zeros((), device=policy_loss.device)
-        self.actor_optimizer.step()
-        out["Grads/actor"] = actor_grads.detach()
-        out["Loss/policy_loss"] = policy_loss.detach()
+        policy_loss = -torch.mean(st["discount"][:-1].detach() * (objective + entropy.unsqueeze(-1)[:-1]))
+        policy_loss.backward()
+        st["out"]["Loss/policy_loss"] = policy_loss.detach()
 
-        # ---------------- critic
-        traj = imagined_trajectories.detach()[:-1]
-        qv_logits = critic(traj)
+    def _phase_critic(self, data: Dict[str, Tensor]) -> None:
+        cfg, st = self.cfg, self._st
+        clip = cfg.algo.actor.clip_gradients
+        if clip is not None and clip > 0:
+            st["out"]["Grads/actor"] = self.runner.clip_gradients(self.actor, self.actor_optimizer, max_norm=clip).detach()
+        else:
+            st["out"]["Grads/actor"] = torch.zeros((), device=data["rewards"].device)
+        self.actor_optimizer.step()
+        traj = st["imagined_trajectories"].detach()[:-1]
+        qv_logits = self.critic(traj)
         with torch.no_grad():
             target_values = ops.twohot_mean(self.target_critic(traj))
         self.critic_optimizer.zero_grad(set_to_none=True)
-        value_loss = ops.twohot_nll(qv_logits, lambda_values.detach()) + ops.twohot_nll(qv_logits, target_values)
-        value_loss = torch.mean(value_loss * discount[:-1].squeeze(-1))
-        runner.backward(value_loss, self.critic_optimizer)
-        critic_grads = runner.clip_gradients(critic, self.critic_optimizer, max_norm=cfg.algo.critic.clip_gradients) \
-            if cfg.algo.critic.clip_gradients is not None and cfg.algo.critic.clip_gradients > 0 else torch.zeros((), device=value_loss.device)
-        self.critic_optimizer.step()
-        out["Grads/critic"] = critic_grads.detach()
-        out["Loss/value_loss"] = value_loss.detach()
+        value_loss = ops.twohot_nll(qv_logits, st["lambda_values"].detach()) + ops.twohot_nll(qv_logits, target_values)
+        value_loss = torch.mean(value_loss * st["discount"][:-1].squeeze(-1))
+        value_loss.backward()
+        st["out"]["Loss/value_loss"] = value_loss.detach()
 
+    def _phase_final(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        cfg, st = self.cfg, self._st
+        clip = cfg.algo.critic.clip_gradients
+        if clip is not None and clip > 0:
+            st["out"]["Grads/critic"] = self.runner.clip_gradients(self.critic, self.critic_optimizer, max_norm=clip).detach()
+        else:
+            st["out"]["Grads/critic"] = torch.zeros((), device=data["rewards"].device)
+        self.critic_optimizer.step()
         self.actor_optimizer.zero_grad(set_to_none=True)
         self.critic_optimizer.zero_grad(set_to_none=True)
         self.world_optimizer.zero_grad(set_to_none=True)
-        return out
+        return dict(st["out"])
 
 
 def make_aggregator(cfg) -> MetricAggregator:

@@ -265,6 +265,9 @@ __global__ void __launch_bounds__(256) colsum2_kernel(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------- NCHW (normalise over C)
+// One thread per pixel.  C <= MAXC: the pixel's C values stay in registers (1 read + 1 write of the
+// tensor); otherwise 3 passes over global memory.
+template <int MAXC>
 __global__ void __launch_bounds__(256) ln_nchw_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* __restrict__ y,
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
@@ -273,25 +276,53 @@ __global__ void __launch_bounds__(256) ln_nchw_fwd_kernel(const float* __restric
   if (pix >= (int64_t)B * HW) return;
   int b = pix / HW, p = pix % HW;
   const float* xb = x + (int64_t)b * C * HW + p;
-  float s = 0.f;
-  for (int c = 0; c < C; ++c) s += xb[(int64_t)c * HW];
-  float mu = s / C;
-  float q = 0.f;
-  for (int c = 0; c < C; ++c) {
-    float d = xb[(int64_t)c * HW] - mu;
-    q += d * d;
-  }
-  float rs = rsqrtf(q / C + eps);
   float* yb = y + (int64_t)b * C * HW + p;
-  for (int c = 0; c < C; ++c) {
-    float z = (xb[(int64_t)c * HW] - mu) * rs;
-    if (gamma) z = z * gamma[c] + beta[c];
-    yb[(int64_t)c * HW] = act_fwd(z, act);
+  float mu, rs;
+  if (MAXC > 0 && C <= MAXC) {
+    float v[MAXC > 0 ? MAXC : 1];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      v[c] = c < C ? xb[(int64_t)c * HW] : 0.f;
+      s += v[c];
+    }
+    mu = s / C;
+    float q = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      float d = c < C ? v[c] - mu : 0.f;
+      q += d * d;
+    }
+    rs = rsqrtf(q / C + eps);
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      if (c < C) {
+        float z = (v[c] - mu) * rs;
+        if (gamma) z = z * gamma[c] + beta[c];
+        yb[(int64_t)c * HW] = act_fwd(z, act);
+      }
+    }
+  } else {
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += xb[(int64_t)c * HW];
+    mu = s / C;
+    float q = 0.f;
+    for (int c = 0; c < C; ++c) {
+      float d = xb[(int64_t)c * HW] - mu;
+      q += d * d;
+    }
+    rs = rsqrtf(q / C + eps);
+    for (int c = 0; c < C; ++c) {
+      float z = (xb[(int64_t)c * HW] - mu) * rs;
+      if (gamma) z = z * gamma[c] + beta[c];
+      yb[(int64_t)c * HW] = act_fwd(z, act);
+    }
   }
   mean_out[pix] = mu;
   rstd_out[pix] = rs;
 }
 
+template <int MAXC>
 __global__ void __launch_bounds__(256) ln_nchw_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -302,6 +333,30 @@ __global__ void __launch_bounds__(256) ln_nchw_bwd_kernel(const float* __restric
   const int64_t base = (int64_t)b * C * HW + p;
   const float mu = mean[pix], rs = rstd[pix];
   float s1 = 0.f, s2 = 0.f;
+  if (MAXC > 0 && C <= MAXC) {
+    float hv[MAXC > 0 ? MAXC : 1], dv[MAXC > 0 ? MAXC : 1];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      hv[c] = dv[c] = 0.f;
+      if (c < C) {
+        int64_t o = base + (int64_t)c * HW;
+        float h = (x[o] - mu) * rs;
+        float g = gamma ? gamma[c] : 1.f;
+        float z = gamma ? h * g + beta[c] : h;
+        float dxh = dy[o] * act_grad(z, act) * g;
+        hv[c] = h;
+        dv[c] = dxh;
+        s1 += dxh;
+        s2 += dxh * h;
+      }
+    }
+    s1 /= C;
+    s2 /= C;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c < C) dx[base + (int64_t)c * HW] = rs * (dv[c] - s1 - hv[c] * s2);
+    return;
+  }
   for (int c = 0; c < C; ++c) {
     int64_t o = base + (int64_t)c * HW;
     float h = (x[o] - mu) * rs;
@@ -375,7 +430,7 @@ int ln_bwd_grid(int M, int N, int G) {
   if (mode == 0) {
     int waves = M;                      // one wave per row
     int g = cdiv(waves, 4);
-    if (g > 256) g = 256;
+    if (g > 1024) g = 1024;
     if (g < 1) g = 1;
     if (G > 1 && (g * 4) % G) g += 1;   // nwaves must be a multiple of G
     return g;
@@ -436,8 +491,10 @@ reduce:
 void launch_ln_nchw_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean, float* rstd, int B,
                         int C, int HW, float eps, int act, hipStream_t st) {
   int64_t P = (int64_t)B * HW;
-  hipLaunchKernelGGL(ln_nchw_fwd_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, x, gamma, beta, y, mean, rstd,
-                     B, C, HW, eps, act);
+  dim3 g((unsigned)((P + 255) / 256)), b(256);
+  if (C <= 32) hipLaunchKernelGGL(ln_nchw_fwd_kernel<32>, g, b, 0, st, x, gamma, beta, y, mean, rstd, B, C, HW, eps, act);
+  else if (C <= 64) hipLaunchKernelGGL(ln_nchw_fwd_kernel<64>, g, b, 0, st, x, gamma, beta, y, mean, rstd, B, C, HW, eps, act);
+  else hipLaunchKernelGGL(ln_nchw_fwd_kernel<0>, g, b, 0, st, x, gamma, beta, y, mean, rstd, B, C, HW, eps, act);
 }
 
 int ln_nchw_splits(int B, int HW) {
@@ -451,8 +508,9 @@ void launch_ln_nchw_bwd(const float* x, const float* dy, const float* gamma, con
                         const float* rstd, float* dx, float* pdg, float* pdb, float* dgamma, float* dbeta, int B, int C,
                         int HW, int act, hipStream_t st) {
   int64_t P = (int64_t)B * HW;
-  hipLaunchKernelGGL(ln_nchw_bwd_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, x, dy, gamma, beta, mean, rstd,
-                     dx, B, C, HW, act);
+  dim3 gg((unsigned)((P + 255) / 256)), bb(256);
+  if (C <= 32) hipLaunchKernelGGL(ln_nchw_bwd_kernel<32>, gg, bb, 0, st, x, dy, gamma, beta, mean, rstd, dx, B, C, HW, act);
+  else hipLaunchKernelGGL(ln_nchw_bwd_kernel<0>, gg, bb, 0, st, x, dy, gamma, beta, mean, rstd, dx, B, C, HW, act);
   if (gamma) {
     int S = ln_nchw_splits(B, HW);
     hipLaunchKernelGGL(ln_nchw_dgb_kernel, dim3(C, S), dim3(256), 0, st, x, dy, gamma, beta, mean, rstd, pdg, pdb, B, C, HW,

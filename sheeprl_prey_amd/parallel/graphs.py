@@ -59,3 +59,71 @@ class GraphedStep:
         # capture recorded the work without executing it: run this step for real
         self.graph.replay()
         return self.static_out
+
+
+class SegmentedGraph:
+    """A step made of phases separated by collectives: each phase is captured in its own hipGraph
+    (sharing one memory pool, so tensors handed from phase to phase keep their addresses) and the
+    collectives run eagerly between replays.  Used for multi-rank training: RCCL calls never enter
+    a captured graph, yet ~all kernels of the step are graph-launched.
+
+    ``phases[i](data)`` may stash tensors on the owner for later phases; the last phase returns the
+    step outputs.  ``colls[i]()`` runs between ``phases[i]`` and ``phases[i+1]``; ``colls[i](dry=True)``
+    must only (re)bind the buffers the next phase reads (it is called between captures)."""
+
+    def __init__(self, phases, colls, warmup: int = 2):
+        assert len(colls) == len(phases) - 1
+        self.phases, self.colls = phases, colls
+        self.warmup = warmup
+        self.graphs = None
+        self.static_in: Optional[Dict[str, Tensor]] = None
+        self.static_out = None
+        self._calls = 0
+
+    def _run_eager(self, data):
+        out = None
+        for i, ph in enumerate(self.phases):
+            out = ph(data)
+            if i < len(self.colls):
+                self.colls[i]()
+        return out
+
+    def __call__(self, data: Dict[str, Tensor]):
+        if self.static_in is None:
+            self.static_in = {k: v.detach().clone() for k, v in data.items()}
+        for k, v in data.items():
+            self.static_in[k].copy_(v, non_blocking=True)
+        if self.graphs is not None:
+            for i, g in enumerate(self.graphs):
+                g.replay()
+                if i < len(self.colls):
+                    self.colls[i]()
+            return self.static_out
+        if self._calls < self.warmup:
+            self._calls += 1
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                out = self._run_eager(self.static_in)
+            torch.cuda.current_stream().wait_stream(s)
+            return out
+        torch.cuda.synchronize()
+        graphs = []
+        pool = None
+        out = None
+        for i, ph in enumerate(self.phases):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                out = ph(self.static_in)
+            pool = g.pool()
+            graphs.append(g)
+            if i < len(self.colls):
+                self.colls[i](dry=True)  # re-bind hand-off buffers to the captured tensors
+        self.graphs = graphs
+        self.static_out = out
+        # the captures recorded work without running it: execute this step for real
+        for i, g in enumerate(self.graphs):
+            g.replay()
+            if i < len(self.colls):
+                self.colls[i]()
+        return self.static_out
