@@ -182,3 +182,26 @@ def to_torch_obs(obs: Dict[str, np.ndarray], keys: Sequence[str], mlp_keys: Sequ
             t = t.float()
         out[k] = t.to(device, non_blocking=True)
     return out
+
+
+def shard_indices(n: int, runner, shuffle: bool, seed: int, epoch: int) -> torch.Tensor:
+    """DistributedSampler semantics: a seeded permutation, padded to a multiple of world, strided."""
+    g = torch.Generator().manual_seed(seed + epoch)
+    idx = torch.randperm(n, generator=g) if shuffle else torch.arange(n)
+    ws, rk = runner.world_size, runner.global_rank
+    total = ((n + ws - 1) // ws) * ws
+    if total > n:
+        idx = torch.cat([idx, idx[: total - n]])
+    return idx[rk:total:ws]
+
+
+def restore_replay_buffer(rb, saved, runner) -> None:
+    """Resume a replay buffer saved by ``CheckpointCallback``: a per-rank list (gathered on rank 0)
+    or a single state (reference ``sac/sac.py:186-193``)."""
+    if isinstance(saved, list):
+        if len(saved) != runner.world_size:
+            raise RuntimeError(f"Given {len(saved)}, but {runner.world_size} processes are instantiated")
+        saved = saved[runner.global_rank]
+    if not isinstance(saved, dict):
+        raise RuntimeError("unrecognised replay buffer checkpoint format")
+    rb.load_state_dict(saved)

@@ -42,7 +42,7 @@ from sheeprl_prey_amd.algos.dreamer_v3.loss import reconstruction_loss
 from sheeprl_prey_amd.algos.dreamer_v3.utils import Moments, compute_lambda_values, test
 from sheeprl_prey_amd.data.buffers import AsyncReplayBuffer
 from sheeprl_prey_amd.data.tensordict import TensorDict
-from sheeprl_prey_amd.parallel.flat_optim import build_optimizer
+from sheeprl_prey_amd.parallel.flat_optim import flatten_like, build_optimizer
 from sheeprl_prey_amd.parallel.graphs import GraphedStep
 from sheeprl_prey_amd.utils.distribution import OneHotCategoricalValidateArgs
 from sheeprl_prey_amd.utils.metric import MeanMetric, MetricAggregator
@@ -57,18 +57,6 @@ METRIC_KEYS = (
     "Loss/state_loss", "Loss/continue_loss", "State/kl", "State/post_entropy", "State/prior_entropy",
     "Grads/world_model", "Grads/actor", "Grads/critic",
 )
-
-
-def flatten_like(target: torch.nn.Module, source_opt) -> Tensor:
-    """Re-point ``target``'s parameters into a flat slab laid out like ``source_opt.flat_param``."""
-    flat = torch.zeros_like(source_opt.flat_param)
-    with torch.no_grad():
-        for sp, tp, off in zip(source_opt.params, target.parameters(), source_opt.offsets):
-            n = tp.numel()
-            assert sp.shape == tp.shape, "target/source parameter layout mismatch"
-            flat[off : off + n].copy_(tp.detach().reshape(-1))
-            tp.data = flat[off : off + n].view_as(tp)
-    return flat
 
 
 def _entropy_categorical(logits: Tensor) -> Tensor:

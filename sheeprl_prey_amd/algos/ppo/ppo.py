@@ -23,6 +23,7 @@ from sheeprl_prey_amd.algos.common import (
     load_resume,
     log_throughput,
     setup_logger,
+    shard_indices,
     warn_log_ckpt_every,
 )
 from sheeprl_prey_amd.algos.ppo.agent import PPOAgent
@@ -35,17 +36,6 @@ from sheeprl_prey_amd.utils.metric import MeanMetric, MetricAggregator
 from sheeprl_prey_amd.utils.registry import register_algorithm
 from sheeprl_prey_amd.utils.timer import timer
 from sheeprl_prey_amd.utils.utils import gae, normalize_tensor, polynomial_decay
-
-
-def shard_indices(n: int, runner, shuffle: bool, seed: int, epoch: int) -> torch.Tensor:
-    """DistributedSampler semantics: a seeded permutation, padded to a multiple of world, strided."""
-    g = torch.Generator().manual_seed(seed + epoch)
-    idx = torch.randperm(n, generator=g) if shuffle else torch.arange(n)
-    ws, rk = runner.world_size, runner.global_rank
-    total = ((n + ws - 1) // ws) * ws
-    if total > n:
-        idx = torch.cat([idx, idx[: total - n]])
-    return idx[rk:total:ws]
 
 
 def train(runner, agent, optimizer, data: TensorDict, aggregator: MetricAggregator, cfg: Dict[str, Any]) -> None:

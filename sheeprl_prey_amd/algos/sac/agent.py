@@ -1,0 +1,191 @@
+"""SAC agent (reference: ``sheeprl/algos/sac/agent.py:16-275``).
+
+* ``SACActor``: MLP(obs -> 256 -> 256, ReLU) -> (mean, log_std); the tanh-squashed reparameterised
+  sample and its Eq.26 log-prob are one fused HIP kernel (``ops.squashed_gaussian``, K14).
+* critics: the reference's ``n`` separate ``SACCritic`` MLPs become one ``EnsembleMLP`` (stacked
+  weights; one GEMM / batched GEMM per layer for all critics, K15).  ``SACCritic`` (single MLP on
+  obs||act) is kept for API parity.
+* ``SACAgent``: critics + deep-copied target critics, learnable ``log_alpha``, target entropy -|A|,
+  Polyak EMA.  ``alpha_t`` is the device-side alpha used inside captured graphs (the reference
+  calls ``log_alpha.exp().item()``, a host sync, every step); ``alpha`` keeps the float API.
+"""
+from __future__ import annotations
+
+import copy
+from typing import Any, Dict, Optional, SupportsFloat, Tuple, Union
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+from sheeprl_prey_amd import ops
+from sheeprl_prey_amd.models.ensemble import EnsembleMLP
+from sheeprl_prey_amd.models.models import MLP
+
+LOG_STD_MAX = 2
+LOG_STD_MIN = -5
+
+
+class SACCritic(nn.Module):
+    """One Q-function ``Q(s, a)`` (reference ``sac/agent.py:16-50``)."""
+
+    def __init__(self, observation_dim: int, hidden_size: int = 256, num_critics: int = 1):
+        super().__init__()
+        self.model = MLP(input_dims=observation_dim, output_dim=num_critics, hidden_sizes=(hidden_size, hidden_size),
+                         activation=nn.ReLU, flatten_dim=None)
+
+    def forward(self, obs: Tensor, action: Tensor) -> Tensor:
+        return self.model(torch.cat([obs, action], -1))
+
+
+class SACCriticEnsemble(nn.Module):
+    """``n`` Q-functions evaluated as one ensemble: ``forward(obs, act) -> [B, n]``."""
+
+    def __init__(self, observation_dim: int, n: int = 2, hidden_size: int = 256, dropout: float = 0.0,
+                 layer_norm: bool = False):
+        super().__init__()
+        self.n = n
+        self.model = EnsembleMLP(n, observation_dim, (hidden_size, hidden_size), 1, activation="relu",
+                                 dropout=dropout, layer_norm=layer_norm)
+
+    def forward(self, obs: Tensor, action: Tensor) -> Tensor:
+        q = self.model(torch.cat([obs, action], -1))  # [n, B, 1]
+        return q.squeeze(-1).transpose(0, 1)
+
+    def member(self, obs: Tensor, action: Tensor, i: int) -> Tensor:
+        return self.forward(obs, action)[:, i : i + 1]
+
+
+class SACActor(nn.Module):
+    """Reference ``sac/agent.py:53-152``."""
+
+    log_std_mode = 0  # clamp(log_std, LOG_STD_MIN, LOG_STD_MAX)
+
+    def __init__(self, observation_dim: int, action_dim: int, distribution_cfg: Optional[Dict[str, Any]] = None,
+                 hidden_size: int = 256, action_low: Union[SupportsFloat, np.ndarray] = -1.0,
+                 action_high: Union[SupportsFloat, np.ndarray] = 1.0):
+        super().__init__()
+        self.distribution_cfg = distribution_cfg or {}
+        self.model = MLP(input_dims=observation_dim, hidden_sizes=(hidden_size, hidden_size), flatten_dim=None)
+        self.fc_mean = nn.Linear(self.model.output_dim, action_dim)
+        self.fc_logstd = nn.Linear(self.model.output_dim, action_dim)
+        low = np.asarray(action_low, dtype=np.float32)
+        high = np.asarray(action_high, dtype=np.float32)
+        scale = np.broadcast_to((high - low) / 2.0, (action_dim,)).copy()
+        bias = np.broadcast_to((high + low) / 2.0, (action_dim,)).copy()
+        self.register_buffer("action_scale", torch.tensor(scale, dtype=torch.float32))
+        self.register_buffer("action_bias", torch.tensor(bias, dtype=torch.float32))
+
+    def forward(self, obs: Tensor) -> Tuple[Tensor, Tensor]:
+        x = self.model(obs)
+        return self.get_actions_and_log_probs(self.fc_mean(x), self.fc_logstd(x))
+
+    def get_actions_and_log_probs(self, mean: Tensor, log_std: Tensor) -> Tuple[Tensor, Tensor]:
+        """Tanh-squashed reparameterised sample, rescaled to the action bounds, and its log-prob
+        (one fused kernel on GPU).  Takes the raw (unclamped) ``log_std``."""
+        return ops.squashed_gaussian(mean, log_std, self.action_scale, self.action_bias, self.log_std_mode,
+                                     LOG_STD_MIN, LOG_STD_MAX)
+
+    def get_greedy_actions(self, obs: Tensor) -> Tensor:
+        x = self.model(obs)
+        return torch.tanh(self.fc_mean(x)) * self.action_scale + self.action_bias
+
+
+class SACAgent(nn.Module):
+    """Reference ``sac/agent.py:155-275``."""
+
+    def __init__(self, actor: SACActor, critic: SACCriticEnsemble, target_entropy: float, alpha: float = 1.0,
+                 tau: float = 0.005, device: Union[str, torch.device] = "cpu"):
+        super().__init__()
+        self.actor = actor
+        self.critic = critic
+        self.critic_target = copy.deepcopy(critic)
+        for p in self.critic_target.parameters():
+            p.requires_grad = False
+        self.register_buffer("target_entropy", torch.tensor(float(target_entropy), device=device))
+        self.log_alpha = nn.Parameter(torch.log(torch.tensor([float(alpha)], device=device)))
+        self._tau = tau
+        self._target_flat: Optional[Tensor] = None
+        self._source_flat: Optional[Tensor] = None
+
+    # ------------------------------------------------------------------ properties (reference API)
+    @property
+    def num_critics(self) -> int:
+        return self.critic.n
+
+    @property
+    def qfs(self) -> nn.Module:
+        return self.critic
+
+    @property
+    def qfs_target(self) -> nn.Module:
+        return self.critic_target
+
+    @property
+    def alpha(self) -> float:
+        return float(self.log_alpha.detach().exp().item())
+
+    @property
+    def alpha_t(self) -> Tensor:
+        return self.log_alpha.detach().exp()
+
+    @property
+    def tau(self) -> float:
+        return self._tau
+
+    # ------------------------------------------------------------------ compute
+    def get_actions_and_log_probs(self, obs: Tensor) -> Tuple[Tensor, Tensor]:
+        return self.actor(obs)
+
+    def get_greedy_actions(self, obs: Tensor) -> Tensor:
+        return self.actor.get_greedy_actions(obs)
+
+    def get_q_values(self, obs: Tensor, action: Tensor) -> Tensor:
+        return self.critic(obs, action)
+
+    @torch.no_grad()
+    def get_target_q_values(self, obs: Tensor, action: Tensor) -> Tensor:
+        return self.critic_target(obs, action)
+
+    @torch.no_grad()
+    def get_next_target_q_values(self, next_obs: Tensor, rewards: Tensor, dones: Tensor, gamma: float) -> Tensor:
+        next_actions, next_logp = self.get_actions_and_log_probs(next_obs)
+        q_next = self.get_target_q_values(next_obs, next_actions)
+        min_q = torch.min(q_next, dim=-1, keepdim=True)[0] - self.alpha_t * next_logp
+        return rewards + (1 - dones) * gamma * min_q
+
+    # ------------------------------------------------------------------ target network
+    def bind_target_slab(self, critic_optimizer) -> None:
+        """Lay the target critic out like the critic optimiser's flat slab: EMA = one lerp."""
+        from sheeprl_prey_amd.parallel.flat_optim import flatten_like
+
+        self._target_flat = flatten_like(self.critic_target, critic_optimizer)
+        self._source_flat = critic_optimizer.flat_param
+
+    @torch.no_grad()
+    def qfs_target_ema(self, weight: Optional[Union[float, Tensor]] = None) -> None:
+        """theta' <- tau*theta + (1-tau)*theta'.  ``weight`` overrides tau (a device tensor keeps
+        the update inside a captured graph, e.g. ``tau * do_update``)."""
+        w = self._tau if weight is None else weight
+        if self._target_flat is not None:
+            self._target_flat.lerp_(self._source_flat, w)
+            return
+        for p, tp in zip(self.critic.parameters(), self.critic_target.parameters()):
+            tp.lerp_(p, w)
+
+
+def build_agent(runner, cfg: Dict[str, Any], obs_dim: int, action_space, state: Optional[Dict[str, Any]] = None,
+                dropout: float = 0.0, layer_norm: bool = False) -> SACAgent:
+    act_dim = int(np.prod(action_space.shape))
+    actor = SACActor(obs_dim, act_dim, cfg.distribution, cfg.algo.actor.hidden_size, action_space.low,
+                     action_space.high)
+    critic = SACCriticEnsemble(obs_dim + act_dim, cfg.algo.critic.n, cfg.algo.critic.hidden_size, dropout=dropout,
+                               layer_norm=layer_norm)
+    agent = SACAgent(actor, critic, target_entropy=-act_dim, alpha=cfg.algo.alpha.alpha, tau=cfg.algo.tau)
+    if state is not None:
+        agent.load_state_dict(state)
+    agent = agent.to(runner.device)
+    # every rank starts from rank 0's weights (the reference's DDP wrap broadcasts them)
+    runner.setup_module(agent)
+    return agent

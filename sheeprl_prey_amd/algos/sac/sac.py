@@ -1,0 +1,349 @@
+"""SAC, coupled (reference: ``sheeprl/algos/sac/sac.py:34-406``).
+
+Per env step every rank samples ``G*B`` transitions from its (device-resident) replay buffer, the
+samples are all-gathered in ONE packed collective and re-sharded with ``DistributedSampler``
+semantics, then each minibatch runs
+
+    critic update  : target Q (actor + target ensemble), twin-Q ensemble fwd/bwd | all-reduce | Adam, EMA
+    actor update   : squashed-Gaussian actor, ensemble Q, policy + alpha losses  | all-reduce | Adam x2
+
+Each update is a ``PhasedStep``: one hipGraph per update on a single GPU, per-phase graphs with
+RCCL between them on N GPUs.  The EMA's "every k updates" gate is a device scalar fed with the
+batch (``ema_w = tau * do_update``), so the same graph serves every step.
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict, Optional
+
+import numpy as np
+import torch
+from torch import Tensor
+
+from sheeprl_prey_amd.algos.common import (
+    episode_stats,
+    load_resume,
+    log_throughput,
+    restore_replay_buffer,
+    setup_logger,
+    shard_indices,
+    warn_log_ckpt_every,
+)
+from sheeprl_prey_amd.algos.sac.agent import SACAgent, build_agent
+from sheeprl_prey_amd.algos.sac.loss import critic_loss, entropy_loss, policy_loss
+from sheeprl_prey_amd.algos.sac.utils import obs_to_tensor, test
+from sheeprl_prey_amd.data.buffers import ReplayBuffer
+from sheeprl_prey_amd.data.tensordict import TensorDict
+from sheeprl_prey_amd.envs import spaces
+from sheeprl_prey_amd.parallel.flat_optim import build_optimizer
+from sheeprl_prey_amd.parallel.graphs import PhasedStep
+from sheeprl_prey_amd.utils.metric import MeanMetric, MetricAggregator
+from sheeprl_prey_amd.utils.registry import register_algorithm
+from sheeprl_prey_amd.utils.timer import timer
+
+
+class SACTrainer:
+    """Critic / actor updates of SAC-style agents as captured phased steps.
+
+    ``actor_q_reduce``: "min" (SAC, ``sac/sac.py:64``) or "mean" (DroQ, ``droq/droq.py:115``)."""
+
+    def __init__(self, runner, cfg, agent: SACAgent, actor_optimizer, qf_optimizer, alpha_optimizer,
+                 actor_q_reduce: str = "min", graphs: Optional[bool] = None):
+        self.runner, self.cfg, self.agent = runner, cfg, agent
+        self.actor_optimizer, self.qf_optimizer, self.alpha_optimizer = actor_optimizer, qf_optimizer, alpha_optimizer
+        self.gamma = float(cfg.algo.gamma)
+        self.actor_q_reduce = actor_q_reduce
+        agent.bind_target_slab(qf_optimizer)
+        self.critic_params = list(agent.critic.parameters())
+        self.actor_params = [p for p in agent.actor.parameters() if p.requires_grad]
+        self._st: Dict[str, Tensor] = {}
+        use_graphs = bool(cfg.fabric.get("cuda_graphs", False)) if graphs is None else graphs
+        self.critic_step = PhasedStep(runner, [self._critic_fwd_bwd, self._critic_apply], [self._coll_critic],
+                                      graphs=use_graphs, name="sac_critic")
+        self.actor_step = PhasedStep(runner, [self._actor_fwd_bwd, self._actor_apply], [self._coll_actor],
+                                     graphs=use_graphs, name="sac_actor")
+
+    # ------------------------------------------------------------------ critic
+    def _critic_fwd_bwd(self, d: Dict[str, Tensor]) -> None:
+        a = self.agent
+        target = a.get_next_target_q_values(d["next_observations"], d["rewards"], d["dones"], self.gamma)
+        q = a.get_q_values(d["observations"], d["actions"])
+        loss = critic_loss(q, target, a.num_critics)
+        self.qf_optimizer.zero_grad(set_to_none=True)
+        loss.backward(inputs=self.critic_params)
+        self._st["qf_loss"] = loss.detach()
+
+    def _coll_critic(self, dry: bool = False) -> None:
+        if not dry:
+            self.runner.sync_gradients(self.qf_optimizer)
+
+    def _critic_apply(self, d: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        self.qf_optimizer.step()
+        self.agent.qfs_target_ema(d["ema_w"])
+        return {"Loss/value_loss": self._st["qf_loss"]}
+
+    # ------------------------------------------------------------------ actor + alpha
+    def _actor_fwd_bwd(self, d: Dict[str, Tensor]) -> None:
+        a = self.agent
+        obs = d["observations"]
+        actions, logp = a.get_actions_and_log_probs(obs)
+        q = a.get_q_values(obs, actions)
+        q_red = q.min(-1, keepdim=True)[0] if self.actor_q_reduce == "min" else q.mean(-1, keepdim=True)
+        actor_loss = policy_loss(a.alpha_t, logp, q_red)
+        self.actor_optimizer.zero_grad(set_to_none=True)
+        actor_loss.backward(inputs=self.actor_params)
+        alpha_loss = entropy_loss(a.log_alpha, logp.detach(), a.target_entropy)
+        self.alpha_optimizer.zero_grad(set_to_none=True)
+        alpha_loss.backward(inputs=[a.log_alpha])
+        self._st["actor_loss"] = actor_loss.detach()
+        self._st["alpha_loss"] = alpha_loss.detach()
+
+    def _coll_actor(self, dry: bool = False) -> None:
+        if not dry:
+            self.runner.sync_gradients(self.actor_optimizer)
+            # log_alpha is not DDP-wrapped in the reference: its grad is all-reduced explicitly (sac.py:76)
+            self.runner.sync_gradients(self.alpha_optimizer)
+
+    def _actor_apply(self, d: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        self.actor_optimizer.step()
+        self.alpha_optimizer.step()
+        return {"Loss/policy_loss": self._st["actor_loss"], "Loss/alpha_loss": self._st["alpha_loss"]}
+
+    # ------------------------------------------------------------------ API
+    def ema_weight(self, do_update: bool, device) -> Tensor:
+        return torch.tensor([self.agent.tau if do_update else 0.0], device=device)
+
+    def train(self, data: Dict[str, Tensor], do_ema: bool, aggregator: Optional[MetricAggregator] = None) -> None:
+        """One SAC ``train`` call (reference ``sac/sac.py:34-78``) on a minibatch."""
+        dev = data["rewards"].device
+        d = dict(data)
+        d["ema_w"] = self.ema_weight(do_ema, dev)
+        out = dict(self.critic_step(d))
+        out.update(self.actor_step({"observations": data["observations"]}))
+        if aggregator is not None:
+            for k, v in out.items():
+                if k in aggregator:
+                    aggregator.update(k, v)
+
+
+def make_aggregator(cfg) -> MetricAggregator:
+    keys = ["Rewards/rew_avg", "Game/ep_len_avg", "Loss/value_loss", "Loss/policy_loss", "Loss/alpha_loss"]
+    return MetricAggregator({k: MeanMetric(sync_on_compute=cfg.metric.sync_on_compute) for k in keys})
+
+
+def check_sac_spaces(cfg, envs) -> None:
+    if "minedojo" in str(cfg.env.wrapper.get("_target_", "")).lower():
+        raise ValueError(
+            "MineDojo is not currently supported by SAC agent, since it does not take into consideration the action "
+            "masks provided by the environment, but needed in order to play correctly the game. As an alternative you "
+            "can use one of the Dreamers' agents."
+        )
+    if not isinstance(envs.single_action_space, spaces.Box):
+        raise ValueError("Only continuous action space is supported for the SAC agent")
+    obs_space = envs.single_observation_space
+    if not isinstance(obs_space, spaces.Dict):
+        raise RuntimeError(f"Unexpected observation type, should be of type Dict, got: {obs_space}")
+    if len(cfg.mlp_keys.encoder) == 0:
+        raise RuntimeError("You should specify at least one MLP key for the encoder: `mlp_keys.encoder=[state]`")
+    for k in cfg.mlp_keys.encoder:
+        if len(obs_space[k].shape) > 1:
+            raise ValueError("Only environments with vector-only observations are supported by the SAC agent. "
+                             f"Provided environment: {cfg.env.id}")
+
+
+def real_next_obs(next_obs: Dict[str, np.ndarray], infos: Dict[str, Any]) -> Dict[str, np.ndarray]:
+    """Replace auto-reset observations with the true final observations (reference ``sac.py:292-297``)."""
+    if "final_observation" not in infos:
+        return next_obs
+    out = {k: np.array(v, copy=True) for k, v in next_obs.items()}
+    for idx, final in enumerate(infos["final_observation"]):
+        if final is not None:
+            for k, v in final.items():
+                if k in out:
+                    out[k][idx] = v
+    return out
+
+
+def gather_and_shard(runner, sample: TensorDict, cfg) -> TensorDict:
+    """all_gather the per-rank samples (one packed collective) and take this rank's shard with
+    ``DistributedSampler`` semantics (reference ``sac.py:310-331``)."""
+    gathered = runner.all_gather(sample.to_dict())  # {k: [W, G*B, 1, ...]}
+    flat = {k: v.reshape(-1, *v.shape[3:]) for k, v in gathered.items()}  # [W*G*B, ...]
+    n = next(iter(flat.values())).shape[0]
+    data = TensorDict(flat, batch_size=[n], device=next(iter(flat.values())).device)
+    if runner.world_size > 1:
+        idx = shard_indices(n, runner, True, cfg.seed, 0).to(data.device)
+        data = data[idx]
+    return data
+
+
+@register_algorithm()
+def main(runner, cfg: Dict[str, Any]):
+    run_sac_family(runner, cfg, variant="sac")
+
+
+def sac_train_update(trainer: SACTrainer, runner, cfg, rb, update: int, learning_starts: int, ema_every: int,
+                     aggregator) -> bool:
+    """SAC's per-env-step training (reference ``sac/sac.py:308-345``); returns whether it trained."""
+    if update < learning_starts:
+        return False
+    training_steps = learning_starts if update == learning_starts else 1
+    sample = rb.sample(max(training_steps, 1) * cfg.algo.per_rank_gradient_steps * cfg.per_rank_batch_size,
+                       sample_next_obs=cfg.buffer.sample_next_obs)
+    data = gather_and_shard(runner, sample, cfg).to(runner.device)
+    with timer("Time/train_time"):
+        do_ema = update % ema_every == 0
+        for start in range(0, data.shape[0], cfg.per_rank_batch_size):
+            batch = data[start : start + cfg.per_rank_batch_size]
+            bd = {k: batch[k] for k in ("observations", "next_observations", "actions", "rewards", "dones")}
+            if bd["observations"].shape[0] != cfg.per_rank_batch_size and trainer.critic_step.enabled:
+                # ragged tail batch: static graph shapes do not fit, run it eagerly
+                _eager_train(trainer, bd, do_ema, aggregator)
+            else:
+                trainer.train(bd, do_ema, aggregator)
+    return True
+
+
+def run_sac_family(runner, cfg: Dict[str, Any], variant: str = "sac"):
+    """Shared coupled main loop of SAC (``sac/sac.py:81-406``) and DroQ (``droq/droq.py:128-416``)."""
+    cfg, state = load_resume(runner, cfg)
+    device = runner.device
+    rank, world_size = runner.global_rank, runner.world_size
+    runner.seed_everything(cfg.seed)
+
+    if len(cfg.cnn_keys.encoder) > 0:
+        import warnings
+
+        warnings.warn("SAC algorithm cannot allow to use images as observations, the CNN keys will be ignored")
+        cfg.cnn_keys.encoder = []
+
+    logger, log_dir = setup_logger(runner, cfg)
+    from sheeprl_prey_amd.algos.common import build_envs
+
+    envs = build_envs(runner, cfg, log_dir)
+    check_sac_spaces(cfg, envs)
+    action_space = envs.single_action_space
+    obs_space = envs.single_observation_space
+    obs_dim = int(sum(int(np.prod(obs_space[k].shape)) for k in cfg.mlp_keys.encoder))
+
+    droq = variant == "droq"
+    agent = build_agent(runner, cfg, obs_dim, action_space, state["agent"] if state else None,
+                        dropout=float(cfg.algo.critic.get("dropout", 0.0)) if droq else 0.0, layer_norm=droq)
+    qf_optimizer = build_optimizer(cfg.algo.critic.optimizer, agent.critic.parameters())
+    actor_optimizer = build_optimizer(cfg.algo.actor.optimizer, agent.actor.parameters())
+    alpha_optimizer = build_optimizer(cfg.algo.alpha.optimizer, [agent.log_alpha])
+    if state:
+        qf_optimizer.load_state_dict(state["qf_optimizer"])
+        actor_optimizer.load_state_dict(state["actor_optimizer"])
+        alpha_optimizer.load_state_dict(state["alpha_optimizer"])
+    trainer = SACTrainer(runner, cfg, agent, actor_optimizer, qf_optimizer, alpha_optimizer,
+                         actor_q_reduce="mean" if droq else "min")
+    aggregator = make_aggregator(cfg)
+
+    buffer_size = cfg.buffer.size // int(cfg.env.num_envs * world_size) if not cfg.dry_run else 1
+    rb = ReplayBuffer(buffer_size, cfg.env.num_envs, device=device if device.type == "cuda" else "cpu",
+                      memmap=cfg.buffer.memmap and device.type == "cpu",
+                      memmap_dir=os.path.join(log_dir, "memmap_buffer", f"rank_{rank}"))
+    if state and cfg.buffer.checkpoint and "rb" in state:
+        restore_replay_buffer(rb, state["rb"], runner)
+    step_data = TensorDict({}, batch_size=[cfg.env.num_envs], device=rb.device)
+
+    last_train = 0
+    train_step = 0
+    start_step = state["update"] // world_size if state else 1
+    policy_step = state["update"] * cfg.env.num_envs if state else 0
+    last_log = state["last_log"] if state else 0
+    last_checkpoint = state["last_checkpoint"] if state else 0
+    policy_steps_per_update = int(cfg.env.num_envs * world_size)
+    num_updates = int(cfg.total_steps // policy_steps_per_update) if not cfg.dry_run else 1
+    learning_starts = cfg.algo.learning_starts // policy_steps_per_update if not cfg.dry_run else 0
+    if state and not cfg.buffer.checkpoint:
+        learning_starts += start_step
+    warn_log_ckpt_every(cfg, policy_steps_per_update)
+    ema_every = cfg.algo.critic.target_network_frequency // policy_steps_per_update + 1
+
+    o = envs.reset(seed=cfg.seed)[0]
+    obs = obs_to_tensor(o, cfg.mlp_keys.encoder, rb.device, cfg.env.num_envs)
+
+    for update in range(start_step, num_updates + 1):
+        policy_step += cfg.env.num_envs * world_size
+        with timer("Time/env_interaction_time"):
+            if update <= learning_starts:
+                actions = envs.action_space.sample()
+            else:
+                with torch.no_grad():
+                    actions, _ = agent.actor(obs.to(device))
+                    actions = actions.cpu().numpy()
+            next_o, rewards, dones, truncated, infos = envs.step(actions.reshape(envs.action_space.shape))
+            dones = np.logical_or(dones, truncated)
+
+        for i, ep_rew, ep_len in episode_stats(infos):
+            aggregator.update("Rewards/rew_avg", ep_rew)
+            aggregator.update("Game/ep_len_avg", ep_len)
+            runner.print(f"Rank-0: policy_step={policy_step}, reward_env_{i}={ep_rew[-1]}")
+
+        next_obs = obs_to_tensor(next_o, cfg.mlp_keys.encoder, rb.device, cfg.env.num_envs)
+        step_data["dones"] = torch.as_tensor(dones, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
+        step_data["actions"] = torch.as_tensor(actions, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
+        step_data["observations"] = obs
+        if not cfg.buffer.sample_next_obs:
+            step_data["next_observations"] = obs_to_tensor(real_next_obs(next_o, infos), cfg.mlp_keys.encoder,
+                                                           rb.device, cfg.env.num_envs)
+        step_data["rewards"] = torch.as_tensor(rewards, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
+        rb.add(step_data.unsqueeze(0))
+        obs = next_obs
+
+        if droq:
+            from sheeprl_prey_amd.algos.droq.droq import droq_train_update
+
+            trained = droq_train_update(trainer, runner, cfg, rb, update, learning_starts, aggregator)
+        else:
+            trained = sac_train_update(trainer, runner, cfg, rb, update, learning_starts, ema_every, aggregator)
+        if trained:
+            train_step += world_size
+
+        if policy_step - last_log >= cfg.metric.log_every or update == num_updates or cfg.dry_run:
+            runner.log_dict(aggregator.compute(), policy_step)
+            aggregator.reset()
+            log_throughput(runner, timer.compute(), policy_step, last_log, train_step, last_train,
+                           cfg.env.action_repeat)
+            timer.reset()
+            last_log = policy_step
+            last_train = train_step
+
+        if (cfg.checkpoint.every > 0 and policy_step - last_checkpoint >= cfg.checkpoint.every) or cfg.dry_run or \
+                update == num_updates:
+            last_checkpoint = policy_step
+            ckpt_state = {
+                "agent": agent.state_dict(),
+                "qf_optimizer": qf_optimizer.state_dict(),
+                "actor_optimizer": actor_optimizer.state_dict(),
+                "alpha_optimizer": alpha_optimizer.state_dict(),
+                "update": update * world_size,
+                "batch_size": cfg.per_rank_batch_size * world_size,
+                "last_log": last_log,
+                "last_checkpoint": last_checkpoint,
+            }
+            ckpt_path = os.path.join(log_dir, f"checkpoint/ckpt_{policy_step}_{rank}.ckpt")
+            runner.call("on_checkpoint_coupled", ckpt_path=ckpt_path, state=ckpt_state,
+                        replay_buffer=rb if cfg.buffer.checkpoint else None)
+
+    envs.close()
+    if runner.is_global_zero:
+        test(agent.actor, runner, cfg, log_dir)
+
+
+def _eager_train(trainer: SACTrainer, bd, do_ema, aggregator) -> None:
+    d = dict(bd)
+    d["ema_w"] = trainer.ema_weight(do_ema, bd["rewards"].device)
+    out = {}
+    trainer._critic_fwd_bwd(d)
+    trainer._coll_critic()
+    out.update(trainer._critic_apply(d))
+    trainer._actor_fwd_bwd(d)
+    trainer._coll_actor()
+    out.update(trainer._actor_apply(d))
+    if aggregator is not None:
+        for k, v in out.items():
+            if k in aggregator:
+                aggregator.update(k, v)

@@ -42,7 +42,7 @@ class _DummyBase(Env):
 class ContinuousDummyEnv(_DummyBase):
     def __init__(self, action_dim: int = 2, size: Tuple[int, int, int] = (3, 64, 64), n_steps: int = 128):
         super().__init__(size, n_steps, random_obs=False)
-        self.action_space = spaces.Box(-np.inf, np.inf, shape=(action_dim,))
+        self.action_space = spaces.Box(-1.0, 1.0, shape=(action_dim,))
 
 
 class DiscreteDummyEnv(_DummyBase):

@@ -355,3 +355,37 @@ __all__ = [
     "ln_act", "ln_act_nchw", "ln_gru", "unimix_sample", "twohot_nll", "twohot_mean", "twohot_bins", "kl_balance",
     "lambda_returns", "gae_scan", "flat_grad_norm", "flat_advance", "flat_adam", "native_available", "set_fused",
 ]
+
+
+# =============================================================== tanh-squashed Gaussian (SAC actors)
+class _SquashedGaussian(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, mean, log_std, eps, scale, bias, mode, lo, hi):
+        m, r, e = mean.contiguous(), log_std.contiguous(), eps.contiguous()
+        action, logp = _ext().squashed_gaussian_fwd(m, r, e, scale, bias, mode, lo, hi)
+        ctx.save_for_backward(m, r, e, scale)
+        ctx.cfg = (mode, lo, hi)
+        return action, logp
+
+    @staticmethod
+    def backward(ctx, ga, glp):
+        m, r, e, scale = ctx.saved_tensors
+        dmean, draw = _ext().squashed_gaussian_bwd(
+            m, r, e, scale, ga.contiguous() if ga is not None else None,
+            glp.contiguous() if glp is not None else None, *ctx.cfg)
+        return dmean, draw, None, None, None, None, None, None
+
+
+def squashed_gaussian(mean: Tensor, log_std: Tensor, scale: Tensor, bias: Tensor, mode: int = 0, lo: float = -5.0,
+                      hi: float = 2.0, eps: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    """Reparameterised tanh-squashed Gaussian sample and its log-prob (SAC Eq. 26).
+
+    ``mode=0``: ``log_std`` clamped to [lo, hi] (SAC/DroQ); ``mode=1``: tanh-rescaled into [lo, hi]
+    (SAC-AE).  Returns (action [..., A], logp [..., 1])."""
+    if eps is None:
+        eps = torch.randn_like(mean)
+    A = mean.shape[-1]
+    if _native(mean) and mean.dtype == torch.float32 and A <= 64:
+        return _SquashedGaussian.apply(mean, log_std, eps, scale.float().contiguous(), bias.float().contiguous(),
+                                       int(mode), float(lo), float(hi))
+    return ref.squashed_gaussian(mean, log_std, eps, scale, bias, mode, lo, hi)

@@ -43,6 +43,10 @@ void launch_lambda_fwd(const float*, const float*, const float*, float*, int, in
 void launch_lambda_bwd(const float*, const float*, const float*, const float*, float*, float*, float*, int, int, float,
                        hipStream_t);
 void launch_gae(const float*, const float*, const float*, const float*, float*, float*, int, int, float, float, hipStream_t);
+void launch_squashed_gaussian_fwd(const float*, const float*, const float*, const float*, const float*, float*, float*, int,
+                                  int, int, float, float, hipStream_t);
+void launch_squashed_gaussian_bwd(const float*, const float*, const float*, const float*, const float*, const float*, float*,
+                                  float*, int, int, int, float, float, hipStream_t);
 
 namespace {
 
@@ -201,6 +205,48 @@ std::vector<torch::Tensor> ln_gru_bwd(torch::Tensor x, torch::Tensor h, torch::T
                               db.data_ptr<float>(), M, H, cur_stream());
   TORCH_CHECK(ok, "ln_gru_bwd: unsupported hidden size ", H);
   return {dx, dh, dg, db};
+}
+
+// ------------------------------------------------------------------ tanh-squashed Gaussian (SAC heads)
+std::vector<torch::Tensor> squashed_gaussian_fwd(torch::Tensor mean, torch::Tensor raw, torch::Tensor eps,
+                                                 torch::Tensor scale, torch::Tensor bias, int64_t mode, double lo,
+                                                 double hi) {
+  check_f32(mean, "mean");
+  check_f32(raw, "log_std");
+  check_f32(eps, "eps");
+  check_f32(scale, "scale");
+  check_f32(bias, "bias");
+  const int A = mean.size(-1);
+  TORCH_CHECK(A >= 1 && A <= 64, "squashed_gaussian: action dim must be in [1, 64], got ", A);
+  TORCH_CHECK(raw.sizes() == mean.sizes() && eps.sizes() == mean.sizes(), "squashed_gaussian: shape mismatch");
+  TORCH_CHECK(scale.numel() == A && bias.numel() == A, "squashed_gaussian: scale/bias must have A elements");
+  const int R = mean.numel() / A;
+  auto action = torch::empty_like(mean);
+  auto sizes = mean.sizes().vec();
+  sizes.back() = 1;
+  auto logp = torch::empty(sizes, mean.options());
+  launch_squashed_gaussian_fwd(mean.data_ptr<float>(), raw.data_ptr<float>(), eps.data_ptr<float>(),
+                               scale.data_ptr<float>(), bias.data_ptr<float>(), action.data_ptr<float>(),
+                               logp.data_ptr<float>(), R, A, (int)mode, (float)lo, (float)hi, cur_stream());
+  return {action, logp};
+}
+
+std::vector<torch::Tensor> squashed_gaussian_bwd(torch::Tensor mean, torch::Tensor raw, torch::Tensor eps,
+                                                 torch::Tensor scale, c10::optional<torch::Tensor> ga,
+                                                 c10::optional<torch::Tensor> glp, int64_t mode, double lo, double hi) {
+  const int A = mean.size(-1);
+  const int R = mean.numel() / A;
+  if (ga.has_value() && ga->defined()) check_f32(*ga, "grad_action");
+  if (glp.has_value() && glp->defined()) {
+    check_f32(*glp, "grad_logp");
+    TORCH_CHECK(glp->numel() == R, "grad_logp must have one value per row");
+  }
+  auto dmean = torch::empty_like(mean);
+  auto draw = torch::empty_like(raw);
+  launch_squashed_gaussian_bwd(mean.data_ptr<float>(), raw.data_ptr<float>(), eps.data_ptr<float>(),
+                               scale.data_ptr<float>(), opt_ptr(ga), opt_ptr(glp), dmean.data_ptr<float>(),
+                               draw.data_ptr<float>(), R, A, (int)mode, (float)lo, (float)hi, cur_stream());
+  return {dmean, draw};
 }
 
 // ------------------------------------------------------------------ distributions
@@ -438,6 +484,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lambda_fwd", &lambda_fwd);
   m.def("lambda_bwd", &lambda_bwd);
   m.def("gae", &gae);
+  m.def("squashed_gaussian_fwd", &squashed_gaussian_fwd);
+  m.def("squashed_gaussian_bwd", &squashed_gaussian_bwd);
   m.def("ln_act_fwd_into", &ln_act_fwd_into);
   m.def("ln_act_bwd_into", &ln_act_bwd_into);
   m.def("ln_bwd_grid", &ln_bwd_grid_py);

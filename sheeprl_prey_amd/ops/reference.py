@@ -9,6 +9,7 @@ the KL balancing of ``dreamer_v3/loss.py:65-110``, ``compute_lambda_values``
 """
 from __future__ import annotations
 
+import math
 from typing import Optional, Tuple
 
 import torch
@@ -160,3 +161,20 @@ def gae(rewards, values, dones, next_value, gamma, lam):
         last = delta + nnt * last * gamma * lam
         adv[t] = last
     return adv + values, adv
+
+
+def squashed_gaussian(mean: Tensor, log_std: Tensor, eps: Tensor, scale: Tensor, bias: Tensor, mode: int, lo: float,
+                      hi: float):
+    """Eager oracle of the tanh-squashed Gaussian head (reference ``sac/agent.py:100-138``,
+    ``sac_ae/agent.py:283-320``): returns (action, logp[..., 1])."""
+    if mode == 0:
+        ls = torch.clamp(log_std, lo, hi)
+    else:
+        ls = lo + 0.5 * (hi - lo) * (torch.tanh(log_std) + 1)
+    std = ls.exp()
+    x = mean + std * eps
+    y = torch.tanh(x)
+    action = y * scale + bias
+    logp = -0.5 * eps.pow(2) - ls - 0.5 * math.log(2 * math.pi)
+    logp = logp - torch.log(scale * (1 - y.pow(2)) + 1e-6)
+    return action, logp.sum(-1, keepdim=True)

@@ -15,6 +15,8 @@ reference's layout (``{"state": {i: {step, exp_avg, exp_avg_sq}}, "param_groups"
 """
 from __future__ import annotations
 
+import weakref
+
 import math
 from typing import Any, Dict, Iterable, List, Optional
 
@@ -56,20 +58,46 @@ class FlatOptimizer:
             self.offsets.append(total)
             total += _aligned(p.numel())
         self.numel = total
-        self.flat_param = torch.zeros(total, device=device, dtype=torch.float32)
-        self.flat_grad = torch.zeros(total, device=device, dtype=torch.float32)
-        with torch.no_grad():
-            for p, off in zip(plist, self.offsets):
-                n = p.numel()
-                self.flat_param[off : off + n].copy_(p.detach().reshape(-1))
-                p.data = self.flat_param[off : off + n].view_as(p)
-                p.grad = self.flat_grad[off : off + n].view_as(p)
+        owner = self._shared_owner(plist)
+        if owner is not None:
+            # every param already lives, in this order, in a contiguous run of another optimiser's
+            # slab (e.g. SAC-AE's encoder: in both the critic and the encoder optimiser): share it,
+            # keep separate optimiser state
+            slab, base = owner
+            self.flat_param = slab.flat_param[base : base + total]
+            self.flat_grad = slab.flat_grad[base : base + total]
+        else:
+            self.flat_param = torch.zeros(total, device=device, dtype=torch.float32)
+            self.flat_grad = torch.zeros(total, device=device, dtype=torch.float32)
+            with torch.no_grad():
+                for p, off in zip(plist, self.offsets):
+                    n = p.numel()
+                    self.flat_param[off : off + n].copy_(p.detach().reshape(-1))
+                    p.data = self.flat_param[off : off + n].view_as(p)
+                    p.grad = self.flat_grad[off : off + n].view_as(p)
+                    p._flat_slab = (weakref.ref(self), off)
         # [step, clip_coef, last_norm, pad]
         self.scalars = torch.tensor([0.0, 1.0, 0.0, 0.0], device=device, dtype=torch.float32)
         self.param_groups = [dict(params=self.params, lr=lr, weight_decay=weight_decay, **defaults)]
         self.defaults = dict(lr=lr, weight_decay=weight_decay, **defaults)
         self._advanced = False
         self._init_state()
+
+    def _shared_owner(self, plist: List[Tensor]):
+        tags = [getattr(p, "_flat_slab", None) for p in plist]
+        if all(t is None for t in tags):
+            return None
+        if any(t is None for t in tags) or len({id(t[0]()) for t in tags}) != 1:
+            raise ValueError("FlatOptimizer: parameters are partly owned by another optimiser's flat slab; "
+                             "a shared slab must cover exactly a contiguous run of the owner's parameters")
+        slab = tags[0][0]()
+        if slab is None:
+            return None
+        base = tags[0][1]
+        for t, off in zip(tags, self.offsets):
+            if t[1] - base != off:
+                raise ValueError("FlatOptimizer: shared parameters are not contiguous/in order in the owner's slab")
+        return slab, base
 
     # ------------------------------------------------------------------ to override
     def _init_state(self) -> None:
@@ -244,6 +272,21 @@ _TARGETS = {
     "sheeprl_prey_amd.parallel.flat_optim.FlatAdamW": FlatAdamW,
     "sheeprl_prey_amd.parallel.flat_optim.FlatSGD": FlatSGD,
 }
+
+
+def flatten_like(target: torch.nn.Module, source_opt: FlatOptimizer) -> Tensor:
+    """Re-point ``target``'s parameters (e.g. a target network) into a flat slab laid out like
+    ``source_opt.flat_param``, so Polyak averaging is one ``lerp_`` over the slab."""
+    flat = torch.zeros_like(source_opt.flat_param)
+    tparams = list(target.parameters())
+    assert len(tparams) == len(source_opt.params), "target/source parameter count mismatch"
+    with torch.no_grad():
+        for sp, tp, off in zip(source_opt.params, tparams, source_opt.offsets):
+            n = tp.numel()
+            assert sp.shape == tp.shape, "target/source parameter layout mismatch"
+            flat[off : off + n].copy_(tp.detach().reshape(-1))
+            tp.data = flat[off : off + n].view_as(tp)
+    return flat
 
 
 def build_optimizer(cfg: Dict[str, Any], params) -> FlatOptimizer:

@@ -127,3 +127,43 @@ class SegmentedGraph:
             if i < len(self.colls):
                 self.colls[i]()
         return self.static_out
+
+
+class PhasedStep:
+    """A training step given as ``phases`` separated by ``colls`` (gradient all-reduces etc.).
+
+    * ``graphs`` and one rank: the whole step (phases + the no-op collectives) is ONE hipGraph;
+    * ``graphs`` and N ranks: ``SegmentedGraph`` (per-phase graphs, RCCL eagerly in between);
+    * otherwise eager.
+    Phase/collective contract as in ``SegmentedGraph``."""
+
+    def __init__(self, runner, phases, colls, graphs: bool = True, warmup: int = 2, name: str = "step",
+                 force_segmented: bool = False):
+        assert len(colls) == len(phases) - 1
+        self.phases, self.colls = list(phases), list(colls)
+        use = bool(graphs) and torch.cuda.is_available() and runner.device.type == "cuda"
+        if not use:
+            self.mode = "eager"
+        elif runner.world_size > 1 or force_segmented:
+            self.mode = "segmented"
+            self._impl = SegmentedGraph(self.phases, self.colls, warmup=warmup)
+        else:
+            self.mode = "single"
+            self._impl = GraphedStep(self._run, warmup=warmup, enabled=True, name=name)
+
+    @property
+    def enabled(self) -> bool:
+        return self.mode != "eager"
+
+    def _run(self, data):
+        out = None
+        for i, ph in enumerate(self.phases):
+            out = ph(data)
+            if i < len(self.colls):
+                self.colls[i]()
+        return out
+
+    def __call__(self, data: Dict[str, Tensor]):
+        if self.mode == "eager":
+            return self._run(data)
+        return self._impl(data)

@@ -310,10 +310,13 @@ class Runner:
         return x
 
     def all_gather(self, data: Union[Tensor, Dict[str, Tensor]], group=None, sync_grads: bool = False):
-        """Gather tensors (or dicts of tensors) into a new leading [world] dim."""
+        """Gather tensors (or dicts of tensors) into a new leading [world] dim.  A dict is packed
+        into ONE byte buffer and gathered with a single collective (instead of one per key)."""
         group = group if group is not None else self.group
         if isinstance(data, dict):
-            return {k: self.all_gather(v, group=group) for k, v in data.items()}
+            if self.world_size <= 1:
+                return {k: v.unsqueeze(0) for k, v in data.items()}
+            return self._all_gather_packed(data, group)
         if self.world_size <= 1:
             return data.unsqueeze(0)
         ws = dist.get_world_size(group)
@@ -328,6 +331,21 @@ class Runner:
             dist.all_gather(parts, t, group=group)
             out = torch.stack(parts)
         return out.to(data.device)
+
+    def _all_gather_packed(self, data: Dict[str, Tensor], group) -> Dict[str, Tensor]:
+        keys = list(data.keys())
+        tensors = [data[k].contiguous() for k in keys]
+        dev = tensors[0].device
+        parts = [t.to(dev).reshape(-1).view(torch.uint8) for t in tensors]
+        sizes = [p.numel() for p in parts]
+        packed = torch.cat(parts) if len(parts) > 1 else parts[0]
+        gathered = self.all_gather(packed, group=group)  # [ws, nbytes]
+        out, off = {}, 0
+        for k, t, n in zip(keys, tensors, sizes):
+            chunk = gathered[:, off : off + n].contiguous()
+            out[k] = chunk.view(t.dtype).view((gathered.shape[0],) + tuple(t.shape)).to(data[k].device)
+            off += n
+        return out
 
     def broadcast(self, x: Tensor, src: int = 0, group=None) -> Tensor:
         group = group if group is not None else self.group
@@ -390,8 +408,3 @@ class Runner:
             fn = getattr(cb, hook, None)
             if fn is not None:
                 fn(runner=self, **kwargs)
-
-    def send_object_to_player(self, obj: Any, group) -> None:
-        """Trainer rank 1 -> player rank 0 over the {0,1} group (decoupled checkpoints)."""
-        lst = [obj]
-        dist.broadcast_object_list(lst, src=1, group=group)

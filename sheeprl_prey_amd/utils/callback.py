@@ -27,6 +27,16 @@ def _mark_truncated(rb) -> list:
     return restore
 
 
+def _to_cpu(obj):
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().cpu()
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_cpu(v) for v in obj)
+    return obj
+
+
 class CheckpointCallback:
     def __init__(self, keep_last: Optional[int] = None):
         self.keep_last = keep_last
@@ -48,13 +58,26 @@ class CheckpointCallback:
             state.pop("rb", None)
         self._prune(runner, ckpt_path)
 
-    def on_checkpoint_player(self, runner, ckpt_path: str, state: Dict[str, Any]) -> None:
-        runner.save(ckpt_path, state)
+    def on_checkpoint_player(self, runner, comm, ckpt_path: str, replay_buffer=None) -> None:
+        """Decoupled player (rank 0): receive the trainers' state from trainer rank 1, add the
+        replay buffer and write the checkpoint (reference ``callback.py:68-88``)."""
+        state = comm.player_trainer_object(None)
+        restore = []
+        if replay_buffer is not None:
+            restore = _mark_truncated(replay_buffer)
+            state["rb"] = replay_buffer.state_dict()
+        path = ckpt_path
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        tmp = path + ".tmp"
+        torch.save(state, tmp)
+        os.replace(tmp, path)
+        for buf, idx, old in restore:
+            buf["dones"][idx] = old
         self._prune(runner, ckpt_path)
 
-    def on_checkpoint_trainer(self, runner, player_trainer_group, ckpt_path: str, state: Dict[str, Any]) -> None:
-        # trainer rank 1 ships its state to the player (rank 0), which writes it
-        runner.send_object_to_player(state, player_trainer_group)
+    def on_checkpoint_trainer(self, runner, comm, state: Dict[str, Any]) -> None:
+        """Decoupled trainer rank 1 ships its state to the player, which writes it."""
+        comm.player_trainer_object(_to_cpu(state))
 
     def _prune(self, runner, ckpt_path: str) -> None:
         if not self.keep_last or not runner.is_global_zero:

@@ -154,15 +154,22 @@ def make_env(
     return thunk
 
 
-def get_dummy_env(id: str):
+def get_dummy_env(id: str, size=None):
+    """Test envs (reference ``utils/env.py`` dummy branch).  ``*_vec`` ids (or a 1-D ``size``) give
+    vector observations (mapped to the ``state`` key) for the vector-only agents (SAC, DroQ)."""
     from sheeprl_prey_amd.envs.dummy import ContinuousDummyEnv, DiscreteDummyEnv, MultiDiscreteDummyEnv
 
+    kw = {}
+    if size is not None:
+        kw["size"] = tuple(size)
+    elif id.endswith("_vec"):
+        kw["size"] = (8,)
     if "continuous" in id:
-        return ContinuousDummyEnv()
+        return ContinuousDummyEnv(**kw)
     if "multidiscrete" in id:
-        return MultiDiscreteDummyEnv()
+        return MultiDiscreteDummyEnv(**kw)
     if "discrete" in id:
-        return DiscreteDummyEnv()
+        return DiscreteDummyEnv(**kw)
     raise ValueError(f"Unrecognized dummy environment: {id}")
 
 

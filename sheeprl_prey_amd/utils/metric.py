@@ -76,6 +76,9 @@ class MetricAggregator:
     def __iter__(self):
         return iter(self.metrics.keys())
 
+    def __contains__(self, name: str) -> bool:
+        return name in self.metrics
+
     def add(self, name: str, metric: Any) -> None:
         if self.disabled:
             return
