@@ -1,0 +1,137 @@
+"""End-to-end algorithm tests (CPU, gloo) - the reference's ``tests/test_algos/test_algos.py``
+strategy: run the real CLI in-process with ``dry_run=True`` and tiny models, then check the
+checkpoint key set and the saved ``.hydra/config.yaml``.  ``devices=2`` runs two gloo ranks
+(spawned processes) exercising the gradient all-reduce / all-gather / decoupled paths.
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+from unittest import mock
+
+import pytest
+import torch
+
+from sheeprl_prey_amd.cli import run
+
+STD = [
+    "dry_run=True",
+    "env.num_envs=1",
+    "env.sync_env=True",
+    "env.capture_video=False",
+]
+
+
+def _run(args, devices: int):
+    with mock.patch.dict(os.environ, {"LT_ACCELERATOR": "cpu", "LT_DEVICES": str(devices)}, clear=False):
+        run(list(args))
+
+
+def _check_ckpt(root: str, run_name: str, keys: set, rb: bool) -> dict:
+    base = Path("logs", "runs", root, run_name)
+    versions = sorted(base.iterdir())
+    ck_dir = versions[-1] / "checkpoint"
+    assert ck_dir.is_dir(), f"no checkpoint dir under {versions[-1]}"
+    ckpts = sorted(ck_dir.glob("*.ckpt"))
+    assert ckpts, "no checkpoint written"
+    state = torch.load(ckpts[-1], map_location="cpu", weights_only=True)
+    want = set(keys) | ({"rb"} if rb else set())
+    assert set(state.keys()) == want, f"checkpoint keys {sorted(state)} != {sorted(want)}"
+    assert (versions[-1] / ".." / ".hydra" / "config.yaml").resolve().exists() or \
+        (base / ".hydra" / "config.yaml").exists()
+    return state
+
+
+SAC_KEYS = {"agent", "qf_optimizer", "actor_optimizer", "alpha_optimizer", "update", "last_log", "last_checkpoint",
+            "batch_size"}
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("devices", [1, 2])
+@pytest.mark.parametrize("checkpoint_buffer", [True, False])
+def test_sac(devices, checkpoint_buffer):
+    _run(STD + ["exp=sac", "env=dummy", "env.id=continuous_dummy_vec", "per_rank_batch_size=1",
+                f"buffer.size={devices}", "algo.learning_starts=0", "algo.per_rank_gradient_steps=1",
+                "algo.hidden_size=8", "root_dir=sac", f"run_name=r{devices}{int(checkpoint_buffer)}",
+                f"buffer.checkpoint={checkpoint_buffer}"], devices)
+    st = _check_ckpt("sac", f"r{devices}{int(checkpoint_buffer)}", SAC_KEYS, checkpoint_buffer)
+    if checkpoint_buffer and devices == 2:
+        assert isinstance(st["rb"], list) and len(st["rb"]) == 2
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("devices", [1, 2])
+def test_droq(devices):
+    _run(STD + ["exp=droq", "env=dummy", "env.id=continuous_dummy_vec", "per_rank_batch_size=1",
+                f"buffer.size={devices}", "algo.learning_starts=0", "algo.per_rank_gradient_steps=1",
+                "algo.hidden_size=8", "root_dir=droq", "run_name=r", "buffer.checkpoint=True"], devices)
+    _check_ckpt("droq", "r", SAC_KEYS, True)
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("devices", [1, 2])
+def test_sac_ae(devices):
+    _run(STD + ["exp=sac_ae", "env.id=Pendulum-v1", "per_rank_batch_size=1", f"buffer.size={devices}",
+                "algo.learning_starts=0", "algo.per_rank_gradient_steps=1", "root_dir=sac_ae", "run_name=r",
+                "mlp_keys.encoder=[state]", "cnn_keys.encoder=[rgb]", "env.screen_size=64", "algo.hidden_size=4",
+                "algo.dense_units=4", "algo.cnn_channels_multiplier=2", "algo.actor.network_frequency=1",
+                "algo.decoder.update_freq=1", "buffer.checkpoint=True"], devices)
+    _check_ckpt("sac_ae", "r", SAC_KEYS | {"encoder", "decoder", "encoder_optimizer", "decoder_optimizer"}, True)
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("devices", [2, 3])
+def test_sac_decoupled(devices):
+    _run(STD + ["exp=sac_decoupled", "env=dummy", "env.id=continuous_dummy_vec", "per_rank_batch_size=1",
+                "algo.learning_starts=0", "algo.per_rank_gradient_steps=1", "algo.hidden_size=8",
+                "root_dir=sac_dec", f"run_name=r{devices}", "buffer.checkpoint=True"], devices)
+    _check_ckpt("sac_dec", f"r{devices}", SAC_KEYS, True)
+
+
+PPO_KEYS = {"agent", "optimizer", "scheduler", "update", "batch_size", "last_log", "last_checkpoint"}
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("devices", [1, 2])
+@pytest.mark.parametrize("env_id", ["discrete_dummy", "multidiscrete_dummy", "continuous_dummy"])
+def test_ppo(devices, env_id):
+    _run(STD + ["exp=ppo", "env=dummy", f"env.id={env_id}", f"algo.rollout_steps={devices}",
+                "per_rank_batch_size=1", "root_dir=ppo", f"run_name={env_id}{devices}"], devices)
+    _check_ckpt("ppo", f"{env_id}{devices}", PPO_KEYS, False)
+
+
+DV3_KEYS = {"world_model", "actor", "critic", "target_critic", "world_optimizer", "actor_optimizer",
+            "critic_optimizer", "expl_decay_steps", "moments", "update", "batch_size", "last_log", "last_checkpoint"}
+
+TINY_DREAMER = [
+    "per_rank_sequence_length=1", "per_rank_batch_size=1", "algo.learning_starts=0", "algo.horizon=8",
+    "algo.per_rank_gradient_steps=1", "algo.dense_units=8", "algo.world_model.encoder.cnn_channels_multiplier=2",
+    "algo.world_model.recurrent_model.recurrent_state_size=8", "algo.world_model.representation_model.hidden_size=8",
+    "algo.world_model.transition_model.hidden_size=8", "algo.layer_norm=True", "algo.train_every=1",
+    "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]",
+]
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("devices", [1, 2])
+@pytest.mark.parametrize("env_id", ["discrete_dummy", "continuous_dummy"])
+def test_dreamer_v3(devices, env_id):
+    _run(STD + ["exp=dreamer_v3", "env=dummy", f"env.id={env_id}", f"buffer.size={devices}", "root_dir=dv3",
+                f"run_name={env_id}{devices}", "buffer.checkpoint=True"] + TINY_DREAMER, devices)
+    _check_ckpt("dv3", f"{env_id}{devices}", DV3_KEYS, True)
+
+
+def test_fsdp_rejected():
+    with pytest.raises(ValueError, match="FSDP"):
+        _run(["exp=ppo", "env=dummy", "fabric.strategy=fsdp", "dry_run=True"], 1)
+
+
+def test_resume_sac(tmp_path):
+    args = STD + ["exp=sac", "env=dummy", "env.id=continuous_dummy_vec", "per_rank_batch_size=1", "buffer.size=4",
+                  "algo.learning_starts=0", "algo.per_rank_gradient_steps=1", "algo.hidden_size=8",
+                  "root_dir=resume", "run_name=a", "buffer.checkpoint=True"]
+    _run(args, 1)
+    ck = sorted(Path("logs", "runs", "resume", "a").rglob("*.ckpt"))[-1]
+    _run(STD + ["exp=sac", "env=dummy", "env.id=continuous_dummy_vec", f"checkpoint.resume_from={ck}",
+                "root_dir=resume", "run_name=b"], 1)
+    assert list(Path("logs", "runs", "resume", "b").rglob("*.ckpt"))

@@ -1,0 +1,56 @@
+"""The same CLI dry runs as ``test_algos.py`` on one MI355X (fused HIP ops, hipGraph-captured updates)."""
+from __future__ import annotations
+
+import os
+from unittest import mock
+
+import pytest
+
+from sheeprl_prey_amd.cli import run
+from tests.test_algos import DV3_KEYS, PPO_KEYS, SAC_KEYS, STD, TINY_DREAMER, _check_ckpt
+
+pytestmark = pytest.mark.gpu
+
+GPU = ["fabric.accelerator=cuda", "fabric.cuda_graphs=True"]
+
+
+def _run(args):
+    with mock.patch.dict(os.environ, {"LT_ACCELERATOR": "cuda", "LT_DEVICES": "1"}, clear=False):
+        run(list(args) + GPU)
+
+
+def test_sac_gpu():
+    _run(STD + ["exp=sac", "env=dummy", "env.id=continuous_dummy_vec", "per_rank_batch_size=4", "buffer.size=8",
+                "algo.learning_starts=0", "algo.per_rank_gradient_steps=4", "root_dir=sac", "run_name=g",
+                "buffer.checkpoint=True"])
+    _check_ckpt("sac", "g", SAC_KEYS, True)
+
+
+def test_droq_gpu():
+    _run(STD + ["exp=droq", "env=dummy", "env.id=continuous_dummy_vec", "per_rank_batch_size=4", "buffer.size=8",
+                "algo.learning_starts=0", "algo.per_rank_gradient_steps=4", "root_dir=droq", "run_name=g",
+                "buffer.checkpoint=True"])
+    _check_ckpt("droq", "g", SAC_KEYS, True)
+
+
+def test_sac_ae_gpu():
+    _run(STD + ["exp=sac_ae", "env.id=Pendulum-v1", "per_rank_batch_size=2", "buffer.size=4",
+                "algo.learning_starts=0", "algo.per_rank_gradient_steps=4", "root_dir=sac_ae", "run_name=g",
+                "mlp_keys.encoder=[state]", "cnn_keys.encoder=[rgb]", "env.screen_size=64", "algo.hidden_size=16",
+                "algo.dense_units=16", "algo.cnn_channels_multiplier=2", "algo.actor.network_frequency=1",
+                "algo.decoder.update_freq=1", "buffer.checkpoint=True"])
+    _check_ckpt("sac_ae", "g", SAC_KEYS | {"encoder", "decoder", "encoder_optimizer", "decoder_optimizer"}, True)
+
+
+@pytest.mark.parametrize("env_id", ["discrete_dummy", "continuous_dummy"])
+def test_ppo_gpu(env_id):
+    _run(STD + ["exp=ppo", "env=dummy", f"env.id={env_id}", "algo.rollout_steps=4", "per_rank_batch_size=2",
+                "root_dir=ppo", f"run_name={env_id}"])
+    _check_ckpt("ppo", env_id, PPO_KEYS, False)
+
+
+@pytest.mark.parametrize("env_id", ["discrete_dummy", "continuous_dummy"])
+def test_dreamer_v3_gpu(env_id):
+    _run(STD + ["exp=dreamer_v3", "env=dummy", f"env.id={env_id}", "buffer.size=4", "root_dir=dv3",
+                f"run_name={env_id}", "buffer.checkpoint=True"] + TINY_DREAMER)
+    _check_ckpt("dv3", env_id, DV3_KEYS, True)

@@ -1,0 +1,254 @@
+"""CPU unit tests: config composition, models, fused-op oracles, flat optimisers, logger, envs."""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from sheeprl_prey_amd import ops
+from sheeprl_prey_amd.config.compose import compose
+from sheeprl_prey_amd.models.ensemble import EnsembleMLP
+from sheeprl_prey_amd.models.models import CNN, MLP
+from sheeprl_prey_amd.parallel.flat_optim import FlatAdam, build_optimizer, flatten_like
+
+CONFIG_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "sheeprl_prey_amd", "configs")
+PRESETS = sorted(f[:-5] for f in os.listdir(os.path.join(CONFIG_DIR, "exp")) if f.endswith(".yaml") and f != "default.yaml")
+
+
+# ---------------------------------------------------------------- config
+@pytest.mark.parametrize("exp", PRESETS)
+def test_every_preset_composes(exp):
+    cfg = compose([f"exp={exp}"])
+    assert cfg["algo"]["name"] != "???"
+    assert "fabric" in cfg and "env" in cfg and "buffer" in cfg
+    assert isinstance(cfg["total_steps"], int)
+
+
+def test_cli_style_overrides():
+    cfg = compose(["exp=ppo", "algo.optimizer.lr=0.5", "+new_key=3", "env.num_envs=7"])
+    assert cfg["algo"]["optimizer"]["lr"] == 0.5
+    assert cfg["new_key"] == 3
+    assert cfg["env"]["num_envs"] == 7
+    assert cfg["algo"]["name"] == "ppo"
+
+
+def test_dv3_100k_preset_values():
+    cfg = compose(["exp=dreamer_v3_100k_ms_pacman"])
+    a = cfg["algo"]
+    assert a["world_model"]["recurrent_model"]["recurrent_state_size"] == 512
+    assert a["dense_units"] == 512 and a["mlp_layers"] == 2
+    assert cfg["per_rank_batch_size"] == 16 and cfg["per_rank_sequence_length"] == 64
+    assert a["replay_ratio"] if "replay_ratio" in a else a["train_every"] == 1
+
+
+# ---------------------------------------------------------------- models
+def test_mlp_shapes_and_errors():
+    with pytest.raises(ValueError):
+        MLP(10)
+    m = MLP(10, 3, (16, 16), norm_layer=nn.LayerNorm, norm_args={"normalized_shape": 16})
+    assert m(torch.rand(4, 10)).shape == (4, 3)
+    assert m(torch.rand(2, 5, 10)).shape == (2, 5, 3)
+    m2 = MLP((2, 5), 4, (8,), flatten_dim=1)
+    assert m2(torch.rand(3, 2, 5)).shape == (3, 4)
+
+
+def test_cnn_shapes():
+    c = CNN(3, [8, 16], layer_args={"kernel_size": 3, "stride": 2})
+    assert c(torch.rand(2, 3, 32, 32)).shape == (2, 16, 7, 7)
+    with pytest.raises(ValueError):
+        CNN(3, [], layer_args={"kernel_size": 3})
+
+
+def test_ensemble_equals_separate_mlps():
+    torch.manual_seed(0)
+    n, d, h = 3, 7, 16
+    ens = EnsembleMLP(n, d, (h, h), 1, activation="relu", layer_norm=True)
+    x = torch.randn(5, d)
+    y = ens(x)  # [n, 5, 1]
+    for i in range(n):
+        z = x
+        for j, lin in enumerate(ens.layers):
+            z = z @ lin.weight[i].T + lin.bias[i]
+            z = torch.nn.functional.layer_norm(z, (h,), ens.norms[j].weight[i], ens.norms[j].bias[i])
+            z = torch.relu(z)
+        z = z @ ens.head.weight[i].T + ens.head.bias[i]
+        torch.testing.assert_close(y[i], z)
+
+
+def test_ensemble_member_grads_are_independent():
+    ens = EnsembleMLP(2, 4, (8,), 1)
+    x = torch.randn(6, 4)
+    y = ens(x)
+    y[0].sum().backward()
+    assert ens.layers[0].weight.grad[1].abs().sum() == 0
+    assert ens.layers[0].weight.grad[0].abs().sum() > 0
+
+
+# ---------------------------------------------------------------- op oracles
+@pytest.mark.parametrize("mode", [0, 1])
+def test_squashed_gaussian_oracle_matches_torch_distributions(mode):
+    torch.manual_seed(0)
+    mean = torch.randn(6, 3, requires_grad=True)
+    raw = torch.randn(6, 3, requires_grad=True) * 3
+    eps = torch.randn(6, 3)
+    scale, bias = torch.tensor([1.0, 2.0, 0.5]), torch.tensor([0.0, 1.0, -1.0])
+    lo, hi = (-5.0, 2.0) if mode == 0 else (-10.0, 2.0)
+    a, lp = ops.squashed_gaussian(mean, raw, scale, bias, mode, lo, hi, eps=eps)
+    ls = raw.clamp(lo, hi) if mode == 0 else lo + 0.5 * (hi - lo) * (torch.tanh(raw) + 1)
+    dist = torch.distributions.Normal(mean, ls.exp())
+    x = mean + ls.exp() * eps
+    y = torch.tanh(x)
+    lp_ref = (dist.log_prob(x) - torch.log(scale * (1 - y.pow(2)) + 1e-6)).sum(-1, keepdim=True)
+    torch.testing.assert_close(a, y * scale + bias)
+    # (x-mean)/std recomputed by Normal.log_prob loses digits for std ~ e^-10; the oracle uses eps directly
+    torch.testing.assert_close(lp, lp_ref, rtol=1e-4, atol=1e-3)
+
+
+def test_gae_oracle():
+    from sheeprl_prey_amd.ops import reference as ref
+
+    T, B = 5, 2
+    r, v, d = torch.rand(T, B, 1), torch.rand(T, B, 1), (torch.rand(T, B, 1) > 0.7).float()
+    nv = torch.rand(B, 1)
+    ret, adv = ref.gae(r, v, d, nv, 0.99, 0.95)
+    # explicit recursion
+    last = torch.zeros(B, 1)
+    exp = torch.zeros(T, B, 1)
+    for t in reversed(range(T)):
+        nxt = nv if t == T - 1 else v[t + 1]
+        delta = r[t] + 0.99 * nxt * (1 - d[t]) - v[t]
+        last = delta + 0.99 * 0.95 * (1 - d[t]) * last
+        exp[t] = last
+    torch.testing.assert_close(adv, exp)
+    torch.testing.assert_close(ret, exp + v)
+
+
+# ---------------------------------------------------------------- flat optimisers
+def test_flat_adam_matches_torch_adam():
+    torch.manual_seed(0)
+    a = nn.Sequential(nn.Linear(5, 7), nn.Tanh(), nn.Linear(7, 3))
+    b = nn.Sequential(nn.Linear(5, 7), nn.Tanh(), nn.Linear(7, 3))
+    b.load_state_dict(a.state_dict())
+    oa = torch.optim.Adam(a.parameters(), lr=1e-2, eps=1e-5, weight_decay=0.01)
+    ob = build_optimizer({"_target_": "torch.optim.Adam", "lr": 1e-2, "eps": 1e-5, "weight_decay": 0.01},
+                         b.parameters())
+    for _ in range(5):
+        x = torch.randn(8, 5)
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad()
+            m(x).pow(2).mean().backward()
+            o.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
+    sd = ob.state_dict()
+    assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
+
+
+def test_flat_clip_matches_torch():
+    torch.manual_seed(1)
+    a = nn.Linear(4, 4)
+    b = nn.Linear(4, 4)
+    b.load_state_dict(a.state_dict())
+    oa = torch.optim.SGD(a.parameters(), lr=0.1)
+    ob = build_optimizer({"_target_": "torch.optim.SGD", "lr": 0.1}, b.parameters())
+    x = torch.randn(3, 4) * 10
+    for m, o in ((a, oa), (b, ob)):
+        o.zero_grad()
+        m(x).pow(2).sum().backward()
+    torch.nn.utils.clip_grad_norm_(a.parameters(), 0.5)
+    ob.clip_grad_norm_(0.5)
+    oa.step()
+    ob.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
+
+
+def test_shared_slab_optimisers():
+    enc, head = nn.Linear(3, 4), nn.Linear(4, 1)
+    critic = nn.Sequential(enc, head)
+    o_all = FlatAdam(critic.parameters(), lr=0.1)
+    o_enc = FlatAdam(enc.parameters(), lr=0.1)
+    assert o_enc.flat_param.data_ptr() == o_all.flat_param.data_ptr()
+    o_enc.zero_grad()
+    enc(torch.randn(2, 3)).sum().backward()
+    o_enc.step()
+    # writes through the shared storage
+    torch.testing.assert_close(enc.weight.view(-1), o_all.flat_param[: enc.weight.numel()])
+    with pytest.raises(ValueError):
+        FlatAdam(list(head.parameters()) + [nn.Parameter(torch.zeros(2))], lr=0.1)
+
+
+def test_flatten_like_target_ema():
+    src = nn.Linear(3, 2)
+    tgt = nn.Linear(3, 2)
+    opt = FlatAdam(src.parameters(), lr=0.1)
+    flat = flatten_like(tgt, opt)
+    before = tgt.weight.detach().clone()
+    flat.lerp_(opt.flat_param, 0.25)
+    torch.testing.assert_close(tgt.weight, before + 0.25 * (src.weight - before))
+
+
+# ---------------------------------------------------------------- logger
+def test_tfevents_roundtrip(tmp_path):
+    from sheeprl_prey_amd.utils.logger import TensorBoardLogger, read_events
+
+    lg = TensorBoardLogger(str(tmp_path), name="run")
+    lg.log_metrics({"Loss/a": 1.5, "Loss/b": -2.0}, 3)
+    lg.log_metrics({"Loss/a": 0.5}, 4)
+    lg.finalize("success")
+    files = [os.path.join(dp, f) for dp, _, fs in os.walk(lg.log_dir) for f in fs if "tfevents" in f]
+    assert files
+    ev = read_events(files[0])
+    assert ("Loss/a", 1.5, 3) in [(t, round(v, 4), s) for t, v, s in ev]
+    assert ("Loss/a", 0.5, 4) in [(t, round(v, 4), s) for t, v, s in ev]
+
+
+# ---------------------------------------------------------------- envs
+def test_vector_env_autoreset_and_final_info():
+    from sheeprl_prey_amd.envs.registry import make
+    from sheeprl_prey_amd.envs.core import RecordEpisodeStatistics
+    from sheeprl_prey_amd.envs.vector import SyncVectorEnv
+
+    envs = SyncVectorEnv([lambda: RecordEpisodeStatistics(make("CartPole-v1")) for _ in range(2)])
+    envs.reset(seed=0)
+    saw_final = False
+    for _ in range(600):
+        _, _, term, trunc, info = envs.step(envs.action_space.sample())
+        if np.any(term | trunc):
+            assert "final_observation" in info and "final_info" in info
+            idx = int(np.nonzero(term | trunc)[0][0])
+            assert info["final_info"][idx]["episode"]["l"] > 0
+            saw_final = True
+            break
+    envs.close()
+    assert saw_final
+
+
+def test_make_env_dict_obs_and_frame_stack():
+    from sheeprl_prey_amd.utils.env import make_env
+    from sheeprl_prey_amd.utils.utils import dotdict
+
+    cfg = dotdict(compose(["exp=dreamer_v3", "env=dummy", "env.id=discrete_dummy", "cnn_keys.encoder=[rgb]",
+                           "env.frame_stack=2", "env.screen_size=32"]))
+    env = make_env(cfg, 0, 0, None, "test")()
+    o, _ = env.reset(seed=0)
+    assert set(o) == {"rgb"}
+    assert o["rgb"].shape == env.observation_space["rgb"].shape == (2, 3, 32, 32)
+
+
+def test_mask_velocities_requires_known_env():
+    from sheeprl_prey_amd.envs.registry import make
+    from sheeprl_prey_amd.envs.wrappers import MaskVelocityWrapper
+
+    from sheeprl_prey_amd.envs.dummy import ContinuousDummyEnv
+
+    w = MaskVelocityWrapper(make("CartPole-v1"))
+    o, _ = w.reset(seed=0)
+    o, *_ = w.step(0)
+    assert o[1] == 0 and o[3] == 0
+    with pytest.raises(NotImplementedError):
+        MaskVelocityWrapper(ContinuousDummyEnv(size=(4,)))
