@@ -254,3 +254,24 @@ def stack(tds: Sequence[TensorDict], dim: int = 0) -> TensorDict:
     for k in tds[0].keys():
         out._data[k] = torch.stack([t[k] for t in tds], dim=d)
     return out
+
+
+def pad_sequence(seqs: Sequence[TensorDict], return_mask: bool = True) -> TensorDict:
+    """Stack variable-length ``[L_i, ...]`` TensorDicts into ``[L_max, N, ...]`` (zero padding at
+    the END of each sequence) plus a boolean ``mask`` ``[L_max, N]`` (True on real steps)."""
+    if not seqs:
+        raise ValueError("pad_sequence needs at least one sequence")
+    L = max(s.shape[0] for s in seqs)
+    N = len(seqs)
+    dev = seqs[0]._first_device()
+    out = {}
+    for k in seqs[0].keys():
+        ref = seqs[0][k]
+        buf = torch.zeros((L, N) + tuple(ref.shape[1:]), dtype=ref.dtype, device=ref.device)
+        for i, s in enumerate(seqs):
+            buf[: s.shape[0], i] = s[k]
+        out[k] = buf
+    if return_mask:
+        lengths = torch.tensor([s.shape[0] for s in seqs], device=dev)
+        out["mask"] = torch.arange(L, device=dev).unsqueeze(1) < lengths.unsqueeze(0)
+    return TensorDict(out, batch_size=[L, N], device=dev)

@@ -291,6 +291,41 @@ class Runner:
         params = [p for p in (module.parameters() if module is not None else []) if p.grad is not None]
         return torch.nn.utils.clip_grad_norm_(params, max_norm, norm_type=norm_type, error_if_nonfinite=error_if_nonfinite)
 
+    # ------------------------------------------------------------------ uneven inputs (DDP ``Join``)
+    def max_steps(self, n_local: int) -> int:
+        """Ranks with different numbers of optimisation steps (uneven data) agree on the max; the
+        ranks that run out shadow the remaining gradient all-reduces (``shadow_step``) like
+        ``torch.distributed.algorithms.Join`` does for DDP (reference ``ppo_recurrent.py:54``)."""
+        if self.world_size <= 1:
+            return n_local
+        dev = self.device if self.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([n_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+    def shadow_step(self, optimizer) -> None:
+        """Contribute zero gradients to a collective the other ranks are running (no update)."""
+        optimizer.zero_grad()
+        self.sync_gradients(optimizer)
+
+    def sync_from_last_joiner(self, module: nn.Module, n_local: int, n_max: int) -> None:
+        """After uneven training every rank takes the weights of a rank that ran all ``n_max``
+        steps (DDP Join's final model sync)."""
+        if self.world_size <= 1:
+            return
+        dev = self.device if self.backend == "nccl" else torch.device("cpu")
+        cand = torch.tensor([self.global_rank if n_local == n_max else 1 << 30], dtype=torch.int64, device=dev)
+        dist.all_reduce(cand, op=dist.ReduceOp.MIN, group=self.group)
+        src = int(cand.item())
+        with torch.no_grad():
+            flat = torch.cat([p.data.reshape(-1) for p in module.parameters()])
+            self.broadcast(flat, src=src)
+            off = 0
+            for p in module.parameters():
+                n = p.numel()
+                p.data.copy_(flat[off : off + n].view_as(p))
+                off += n
+
     # ------------------------------------------------------------------ collectives
     def barrier(self, *_args, **_kw) -> None:
         if self.world_size > 1:

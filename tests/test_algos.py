@@ -135,3 +135,52 @@ def test_resume_sac(tmp_path):
     _run(STD + ["exp=sac", "env=dummy", "env.id=continuous_dummy_vec", f"checkpoint.resume_from={ck}",
                 "root_dir=resume", "run_name=b"], 1)
     assert list(Path("logs", "runs", "resume", "b").rglob("*.ckpt"))
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("devices", [1, 2, 3])
+@pytest.mark.parametrize("env_id", ["discrete_dummy", "continuous_dummy"])
+def test_ppo_decoupled(devices, env_id):
+    args = STD + ["exp=ppo_decoupled", "env=dummy", f"env.id={env_id}", f"algo.rollout_steps={devices}",
+                  "per_rank_batch_size=1", "algo.update_epochs=1", "root_dir=ppo_dec", f"run_name={env_id}{devices}"]
+    if devices == 1:
+        with pytest.raises(RuntimeError, match="greater than 1"):
+            _run(args, devices)
+        return
+    _run(args, devices)
+    _check_ckpt("ppo_dec", f"{env_id}{devices}", PPO_KEYS, False)
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("devices", [1, 2])
+def test_ppo_recurrent(devices):
+    _run(STD + ["exp=ppo_recurrent", "algo.rollout_steps=2", "per_rank_batch_size=1", "per_rank_sequence_length=2",
+                "algo.update_epochs=2", "root_dir=ppo_rec", f"run_name=r{devices}"], devices)
+    _check_ckpt("ppo_rec", f"r{devices}", PPO_KEYS, False)
+
+
+def test_pad_sequence_and_masked_losses():
+    from sheeprl_prey_amd.algos.ppo_recurrent.ppo_recurrent import masked_losses
+    from sheeprl_prey_amd.data.tensordict import TensorDict, pad_sequence
+    from sheeprl_prey_amd.utils.utils import dotdict
+
+    a = TensorDict({"x": torch.arange(3.0).view(3, 1)}, batch_size=[3])
+    b = TensorDict({"x": torch.arange(5.0).view(5, 1)}, batch_size=[5])
+    p = pad_sequence([a, b])
+    assert tuple(p.shape) == (5, 2) and p["mask"].sum() == 8 and p["x"][4, 0] == 0
+    # masked losses == losses over the gathered valid entries
+    torch.manual_seed(0)
+    shape = (5, 2, 1)
+    lp, olp, adv, v, ov, ret, ent = (torch.randn(shape) for _ in range(7))
+    m = p["mask"].unsqueeze(-1).float()
+    cfg = dotdict({"algo": {"normalize_advantages": True, "clip_coef": 0.2, "clip_vloss": True, "loss_reduction": "mean"}})
+    pg, vl, el = masked_losses(lp, olp, adv, v, ov, ret, ent, m, cfg)
+    sel = p["mask"].unsqueeze(-1)
+    A = adv[sel]
+    A = (A - A.mean()) / (A.std() + 1e-8)
+    r = (lp[sel] - olp[sel]).exp()
+    pg_ref = (-torch.min(A * r, A * r.clamp(0.8, 1.2))).mean()
+    pred = ov[sel] + (v[sel] - ov[sel]).clamp(-0.2, 0.2)
+    torch.testing.assert_close(pg, pg_ref)
+    torch.testing.assert_close(vl, (pred - ret[sel]).pow(2).mean())
+    torch.testing.assert_close(el, -ent[sel].mean())
