@@ -333,7 +333,8 @@ class Actor(nn.Module):
 
     def __init__(self, latent_state_size: int, actions_dim: Sequence[int], is_continuous: bool,
                  distribution_cfg: Dict[str, Any], init_std: float = 0.0, min_std: float = 0.1, dense_units: int = 1024,
-                 activation: ModuleType = nn.SiLU, mlp_layers: int = 5, layer_norm: bool = True, unimix: float = 0.01) -> None:
+                 activation: ModuleType = nn.SiLU, mlp_layers: int = 5, layer_norm: bool = True, unimix: float = 0.01,
+                 ln_eps: float = 1e-3, bias: Optional[bool] = None) -> None:
         super().__init__()
         self.distribution_cfg = distribution_cfg
         dist = str(distribution_cfg.get("type", "auto")).lower()
@@ -349,9 +350,9 @@ class Actor(nn.Module):
         self.distribution = dist
         self.model = MLP(
             input_dims=latent_state_size, output_dim=None, hidden_sizes=[dense_units] * mlp_layers, activation=activation,
-            flatten_dim=None, layer_args={"bias": not layer_norm},
+            flatten_dim=None, layer_args={"bias": (not layer_norm) if bias is None else bias},
             norm_layer=[nn.LayerNorm for _ in range(mlp_layers)] if layer_norm else None,
-            norm_args=[{"normalized_shape": dense_units, "eps": 1e-3} for _ in range(mlp_layers)] if layer_norm else None,
+            norm_args=[{"normalized_shape": dense_units, "eps": ln_eps} for _ in range(mlp_layers)] if layer_norm else None,
         )
         if is_continuous:
             self.mlp_heads = nn.ModuleList([nn.Linear(dense_units, int(np.sum(actions_dim)) * 2)])

@@ -62,7 +62,7 @@ def compute_lambda_values(rewards: Tensor, values: Tensor, continues: Tensor, lm
 
 @torch.no_grad()
 def test(player, runner, cfg: Dict[str, Any], log_dir: str, test_name: str = "", sample_actions: bool = False,
-         render: bool = False) -> float:
+         render: bool = False, obs_offset: float = 0.0) -> float:
     """One greedy (or sampled) episode; logs ``Test/cumulative_reward``."""
     env = make_env(cfg, cfg.seed, 0, log_dir, "test" + (f"_{test_name}" if test_name != "" else ""))()
     done = False
@@ -76,7 +76,7 @@ def test(player, runner, cfg: Dict[str, Any], log_dir: str, test_name: str = "",
         for k, v in next_obs.items():
             t = torch.as_tensor(np.asarray(v), device=device).view(1, 1, *np.asarray(v).shape).float()
             if k in cfg.cnn_keys.encoder:
-                pre[k] = t / 255
+                pre[k] = t / 255 + obs_offset
             elif k in cfg.mlp_keys.encoder:
                 pre[k] = t
         mask = {k: v for k, v in pre.items() if k.startswith("mask")} or None

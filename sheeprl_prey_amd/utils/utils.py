@@ -105,8 +105,13 @@ def symexp(x: Tensor) -> Tensor:
 
 
 def init_weights(m: torch.nn.Module) -> None:
-    """Kaiming init (reference ``utils.py:119-125``)."""
-    if isinstance(m, (torch.nn.Linear, torch.nn.Conv2d)):
+    """Kaiming-uniform init, zero bias (reference ``utils/utils.py:75-89``): convolutions with the
+    ReLU gain, linears with the default (leaky-ReLU a=0) gain."""
+    if isinstance(m, (torch.nn.Conv2d, torch.nn.ConvTranspose2d)):
+        torch.nn.init.kaiming_uniform_(m.weight, nonlinearity="relu")
+        if m.bias is not None:
+            m.bias.data.zero_()
+    elif isinstance(m, torch.nn.Linear):
         torch.nn.init.kaiming_uniform_(m.weight)
         if m.bias is not None:
             m.bias.data.zero_()

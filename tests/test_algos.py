@@ -184,3 +184,89 @@ def test_pad_sequence_and_masked_losses():
     torch.testing.assert_close(pg, pg_ref)
     torch.testing.assert_close(vl, (pred - ret[sel]).pow(2).mean())
     torch.testing.assert_close(el, -ent[sel].mean())
+
+
+DV1_KEYS = {"world_model", "actor", "critic", "world_optimizer", "actor_optimizer", "critic_optimizer",
+            "expl_decay_steps", "update", "batch_size", "last_log", "last_checkpoint"}
+DV2_KEYS = DV1_KEYS | {"target_critic"}
+P2E1_KEYS = {"world_model", "actor_task", "critic_task", "ensembles", "world_optimizer", "actor_task_optimizer",
+             "critic_task_optimizer", "ensemble_optimizer", "expl_decay_steps", "update", "batch_size",
+             "actor_exploration", "critic_exploration", "actor_exploration_optimizer", "critic_exploration_optimizer",
+             "last_log", "last_checkpoint"}
+P2E2_KEYS = P2E1_KEYS | {"target_critic_task", "target_critic_exploration"}
+SMALL_WM = ["algo.dense_units=8", "algo.world_model.encoder.cnn_channels_multiplier=2",
+            "algo.world_model.recurrent_model.recurrent_state_size=8", "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]",
+            "algo.learning_starts=0", "algo.per_rank_gradient_steps=1"]
+DV2_EXTRA = ["algo.world_model.representation_model.hidden_size=8", "algo.world_model.transition_model.hidden_size=8"]
+ENVS3 = ["discrete_dummy", "multidiscrete_dummy", "continuous_dummy"]
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("env_id", ENVS3)
+@pytest.mark.parametrize("checkpoint_buffer", [True, False])
+def test_dreamer_v1(env_id, checkpoint_buffer):
+    name = f"{env_id}{int(checkpoint_buffer)}"
+    _run(STD + ["exp=dreamer_v1", "env=dummy", f"env.id={env_id}", "per_rank_batch_size=1", "per_rank_sequence_length=1",
+                "buffer.size=1", "algo.horizon=2", "root_dir=dv1", f"run_name={name}",
+                f"buffer.checkpoint={checkpoint_buffer}"] + SMALL_WM, 1)
+    _check_ckpt("dv1", name, DV1_KEYS, checkpoint_buffer)
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("env_id", ENVS3)
+@pytest.mark.parametrize("buffer_type", ["sequential", "episode"])
+def test_dreamer_v2(env_id, buffer_type):
+    name = f"{env_id}{buffer_type}"
+    _run(STD + ["exp=dreamer_v2", "env=dummy", f"env.id={env_id}", "per_rank_batch_size=1", "per_rank_sequence_length=1",
+                "buffer.size=2", "algo.horizon=8", "root_dir=dv2", f"run_name={name}", f"buffer.type={buffer_type}",
+                "buffer.checkpoint=True", "algo.world_model.use_continues=True"] + SMALL_WM + DV2_EXTRA, 1)
+    _check_ckpt("dv2", name, DV2_KEYS, True)
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("env_id", ENVS3)
+def test_p2e_dv1(env_id):
+    _run(STD + ["exp=p2e_dv1", "env=dummy", f"env.id={env_id}", "per_rank_batch_size=2", "per_rank_sequence_length=2",
+                "buffer.size=1", "algo.horizon=8", "root_dir=p2e1", f"run_name={env_id}", "buffer.checkpoint=True",
+                "algo.ensembles.n=3"] + SMALL_WM, 1)
+    _check_ckpt("p2e1", env_id, P2E1_KEYS, True)
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("env_id", ENVS3)
+def test_p2e_dv2(env_id):
+    _run(STD + ["exp=p2e_dv2", "env=dummy", f"env.id={env_id}", "per_rank_batch_size=2", "per_rank_sequence_length=2",
+                "buffer.size=1", "algo.horizon=8", "root_dir=p2e2", f"run_name={env_id}", "buffer.checkpoint=True",
+                "algo.ensembles.n=3"] + SMALL_WM + DV2_EXTRA, 1)
+    _check_ckpt("p2e2", env_id, P2E2_KEYS, True)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("algo", ["dreamer_v1", "dreamer_v2", "p2e_dv2"])
+def test_dreamers_two_ranks(algo):
+    extra = DV2_EXTRA if algo != "dreamer_v1" else []
+    _run(STD + [f"exp={algo}", "env=dummy", "env.id=discrete_dummy", "per_rank_batch_size=1",
+                "per_rank_sequence_length=1", "buffer.size=2", "algo.horizon=4", "root_dir=dr2", f"run_name={algo}",
+                "buffer.checkpoint=True"] + (["algo.ensembles.n=2"] if "p2e" in algo else []) + SMALL_WM + extra, 2)
+    keys = {"dreamer_v1": DV1_KEYS, "dreamer_v2": DV2_KEYS, "p2e_dv2": P2E2_KEYS}[algo]
+    _check_ckpt("dr2", algo, keys, True)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("algo", ["p2e_dv1", "p2e_dv2"])
+@pytest.mark.parametrize("env_id", ["discrete_dummy", "continuous_dummy"])
+def test_p2e_explores_then_switches(algo, env_id):
+    """Not a dry run: 3 exploration updates (ensemble + exploration actor/critic phases), then the task phases."""
+    extra = DV2_EXTRA if algo == "p2e_dv2" else []
+    args = ["dry_run=False", "env.num_envs=1", "env.sync_env=True", "env.capture_video=False", f"exp={algo}",
+            "env=dummy", f"env.id={env_id}", "per_rank_batch_size=2", "per_rank_sequence_length=2", "buffer.size=16",
+            "algo.horizon=3", "total_steps=5", "exploration_steps=3", "algo.train_every=1", "checkpoint.every=0",
+            "metric.log_every=1", "algo.ensembles.n=3", "root_dir=p2e_x", f"run_name={algo}{env_id}",
+            "algo.per_rank_pretrain_steps=1"] + SMALL_WM + extra
+    _run(args, 1)
+    import json
+
+    rows = [json.loads(l) for l in open(next(Path("logs", "runs", "p2e_x", f"{algo}{env_id}").rglob("metrics.jsonl")))]
+    keys = set().union(*[r.keys() for r in rows])
+    assert {"Loss/ensemble_loss", "Loss/policy_loss_exploration", "Loss/value_loss_exploration",
+            "Loss/policy_loss_task", "Rewards/intrinsic"} <= keys, keys

@@ -54,3 +54,39 @@ def test_dreamer_v3_gpu(env_id):
     _run(STD + ["exp=dreamer_v3", "env=dummy", f"env.id={env_id}", "buffer.size=4", "root_dir=dv3",
                 f"run_name={env_id}", "buffer.checkpoint=True"] + TINY_DREAMER)
     _check_ckpt("dv3", env_id, DV3_KEYS, True)
+
+
+from tests.test_algos import DV1_KEYS, DV2_KEYS, DV2_EXTRA, P2E1_KEYS, P2E2_KEYS, SMALL_WM  # noqa: E402
+
+
+def test_dreamer_v1_gpu():
+    _run(STD + ["exp=dreamer_v1", "env=dummy", "env.id=continuous_dummy", "per_rank_batch_size=4",
+                "per_rank_sequence_length=4", "buffer.size=16", "algo.horizon=4", "root_dir=dv1", "run_name=g",
+                "buffer.checkpoint=True", "algo.per_rank_pretrain_steps=4"] + SMALL_WM[:-1] +
+         ["algo.per_rank_gradient_steps=4"])
+    _check_ckpt("dv1", "g", DV1_KEYS, True)
+
+
+@pytest.mark.parametrize("env_id", ["discrete_dummy", "continuous_dummy"])
+def test_dreamer_v2_gpu(env_id):
+    _run(STD + ["exp=dreamer_v2", "env=dummy", f"env.id={env_id}", "per_rank_batch_size=4",
+                "per_rank_sequence_length=4", "buffer.size=16", "algo.horizon=4", "root_dir=dv2", f"run_name={env_id}",
+                "buffer.checkpoint=True", "algo.per_rank_pretrain_steps=4"] + SMALL_WM + DV2_EXTRA)
+    _check_ckpt("dv2", env_id, DV2_KEYS, True)
+
+
+@pytest.mark.parametrize("algo", ["p2e_dv1", "p2e_dv2"])
+def test_p2e_gpu_explore_phases(algo):
+    """Exploration (7-phase captured step) for 3 updates, then the task step."""
+    import json
+    from pathlib import Path
+
+    extra = DV2_EXTRA if algo == "p2e_dv2" else []
+    _run(["dry_run=False", "env.num_envs=1", "env.sync_env=True", "env.capture_video=False", f"exp={algo}",
+          "env=dummy", "env.id=discrete_dummy", "per_rank_batch_size=4", "per_rank_sequence_length=4",
+          "buffer.size=32", "algo.horizon=3", "total_steps=8", "exploration_steps=5", "algo.train_every=1",
+          "checkpoint.every=0", "metric.log_every=1", "algo.ensembles.n=4", "root_dir=p2e_g", f"run_name={algo}",
+          "algo.per_rank_pretrain_steps=1"] + SMALL_WM + extra)
+    rows = [json.loads(l) for l in open(next(Path("logs", "runs", "p2e_g", algo).rglob("metrics.jsonl")))]
+    keys = set().union(*[r.keys() for r in rows])
+    assert {"Loss/ensemble_loss", "Loss/policy_loss_exploration", "Loss/policy_loss_task"} <= keys
