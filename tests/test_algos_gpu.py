@@ -58,35 +58,34 @@ def test_dreamer_v3_gpu(env_id):
 
 from tests.test_algos import DV1_KEYS, DV2_KEYS, DV2_EXTRA, P2E1_KEYS, P2E2_KEYS, SMALL_WM  # noqa: E402
 
+# short real runs (not dry runs): the replay must hold a full sequence before the first update
+SHORT = ["dry_run=False", "env.num_envs=1", "env.sync_env=True", "env.capture_video=False", "per_rank_batch_size=4",
+         "per_rank_sequence_length=4", "buffer.size=64", "algo.horizon=4", "total_steps=12", "algo.train_every=1",
+         "checkpoint.every=0", "metric.log_every=1", "algo.per_rank_pretrain_steps=2", "buffer.checkpoint=True"]
+WM_GPU = [a for a in SMALL_WM if not a.startswith("algo.learning_starts")] + ["algo.learning_starts=6"]
+
 
 def test_dreamer_v1_gpu():
-    _run(STD + ["exp=dreamer_v1", "env=dummy", "env.id=continuous_dummy", "per_rank_batch_size=4",
-                "per_rank_sequence_length=4", "buffer.size=16", "algo.horizon=4", "root_dir=dv1", "run_name=g",
-                "buffer.checkpoint=True", "algo.per_rank_pretrain_steps=4"] + SMALL_WM[:-1] +
-         ["algo.per_rank_gradient_steps=4"])
+    _run(SHORT + ["exp=dreamer_v1", "env=dummy", "env.id=continuous_dummy", "root_dir=dv1", "run_name=g"] + WM_GPU)
     _check_ckpt("dv1", "g", DV1_KEYS, True)
 
 
 @pytest.mark.parametrize("env_id", ["discrete_dummy", "continuous_dummy"])
 def test_dreamer_v2_gpu(env_id):
-    _run(STD + ["exp=dreamer_v2", "env=dummy", f"env.id={env_id}", "per_rank_batch_size=4",
-                "per_rank_sequence_length=4", "buffer.size=16", "algo.horizon=4", "root_dir=dv2", f"run_name={env_id}",
-                "buffer.checkpoint=True", "algo.per_rank_pretrain_steps=4"] + SMALL_WM + DV2_EXTRA)
+    _run(SHORT + ["exp=dreamer_v2", "env=dummy", f"env.id={env_id}", "root_dir=dv2", f"run_name={env_id}"]
+         + WM_GPU + DV2_EXTRA)
     _check_ckpt("dv2", env_id, DV2_KEYS, True)
 
 
 @pytest.mark.parametrize("algo", ["p2e_dv1", "p2e_dv2"])
 def test_p2e_gpu_explore_phases(algo):
-    """Exploration (7-phase captured step) for 3 updates, then the task step."""
+    """Exploration (7-phase captured step) until update 9, then the task step."""
     import json
     from pathlib import Path
 
     extra = DV2_EXTRA if algo == "p2e_dv2" else []
-    _run(["dry_run=False", "env.num_envs=1", "env.sync_env=True", "env.capture_video=False", f"exp={algo}",
-          "env=dummy", "env.id=discrete_dummy", "per_rank_batch_size=4", "per_rank_sequence_length=4",
-          "buffer.size=32", "algo.horizon=3", "total_steps=8", "exploration_steps=5", "algo.train_every=1",
-          "checkpoint.every=0", "metric.log_every=1", "algo.ensembles.n=4", "root_dir=p2e_g", f"run_name={algo}",
-          "algo.per_rank_pretrain_steps=1"] + SMALL_WM + extra)
+    _run(SHORT + [f"exp={algo}", "env=dummy", "env.id=discrete_dummy", "exploration_steps=9", "algo.ensembles.n=4",
+                  "root_dir=p2e_g", f"run_name={algo}"] + WM_GPU + extra)
     rows = [json.loads(l) for l in open(next(Path("logs", "runs", "p2e_g", algo).rglob("metrics.jsonl")))]
     keys = set().union(*[r.keys() for r in rows])
     assert {"Loss/ensemble_loss", "Loss/policy_loss_exploration", "Loss/policy_loss_task"} <= keys
