@@ -30,8 +30,9 @@ def balanced_kl(posteriors_logits: Tensor, priors_logits: Tensor, groups: int, c
     """(kl_loss, kl[T,B]) with DreamerV2 KL balancing."""
     if free_avg:
         per, kl = ops.kl_balance(posteriors_logits, priors_logits, groups, classes, alpha, 1.0 - alpha, 0.0)
-        free = torch.tensor(free_nats, device=kl.device, dtype=kl.dtype)
-        return torch.where(kl.mean() > free, per.mean(), free), kl
+        m = kl.mean()
+        free = m.new_full((), float(free_nats))  # fill kernel: capturable (no host->device copy)
+        return torch.where(m > free, per.mean(), free), kl
     per, kl = ops.kl_balance(posteriors_logits, priors_logits, groups, classes, alpha, 1.0 - alpha, free_nats)
     return per.mean(), kl
 

@@ -374,7 +374,10 @@ class Actor(nn.Module):
         if self.distribution == "normal":
             return Independent(Normal(mean, std, validate_args=va), 1, validate_args=va)
         std = 2 * torch.sigmoid((std + self.init_std) / 2) + self.min_std
-        return Independent(TruncatedNormal(torch.tanh(mean), std, -1, 1, validate_args=va), 1, validate_args=va)
+        # bounds as device tensors (fill kernels): python scalars would be H2D-copied, which a hipGraph
+        # capture does not allow
+        lo, hi = mean.new_full((), -1.0), mean.new_full((), 1.0)
+        return Independent(TruncatedNormal(torch.tanh(mean), std, lo, hi, validate_args=va), 1, validate_args=va)
 
     def forward(self, state: Tensor, is_training: bool = True, mask: Optional[Dict[str, np.ndarray]] = None):
         out = self.model(state)

@@ -184,3 +184,20 @@ def batch_space(space: Space, n: int) -> Space:
     if isinstance(space, Dict):
         return Dict(OrderedDict((k, batch_space(s, n)) for k, s in space.spaces.items()))
     raise TypeError(f"cannot batch {space}")
+
+
+def from_external(space) -> Space:
+    """Convert a gymnasium/gym space (duck-typed by class name) into the native space classes, so
+    third-party envs (DMC, Crafter, DIAMBRA, MineDojo, MineRL) plug into the native wrappers."""
+    name = type(space).__name__
+    if isinstance(space, Space):
+        return space
+    if name == "Box":
+        return Box(space.low, space.high, tuple(space.shape), space.dtype)
+    if name == "Discrete":
+        return Discrete(int(space.n))
+    if name == "MultiDiscrete":
+        return MultiDiscrete(list(np.asarray(space.nvec).tolist()))
+    if name == "Dict":
+        return Dict({k: from_external(v) for k, v in space.spaces.items()})
+    raise TypeError(f"Unsupported external space: {space!r}")

@@ -89,3 +89,16 @@ def test_p2e_gpu_explore_phases(algo):
     rows = [json.loads(l) for l in open(next(Path("logs", "runs", "p2e_g", algo).rglob("metrics.jsonl")))]
     keys = set().union(*[r.keys() for r in rows])
     assert {"Loss/ensemble_loss", "Loss/policy_loss_exploration", "Loss/policy_loss_task"} <= keys
+
+
+def test_dreamer_v3_continuous_graph_capture():
+    """Continuous DV3 (truncated-normal actor, differentiable imagination) through a captured hipGraph."""
+    _run(SHORT + ["exp=dreamer_v3", "env=dummy", "env.id=continuous_dummy", "root_dir=dv3c", "run_name=g",
+                  "algo.dense_units=8", "algo.world_model.encoder.cnn_channels_multiplier=2",
+                  "algo.world_model.recurrent_model.recurrent_state_size=8",
+                  "algo.world_model.representation_model.hidden_size=8",
+                  "algo.world_model.transition_model.hidden_size=8", "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]",
+                  "algo.learning_starts=6", "algo.per_rank_gradient_steps=1"])
+    from tests.test_algos import DV3_KEYS
+
+    _check_ckpt("dv3c", "g", DV3_KEYS, True)

@@ -1,0 +1,114 @@
+"""Third-party env adapters: import gating (simulators are absent in this image) and the
+simulator-independent action / inventory logic (parity with reference ``envs/minedojo.py`` and
+``envs/minerl.py`` semantics; the simulators themselves are "parity unpinned")."""
+import numpy as np
+import pytest
+
+from sheeprl_prey_amd.envs import spaces
+
+
+@pytest.mark.parametrize("mod,cls,kw", [
+    ("dmc", "DMCWrapper", dict(id="walker_walk", from_pixels=True)),
+    ("crafter", "CrafterWrapper", dict(id="reward")),
+    ("diambra", "DiambraWrapper", dict(id="doapp")),
+    ("minedojo", "MineDojoWrapper", dict(id="open-ended")),
+    ("minerl", "MineRLWrapper", dict(id="custom_navigate")),
+])
+def test_missing_simulators_fail_with_hint(mod, cls, kw):
+    import importlib
+
+    m = importlib.import_module(f"sheeprl_prey_amd.envs.{mod}")  # module import never needs the simulator
+    with pytest.raises(ModuleNotFoundError, match="not installed"):
+        getattr(m, cls)(**kw)
+
+
+def test_make_env_dmc_config_raises_helpfully():
+    from sheeprl_prey_amd.config.compose import compose
+    from sheeprl_prey_amd.utils.env import make_env
+
+    from sheeprl_prey_amd.utils.utils import dotdict
+
+    cfg = dotdict(compose(["exp=dreamer_v3", "env=dmc", "env.id=walker_walk"]))
+    with pytest.raises(ModuleNotFoundError):
+        make_env(cfg, 0, 0, None, "train")()
+
+
+def test_minedojo_action_map_and_sticky():
+    from sheeprl_prey_amd.envs.minedojo import ACTION_MAP, F_ATTACK, FUNC, JUMP, MOVE, MinedojoActionMap
+
+    assert ACTION_MAP.shape == (19, 8)
+    am = MinedojoActionMap(sticky_attack=3, sticky_jump=2)
+    v = am([14, 0, 0])  # attack
+    assert v[FUNC] == F_ATTACK
+    assert am([0, 0, 0])[FUNC] == F_ATTACK  # noop -> sticky attack (2 left -> 1)
+    assert am([0, 0, 0])[FUNC] == F_ATTACK
+    assert am([0, 0, 0])[FUNC] == 0  # exhausted
+    am([14, 0, 0])
+    assert am([12, 0, 0])[FUNC] == 1  # "use" interrupts the sticky attack
+    assert am([0, 0, 0])[FUNC] == 0
+    am.reset()
+    v = am([5, 0, 0])  # jump + forward
+    assert v[JUMP] == 1 and v[MOVE] == 1
+    v = am([0, 0, 0])
+    assert v[JUMP] == 1 and v[MOVE] == 1  # sticky jump keeps going forward
+    v = am([3, 0, 0])  # strafing left: sticky jump exhausted (sticky_jump - 1 = 1 repeat)
+    assert v[JUMP] == 0
+    # craft argument only with the craft functional action; slot argument via inventory lookup
+    v = am([15, 7, 0])
+    assert v[6] == 7
+    v = am([16, 7, 2], slot_of_item=lambda i: 10 + i)
+    assert v[6] == 0 and v[7] == 12
+
+
+def test_minedojo_item_table():
+    from sheeprl_prey_amd.envs.minedojo import ItemTable
+
+    t = ItemTable(["air", "dirt", "oak log", "stick"])
+    inv = t.inventory(["dirt", "oak log", "dirt", "air"], [3, 1, 2, 1])
+    np.testing.assert_array_equal(inv, [1, 5, 1, 0])
+    assert t.slot_of(1) == 0 and t.slot_of(2) == 1
+    t.inventory(["dirt"], [1])
+    np.testing.assert_array_equal(t.inventory_max, [1, 5, 1, 0])
+    d = t.delta({"inc_name_by_craft": ["stick"], "inc_quantity_by_craft": [4], "dec_name_by_craft": ["oak log"],
+                 "dec_quantity_by_craft": [1], "inc_name_by_other": [], "inc_quantity_by_other": [],
+                 "dec_name_by_other": ["dirt"], "dec_quantity_by_other": [2]})
+    np.testing.assert_array_equal(d, [0, -2, -1, 4])
+    t.inventory(["dirt", "stick"], [1, 1])
+    m = t.masks({"equip": [True, False], "destroy": [False, False], "action_type": np.ones(8, bool),
+                 "craft_smelt": np.array([1, 0])})
+    assert m["mask_action_type"].shape == (19,) and m["mask_action_type"][:12].all()
+    assert not m["mask_action_type"][-1]  # destroy disabled: nothing destroyable
+    assert m["mask_equip/place"].tolist() == [False, True, False, False]
+
+
+def test_minerl_action_map_and_sticky():
+    from sheeprl_prey_amd.envs.minerl import NOOP, StickyKeys, build_action_map
+
+    keys = [("forward", None), ("jump", None), ("attack", None), ("camera", None),
+            ("place", ["none", "dirt"]), ("craft", ["none", "stick", "planks"])]
+    table = build_action_map(keys)
+    assert table[0] == {}
+    assert table[2] == {"jump": 1, "forward": 1}
+    assert len(table) == 1 + 3 + 4 + 1 + 2
+    s = StickyKeys(sticky_attack=2, sticky_jump=0)
+    a = dict(NOOP, attack=1)
+    assert s(a)["attack"] == 1
+    assert s(dict(NOOP))["attack"] == 1
+    assert s(dict(NOOP))["attack"] == 0
+
+
+def test_external_space_conversion():
+    class Box:  # duck-typed gymnasium spaces
+        def __init__(self):
+            self.low, self.high, self.shape, self.dtype = np.zeros(3), np.ones(3), (3,), np.float32
+
+    class Discrete:
+        n = 5
+
+    class Dict:
+        def __init__(self):
+            self.spaces = {"a": Box(), "b": Discrete()}
+
+    s = spaces.from_external(Dict())
+    assert isinstance(s, spaces.Dict)
+    assert s["a"].shape == (3,) and s["b"].n == 5
