@@ -39,3 +39,9 @@ def find_algorithm(name: str):
             if e["name"] == name:
                 return module_path, e
     return None, None
+
+
+def algorithm_names() -> List[str]:
+    import sheeprl_prey_amd  # noqa: F401  (importing the package registers every algorithm)
+
+    return [e["name"] for entries in tasks.values() for e in entries]

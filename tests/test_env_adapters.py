@@ -112,3 +112,30 @@ def test_external_space_conversion():
     s = spaces.from_external(Dict())
     assert isinstance(s, spaces.Dict)
     assert s["a"].shape == (3,) and s["b"].n == 5
+
+
+def test_observation_space_example(capsys):
+    import importlib.util
+    import pathlib
+
+    p = pathlib.Path(__file__).parents[1] / "examples" / "observation_space.py"
+    spec = importlib.util.spec_from_file_location("obs_space_example", p)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    m.main(["agent=ppo", "env=dummy", "env.id=discrete_dummy"])
+    assert "Observation space" in capsys.readouterr().out
+
+
+def test_architecture_template_runs_five_ranks():
+    import os
+    import pathlib
+    import subprocess
+    import sys
+
+    root = pathlib.Path(__file__).parents[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "5", "--master-addr", "127.0.0.1",
+           "--master-port", "29561", str(root / "examples" / "architecture_template.py")]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "[buffer] stored 48 transitions" in r.stdout
