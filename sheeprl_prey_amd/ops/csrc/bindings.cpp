@@ -5,6 +5,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "scan4.h"
+
 // ---- launchers (defined in the .hip translation units)
 void launch_flat_grad_norm(const float*, int64_t, float*, int, float*, float*, float, hipStream_t);
 void launch_flat_advance(float*, hipStream_t);
@@ -47,6 +49,11 @@ void launch_squashed_gaussian_fwd(const float*, const float*, const float*, cons
                                   int, int, float, float, hipStream_t);
 void launch_squashed_gaussian_bwd(const float*, const float*, const float*, const float*, const float*, const float*, float*,
                                   float*, int, int, int, float, float, hipStream_t);
+
+void launch_scan4_fwd(const srl::scan4::SP&, hipStream_t);
+void launch_scan4_bwd(const srl::scan4::SP&, hipStream_t);
+int scan4_fwd_lds(int, int, int, int);
+int scan4_bwd_lds(int, int, int, int);
 
 namespace {
 
@@ -460,6 +467,72 @@ void unimix_sample_bwd_into(torch::Tensor logits, c10::optional<torch::Tensor> g
   TORCH_CHECK(ok, "unimix_sample_bwd_into: too many classes ", C);
 }
 
+// ------------------------------------------------------------------ 4-launch RSSM scan
+// tensors (fixed order, see ops/rssm.py RSSMScan4Fn): 32 forward buffers, then 20 backward ones;
+// an undefined / empty tensor is a null pointer.
+srl::scan4::SP scan4_params(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints,
+                            const std::vector<double>& fl) {
+  TORCH_CHECK(ints.size() == 9 && fl.size() == 4, "scan4: bad scalar arguments");
+  srl::scan4::SP p{};
+  p.T = ints[0]; p.B = ints[1]; p.S = ints[2]; p.D = ints[3]; p.H = ints[4]; p.hid = ints[5]; p.C = ints[6];
+  p.act1 = ints[7]; p.act2 = ints[8];
+  p.alpha = fl[0]; p.eps1 = fl[1]; p.epsg = fl[2]; p.eps2 = fl[3];
+  TORCH_CHECK(p.B >= 1 && p.B <= 16, "scan4: batch must be <= 16");
+  TORCH_CHECK(p.H <= 512, "scan4: recurrent size must be <= 512");
+  TORCH_CHECK(p.S % 32 == 0 && p.D % 16 == 0 && p.H % 16 == 0 && p.hid % 16 == 0, "scan4: dims must be multiples of 16/32");
+  TORCH_CHECK(p.C >= 1 && p.C <= 32 && (32 % p.C) == 0, "scan4: classes must divide 32");
+  auto P = [&](size_t i) -> float* {
+    if (i >= ts.size() || !ts[i].defined() || ts[i].numel() == 0) return nullptr;
+    TORCH_CHECK(ts[i].is_cuda() && ts[i].scalar_type() == torch::kFloat32 && ts[i].is_contiguous(),
+                "scan4: tensor ", i, " must be a contiguous float32 GPU tensor");
+    return ts[i].data_ptr<float>();
+  };
+  size_t k = 0;
+  p.a_proj = P(k++); p.P = P(k++); p.first = P(k++); p.uni = P(k++); p.z0 = P(k++); p.Wz = P(k++); p.ln1w = P(k++);
+  p.ln1b = P(k++); p.Wg = P(k++); p.lngw = P(k++); p.lngb = P(k++); p.W1 = P(k++); p.ln2w = P(k++); p.ln2b = P(k++);
+  p.W2 = P(k++); p.b2 = P(k++);
+  p.cat = P(k++); p.zm = P(k++); p.xr = P(k++); p.m1 = P(k++); p.r1 = P(k++); p.gx = P(k++); p.mg = P(k++); p.rg = P(k++);
+  p.hs = P(k++); p.u = P(k++); p.v = P(k++); p.m2 = P(k++); p.r2 = P(k++); p.logits = P(k++); p.mixed = P(k++);
+  p.samples = P(k++);
+  p.WzT = P(k++); p.WgT = P(k++); p.W1T = P(k++); p.W2T = P(k++); p.dpost = P(k++); p.dmixed = P(k++);
+  p.DH = P(k++); p.dlog = P(k++); p.dv = P(k++); p.du = P(k++); p.dgx = P(k++); p.dx = P(k++); p.dcat = P(k++);
+  p.dhp = P(k++); p.p1g = P(k++); p.p1b = P(k++); p.pgg = P(k++); p.pgb = P(k++); p.p2g = P(k++); p.p2b = P(k++);
+  p.prof = nullptr;
+  return p;
+}
+
+long long* g_scan4_prof = nullptr;  // debug phase timestamps (set_scan4_prof)
+
+void set_scan4_prof(c10::optional<torch::Tensor> buf) {
+  if (buf.has_value() && buf->defined()) {
+    TORCH_CHECK(buf->scalar_type() == torch::kInt64 && buf->numel() >= 128 && buf->is_cuda(), "prof buffer: int64[128] on GPU");
+    g_scan4_prof = (long long*)buf->data_ptr<int64_t>();
+  } else {
+    g_scan4_prof = nullptr;
+  }
+}
+
+void scan4_fwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints, const std::vector<double>& fl) {
+  TORCH_CHECK(ts.size() == 32, "scan4_fwd: expects 32 tensors");
+  auto p = scan4_params(ts, ints, fl);
+  p.prof = g_scan4_prof;
+  TORCH_CHECK(p.uni && p.z0 && p.logits && p.samples, "scan4_fwd: missing tensors");
+  launch_scan4_fwd(p, cur_stream());
+}
+
+void scan4_bwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints, const std::vector<double>& fl) {
+  TORCH_CHECK(ts.size() == 52, "scan4_bwd: expects 52 tensors");
+  auto p = scan4_params(ts, ints, fl);
+  p.prof = g_scan4_prof;
+  TORCH_CHECK(p.dmixed && p.DH && p.dlog && p.WzT, "scan4_bwd: missing tensors");
+  launch_scan4_bwd(p, cur_stream());
+}
+
+int64_t scan4_lds(int64_t S, int64_t D, int64_t H, int64_t hid) {
+  int a = scan4_fwd_lds(S, D, H, hid), b = scan4_bwd_lds(S, D, H, hid);
+  return a > b ? a : b;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -497,4 +570,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rssm_mask_bwd", &rssm_mask_bwd);
   m.def("unimix_sample_fwd_into", &unimix_sample_fwd_into);
   m.def("unimix_sample_bwd_into", &unimix_sample_bwd_into);
+  m.def("scan4_fwd", &scan4_fwd);
+  m.def("scan4_bwd", &scan4_bwd);
+  m.def("scan4_lds", &scan4_lds);
+  m.def("set_scan4_prof", &set_scan4_prof);
 }

@@ -19,6 +19,7 @@ autograd handles their (large, efficient) GEMM backward.
 """
 from __future__ import annotations
 
+import os
 from typing import Tuple
 
 import torch
@@ -152,6 +153,87 @@ class RSSMScanFn(torch.autograd.Function):
         return (dx, du, None, None, None, dWz, dln1_w, dln1_b, dWg, dlng_w, dlng_b, dW1, dln2_w, dln2_b, dW2, db2, None)
 
 
+class RSSMScan4Fn(torch.autograd.Function):
+    """Same contract as :class:`RSSMScanFn`, 4 + 4 launches per step (``csrc/rssm_scan.hip``):
+    every launch is a 16-row MFMA GEMM whose prologue rebuilds its A operand from the previous
+    launch's raw output (LN, LN-GRU, masking, their adjoints) and whose epilogue holds the bias /
+    unimix sample / unimix adjoint.  Requires batch <= 16, classes dividing 32 (see
+    :func:`scan4_supported`).  Buffers are group-major ([2, T, B, S]) so the prior half of the
+    categorical adjoint is one launch for all steps."""
+
+    @staticmethod
+    def forward(ctx, a_proj, P, is_first, uniform, z0, Wz, ln1_w, ln1_b, Wg, lng_w, lng_b, W1, ln2_w, ln2_b, W2, b2, meta):
+        from sheeprl_prey_amd.ops import _ext
+
+        C = _ext()
+        T, B, D = a_proj.shape
+        S = Wz.shape[1]
+        H = lng_w.shape[0] // 3
+        hid = W1.shape[0] // 2
+        disc, alpha, eps1, epsg, eps2, act1, act2 = meta
+        dev, f32 = a_proj.device, torch.float32
+        e = lambda *shape: torch.empty(*shape, device=dev, dtype=f32)  # noqa: E731
+        first = is_first.reshape(T, B).contiguous()
+        Wz_c = Wz.contiguous()
+        fwd = [a_proj, P, first, uniform.contiguous(), z0, Wz_c, ln1_w.contiguous(), ln1_b.contiguous(), Wg.contiguous(),
+               lng_w.contiguous(), lng_b.contiguous(), W1.contiguous(), ln2_w.contiguous(), ln2_b.contiguous(),
+               W2.contiguous(), b2.reshape(2, S).contiguous(),
+               e(T, B, H + D), e(T, B, S), e(T, B, D), e(T, B), e(T, B), e(T, B, 3 * H), e(T, B), e(T, B), e(T, B, H),
+               e(T, B, 2 * hid), e(2, T, B, hid), e(T, 2 * B), e(T, 2 * B), e(2, T, B, S), e(2, T, B, S), e(2, T, B, S)]
+        dims = [T, B, S, D, H, hid, disc, act1, act2]
+        fl = [alpha, eps1, epsg, eps2]
+        C.scan4_fwd(fwd, dims, fl)
+        ctx.save_for_backward(*fwd[:32])
+        ctx.dims, ctx.fl = dims, fl
+        hs, mixed, samples = fwd[24], fwd[30], fwd[31]
+        return hs, samples[1], mixed[1], mixed[0]
+
+    @staticmethod
+    def backward(ctx, d_hs, d_post, d_post_mixed, d_prior_mixed):
+        from sheeprl_prey_amd.ops import _ext
+
+        C = _ext()
+        fwd = list(ctx.saved_tensors)
+        T, B, S, D, H, hid = ctx.dims[:6]
+        dev, f32 = fwd[0].device, torch.float32
+        e = lambda *shape: torch.empty(*shape, device=dev, dtype=f32)  # noqa: E731
+        Wz, Wg, W1, W2 = fwd[5], fwd[8], fwd[11], fwd[14]
+        dmixed = torch.zeros(2, T, B, S, device=dev, dtype=f32)
+        if d_prior_mixed is not None:
+            dmixed[0].copy_(d_prior_mixed)
+        if d_post_mixed is not None:
+            dmixed[1].copy_(d_post_mixed)
+        DH = d_hs.contiguous().clone() if d_hs is not None else torch.zeros(T, B, H, device=dev, dtype=f32)
+        dpost = d_post.contiguous() if d_post is not None else torch.empty(0, device=dev, dtype=f32)
+        dlog, dv, du, dgx, dx = e(2, T, B, S), e(2, T, B, hid), e(T, B, 2 * hid), e(T, B, 3 * H), e(T, B, D)
+        p1g, p1b, pgg, pgb, p2g, p2b = e(T, D), e(T, D), e(T, 3 * H), e(T, 3 * H), e(T, 2 * hid), e(T, 2 * hid)
+        bwd = [Wz.t().contiguous(), Wg.t().contiguous(), W1.t().contiguous(), W2.transpose(1, 2).contiguous(), dpost,
+               dmixed, DH, dlog, dv, du, dgx, dx, e(B, H + D), e(B, H), p1g, p1b, pgg, pgb, p2g, p2b]
+        C.scan4_bwd(fwd + bwd, ctx.dims, ctx.fl)
+        cat, zm, hs, v = fwd[16], fwd[17], fwd[24], fwd[26]
+        TB = T * B
+        dWz = dx.reshape(TB, D).t().mm(zm.reshape(TB, S))
+        dWg = dgx.reshape(TB, 3 * H).t().mm(cat.reshape(TB, H + D))
+        dW1 = du.reshape(TB, 2 * hid).t().mm(hs.reshape(TB, H))
+        dlog_g = dlog.reshape(2, TB, S)
+        dW2 = torch.bmm(dlog_g.transpose(1, 2), v.reshape(2, TB, hid))
+        db2 = dlog_g.sum(1, keepdim=True)
+        return (dx, du, None, None, None, dWz, p1g.sum(0), p1b.sum(0), dWg, pgg.sum(0), pgb.sum(0), dW1,
+                p2g.sum(0).view(2, hid), p2b.sum(0).view(2, hid), dW2, db2, None)
+
+
+def scan4_supported(B: int, S: int, D: int, H: int, hid: int, classes: int) -> bool:
+    """Shape gate of the 4-launch scan: 16-row tiles, 16/32-column tiles, whole categorical groups
+    per 32-column tile, every A operand fits the 160 KiB LDS of one workgroup."""
+    if not (1 <= B <= 16 and S % 32 == 0 and D % 16 == 0 and H % 16 == 0 and hid % 16 == 0 and H <= 512):
+        return False
+    if not (1 <= classes <= 32 and 32 % classes == 0):
+        return False
+    from sheeprl_prey_amd.ops import _ext
+
+    return int(_ext().scan4_lds(S, D, H, hid)) <= 160 * 1024
+
+
 def fused_scan_supported(rssm) -> bool:
     """The fused scan covers the DreamerV3 RSSM layout: LN+act MLPs, LN-GRU, equal prior/posterior widths."""
     import torch.nn as nn
@@ -203,6 +285,10 @@ def fused_scan(rssm, embedded_obs: Tensor, actions: Tensor, is_first: Tensor, z0
         uniform = torch.rand(T, 2 * B * (S // rssm.discrete), device=embedded_obs.device)
     meta = (rssm.discrete, float(rssm.unimix), float(rec[1].eps), float(gru.layer_norm.eps), float(tr[1].eps),
             ACTS[rec[1].act], ACTS[tr[1].act])
-    return RSSMScanFn.apply(a_proj.contiguous(), P.contiguous(), is_first.contiguous(), uniform, z0.reshape(-1).contiguous(),
+    fn = RSSMScanFn
+    if getattr(rssm, "scan_impl", os.environ.get("SRL_SCAN_IMPL", "scan4")) == "scan4" and scan4_supported(B, S, rec_lin.out_features, H, hid,
+                                                                         rssm.discrete):
+        fn = RSSMScan4Fn
+    return fn.apply(a_proj.contiguous(), P.contiguous(), is_first.contiguous(), uniform, z0.reshape(-1).contiguous(),
                             Wz, rec[1].weight, rec[1].bias, gru.linear.weight, gru.layer_norm.weight, gru.layer_norm.bias,
                             W1, ln2_w, ln2_b, W2, b2, meta)

@@ -68,9 +68,11 @@ def test_dv3_graph_matches_eager_losses():
     assert abs(la - lb) / abs(la) < 1e-4
 
 
+@pytest.mark.parametrize("impl", ["scan4", "scan9"])
 @pytest.mark.parametrize("H,D,hid,B,T", [(64, 64, 64, 4, 16), (512, 512, 512, 16, 8), (96, 80, 48, 3, 5)])
-def test_fused_rssm_scan_matches_python_scan(H, D, hid, B, T):
-    """The fused scan (9+9 launches/step, batched weight grads) vs the python step loop, same noise."""
+def test_fused_rssm_scan_matches_python_scan(H, D, hid, B, T, impl):
+    """The fused scans (scan4: 4+4 MFMA launches/step; scan9: 9+9 launches/step; batched weight
+    grads) vs the python step loop, same noise."""
     import copy
 
     from sheeprl_prey_amd.algos.dreamer_v3.agent import RSSM, RecurrentModel, init_weights
@@ -87,6 +89,7 @@ def test_fused_rssm_scan_matches_python_scan(H, D, hid, B, T):
             p.data.add_(0.1 * torch.randn_like(p))
     rssm_ref = copy.deepcopy(rssm)
     rssm_ref.fused_scan = False
+    rssm.scan_impl = impl
     emb = torch.randn(T, B, E, device="cuda")
     act = torch.nn.functional.one_hot(torch.randint(0, A, (T, B), device="cuda"), A).float()
     first = (torch.rand(T, B, 1, device="cuda") < 0.2).float()
@@ -97,6 +100,8 @@ def test_fused_rssm_scan_matches_python_scan(H, D, hid, B, T):
     e1, e2 = emb.clone().requires_grad_(), emb.clone().requires_grad_()
     out1 = rssm.scan_dynamic(e1, act, first, uniform=uni)
     out2 = rssm_ref.scan_dynamic(e2, act, first, uniform=uni_post)
+    if impl == "scan4":
+        assert type(out1[0].grad_fn).__name__ == "RSSMScan4FnBackward"
     names = ["h", "post", "post_logits", "prior_logits"]
     for n, a, b in zip(names, out1, out2):
         torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-4, msg=lambda m: f"{n}: {m}")
