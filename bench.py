@@ -35,6 +35,8 @@ def parse():
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--eager-ops", action="store_true", help="route GPU ops through the eager reference (A/B only)")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--phase-times", action="store_true",
+                   help="per-phase hipGraphs with event timing (diagnostic; adds syncs, not a bench number)")
     p.add_argument("overrides", nargs="*")
     return p.parse_args()
 
@@ -93,7 +95,7 @@ def main():
     moments = Moments(runner, cfg.algo.actor.moments.decay, cfg.algo.actor.moments.max,
                       cfg.algo.actor.moments.percentile.low, cfg.algo.actor.moments.percentile.high).to(device)
     trainer = DreamerV3Trainer(runner, cfg, world_model, actor, critic, target_critic, wopt, aopt, copt, moments,
-                               is_continuous, actions_dim)
+                               is_continuous, actions_dim, force_segmented=args.phase_times)
     n_params = sum(p.numel() for m in (world_model, actor, critic) for p in m.parameters())
     rb = AsyncReplayBuffer(cfg.buffer.size // (cfg.env.num_envs * world), cfg.env.num_envs, device=device, sequential=True)
     obs_keys = list(cfg.cnn_keys.encoder)
@@ -149,8 +151,17 @@ def main():
     for _ in range(max(args.prefill, cfg.per_rank_sequence_length + 1)):
         env_step(True)
 
+    env_ms = [0.0]
+
     def one_step():
-        env_step(False)
+        if args.phase_times:
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            env_step(False)
+            torch.cuda.synchronize()
+            env_ms[0] += (time.perf_counter() - t) * 1e3
+        else:
+            env_step(False)
         return train_once()
 
     for _ in range(args.warmup):
@@ -159,6 +170,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if args.phase_times:
+        trainer.seg.enable_timing()
     if args.profile_steps:
         torch.cuda._sleep(1000)  # marker kernel: scripts/trace_window.py aggregates the dispatches after it
         torch.cuda.synchronize()
@@ -170,6 +183,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if args.phase_times and rank == 0:
+        seg = trainer.seg
+        if seg.phase_ms is not None and seg.timed_steps:
+            names = DreamerV3Trainer.PHASES
+            print(f"player+env ms/step: {env_ms[0] / (args.steps + args.warmup):.3f}; phase ms/step: "
+                  + ", ".join(f"{n} {v / seg.timed_steps:.3f}" for n, v in zip(names, seg.phase_ms)),
+                  file=sys.stderr, flush=True)
     loss = float(out["Loss/world_model_loss"].item())
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:

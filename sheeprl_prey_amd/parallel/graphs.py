@@ -79,6 +79,31 @@ class SegmentedGraph:
         self.static_in: Optional[Dict[str, Tensor]] = None
         self.static_out = None
         self._calls = 0
+        # opt-in per-phase timing (``enable_timing()``): hipEvents around every phase replay
+        self.phase_ms = None
+        self._events = None
+
+    def enable_timing(self) -> None:
+        self.phase_ms = [0.0] * len(self.phases)
+        self.timed_steps = 0
+
+    def _replay_all(self) -> None:
+        timing = self.phase_ms is not None
+        if timing and self._events is None:
+            self._events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * len(self.graphs))]
+        for i, g in enumerate(self.graphs):
+            if timing:
+                self._events[2 * i].record()
+            g.replay()
+            if timing:
+                self._events[2 * i + 1].record()
+            if i < len(self.colls):
+                self.colls[i]()
+        if timing:
+            torch.cuda.synchronize()
+            for i in range(len(self.graphs)):
+                self.phase_ms[i] += self._events[2 * i].elapsed_time(self._events[2 * i + 1])
+            self.timed_steps += 1
 
     def _run_eager(self, data):
         out = None
@@ -94,10 +119,7 @@ class SegmentedGraph:
         for k, v in data.items():
             self.static_in[k].copy_(v, non_blocking=True)
         if self.graphs is not None:
-            for i, g in enumerate(self.graphs):
-                g.replay()
-                if i < len(self.colls):
-                    self.colls[i]()
+            self._replay_all()
             return self.static_out
         if self._calls < self.warmup:
             self._calls += 1
