@@ -12,6 +12,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from sheeprl_prey_amd.algos.dreamer_v3.agent import CNNDecoder, CNNEncoder
+from sheeprl_prey_amd.ops import conv as conv_ops
 
 
 def run(layout: str, N: int, iters: int = 20):
@@ -19,6 +20,7 @@ def run(layout: str, N: int, iters: int = 20):
     enc = CNNEncoder(["rgb"], [3], (64, 64), 32).cuda()
     dec = CNNDecoder(["rgb"], [3], 32, 1536, enc.output_dim, (64, 64)).cuda()
     cl = layout == "nhwc"
+    conv_ops.ENABLED = layout == "fused"
     if cl:
         enc = enc.to(memory_format=torch.channels_last)
         dec = dec.to(memory_format=torch.channels_last)
@@ -63,5 +65,9 @@ def run(layout: str, N: int, iters: int = 20):
 
 if __name__ == "__main__":
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-    for layout in ("nchw", "nhwc", "nchw", "nhwc"):
+    bm = os.environ.get("CONV_BENCHMARK", "0") == "1"
+    torch.backends.cudnn.benchmark = bm
+    print("cudnn.benchmark =", bm)
+    layouts = os.environ.get("CONV_LAYOUTS", "nchw,fused,nchw,fused").split(",")
+    for layout in layouts:
         run(layout, N)

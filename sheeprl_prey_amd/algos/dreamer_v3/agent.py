@@ -24,6 +24,7 @@ from torch import Tensor, nn
 from torch.distributions import Distribution, Independent, Normal, TanhTransform, TransformedDistribution
 
 from sheeprl_prey_amd import ops
+from sheeprl_prey_amd.ops import conv as conv_ops
 from sheeprl_prey_amd.config.instantiate import get_class
 from sheeprl_prey_amd.models.models import CNN, MLP, DeCNN, LayerNormGRUCell, MultiDecoder, MultiEncoder
 from sheeprl_prey_amd.models.world_model import WorldModel
@@ -109,6 +110,13 @@ class CNNEncoder(nn.Module):
 
     def forward(self, obs: Dict[str, Tensor]) -> Tensor:
         x = torch.cat([obs[k] for k in self.keys], -3)
+        if x.is_cuda and x.dtype == torch.float32 and ops.fused_enabled() and conv_ops.ENABLED:
+            if not hasattr(self, "_fused_spec"):
+                self._fused_spec = conv_ops.encoder_spec(self.model, tuple(self.input_dim[1:]), self.input_dim[0])
+            if self._fused_spec is not None:
+                # whole stack as one implicit-GEMM autograd op (ops/conv.py): NHWC, LN+SiLU fused
+                flat = x.reshape(-1, *x.shape[-3:])
+                return conv_ops.encoder_forward(self._fused_spec, flat).reshape(*x.shape[:-3], -1)
         return cnn_forward(self.model, x, x.shape[-3:], (-1,))
 
 
@@ -160,7 +168,17 @@ class CNNDecoder(nn.Module):
         )
 
     def forward(self, latent_states: Tensor) -> Dict[str, Tensor]:
-        out = cnn_forward(self.model, latent_states, (latent_states.shape[-1],), self.output_dim) + 0.5
+        out = None
+        if latent_states.is_cuda and latent_states.dtype == torch.float32 and ops.fused_enabled() and conv_ops.ENABLED:
+            if not hasattr(self, "_fused_spec"):
+                self._fused_spec = conv_ops.decoder_spec(self.model, self.output_dim[0])
+            if self._fused_spec is not None:
+                lin, stages = self._fused_spec
+                x = latent_states.reshape(-1, latent_states.shape[-1])
+                out = conv_ops.decoder_forward(stages, lin(x), 0.5)
+                out = out.reshape(*latent_states.shape[:-1], *self.output_dim)
+        if out is None:
+            out = cnn_forward(self.model, latent_states, (latent_states.shape[-1],), self.output_dim) + 0.5
         return {k: o for k, o in zip(self.keys, torch.split(out, self.output_channels, -3))}
 
 

@@ -535,7 +535,10 @@ int64_t scan4_lds(int64_t S, int64_t D, int64_t H, int64_t hid) {
 
 }  // namespace
 
+void register_conv(pybind11::module& m);
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  register_conv(m);
   m.doc() = "sheeprl_prey_amd HIP kernels (gfx950)";
   m.def("flat_grad_norm", &flat_grad_norm);
   m.def("flat_advance", &flat_advance);

@@ -1,0 +1,950 @@
+// Implicit-GEMM k4 s2 p1 convolutions for the Dreamer CNN encoder / decoder on CDNA4 MFMA
+// (reference: dreamer_v3/agent.py:48-80 CNNEncoder, :160-206 CNNDecoder; LN channel-last
+// utils/model.py:225-235).  fp32 in, fp32 accumulate: v_mfma_f32_32x32x2_f32 (exact fp32 products,
+// 64 FLOP/clk/SIMD = the chip's fp32 peak).
+//
+// Activations are NHWC ("channels last"): the channel dim is the GEMM K (or N) dim, contiguous.
+// A k4 s2 p1 conv links a LARGE spatial grid (2SH x 2SW) to a SMALL one (SH x SW).  Three GEMM forms
+// cover every pass of both Conv2d and ConvTranspose2d:
+//
+//   DOWN  out[m=(n,p,q)][a]   = sum_{tap,b} Q[n, 2p-1+kh, 2q-1+kw, b] * W[a][b][kh][kw]
+//         (Conv2d forward: Q=x, W=conv weight [co][ci];  ConvT data-grad: Q=dy, W=convT weight [ci][co])
+//   UP    out[(n,y,x)][b]     = sum_{2x2 taps of y,x parity, a} P[n, p, q, a] * W[a][b][kh][kw]
+//         (ConvT forward: P=x, W=[ci][co];  Conv2d data-grad: P=dy, W=[co][ci]); one parity class per
+//         blockIdx.z, so each class is a dense GEMM with K = 4*Ca
+//   WGRAD dW[a][tap][b]       = sum_{m=(n,p,q)} P[m][a] * Q[n, 2p-1+kh, 2q-1+kw, b]
+//         split-K over pixels into partial slabs, reduced (and permuted to [a][b][kh][kw]) by a 2nd kernel
+//
+// Epilogues fuse the channel LayerNorm: the workgroup tile spans the whole channel row (N <= 256), so
+//   LN_ACT : z = acc; y = act(LN(z)) (+ per-pixel mean/rstd)        (forward of conv -> LN -> act)
+//   LN_BWD : acc = dy of the NEXT-lower layer's output; dz = LN/act backward, dgamma/dbeta atomics
+//   PLAIN  : out = acc + bias + c0, NHWC or NCHW (for the 3-channel image / the flat Linear seam)
+// All spatial sizes and channel counts on this path are powers of two (host-checked).
+#include "common.h"
+#include "conv.h"
+
+namespace srl {
+namespace conv {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 32;        // K per LDS stage
+constexpr int LDK = BK + 4;   // LDS row stride (floats): conflict-free float4 fragment reads
+
+__device__ __forceinline__ f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
+__device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float cact(float z, int act) {
+  switch (act) {
+    case ACT_SILU: return z * fsig(z);
+    case ACT_ELU: return z > 0.f ? z : __expf(z) - 1.f;
+    case ACT_RELU: return z > 0.f ? z : 0.f;
+    case ACT_TANH: return 2.f * fsig(2.f * z) - 1.f;
+    default: return z;
+  }
+}
+__device__ __forceinline__ float cact_grad(float z, int act) {
+  switch (act) {
+    case ACT_SILU: {
+      const float s = fsig(z);
+      return s * (1.f + z * (1.f - s));
+    }
+    case ACT_ELU: return z > 0.f ? 1.f : __expf(z);
+    case ACT_RELU: return z > 0.f ? 1.f : 0.f;
+    case ACT_TANH: {
+      const float t = 2.f * fsig(2.f * z) - 1.f;
+      return 1.f - t * t;
+    }
+    default: return 1.f;
+  }
+}
+
+// ------------------------------------------------------------------------------------- loaders
+// A loader fills a ROWS x BK tile (row-major, k contiguous, stride LDK) of LDS from one K stage.
+// Each thread owns NV float4 slots; load() issues the global reads into registers (so the next
+// stage's latency hides behind the current stage's MFMAs), store() writes them to LDS.
+
+// DOWN gather: rows = small-grid pixels m=(n,p,q), k = tap*Cb + b; Q is NHWC on the large grid.
+template <int ROWS, int NTH>
+struct DownGather {
+  static constexpr int NV = ROWS * BK / 4 / NTH;
+  const float* Q;
+  int lCb, lSH, lSW, M;
+  int pix[NV], py[NV], px[NV];  // per slot: n*LH*LW, 2p-1, 2q-1 (pix = -1: row out of range)
+  __device__ void init(int m0) {
+    const int LH = 2 << lSH, LW = 2 << lSW;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = threadIdx.x + NTH * v, m = m0 + (idx >> 3);
+      const int n = m >> (lSH + lSW), p = (m >> lSW) & ((1 << lSH) - 1), q = m & ((1 << lSW) - 1);
+      pix[v] = m < M ? n * LH * LW : -1;
+      py[v] = 2 * p - 1;
+      px[v] = 2 * q - 1;
+    }
+  }
+  __device__ void load(int k0, f4* r) const {
+    const int LH = 2 << lSH, LW = 2 << lSW, Cb = 1 << lCb;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int k = k0 + 4 * ((threadIdx.x + NTH * v) & 7);
+      const int tap = k >> lCb, b = k & (Cb - 1);
+      const int iy = py[v] + (tap >> 2), ix = px[v] + (tap & 3);
+      f4 val = zero4();
+      if (pix[v] >= 0 && iy >= 0 && iy < LH && ix >= 0 && ix < LW)
+        val = *(const f4*)(Q + ((size_t)(pix[v] + iy * LW + ix) << lCb) + b);
+      r[v] = val;
+    }
+  }
+  __device__ void store(const f4* r, float* s) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = threadIdx.x + NTH * v;
+      *(f4*)(s + (idx >> 3) * LDK + 4 * (idx & 7)) = r[v];
+    }
+  }
+};
+
+// UP gather: rows = large-grid pixels of parity class (cy,cx) (blockIdx.z), m=(n,u,v) -> (2u+cy, 2v+cx);
+// k = t*Ca + a with t = (th,tw) in 2x2; source pixel (u+cy-th, v+cx-tw) of P (NHWC, small grid).
+template <int ROWS, int NTH>
+struct UpGather {
+  static constexpr int NV = ROWS * BK / 4 / NTH;
+  const float* P;
+  int lCa, lSH, lSW, M;
+  int pix[NV], pu[NV], pv[NV];
+  __device__ void init(int m0) {
+    const int cy = blockIdx.z >> 1, cx = blockIdx.z & 1;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = threadIdx.x + NTH * v, m = m0 + (idx >> 3);
+      const int n = m >> (lSH + lSW), u = (m >> lSW) & ((1 << lSH) - 1), w = m & ((1 << lSW) - 1);
+      pix[v] = m < M ? n << (lSH + lSW) : -1;
+      pu[v] = u + cy;
+      pv[v] = w + cx;
+    }
+  }
+  __device__ void load(int k0, f4* r) const {
+    const int SH = 1 << lSH, SW = 1 << lSW, Ca = 1 << lCa;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int k = k0 + 4 * ((threadIdx.x + NTH * v) & 7);
+      const int t = k >> lCa, a = k & (Ca - 1);
+      const int p = pu[v] - (t >> 1), q = pv[v] - (t & 1);
+      f4 val = zero4();
+      if (pix[v] >= 0 && p >= 0 && p < SH && q >= 0 && q < SW)
+        val = *(const f4*)(P + ((size_t)(pix[v] + p * SW + q) << lCa) + a);
+      r[v] = val;
+    }
+  }
+  __device__ void store(const f4* r, float* s) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = threadIdx.x + NTH * v;
+      *(f4*)(s + (idx >> 3) * LDK + 4 * (idx & 7)) = r[v];
+    }
+  }
+};
+
+// Packed weights, rows = output columns, k contiguous: W + (n0 + row) * K + k (+ class offset).
+template <int ROWS, int NTH>
+struct Dense {
+  static constexpr int NV = ROWS * BK / 4 / NTH;
+  const float* W;
+  int K;
+  size_t cls_stride;  // UP: per parity-class packed block (blockIdx.z); 0 otherwise
+  const float* base;
+  __device__ void init(int n0) { base = W + cls_stride * blockIdx.z + (size_t)n0 * K; }
+  __device__ void load(int k0, f4* r) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = threadIdx.x + NTH * v;
+      r[v] = *(const f4*)(base + (size_t)(idx >> 3) * K + k0 + 4 * (idx & 7));
+    }
+  }
+  __device__ void store(const f4* r, float* s) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = threadIdx.x + NTH * v;
+      *(f4*)(s + (idx >> 3) * LDK + 4 * (idx & 7)) = r[v];
+    }
+  }
+};
+
+// WGRAD operand A: rows = channels a of P (NHWC, small grid), k = pixels: float4 along a, transposed
+// into LDS (4 scalar writes; consecutive lanes = consecutive pixels: conflict-free).
+template <int ROWS, int NTH>
+struct WgP {
+  static constexpr int NV = ROWS * BK / 4 / NTH;
+  const float* P;
+  int lCa, M, a0;
+  __device__ void init(int r0) { a0 = r0; }
+  __device__ void load(int k0, f4* r) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = threadIdx.x + NTH * v;
+      const int m = k0 + (idx & 31), a = a0 + 4 * (idx >> 5);
+      r[v] = m < M ? *(const f4*)(P + ((size_t)m << lCa) + a) : zero4();
+    }
+  }
+  __device__ void store(const f4* r, float* s) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = threadIdx.x + NTH * v;
+      float* d = s + 4 * (idx >> 5) * LDK + (idx & 31);
+      d[0] = r[v][0];
+      d[LDK] = r[v][1];
+      d[2 * LDK] = r[v][2];
+      d[3 * LDK] = r[v][3];
+    }
+  }
+};
+
+// WGRAD operand B: rows j = tap*Cb + b, k = small-grid pixels m=(n,p,q); value Q[n, 2p-1+kh, 2q-1+kw, b].
+template <int ROWS, int NTH>
+struct WgQ {
+  static constexpr int NV = ROWS * BK / 4 / NTH;
+  const float* Q;
+  int lCb, lSH, lSW, M, j0;
+  __device__ void init(int r0) { j0 = r0; }
+  __device__ void load(int k0, f4* r) const {
+    const int LH = 2 << lSH, LW = 2 << lSW, Cb = 1 << lCb;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = threadIdx.x + NTH * v;
+      const int m = k0 + (idx & 31), j = j0 + 4 * (idx >> 5);
+      const int tap = j >> lCb, b = j & (Cb - 1);
+      const int n = m >> (lSH + lSW), p = (m >> lSW) & ((1 << lSH) - 1), q = m & ((1 << lSW) - 1);
+      const int iy = 2 * p - 1 + (tap >> 2), ix = 2 * q - 1 + (tap & 3);
+      f4 val = zero4();
+      if (m < M && iy >= 0 && iy < LH && ix >= 0 && ix < LW)
+        val = *(const f4*)(Q + ((size_t)((n * LH + iy) * LW + ix) << lCb) + b);
+      r[v] = val;
+    }
+  }
+  __device__ void store(const f4* r, float* s) const {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int idx = threadIdx.x + NTH * v;
+      float* d = s + 4 * (idx >> 5) * LDK + (idx & 31);
+      d[0] = r[v][0];
+      d[LDK] = r[v][1];
+      d[2 * LDK] = r[v][2];
+      d[3 * LDK] = r[v][3];
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------ row geometry
+// Maps a GEMM output row (pixel of the kernel's M space) to its pixel index in the output grid.
+struct RowDown {  // rows are the output pixels themselves
+  __device__ int operator()(int m) const { return m; }
+};
+struct RowUp {  // rows are parity-class pixels of the large grid
+  int lSH, lSW;
+  __device__ int operator()(int m) const {
+    const int n = m >> (lSH + lSW), u = (m >> lSW) & ((1 << lSH) - 1), v = m & ((1 << lSW) - 1);
+    const int cy = blockIdx.z >> 1, cx = blockIdx.z & 1;
+    return ((n << (lSH + 1)) + 2 * u + cy) * (2 << lSW) + 2 * v + cx;
+  }
+};
+
+// acc element (i, j, r) of a wave -> tile row / col (v_mfma_f32_32x32x2_f32 C/D layout)
+template <int TM, int TN, int WN>
+struct Frag {
+  int wm, wn, lane;
+  __device__ int row(int i, int r) const { return wm * TM * 32 + i * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3); }
+  __device__ int col(int j) const { return wn * TN * 32 + j * 32 + (lane & 31); }
+};
+
+// The LayerNorm epilogues work on whole channel rows: the accumulator tile is staged through LDS
+// in TM chunks of WM*32 rows ([row][BN + 4] floats, fits the main-loop LDS), then every row is
+// processed by LPR lanes (CPL contiguous channels each: vector loads/stores, row reductions by xor
+// shuffles inside the LPR-lane segment).  This keeps the epilogue's register footprint small, so
+// the MFMA main loop keeps its occupancy.
+template <int BN>
+struct RowGeo {
+  static constexpr int LPR = BN < 64 ? BN : 64;  // lanes per row
+  static constexpr int RPW = 64 / LPR;           // rows per wave pass
+  static constexpr int CPL = BN / LPR;           // channels per lane
+  static constexpr int PITCH = BN + 4;           // LDS row pitch (floats)
+};
+
+template <int TM, int TN, int WN>
+__device__ __forceinline__ void stage_chunk(const f16v (&acc)[TM][TN], int i, const Frag<TM, TN, WN>& f, float* s,
+                                            int pitch) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      s[(f.wm * 32 + 8 * (r >> 2) + 4 * (f.lane >> 5) + (r & 3)) * pitch + f.col(j)] = acc[i][j][r];
+}
+
+template <int LPR>
+__device__ __forceinline__ float lseg_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < LPR; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int CPL>
+__device__ __forceinline__ void ld_cpl(const float* p, float (&v)[CPL]) {
+  if constexpr (CPL == 4) {
+    const f4 t = *(const f4*)p;
+    v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+  } else if constexpr (CPL == 2) {
+    const float2 t = *(const float2*)p;
+    v[0] = t.x; v[1] = t.y;
+  } else {
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) v[e] = p[e];
+  }
+}
+template <int CPL>
+__device__ __forceinline__ void st_cpl(float* p, const float (&v)[CPL]) {
+  if constexpr (CPL == 4) {
+    *(f4*)p = f4{v[0], v[1], v[2], v[3]};
+  } else if constexpr (CPL == 2) {
+    *(float2*)p = make_float2(v[0], v[1]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) p[e] = v[e];
+  }
+}
+
+// ------------------------------------------------------------------------------------ epilogues
+struct EpiLNAct : EpiLNActP {  // z = acc (NHWC), y = act(LN_c(z)) (NHWC or NCHW-flat), mean/rstd per pixel
+  template <int BM, int BN, int TM, int TN, int WN, class RM>
+  __device__ void run(f16v (&acc)[TM][TN], const Frag<TM, TN, WN>& f, int m0, float* lds, const RM& rm) {
+    using G = RowGeo<BN>;
+    constexpr int WM = 4 / WN, R = WM * 32, CPL = G::CPL, LPR = G::LPR;
+    const int w = threadIdx.x >> 6, lr = f.lane / LPR, lc = f.lane % LPR, c0 = lc * CPL;
+    float gam[CPL], bet[CPL];
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) {
+      gam[e] = gamma ? gamma[c0 + e] : 1.f;
+      bet[e] = beta ? beta[c0 + e] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      __syncthreads();
+      stage_chunk<TM, TN, WN>(acc, i, f, lds, G::PITCH);
+      __syncthreads();
+      for (int q0 = w * G::RPW; q0 < R; q0 += 4 * G::RPW) {
+        const int q = q0 + lr;
+        const int m = m0 + (q >> 5) * TM * 32 + i * 32 + (q & 31);
+        float v[CPL];
+        ld_cpl<CPL>(lds + q * G::PITCH + c0, v);
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) s += v[e];
+        const float mu = lseg_sum<LPR>(s) * (1.f / BN);
+        float d = 0.f;
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) d += (v[e] - mu) * (v[e] - mu);
+        const float rs = rsqrtf(lseg_sum<LPR>(d) * (1.f / BN) + eps);
+        if (m < M) {
+          const int pix = rm(m);
+          st_cpl<CPL>(z + (size_t)pix * BN + c0, v);
+          float yv[CPL];
+#pragma unroll
+          for (int e = 0; e < CPL; ++e) yv[e] = cact((v[e] - mu) * rs * gam[e] + bet[e], act);
+          if (y_nchw) {
+            const int n = pix >> lHW, hw = pix & ((1 << lHW) - 1);
+#pragma unroll
+            for (int e = 0; e < CPL; ++e) y[(((size_t)n * BN + c0 + e) << lHW) + hw] = yv[e];
+          } else {
+            st_cpl<CPL>(y + (size_t)pix * BN + c0, yv);
+          }
+          if (lc == 0) {
+            mean[pix] = mu;
+            rstd[pix] = rs;
+          }
+        }
+      }
+    }
+  }
+};
+
+struct EpiLNBwd : EpiLNBwdP {  // acc = dy (grad of y = act(LN(z))); dz = d/dz; dgamma/dbeta += column sums
+  template <int BM, int BN, int TM, int TN, int WN, class RM>
+  __device__ void run(f16v (&acc)[TM][TN], const Frag<TM, TN, WN>& f, int m0, float* lds, const RM& rm) {
+    using G = RowGeo<BN>;
+    constexpr int WM = 4 / WN, R = WM * 32, CPL = G::CPL, LPR = G::LPR;
+    const int w = threadIdx.x >> 6, lr = f.lane / LPR, lc = f.lane % LPR, c0 = lc * CPL;
+    float gam[CPL], bet[CPL], cg[CPL], cb[CPL];
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) {
+      gam[e] = gamma ? gamma[c0 + e] : 1.f;
+      bet[e] = beta ? beta[c0 + e] : 0.f;
+      cg[e] = 0.f;
+      cb[e] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      __syncthreads();
+      stage_chunk<TM, TN, WN>(acc, i, f, lds, G::PITCH);
+      __syncthreads();
+      for (int q0 = w * G::RPW; q0 < R; q0 += 4 * G::RPW) {
+        const int q = q0 + lr;
+        const int m = m0 + (q >> 5) * TM * 32 + i * 32 + (q & 31);
+        const bool ok = m < M;
+        const int pix = ok ? rm(m) : 0;
+        float dy[CPL], zz[CPL], x[CPL], dx[CPL];
+        ld_cpl<CPL>(lds + q * G::PITCH + c0, dy);
+        if (ok) {
+          ld_cpl<CPL>(z + (size_t)pix * BN + c0, zz);
+        } else {
+#pragma unroll
+          for (int e = 0; e < CPL; ++e) zz[e] = 0.f;
+        }
+        const float mu = ok ? mean[pix] : 0.f, rs = ok ? rstd[pix] : 0.f;
+        float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) {
+          x[e] = (zz[e] - mu) * rs;
+          const float da = ok ? dy[e] * cact_grad(x[e] * gam[e] + bet[e], act) : 0.f;
+          cg[e] += da * x[e];
+          cb[e] += da;
+          dx[e] = da * gam[e];
+          a1 += dx[e];
+          a2 += dx[e] * x[e];
+        }
+        a1 = lseg_sum<LPR>(a1) * (1.f / BN);
+        a2 = lseg_sum<LPR>(a2) * (1.f / BN);
+        if (ok) {
+          float o[CPL];
+#pragma unroll
+          for (int e = 0; e < CPL; ++e) o[e] = rs * (dx[e] - a1 - x[e] * a2);
+          st_cpl<CPL>(dz + (size_t)pix * BN + c0, o);
+        }
+      }
+    }
+    if (dgamma || dbeta) {
+      // rows of a wave pass share columns: fold the RPW row groups, then the 4 waves through LDS
+#pragma unroll
+      for (int e = 0; e < CPL; ++e)
+#pragma unroll
+        for (int o = LPR; o < 64; o <<= 1) {
+          cg[e] += __shfl_xor(cg[e], o, 64);
+          cb[e] += __shfl_xor(cb[e], o, 64);
+        }
+      __syncthreads();
+      if (lr == 0) {
+#pragma unroll
+        for (int e = 0; e < CPL; ++e) {
+          lds[w * BN + c0 + e] = cg[e];
+          lds[4 * BN + w * BN + c0 + e] = cb[e];
+        }
+      }
+      __syncthreads();
+      for (int c = threadIdx.x; c < BN; c += 256) {
+        const float sg = lds[c] + lds[BN + c] + lds[2 * BN + c] + lds[3 * BN + c];
+        const float sb = lds[4 * BN + c] + lds[5 * BN + c] + lds[6 * BN + c] + lds[7 * BN + c];
+        if (dgamma) atomicAdd(dgamma + c, sg);
+        if (dbeta) atomicAdd(dbeta + c, sb);
+      }
+    }
+  }
+};
+
+struct EpiPlain : EpiPlainP {  // out = acc + bias[c] + c0 for c < Nreal; NHWC (ld = Nreal) or NCHW-flat
+  template <int BM, int BN, int TM, int TN, int WN, class RM>
+  __device__ void run(f16v (&acc)[TM][TN], const Frag<TM, TN, WN>& f, int m0, float*, const RM& rm) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + f.row(i, r);
+        if (m >= M) continue;
+        const int pix = rm(m);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int c = f.col(j);
+          if (c >= Nreal) continue;
+          const float v = acc[i][j][r] + (bias ? bias[c] : 0.f) + c0;
+          if (nchw) {
+            const int n = pix >> lHW, hw = pix & ((1 << lHW) - 1);
+            out[(((size_t)n * Nreal + c) << lHW) + hw] = v;
+          } else {
+            out[(size_t)pix * Nreal + c] = v;
+          }
+        }
+      }
+  }
+};
+
+// --------------------------------------------------------------------------- GEMM main loops
+// Tile BM x BN, WM x WN waves of (TM*32) x (TN*32); 64*WM*WN threads; one LDS stage + register
+// prefetch of the next stage.
+template <int BM, int BN, int WM, int WN, class LA, class LB, class EP, class RM>
+__global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep, RM rm, int K) {
+  constexpr int NTH = 64 * WM * WN, TM = BM / WM / 32, TN = BN / WN / 32;
+  static_assert(TM >= 1 && TN >= 1 && TM * WM * 32 == BM && TN * WN * 32 == BN, "bad tile");
+  constexpr int LDS_MAIN = (BM + BN) * LDK;
+  constexpr int LDS_EPI = (4 / WN) * 32 * (BN + 4) > 8 * BN ? (4 / WN) * 32 * (BN + 4) : 8 * BN;
+  __shared__ float lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
+  float* As = lds;
+  float* Bs = lds + BM * LDK;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  la.init(m0);
+  lb.init(n0);
+  Frag<TM, TN, WN> f;
+  f.lane = threadIdx.x & 63;
+  f.wm = (threadIdx.x >> 6) / WN;
+  f.wn = (threadIdx.x >> 6) % WN;
+  f16v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  f4 ra[LA::NV], rb[LB::NV];
+  la.load(0, ra);
+  lb.load(0, rb);
+  const int arow = f.wm * TM * 32 + (f.lane & 31), brow = f.wn * TN * 32 + (f.lane & 31), kof = 4 * (f.lane >> 5);
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    __syncthreads();
+    la.store(ra, As);
+    lb.store(rb, Bs);
+    __syncthreads();
+    if (k0 + BK < K) {
+      la.load(k0 + BK, ra);
+      lb.load(k0 + BK, rb);
+    }
+#pragma unroll
+    for (int s = 0; s < BK / 8; ++s) {
+      f4 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = *(const f4*)(As + (arow + 32 * i) * LDK + 8 * s + kof);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *(const f4*)(Bs + (brow + 32 * j) * LDK + 8 * s + kof);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  ep.template run<BM, BN, TM, TN, WN>(acc, f, m0, lds, rm);
+}
+
+// WGRAD: rows a (Ca), cols (tap,b) (16 Cb), K = pixel range of split blockIdx.z; writes the partial slab.
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM* WN) void wgrad_kernel(WgP<BM, 64 * WM * WN> la, WgQ<BN, 64 * WM * WN> lb,
+                                                              float* slab, int ldn, int Mrows, int kper) {
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  __shared__ float lds[(BM + BN) * LDK];
+  float* As = lds;
+  float* Bs = lds + BM * LDK;
+  const int r0 = blockIdx.x * BM, c0 = blockIdx.y * BN;
+  la.init(r0);
+  lb.init(c0);
+  const int kb = blockIdx.z * kper, ke = kb + kper;
+  Frag<TM, TN, WN> f;
+  f.lane = threadIdx.x & 63;
+  f.wm = (threadIdx.x >> 6) / WN;
+  f.wn = (threadIdx.x >> 6) % WN;
+  f16v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  f4 ra[WgP<BM, 64 * WM * WN>::NV], rb[WgQ<BN, 64 * WM * WN>::NV];
+  la.load(kb, ra);
+  lb.load(kb, rb);
+  const int arow = f.wm * TM * 32 + (f.lane & 31), brow = f.wn * TN * 32 + (f.lane & 31), kof = 4 * (f.lane >> 5);
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    __syncthreads();
+    la.store(ra, As);
+    lb.store(rb, Bs);
+    __syncthreads();
+    if (k0 + BK < ke) {
+      la.load(k0 + BK, ra);
+      lb.load(k0 + BK, rb);
+    }
+#pragma unroll
+    for (int s = 0; s < BK / 8; ++s) {
+      f4 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = *(const f4*)(As + (arow + 32 * i) * LDK + 8 * s + kof);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *(const f4*)(Bs + (brow + 32 * j) * LDK + 8 * s + kof);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
+    }
+  }
+  float* out = slab + (size_t)blockIdx.z * Mrows * ldn;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) out[(size_t)(r0 + f.row(i, r)) * ldn + c0 + f.col(j)] = acc[i][j][r];
+}
+
+// dW[a][b][kh][kw] = sum_s slab[s][a][tap*Cbp + b]   (b < Cb).  Block = 16 float4 columns (64 slab
+// entries) x 16 split groups; each thread sums every 16th split of its float4, LDS combines the groups.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dw, int S,
+                                                           int Ca, int Cbp, int Cb) {
+  __shared__ f4 part[16][17];
+  const int per = 16 * Cbp, tot = Ca * per;
+  const int col = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int idx = (blockIdx.x * 16 + col) * 4;  // first of 4 consecutive slab entries
+  f4 acc = zero4();
+  if (idx < tot) {
+    const f4* src = (const f4*)(slab + idx);
+    const size_t stride = (size_t)tot / 4;
+#pragma unroll 4
+    for (int k = grp; k < S; k += 16) acc += src[k * stride];
+  }
+  part[grp][col] = acc;
+  __syncthreads();
+  if (grp == 0 && idx < tot) {
+    f4 s = zero4();
+#pragma unroll
+    for (int g = 0; g < 16; ++g) s += part[g][col];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = idx + e, a = i / per, rem = i - a * per, tap = rem / Cbp, b = rem - tap * Cbp;
+      if (b < Cb) dw[((size_t)a * Cb + b) * 16 + tap] = s[e];
+    }
+  }
+}
+
+// W[A][B][4][4] -> DOWN pack [A][16][Bp] (b >= B zero)
+__global__ void pack_down_kernel(const float* __restrict__ w, float* __restrict__ out, int A, int B, int Bp) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= A * 16 * Bp) return;
+  const int a = idx / (16 * Bp), rem = idx - a * 16 * Bp, tap = rem / Bp, b = rem - tap * Bp;
+  out[idx] = b < B ? w[((size_t)a * B + b) * 16 + tap] : 0.f;
+}
+
+// W[A][B][4][4] -> UP pack [4 classes][Bp][4 t][A]: class (cy,cx), t = (th,tw), kh = 1-cy+2th, kw = 1-cx+2tw
+__global__ void pack_up_kernel(const float* __restrict__ w, float* __restrict__ out, int A, int B, int Bp) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 4 * Bp * 4 * A) return;
+  const int a = idx % A, t = (idx / A) & 3, b = (idx / (4 * A)) % Bp, cls = idx / (4 * A * Bp);
+  const int kh = 1 - (cls >> 1) + 2 * (t >> 1), kw = 1 - (cls & 1) + 2 * (t & 1);
+  out[idx] = b < B ? w[((size_t)a * B + b) * 16 + kh * 4 + kw] : 0.f;
+}
+
+// NCHW (uint8 or f32) with C <= 4 channels -> NHWC4 f32, scaled; channel C..3 = 0
+template <typename T>
+__global__ void to_nhwc4_kernel(const T* __restrict__ x, f4* __restrict__ out, int N, int C, int HW, float scale) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * HW) return;
+  const int n = idx / HW, hw = idx - n * HW;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < C; ++c) v[c] = (float)x[((size_t)n * C + c) * HW + hw] * scale;
+  out[idx] = f4{v[0], v[1], v[2], v[3]};
+}
+
+// Row LayerNorm+act backward with dy in NCHW-flat order (the encoder's last stage feeds the flat
+// embedding); z NHWC [M][C]; one wave per pixel row, C/64 channels per lane; column partials per
+// block, one atomic per channel per block.
+template <int CPL>
+__global__ __launch_bounds__(256) void ln_bwd_flat_kernel(const float* __restrict__ dy, const float* __restrict__ z,
+                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          float* __restrict__ dz, float* dgamma, float* dbeta, int M,
+                                                          int lHW, int act, int rows_per_block) {
+  constexpr int C = 64 * CPL;
+  __shared__ float cr[2][4][C];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float cg[CPL], cb[CPL];
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) cg[e] = cb[e] = 0.f;
+  const int rb = blockIdx.x * rows_per_block;
+  for (int m = rb + w; m < min(M, rb + rows_per_block); m += 4) {
+    const float mu = mean[m], rs = rstd[m];
+    const int n = m >> lHW, hw = m & ((1 << lHW) - 1);
+    float xh[CPL], dxh[CPL], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) {
+      const int c = lane + 64 * e;
+      const float g = gamma ? gamma[c] : 1.f;
+      xh[e] = (z[(size_t)m * C + c] - mu) * rs;
+      const float a = xh[e] * g + (beta ? beta[c] : 0.f);
+      const float da = dy[(((size_t)n * C + c) << lHW) + hw] * cact_grad(a, act);
+      cg[e] += da * xh[e];
+      cb[e] += da;
+      dxh[e] = da * g;
+      s1 += dxh[e];
+      s2 += dxh[e] * xh[e];
+    }
+    s1 = wave_sum(s1) * (1.f / C);
+    s2 = wave_sum(s2) * (1.f / C);
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) dz[(size_t)m * C + lane + 64 * e] = rs * (dxh[e] - s1 - xh[e] * s2);
+  }
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) {
+    cr[0][w][lane + 64 * e] = cg[e];
+    cr[1][w][lane + 64 * e] = cb[e];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float sg = cr[0][0][c] + cr[0][1][c] + cr[0][2][c] + cr[0][3][c];
+    const float sb = cr[1][0][c] + cr[1][1][c] + cr[1][2][c] + cr[1][3][c];
+    if (dgamma) atomicAdd(dgamma + c, sg);
+    if (dbeta) atomicAdd(dbeta + c, sb);
+  }
+}
+
+// ConvT forward to a tiny channel count (the decoder's last layer, 3 image channels), on VALU:
+// a workgroup owns a 16x16 tile of small-grid pixels of one image (+1 halo) staged in LDS (NHWC,
+// Ca channels) and produces the 32x32 large-grid outputs; weights [Ca][CO][4][4] in LDS.
+// out NCHW [n][co][y][x] = bias[co] + c0 + sum.
+template <int CO, int CA>
+__global__ __launch_bounds__(256) void up_small_kernel(const float* __restrict__ P, const float* __restrict__ W,
+                                                       const float* __restrict__ bias, float c0, float* __restrict__ out,
+                                                       int lSH, int lSW) {
+  constexpr int T = 16, TH = T + 2;
+  __shared__ float tile[TH * TH * (CA + 1)];
+  __shared__ float ws[CA * CO * 16];
+  const int SH = 1 << lSH, SW = 1 << lSW;
+  const int tx = SW / T;
+  const int n = blockIdx.y, ty0 = (blockIdx.x / tx) * T, tx0 = (blockIdx.x % tx) * T;
+  for (int i = threadIdx.x; i < CA * CO * 16; i += 256) ws[i] = W[i];
+  for (int i = threadIdx.x; i < TH * TH * (CA / 4); i += 256) {
+    const int pixl = i / (CA / 4), aq = i % (CA / 4);
+    const int p = ty0 - 1 + pixl / TH, q = tx0 - 1 + pixl % TH;
+    f4 v = zero4();
+    if (p >= 0 && p < SH && q >= 0 && q < SW) v = *(const f4*)(P + ((((size_t)n * SH + p) * SW + q) * CA) + 4 * aq);
+    float* d = tile + pixl * (CA + 1) + 4 * aq;
+    d[0] = v[0];
+    d[1] = v[1];
+    d[2] = v[2];
+    d[3] = v[3];
+  }
+  __syncthreads();
+  const int LH = 2 * SH, LW = 2 * SW;
+  // 1024 outputs per block (32x32), 4 per thread: thread -> (yy, xx pair)
+  for (int o = threadIdx.x; o < 4 * T * T; o += 256) {
+    const int yy = o / (2 * T), xx = o % (2 * T);
+    const int y = 2 * ty0 + yy, x = 2 * tx0 + xx;
+    const int cy = yy & 1, cx = xx & 1, u = yy >> 1, v = xx >> 1;
+    float s[CO];
+#pragma unroll
+    for (int c = 0; c < CO; ++c) s[c] = 0.f;
+#pragma unroll
+    for (int th = 0; th < 2; ++th)
+#pragma unroll
+      for (int tw = 0; tw < 2; ++tw) {
+        const int pl = (u + cy - th + 1) * TH + (v + cx - tw + 1);
+        const int kh = 1 - cy + 2 * th, kw = 1 - cx + 2 * tw;
+        const float* src = tile + pl * (CA + 1);
+#pragma unroll 8
+        for (int a = 0; a < CA; ++a) {
+          const float pv = src[a];
+#pragma unroll
+          for (int c = 0; c < CO; ++c) s[c] += pv * ws[(a * CO + c) * 16 + kh * 4 + kw];
+        }
+      }
+#pragma unroll
+    for (int c = 0; c < CO; ++c) out[(((size_t)n * CO + c) * LH + y) * LW + x] = s[c] + (bias ? bias[c] : 0.f) + c0;
+  }
+}
+
+}  // namespace conv
+}  // namespace srl
+
+// =============================================================================== host launchers
+using namespace srl::conv;
+
+namespace {
+int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+template <class K, class... Args>
+void launch(K kernel, dim3 grid, dim3 block, hipStream_t st, Args... args) {
+  hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
+}
+}  // namespace
+
+template <int BM, int BN, int WM, int WN, class LA, class RM>
+static void dispatch_epi(const LA& la, const Dense<BN, 64 * WM * WN>& lb, const ConvEpi& e, const RM& rm, int K, dim3 grid,
+                         hipStream_t st) {
+  dim3 block(64 * WM * WN);
+  if (e.mode == 0) {
+    EpiLNAct ep;
+    static_cast<EpiLNActP&>(ep) = e.ln;
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNAct, RM>, grid, block, st, la, lb, ep, rm, K);
+  } else if (e.mode == 1) {
+    EpiLNBwd ep;
+    static_cast<EpiLNBwdP&>(ep) = e.lb;
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNBwd, RM>, grid, block, st, la, lb, ep, rm, K);
+  } else {
+    EpiPlain ep;
+    static_cast<EpiPlainP&>(ep) = e.pl;
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiPlain, RM>, grid, block, st, la, lb, ep, rm, K);
+  }
+}
+
+// DOWN: out grid (N, SH, SW) with Nc output channels (32..256, pow2), input Q NHWC (N, 2SH, 2SW, Cb)
+template <int BM, int BN, int WM, int WN>
+static void down_cfg(const float* Q, const float* Wp, int N, int SH, int SW, int Cb, const ConvEpi& e, hipStream_t st) {
+  constexpr int NTH = 64 * WM * WN;
+  const int M = N * SH * SW;
+  DownGather<BM, NTH> la;
+  la.Q = Q;
+  la.lCb = ilog2(Cb);
+  la.lSH = ilog2(SH);
+  la.lSW = ilog2(SW);
+  la.M = M;
+  Dense<BN, NTH> lb;
+  lb.W = Wp;
+  lb.K = 16 * Cb;
+  lb.cls_stride = 0;
+  dispatch_epi<BM, BN, WM, WN>(la, lb, e, RowDown{}, 16 * Cb, dim3((M + BM - 1) / BM, 1, 1), st);
+}
+
+bool launch_conv_down(const float* Q, const float* Wp, int N, int SH, int SW, int Cb, int Nc, const ConvEpi& e,
+                      hipStream_t st) {
+  switch (Nc) {
+    case 256: down_cfg<64, 256, 1, 4>(Q, Wp, N, SH, SW, Cb, e, st); return true;
+    case 128: down_cfg<128, 128, 2, 2>(Q, Wp, N, SH, SW, Cb, e, st); return true;
+    case 64: down_cfg<256, 64, 4, 1>(Q, Wp, N, SH, SW, Cb, e, st); return true;
+    case 32: down_cfg<256, 32, 4, 1>(Q, Wp, N, SH, SW, Cb, e, st); return true;
+    default: return false;
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+static void up_cfg(const float* P, const float* Wp, int N, int SH, int SW, int Ca, int Bp, const ConvEpi& e, hipStream_t st) {
+  constexpr int NTH = 64 * WM * WN;
+  const int M = N * SH * SW;
+  UpGather<BM, NTH> la;
+  la.P = P;
+  la.lCa = ilog2(Ca);
+  la.lSH = ilog2(SH);
+  la.lSW = ilog2(SW);
+  la.M = M;
+  Dense<BN, NTH> lb;
+  lb.W = Wp;
+  lb.K = 4 * Ca;
+  lb.cls_stride = (size_t)Bp * 4 * Ca;
+  RowUp rm{ilog2(SH), ilog2(SW)};
+  dispatch_epi<BM, BN, WM, WN>(la, lb, e, rm, 4 * Ca, dim3((M + BM - 1) / BM, 1, 4), st);
+}
+
+// UP: P NHWC (N, SH, SW, Ca) -> out grid (N, 2SH, 2SW) with Bp output channels (pack padding)
+bool launch_conv_up(const float* P, const float* Wp, int N, int SH, int SW, int Ca, int Bp, const ConvEpi& e,
+                    hipStream_t st) {
+  switch (Bp) {
+    case 256: up_cfg<64, 256, 1, 4>(P, Wp, N, SH, SW, Ca, Bp, e, st); return true;
+    case 128: up_cfg<128, 128, 2, 2>(P, Wp, N, SH, SW, Ca, Bp, e, st); return true;
+    case 64: up_cfg<256, 64, 4, 1>(P, Wp, N, SH, SW, Ca, Bp, e, st); return true;
+    case 32: up_cfg<256, 32, 4, 1>(P, Wp, N, SH, SW, Ca, Bp, e, st); return true;
+    default: return false;
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+static void wgrad_cfg(const float* P, const float* Q, float* slab, int S, int kper, int N, int SH, int SW, int Ca, int Cbp,
+                      hipStream_t st) {
+  constexpr int NTH = 64 * WM * WN;
+  const int M = N * SH * SW;
+  WgP<BM, NTH> la;
+  la.P = P;
+  la.lCa = ilog2(Ca);
+  la.M = M;
+  WgQ<BN, NTH> lb;
+  lb.Q = Q;
+  lb.lCb = ilog2(Cbp);
+  lb.lSH = ilog2(SH);
+  lb.lSW = ilog2(SW);
+  lb.M = M;
+  dim3 grid(Ca / BM, 16 * Cbp / BN, S);
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN>), grid, dim3(NTH), 0, st, la, lb, slab, 16 * Cbp, Ca, kper);
+}
+
+// number of K splits (and pixels per split) for a WGRAD problem; slab = S * Ca * 16 * Cbp floats
+void conv_wgrad_plan(int N, int SH, int SW, int Ca, int Cbp, int* S, int* kper) {
+  const int M = N * SH * SW;
+  const int BM = Ca >= 128 ? 128 : Ca, BN = 128 < 16 * Cbp ? 128 : 16 * Cbp;
+  const int tiles = (Ca / BM) * (16 * Cbp / BN);
+  // ~512 workgroups (2 per CU); 1024 for a single-tile problem (E1 / D4: 2K outputs, 1M pixels)
+  int want = tiles == 1 ? 1024 : (512 + tiles - 1) / tiles;
+  int kp = (M + want - 1) / want;
+  kp = ((kp + 31) / 32) * 32;
+  if (kp < 1024) kp = 1024;
+  *kper = kp;
+  *S = (M + kp - 1) / kp;
+}
+
+bool launch_conv_wgrad(const float* P, const float* Q, float* slab, float* dw, int N, int SH, int SW, int Ca, int Cbp, int Cb,
+                       hipStream_t st) {
+  int S, kper;
+  conv_wgrad_plan(N, SH, SW, Ca, Cbp, &S, &kper);
+  if (Ca >= 128 && 16 * Cbp >= 128)
+    wgrad_cfg<128, 128, 2, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+  else if (Ca == 64 && 16 * Cbp >= 128)
+    wgrad_cfg<64, 128, 1, 4>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+  else if (Ca == 32 && 16 * Cbp >= 128)
+    wgrad_cfg<32, 128, 1, 4>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+  else if (Ca == 32 && 16 * Cbp == 64)
+    wgrad_cfg<32, 64, 1, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+  else if (Ca == 64 && 16 * Cbp == 64)
+    wgrad_cfg<64, 64, 1, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+  else if (Ca >= 128 && 16 * Cbp == 64)
+    wgrad_cfg<128, 64, 2, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+  else
+    return false;
+  const int tot = Ca * 16 * Cbp;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((tot + 63) / 64), dim3(256), 0, st, slab, dw, S, Ca, Cbp, Cb);
+  return true;
+}
+
+void launch_pack_down(const float* w, float* out, int A, int B, int Bp, hipStream_t st) {
+  const int tot = A * 16 * Bp;
+  hipLaunchKernelGGL(pack_down_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, w, out, A, B, Bp);
+}
+
+void launch_pack_up(const float* w, float* out, int A, int B, int Bp, hipStream_t st) {
+  const int tot = 16 * Bp * A;
+  hipLaunchKernelGGL(pack_up_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, w, out, A, B, Bp);
+}
+
+void launch_to_nhwc4(const void* x, bool u8, float* out, int N, int C, int HW, float scale, hipStream_t st) {
+  const int tot = N * HW;
+  if (u8)
+    hipLaunchKernelGGL(to_nhwc4_kernel<uint8_t>, dim3((tot + 255) / 256), dim3(256), 0, st, (const uint8_t*)x, (f4*)out, N,
+                       C, HW, scale);
+  else
+    hipLaunchKernelGGL(to_nhwc4_kernel<float>, dim3((tot + 255) / 256), dim3(256), 0, st, (const float*)x, (f4*)out, N, C,
+                       HW, scale);
+}
+
+bool launch_ln_bwd_flat(const float* dy, const float* z, const float* mean, const float* rstd, const float* gamma,
+                        const float* beta, float* dz, float* dgamma, float* dbeta, int M, int C, int HW, int act,
+                        hipStream_t st) {
+  const int rpb = 64;
+  dim3 grid((M + rpb - 1) / rpb);
+  const int lHW = ilog2(HW);
+  switch (C) {
+    case 64: hipLaunchKernelGGL(ln_bwd_flat_kernel<1>, grid, dim3(256), 0, st, dy, z, mean, rstd, gamma, beta, dz, dgamma, dbeta, M, lHW, act, rpb); return true;
+    case 128: hipLaunchKernelGGL(ln_bwd_flat_kernel<2>, grid, dim3(256), 0, st, dy, z, mean, rstd, gamma, beta, dz, dgamma, dbeta, M, lHW, act, rpb); return true;
+    case 256: hipLaunchKernelGGL(ln_bwd_flat_kernel<4>, grid, dim3(256), 0, st, dy, z, mean, rstd, gamma, beta, dz, dgamma, dbeta, M, lHW, act, rpb); return true;
+    default: return false;
+  }
+}
+
+bool launch_up_small(const float* P, const float* W, const float* bias, float c0, float* out, int N, int SH, int SW, int Ca,
+                     int CO, hipStream_t st) {
+  if (SH % 16 || SW % 16 || CO != 3 || Ca != 32) return false;
+  dim3 grid((SH / 16) * (SW / 16), N);
+  hipLaunchKernelGGL((up_small_kernel<3, 32>), grid, dim3(256), 0, st, P, W, bias, c0, out, ilog2(SH), ilog2(SW));
+  return true;
+}

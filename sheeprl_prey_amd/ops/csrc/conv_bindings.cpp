@@ -1,0 +1,236 @@
+// Torch bindings of the implicit-GEMM k4 s2 p1 convolutions (conv.hip).  Shapes are checked here,
+// before any launch: every kernel assumes power-of-two grids / channel counts and NHWC inputs.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <hip/hip_runtime.h>
+
+#include "conv.h"
+
+using srl::conv::ConvEpi;
+
+bool launch_conv_down(const float*, const float*, int, int, int, int, int, const ConvEpi&, hipStream_t);
+bool launch_conv_up(const float*, const float*, int, int, int, int, int, const ConvEpi&, hipStream_t);
+void conv_wgrad_plan(int, int, int, int, int, int*, int*);
+bool launch_conv_wgrad(const float*, const float*, float*, float*, int, int, int, int, int, int, hipStream_t);
+void launch_pack_down(const float*, float*, int, int, int, hipStream_t);
+void launch_pack_up(const float*, float*, int, int, int, hipStream_t);
+void launch_to_nhwc4(const void*, bool, float*, int, int, int, float, hipStream_t);
+bool launch_ln_bwd_flat(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
+                        float*, int, int, int, int, hipStream_t);
+bool launch_up_small(const float*, const float*, const float*, float, float*, int, int, int, int, int, hipStream_t);
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+bool pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
+
+void chk(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous(), name,
+              " must be a contiguous float32 GPU tensor");
+}
+const float* optp(const c10::optional<torch::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  chk(*t, "optional operand");
+  return t->data_ptr<float>();
+}
+float* optw(const c10::optional<torch::Tensor>& t) { return const_cast<float*>(optp(t)); }
+
+// x: [N, H, W, C] NHWC
+void chk_nhwc(const torch::Tensor& x, const char* name) {
+  chk(x, name);
+  TORCH_CHECK(x.dim() == 4, name, " must be NHWC [N,H,W,C]");
+  TORCH_CHECK(pow2(x.size(1)) && pow2(x.size(2)) && pow2(x.size(3)) && x.size(3) >= 4, name,
+              ": H, W and C must be powers of two (C >= 4)");
+}
+
+ConvEpi make_epi(int64_t mode, int64_t M, int64_t Nc, const torch::Tensor& out0, const c10::optional<torch::Tensor>& gamma,
+                 const c10::optional<torch::Tensor>& beta, double eps, int64_t act) {
+  ConvEpi e{};
+  e.mode = (int)mode;
+  (void)out0;
+  (void)Nc;
+  e.ln.gamma = optp(gamma);
+  e.ln.beta = optp(beta);
+  e.ln.eps = (float)eps;
+  e.ln.act = (int)act;
+  e.ln.M = (int)M;
+  e.lb.gamma = e.ln.gamma;
+  e.lb.beta = e.ln.beta;
+  e.lb.act = (int)act;
+  e.lb.M = (int)M;
+  e.pl.M = (int)M;
+  return e;
+}
+
+int ilog2(int64_t v) {
+  int l = 0;
+  while ((int64_t(1) << l) < v) ++l;
+  return l;
+}
+
+}  // namespace
+
+torch::Tensor conv_pack_down(torch::Tensor w, int64_t Bp) {
+  chk(w, "w");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 4 && w.size(3) == 4, "pack_down: weight must be [A,B,4,4]");
+  TORCH_CHECK(Bp >= w.size(1) && Bp % 4 == 0, "pack_down: bad padding");
+  auto out = torch::empty({w.size(0), 16, Bp}, w.options());
+  launch_pack_down(w.data_ptr<float>(), out.data_ptr<float>(), w.size(0), w.size(1), Bp, stream());
+  return out;
+}
+
+torch::Tensor conv_pack_up(torch::Tensor w, int64_t Bp) {
+  chk(w, "w");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 4 && w.size(3) == 4, "pack_up: weight must be [A,B,4,4]");
+  TORCH_CHECK(Bp >= w.size(1), "pack_up: bad padding");
+  auto out = torch::empty({4, Bp, 4, w.size(0)}, w.options());
+  launch_pack_up(w.data_ptr<float>(), out.data_ptr<float>(), w.size(0), w.size(1), Bp, stream());
+  return out;
+}
+
+// DOWN: Q NHWC [N, 2SH, 2SW, Cb], Wp [Nc, 16, Cb] -> outputs on [N, SH, SW, Nc]
+// mode 0: LN_ACT -> (z, y, mean, rstd); y_nchw: y as [N, Nc*SH*SW] (C,H,W order)
+// mode 1: LN_BWD (ln_z/ln_mean/ln_rstd of the output layer, dgamma/dbeta accumulated) -> (dz)
+// mode 2: PLAIN (bias, c0, Nreal, nchw) -> (out)
+std::vector<torch::Tensor> conv_gemm(int64_t kind, torch::Tensor src, torch::Tensor Wp, int64_t Nc, int64_t mode,
+                                     c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, double eps,
+                                     int64_t act, bool out_nchw, c10::optional<torch::Tensor> ln_z,
+                                     c10::optional<torch::Tensor> ln_mean, c10::optional<torch::Tensor> ln_rstd,
+                                     c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta,
+                                     c10::optional<torch::Tensor> bias, double c0, int64_t Nreal) {
+  chk_nhwc(src, "conv input");
+  chk(Wp, "packed weight");
+  const bool down = kind == 0;
+  const int64_t N = src.size(0), H = src.size(1), W = src.size(2), C = src.size(3);
+  TORCH_CHECK(Nc == 32 || Nc == 64 || Nc == 128 || Nc == 256, "conv: output channel tile must be 32..256");
+  int64_t OH, OW, M;
+  if (down) {
+    TORCH_CHECK(H >= 2 && W >= 2, "conv down: input too small");
+    OH = H / 2;
+    OW = W / 2;
+    M = N * OH * OW;
+    TORCH_CHECK(Wp.numel() == Nc * 16 * C, "conv down: packed weight has the wrong size");
+  } else {
+    TORCH_CHECK(C >= 32, "conv up: input channels must be >= 32");
+    OH = 2 * H;
+    OW = 2 * W;
+    M = N * H * W;  // per parity class
+    TORCH_CHECK(Wp.numel() == 4 * Nc * 4 * C, "conv up: packed weight has the wrong size");
+  }
+  TORCH_CHECK(N * OH * OW * Nc < (int64_t(1) << 31), "conv: tensor too large for 32-bit pixel indices");
+  auto opts = src.options();
+  ConvEpi e = make_epi(mode, M, Nc, src, gamma, beta, eps, act);
+  std::vector<torch::Tensor> outs;
+  const int lHW = ilog2(OH * OW);
+  if (mode == 0) {
+    auto z = torch::empty({N, OH, OW, Nc}, opts);
+    auto y = out_nchw ? torch::empty({N, Nc * OH * OW}, opts) : torch::empty({N, OH, OW, Nc}, opts);
+    auto mean = torch::empty({N * OH * OW}, opts);
+    auto rstd = torch::empty({N * OH * OW}, opts);
+    e.ln.z = z.data_ptr<float>();
+    e.ln.y = y.data_ptr<float>();
+    e.ln.mean = mean.data_ptr<float>();
+    e.ln.rstd = rstd.data_ptr<float>();
+    e.ln.y_nchw = out_nchw ? 1 : 0;
+    e.ln.lHW = lHW;
+    outs = {z, y, mean, rstd};
+  } else if (mode == 1) {
+    TORCH_CHECK(ln_z.has_value() && ln_mean.has_value() && ln_rstd.has_value(), "conv LN_BWD needs z/mean/rstd");
+    TORCH_CHECK(ln_z->numel() == N * OH * OW * Nc && ln_mean->numel() == N * OH * OW, "conv LN_BWD: saved stats size");
+    auto dz = torch::empty({N, OH, OW, Nc}, opts);
+    e.lb.z = optp(ln_z);
+    e.lb.mean = optp(ln_mean);
+    e.lb.rstd = optp(ln_rstd);
+    e.lb.dz = dz.data_ptr<float>();
+    e.lb.dgamma = optw(dgamma);
+    e.lb.dbeta = optw(dbeta);
+    outs = {dz};
+  } else {
+    TORCH_CHECK(Nreal >= 1 && Nreal <= Nc, "conv PLAIN: bad Nreal");
+    auto out = out_nchw ? torch::empty({N, Nreal, OH, OW}, opts) : torch::empty({N, OH, OW, Nreal}, opts);
+    e.pl.out = out.data_ptr<float>();
+    e.pl.bias = optp(bias);
+    e.pl.c0 = (float)c0;
+    e.pl.Nreal = (int)Nreal;
+    e.pl.nchw = out_nchw ? 1 : 0;
+    e.pl.lHW = lHW;
+    outs = {out};
+  }
+  bool ok = down ? launch_conv_down(src.data_ptr<float>(), Wp.data_ptr<float>(), N, OH, OW, C, Nc, e, stream())
+                 : launch_conv_up(src.data_ptr<float>(), Wp.data_ptr<float>(), N, H, W, C, Nc, e, stream());
+  TORCH_CHECK(ok, "conv: unsupported configuration");
+  return outs;
+}
+
+// dW[a][b][4][4] = sum_m P[m][a] Q[gather(m, tap)][b]; P NHWC small grid [N,SH,SW,Ca], Q NHWC large [N,2SH,2SW,Cbp]
+torch::Tensor conv_wgrad(torch::Tensor P, torch::Tensor Q, int64_t Cb) {
+  chk_nhwc(P, "wgrad P");
+  chk_nhwc(Q, "wgrad Q");
+  const int64_t N = P.size(0), SH = P.size(1), SW = P.size(2), Ca = P.size(3), Cbp = Q.size(3);
+  TORCH_CHECK(Q.size(0) == N && Q.size(1) == 2 * SH && Q.size(2) == 2 * SW, "wgrad: P/Q grids do not match");
+  TORCH_CHECK(Ca >= 32 && Ca <= 4096 && Cb <= Cbp, "wgrad: channel counts");
+  TORCH_CHECK(N * SH * SW < (int64_t(1) << 31), "wgrad: too many pixels");
+  int S, kper;
+  conv_wgrad_plan(N, SH, SW, Ca, Cbp, &S, &kper);
+  auto slab = torch::empty({(int64_t)S, Ca, 16 * Cbp}, P.options());
+  auto dw = torch::empty({Ca, Cb, 4, 4}, P.options());
+  bool ok = launch_conv_wgrad(P.data_ptr<float>(), Q.data_ptr<float>(), slab.data_ptr<float>(), dw.data_ptr<float>(), N,
+                              SH, SW, Ca, Cbp, Cb, stream());
+  TORCH_CHECK(ok, "wgrad: unsupported configuration");
+  return dw;
+}
+
+// NCHW (uint8 or float32, C <= 4) -> NHWC4 float32 scaled
+torch::Tensor conv_to_nhwc4(torch::Tensor x, double scale) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4 && x.size(1) <= 4, "to_nhwc4: x must be NCHW with C <= 4");
+  const bool u8 = x.scalar_type() == torch::kUInt8;
+  TORCH_CHECK(u8 || x.scalar_type() == torch::kFloat32, "to_nhwc4: uint8 or float32");
+  auto out = torch::empty({x.size(0), x.size(2), x.size(3), 4}, x.options().dtype(torch::kFloat32));
+  launch_to_nhwc4(x.data_ptr(), u8, out.data_ptr<float>(), x.size(0), x.size(1), x.size(2) * x.size(3), (float)scale,
+                  stream());
+  return out;
+}
+
+// row LN+act backward, dy NCHW-flat [N, C*HW], z NHWC [N, HW, C]
+torch::Tensor conv_ln_bwd_flat(torch::Tensor dy, torch::Tensor z, torch::Tensor mean, torch::Tensor rstd,
+                               c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, int64_t act,
+                               c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta) {
+  chk(dy, "dy");
+  chk_nhwc(z, "z");
+  chk(mean, "mean");
+  chk(rstd, "rstd");
+  const int64_t N = z.size(0), HW = z.size(1) * z.size(2), C = z.size(3);
+  TORCH_CHECK(dy.numel() == z.numel() && mean.numel() == N * HW, "ln_bwd_flat: sizes");
+  auto dz = torch::empty_like(z);
+  bool ok = launch_ln_bwd_flat(dy.data_ptr<float>(), z.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                               optp(gamma), optp(beta), dz.data_ptr<float>(), optw(dgamma), optw(dbeta), N * HW, C, HW,
+                               (int)act, stream());
+  TORCH_CHECK(ok, "ln_bwd_flat: channel count must be 64, 128 or 256");
+  return dz;
+}
+
+// ConvT forward to 3 channels (VALU kernel): P NHWC [N,SH,SW,32], W [32,3,4,4] -> NCHW [N,3,2SH,2SW]
+torch::Tensor conv_up_small(torch::Tensor P, torch::Tensor W, c10::optional<torch::Tensor> bias, double c0) {
+  chk_nhwc(P, "P");
+  chk(W, "W");
+  const int64_t N = P.size(0), SH = P.size(1), SW = P.size(2), Ca = P.size(3);
+  TORCH_CHECK(W.dim() == 4 && W.size(0) == Ca && W.size(2) == 4 && W.size(3) == 4, "up_small: weight shape");
+  const int64_t CO = W.size(1);
+  auto out = torch::empty({N, CO, 2 * SH, 2 * SW}, P.options());
+  bool ok = launch_up_small(P.data_ptr<float>(), W.data_ptr<float>(), optp(bias), (float)c0, out.data_ptr<float>(), N, SH,
+                            SW, Ca, CO, stream());
+  TORCH_CHECK(ok, "up_small: needs Ca = 32, 3 outputs and a grid multiple of 16");
+  return out;
+}
+
+void register_conv(pybind11::module& m) {
+  m.def("conv_pack_down", &conv_pack_down);
+  m.def("conv_pack_up", &conv_pack_up);
+  m.def("conv_gemm", &conv_gemm);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_to_nhwc4", &conv_to_nhwc4);
+  m.def("conv_ln_bwd_flat", &conv_ln_bwd_flat);
+  m.def("conv_up_small", &conv_up_small);
+}

@@ -1,0 +1,124 @@
+"""Implicit-GEMM k4 s2 p1 convolutions (ops/csrc/conv.hip) against fp32 PyTorch references:
+each GEMM form on its own (DOWN = Conv2d fwd / ConvT data-grad, UP = ConvT fwd / Conv2d data-grad,
+WGRAD) and the whole DreamerV3 encoder / decoder stacks, forward and every parameter gradient."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from sheeprl_prey_amd import ops
+from sheeprl_prey_amd.ops import conv as conv_ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, rtol=2e-4, atol=2e-4):
+    scale = b.abs().max().clamp_min(1.0)
+    torch.testing.assert_close(a / scale, b / scale, rtol=rtol, atol=atol)
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("cin,cout,hw,n", [(4, 32, 64, 3), (32, 64, 32, 2), (64, 128, 16, 5), (128, 256, 8, 4)])
+def test_down_plain_matches_conv2d(cin, cout, hw, n):
+    C = ops._ext()
+    torch.manual_seed(0)
+    x = torch.randn(n, cin, hw, hw, device=DEV)
+    w = torch.randn(cout, cin, 4, 4, device=DEV) * 0.1
+    ref = F.conv2d(x, w, stride=2, padding=1)
+    wp = C.conv_pack_down(w, cin)
+    out = C.conv_gemm(0, _nhwc(x), wp, cout, 2, None, None, 0.0, 0, True, None, None, None, None, None, None, 0.0, cout)[0]
+    _close(out, ref)
+
+
+@pytest.mark.parametrize("cin,cout,hw,n", [(256, 128, 4, 3), (128, 64, 8, 2), (64, 32, 16, 5), (64, 256, 4, 2)])
+def test_up_plain_matches_conv_transpose(cin, cout, hw, n):
+    C = ops._ext()
+    torch.manual_seed(0)
+    x = torch.randn(n, cin, hw, hw, device=DEV)
+    w = torch.randn(cin, cout, 4, 4, device=DEV) * 0.1
+    b = torch.randn(cout, device=DEV)
+    ref = F.conv_transpose2d(x, w, b, stride=2, padding=1) + 0.5
+    wp = C.conv_pack_up(w, cout)
+    out = C.conv_gemm(1, _nhwc(x), wp, cout, 2, None, None, 0.0, 0, True, None, None, None, None, None, b, 0.5, cout)[0]
+    _close(out, ref)
+
+
+@pytest.mark.parametrize("cin,cout,hw,n", [(4, 32, 64, 3), (32, 64, 32, 2), (64, 128, 16, 3), (128, 256, 8, 4)])
+def test_wgrad_matches_autograd(cin, cout, hw, n):
+    C = ops._ext()
+    torch.manual_seed(0)
+    x = torch.randn(n, cin, hw, hw, device=DEV)
+    w = (torch.randn(cout, cin, 4, 4, device=DEV) * 0.1).requires_grad_(True)
+    y = F.conv2d(x, w, stride=2, padding=1)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    dw = C.conv_wgrad(_nhwc(g), _nhwc(x), cin)
+    _close(dw, w.grad, rtol=5e-4, atol=5e-4)
+
+
+def test_up_small_matches_conv_transpose():
+    C = ops._ext()
+    torch.manual_seed(0)
+    x = torch.randn(2, 32, 32, 32, device=DEV)
+    w = torch.randn(32, 3, 4, 4, device=DEV) * 0.1
+    b = torch.randn(3, device=DEV)
+    ref = F.conv_transpose2d(x, w, b, stride=2, padding=1) + 0.5
+    out = C.conv_up_small(_nhwc(x), w, b, 0.5)
+    _close(out, ref)
+
+
+def _encoder_decoder(mult=32):
+    from sheeprl_prey_amd.algos.dreamer_v3.agent import CNNDecoder, CNNEncoder
+
+    torch.manual_seed(0)
+    enc = CNNEncoder(["rgb"], [3], (64, 64), mult).to(DEV)
+    dec = CNNDecoder(["rgb"], [3], mult, 96, enc.output_dim, (64, 64)).to(DEV)
+    with torch.no_grad():  # non-trivial LN affine parameters
+        for m in list(enc.modules()) + list(dec.modules()):
+            if isinstance(m, torch.nn.LayerNorm):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    return enc, dec
+
+
+def _run(enc, dec, x, lat, g_e, g_d, fused):
+    ops.set_fused(fused)
+    try:
+        for p in list(enc.parameters()) + list(dec.parameters()):
+            p.grad = None
+        lat = lat.detach().clone().requires_grad_(True)
+        e = enc({"rgb": x})
+        r = dec(lat)["rgb"]
+        ((e * g_e).sum() + (r * g_d).sum()).backward()
+        grads = {n: p.grad.clone() for n, p in list(enc.named_parameters()) + [("d." + k, v) for k, v in dec.named_parameters()]}
+        return e.detach(), r.detach(), lat.grad.clone(), grads
+    finally:
+        ops.set_fused(True)
+
+
+@pytest.mark.parametrize("lead", [(6,), (3, 2)])
+def test_encoder_decoder_stacks_match_eager(lead):
+    enc, dec = _encoder_decoder()
+    assert conv_ops.encoder_spec(enc.model, (64, 64), 3) is not None
+    assert conv_ops.decoder_spec(dec.model, 3) is not None
+    x = torch.rand(*lead, 3, 64, 64, device=DEV)
+    lat = torch.randn(*lead, 96, device=DEV)
+    g_e = torch.randn(*lead, enc.output_dim, device=DEV)
+    g_d = torch.randn(*lead, 3, 64, 64, device=DEV)
+    e1, r1, dl1, gr1 = _run(enc, dec, x, lat, g_e, g_d, True)
+    e0, r0, dl0, gr0 = _run(enc, dec, x, lat, g_e, g_d, False)
+    _close(e1, e0)
+    _close(r1, r0)
+    _close(dl1, dl0, rtol=5e-4, atol=5e-4)
+    for k in gr0:
+        _close(gr1[k], gr0[k], rtol=1e-3, atol=1e-3)
+
+
+def test_stack_ineligible_falls_back():
+    enc, _ = _encoder_decoder(mult=4)  # channels 4..32: not on the fused path
+    assert conv_ops.encoder_spec(enc.model, (64, 64), 3) is None
+    out = enc({"rgb": torch.rand(2, 3, 64, 64, device=DEV)})
+    assert out.shape == (2, enc.output_dim)
