@@ -29,6 +29,8 @@ import torch.distributed as dist
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--algo", default="dreamer_v3", choices=["dreamer_v3", "ppo"],
+                   help="dreamer_v3: the headline DV3 Atari-100k bench; ppo: PPO CartPole-v1 (exp=ppo) steps/sec")
     p.add_argument("--steps", type=int, default=40)
     p.add_argument("--warmup", type=int, default=8)
     p.add_argument("--prefill", type=int, default=1024, help="random-action steps before training (learning_starts)")
@@ -51,6 +53,8 @@ def main():
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
                "--master-addr=127.0.0.1", "--master-port=29517", __file__] + sys.argv[1:]
         sys.exit(subprocess.call(cmd))
+    if args.algo == "ppo":
+        return bench_ppo(args)
 
     from sheeprl_prey_amd import ops
     from sheeprl_prey_amd.algos.common import action_info
@@ -225,6 +229,131 @@ def main():
             "policy_steps_per_s": round(policy_steps / elapsed, 3),
             "grad_steps_per_s": round(args.steps * world / elapsed, 3),
             "final_wm_loss": round(loss, 4),
+        }
+        print(json.dumps(rec), flush=True)
+    envs.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def bench_ppo(args):
+    """PPO coupled on CartPole-v1 (``exp=ppo``: 1 env per rank, rollout 128, 10 epochs, minibatch 64,
+    64-unit tanh MLPs).  One bench step = one PPO update: the 128-step rollout (policy forward +
+    env step + buffer add, per env step), GAE and the full update_epochs x minibatch optimisation.
+    value = whole-job policy steps/s."""
+    from sheeprl_prey_amd.algos.common import action_info
+    from sheeprl_prey_amd.algos.ppo.agent import PPOAgent
+    from sheeprl_prey_amd.algos.ppo.ppo import PPOPlayer, PPOTrainer
+    from sheeprl_prey_amd.config.compose import compose
+    from sheeprl_prey_amd.data.tensordict import TensorDict
+    from sheeprl_prey_amd.parallel.flat_optim import build_optimizer
+    from sheeprl_prey_amd.parallel.runner import Runner
+    from sheeprl_prey_amd.utils.env import make_env, make_vector_env
+    from sheeprl_prey_amd.utils.utils import dotdict, gae
+
+    overrides = ["exp=ppo", "mlp_keys.encoder=[state]", "env.sync_env=True", "fabric.accelerator=cuda",
+                 f"fabric.cuda_graphs={not args.no_graphs}",
+                 "metric.log_every=1000000000"] + list(args.overrides)
+    cfg = dotdict(compose(overrides))
+    cfg.pop("hydra", None)
+    runner = Runner(**{k: v for k, v in cfg.fabric.items()})
+    runner._init_distributed()
+    rank, world = runner.global_rank, runner.world_size
+    device = runner.device
+    runner.seed_everything(cfg.seed + rank)
+    ne = cfg.env.num_envs
+    envs = make_vector_env(cfg, [make_env(cfg, cfg.seed + rank * ne + i, rank * ne, None, "train", i) for i in range(ne)])
+    obs_space = envs.single_observation_space
+    is_continuous, _, actions_dim = action_info(envs.single_action_space)
+    obs_keys = list(cfg.cnn_keys.encoder) + list(cfg.mlp_keys.encoder)
+    agent = runner.setup_module(PPOAgent(actions_dim, obs_space, cfg.algo.encoder, cfg.algo.actor, cfg.algo.critic,
+                                         cfg.cnn_keys.encoder, cfg.mlp_keys.encoder, cfg.env.screen_size,
+                                         cfg.distribution, is_continuous))
+    optimizer = build_optimizer(cfg.algo.optimizer, agent.parameters())
+    player = PPOPlayer(agent, cfg, is_continuous, enabled=runner.cuda_graphs)
+    T = cfg.algo.rollout_steps
+    trainer = PPOTrainer(runner, agent, optimizer, cfg, T * ne)
+    # rollout staging: env-side arrays stay on the host (one H2D per rollout), policy outputs are
+    # copied into device rollout tensors; the obs for the next policy step goes H2D from pinned memory
+    o = envs.reset(seed=cfg.seed + rank)[0]
+    cur = {k: np.asarray(o[k], dtype=np.float32) for k in obs_keys}
+    obs_host = {k: np.zeros((T, ne) + cur[k].shape[1:], np.float32) for k in obs_keys}
+    rew_host = np.zeros((T, ne, 1), np.float32)
+    done_host = np.zeros((T, ne, 1), np.float32)
+    pinned = {k: torch.empty(cur[k].shape, dtype=torch.float32).pin_memory() for k in obs_keys}
+    obs_dev = {k: torch.empty(cur[k].shape, dtype=torch.float32, device=device) for k in obs_keys}
+    buf = {n: torch.zeros(T, ne, d, device=device) for n, d in (("actions", sum(actions_dim) if not is_continuous
+                                                                    else actions_dim[0]), ("logprobs", 1), ("values", 1))}
+    returns_seen = []
+
+    def update():
+        nonlocal cur
+        for t in range(T):
+            for k in obs_keys:
+                obs_host[k][t] = cur[k]
+                pinned[k].numpy()[...] = cur[k]
+                obs_dev[k].copy_(pinned[k], non_blocking=True)
+            pout = player(obs_dev)
+            for n in buf:
+                buf[n][t].copy_(pout[n])
+            real = pout["real"].cpu().numpy()
+            o, r, d, tr, info = envs.step(real.reshape(envs.action_space.shape))
+            rew_host[t, :, 0] = r
+            done_host[t, :, 0] = np.logical_or(d, tr)
+            cur = {k: np.asarray(o[k], dtype=np.float32) for k in obs_keys}
+            if "final_info" in info:
+                for ep in info["final_info"]:
+                    if ep is not None and "episode" in ep:
+                        returns_seen.append(float(np.asarray(ep["episode"]["r"]).reshape(-1)[0]))
+        data = {k: torch.from_numpy(obs_host[k]).to(device, non_blocking=True) for k in obs_keys}
+        data["rewards"] = torch.from_numpy(rew_host).to(device, non_blocking=True)
+        data["dones"] = torch.from_numpy(done_host).to(device, non_blocking=True)
+        data.update({n: v for n, v in buf.items()})
+        with torch.no_grad():
+            nv = agent.get_value({k: torch.from_numpy(cur[k]).to(device) for k in obs_keys})
+            ret, adv = gae(data["rewards"], data["values"], data["dones"], nv, T, cfg.algo.gamma, cfg.algo.gae_lambda)
+        data["returns"], data["advantages"] = ret.float(), adv.float()
+        trainer(TensorDict({k: v.reshape(T * ne, *v.shape[2:]) for k, v in data.items()}, batch_size=[T * ne]), None)
+
+    for _ in range(args.warmup):
+        update()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        update()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    policy_steps = args.steps * cfg.algo.rollout_steps * ne * world
+    if rank == 0:
+        rec = {
+            "metric": "PPO CartPole-v1 policy steps/sec (whole node)",
+            "value": round(policy_steps / elapsed, 3),
+            "unit": "policy_steps/s (whole job)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "CartPole-v1 dynamics (native env), random-init weights",
+            "config": {"model": "PPO MLP 2x64 tanh (exp=ppo)", "global_batch": cfg.per_rank_batch_size * world,
+                       "rollout_steps": cfg.algo.rollout_steps, "num_envs_per_rank": ne,
+                       "update_epochs": cfg.algo.update_epochs, "parallelism": f"dp{world}",
+                       "hipgraph": bool(trainer.graphed.enabled)},
+            "mean_episode_return": round(float(np.mean(returns_seen[-20:])), 2) if returns_seen else None,
         }
         print(json.dumps(rec), flush=True)
     envs.close()

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import copy
 import os
-from typing import Any, Dict
+from typing import Any, Dict, Optional
 
 import numpy as np
 import torch
@@ -39,6 +39,8 @@ from sheeprl_prey_amd.utils.utils import gae, normalize_tensor, polynomial_decay
 
 
 def train(runner, agent, optimizer, data: TensorDict, aggregator: MetricAggregator, cfg: Dict[str, Any]) -> None:
+    """Eager update_epochs x minibatch SGD (reference ``ppo.py:32-104``); see ``PPOTrainer`` for the
+    captured single-rank form used on GPU."""
     n = data.shape[0]
     obs_keys = list(cfg.mlp_keys.encoder) + list(cfg.cnn_keys.encoder)
     for epoch in range(cfg.algo.update_epochs):
@@ -49,24 +51,105 @@ def train(runner, agent, optimizer, data: TensorDict, aggregator: MetricAggregat
         idx = idx.to(data["rewards"].device)
         for start in range(0, len(idx), cfg.per_rank_batch_size):
             batch = data[idx[start : start + cfg.per_rank_batch_size]]
-            obs = {k: batch[k] / 255 - 0.5 if k in cfg.cnn_keys.encoder else batch[k] for k in obs_keys}
-            _, logprobs, entropy, new_values = agent(obs, torch.split(batch["actions"], agent.actions_dim, dim=-1))
-            adv = batch["advantages"]
-            if cfg.algo.normalize_advantages:
-                adv = normalize_tensor(adv)
-            pg_loss = policy_loss(logprobs, batch["logprobs"], adv, cfg.algo.clip_coef, cfg.algo.loss_reduction)
-            v_loss = value_loss(new_values, batch["values"], batch["returns"], cfg.algo.clip_coef, cfg.algo.clip_vloss,
-                                cfg.algo.loss_reduction)
-            ent_loss = entropy_loss(entropy, cfg.algo.loss_reduction)
-            loss = pg_loss + cfg.algo.vf_coef * v_loss + cfg.algo.ent_coef * ent_loss
-            optimizer.zero_grad(set_to_none=True)
-            runner.backward(loss, optimizer)
-            if cfg.algo.max_grad_norm > 0.0:
-                runner.clip_gradients(agent, optimizer, max_norm=cfg.algo.max_grad_norm)
-            optimizer.step()
-            aggregator.update("Loss/policy_loss", pg_loss.detach())
-            aggregator.update("Loss/value_loss", v_loss.detach())
-            aggregator.update("Loss/entropy_loss", ent_loss.detach())
+            pg_loss, v_loss, ent_loss = _minibatch_step(runner, agent, optimizer, batch, obs_keys, cfg, cfg.algo.clip_coef,
+                                                        cfg.algo.ent_coef)
+            if aggregator is not None:
+                aggregator.update("Loss/policy_loss", pg_loss.detach())
+                aggregator.update("Loss/value_loss", v_loss.detach())
+                aggregator.update("Loss/entropy_loss", ent_loss.detach())
+
+
+def _minibatch_step(runner, agent, optimizer, batch, obs_keys, cfg, clip_coef, ent_coef):
+    obs = {k: batch[k] / 255 - 0.5 if k in cfg.cnn_keys.encoder else batch[k] for k in obs_keys}
+    _, logprobs, entropy, new_values = agent(obs, torch.split(batch["actions"], agent.actions_dim, dim=-1))
+    adv = batch["advantages"]
+    if cfg.algo.normalize_advantages:
+        adv = normalize_tensor(adv)
+    pg_loss = policy_loss(logprobs, batch["logprobs"], adv, clip_coef, cfg.algo.loss_reduction)
+    v_loss = value_loss(new_values, batch["values"], batch["returns"], clip_coef, cfg.algo.clip_vloss, cfg.algo.loss_reduction)
+    ent_loss = entropy_loss(entropy, cfg.algo.loss_reduction)
+    loss = pg_loss + cfg.algo.vf_coef * v_loss + ent_coef * ent_loss
+    optimizer.zero_grad(set_to_none=True)
+    runner.backward(loss, optimizer)
+    if cfg.algo.max_grad_norm > 0.0:
+        runner.clip_gradients(agent, optimizer, max_norm=cfg.algo.max_grad_norm)
+    optimizer.step()
+    return pg_loss, v_loss, ent_loss
+
+
+class PPOTrainer:
+    """All ``update_epochs`` x minibatch steps of one PPO update as ONE hipGraph (single rank, GPU,
+    ``fabric.cuda_graphs``): permutations are drawn on device (``argsort`` of uniform keys), the
+    clip / entropy coefficients are device scalars refreshed before each replay (annealing works),
+    the loss means come back as graph outputs.  Multi-rank or ``anneal_lr`` runs use ``train``
+    (per-minibatch RCCL all-reduce; the flat Adam takes its lr as a launch argument)."""
+
+    def __init__(self, runner, agent, optimizer, cfg, n: int):
+        from sheeprl_prey_amd.parallel.graphs import GraphedStep
+
+        self.runner, self.agent, self.optimizer, self.cfg, self.n = runner, agent, optimizer, cfg, n
+        dev = runner.device
+        self.obs_keys = list(cfg.mlp_keys.encoder) + list(cfg.cnn_keys.encoder)
+        self.clip_t = torch.tensor(float(cfg.algo.clip_coef), device=dev)
+        self.ent_t = torch.tensor(float(cfg.algo.ent_coef), device=dev)
+        enabled = (dev.type == "cuda" and bool(getattr(runner, "cuda_graphs", False)) and runner.world_size == 1
+                   and not cfg.algo.anneal_lr)
+        self.graphed = GraphedStep(self._train, warmup=2, enabled=enabled, name="ppo_train")
+
+    def _train(self, data: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        cfg = self.cfg
+        n, bs = self.n, cfg.per_rank_batch_size
+        dev = data["rewards"].device
+        sums = torch.zeros(3, device=dev)
+        steps = 0
+        for _ in range(cfg.algo.update_epochs):
+            idx = torch.argsort(torch.rand(n, device=dev))
+            for start in range(0, n, bs):
+                sel = idx[start : start + bs]
+                batch = {k: v.index_select(0, sel) for k, v in data.items()}
+                pg, vl, el = _minibatch_step(self.runner, self.agent, self.optimizer, batch, self.obs_keys, cfg,
+                                             self.clip_t, self.ent_t)
+                sums = sums + torch.stack((pg.detach(), vl.detach(), el.detach()))
+                steps += 1
+        sums = sums / steps
+        return {"Loss/policy_loss": sums[0], "Loss/value_loss": sums[1], "Loss/entropy_loss": sums[2]}
+
+    def __call__(self, data: TensorDict, aggregator: Optional[MetricAggregator] = None) -> None:
+        if not self.graphed.enabled:
+            train(self.runner, self.agent, self.optimizer, data, aggregator, self.cfg)
+            return
+        self.clip_t.fill_(float(self.cfg.algo.clip_coef))
+        self.ent_t.fill_(float(self.cfg.algo.ent_coef))
+        out = self.graphed({k: data[k] for k in data.keys()})
+        if aggregator is not None:
+            for k, v in out.items():
+                aggregator.update(k, v.clone())
+
+
+class PPOPlayer:
+    """Rollout policy step (reference ``ppo.py:289-300``): forward + sampling, returning the one-hot
+    actions, env actions, log-probs and values.  With ``fabric.cuda_graphs`` on GPU the whole step
+    is one hipGraph replay (sampling via Philox, graph-safe); outputs are static buffers the caller
+    copies (``ReplayBuffer.add``) before the next call."""
+
+    def __init__(self, agent, cfg, is_continuous: bool, enabled: bool):
+        from sheeprl_prey_amd.parallel.graphs import GraphedStep
+
+        self.agent, self.cfg, self.is_continuous = agent, cfg, is_continuous
+        self.graphed = GraphedStep(self._step, warmup=2, enabled=enabled, name="ppo_player")
+
+    @torch.no_grad()
+    def _step(self, obs: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        nobs = {k: v / 255 - 0.5 if k in self.cfg.cnn_keys.encoder else v for k, v in obs.items()}
+        actions, logprobs, _, values = self.agent(nobs)
+        if self.is_continuous:
+            real = torch.cat(actions, -1)
+        else:
+            real = torch.stack([a.argmax(dim=-1) for a in actions], dim=-1)
+        return {"actions": torch.cat(actions, -1), "real": real, "logprobs": logprobs, "values": values}
+
+    def __call__(self, obs: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        return self.graphed(obs)
 
 
 @register_algorithm()
@@ -126,6 +209,8 @@ def main(runner, cfg: Dict[str, Any]):
         if state and state.get("scheduler"):
             scheduler.load_state_dict(state["scheduler"])
 
+    trainer = None
+    player = PPOPlayer(agent, cfg, is_continuous, enabled=device.type == "cuda" and bool(runner.cuda_graphs))
     o = envs.reset(seed=cfg.seed)[0]
     next_obs = {}
     for k in obs_keys:
@@ -141,14 +226,9 @@ def main(runner, cfg: Dict[str, Any]):
         for _ in range(cfg.algo.rollout_steps):
             policy_step += cfg.env.num_envs * world_size
             with timer("Time/env_interaction_time"):
-                with torch.no_grad():
-                    nobs = {k: next_obs[k] / 255 - 0.5 if k in cfg.cnn_keys.encoder else next_obs[k] for k in obs_keys}
-                    actions, logprobs, _, values = agent(nobs)
-                    if is_continuous:
-                        real_actions = torch.cat(actions, -1).cpu().numpy()
-                    else:
-                        real_actions = np.stack([a.argmax(dim=-1).cpu().numpy() for a in actions], axis=-1)
-                    actions = torch.cat(actions, -1)
+                pout = player({k: next_obs[k] for k in obs_keys})
+                actions, logprobs, values = pout["actions"], pout["logprobs"], pout["values"]
+                real_actions = pout["real"].cpu().numpy()
                 o, rewards, dones, truncated, info = envs.step(real_actions.reshape(envs.action_space.shape))
                 truncated_envs = np.nonzero(truncated)[0]
                 if len(truncated_envs) > 0:
@@ -205,7 +285,9 @@ def main(runner, cfg: Dict[str, Any]):
             n = next(iter(gathered.values())).shape[0] * local_data.shape[0]
             local_data = TensorDict({k: v.reshape(n, *v.shape[2:]) for k, v in gathered.items()}, batch_size=[n])
         with timer("Time/train_time"):
-            train(runner, agent, optimizer, local_data, aggregator, cfg)
+            if trainer is None or trainer.n != local_data.shape[0]:
+                trainer = PPOTrainer(runner, agent, optimizer, cfg, local_data.shape[0])
+            trainer(local_data, aggregator)
         train_step += world_size
 
         if cfg.algo.anneal_lr:

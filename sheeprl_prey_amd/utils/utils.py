@@ -83,8 +83,8 @@ def gae(
 
 
 def normalize_tensor(tensor: Tensor, eps: float = 1e-8, mask: Optional[Tensor] = None) -> Tensor:
-    if mask is None:
-        mask = torch.ones_like(tensor, dtype=torch.bool)
+    if mask is None:  # no boolean indexing: keeps the op free of host syncs (graph-capturable)
+        return (tensor - tensor.mean()) / (tensor.std() + eps)
     return (tensor - tensor[mask].mean()) / (tensor[mask].std() + eps)
 
 
