@@ -81,6 +81,7 @@ class FlatOptimizer:
         self.param_groups = [dict(params=self.params, lr=lr, weight_decay=weight_decay, **defaults)]
         self.defaults = dict(lr=lr, weight_decay=weight_decay, **defaults)
         self._advanced = False
+        self._detached = False  # grads live outside the slab until ``_gather`` (see zero_grad)
         self._init_state()
 
     def _shared_owner(self, plist: List[Tensor]):
@@ -122,17 +123,53 @@ class FlatOptimizer:
                 p.grad = self.flat_grad[off : off + p.numel()].view_as(p)
 
     def zero_grad(self, set_to_none: bool = True) -> None:
+        """``set_to_none`` (default): the next backward lets autograd hand each parameter its freshly
+        computed gradient (AccumulateGrad steals the buffer: no per-parameter accumulate kernel), and
+        the slab is rebuilt by ``_gather`` - one memset + multi-tensor copies - before anything reads
+        it.  Otherwise the slab is zeroed and grads accumulate into it in place."""
+        if set_to_none:
+            for p in self.params:
+                p.grad = None
+            self._detached = True
+            return
         self.flat_grad.zero_()
         self._relink()
+        self._detached = False
+
+    def _gather(self) -> None:
+        if not self._detached:
+            return
+        self._detached = False
+        views, grads, missing, in_slab = [], [], [], False
+        for p, off in zip(self.params, self.offsets):
+            v = self.flat_grad[off : off + p.numel()].view_as(p)
+            g = p.grad
+            if g is None:
+                missing.append(v)
+            elif g.data_ptr() != v.data_ptr():
+                views.append(v)
+                grads.append(g if g.dtype == v.dtype else g.to(v.dtype))
+            else:
+                in_slab = True
+            p.grad = v
+        if missing:
+            if in_slab:
+                torch._foreach_zero_(missing)
+            else:
+                self.flat_grad.zero_()  # one memset (also clears the alignment padding)
+        if grads:
+            torch._foreach_copy_(views, grads)
 
     def clip_grad_norm_(self, max_norm: float) -> Tensor:
         from sheeprl_prey_amd import ops
 
+        self._gather()
         norm = ops.flat_grad_norm(self.flat_grad, self.scalars, float(max_norm))
         self._advanced = True
         return norm
 
     def all_reduce_grads(self, group=None, world_size: int = 1, bucket_mb: int = 32) -> None:
+        self._gather()
         if world_size <= 1:
             return
         g = self.flat_grad
@@ -152,6 +189,7 @@ class FlatOptimizer:
     def step(self, closure=None):
         from sheeprl_prey_amd import ops
 
+        self._gather()
         if not self._advanced:
             ops.flat_advance(self.scalars)
         self._advanced = False
