@@ -265,6 +265,65 @@ class RSSM(nn.Module):
         _, imagined_prior = self._transition(recurrent_state)
         return imagined_prior, recurrent_state
 
+    # ---- MI355X imagination: buffer-resident no-grad rollout ---------------------------
+    def imagine_fast_ok(self, actor) -> bool:
+        gru = self.recurrent_model.rnn
+        rec = list(self.recurrent_model.mlp.model)
+        return (isinstance(gru.layer_norm, nn.LayerNorm) and isinstance(rec[0], nn.Linear)
+                and type(actor) is Actor and not actor.is_continuous and ops.native_available() and ops.fused_enabled()
+                and gru.layer_norm.weight is not None and gru.layer_norm.bias is not None)
+
+    @torch.no_grad()
+    def imagine_discrete(self, post: Tensor, h: Tensor, actor: "Actor", horizon: int) -> Tuple[Tensor, Tensor]:
+        """Imagination rollout for discrete actors without autograd (reference loop: ``dreamer_v3.py:
+        235-257`` over ``RSSM.imagination`` + ``Actor.forward``; the discrete objective back-propagates
+        only through log-probs of detached actions, so no graph is needed).
+
+        Every step writes straight into one buffer ``[H+1, M, A + S + Hd]`` holding (action | prior |
+        h): the LN-GRU and unimix-sample kernels store into row-strided slices of it, the recurrent
+        GEMM reads (action | prior) in place (weight columns permuted once), the GRU input projection
+        is two GEMMs (feat, then h accumulated) instead of a concat.  No per-step concatenations and no
+        final stacks: the trajectories ``[H+1, M, S + Hd]`` and actions ``[H+1, M, A]`` are views."""
+        C = ops._ext()
+        M, S = post.shape
+        Hd = h.shape[1]
+        A = int(sum(actor.actions_dim))
+        buf = post.new_empty(horizon + 1, M, A + S + Hd)
+        buf[0, :, A:A + S].copy_(post)
+        buf[0, :, A + S:].copy_(h)
+        rec = list(self.recurrent_model.mlp.model)
+        rec_lin, rec_rest = rec[0], rec[1:]
+        W = rec_lin.weight  # columns: (prior | action)
+        Wp = torch.cat((W[:, S:], W[:, :S]), 1)  # columns: (action | prior)
+        gru = self.recurrent_model.rnn
+        Wg = gru.linear.weight  # columns: (h | feat)
+        WgT_h, WgT_f = Wg[:, :Hd].t(), Wg[:, Hd:].t()
+        ln = gru.layer_norm
+        disc = self.discrete
+        for t in range(horizon + 1):
+            out = actor.model(buf[t, :, A:])
+            c0 = 0
+            for head, a in zip(actor.mlp_heads, actor.actions_dim):
+                u = torch.rand(M, device=post.device)
+                C.unimix_sample_into(head(out), u, int(a), float(actor._unimix), buf[t, :, c0:c0 + a])
+                c0 += a
+            if t == horizon:
+                break
+            x = torch.mm(buf[t, :, :A + S], Wp.t())
+            if rec_lin.bias is not None:
+                x = x + rec_lin.bias
+            for m in rec_rest:
+                x = m(x)
+            gx = torch.mm(x, WgT_f)
+            gx.addmm_(buf[t, :, A + S:], WgT_h)
+            if gru.linear.bias is not None:
+                gx = gx + gru.linear.bias
+            C.ln_gru_into(gx, buf[t, :, A + S:], ln.weight, ln.bias, float(ln.eps), buf[t + 1, :, A + S:])
+            logits = self.transition_model(buf[t + 1, :, A + S:])
+            u = torch.rand(M * (S // disc), device=post.device)
+            C.unimix_sample_into(logits.contiguous(), u, disc, float(self.unimix), buf[t + 1, :, A:A + S])
+        return buf[:, :, A:], buf[:, :, :A]
+
     # ---- MI355X scan: T-step posterior rollout with hoisted GEMMs --------------------
     def _mlp_head(self, mlp: MLP, x_pre: Tensor) -> Tensor:
         """Finish an ``MLP(hidden=[h], out=o)`` whose first Linear output is ``x_pre``."""

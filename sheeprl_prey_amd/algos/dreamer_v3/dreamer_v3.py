@@ -230,18 +230,23 @@ class DreamerV3Trainer:
         with grad_ctx:
             prior = st["posteriors"].reshape(-1, S)
             h = st["recurrent_states"].reshape(-1, H)
-            latent = torch.cat((prior, h), -1)
-            trajectories: List[Tensor] = [latent]
-            actions = torch.cat(actor(latent.detach())[0], dim=-1)
-            imagined_actions: List[Tensor] = [actions]
-            for _ in range(cfg.algo.horizon):
-                prior, h = wm.rssm.imagination(prior, h, actions)
-                prior = prior.reshape(-1, S)
+            fast = (not self.is_continuous and prior.is_cuda and wm.rssm.imagine_fast_ok(actor))
+            if fast:
+                imagined_trajectories, imagined_actions_t = wm.rssm.imagine_discrete(prior, h, actor, cfg.algo.horizon)
+            else:
                 latent = torch.cat((prior, h), -1)
-                trajectories.append(latent)
+                trajectories: List[Tensor] = [latent]
                 actions = torch.cat(actor(latent.detach())[0], dim=-1)
-                imagined_actions.append(actions)
-            imagined_trajectories = torch.stack(trajectories)
+                imagined_actions: List[Tensor] = [actions]
+                for _ in range(cfg.algo.horizon):
+                    prior, h = wm.rssm.imagination(prior, h, actions)
+                    prior = prior.reshape(-1, S)
+                    latent = torch.cat((prior, h), -1)
+                    trajectories.append(latent)
+                    actions = torch.cat(actor(latent.detach())[0], dim=-1)
+                    imagined_actions.append(actions)
+                imagined_trajectories = torch.stack(trajectories)
+                imagined_actions_t = torch.stack(imagined_actions)
             predicted_values = ops.twohot_mean(critic(imagined_trajectories))
             predicted_rewards = ops.twohot_mean(wm.reward_model(imagined_trajectories))
             continues = (wm.continue_model(imagined_trajectories) > 0).to(predicted_values.dtype)
@@ -252,7 +257,7 @@ class DreamerV3Trainer:
         with torch.no_grad():
             st["discount"] = torch.cumprod(continues * cfg.algo.gamma, dim=0) / cfg.algo.gamma
         st["imagined_trajectories"] = imagined_trajectories
-        st["imagined_actions"] = torch.stack(imagined_actions)
+        st["imagined_actions"] = imagined_actions_t
         st["predicted_values"] = predicted_values
         st["lambda_values"] = lambda_values
 

@@ -28,11 +28,12 @@ int ln_nchw_splits(int, int);
 void launch_ln_nchw_bwd(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
                         float*, float*, float*, int, int, int, int, hipStream_t);
 bool launch_ln_gru_fwd(const float*, const float*, int, const float*, const float*, float*, float*, float*, int, int, float,
-                       hipStream_t);
+                       hipStream_t, int ldo = 0);
 int ln_gru_bwd_grid(int);
 bool launch_ln_gru_bwd(const float*, const float*, int, const float*, const float*, const float*, const float*, const float*,
                        float*, float*, float*, float*, float*, float*, int, int, hipStream_t);
-bool launch_unimix_sample_fwd(const float*, const float*, float*, float*, int, int, float, hipStream_t);
+bool launch_unimix_sample_fwd(const float*, const float*, float*, float*, int, int, float, hipStream_t, int G = 0,
+                              int lds = 0);
 bool launch_unimix_sample_bwd(const float*, const float*, const float*, float*, int, int, float, hipStream_t);
 bool launch_twohot_nll_fwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
 bool launch_twohot_nll_bwd(const float*, const float*, const float*, const float*, float*, int, int, hipStream_t);
@@ -535,10 +536,43 @@ int64_t scan4_lds(int64_t S, int64_t D, int64_t H, int64_t hid) {
 
 }  // namespace
 
+// ------------------------------------------------------------------ strided-output (no-grad) forms
+// Write into a caller-owned row-strided view (e.g. a slice of an imagination trajectory buffer):
+// out must have unit stride in its last dim; rows may be strided.
+void ln_gru_into(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::Tensor beta, double eps, torch::Tensor out) {
+  check_f32(x, "x");
+  check_f32(gamma, "gamma");
+  check_f32(beta, "beta");
+  TORCH_CHECK(h.is_cuda() && h.dim() == 2 && h.stride(1) == 1 && out.dim() == 2 && out.stride(1) == 1,
+              "ln_gru_into: h/out must be row-strided 2-D views");
+  const int H = h.size(1), M = h.size(0);
+  TORCH_CHECK(x.numel() == (int64_t)M * 3 * H && out.size(0) == M && out.size(1) == H, "ln_gru_into: shapes");
+  auto mean = torch::empty({M}, x.options());
+  auto rstd = torch::empty({M}, x.options());
+  bool ok = launch_ln_gru_fwd(x.data_ptr<float>(), h.data_ptr<float>(), h.stride(0), gamma.data_ptr<float>(),
+                              beta.data_ptr<float>(), out.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                              M, H, (float)eps, cur_stream(), out.stride(0));
+  TORCH_CHECK(ok, "ln_gru_into: unsupported hidden size ", H);
+}
+
+void unimix_sample_into(torch::Tensor logits, c10::optional<torch::Tensor> uniform, int64_t classes, double alpha,
+                        torch::Tensor out) {
+  check_f32(logits, "logits");
+  TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.stride(1) == 1, "unimix_sample_into: out must be a row-strided 2-D view");
+  const int C = classes, N = out.size(1), M = out.size(0);
+  TORCH_CHECK(N % C == 0 && logits.numel() == (int64_t)M * N, "unimix_sample_into: shapes");
+  const int R = M * (N / C);
+  bool ok = launch_unimix_sample_fwd(logits.data_ptr<float>(), opt_ptr(uniform), nullptr, out.data_ptr<float>(), R, C,
+                                     (float)alpha, cur_stream(), N / C, out.stride(0));
+  TORCH_CHECK(ok, "unimix_sample_into: classes must be <= 64");
+}
+
 void register_conv(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_conv(m);
+  m.def("ln_gru_into", &ln_gru_into);
+  m.def("unimix_sample_into", &unimix_sample_into);
   m.doc() = "sheeprl_prey_amd HIP kernels (gfx950)";
   m.def("flat_grad_norm", &flat_grad_norm);
   m.def("flat_advance", &flat_advance);

@@ -36,7 +36,7 @@ __device__ __forceinline__ int seg_argmax(float v, int idx, int width) {
 __global__ void __launch_bounds__(256) unimix_sample_fwd_kernel(const float* __restrict__ logits,
                                                                 const float* __restrict__ uniform,
                                                                 float* __restrict__ mixed, float* __restrict__ sample,
-                                                                int R, int C, int W, float alpha) {
+                                                                int R, int C, int W, float alpha, int G, int lds) {
   const int lane = threadIdx.x & 63;
   const int seg_per_wave = 64 / W;
   const int gwave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -72,8 +72,10 @@ __global__ void __launch_bounds__(256) unimix_sample_fwd_kernel(const float* __r
     pick = seg_argmax(valid ? p : -1.f, k, W);
   }
   if (valid) {
-    mixed[off] = m;
-    sample[off] = (k == pick) ? 1.f : 0.f;
+    if (mixed) mixed[off] = m;
+    // sample rows may be strided: G categoricals per row, row stride lds (G*C when contiguous)
+    const int64_t so = (int64_t)(r / G) * lds + (int64_t)(r % G) * C + k;
+    sample[so] = (k == pick) ? 1.f : 0.f;
   }
 }
 
@@ -353,12 +355,16 @@ static int next_pow2(int c) {
 }
 
 bool launch_unimix_sample_fwd(const float* logits, const float* uniform, float* mixed, float* sample, int R, int C,
-                              float alpha, hipStream_t st) {
+                              float alpha, hipStream_t st, int G, int lds) {
   if (C > 64) return false;
+  if (G <= 0) {
+    G = 1;
+    lds = C;
+  }
   int W = next_pow2(C);
   int segs_per_block = 4 * (64 / W);
   hipLaunchKernelGGL(unimix_sample_fwd_kernel, dim3(cdiv(R, segs_per_block)), dim3(256), 0, st, logits, uniform, mixed,
-                     sample, R, C, W, alpha);
+                     sample, R, C, W, alpha, G, lds);
   return true;
 }
 

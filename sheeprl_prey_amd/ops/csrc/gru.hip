@@ -12,7 +12,8 @@ template <int MAXH>
 __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict__ x, const float* __restrict__ h, int ldh,
                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
                                                          float* __restrict__ hn, float* __restrict__ mean_out,
-                                                         float* __restrict__ rstd_out, int M, int H, float eps) {
+                                                         float* __restrict__ rstd_out, int M, int H, float eps,
+                                                         int ldo) {
   __shared__ float red[4];
   const int T = 256, N = 3 * H;
   for (int row = blockIdx.x; row < M; row += gridDim.x) {
@@ -51,7 +52,7 @@ __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict
         float c = tanhf(r * zc);
         float u = sigmoidf_(zu - 1.f);
         float hp = h[(int64_t)row * ldh + j];
-        hn[(int64_t)row * H + j] = u * c + (1.f - u) * hp;
+        hn[(int64_t)row * ldo + j] = u * c + (1.f - u) * hp;
       }
     }
     if (threadIdx.x == 0) {
@@ -151,14 +152,15 @@ static int gru_maxh(int H) {
 }
 
 bool launch_ln_gru_fwd(const float* x, const float* h, int ldh, const float* gamma, const float* beta, float* hn,
-                       float* mean, float* rstd, int M, int H, float eps, hipStream_t st) {
+                       float* mean, float* rstd, int M, int H, float eps, hipStream_t st, int ldo) {
+  if (ldo <= 0) ldo = H;
   int mh = gru_maxh(H);
   dim3 g(M < 8192 ? M : 8192), b(256);
   switch (mh) {
-    case 2: hipLaunchKernelGGL(ln_gru_fwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps); return true;
-    case 4: hipLaunchKernelGGL(ln_gru_fwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps); return true;
-    case 8: hipLaunchKernelGGL(ln_gru_fwd_kernel<8>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps); return true;
-    case 16: hipLaunchKernelGGL(ln_gru_fwd_kernel<16>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps); return true;
+    case 2: hipLaunchKernelGGL(ln_gru_fwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo); return true;
+    case 4: hipLaunchKernelGGL(ln_gru_fwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo); return true;
+    case 8: hipLaunchKernelGGL(ln_gru_fwd_kernel<8>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo); return true;
+    case 16: hipLaunchKernelGGL(ln_gru_fwd_kernel<16>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo); return true;
     default: return false;
   }
 }
