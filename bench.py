@@ -110,11 +110,11 @@ def main():
     step_data["dones"] = torch.zeros(cfg.env.num_envs, 1)
     step_data["rewards"] = torch.zeros(cfg.env.num_envs, 1)
     step_data["is_first"] = torch.ones(cfg.env.num_envs, 1)
+    player.use_graphs = runner.cuda_graphs
     player.init_states()
     obs = {k: step_data[k] for k in obs_keys}
 
-    def env_step(random_actions: bool):
-        nonlocal obs
+    def act_and_add(random_actions: bool):
         if random_actions:
             real = np.array(envs.action_space.sample())
             acts = np.concatenate([np.eye(d, dtype=np.float32)[a] for a, d in zip(real.reshape(len(actions_dim), -1), actions_dim)], -1)
@@ -126,6 +126,10 @@ def main():
                 real = np.array([x.argmax(-1).cpu().numpy() for x in a])
         step_data["actions"] = torch.from_numpy(np.asarray(acts)).view(cfg.env.num_envs, -1).float()
         rb.add(step_data[None, ...])
+        return real
+
+    def env_advance(real):
+        nonlocal obs
         o, r, d, tr, infos = envs.step(real.reshape(envs.action_space.shape))
         d = np.logical_or(d, tr)
         step_data["is_first"] = torch.zeros(cfg.env.num_envs, 1)
@@ -153,20 +157,25 @@ def main():
         return out
 
     for _ in range(max(args.prefill, cfg.per_rank_sequence_length + 1)):
-        env_step(True)
+        env_advance(act_and_add(True))
 
     env_ms = [0.0]
 
     def one_step():
+        # act (weights W_t) -> store the row -> launch the gradient step (async, W_t -> W_t+1) -> step
+        # the env on the CPU while the GPU trains (the env step needs only the action): the same
+        # order of effects as the reference's act / env-step / add / train loop
         if args.phase_times:
             torch.cuda.synchronize()
             t = time.perf_counter()
-            env_step(False)
+            real = act_and_add(False)
             torch.cuda.synchronize()
             env_ms[0] += (time.perf_counter() - t) * 1e3
         else:
-            env_step(False)
-        return train_once()
+            real = act_and_add(False)
+        out = train_once()
+        env_advance(real)
+        return out
 
     for _ in range(args.warmup):
         out = one_step()

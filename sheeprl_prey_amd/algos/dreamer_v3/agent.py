@@ -529,13 +529,24 @@ class PlayerDV3(nn.Module):
         self.discrete_size = discrete_size
         self.recurrent_state_size = recurrent_state_size
         self.num_envs = num_envs
+        # ``use_graphs``: each exploration step is one hipGraph replay (the ~60 small launches of
+        # encoder + RSSM step + actor collapse into one); (h, z, a) then live in fixed buffers that the
+        # graph updates in place, so resets must write into them (``init_states`` does).
+        self.use_graphs = False
+        self._graphed = None
 
     @torch.no_grad()
     def init_states(self, reset_envs: Optional[Sequence[int]] = None) -> None:
         if reset_envs is None or len(reset_envs) == 0:
-            self.actions = torch.zeros(1, self.num_envs, int(np.sum(self.actions_dim)), device=self.device)
-            self.recurrent_state = torch.tanh(torch.zeros(1, self.num_envs, self.recurrent_state_size, device=self.device))
-            self.stochastic_state = self.rssm._transition(self.recurrent_state, sample_state=False)[1].reshape(1, self.num_envs, -1)
+            actions = torch.zeros(1, self.num_envs, int(np.sum(self.actions_dim)), device=self.device)
+            h = torch.tanh(torch.zeros(1, self.num_envs, self.recurrent_state_size, device=self.device))
+            z = self.rssm._transition(h, sample_state=False)[1].reshape(1, self.num_envs, -1)
+            if self._graphed is not None:  # keep the captured buffers' addresses
+                self.actions.copy_(actions)
+                self.recurrent_state.copy_(h)
+                self.stochastic_state.copy_(z)
+            else:
+                self.actions, self.recurrent_state, self.stochastic_state = actions, h, z
         else:
             idx = torch.as_tensor(list(reset_envs), device=self.device)
             self.actions[:, idx] = 0
@@ -544,21 +555,48 @@ class PlayerDV3(nn.Module):
                 1, len(reset_envs), -1)
 
     def get_exploration_action(self, obs: Dict[str, Tensor], is_continuous: bool, mask=None) -> Tuple[Tensor, ...]:
+        if self.use_graphs and mask is None and torch.cuda.is_available() and self.actions.is_cuda:
+            if self._graphed is None:
+                from sheeprl_prey_amd.parallel.graphs import GraphedStep
+
+                self._is_continuous = is_continuous
+                self._expl_t = torch.zeros((), device=self.actions.device)
+                self._graphed = GraphedStep(self._graph_step, warmup=2, enabled=True, name="dv3_player")
+            self._expl_t.fill_(float(self.expl_amount))  # decayed amount: a device scalar the graph reads
+            out = self._graphed(obs)
+            return tuple(out[f"a{i}"] for i in range(len(out)))
+        return self._exploration_action(obs, is_continuous, mask)
+
+    @torch.no_grad()
+    def _graph_step(self, obs: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        bufs = (self.actions, self.recurrent_state, self.stochastic_state)
+        acts = self._exploration_action(obs, self._is_continuous, None, expl=self._expl_t)
+        for b, new in zip(bufs, (self.actions, self.recurrent_state, self.stochastic_state)):
+            b.copy_(new)
+        self.actions, self.recurrent_state, self.stochastic_state = bufs
+        return {f"a{i}": a for i, a in enumerate(acts)}
+
+    def _exploration_action(self, obs: Dict[str, Tensor], is_continuous: bool, mask=None,
+                            expl: Optional[Tensor] = None) -> Tuple[Tensor, ...]:
+        """``expl``: device-scalar exploration amount (graph path: always applied, a zero amount is
+        the identity); otherwise the Python ``expl_amount`` gates the exploration ops."""
         actions = self.get_greedy_action(obs, mask=mask)
+        amount = expl if expl is not None else self.expl_amount
+        explore = expl is not None or self.expl_amount > 0.0
         if is_continuous:
             self.actions = torch.cat(actions, -1)
-            if self.expl_amount > 0.0:
-                self.actions = torch.clip(Normal(self.actions, self.expl_amount).sample(), -1, 1)
-            expl = [self.actions]
+            if explore:  # Normal(a, expl) draw via randn (capturable)
+                self.actions = torch.clip(self.actions + amount * torch.randn_like(self.actions), -1, 1)
+            out = [self.actions]
         else:
-            expl = []
+            out = []
             for act in actions:
-                if self.expl_amount > 0.0:
+                if explore:
                     rnd = F.one_hot(torch.randint(0, act.shape[-1], act.shape[:-1], device=act.device), act.shape[-1]).to(act)
-                    act = torch.where(torch.rand(act.shape[:1], device=self.device).view(-1, *([1] * (act.dim() - 1))) < self.expl_amount, rnd, act)
-                expl.append(act)
-            self.actions = torch.cat(expl, -1)
-        return tuple(expl)
+                    act = torch.where(torch.rand(act.shape[:1], device=act.device).view(-1, *([1] * (act.dim() - 1))) < amount, rnd, act)
+                out.append(act)
+            self.actions = torch.cat(out, -1)
+        return tuple(out)
 
     def get_greedy_action(self, obs: Dict[str, Tensor], is_training: bool = True, mask=None) -> Sequence[Tensor]:
         embedded_obs = self.encoder(obs)

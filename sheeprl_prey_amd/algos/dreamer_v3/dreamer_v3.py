@@ -425,6 +425,7 @@ def main(runner, cfg: Dict[str, Any]):
     step_data["dones"] = torch.zeros(cfg.env.num_envs, 1)
     step_data["rewards"] = torch.zeros(cfg.env.num_envs, 1)
     step_data["is_first"] = torch.ones_like(step_data["dones"])
+    player.use_graphs = bool(runner.cuda_graphs) and cfg.algo.actor.cls.endswith(".Actor")
     player.init_states()
 
     per_rank_gradient_steps = 0

@@ -166,3 +166,32 @@ def test_imagine_discrete_matches_reference_loop():
     same_rows = (traj[:, :, :S] == ref_t[:, :, :S]).all(-1).all(0) & (acts == ref_a).all(-1).all(0)
     assert same_rows.float().mean() > 0.95, same_rows.float().mean()
     torch.testing.assert_close(traj[:, same_rows], ref_t[:, same_rows], rtol=1e-4, atol=1e-4)
+
+
+def test_player_graphed_steps_and_resets():
+    from sheeprl_prey_amd.algos.dreamer_v3.agent import PlayerDV3
+
+    tr = _build(graphs=True)
+    wm, actor = tr.world_model, tr.actor
+    player = PlayerDV3(wm.encoder, wm.rssm, actor, [5], 0.0, 3, 32, 64, torch.device("cuda"), discrete_size=32)
+    player.use_graphs = True
+    player.init_states()
+    h0 = player.recurrent_state.clone()
+    z0 = player.stochastic_state.clone()
+    buf_ptr = player.recurrent_state.data_ptr()
+    for _ in range(5):
+        obs = {"rgb": torch.rand(1, 3, 3, 64, 64, device="cuda")}
+        acts = player.get_exploration_action(obs, False)
+        a = acts[0]
+        assert a.shape == (1, 3, 5)
+        assert torch.all(a.sum(-1) == 1)
+    assert player._graphed is not None and player._graphed.graph is not None
+    assert player.recurrent_state.data_ptr() == buf_ptr, "state must stay in the captured buffers"
+    assert not torch.equal(player.recurrent_state, h0)
+    player.init_states([1])
+    torch.testing.assert_close(player.recurrent_state[:, 1], h0[:, 1])
+    torch.testing.assert_close(player.stochastic_state[:, 1], z0[:, 1])
+    assert torch.all(player.actions[:, 1] == 0)
+    player.init_states()
+    assert player.recurrent_state.data_ptr() == buf_ptr
+    torch.testing.assert_close(player.recurrent_state, h0)
