@@ -513,11 +513,17 @@ void set_scan4_prof(c10::optional<torch::Tensor> buf) {
   }
 }
 
-void scan4_fwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints, const std::vector<double>& fl) {
+void scan4_fwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints, const std::vector<double>& fl,
+               torch::Tensor WzT, torch::Tensor c0) {
   TORCH_CHECK(ts.size() == 32, "scan4_fwd: expects 32 tensors");
   auto p = scan4_params(ts, ints, fl);
   p.prof = g_scan4_prof;
   TORCH_CHECK(p.uni && p.z0 && p.logits && p.samples, "scan4_fwd: missing tensors");
+  check_f32(WzT, "WzT");
+  check_f32(c0, "c0");
+  TORCH_CHECK(WzT.size(0) == p.S && WzT.size(1) == p.D && c0.numel() == p.D, "scan4_fwd: WzT [S, D] / c0 [D]");
+  p.WzT = WzT.data_ptr<float>();
+  p.c0 = c0.data_ptr<float>();
   launch_scan4_fwd(p, cur_stream());
 }
 

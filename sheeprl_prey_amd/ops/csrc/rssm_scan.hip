@@ -406,6 +406,24 @@ __global__ void __launch_bounds__(NTH) f3_kernel(SP p, int t) {
   chunk(B * H, lo, hi);
   float* hs = p.hs + (size_t)t * B * H;
   for (int e = lo + threadIdx.x; e < hi; e += NTH) hs[e] = As[(e / H) * lda + e % H];
+  if (t + 1 < p.T) {
+    // step t+1's F1 work that does not need the posterior sample: the masked h half of its GRU input
+    // and the recurrent input xr[t+1] = a_proj[t+1] (+ z0 Wz^T for reset rows); F4 adds z_t Wz^T
+    const float* first1 = p.first + (size_t)(t + 1) * B;
+    float* cat1 = p.cat + (size_t)(t + 1) * B * HD;
+    for (int e = lo + threadIdx.x; e < hi; e += NTH) {
+      const int b = e / H, j = e - b * H;
+      cat1[(size_t)b * HD + j] = (1.f - first1[b]) * As[b * lda + j];
+    }
+    int lo2, hi2;
+    chunk(B * p.D, lo2, hi2);
+    const float* ap = p.a_proj + (size_t)(t + 1) * B * p.D;
+    float* xr1 = p.xr + (size_t)(t + 1) * B * p.D;
+    for (int e = lo2 + threadIdx.x; e < hi2; e += NTH) {
+      const int b = e / p.D, j = e - b * p.D;
+      xr1[e] = ap[e] + first1[b] * p.c0[j];
+    }
+  }
   STAMP(2, 3);
   gemm16<1, 4>(wt, As, lda, p.W1 + (size_t)n0 * K, K, K, red, ct);
   STAMP(2, 4);
@@ -495,6 +513,30 @@ __global__ void __launch_bounds__(NTH) f4_kernel(SP p, int t) {
       p.logits[o] = l;
       p.mixed[o] = m;
       p.samples[o] = (k == pick) ? 1.f : 0.f;
+    }
+    if (g == 1 && t + 1 < T) {
+      // posterior z_t feeds step t+1: masked copy zm[t+1], and its selected rows go to the LDS list
+      const float f1 = valid ? p.first[(size_t)(t + 1) * B + b] : 1.f;
+      if (valid) {
+        const size_t o = ((size_t)(t + 1) * B + b) * S + n0 + c;
+        p.zm[o] = (1.f - f1) * (k == pick ? 1.f : 0.f) + f1 * p.z0[n0 + c];
+      }
+      // [16 rows][32 / C groups]: selected WzT row, -1 = reset row (is_first is binary) / padding row
+      int* sel = (int*)red;
+      if (k == 0) sel[b * (32 / C) + c / C] = (valid && f1 == 0.f) ? n0 + (c - k) + pick : -1;
+    }
+  }
+  if (g == 1 && t + 1 < T) {
+    // xr[t+1][b][:] += WzT[sel][:] for every (row, group) of this workgroup: one coalesced row gather
+    // + no-return atomics per pair (the 32 / C group workgroups of a row add into the same row)
+    __syncthreads();
+    const int* sel = (const int*)red;
+    const int npair = 16 * (32 / C), D = p.D;
+    float* xr1 = p.xr + (size_t)(t + 1) * B * D;
+    for (int e = threadIdx.x; e < npair * D; e += NTH) {
+      const int pr = e / D, j = e - pr * D;
+      const int row = sel[pr];
+      if (row >= 0) atomicAdd(xr1 + (size_t)(pr / (32 / C)) * D + j, p.WzT[(size_t)row * D + j]);
     }
   }
   STAMP(3, 5);
@@ -871,7 +913,8 @@ void launch_scan4_fwd(const SP& p, hipStream_t st) {
   }
   const Lds l = scan4_lds_sizes(p.S, p.D, p.H, p.hid);
   for (int t = 0; t < p.T; ++t) {
-    hipLaunchKernelGGL(f1_kernel, dim3(p.D / 16), dim3(NTH), l.f1, st, p, t);
+    // F1 only starts the scan: later steps get xr / masked z / masked h from F3 and F4 of step t-1
+    if (t == 0) hipLaunchKernelGGL(f1_kernel, dim3(p.D / 16), dim3(NTH), l.f1, st, p, t);
     hipLaunchKernelGGL(f2_kernel, dim3(3 * p.H / 16), dim3(NTH), l.f2, st, p, t);
     hipLaunchKernelGGL(f3_kernel, dim3(2 * p.hid / 16), dim3(NTH), l.f3, st, p, t);
     hipLaunchKernelGGL(f4_kernel, dim3(2 * p.S / 32), dim3(NTH), l.f4, st, p, t);

@@ -15,6 +15,9 @@ struct SP {
   // backward
   const float *WzT, *WgT, *W1T, *W2T, *dpost, *dmixed;
   float *DH, *dlog, *dv, *du, *dgx, *dx, *dcat, *dhp, *p1g, *p1b, *pgg, *pgb, *p2g, *p2b;
+  // forward: z0 Wz^T (the recurrent input of a reset row), so F4 can fold the one-hot posterior
+  // into the next step's recurrent input by row gathers of WzT instead of an F1 GEMM launch
+  const float* c0;
   // optional phase timestamps (block 0, thread 0): prof[kernel * 16 + phase] = s_memtime
   long long* prof;
 };

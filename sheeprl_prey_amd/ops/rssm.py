@@ -182,8 +182,10 @@ class RSSMScan4Fn(torch.autograd.Function):
                e(T, B, 2 * hid), e(2, T, B, hid), e(T, 2 * B), e(T, 2 * B), e(2, T, B, S), e(2, T, B, S), e(2, T, B, S)]
         dims = [T, B, S, D, H, hid, disc, act1, act2]
         fl = [alpha, eps1, epsg, eps2]
-        C.scan4_fwd(fwd, dims, fl)
-        ctx.save_for_backward(*fwd[:32])
+        WzT = Wz_c.t().contiguous()
+        c0 = torch.mv(Wz_c, z0.reshape(-1))  # recurrent input of a reset row
+        C.scan4_fwd(fwd, dims, fl, WzT, c0)
+        ctx.save_for_backward(*fwd[:32], WzT)
         ctx.dims, ctx.fl = dims, fl
         hs, mixed, samples = fwd[24], fwd[30], fwd[31]
         return hs, samples[1], mixed[1], mixed[0]
@@ -194,6 +196,7 @@ class RSSMScan4Fn(torch.autograd.Function):
 
         C = _ext()
         fwd = list(ctx.saved_tensors)
+        WzT = fwd.pop()
         T, B, S, D, H, hid = ctx.dims[:6]
         dev, f32 = fwd[0].device, torch.float32
         e = lambda *shape: torch.empty(*shape, device=dev, dtype=f32)  # noqa: E731
@@ -207,7 +210,7 @@ class RSSMScan4Fn(torch.autograd.Function):
         dpost = d_post.contiguous() if d_post is not None else torch.empty(0, device=dev, dtype=f32)
         dlog, dv, du, dgx, dx = e(2, T, B, S), e(2, T, B, hid), e(T, B, 2 * hid), e(T, B, 3 * H), e(T, B, D)
         p1g, p1b, pgg, pgb, p2g, p2b = e(T, D), e(T, D), e(T, 3 * H), e(T, 3 * H), e(T, 2 * hid), e(T, 2 * hid)
-        bwd = [Wz.t().contiguous(), Wg.t().contiguous(), W1.t().contiguous(), W2.transpose(1, 2).contiguous(), dpost,
+        bwd = [WzT, Wg.t().contiguous(), W1.t().contiguous(), W2.transpose(1, 2).contiguous(), dpost,
                dmixed, DH, dlog, dv, du, dgx, dx, e(B, H + D), e(B, H), p1g, p1b, pgg, pgb, p2g, p2b]
         C.scan4_bwd(fwd + bwd, ctx.dims, ctx.fl)
         cat, zm, hs, v = fwd[16], fwd[17], fwd[24], fwd[26]
