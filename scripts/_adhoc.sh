@@ -2,7 +2,4 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -3 gpurun_out/pytest_gpu.log
-if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 300 python bench.py --steps 30 --warmup 6 > gpurun_out/bench.log 2>&1; rc=$?
-tail -1 gpurun_out/bench.log
 exit $rc

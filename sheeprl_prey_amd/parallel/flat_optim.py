@@ -27,6 +27,18 @@ from torch import Tensor
 _ALIGN = 4  # floats -> 16 B
 
 
+_LIVE: "weakref.WeakSet[FlatOptimizer]" = weakref.WeakSet()
+
+
+def gather_all_pending() -> None:
+    """Rebuild every live optimiser's gradient slab whose grads still sit outside it (see
+    ``FlatOptimizer.zero_grad``).  ``SegmentedGraph`` calls this at the end of each captured phase,
+    so the copies are recorded in the phase that ran the backward - before the eager RCCL
+    all-reduce that follows it between graph replays."""
+    for opt in list(_LIVE):
+        opt._gather()
+
+
 def _aligned(n: int) -> int:
     return (n + _ALIGN - 1) // _ALIGN * _ALIGN
 
@@ -82,6 +94,7 @@ class FlatOptimizer:
         self.defaults = dict(lr=lr, weight_decay=weight_decay, **defaults)
         self._advanced = False
         self._detached = False  # grads live outside the slab until ``_gather`` (see zero_grad)
+        _LIVE.add(self)
         self._init_state()
 
     def _shared_owner(self, plist: List[Tensor]):

@@ -14,6 +14,8 @@ from typing import Any, Callable, Dict, Optional
 import torch
 from torch import Tensor
 
+from sheeprl_prey_amd.parallel.flat_optim import gather_all_pending
+
 
 class GraphedStep:
     def __init__(self, fn: Callable[[Dict[str, Tensor]], Dict[str, Tensor]], warmup: int = 2, enabled: bool = True,
@@ -137,6 +139,9 @@ class SegmentedGraph:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool):
                 out = ph(self.static_in)
+                # grads handed over by autograd must reach the flat slabs INSIDE this phase's graph:
+                # the collective after it runs eagerly between replays
+                gather_all_pending()
             pool = g.pool()
             graphs.append(g)
             if i < len(self.colls):
