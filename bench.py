@@ -208,6 +208,14 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    # data-parallel consistency: every rank must hold the same weights after the timed steps
+    spread = 0.0
+    if world > 1:
+        cs = torch.stack([o.flat_param.double().sum() for o in (wopt, aopt, copt)])
+        lo, hi = cs.clone(), cs.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        spread = float((hi - lo).abs().max().item())
     ms_per_step = elapsed / args.steps * 1e3
     policy_steps = args.steps * cfg.env.num_envs * world
     env_steps_per_s = policy_steps * cfg.env.action_repeat / elapsed
@@ -238,6 +246,7 @@ def main():
             "policy_steps_per_s": round(policy_steps / elapsed, 3),
             "grad_steps_per_s": round(args.steps * world / elapsed, 3),
             "final_wm_loss": round(loss, 4),
+            "dp_param_spread": spread,
         }
         print(json.dumps(rec), flush=True)
     envs.close()

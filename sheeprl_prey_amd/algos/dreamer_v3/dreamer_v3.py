@@ -155,7 +155,7 @@ class DreamerV3Trainer:
         self._st["gathered"] = self._gather_buf
         if dry:
             return
-        if lam.is_cuda:
+        if lam.is_cuda and self.runner.backend == "nccl":
             dist.all_gather_into_tensor(self._gather_buf, lam.detach().contiguous(), group=self.runner.group)
         else:
             dist.all_gather(list(self._gather_buf.unbind(0)), lam.detach().contiguous(), group=self.runner.group)

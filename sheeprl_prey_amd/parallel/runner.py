@@ -147,7 +147,12 @@ class Runner:
 
     @property
     def backend(self) -> str:
-        # On ROCm the "nccl" backend string IS RCCL.
+        # On ROCm the "nccl" backend string IS RCCL.  SRL_DIST_BACKEND=gloo forces gloo with GPU
+        # tensors (rehearsing the multi-rank GPU code path with several ranks on ONE GPU, where RCCL
+        # would refuse the duplicate device).
+        forced = os.environ.get("SRL_DIST_BACKEND")
+        if forced:
+            return forced
         return "nccl" if self.accelerator == "cuda" else "gloo"
 
     @property
@@ -165,7 +170,7 @@ class Runner:
             torch.cuda.set_device(self.device)
         if ws > 1 and not dist.is_initialized():
             kwargs = dict(backend=self.backend, timeout=datetime.timedelta(minutes=30))
-            if self.accelerator == "cuda":
+            if self.accelerator == "cuda" and self.backend == "nccl":
                 kwargs["device_id"] = self.device
             dist.init_process_group(**kwargs)
 
