@@ -17,6 +17,14 @@ from sheeprl_prey_amd import ops
 from sheeprl_prey_amd.utils.model import ArgsType, ModuleType, cnn_forward, create_layers, fuse_norm_act, miniblock
 
 
+class Linear(nn.Linear):
+    """``nn.Linear`` (same parameters and state_dict) whose GPU backward takes the bias gradient with
+    a parallel column-sum kernel (``ops.linear``)."""
+
+    def forward(self, input: Tensor) -> Tensor:
+        return ops.linear(input, self.weight, self.bias)
+
+
 class MLP(nn.Module):
     """``[Linear -> dropout -> norm -> act] * len(hidden_sizes) (-> Linear(output_dim))``."""
 
@@ -50,11 +58,11 @@ class MLP(nn.Module):
         model = []
         for i in range(num_layers):
             model += miniblock(
-                sizes[i], sizes[i + 1], nn.Linear, layer_args_list[i], dropout_layer_list[i], dropout_args_list[i],
+                sizes[i], sizes[i + 1], Linear, layer_args_list[i], dropout_layer_list[i], dropout_args_list[i],
                 norm_layer_list[i], norm_args_list[i], activation_list[i], act_args_list[i],
             )
         if output_dim is not None:
-            model += [nn.Linear(sizes[-1], output_dim)]
+            model += [Linear(sizes[-1], output_dim)]
         self._output_dim = output_dim or sizes[-1]
         self._model = fuse_norm_act(nn.Sequential(*model))
         self._flatten_dim = flatten_dim

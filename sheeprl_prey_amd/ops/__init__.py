@@ -67,6 +67,39 @@ def _act_code(act: str) -> int:
     return ACTS[a]
 
 
+# =============================================================== Linear (library GEMMs, column-sum bias grad)
+class _Linear(torch.autograd.Function):
+    """``F.linear`` whose backward takes the bias gradient with a row-split column-sum kernel
+    (``norm.hip: colsum1``): torch's dim-0 sum of a [15360, 255] two-hot head gradient ran 165 us on
+    gfx950 and rocBLAS gemv ~68 us; dX / dW are the usual two GEMMs (hipBLASLt); row-strided inputs
+    (views into the imagination trajectory buffer) are used in place."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return torch.nn.functional.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        g2 = gy.reshape(-1, gy.shape[-1])
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (g2 @ w).view(*gy.shape[:-1], w.shape[1])
+        if ctx.needs_input_grad[1]:
+            dw = g2.t() @ x.reshape(-1, x.shape[-1])
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = _ext().colsum(g2 if g2.stride(-1) == 1 else g2.contiguous())
+        return dx, dw, db
+
+
+def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None) -> Tensor:
+    if _native(x) and x.dtype == torch.float32 and x.dim() >= 2 and torch.is_grad_enabled():
+        return _Linear.apply(x, weight, bias)
+    return torch.nn.functional.linear(x, weight, bias)
+
+
 # =============================================================== LayerNorm + activation
 class _LNAct(torch.autograd.Function):
     @staticmethod

@@ -21,6 +21,10 @@ from torch import Tensor, nn
 
 _OK_CH = (32, 64, 128, 256)
 ENABLED = True  # A/B switch: False routes the stacks through the per-layer modules (MIOpen + LN kernels)
+# Below this many frames (e.g. the env-interaction player, one frame per env) the deepest stage has
+# too few output rows to fill the chip (E4: 16 rows per frame) and a single workgroup walks all of K:
+# MIOpen's per-layer kernels are faster there.
+MIN_FRAMES = 64
 
 
 def _C():

@@ -18,6 +18,7 @@ int ln_bwd_grid(int, int, int);
 bool launch_ln_act_bwd(const float*, int, const float*, int, float*, int, const float*, const float*, const float*,
                        const float*, float*, float*, float*, float*, int, int, int, int, hipStream_t);
 void launch_colsum2(const float*, const float*, float*, float*, int, int, int, hipStream_t);
+void launch_colsum1(const float*, int, float*, int, int, hipStream_t);
 void launch_rssm_mask_fwd(const float*, int, const float*, const float*, const float*, float*, int, float*, int, int, int,
                           hipStream_t);
 void launch_rssm_mask_bwd(const float*, int, const float*, int, const float*, const float*, float*, float*, int, int, int,
@@ -573,11 +574,21 @@ void unimix_sample_into(torch::Tensor logits, c10::optional<torch::Tensor> unifo
   TORCH_CHECK(ok, "unimix_sample_into: classes must be <= 64");
 }
 
+// column sums of a row-strided 2-D view [rows, N] (stride(1) == 1) -> [N]
+torch::Tensor colsum(torch::Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.dim() == 2 && x.stride(1) == 1,
+              "colsum: x must be a row-strided 2-D float32 GPU view");
+  auto out = torch::empty({x.size(1)}, x.options());
+  launch_colsum1(x.data_ptr<float>(), x.stride(0), out.data_ptr<float>(), x.size(0), x.size(1), cur_stream());
+  return out;
+}
+
 void register_conv(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_conv(m);
   m.def("ln_gru_into", &ln_gru_into);
+  m.def("colsum", &colsum);
   m.def("unimix_sample_into", &unimix_sample_into);
   m.doc() = "sheeprl_prey_amd HIP kernels (gfx950)";
   m.def("flat_grad_norm", &flat_grad_norm);

@@ -8,8 +8,8 @@
 //                here consecutive threads own consecutive pixels, so the C-strided reads coalesce).
 // Rows with N <= 2048 are processed one wave per row, 4 waves per block; wider rows use the whole
 // 256-thread block per row.  Backward recomputes x_hat from the saved (mu, rstd); dgamma/dbeta are
-// reduced deterministically (per-block partial rows -> column sums), optionally into per-call
-// "slots" so a time loop can defer the reduction to one kernel after the loop.
+// reduced as per-block partial rows -> column sums (row-split blocks + one atomic per column and
+// split), optionally into per-call "slots" so a time loop can defer the reduction to one kernel.
 #include "common.h"
 
 namespace srl {
@@ -240,27 +240,56 @@ __global__ void __launch_bounds__(256) ln_block_bwd_kernel(const float* __restri
 }
 
 // out_a[g*N + n] = sum_{p : p % G == g} pa[p, n]  (deterministic; 4 row-slices per 64 columns)
+// Column sums of two partial-row arrays: oa[g][n] = sum_{p = g (mod G)} pa[p][n] (same for b).
+// Grid (N/64 column blocks, G, S row splits): each block reduces its split with 4 row slices per
+// column, then adds into the (pre-zeroed) outputs with one atomic per column - the split keeps the
+// reduction parallel when there are few columns and many partial rows (e.g. 1024 x 512).
 __global__ void __launch_bounds__(256) colsum2_kernel(const float* __restrict__ pa, const float* __restrict__ pb,
                                                       float* __restrict__ oa, float* __restrict__ ob, int rows, int N,
                                                       int G) {
   __shared__ float sa[4][64], sb[4][64];
   const int n = blockIdx.x * 64 + (threadIdx.x & 63);
   const int slice = threadIdx.x >> 6;
-  const int g = blockIdx.y;
+  const int g = blockIdx.y, S = gridDim.z, s = blockIdx.z;
+  const int Rg = rows > g ? (rows - g + G - 1) / G : 0;  // partial rows of group g
+  const int j0 = (int)((int64_t)Rg * s / S), j1 = (int)((int64_t)Rg * (s + 1) / S);
   float a = 0.f, b = 0.f;
   if (n < N) {
-    for (int p = g + slice * G; p < rows; p += 4 * G) {
-      a += pa[(int64_t)p * N + n];
-      b += pb[(int64_t)p * N + n];
+    for (int j = j0 + slice; j < j1; j += 4) {
+      const int64_t p = (int64_t)g + (int64_t)G * j;
+      a += pa[p * N + n];
+      b += pb[p * N + n];
     }
   }
   sa[slice][threadIdx.x & 63] = a;
   sb[slice][threadIdx.x & 63] = b;
   __syncthreads();
   if (slice == 0 && n < N) {
-    int c = threadIdx.x & 63;
-    oa[(int64_t)g * N + n] = sa[0][c] + sa[1][c] + sa[2][c] + sa[3][c];
-    ob[(int64_t)g * N + n] = sb[0][c] + sb[1][c] + sb[2][c] + sb[3][c];
+    const int c = threadIdx.x & 63;
+    atomicAdd(oa + (int64_t)g * N + n, sa[0][c] + sa[1][c] + sa[2][c] + sa[3][c]);
+    atomicAdd(ob + (int64_t)g * N + n, sb[0][c] + sb[1][c] + sb[2][c] + sb[3][c]);
+  }
+}
+
+// Single-array column sum out[n] = sum_r x[r * ldx + n] (bias gradients: dY summed over rows),
+// same row-split + atomic layout as colsum2.
+__global__ void __launch_bounds__(256) colsum1_kernel(const float* __restrict__ x, int ldx, float* __restrict__ out,
+                                                      int rows, int N) {
+  __shared__ float sa[4][64];
+  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int slice = threadIdx.x >> 6;
+  const int S = gridDim.z, s = blockIdx.z;
+  const int j0 = (int)((int64_t)rows * s / S), j1 = (int)((int64_t)rows * (s + 1) / S);
+  float a = 0.f;
+  if (n < N) {
+#pragma unroll 4
+    for (int j = j0 + slice; j < j1; j += 4) a += x[(int64_t)j * ldx + n];
+  }
+  sa[slice][threadIdx.x & 63] = a;
+  __syncthreads();
+  if (slice == 0 && n < N) {
+    const int c = threadIdx.x & 63;
+    atomicAdd(out + n, sa[0][c] + sa[1][c] + sa[2][c] + sa[3][c]);
   }
 }
 
@@ -458,8 +487,23 @@ bool launch_ln_act_fwd(const float* x, int ldx, float* y, int ldy, const float* 
   return false;
 }
 
+void launch_colsum1(const float* x, int ldx, float* out, int rows, int N, hipStream_t st) {
+  hipMemsetAsync(out, 0, sizeof(float) * (size_t)N, st);
+  int S = cdiv(rows, 128);
+  if (S > 64) S = 64;
+  if (S < 1) S = 1;
+  hipLaunchKernelGGL(colsum1_kernel, dim3(cdiv(N, 64), 1, S), dim3(256), 0, st, x, ldx, out, rows, N);
+}
+
 void launch_colsum2(const float* pa, const float* pb, float* oa, float* ob, int rows, int N, int G, hipStream_t st) {
-  hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(N, 64), G), dim3(256), 0, st, pa, pb, oa, ob, rows, N, G);
+  // memset nodes + one kernel (graph-capturable); ~64 partial rows per split
+  hipMemsetAsync(oa, 0, sizeof(float) * (size_t)G * N, st);
+  hipMemsetAsync(ob, 0, sizeof(float) * (size_t)G * N, st);
+  const int Rg = cdiv(rows, G > 0 ? G : 1);
+  int S = cdiv(Rg, 64);
+  if (S > 32) S = 32;
+  if (S < 1) S = 1;
+  hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(N, 64), G, S), dim3(256), 0, st, pa, pb, oa, ob, rows, N, G);
 }
 
 // pdg/pdb: [grid*G, N] partial rows (required if gamma != null).  If dgamma != null the partials

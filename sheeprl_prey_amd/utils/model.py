@@ -121,6 +121,11 @@ class LayerNormChannelLast(nn.LayerNorm):
     def forward(self, x: Tensor) -> Tensor:
         if x.dim() != 4:
             raise ValueError(f"Input tensor must be 4D (NCHW), received {len(x.shape)}D instead: {x.shape}")
+        if x.is_cuda and x.shape[0] * x.shape[2] * x.shape[3] < 8192:
+            # few pixels (the env-interaction player): the per-pixel NCHW kernel is latency-bound
+            # there, one wave per pixel row over channels-last data is not
+            y = ops.ln_act(x.permute(0, 2, 3, 1).contiguous(), self.weight, self.bias, self.eps, self.act)
+            return y.permute(0, 3, 1, 2)
         if x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous():
             # NHWC storage (MIOpen's native conv layout): C is the innermost dim, a plain row LN
             y = ops.ln_act(x.permute(0, 2, 3, 1), self.weight, self.bias, self.eps, self.act)

@@ -99,8 +99,9 @@ def _run(enc, dec, x, lat, g_e, g_d, fused):
         ops.set_fused(True)
 
 
-@pytest.mark.parametrize("lead", [(6,), (3, 2)])
-def test_encoder_decoder_stacks_match_eager(lead):
+@pytest.mark.parametrize("lead", [(6,), (3, 2), (66,)])
+def test_encoder_decoder_stacks_match_eager(lead, monkeypatch):
+    monkeypatch.setattr(conv_ops, "MIN_FRAMES", 1)  # small batches normally go to MIOpen
     enc, dec = _encoder_decoder()
     assert conv_ops.encoder_spec(enc.model, (64, 64), 3) is not None
     assert conv_ops.decoder_spec(dec.model, 3) is not None

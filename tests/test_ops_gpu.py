@@ -192,3 +192,17 @@ def test_flat_adam_matches_torch(wd, decoupled, clip):
             o.step()
     for a, b in zip(m1.parameters(), m2.parameters()):
         _close(a, b, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("shape", [(37, 64), (4, 9, 128), (15360, 512)])
+@pytest.mark.parametrize("out_f", [255, 9, 1])
+def test_linear_gemv_bias_grad(shape, out_f):
+    torch.manual_seed(0)
+    x = torch.randn(*shape, device=DEV)
+    w = torch.randn(out_f, shape[-1], device=DEV) * 0.05
+    b = torch.randn(out_f, device=DEV)
+    out1, g1 = _grads(lambda a, c, d: ops.linear(a, c, d), x, w, b)
+    out0, g0 = _grads(lambda a, c, d: torch.nn.functional.linear(a, c, d), x, w, b)
+    _close(out1, out0)
+    for a, c in zip(g1, g0):
+        torch.testing.assert_close(a, c, rtol=1e-4, atol=1e-3)
