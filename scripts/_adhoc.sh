@@ -1,10 +1,5 @@
 set -o pipefail
-mkdir -p gpurun_out/trace
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 500 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace -o run -- \
-  python3 bench.py --steps 4 --warmup 4 --profile-steps 4 > gpurun_out/trace_bench.log 2>&1 || exit $?
-f=$(find gpurun_out/trace -name '*kernel_trace.csv' | head -1)
-python3 scripts/trace_step.py "$f" 4 > gpurun_out/step_seq.tsv
-python3 scripts/trace_window.py "$f" 4 80 > gpurun_out/trace_summary.md
-rm -f "$f"
-head -3 gpurun_out/trace_summary.md
+for i in 1 2; do
+timeout -k 10 300 python scripts/_bench_prev.py --steps 30 --warmup 6 2>&1 | tail -1 | cut -c1-150
+timeout -k 10 300 python bench.py --steps 30 --warmup 6 2>&1 | tail -1 | cut -c1-150
+done

@@ -165,10 +165,18 @@ class ReplayBuffer:
             idxes = idxes[-self._buffer_size :]
             data_to_store = data_to_store[len(data_to_store) - self._buffer_size :]
         self._ensure_storage(data_to_store)
-        idxes = idxes.to(self._first_device())
-        for k, v in data_to_store.items():
-            dst = self._buf._data[k]
-            dst[idxes] = v.to(dst.device, dst.dtype)
+        dev = self._first_device()
+        if dev.type != "cpu" and len(idxes) == next_pos - self._pos > 0:
+            # contiguous rows: a slice copy, no index upload
+            for k, v in data_to_store.items():
+                # pinned / device sources copy without blocking the host (stream-ordered); pageable
+                # host sources still copy synchronously, so callers may reuse them at once
+                self._buf._data[k][self._pos : next_pos].copy_(v, non_blocking=True)
+        else:
+            idxes = idxes.to(dev)
+            for k, v in data_to_store.items():
+                dst = self._buf._data[k]
+                dst[idxes] = v.to(dst.device, dst.dtype)
         if self._pos + data_len >= self._buffer_size:
             self._full = True
         self._pos = next_pos
