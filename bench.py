@@ -37,6 +37,10 @@ def parse():
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--eager-ops", action="store_true", help="route GPU ops through the eager reference (A/B only)")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--device-env", action="store_true",
+                   help="--algo ppo: step CartPole-v1 on the GPU (envs/device.py) and capture the whole rollout")
+    p.add_argument("--no-fused-rollout", action="store_true",
+                   help="PPO --device-env: graph-captured per-op rollout instead of the one-launch kernel")
     p.add_argument("--phase-times", action="store_true",
                    help="per-phase hipGraphs with event timing (diagnostic; adds syncs, not a bench number)")
     p.add_argument("overrides", nargs="*")
@@ -334,9 +338,33 @@ def bench_ppo(args):
         data["returns"], data["advantages"] = ret.float(), adv.float()
         trainer(TensorDict({k: v.reshape(T * ne, *v.shape[2:]) for k, v in data.items()}, batch_size=[T * ne]), None)
 
+    if args.device_env:
+        from sheeprl_prey_amd.algos.ppo.ppo import DeviceRollout, FusedCartPoleRollout
+        from sheeprl_prey_amd.envs.device import make_device_env
+
+        denv = make_device_env(cfg.env.id, ne, device, seed=cfg.seed + rank)
+        denv.reset()
+        if FusedCartPoleRollout.supported(agent, denv) and not args.no_fused_rollout:
+            drollout = FusedCartPoleRollout(agent, denv, cfg, seed=cfg.seed + rank)
+        else:
+            drollout = DeviceRollout(agent, denv, cfg, enabled=runner.cuda_graphs)
+
+        def update():  # noqa: F811  (device-env variant of the update above)
+            buf = drollout()
+            with torch.no_grad():
+                nv = agent.get_value({"state": denv.obs})
+                ret, adv = gae(buf["rewards"], buf["values"], buf["dones"], nv, T, cfg.algo.gamma, cfg.algo.gae_lambda)
+            data = dict(buf)
+            data["returns"], data["advantages"] = ret.float(), adv.float()
+            trainer(TensorDict({k: v.reshape(T * ne, *v.shape[2:]) for k, v in data.items()}, batch_size=[T * ne]), None)
+            rets, _ = drollout.finished_episodes()
+            returns_seen.extend(rets)
+
     for _ in range(args.warmup):
         update()
     torch.cuda.synchronize()
+    if args.profile_steps:
+        torch.cuda._sleep(1000)  # marker kernel for scripts/trace_window.py
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -366,11 +394,13 @@ def bench_ppo(args):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "CartPole-v1 dynamics (native env), random-init weights",
+            "data": ("CartPole-v1 dynamics stepped on the GPU (envs/device.py), random-init weights" if args.device_env
+                     else "CartPole-v1 dynamics (native host env), random-init weights"),
             "config": {"model": "PPO MLP 2x64 tanh (exp=ppo)", "global_batch": cfg.per_rank_batch_size * world,
                        "rollout_steps": cfg.algo.rollout_steps, "num_envs_per_rank": ne,
                        "update_epochs": cfg.algo.update_epochs, "parallelism": f"dp{world}",
-                       "hipgraph": bool(trainer.graphed.enabled)},
+                       "hipgraph": bool(trainer.graphed.enabled), "device_env": bool(args.device_env),
+                       "rollout": type(drollout).__name__ if args.device_env else "host"},
             "mean_episode_return": round(float(np.mean(returns_seen[-20:])), 2) if returns_seen else None,
         }
         print(json.dumps(rec), flush=True)

@@ -13,6 +13,7 @@ from typing import Any, Dict, Optional
 
 import numpy as np
 import torch
+from torch import nn
 
 from sheeprl_prey_amd.algos.common import (
     PolynomialLR,
@@ -150,6 +151,130 @@ class PPOPlayer:
 
     def __call__(self, obs: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         return self.graphed(obs)
+
+
+class DeviceRollout:
+    """The rollout loop (reference ``ppo.py:281-356``) against a device-resident env
+    (``envs/device.py``): ``rollout_steps`` x (policy forward + sampling, env step with autoreset,
+    truncation bootstrap ``r += V(final_obs)``, buffer writes) with no host round trip, captured as
+    ONE hipGraph (``fabric.cuda_graphs``) and replayed once per update.  Buffers are [T, N, ...]."""
+
+    def __init__(self, agent, env, cfg, enabled: bool):
+        from sheeprl_prey_amd.parallel.graphs import GraphedStep
+
+        self.agent, self.env, self.cfg = agent, env, cfg
+        T, N, dev = cfg.algo.rollout_steps, env.num_envs, env.device
+        A = int(sum(agent.actions_dim))
+        z = lambda *s: torch.zeros(*s, device=dev)  # noqa: E731
+        self.buf = {"state": z(T, N, 4), "actions": z(T, N, A), "logprobs": z(T, N, 1), "values": z(T, N, 1),
+                    "rewards": z(T, N, 1), "dones": z(T, N, 1)}
+        self.stats = {"done_ret": z(T, N), "done_len": z(T, N)}
+        self.graphed = GraphedStep(self._rollout, warmup=2, enabled=enabled, name="ppo_device_rollout")
+
+    @torch.no_grad()
+    def _rollout(self, _data: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        env, agent, buf = self.env, self.agent, self.buf
+        for t in range(self.cfg.algo.rollout_steps):
+            obs = env.obs
+            buf["state"][t].copy_(obs)
+            actions, logprobs, _, values = agent({"state": obs})
+            idx = actions[0].argmax(-1)
+            out = env.step(idx)
+            v_final = agent.get_value({"state": out["final_obs"]})
+            buf["actions"][t].copy_(torch.cat(actions, -1))
+            buf["logprobs"][t].copy_(logprobs)
+            buf["values"][t].copy_(values)
+            buf["rewards"][t].copy_(out["reward"].unsqueeze(-1) + out["truncated"].unsqueeze(-1) * v_final)
+            buf["dones"][t].copy_(torch.maximum(out["terminated"], out["truncated"]).unsqueeze(-1))
+            self.stats["done_ret"][t].copy_(out["done_ret"])
+            self.stats["done_len"][t].copy_(out["done_len"])
+        return {}
+
+    def __call__(self) -> Dict[str, torch.Tensor]:
+        self.graphed({})
+        return self.buf
+
+    def finished_episodes(self):
+        """(returns, lengths) of the episodes that ended during the last rollout (one D2H)."""
+        r = self.stats["done_ret"].reshape(-1).cpu()
+        n = self.stats["done_len"].reshape(-1).cpu()
+        m = n > 0
+        return r[m].tolist(), n[m].tolist()
+
+
+_CHAIN_ACTS = {nn.Tanh: 4, nn.ReLU: 3, nn.SiLU: 1, nn.ELU: 2}
+
+
+def _mlp_chain(seq: nn.Module):
+    """``[Linear, act?]*`` -> (weights, biases, act codes) for the fused rollout kernel, or None when
+    the stack holds anything else (LayerNorm, active dropout, widths > 256)."""
+    W, B, A = [], [], []
+    for m in ([seq] if isinstance(seq, nn.Linear) else list(seq)):
+        if isinstance(m, nn.Linear):
+            if max(m.weight.shape) > 256 or m.weight.dtype != torch.float32:
+                return None
+            W.append(m.weight)
+            B.append(m.bias)
+            A.append(0)
+        elif type(m) in _CHAIN_ACTS:
+            if not A or A[-1] != 0:
+                return None
+            A[-1] = _CHAIN_ACTS[type(m)]
+        elif isinstance(m, nn.Identity) or (isinstance(m, nn.Dropout) and (m.p == 0 or not m.training)):
+            continue
+        else:
+            return None
+    return (W, B, A) if 1 <= len(W) <= 8 else None
+
+
+class FusedCartPoleRollout:
+    """The whole rollout (reference ``ppo.py:281-356``) as ONE kernel launch
+    (``ops/csrc/ppo_rollout.hip``): a workgroup per env runs the T steps of policy MLPs,
+    categorical sampling, CartPole step with autoreset and truncation bootstrap back to back.
+    Same buffers / ``finished_episodes`` contract as :class:`DeviceRollout`; applies to discrete
+    MLP-only agents on ``CartPoleDevice`` (``FusedCartPoleRollout.supported``)."""
+
+    def __init__(self, agent, env, cfg, seed: int = 0, lds_weights: bool = True):
+        self.agent, self.env, self.lds_weights = agent, env, lds_weights
+        T, N, dev = cfg.algo.rollout_steps, env.num_envs, env.device
+        z = lambda *s: torch.zeros(*s, device=dev)  # noqa: E731
+        self.buf = {"state": z(T, N, 4), "actions": z(T, N, 2), "logprobs": z(T, N, 1), "values": z(T, N, 1),
+                    "rewards": z(T, N, 1), "dones": z(T, N, 1)}
+        self.stats = {"done_ret": z(T, N), "done_len": z(T, N)}
+        self.chains = self.chains_of(agent)
+        assert self.chains is not None, "agent not supported by the fused rollout"
+        self.seed = int(seed) * 1000003
+
+    @staticmethod
+    def chains_of(agent):
+        fe = agent.feature_extractor
+        if fe.has_cnn_encoder or not fe.has_mlp_encoder or agent.is_continuous or len(agent.actor_heads) != 1:
+            return None
+        chains = [_mlp_chain(fe.mlp_encoder.model.model), _mlp_chain(agent.actor_backbone.model),
+                  _mlp_chain(agent.actor_heads[0]), _mlp_chain(agent.critic.model)]
+        return None if any(c is None for c in chains) else chains
+
+    @classmethod
+    def supported(cls, agent, env) -> bool:
+        from sheeprl_prey_amd.envs.device import CartPoleDevice
+
+        return (isinstance(env, CartPoleDevice) and env.device.type == "cuda" and list(agent.actions_dim) == [2]
+                and cls.chains_of(agent) is not None)
+
+    @torch.no_grad()
+    def __call__(self) -> Dict[str, torch.Tensor]:
+        from sheeprl_prey_amd import ops
+
+        e, a, h, c = self.chains
+        env, b = self.env, self.buf
+        self.seed += 1
+        ops._ext().ppo_cartpole_rollout(*e, *a, *h, *c, env.state, env.steps, env.ep_ret, env.obs,
+                                        [b["state"], b["actions"], b["logprobs"], b["values"], b["rewards"], b["dones"],
+                                         self.stats["done_ret"], self.stats["done_len"]],
+                                        env.max_steps, self.seed & 0x7FFFFFFFFFFFFFFF, self.lds_weights)
+        return b
+
+    finished_episodes = DeviceRollout.finished_episodes
 
 
 @register_algorithm()

@@ -19,6 +19,8 @@ bool launch_ln_act_bwd(const float*, int, const float*, int, float*, int, const 
                        const float*, float*, float*, float*, float*, int, int, int, int, hipStream_t);
 void launch_colsum2(const float*, const float*, float*, float*, int, int, int, hipStream_t);
 void launch_colsum1(const float*, int, float*, int, int, hipStream_t);
+void launch_cartpole_step(float*, int*, float*, const int64_t*, const float*, float*, float*, float*, float*, float*, float*,
+                          float*, int, int, hipStream_t);
 void launch_rssm_mask_fwd(const float*, int, const float*, const float*, const float*, float*, int, float*, int, int, int,
                           hipStream_t);
 void launch_rssm_mask_bwd(const float*, int, const float*, int, const float*, const float*, float*, float*, int, int, int,
@@ -583,12 +585,111 @@ torch::Tensor colsum(torch::Tensor x) {
   return out;
 }
 
+// device CartPole step (envs.hip); state/steps/ep_ret are updated in place, outputs preallocated
+void cartpole_step(torch::Tensor state, torch::Tensor steps, torch::Tensor ep_ret, torch::Tensor action,
+                   torch::Tensor uniform, torch::Tensor obs, torch::Tensor reward, torch::Tensor terminated,
+                   torch::Tensor truncated, torch::Tensor final_obs, torch::Tensor done_ret, torch::Tensor done_len,
+                   int64_t max_steps) {
+  const int64_t N = state.size(0);
+  for (auto* t : {&state, &ep_ret, &uniform, &obs, &reward, &terminated, &truncated, &final_obs, &done_ret, &done_len})
+    check_f32(*t, "cartpole buffer");
+  TORCH_CHECK(state.dim() == 2 && state.size(1) == 4 && obs.numel() == 4 * N && final_obs.numel() == 4 * N &&
+                  uniform.numel() == 4 * N,
+              "cartpole_step: state/obs/final_obs/uniform must be [N, 4]");
+  TORCH_CHECK(steps.is_cuda() && steps.scalar_type() == torch::kInt32 && steps.numel() == N, "cartpole_step: steps int32 [N]");
+  TORCH_CHECK(action.is_cuda() && action.scalar_type() == torch::kInt64 && action.numel() == N && action.is_contiguous(),
+              "cartpole_step: action int64 [N]");
+  TORCH_CHECK(reward.numel() == N && terminated.numel() == N && truncated.numel() == N && done_ret.numel() == N &&
+                  done_len.numel() == N,
+              "cartpole_step: per-env outputs must have N elements");
+  launch_cartpole_step(state.data_ptr<float>(), steps.data_ptr<int>(), ep_ret.data_ptr<float>(), action.data_ptr<int64_t>(),
+                       uniform.data_ptr<float>(), obs.data_ptr<float>(), reward.data_ptr<float>(),
+                       terminated.data_ptr<float>(), truncated.data_ptr<float>(), final_obs.data_ptr<float>(),
+                       done_ret.data_ptr<float>(), done_len.data_ptr<float>(), N, max_steps, cur_stream());
+}
+
+// one-launch PPO rollout on the device CartPole (ppo_rollout.hip)
+#include "ppo_rollout.h"
+void launch_ppo_cartpole_rollout(const srl::RolloutArgs&, hipStream_t);
+
+namespace {
+srl::Chain make_chain(const std::vector<torch::Tensor>& W, const std::vector<c10::optional<torch::Tensor>>& b,
+                      const std::vector<int64_t>& act, int64_t& lds_off) {
+  TORCH_CHECK(W.size() >= 1 && W.size() <= 8 && b.size() == W.size() && act.size() == W.size(), "rollout chain: 1..8 layers");
+  srl::Chain c{};
+  c.n = W.size();
+  for (size_t l = 0; l < W.size(); ++l) {
+    check_f32(W[l], "chain weight");
+    TORCH_CHECK(W[l].dim() == 2 && W[l].size(0) <= 256 && W[l].size(1) <= 256, "rollout chain: widths <= 256");
+    if (l > 0) TORCH_CHECK(W[l].size(1) == W[l - 1].size(0), "rollout chain: layer widths do not chain");
+    c.dout[l] = W[l].size(0);
+    c.din[l] = W[l].size(1);
+    c.act[l] = act[l];
+    c.W[l] = W[l].data_ptr<float>();
+    c.b[l] = opt_ptr(b[l]);
+    c.woff[l] = (int)lds_off;
+    lds_off += (int64_t)c.din[l] * c.dout[l];
+    c.boff[l] = (int)lds_off;
+    lds_off += (c.dout[l] + 3) & ~3;
+  }
+  return c;
+}
+}  // namespace
+
+void ppo_cartpole_rollout(std::vector<torch::Tensor> eW, std::vector<c10::optional<torch::Tensor>> eb, std::vector<int64_t> ea,
+                          std::vector<torch::Tensor> aW, std::vector<c10::optional<torch::Tensor>> ab, std::vector<int64_t> aa,
+                          std::vector<torch::Tensor> hW, std::vector<c10::optional<torch::Tensor>> hb, std::vector<int64_t> ha,
+                          std::vector<torch::Tensor> cW, std::vector<c10::optional<torch::Tensor>> cb, std::vector<int64_t> ca,
+                          torch::Tensor state, torch::Tensor steps, torch::Tensor ep_ret, torch::Tensor obs_out,
+                          std::vector<torch::Tensor> bufs, int64_t max_steps, int64_t seed, bool allow_lds) {
+  srl::RolloutArgs p{};
+  int64_t lds_off = 0;
+  p.enc = make_chain(eW, eb, ea, lds_off);
+  p.actor = make_chain(aW, ab, aa, lds_off);
+  p.head = make_chain(hW, hb, ha, lds_off);
+  p.critic = make_chain(cW, cb, ca, lds_off);
+  p.lds_weights = allow_lds && lds_off <= srl::RO_LDSW ? 1 : 0;
+  TORCH_CHECK(p.enc.din[0] == 4, "rollout: the encoder must take the 4-dim CartPole observation");
+  TORCH_CHECK(p.actor.din[0] == p.enc.dout[p.enc.n - 1] && p.critic.din[0] == p.enc.dout[p.enc.n - 1] &&
+                  p.head.din[0] == p.actor.dout[p.actor.n - 1] && p.critic.dout[p.critic.n - 1] == 1,
+              "rollout: chain shapes");
+  p.A = p.head.dout[p.head.n - 1];
+  TORCH_CHECK(p.A == 2, "rollout: CartPole has 2 actions");
+  check_f32(state, "state");
+  check_f32(ep_ret, "ep_ret");
+  check_f32(obs_out, "obs_out");
+  TORCH_CHECK(steps.is_cuda() && steps.scalar_type() == torch::kInt32, "steps int32");
+  p.N = state.size(0);
+  TORCH_CHECK(bufs.size() == 8, "rollout: 8 buffers (state, actions, logp, values, rewards, dones, done_ret, done_len)");
+  for (auto& t : bufs) check_f32(t, "rollout buffer");
+  p.T = bufs[0].size(0);
+  TORCH_CHECK(bufs[0].numel() == (int64_t)p.T * p.N * 4 && bufs[1].numel() == (int64_t)p.T * p.N * p.A, "rollout: buffer shapes");
+  for (int i = 2; i < 8; ++i) TORCH_CHECK(bufs[i].numel() == (int64_t)p.T * p.N, "rollout: per-step buffers [T, N]");
+  p.max_steps = max_steps;
+  p.seed = (uint64_t)seed;
+  p.state = state.data_ptr<float>();
+  p.steps = steps.data_ptr<int>();
+  p.ep_ret = ep_ret.data_ptr<float>();
+  p.obs_out = obs_out.data_ptr<float>();
+  p.b_state = bufs[0].data_ptr<float>();
+  p.b_actions = bufs[1].data_ptr<float>();
+  p.b_logp = bufs[2].data_ptr<float>();
+  p.b_values = bufs[3].data_ptr<float>();
+  p.b_rewards = bufs[4].data_ptr<float>();
+  p.b_dones = bufs[5].data_ptr<float>();
+  p.b_done_ret = bufs[6].data_ptr<float>();
+  p.b_done_len = bufs[7].data_ptr<float>();
+  launch_ppo_cartpole_rollout(p, cur_stream());
+}
+
 void register_conv(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_conv(m);
   m.def("ln_gru_into", &ln_gru_into);
   m.def("colsum", &colsum);
+  m.def("cartpole_step", &cartpole_step);
+  m.def("ppo_cartpole_rollout", &ppo_cartpole_rollout);
   m.def("unimix_sample_into", &unimix_sample_into);
   m.doc() = "sheeprl_prey_amd HIP kernels (gfx950)";
   m.def("flat_grad_norm", &flat_grad_norm);
