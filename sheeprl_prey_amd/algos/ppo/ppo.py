@@ -78,6 +78,80 @@ def _minibatch_step(runner, agent, optimizer, batch, obs_keys, cfg, clip_coef, e
     return pg_loss, v_loss, ent_loss
 
 
+class FusedPPOTrainer:
+    """The whole PPO update (``update_epochs`` x minibatch steps: forward, clipped-surrogate / value /
+    entropy losses, backward, optional global-norm clip, Adam) as ONE kernel launch
+    (``ops/csrc/ppo_train.hip``) for discrete MLP agents whose weights fit one CU's LDS (the
+    ``exp=ppo`` CartPole agent does).  Semantics follow ``train`` / ``_minibatch_step`` (reference
+    ``ppo.py:32-104``): same minibatch order source (a uniform permutation per epoch), the loss
+    means are reported like ``PPOTrainer``'s graph outputs, and the optimiser's flat slabs
+    (weights, Adam moments, step counter, last gradients) are updated in place."""
+
+    def __init__(self, runner, agent, optimizer, cfg, n: int, plan):
+        self.runner, self.agent, self.optimizer, self.cfg, self.n = runner, agent, optimizer, cfg, n
+        self.layers, self.counts = plan
+        dev = runner.device
+        self.key = list(cfg.mlp_keys.encoder)[0]
+        self.coefs = [torch.tensor([float(cfg.algo.clip_coef)], device=dev), torch.tensor([float(cfg.algo.ent_coef)], device=dev)]
+        self.out = torch.zeros(3, device=dev)
+
+    @staticmethod
+    def plan(runner, agent, optimizer, cfg):
+        """(layers, counts) for the kernel, or None when this setup is not covered."""
+        from sheeprl_prey_amd import ops
+        from sheeprl_prey_amd.parallel.flat_optim import FlatAdam
+
+        if (runner.device.type != "cuda" or runner.world_size != 1 or not isinstance(optimizer, FlatAdam)
+                or len(cfg.mlp_keys.encoder) != 1 or len(cfg.cnn_keys.encoder) != 0 or agent.is_continuous
+                or str(cfg.algo.loss_reduction).lower() != "mean" or not ops.native_available()):
+            return None
+        chains = FusedCartPoleRollout.chains_of(agent)
+        if chains is None:
+            return None
+        offs = {id(p): off for p, off in zip(optimizer.params, optimizer.offsets)}
+        layers = []
+        for W, B, A in chains:
+            for w, b, a in zip(W, B, A):
+                if id(w) not in offs or (b is not None and id(b) not in offs):
+                    return None
+                layers.append([w.shape[1], w.shape[0], a, offs[id(w)], offs[id(b)] if b is not None else -1])
+        counts = [len(c[0]) for c in chains]
+        D0 = layers[0][0]
+        A = int(sum(agent.actions_dim))
+        if not ops._ext().ppo_mlp_train_fits(layers, counts, D0, A):
+            return None
+        n_chain = sum(len(c[0]) + sum(b is not None for b in c[1]) for c in chains)
+        if n_chain != sum(1 for _ in agent.parameters()):
+            return None  # every trainable tensor of the agent must be a chain weight / bias
+        return layers, counts
+
+    def __call__(self, data: TensorDict, aggregator: Optional[MetricAggregator] = None,
+                 perm: Optional[torch.Tensor] = None) -> None:
+        from sheeprl_prey_amd import ops
+
+        cfg, opt, n = self.cfg, self.optimizer, self.n
+        dev = self.out.device
+        if perm is None:  # one uniform permutation per epoch (minibatch order)
+            perm = torch.argsort(torch.rand(int(cfg.algo.update_epochs), n, device=dev), dim=1)
+        f = lambda k: data[k].reshape(n, -1).float().contiguous()  # noqa: E731
+        cols = [f(self.key), f("actions"), f("logprobs").reshape(-1), f("values").reshape(-1), f("returns").reshape(-1),
+                f("advantages").reshape(-1)]
+        self.coefs[0].fill_(float(cfg.algo.clip_coef))
+        self.coefs[1].fill_(float(cfg.algo.ent_coef))
+        opt._gather()
+        g = opt.param_groups[0]
+        b1, b2 = g["betas"]
+        ops._ext().ppo_mlp_train(self.layers, self.counts, cols, perm,
+                                 [opt.flat_param, opt.flat_grad, opt.exp_avg, opt.exp_avg_sq, opt.scalars], self.coefs,
+                                 self.out, int(cfg.per_rank_batch_size), float(cfg.algo.vf_coef),
+                                 float(cfg.algo.max_grad_norm), bool(cfg.algo.clip_vloss),
+                                 bool(cfg.algo.normalize_advantages), float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                 float(g["weight_decay"]), bool(opt.decoupled))
+        if aggregator is not None:
+            for i, k in enumerate(("Loss/policy_loss", "Loss/value_loss", "Loss/entropy_loss")):
+                aggregator.update(k, self.out[i].clone())
+
+
 class PPOTrainer:
     """All ``update_epochs`` x minibatch steps of one PPO update as ONE hipGraph (single rank, GPU,
     ``fabric.cuda_graphs``): permutations are drawn on device (``argsort`` of uniform keys), the
@@ -96,6 +170,10 @@ class PPOTrainer:
         enabled = (dev.type == "cuda" and bool(getattr(runner, "cuda_graphs", False)) and runner.world_size == 1
                    and not cfg.algo.anneal_lr)
         self.graphed = GraphedStep(self._train, warmup=2, enabled=enabled, name="ppo_train")
+        from sheeprl_prey_amd import ops
+
+        plan = FusedPPOTrainer.plan(runner, agent, optimizer, cfg) if cfg.algo.get("fused_update", True) and ops._FUSED else None
+        self.fused = FusedPPOTrainer(runner, agent, optimizer, cfg, n, plan) if plan is not None else None
 
     def _train(self, data: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         cfg = self.cfg
@@ -116,6 +194,9 @@ class PPOTrainer:
         return {"Loss/policy_loss": sums[0], "Loss/value_loss": sums[1], "Loss/entropy_loss": sums[2]}
 
     def __call__(self, data: TensorDict, aggregator: Optional[MetricAggregator] = None) -> None:
+        if self.fused is not None:
+            self.fused(data, aggregator)
+            return
         if not self.graphed.enabled:
             train(self.runner, self.agent, self.optimizer, data, aggregator, self.cfg)
             return

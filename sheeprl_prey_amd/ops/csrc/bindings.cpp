@@ -682,6 +682,155 @@ void ppo_cartpole_rollout(std::vector<torch::Tensor> eW, std::vector<c10::option
   launch_ppo_cartpole_rollout(p, cur_stream());
 }
 
+// one-launch PPO update for MLP agents (ppo_train.hip)
+#include "ppo_train.h"
+void launch_ppo_mlp_train(const srl::PTArgs&, hipStream_t);
+
+namespace {
+int r4(int x) { return (x + 3) & ~3; }
+
+// LDS plan of the fused PPO update; false when the agent does not fit the kernel.
+// layers: [din, dout, act, pw, pb] per Linear, chains in order encoder / actor / head / critic.
+bool pt_plan(const std::vector<std::vector<int64_t>>& layers, const std::vector<int64_t>& counts, int D0, int A,
+             srl::PTArgs& p) {
+  if (counts.size() != 4) return false;
+  p.ne = counts[0];
+  p.na = counts[1];
+  p.nh = counts[2];
+  p.nc = counts[3];
+  const int NL = p.ne + p.na + p.nh + p.nc;
+  if (p.ne < 1 || p.na < 1 || p.nh < 1 || p.nc < 1 || NL > srl::PT_MAXL || (int)layers.size() != NL) return false;
+  int off = 0, tiles = 0, wmax = D0;
+  for (int l = 0; l < NL; ++l) {
+    const auto& d = layers[l];
+    if (d.size() != 5) return false;
+    srl::PTLayer& L = p.L[l];
+    L.din = d[0];
+    L.dout = d[1];
+    L.act = d[2];
+    L.pw = d[3];
+    L.pb = d[4];
+    if (L.act != 0 && L.act != 2 && L.act != 3 && L.act != 4) return false;  // none, elu, relu, tanh (common.h Act)
+    if (L.din < 1 || L.dout < 1 || L.din > 256 || L.dout > 256) return false;
+    L.k4 = r4(L.din + 1);
+    L.ldw = r4(L.dout) + 4;
+    L.wt = off;
+    off += L.k4 * L.ldw;
+    L.tile0 = tiles;
+    L.tj = (L.dout + 3) / 4;
+    L.tk = L.k4 / 4;
+    tiles += L.tj * L.tk;
+    wmax = std::max(wmax, std::max(L.din, L.dout));
+  }
+  p.ntiles = tiles;
+  if (tiles > srl::PT_THREADS * srl::PT_MAXT) return false;
+  // activation buffers: observation, then every layer's output
+  p.node_lo = off;
+  const int obs_node = off, obs_ld = r4(D0 + 1);
+  off += srl::PT_R * obs_ld;
+  for (int l = 0; l < NL; ++l) {
+    p.L[l].out_node = off;
+    p.L[l].out_ld = r4(p.L[l].dout + 1);
+    off += srl::PT_R * p.L[l].out_ld;
+  }
+  const int e_last = p.ne - 1, a0 = p.ne, h0 = p.ne + p.na, c0 = p.ne + p.na + p.nh;
+  for (int l = 0; l < NL; ++l) {
+    srl::PTLayer& L = p.L[l];
+    int src = l - 1;
+    if (l == 0) src = -1;
+    else if (l == a0 || l == c0) src = e_last;
+    if (src < 0) {
+      L.in_node = obs_node;
+      L.in_ld = obs_ld;
+      L.in_act = -1;
+      if (L.din != D0) return false;
+    } else {
+      L.in_node = p.L[src].out_node;
+      L.in_ld = p.L[src].out_ld;
+      L.in_act = p.L[src].act;
+      if (L.din != p.L[src].dout) return false;
+    }
+  }
+  if (p.L[h0 + p.nh - 1].dout != A || p.L[NL - 1].dout != 1 || A > srl::PT_MAXA || D0 > srl::PT_MAXD0) return false;
+  p.tmp_ld = r4(wmax + 1);
+  p.tmpA = off;
+  off += srl::PT_R * p.tmp_ld;
+  p.tmpB = off;
+  off += srl::PT_R * p.tmp_ld;
+  p.tmpD = off;
+  off += srl::PT_R * p.tmp_ld;
+  p.node_hi = off;
+  p.D0 = D0;
+  p.A = A;
+  return off <= srl::PT_LDS;
+}
+}  // namespace
+
+bool ppo_mlp_train_fits(std::vector<std::vector<int64_t>> layers, std::vector<int64_t> counts, int64_t D0, int64_t A) {
+  srl::PTArgs p{};
+  return pt_plan(layers, counts, D0, A, p);
+}
+
+// data: obs [n, D0], actions [n, A] (one-hot), logprobs / values / returns / advantages [n];
+// perm [epochs, n] int64; slabs: flat param, flat grad, exp_avg, exp_avg_sq, scalars (FlatAdam);
+// coefs: device clip / entropy coefficients; out_sums [3]
+void ppo_mlp_train(std::vector<std::vector<int64_t>> layers, std::vector<int64_t> counts, std::vector<torch::Tensor> data,
+                   torch::Tensor perm, std::vector<torch::Tensor> slabs, std::vector<torch::Tensor> coefs,
+                   torch::Tensor out_sums, int64_t bs, double vf_coef, double max_grad_norm, bool clip_vloss,
+                   bool norm_adv, double lr, double b1, double b2, double eps, double wd, bool decoupled) {
+  TORCH_CHECK(data.size() == 6 && slabs.size() == 5 && coefs.size() == 2, "ppo_mlp_train: argument lists");
+  for (auto& t : data) check_f32(t, "ppo_mlp_train data");
+  for (auto& t : slabs) check_f32(t, "ppo_mlp_train slab");
+  for (auto& t : coefs) check_f32(t, "ppo_mlp_train coef");
+  check_f32(out_sums, "out_sums");
+  TORCH_CHECK(perm.is_cuda() && perm.scalar_type() == torch::kInt64 && perm.is_contiguous() && perm.dim() == 2,
+              "perm: contiguous int64 [epochs, n]");
+  const int64_t n = data[0].size(0);
+  const int D0 = data[0].size(1), A = data[1].size(1);
+  srl::PTArgs p{};
+  TORCH_CHECK(pt_plan(layers, counts, D0, A, p), "ppo_mlp_train: agent does not fit the fused kernel");
+  TORCH_CHECK(perm.size(1) == n && data[1].size(0) == n, "ppo_mlp_train: row counts");
+  for (int i = 2; i < 6; ++i) TORCH_CHECK(data[i].numel() == n, "ppo_mlp_train: per-row vectors");
+  const int64_t P = slabs[0].numel();
+  for (int i = 1; i < 4; ++i) TORCH_CHECK(slabs[i].numel() == P, "ppo_mlp_train: slab sizes");
+  TORCH_CHECK(slabs[4].numel() >= 3 && out_sums.numel() >= 3, "ppo_mlp_train: scalars");
+  const int NL = p.ne + p.na + p.nh + p.nc;
+  for (int l = 0; l < NL; ++l) {
+    TORCH_CHECK(p.L[l].pw >= 0 && p.L[l].pw + (int64_t)p.L[l].din * p.L[l].dout <= P, "ppo_mlp_train: weight offset");
+    TORCH_CHECK(p.L[l].pb < 0 || p.L[l].pb + p.L[l].dout <= P, "ppo_mlp_train: bias offset");
+  }
+  TORCH_CHECK(bs >= 1 && bs <= srl::PT_THREADS && n >= 1, "ppo_mlp_train: 1 <= batch size <= 512");
+  p.obs = data[0].data_ptr<float>();
+  p.actions = data[1].data_ptr<float>();
+  p.logp_old = data[2].data_ptr<float>();
+  p.val_old = data[3].data_ptr<float>();
+  p.ret = data[4].data_ptr<float>();
+  p.adv = data[5].data_ptr<float>();
+  p.perm = perm.data_ptr<int64_t>();
+  p.n = n;
+  p.bs = bs;
+  p.epochs = perm.size(0);
+  p.clip_p = coefs[0].data_ptr<float>();
+  p.ent_p = coefs[1].data_ptr<float>();
+  p.vf_coef = vf_coef;
+  p.max_grad_norm = max_grad_norm;
+  p.clip_vloss = clip_vloss;
+  p.norm_adv = norm_adv;
+  p.param = slabs[0].data_ptr<float>();
+  p.grad = slabs[1].data_ptr<float>();
+  p.m = slabs[2].data_ptr<float>();
+  p.v = slabs[3].data_ptr<float>();
+  p.scalars = slabs[4].data_ptr<float>();
+  p.lr = lr;
+  p.b1 = b1;
+  p.b2 = b2;
+  p.eps = eps;
+  p.wd = wd;
+  p.decoupled = decoupled;
+  p.out_sums = out_sums.data_ptr<float>();
+  launch_ppo_mlp_train(p, cur_stream());
+}
+
 void register_conv(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -690,6 +839,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &colsum);
   m.def("cartpole_step", &cartpole_step);
   m.def("ppo_cartpole_rollout", &ppo_cartpole_rollout);
+  m.def("ppo_mlp_train_fits", &ppo_mlp_train_fits);
+  m.def("ppo_mlp_train", &ppo_mlp_train);
   m.def("unimix_sample_into", &unimix_sample_into);
   m.doc() = "sheeprl_prey_amd HIP kernels (gfx950)";
   m.def("flat_grad_norm", &flat_grad_norm);

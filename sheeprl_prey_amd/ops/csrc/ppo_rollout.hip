@@ -219,12 +219,141 @@ __global__ void __launch_bounds__(64 * RO_ENVS_PER_BLOCK) ppo_cartpole_rollout_k
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Register variant (every layer width <= 64): activations live in VGPRs, lane j holding unit j.
+// A layer is y_j = act(b_j + sum_k x_k W^T[k][j]) with x_k broadcast by v_readlane (a VALU op, no
+// LDS round trip) and W^T[k][j] read from LDS by consecutive lanes; no barriers, no LDS writes.
+// Every lane runs the (scalar) env step redundantly, so the state stays uniform in registers.
+__device__ __forceinline__ float lane_bcast(float v, int k) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+
+__device__ __forceinline__ float reg_chain(const Chain& c, const float* __restrict__ sw, float x, int lane) {
+  for (int l = 0; l < c.n; ++l) {
+    const int din = c.din[l], dout = c.dout[l];
+    const int jj = lane < dout ? lane : dout - 1;
+    const float* wt = sw + c.woff[l] + jj;
+    float a0 = sw[c.boff[l] + jj], a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (din == 64) {
+#pragma unroll
+      for (int k = 0; k < 64; k += 4) {
+        a0 = fmaf(lane_bcast(x, k), wt[k * dout], a0);
+        a1 = fmaf(lane_bcast(x, k + 1), wt[(k + 1) * dout], a1);
+        a2 = fmaf(lane_bcast(x, k + 2), wt[(k + 2) * dout], a2);
+        a3 = fmaf(lane_bcast(x, k + 3), wt[(k + 3) * dout], a3);
+      }
+    } else {
+      for (int k = 0; k < din; ++k) a0 = fmaf(lane_bcast(x, k), wt[k * dout], a0);
+    }
+    const float y = ro_act((a0 + a1) + (a2 + a3), c.act[l]);
+    x = lane < dout ? y : 0.f;
+  }
+  return x;
+}
+
+__global__ void __launch_bounds__(64 * RO_ENVS_PER_BLOCK) ppo_cartpole_rollout_reg_kernel(RolloutArgs p) {
+  __shared__ __attribute__((aligned(16))) float s_w[RO_LDSW];
+  stage_chain(p.enc, s_w);
+  stage_chain(p.actor, s_w);
+  stage_chain(p.head, s_w);
+  stage_chain(p.critic, s_w);
+  __syncthreads();  // the only barrier: from here on every wave (env) runs on its own
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = blockIdx.x * RO_ENVS_PER_BLOCK + wave;
+  if (n >= p.N) return;
+  const float gravity = 9.8f, masscart = 1.0f, masspole = 0.1f, total_mass = masspole + masscart, length = 0.5f;
+  const float pml = masspole * length, force_mag = 10.0f, tau = 0.02f;
+  const float theta_thr = 12.f * 2.f * 3.14159265358979323846f / 360.f, x_thr = 2.4f;
+  float x = p.state[4 * n], x_dot = p.state[4 * n + 1], th = p.state[4 * n + 2], th_dot = p.state[4 * n + 3];
+  int steps = p.steps[n];
+  float ep_ret = p.ep_ret[n];
+  for (int t = 0; t < p.T; ++t) {
+    const size_t tn = (size_t)t * p.N + n;
+    const float ob = lane == 0 ? x : lane == 1 ? x_dot : lane == 2 ? th : lane == 3 ? th_dot : 0.f;
+    if (lane < 4) p.b_state[4 * tn + lane] = ob;
+    const float feat = reg_chain(p.enc, s_w, ob, lane);
+    const float logit = reg_chain(p.head, s_w, reg_chain(p.actor, s_w, feat, lane), lane);
+    const float value = lane_bcast(reg_chain(p.critic, s_w, feat, lane), 0);
+    // Gumbel-max sample and log-prob over the A logits (uniform over the wave)
+    float mx = -INFINITY;
+    for (int a = 0; a < p.A; ++a) mx = fmaxf(mx, lane_bcast(logit, a));
+    float se = 0.f;
+    for (int a = 0; a < p.A; ++a) se += __expf(lane_bcast(logit, a) - mx);
+    const float lse = mx + __logf(se);
+    int pick = 0;
+    float best = -INFINITY, lpick = 0.f;
+    for (int a = 0; a < p.A; ++a) {
+      const float la = lane_bcast(logit, a);
+      const float g = la - __logf(-__logf(ro_uniform(p.seed, ((uint64_t)tn << 8) + a)));
+      if (g > best) {
+        best = g;
+        pick = a;
+        lpick = la;
+      }
+    }
+    if (lane < p.A) p.b_actions[tn * p.A + lane] = lane == pick ? 1.f : 0.f;
+    // CartPole-v1 step (dynamics of envs/classic.py) with autoreset
+    const float force = pick == 1 ? force_mag : -force_mag;
+    const float c = cosf(th), s = sinf(th);
+    const float temp = (force + pml * th_dot * th_dot * s) / total_mass;
+    const float thacc = (gravity * s - c * temp) / (length * (4.f / 3.f - masspole * c * c / total_mass));
+    const float xacc = temp - pml * thacc * c / total_mass;
+    const float fx = x + tau * x_dot, fxd = x_dot + tau * xacc, fth = th + tau * th_dot, fthd = th_dot + tau * thacc;
+    const bool term = fx < -x_thr || fx > x_thr || fth < -theta_thr || fth > theta_thr;
+    steps += 1;
+    const bool trunc = !term && steps >= p.max_steps;
+    ep_ret += 1.f;
+    float reward = 1.f;
+    if (trunc) {  // truncation bootstrap: r += V(final_obs)  (wave-uniform branch)
+      const float fo = lane == 0 ? fx : lane == 1 ? fxd : lane == 2 ? fth : lane == 3 ? fthd : 0.f;
+      reward += lane_bcast(reg_chain(p.critic, s_w, reg_chain(p.enc, s_w, fo, lane), lane), 0);
+    }
+    if (lane == 0) {
+      p.b_logp[tn] = lpick - lse;
+      p.b_values[tn] = value;
+      p.b_rewards[tn] = reward;
+      p.b_dones[tn] = (term || trunc) ? 1.f : 0.f;
+      p.b_done_ret[tn] = (term || trunc) ? ep_ret : 0.f;
+      p.b_done_len[tn] = (term || trunc) ? (float)steps : 0.f;
+    }
+    if (term || trunc) {
+      x = ro_uniform(p.seed, ((uint64_t)tn << 8) + 128) * 0.1f - 0.05f;
+      x_dot = ro_uniform(p.seed, ((uint64_t)tn << 8) + 129) * 0.1f - 0.05f;
+      th = ro_uniform(p.seed, ((uint64_t)tn << 8) + 130) * 0.1f - 0.05f;
+      th_dot = ro_uniform(p.seed, ((uint64_t)tn << 8) + 131) * 0.1f - 0.05f;
+      steps = 0;
+      ep_ret = 0.f;
+    } else {
+      x = fx;
+      x_dot = fxd;
+      th = fth;
+      th_dot = fthd;
+    }
+  }
+  if (lane == 0) {
+    p.state[4 * n] = p.obs_out[4 * n] = x;
+    p.state[4 * n + 1] = p.obs_out[4 * n + 1] = x_dot;
+    p.state[4 * n + 2] = p.obs_out[4 * n + 2] = th;
+    p.state[4 * n + 3] = p.obs_out[4 * n + 3] = th_dot;
+    p.steps[n] = steps;
+    p.ep_ret[n] = ep_ret;
+  }
+}
+
 }  // namespace srl
+
+static bool ro_narrow(const srl::Chain& c) {
+  for (int l = 0; l < c.n; ++l)
+    if (c.din[l] > 64 || c.dout[l] > 64) return false;
+  return true;
+}
 
 void launch_ppo_cartpole_rollout(const srl::RolloutArgs& p, hipStream_t st) {
   const int nb = srl::cdiv(p.N, srl::RO_ENVS_PER_BLOCK);
   const int threads = 64 * (p.N < srl::RO_ENVS_PER_BLOCK ? p.N : srl::RO_ENVS_PER_BLOCK);
-  if (p.lds_weights)
+  if (p.lds_weights && p.A <= 64 && ro_narrow(p.enc) && ro_narrow(p.actor) && ro_narrow(p.head) && ro_narrow(p.critic))
+    hipLaunchKernelGGL(srl::ppo_cartpole_rollout_reg_kernel, dim3(nb), dim3(threads), 0, st, p);
+  else if (p.lds_weights)
     hipLaunchKernelGGL(srl::ppo_cartpole_rollout_kernel<true>, dim3(nb), dim3(threads), 0, st, p);
   else
     hipLaunchKernelGGL(srl::ppo_cartpole_rollout_kernel<false>, dim3(nb), dim3(threads), 0, st, p);

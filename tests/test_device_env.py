@@ -75,12 +75,13 @@ def test_device_cartpole_kernel_matches_torch_path():
             torch.testing.assert_close(getattr(gpu, k).cpu(), getattr(cpu, k))
 
 
-def _ppo_setup(n_envs, T, max_steps):
+def _ppo_setup(n_envs, T, max_steps, units=64):
     from sheeprl_prey_amd.algos.ppo.agent import PPOAgent
     from sheeprl_prey_amd.config.compose import compose
     from sheeprl_prey_amd.utils.utils import dotdict
 
-    cfg = dotdict(compose(["exp=ppo", "mlp_keys.encoder=[state]", f"algo.rollout_steps={T}", f"env.num_envs={n_envs}"]))
+    cfg = dotdict(compose(["exp=ppo", "mlp_keys.encoder=[state]", f"algo.rollout_steps={T}", f"env.num_envs={n_envs}",
+                           f"algo.dense_units={units}", f"algo.encoder.mlp_features_dim={units}"]))
     env = CartPoleDevice(n_envs, "cuda", max_episode_steps=max_steps, seed=0)
     env.reset(seed=0)
     torch.manual_seed(0)
@@ -90,15 +91,17 @@ def _ppo_setup(n_envs, T, max_steps):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("lds_weights", [True, False])
-def test_fused_ppo_rollout_matches_policy_and_dynamics(lds_weights):
+# (LDS-staged weights, layer width): register-resident kernel (<= 64), LDS-activation kernel (> 64),
+# global-memory weights
+@pytest.mark.parametrize("lds_weights,units", [(True, 64), (True, 128), (False, 64)])
+def test_fused_ppo_rollout_matches_policy_and_dynamics(lds_weights, units):
     """One-launch rollout kernel (ops/csrc/ppo_rollout.hip): log-probs / values against the torch
     agent on the stored states, env transitions against the torch CartPole step, truncation
     bootstrap r = 1 + V(final_obs), and sampled actions distributed as the policy."""
     from sheeprl_prey_amd.algos.ppo.ppo import FusedCartPoleRollout
 
     N, T = 98, 48  # not a multiple of the 4 envs per workgroup
-    cfg, env, agent = _ppo_setup(N, T, max_steps=20)
+    cfg, env, agent = _ppo_setup(N, T, max_steps=20, units=units)
     assert FusedCartPoleRollout.supported(agent, env)
     ro = FusedCartPoleRollout(agent, env, cfg, seed=1, lds_weights=lds_weights)
     obs0 = env.obs.clone()
