@@ -428,8 +428,36 @@ def main(runner, cfg: Dict[str, Any]):
         step_data[k] = t
         next_obs[k] = t
 
+    # env.device=True: the envs live on the GPU (envs/device.py) and the whole rollout is one
+    # launch (FusedCartPoleRollout) or one hipGraph replay (DeviceRollout)
+    drollout = None
+    if cfg.env.get("device", False):
+        from sheeprl_prey_amd.envs.device import make_device_env
+
+        if device.type != "cuda" or obs_keys != ["state"] or cfg.cnn_keys.encoder:
+            raise ValueError("env.device=True needs a GPU run with mlp_keys.encoder=[state] and no cnn keys")
+        denv = make_device_env(cfg.env.id, cfg.env.num_envs, device, seed=cfg.seed + rank * cfg.env.num_envs,
+                               max_episode_steps=cfg.env.max_episode_steps)
+        denv.reset()
+        if FusedCartPoleRollout.supported(agent, denv):
+            drollout = FusedCartPoleRollout(agent, denv, cfg, seed=cfg.seed + rank)
+        else:
+            drollout = DeviceRollout(agent, denv, cfg, enabled=bool(runner.cuda_graphs))
+
     for update in range(start_step, num_updates + 1):
-        for _ in range(cfg.algo.rollout_steps):
+        if drollout is not None:
+            policy_step += cfg.env.num_envs * world_size * cfg.algo.rollout_steps
+            with timer("Time/env_interaction_time"):
+                buf = drollout()
+                rb.add(TensorDict(dict(buf), batch_size=[cfg.algo.rollout_steps, cfg.env.num_envs]))
+                next_obs = {"state": denv.obs}
+            rets, lens = drollout.finished_episodes()
+            for r, n_ in zip(rets, lens):
+                aggregator.update("Rewards/rew_avg", r)
+                aggregator.update("Game/ep_len_avg", n_)
+            if rets:
+                runner.print(f"Rank-{rank}: policy_step={policy_step}, episodes={len(rets)}, last_reward={rets[-1]}")
+        for _ in range(cfg.algo.rollout_steps if drollout is None else 0):
             policy_step += cfg.env.num_envs * world_size
             with timer("Time/env_interaction_time"):
                 pout = player({k: next_obs[k] for k in obs_keys})

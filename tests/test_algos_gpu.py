@@ -49,6 +49,17 @@ def test_ppo_gpu(env_id):
     _check_ckpt("ppo", env_id, PPO_KEYS, False)
 
 
+@pytest.mark.parametrize("fused", [True, False])
+def test_ppo_device_env_gpu(fused):
+    """env.device=True: CartPole on the GPU, one-launch rollout (or the graph-captured per-op one
+    when the agent is outside the fused kernels: LayerNorm MLPs) and the fused update."""
+    extra = [] if fused else ["algo.layer_norm=True"]
+    _run(STD + ["exp=ppo", "env.id=CartPole-v1", "env.device=True", "mlp_keys.encoder=[state]",
+                "algo.rollout_steps=16", "per_rank_batch_size=8", "env.num_envs=3", "root_dir=ppo_dev",
+                f"run_name=f{int(fused)}"] + extra)
+    _check_ckpt("ppo_dev", f"f{int(fused)}", PPO_KEYS, False)
+
+
 @pytest.mark.parametrize("env_id", ["discrete_dummy", "continuous_dummy"])
 def test_dreamer_v3_gpu(env_id):
     _run(STD + ["exp=dreamer_v3", "env=dummy", f"env.id={env_id}", "buffer.size=4", "root_dir=dv3",
