@@ -152,7 +152,8 @@ class ReplayBuffer:
             )
         data_len = data.shape[0]
         next_pos = (self._pos + data_len) % self._buffer_size
-        if next_pos < self._pos or (data_len >= self._buffer_size and not self._full):
+        # wrap-around (also a whole-buffer add landing back on the write head: next_pos == pos)
+        if next_pos < self._pos or (data_len >= self._buffer_size and (not self._full or next_pos == self._pos)):
             idxes = torch.cat((torch.arange(self._pos, self._buffer_size), torch.arange(0, next_pos)))
         else:
             idxes = torch.arange(self._pos, next_pos)

@@ -223,3 +223,15 @@ def test_async_buffer_per_env_and_reset_rows():
     rb2 = AsyncReplayBuffer(16, 2, sequential=True)
     rb2.load_state_dict(sd)
     torch.testing.assert_close(rb2.buffer[1]["t"], rb.buffer[1]["t"])
+
+
+def test_replay_buffer_whole_buffer_adds_after_full():
+    """Adding exactly ``buffer_size`` rows again once full (PPO with env.device=True adds a whole
+    rollout per update) overwrites every row instead of storing nothing."""
+    rb = ReplayBuffer(4, 2, device="cpu")
+    for i in range(3):
+        rb.add(TensorDict({"a": torch.full((4, 2, 1), float(i))}, batch_size=[4, 2]))
+        assert rb["a"].eq(float(i)).all() and rb._pos == 0 and rb.full
+    rb.add(TensorDict({"a": torch.full((1, 2, 1), 9.0)}, batch_size=[1, 2]))
+    rb.add(TensorDict({"a": torch.arange(4.0).view(4, 1, 1).expand(4, 2, 1)}, batch_size=[4, 2]))
+    assert rb["a"][:, 0, 0].tolist() == [3.0, 0.0, 1.0, 2.0] and rb._pos == 1
