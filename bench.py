@@ -41,6 +41,8 @@ def parse():
                    help="--algo ppo: step CartPole-v1 on the GPU (envs/device.py) and capture the whole rollout")
     p.add_argument("--no-fused-rollout", action="store_true",
                    help="PPO --device-env: graph-captured per-op rollout instead of the one-launch kernel")
+    p.add_argument("--torch-profile", type=int, default=0,
+                   help="DV3: run N extra eager steps under torch.profiler and print the aten op table (stderr)")
     p.add_argument("--phase-times", action="store_true",
                    help="per-phase hipGraphs with event timing (diagnostic; adds syncs, not a bench number)")
     p.add_argument("overrides", nargs="*")
@@ -184,6 +186,26 @@ def main():
     for _ in range(args.warmup):
         out = one_step()
     torch.cuda.synchronize()
+    if args.torch_profile and rank == 0:
+        # op attribution of the small kernels: the same train step run eagerly (graphs off) under
+        # torch.profiler; a graph replay dispatches the very same kernels
+        from torch.profiler import ProfilerActivity, profile
+
+        trainer.graphed.enabled = False
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+            for _ in range(args.torch_profile):
+                one_step()
+            torch.cuda.synchronize()
+        trainer.graphed.enabled = True
+        small = ("aten::cat", "aten::copy_", "aten::fill_", "aten::zero_", "aten::add", "aten::add_", "aten::sum",
+                 "aten::mean", "aten::mul", "aten::sub", "aten::rand", "aten::zeros", "aten::clone", "aten::div",
+                 "aten::neg", "aten::exp", "aten::where", "aten::stack", "aten::contiguous", "aten::index_select",
+                 "aten::lerp_", "aten::_foreach_copy_", "aten::max", "aten::amax", "aten::sort", "aten::quantile")
+        rows = [e for e in prof.key_averages(group_by_stack_n=5) if e.key in small]
+        rows.sort(key=lambda e: -e.count)
+        for e in rows[:60]:
+            stack = " <- ".join(f.split("/")[-1] for f in e.stack[:5])
+            print(f"{e.key:24s} n={e.count / args.torch_profile:6.1f}/step  {stack}", file=sys.stderr, flush=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

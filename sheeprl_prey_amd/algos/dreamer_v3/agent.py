@@ -300,12 +300,14 @@ class RSSM(nn.Module):
         WgT_h, WgT_f = Wg[:, :Hd].t(), Wg[:, Hd:].t()
         ln = gru.layer_norm
         disc = self.discrete
+        nh, G = len(actor.actions_dim), S // disc
+        # every uniform of the rollout in one launch: per step nh x M for the actions, G x M for the prior
+        U = torch.rand(horizon + 1, M * (nh + G), device=post.device)
         for t in range(horizon + 1):
             out = actor.model(buf[t, :, A:])
             c0 = 0
-            for head, a in zip(actor.mlp_heads, actor.actions_dim):
-                u = torch.rand(M, device=post.device)
-                C.unimix_sample_into(head(out), u, int(a), float(actor._unimix), buf[t, :, c0:c0 + a])
+            for i, (head, a) in enumerate(zip(actor.mlp_heads, actor.actions_dim)):
+                C.unimix_sample_into(head(out), U[t, i * M:(i + 1) * M], int(a), float(actor._unimix), buf[t, :, c0:c0 + a])
                 c0 += a
             if t == horizon:
                 break
@@ -320,8 +322,7 @@ class RSSM(nn.Module):
                 gx = gx + gru.linear.bias
             C.ln_gru_into(gx, buf[t, :, A + S:], ln.weight, ln.bias, float(ln.eps), buf[t + 1, :, A + S:])
             logits = self.transition_model(buf[t + 1, :, A + S:])
-            u = torch.rand(M * (S // disc), device=post.device)
-            C.unimix_sample_into(logits.contiguous(), u, disc, float(self.unimix), buf[t + 1, :, A:A + S])
+            C.unimix_sample_into(logits.contiguous(), U[t, nh * M:], disc, float(self.unimix), buf[t + 1, :, A:A + S])
         return buf[:, :, A:], buf[:, :, :A]
 
     # ---- MI355X scan: T-step posterior rollout with hoisted GEMMs --------------------

@@ -94,6 +94,10 @@ class FusedPPOTrainer:
         self.key = list(cfg.mlp_keys.encoder)[0]
         self.coefs = [torch.tensor([float(cfg.algo.clip_coef)], device=dev), torch.tensor([float(cfg.algo.ent_coef)], device=dev)]
         self.out = torch.zeros(3, device=dev)
+        self.err = torch.zeros(1, device=dev)  # > 0: a grid-barrier wait of the multi-workgroup kernel timed out
+        self.prof = torch.empty(0, dtype=torch.int64, device=dev)  # set to int64 [4] for phase cycle totals
+        # workgroups per launch: one 16-row chunk of every minibatch each (grid barriers between steps)
+        self.nwg = int(cfg.algo.get("fused_update_workgroups", 8))
 
     @staticmethod
     def plan(runner, agent, optimizer, cfg):
@@ -146,7 +150,7 @@ class FusedPPOTrainer:
                                  self.out, int(cfg.per_rank_batch_size), float(cfg.algo.vf_coef),
                                  float(cfg.algo.max_grad_norm), bool(cfg.algo.clip_vloss),
                                  bool(cfg.algo.normalize_advantages), float(g["lr"]), float(b1), float(b2), float(g["eps"]),
-                                 float(g["weight_decay"]), bool(opt.decoupled))
+                                 float(g["weight_decay"]), bool(opt.decoupled), self.nwg, self.err, self.prof)
         if aggregator is not None:
             for i, k in enumerate(("Loss/policy_loss", "Loss/value_loss", "Loss/entropy_loss")):
                 aggregator.update(k, self.out[i].clone())

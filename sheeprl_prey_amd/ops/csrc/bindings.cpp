@@ -684,7 +684,7 @@ void ppo_cartpole_rollout(std::vector<torch::Tensor> eW, std::vector<c10::option
 
 // one-launch PPO update for MLP agents (ppo_train.hip)
 #include "ppo_train.h"
-void launch_ppo_mlp_train(const srl::PTArgs&, hipStream_t);
+hipError_t launch_ppo_mlp_train(const srl::PTArgs&, hipStream_t);
 
 namespace {
 int r4(int x) { return (x + 3) & ~3; }
@@ -777,7 +777,8 @@ bool ppo_mlp_train_fits(std::vector<std::vector<int64_t>> layers, std::vector<in
 void ppo_mlp_train(std::vector<std::vector<int64_t>> layers, std::vector<int64_t> counts, std::vector<torch::Tensor> data,
                    torch::Tensor perm, std::vector<torch::Tensor> slabs, std::vector<torch::Tensor> coefs,
                    torch::Tensor out_sums, int64_t bs, double vf_coef, double max_grad_norm, bool clip_vloss,
-                   bool norm_adv, double lr, double b1, double b2, double eps, double wd, bool decoupled) {
+                   bool norm_adv, double lr, double b1, double b2, double eps, double wd, bool decoupled,
+                   int64_t nwg, torch::Tensor err, torch::Tensor prof) {
   TORCH_CHECK(data.size() == 6 && slabs.size() == 5 && coefs.size() == 2, "ppo_mlp_train: argument lists");
   for (auto& t : data) check_f32(t, "ppo_mlp_train data");
   for (auto& t : slabs) check_f32(t, "ppo_mlp_train slab");
@@ -828,7 +829,19 @@ void ppo_mlp_train(std::vector<std::vector<int64_t>> layers, std::vector<int64_t
   p.wd = wd;
   p.decoupled = decoupled;
   p.out_sums = out_sums.data_ptr<float>();
-  launch_ppo_mlp_train(p, cur_stream());
+  // workgroups per minibatch: one 16-row chunk each (a cooperative launch; 1 = single workgroup)
+  p.nwg = (int)std::max<int64_t>(1, std::min<int64_t>({nwg, (bs + srl::PT_R - 1) / srl::PT_R, 16}));
+  check_f32(err, "err");
+  p.err = err.data_ptr<float>();
+  p.prof = prof.numel() >= 4 && prof.is_cuda() && prof.scalar_type() == torch::kInt64 ? reinterpret_cast<long long*>(prof.data_ptr<int64_t>()) : nullptr;
+  p.nparam = (int)P;
+  // zeros: the slab's alignment padding is never written by the gradient tiles and must read as 0
+  torch::Tensor scratch = torch::zeros({(int64_t)p.nwg * P + p.nwg + 4}, slabs[0].options());
+  p.partial = scratch.data_ptr<float>();
+  p.sq = p.partial + (int64_t)p.nwg * P;
+  p.bar = reinterpret_cast<int*>(p.sq + p.nwg);
+  const hipError_t e = launch_ppo_mlp_train(p, cur_stream());
+  TORCH_CHECK(e == hipSuccess, "ppo_mlp_train launch failed: ", hipGetErrorString(e));
 }
 
 void register_conv(pybind11::module& m);

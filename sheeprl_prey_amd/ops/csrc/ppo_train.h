@@ -10,7 +10,7 @@ constexpr int PT_THREADS = 512;   // 8 waves, one workgroup
 constexpr int PT_MAXT = 4;        // 4x4 weight-gradient tiles owned per thread (registers)
 constexpr int PT_LDS = 40928;     // floats of the LDS arena (~160 KB: the whole CU LDS minus a reduction scratch)
 constexpr int PT_R = 16;          // minibatch rows per chunk (2 per wave)
-constexpr int PT_MAXD0 = 16;      // observation width held in registers per minibatch row
+constexpr int PT_MAXD0 = 8;       // observation width held in registers per minibatch row
 constexpr int PT_MAXA = 8;        // actions held in registers per minibatch row
 
 // One Linear(+activation).  W^T augmented with the bias as row `din` lives in LDS at `wt`
@@ -41,7 +41,20 @@ struct PTArgs {
   float *param, *grad, *m, *v, *scalars;
   float lr, b1, b2, eps, wd;
   int decoupled;
-  float* out_sums;        // [3] mean policy / value / entropy loss over the minibatch steps
+  float* out_sums;        // [3] mean policy / value / entropy loss over the minibatch steps (zeroed by the launcher)
+  // workgroup w runs chunks w, w + nwg, ... of every minibatch and publishes its gradient tiles into
+  // partial[w] (flat-slab order); after a grid barrier every workgroup reduces + Adam-updates its
+  // 1/nwg share of each parameter region (coalesced, straight into the slabs) and, after a second
+  // barrier, re-reads the other shares into its LDS weights.  `bar` is a monotonic grid-barrier
+  // counter (zeroed by the launcher), `err` > 0 if a barrier wait timed out.
+  int nwg;
+  int nparam;             // flat-slab length (partial holds nwg copies)
+  float* partial;
+  float* sq;              // [nwg] per-workgroup squared gradient norms (global-norm clip)
+  int* bar;
+  float* err;
+  long long* prof;        // optional [4] s_memtime cycle totals of workgroup 0 (chunk / publish+barrier /
+                          // reduce+Adam / barrier+reload), diagnostics only
 };
 
 }  // namespace srl

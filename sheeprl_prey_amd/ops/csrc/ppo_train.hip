@@ -138,25 +138,69 @@ __device__ __forceinline__ void pt_phase(const PTArgs& p, float* lds, float (&ac
   __syncthreads();
 }
 
+// W^T (bias-augmented) of every layer from the param slab into LDS, reading the slab in order
+// (coalesced) and scattering into the transposed layout; non-temporal loads (L1 bypass) so a
+// re-stage after another workgroup's (or this workgroup's) slab writes never sees a stale L1 line.
+// The padding slots (j >= dout, k > din, k == din without bias) are never written: zero from start.
+__device__ void pt_stage(const PTArgs& p, float* lds, int NL) {
+  for (int l = 0; l < NL; ++l) {
+    const PTLayer& L = p.L[l];
+    for (int o = threadIdx.x; o < L.dout * L.din; o += PT_THREADS) {
+      const int j = o / L.din, k = o - j * L.din;
+      lds[L.wt + k * L.ldw + j] = __builtin_nontemporal_load(p.param + L.pw + o);
+    }
+    if (L.pb >= 0)
+      for (int j = threadIdx.x; j < L.dout; j += PT_THREADS)
+        lds[L.wt + L.din * L.ldw + j] = __builtin_nontemporal_load(p.param + L.pb + j);
+  }
+}
+
+// Grid-wide barrier of the nwg co-resident workgroups (cooperative launch): monotonic counter,
+// producer = every wave drains its stores, lane 0 releases at agent scope and arrives; consumer =
+// relaxed polls, one agent-scope acquire, then the workgroup barrier (MI355X_MICROARCH.md,
+// inter-workgroup visibility).  The poll gives up after ~1 s and flags `err` so a broken launch ends.
+__device__ __forceinline__ void pt_grid_barrier(int* bar, int target, float* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1 << 23)) {
+        atomicAdd(err, 1.f);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(PT_THREADS) ppo_mlp_train_kernel(PTArgs p) {
   __shared__ __attribute__((aligned(16))) float lds[PT_LDS];
   __shared__ float red[PT_THREADS / 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int NL = p.ne + p.na + p.nh + p.nc;
+  const int wg = blockIdx.x, nwg = p.nwg;
+  int bar_target = 0;
+  long long pc[4] = {0, 0, 0, 0}, t_mark = 0;
+#define PT_MARK(i)                                  \
+  do {                                              \
+    if (p.prof) {                                   \
+      const long long now = clock64();              \
+      if ((i) >= 0) pc[(i) < 0 ? 0 : (i)] += now - t_mark; \
+      t_mark = now;                                 \
+    }                                               \
+  } while (0)
 
-  // ---- stage W^T (bias-augmented) into LDS, zero the activation arena
-  for (int l = 0; l < NL; ++l) {
-    const PTLayer& L = p.L[l];
-    for (int i = tid; i < L.k4 * L.ldw; i += PT_THREADS) {
-      const int k = i / L.ldw, j = i - k * L.ldw;
-      float w = 0.f;
-      if (j < L.dout) {
-        if (k < L.din) w = p.param[L.pw + j * L.din + k];
-        else if (k == L.din && L.pb >= 0) w = p.param[L.pb + j];
-      }
-      lds[L.wt + i] = w;
-    }
-  }
+  // ---- stage W^T (bias-augmented) into LDS (padding zeroed first), zero the activation arena
+  for (int i = tid; i < p.node_lo; i += PT_THREADS) lds[i] = 0.f;
+  __syncthreads();
+  pt_stage(p, lds, NL);
   for (int i = p.node_lo + tid; i < p.node_hi; i += PT_THREADS) lds[i] = 0.f;
   __syncthreads();
   if (tid < PT_R) {  // constant-1 bias-input columns
@@ -231,7 +275,8 @@ __global__ void __launch_bounds__(PT_THREADS) ppo_mlp_train_kernel(PTArgs p) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
 
-      for (int c0 = 0; c0 < Bm; c0 += PT_R) {
+      PT_MARK(-1);
+      for (int c0 = wg * PT_R; c0 < Bm; c0 += nwg * PT_R) {
         const int rows = min(PT_R, Bm - c0);
         // ---- observations of the chunk (rows past the minibatch are zero)
         const bool in_chunk = tid >= c0 && tid < c0 + PT_R;
@@ -332,9 +377,10 @@ __global__ void __launch_bounds__(PT_THREADS) ppo_mlp_train_kernel(PTArgs p) {
         }
       }
       // ---- optimiser step: optional global-norm clip, Adam / AdamW on the LDS weights
-      coef = 1.f;
-      if (p.max_grad_norm > 0.f) {
-        float ss = 0.f;
+      PT_MARK(0);
+      // publish this workgroup's gradient tiles into partial[wg] in flat-slab order
+      {
+        float* G = p.partial + (size_t)wg * p.nparam;
 #pragma unroll
         for (int i = 0; i < PT_MAXT; ++i) {
           if (tl[i] < 0) continue;
@@ -342,76 +388,127 @@ __global__ void __launch_bounds__(PT_THREADS) ppo_mlp_train_kernel(PTArgs p) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int j = tj0[i] + (e >> 2), k = tk0[i] + (e & 3);
-            if (j < L.dout && (k < L.din || (k == L.din && L.pb >= 0))) ss += acc[i][e] * acc[i][e];
+            if (j >= L.dout) continue;
+            const int o = k < L.din ? L.pw + j * L.din + k : (k == L.din && L.pb >= 0 ? L.pb + j : -1);
+            if (o >= 0) G[o] = acc[i][e];
           }
         }
-        ss = block_sum<PT_THREADS / 64>(ss, red);
-        norm_last = sqrtf(ss);
-        coef = fminf(p.max_grad_norm / (norm_last + 1e-6f), 1.f);
       }
+      if (nwg > 1) {
+        bar_target += nwg;
+        pt_grid_barrier(p.bar, bar_target, p.err);
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      PT_MARK(1);
+      // optimiser over this workgroup's contiguous slice of the flat slab (coalesced; the slab's
+      // alignment padding has zero gradient, so it stays zero): gradient = sum of the workgroups'
+      // partials (also stored as the grad slab), optional global-norm clip, Adam / AdamW
       tstep += 1.f;
+      const int per = (((p.nparam + nwg - 1) / nwg) + 3) & ~3;
+      const int lo = min(p.nparam, wg * per), hi = min(p.nparam, lo + per);
       const float bc1 = 1.f - powf(p.b1, tstep);
       const float bc2s = sqrtf(1.f - powf(p.b2, tstep));
       const float stp = p.lr / bc1;
       const float decay = p.decoupled ? (1.f - p.lr * p.wd) : 1.f;
       const float l2 = p.decoupled ? 0.f : p.wd;
+      const bool clipping = p.max_grad_norm > 0.f;
+      coef = 1.f;
+      float ss = 0.f;
+      for (int base = lo + tid; base < hi; base += 8 * PT_THREADS) {
+        float g[8];
 #pragma unroll
-      for (int i = 0; i < PT_MAXT; ++i) {
-        if (tl[i] < 0) continue;
-        const PTLayer& L = p.L[tl[i]];
-        int ot[16];
-        float mt[16], vt[16];
+        for (int q = 0; q < 8; ++q) {
+          const int o = base + q * PT_THREADS;
+          g[q] = 0.f;
+          if (o < hi)
+            for (int w = 0; w < nwg; ++w) g[q] += __builtin_nontemporal_load(p.partial + (size_t)w * p.nparam + o);
+        }
+        if (clipping) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {  // issue all 32 moment loads of the tile before using any
-          const int j = tj0[i] + (e >> 2), k = tk0[i] + (e & 3);
-          ot[e] = j >= L.dout ? -1 : (k < L.din ? L.pw + j * L.din + k : (k == L.din && L.pb >= 0 ? L.pb + j : -1));
-          mt[e] = ot[e] >= 0 ? p.m[ot[e]] : 0.f;
-          vt[e] = ot[e] >= 0 ? p.v[ot[e]] : 0.f;
+          for (int q = 0; q < 8; ++q) {
+            const int o = base + q * PT_THREADS;
+            if (o < hi) p.grad[o] = g[q];
+            ss += g[q] * g[q];
+          }
+          continue;
+        }
+        float pw[8], m0[8], v0[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int o = min(base + q * PT_THREADS, hi - 1);
+          pw[q] = p.param[o];
+          m0[q] = p.m[o];
+          v0[q] = p.v[o];
         }
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          if (ot[e] < 0) continue;
-          const int j = tj0[i] + (e >> 2), k = tk0[i] + (e & 3);
-          float* w = lds + L.wt + k * L.ldw + j;
-          const float pw = *w;
-          const float gr = acc[i][e] * coef + l2 * pw;
-          const float mk = mt[e] + (1.f - p.b1) * (gr - mt[e]);
-          const float vk = vt[e] * p.b2 + (1.f - p.b2) * gr * gr;
-          *w = pw * decay - stp * mk / (sqrtf(vk) / bc2s + p.eps);
-          p.m[ot[e]] = mk;
-          p.v[ot[e]] = vk;
+        for (int q = 0; q < 8; ++q) {
+          const int o = base + q * PT_THREADS;
+          if (o >= hi) break;
+          const float gr = g[q] + l2 * pw[q];
+          const float mk = m0[q] + (1.f - p.b1) * (gr - m0[q]);
+          const float vk = v0[q] * p.b2 + (1.f - p.b2) * gr * gr;
+          p.param[o] = pw[q] * decay - stp * mk / (sqrtf(vk) / bc2s + p.eps);
+          p.m[o] = mk;
+          p.v[o] = vk;
+          p.grad[o] = g[q];
         }
       }
+      if (clipping) {
+        ss = block_sum<PT_THREADS / 64>(ss, red);
+        if (nwg > 1) {
+          if (tid == 0) p.sq[wg] = ss;
+          bar_target += nwg;
+          pt_grid_barrier(p.bar, bar_target, p.err);
+          ss = 0.f;
+          for (int w = 0; w < nwg; ++w) ss += __builtin_nontemporal_load(p.sq + w);
+        }
+        norm_last = sqrtf(ss);
+        coef = fminf(p.max_grad_norm / (norm_last + 1e-6f), 1.f);
+        for (int base = lo + tid; base < hi; base += 8 * PT_THREADS) {
+          float g[8], pw[8], m0[8], v0[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int o = min(base + q * PT_THREADS, hi - 1);
+            g[q] = p.grad[o];
+            pw[q] = p.param[o];
+            m0[q] = p.m[o];
+            v0[q] = p.v[o];
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int o = base + q * PT_THREADS;
+            if (o >= hi) break;
+            const float gr = g[q] * coef + l2 * pw[q];
+            const float mk = m0[q] + (1.f - p.b1) * (gr - m0[q]);
+            const float vk = v0[q] * p.b2 + (1.f - p.b2) * gr * gr;
+            p.param[o] = pw[q] * decay - stp * mk / (sqrtf(vk) / bc2s + p.eps);
+            p.m[o] = mk;
+            p.v[o] = vk;
+          }
+        }
+      }
+      // every workgroup re-stages the updated weights (its own slice and the others') into LDS
+      if (nwg > 1) {
+        bar_target += nwg;
+        pt_grid_barrier(p.bar, bar_target, p.err);
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      pt_stage(p, lds, NL);
+      __syncthreads();
+      PT_MARK(3);
       ++nsteps;
       __syncthreads();
     }
   }
 
-  // ---- write back: weights (LDS -> slab), Adam moments, last gradients, step counter, loss means
-  for (int l = 0; l < NL; ++l) {
-    const PTLayer& L = p.L[l];
-    for (int i = tid; i < L.dout * L.din; i += PT_THREADS) {
-      const int j = i / L.din, k = i - j * L.din;
-      p.param[L.pw + i] = lds[L.wt + k * L.ldw + j];
-    }
-    if (L.pb >= 0)
-      for (int j = tid; j < L.dout; j += PT_THREADS) p.param[L.pb + j] = lds[L.wt + L.din * L.ldw + j];
-  }
-#pragma unroll
-  for (int i = 0; i < PT_MAXT; ++i) {
-    if (tl[i] < 0) continue;
-    const PTLayer& L = p.L[tl[i]];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int j = tj0[i] + (e >> 2), k = tk0[i] + (e & 3);
-      if (j >= L.dout) continue;
-      int o = -1;
-      if (k < L.din) o = L.pw + j * L.din + k;
-      else if (k == L.din && L.pb >= 0) o = L.pb + j;
-      if (o < 0) continue;
-      p.grad[o] = acc[i][e];
-    }
-  }
+  if (p.prof && wg == 0 && tid == 0)
+    for (int i = 0; i < 4; ++i) p.prof[i] = pc[i];
+#undef PT_MARK
+  // ---- write back: weights, moments and the last gradients are already in the slabs; loss means, step
   {
     const float a = block_sum<PT_THREADS / 64>(pg_acc, red);
     __syncthreads();
@@ -420,18 +517,31 @@ __global__ void __launch_bounds__(PT_THREADS) ppo_mlp_train_kernel(PTArgs p) {
     const float c = block_sum<PT_THREADS / 64>(e_acc, red);
     if (tid == 0) {
       const float inv = nsteps > 0 ? 1.f / (float)nsteps : 0.f;
-      p.out_sums[0] = a * inv;
-      p.out_sums[1] = b * inv;
-      p.out_sums[2] = c * inv;
-      p.scalars[0] = tstep;
-      p.scalars[1] = coef;
-      if (p.max_grad_norm > 0.f) p.scalars[2] = norm_last;
+      atomicAdd(p.out_sums + 0, a * inv);
+      atomicAdd(p.out_sums + 1, b * inv);
+      atomicAdd(p.out_sums + 2, c * inv);
+      if (wg == 0) {
+        p.scalars[0] = tstep;
+        p.scalars[1] = coef;
+        if (p.max_grad_norm > 0.f) p.scalars[2] = norm_last;
+      }
     }
   }
 }
 
 }  // namespace srl
 
-void launch_ppo_mlp_train(const srl::PTArgs& p, hipStream_t st) {
-  hipLaunchKernelGGL(srl::ppo_mlp_train_kernel, dim3(1), dim3(srl::PT_THREADS), 0, st, p);
+hipError_t launch_ppo_mlp_train(const srl::PTArgs& p, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(p.out_sums, 0, 3 * sizeof(float), st);
+  if (e != hipSuccess) return e;
+  if (p.nwg <= 1) {
+    hipLaunchKernelGGL(srl::ppo_mlp_train_kernel, dim3(1), dim3(srl::PT_THREADS), 0, st, p);
+    return hipGetLastError();
+  }
+  // the workgroups meet at grid barriers: a cooperative launch guarantees (and checks) co-residency
+  e = hipMemsetAsync(p.bar, 0, sizeof(int), st);
+  if (e != hipSuccess) return e;
+  srl::PTArgs a = p;
+  void* args[] = {(void*)&a};
+  return hipLaunchCooperativeKernel((const void*)srl::ppo_mlp_train_kernel, dim3(p.nwg), dim3(srl::PT_THREADS), args, 0, st);
 }

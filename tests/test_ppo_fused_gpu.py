@@ -38,8 +38,11 @@ CASES = {
 }
 
 
+@pytest.mark.parametrize("nwg", [1, 8])
 @pytest.mark.parametrize("case", list(CASES))
-def test_fused_ppo_update_matches_autograd(case):
+def test_fused_ppo_update_matches_autograd(case, nwg):
+    """nwg = 1: one workgroup runs every chunk; 8: one workgroup per 16-row chunk of each minibatch
+    (capped at bs / 16), grid barriers between the optimiser steps."""
     extra, n = CASES[case]
     cfg = dotdict(compose(["exp=ppo", "mlp_keys.encoder=[state]", "fabric.accelerator=cuda"] + extra))
     torch.manual_seed(0)
@@ -66,8 +69,10 @@ def test_fused_ppo_update_matches_autograd(case):
     perm = torch.argsort(torch.rand(E, n, device="cuda", generator=g), dim=1)
 
     fused = FusedPPOTrainer(runner, agent_a, opt_a, cfg, n, plan)
+    fused.nwg = nwg
     fused(data, None, perm=perm)
     torch.cuda.synchronize()
+    assert fused.err.item() == 0.0
 
     sums, steps = torch.zeros(3, device="cuda"), 0
     for e in range(E):
