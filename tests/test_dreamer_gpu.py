@@ -135,25 +135,37 @@ def test_dv3_segmented_graph_matches_single_graph():
     assert abs(la[1] - lb[1]) / abs(la[1]) < 1e-3, (la, lb)
 
 
-def test_imagine_discrete_matches_reference_loop():
+def test_imagine_discrete_matches_reference_loop(monkeypatch):
     """Buffer-resident no-grad imagination (RSSM.imagine_discrete) vs the reference loop
-    (RSSM.imagination + Actor per step): same seed -> same uniform draws in the same order, so the
-    sampled trajectories agree up to rare category flips from GEMM rounding."""
+    (RSSM.imagination + Actor per step).  imagine_discrete draws every uniform of the rollout in one
+    launch, U [H+1, M*(heads + groups)] (actions first, then the prior groups, per step); the
+    reference loop is fed the same slices in its call order, so the sampled trajectories agree up to
+    rare category flips from GEMM rounding."""
+    from sheeprl_prey_amd import ops
+
     tr = _build(graphs=False)
     wm, actor = tr.world_model, tr.actor
-    M, S, H = 96, 32 * 32, 64
+    M, S, H, Hz = 96, 32 * 32, 64, 4
     g = torch.Generator(device="cuda").manual_seed(3)
     post = torch.nn.functional.one_hot(torch.randint(0, 32, (M, 32), device="cuda", generator=g), 32).float().view(M, S)
     h = torch.randn(M, H, device="cuda", generator=g)
     assert wm.rssm.imagine_fast_ok(actor)
     torch.manual_seed(7)
-    traj, acts = wm.rssm.imagine_discrete(post, h, actor, 4)
+    traj, acts = wm.rssm.imagine_discrete(post, h, actor, Hz)
     torch.manual_seed(7)
+    U = torch.rand(Hz + 1, M * (1 + S // 32), device="cuda")
+    feed = iter([U[t, :M] if i == 0 else U[t, M:] for t in range(Hz + 1) for i in range(2)])
+    real = ops.unimix_sample
+
+    def fed(logits, classes, unimix=0.01, sample=True, uniform=None):
+        return real(logits, classes, unimix, sample=sample, uniform=next(feed) if sample else None)
+
+    monkeypatch.setattr(ops, "unimix_sample", fed)
     with torch.no_grad():
         prior, hh = post, h
         lat = torch.cat((prior, hh), -1)
         ref_t, ref_a = [lat], [torch.cat(actor(lat)[0], -1)]
-        for _ in range(4):
+        for _ in range(Hz):
             prior, hh = wm.rssm.imagination(prior, hh, ref_a[-1])
             prior = prior.reshape(M, S)
             lat = torch.cat((prior, hh), -1)
