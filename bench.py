@@ -45,6 +45,8 @@ def parse():
                    help="DV3: run N extra eager steps under torch.profiler and print the aten op table (stderr)")
     p.add_argument("--phase-times", action="store_true",
                    help="per-phase hipGraphs with event timing (diagnostic; adds syncs, not a bench number)")
+    p.add_argument("--check-finite", type=int, default=0,
+                   help="diagnostic: run N untimed steps, report the first non-finite train output per step")
     p.add_argument("overrides", nargs="*")
     return p.parse_args()
 
@@ -126,7 +128,7 @@ def main():
             acts = np.concatenate([np.eye(d, dtype=np.float32)[a] for a, d in zip(real.reshape(len(actions_dim), -1), actions_dim)], -1)
         else:
             with torch.no_grad():
-                pre = {k: v[None].to(device, non_blocking=True) / 255.0 for k, v in obs.items()}
+                pre = {k: v[None].to(device) / 255.0 for k, v in obs.items()}  # pageable source: sync copy
                 a = player.get_exploration_action(pre, is_continuous)
                 acts = torch.cat(a, -1).cpu().numpy()
                 real = np.array([x.argmax(-1).cpu().numpy() for x in a])
@@ -152,12 +154,14 @@ def main():
             player.init_states(idx)
 
     grad_steps = 0
+    last_batch = [None]
 
     def train_once():
         nonlocal grad_steps
         data = rb.sample(cfg.per_rank_batch_size, sequence_length=cfg.per_rank_sequence_length, n_samples=1)
         trainer.update_target(1.0 if grad_steps == 0 else cfg.algo.critic.tau)
         batch = {k: (v[0] if v.dtype == torch.uint8 else v[0].float()) for k, v in data.items()}
+        last_batch[0] = batch
         out = trainer.train_step(batch)
         grad_steps += 1
         return out
@@ -183,6 +187,9 @@ def main():
         env_advance(real)
         return out
 
+    if args.check_finite:
+        check_finite_steps(args, trainer, rb, cfg, one_step, lambda: trainer.train_step(last_batch[0]), (world_model, actor, critic),
+                           (wopt, aopt, copt), moments)
     for _ in range(args.warmup):
         out = one_step()
     torch.cuda.synchronize()
@@ -281,6 +288,70 @@ def main():
         dist.destroy_process_group()
 
 
+def check_finite_steps(args, trainer, rb, cfg, one_step, train_once, models, opts, moments):
+    """Diagnostic (``--check-finite N``): runs N untimed bench steps; before each one snapshots every
+    optimiser slab/state, the target critic and Moments.  At the first step with a non-finite output it
+    names the parameters whose gradients are non-finite, then restores the snapshot and re-runs a
+    gradient step eagerly (graphs off) to tell a capture bug from a numerics bug."""
+    names = {}
+    for m in models:
+        for n, p in m.named_parameters():
+            names[id(p)] = n
+
+    def state():
+        t = {}
+        for j, o in enumerate(opts):
+            for k, v in vars(o).items():
+                if torch.is_tensor(v):
+                    t[(j, k)] = v
+        t[("tgt", "flat")] = trainer.target_flat
+        t[("mom", "low")], t[("mom", "high")] = moments.low, moments.high
+        return t
+
+    for i in range(args.check_finite):
+        snap = {k: v.detach().clone() for k, v in state().items()}
+        rng = torch.cuda.get_rng_state()
+        out = one_step()
+        bad = [k for k, v in out.items() if torch.is_tensor(v) and not bool(torch.isfinite(v).all())]
+        vals = {k: round(float(v.float().mean()), 4) for k, v in out.items() if torch.is_tensor(v) and k.startswith("Loss/")}
+        print(f"check step {i}: non-finite={bad} {vals}", file=sys.stderr, flush=True)
+        if not bad:
+            continue
+        def report(tag):
+            for j, o in enumerate(opts):
+                stats = []
+                for p, off in zip(o.params, o.offsets):
+                    g = o.flat_grad[off:off + p.numel()]
+                    stats.append((float(g.abs().max()), float(g.double().pow(2).sum()), names.get(id(p), "?")))
+                nf = [n for m, _, n in stats if not m == m or m == float("inf")]
+                top = sorted(stats, key=lambda x: -x[0] if x[0] == x[0] else -float("inf"))[:6]
+                pad = sum(float(o.flat_grad[off + p.numel():(o.offsets[i + 1] if i + 1 < len(o.offsets) else o.numel)].abs().sum())
+                          for i, (p, off) in enumerate(zip(o.params, o.offsets)))
+                print(f"  [{tag}] opt{j}: scalars={o.scalars.tolist()} non-finite={nf[:6]} pad_abs_sum={pad:.3g} "
+                      f"sumsq={sum(x[1] for x in stats):.4g} top={[(n, f'{m:.3g}') for m, _, n in top]}",
+                      file=sys.stderr, flush=True)
+
+        report("graphed")
+        for k, v in state().items():
+            v.copy_(snap[k])
+        torch.cuda.set_rng_state(rng)
+        trainer.graphed.enabled = False
+        out2 = train_once()
+        torch.cuda.synchronize()
+        bad2 = [k for k, v in out2.items() if torch.is_tensor(v) and not bool(torch.isfinite(v).all())]
+        print(f"  eager re-run from the snapshot (same batch): non-finite={bad2}", file=sys.stderr, flush=True)
+        report("eager")
+        for k, v in state().items():
+            v.copy_(snap[k])
+        trainer.graphed.enabled = True
+        out3 = train_once()
+        torch.cuda.synchronize()
+        bad3 = [k for k, v in out3.items() if torch.is_tensor(v) and not bool(torch.isfinite(v).all())]
+        print(f"  graphed re-run from the snapshot (same batch): non-finite={bad3}", file=sys.stderr, flush=True)
+        report("graphed again")
+        raise SystemExit(3)
+
+
 def bench_ppo(args):
     """PPO coupled on CartPole-v1 (``exp=ppo``: 1 env per rank, rollout 128, 10 epochs, minibatch 64,
     64-unit tanh MLPs).  One bench step = one PPO update: the 128-step rollout (policy forward +
@@ -350,9 +421,9 @@ def bench_ppo(args):
                 for ep in info["final_info"]:
                     if ep is not None and "episode" in ep:
                         returns_seen.append(float(np.asarray(ep["episode"]["r"]).reshape(-1)[0]))
-        data = {k: torch.from_numpy(obs_host[k]).to(device, non_blocking=True) for k in obs_keys}
-        data["rewards"] = torch.from_numpy(rew_host).to(device, non_blocking=True)
-        data["dones"] = torch.from_numpy(done_host).to(device, non_blocking=True)
+        data = {k: torch.from_numpy(obs_host[k]).to(device) for k in obs_keys}
+        data["rewards"] = torch.from_numpy(rew_host).to(device)
+        data["dones"] = torch.from_numpy(done_host).to(device)
         data.update({n: v for n, v in buf.items()})
         with torch.no_grad():
             nv = agent.get_value({k: torch.from_numpy(cur[k]).to(device) for k in obs_keys})

@@ -180,7 +180,7 @@ def to_torch_obs(obs: Dict[str, np.ndarray], keys: Sequence[str], mlp_keys: Sequ
             t = t.view(num_envs, -1, *t.shape[-2:])
         if k in mlp_keys:
             t = t.float()
-        out[k] = t.to(device, non_blocking=True)
+        out[k] = t.to(device, non_blocking=t.is_pinned())
     return out
 
 

@@ -140,7 +140,7 @@ def run_dreamer_loop(runner, cfg, state, envs, spec: DreamerSpec, aggregator, rb
                 with torch.no_grad():
                     pre = {}
                     for k, v in obs.items():
-                        v = v[None].to(device, non_blocking=True)
+                        v = v[None].to(device, non_blocking=v.is_pinned())
                         pre[k] = v / 255.0 + spec.obs_offset if k in cfg.cnn_keys.encoder else v
                     mask = {k: v for k, v in pre.items() if k.startswith("mask")} or None
                     real_actions = actions = player.get_exploration_action(pre, is_continuous, mask)

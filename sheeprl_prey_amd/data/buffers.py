@@ -170,9 +170,12 @@ class ReplayBuffer:
         if dev.type != "cpu" and len(idxes) == next_pos - self._pos > 0:
             # contiguous rows: a slice copy, no index upload
             for k, v in data_to_store.items():
-                # pinned / device sources copy without blocking the host (stream-ordered); pageable
-                # host sources still copy synchronously, so callers may reuse them at once
-                self._buf._data[k][self._pos : next_pos].copy_(v, non_blocking=True)
+                # pinned / device sources copy without blocking the host (stream-ordered).  A pageable
+                # host source must copy synchronously: an async DMA from pageable memory may read it
+                # after the caller has freed or overwritten it (seen as NaN gradients once the
+                # stream runs a captured train step ahead of the host)
+                nb = v.device.type != "cpu" or v.is_pinned()
+                self._buf._data[k][self._pos : next_pos].copy_(v, non_blocking=nb)
         else:
             idxes = idxes.to(dev)
             for k, v in data_to_store.items():

@@ -487,8 +487,23 @@ bool launch_ln_act_fwd(const float* x, int ldx, float* y, int ldy, const float* 
   return false;
 }
 
+// Zero the atomic-accumulation targets with a kernel, not hipMemsetAsync: under hipGraph stream
+// capture the memset did not reliably precede the atomics (stale sums showed up as garbage bias
+// gradients, up to 1.5e38, in replayed DreamerV3 steps; eager runs were clean).
+__global__ void __launch_bounds__(256) zero2_kernel(float* __restrict__ a, float* __restrict__ b, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    a[i] = 0.f;
+    if (b) b[i] = 0.f;
+  }
+}
+
+static void launch_zero2(float* a, float* b, int n, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(zero2_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, a, b, n);
+}
+
 void launch_colsum1(const float* x, int ldx, float* out, int rows, int N, hipStream_t st) {
-  hipMemsetAsync(out, 0, sizeof(float) * (size_t)N, st);
+  launch_zero2(out, nullptr, N, st);
   int S = cdiv(rows, 128);
   if (S > 64) S = 64;
   if (S < 1) S = 1;
@@ -496,9 +511,8 @@ void launch_colsum1(const float* x, int ldx, float* out, int rows, int N, hipStr
 }
 
 void launch_colsum2(const float* pa, const float* pb, float* oa, float* ob, int rows, int N, int G, hipStream_t st) {
-  // memset nodes + one kernel (graph-capturable); ~64 partial rows per split
-  hipMemsetAsync(oa, 0, sizeof(float) * (size_t)G * N, st);
-  hipMemsetAsync(ob, 0, sizeof(float) * (size_t)G * N, st);
+  // zero kernel + one reduction kernel (graph-capturable); ~64 partial rows per split
+  launch_zero2(oa, ob, G * N, st);
   const int Rg = cdiv(rows, G > 0 ? G : 1);
   int S = cdiv(Rg, 64);
   if (S > 32) S = 32;

@@ -529,18 +529,24 @@ __global__ void __launch_bounds__(PT_THREADS) ppo_mlp_train_kernel(PTArgs p) {
   }
 }
 
+// resets the loss sums and the grid-barrier counter; a kernel rather than hipMemsetAsync so the
+// reset is ordered like every other captured kernel inside a hipGraph (see norm.hip: zero2_kernel)
+__global__ void ppo_reset_kernel(float* sums, int* bar) {
+  if (threadIdx.x < 3) sums[threadIdx.x] = 0.f;
+  if (threadIdx.x == 0 && bar) *bar = 0;
+}
+
 }  // namespace srl
 
 hipError_t launch_ppo_mlp_train(const srl::PTArgs& p, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(p.out_sums, 0, 3 * sizeof(float), st);
+  hipLaunchKernelGGL(srl::ppo_reset_kernel, dim3(1), dim3(64), 0, st, p.out_sums, p.nwg <= 1 ? nullptr : p.bar);
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (p.nwg <= 1) {
     hipLaunchKernelGGL(srl::ppo_mlp_train_kernel, dim3(1), dim3(srl::PT_THREADS), 0, st, p);
     return hipGetLastError();
   }
   // the workgroups meet at grid barriers: a cooperative launch guarantees (and checks) co-residency
-  e = hipMemsetAsync(p.bar, 0, sizeof(int), st);
-  if (e != hipSuccess) return e;
   srl::PTArgs a = p;
   void* args[] = {(void*)&a};
   return hipLaunchCooperativeKernel((const void*)srl::ppo_mlp_train_kernel, dim3(p.nwg), dim3(srl::PT_THREADS), args, 0, st);

@@ -32,7 +32,7 @@ class GraphedStep:
 
     def _copy_in(self, data: Dict[str, Tensor]) -> None:
         for k, v in data.items():
-            self.static_in[k].copy_(v, non_blocking=True)
+            self.static_in[k].copy_(v, non_blocking=v.device.type != "cpu" or v.is_pinned())
 
     def __call__(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:
         if not self.enabled:
@@ -119,7 +119,7 @@ class SegmentedGraph:
         if self.static_in is None:
             self.static_in = {k: v.detach().clone() for k, v in data.items()}
         for k, v in data.items():
-            self.static_in[k].copy_(v, non_blocking=True)
+            self.static_in[k].copy_(v, non_blocking=v.device.type != "cpu" or v.is_pinned())
         if self.graphs is not None:
             self._replay_all()
             return self.static_out

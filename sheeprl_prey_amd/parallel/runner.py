@@ -223,7 +223,7 @@ class Runner:
 
     def to_device(self, x):
         if isinstance(x, Tensor):
-            return x.to(self.device, non_blocking=True)
+            return x.to(self.device, non_blocking=x.is_pinned() or x.device.type != "cpu")
         if isinstance(x, dict):
             return {k: self.to_device(v) for k, v in x.items()}
         return x

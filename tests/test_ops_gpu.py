@@ -206,3 +206,34 @@ def test_linear_gemv_bias_grad(shape, out_f):
     _close(out1, out0)
     for a, c in zip(g1, g0):
         torch.testing.assert_close(a, c, rtol=1e-4, atol=1e-3)
+
+
+def test_colsum_graph_replay_zeroes_accumulator():
+    """Regression: colsum1/colsum2 accumulate with atomics into a zeroed output.  Under hipGraph
+    capture a hipMemsetAsync zeroing did not reliably precede the atomics, so replays summed onto
+    stale values (garbage Linear bias / LN gradients in captured DreamerV3 steps).  The zeroing is a
+    kernel now: dirty the outputs between replays and require exact sums every time."""
+    C = ops._ext()
+    x = torch.randn(4096, 255, device=DEV)
+    pa, pb = torch.randn(96, 512, device=DEV), torch.randn(96, 512, device=DEV)
+    oa, ob = torch.empty(2, 512, device=DEV), torch.empty(2, 512, device=DEV)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        out = C.colsum(x)
+        C.colsum2(pa, pb, oa, ob, 96, 512, 2)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = C.colsum(x)
+        C.colsum2(pa, pb, oa, ob, 96, 512, 2)
+    ref_a = torch.stack([pa[0::2].sum(0), pa[1::2].sum(0)])
+    ref_b = torch.stack([pb[0::2].sum(0), pb[1::2].sum(0)])
+    for _ in range(3):
+        for t in (out, oa, ob):
+            t.fill_(1e30)
+        g.replay()
+        torch.cuda.synchronize()
+        _close(out, x.sum(0), rtol=1e-4, atol=1e-3)
+        _close(oa, ref_a, rtol=1e-4, atol=1e-4)
+        _close(ob, ref_b, rtol=1e-4, atol=1e-4)
