@@ -71,7 +71,7 @@ struct DownGather {
   const float* Q;
   int lCb, lSH, lSW, M;
   int pix[NV], py[NV], px[NV];  // per slot: n*LH*LW, 2p-1, 2q-1 (pix = -1: row out of range)
-  __device__ void init(int m0) {
+  __device__ void init(int m0, int) {
     const int LH = 2 << lSH, LW = 2 << lSW;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -112,8 +112,8 @@ struct UpGather {
   const float* P;
   int lCa, lSH, lSW, M;
   int pix[NV], pu[NV], pv[NV];
-  __device__ void init(int m0) {
-    const int cy = blockIdx.z >> 1, cx = blockIdx.z & 1;
+  __device__ void init(int m0, int cls) {
+    const int cy = cls >> 1, cx = cls & 1;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int idx = threadIdx.x + NTH * v, m = m0 + (idx >> 3);
@@ -151,9 +151,9 @@ struct Dense {
   static constexpr int NV = ROWS * BK / 4 / NTH;
   const float* W;
   int K;
-  size_t cls_stride;  // UP: per parity-class packed block (blockIdx.z); 0 otherwise
+  size_t cls_stride;  // UP: per parity-class packed block; 0 otherwise
   const float* base;
-  __device__ void init(int n0) { base = W + cls_stride * blockIdx.z + (size_t)n0 * K; }
+  __device__ void init(int n0, int cls) { base = W + cls_stride * cls + (size_t)n0 * K; }
   __device__ void load(int k0, f4* r) const {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -237,13 +237,15 @@ struct WgQ {
 // ------------------------------------------------------------------------------ row geometry
 // Maps a GEMM output row (pixel of the kernel's M space) to its pixel index in the output grid.
 struct RowDown {  // rows are the output pixels themselves
+  int cls;
   __device__ int operator()(int m) const { return m; }
 };
 struct RowUp {  // rows are parity-class pixels of the large grid
   int lSH, lSW;
+  int cls;  // parity class of this workgroup (set by the kernel)
   __device__ int operator()(int m) const {
     const int n = m >> (lSH + lSW), u = (m >> lSW) & ((1 << lSH) - 1), v = m & ((1 << lSW) - 1);
-    const int cy = blockIdx.z >> 1, cx = blockIdx.z & 1;
+    const int cy = cls >> 1, cx = cls & 1;
     return ((n << (lSH + 1)) + 2 * u + cy) * (2 << lSW) + 2 * v + cx;
   }
 };
@@ -261,12 +263,17 @@ struct Frag {
 // processed by LPR lanes (CPL contiguous channels each: vector loads/stores, row reductions by xor
 // shuffles inside the LPR-lane segment).  This keeps the epilogue's register footprint small, so
 // the MFMA main loop keeps its occupancy.
+// Four channels per lane (16 B vector LDS reads / global stores; a row of 32 channels is 8 lanes, so a
+// row reduction is 3 xor levels and a wave covers 8 rows per pass).  One channel per lane (the first
+// version, 32/64 lanes per row) made the LN epilogue of the narrow E1 / D4 layers (K = 64: two
+// main-loop stages) dominate their kernels: 14% MFMA busy, 57% of wave cycles parked.
 template <int BN>
 struct RowGeo {
-  static constexpr int LPR = BN < 64 ? BN : 64;  // lanes per row
+  static constexpr int CPL = 4;                  // channels per lane
+  static constexpr int LPR = BN / CPL;           // lanes per row
   static constexpr int RPW = 64 / LPR;           // rows per wave pass
-  static constexpr int CPL = BN / LPR;           // channels per lane
   static constexpr int PITCH = BN + 4;           // LDS row pitch (floats)
+  static_assert(LPR >= 1 && LPR <= 64 && BN % CPL == 0, "RowGeo: BN must be 4..256");
 };
 
 template <int TM, int TN, int WN>
@@ -477,7 +484,7 @@ struct EpiPlain : EpiPlainP {  // out = acc + bias[c] + c0 for c < Nreal; NHWC (
 // Tile BM x BN, WM x WN waves of (TM*32) x (TN*32); 64*WM*WN threads; one LDS stage + register
 // prefetch of the next stage.
 template <int BM, int BN, int WM, int WN, class LA, class LB, class EP, class RM>
-__global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep, RM rm, int K) {
+__global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep, RM rm, int K, int ncls, int remap) {
   constexpr int NTH = 64 * WM * WN, TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(TM >= 1 && TN >= 1 && TM * WM * 32 == BM && TN * WN * 32 == BN, "bad tile");
   constexpr int LDS_MAIN = (BM + BN) * LDK;
@@ -485,9 +492,22 @@ __global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep,
   __shared__ float lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
   float* As = lds;
   float* Bs = lds + BM * LDK;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  la.init(m0);
-  lb.init(n0);
+  // XCD-aware tile order (remap): the hardware deals workgroups round-robin over the 8 XCDs, so
+  // XCD x runs blocks x, x+8, ...; give it a contiguous run of M tiles (halo rows shared in its L2)
+  // with the ncls parity classes of a tile back to back (UP: the 4 classes read the same input pixels)
+  int mt, cls;
+  if (remap) {
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3, per = ((int)gridDim.x >> 3) / ncls;
+    cls = j % ncls;
+    mt = x * per + j / ncls;
+  } else {
+    mt = blockIdx.x;
+    cls = blockIdx.z;
+  }
+  const int m0 = mt * BM, n0 = blockIdx.y * BN;
+  la.init(m0, cls);
+  lb.init(n0, cls);
+  rm.cls = cls;
   Frag<TM, TN, WN> f;
   f.lane = threadIdx.x & 63;
   f.wm = (threadIdx.x >> 6) / WN;
@@ -774,21 +794,23 @@ void launch(K kernel, dim3 grid, dim3 block, hipStream_t st, Args... args) {
 }  // namespace
 
 template <int BM, int BN, int WM, int WN, class LA, class RM>
-static void dispatch_epi(const LA& la, const Dense<BN, 64 * WM * WN>& lb, const ConvEpi& e, const RM& rm, int K, dim3 grid,
-                         hipStream_t st) {
+static void dispatch_epi(const LA& la, const Dense<BN, 64 * WM * WN>& lb, const ConvEpi& e, const RM& rm, int K, int mtiles,
+                         int ncls, hipStream_t st) {
   dim3 block(64 * WM * WN);
+  const int remap = mtiles % 8 == 0 ? 1 : 0;
+  const dim3 grid = remap ? dim3(mtiles * ncls, 1, 1) : dim3(mtiles, 1, ncls);
   if (e.mode == 0) {
     EpiLNAct ep;
     static_cast<EpiLNActP&>(ep) = e.ln;
-    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNAct, RM>, grid, block, st, la, lb, ep, rm, K);
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNAct, RM>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
   } else if (e.mode == 1) {
     EpiLNBwd ep;
     static_cast<EpiLNBwdP&>(ep) = e.lb;
-    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNBwd, RM>, grid, block, st, la, lb, ep, rm, K);
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNBwd, RM>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
   } else {
     EpiPlain ep;
     static_cast<EpiPlainP&>(ep) = e.pl;
-    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiPlain, RM>, grid, block, st, la, lb, ep, rm, K);
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiPlain, RM>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
   }
 }
 
@@ -807,7 +829,7 @@ static void down_cfg(const float* Q, const float* Wp, int N, int SH, int SW, int
   lb.W = Wp;
   lb.K = 16 * Cb;
   lb.cls_stride = 0;
-  dispatch_epi<BM, BN, WM, WN>(la, lb, e, RowDown{}, 16 * Cb, dim3((M + BM - 1) / BM, 1, 1), st);
+  dispatch_epi<BM, BN, WM, WN>(la, lb, e, RowDown{0}, 16 * Cb, (M + BM - 1) / BM, 1, st);
 }
 
 bool launch_conv_down(const float* Q, const float* Wp, int N, int SH, int SW, int Cb, int Nc, const ConvEpi& e,
@@ -835,8 +857,8 @@ static void up_cfg(const float* P, const float* Wp, int N, int SH, int SW, int C
   lb.W = Wp;
   lb.K = 4 * Ca;
   lb.cls_stride = (size_t)Bp * 4 * Ca;
-  RowUp rm{ilog2(SH), ilog2(SW)};
-  dispatch_epi<BM, BN, WM, WN>(la, lb, e, rm, 4 * Ca, dim3((M + BM - 1) / BM, 1, 4), st);
+  RowUp rm{ilog2(SH), ilog2(SW), 0};
+  dispatch_epi<BM, BN, WM, WN>(la, lb, e, rm, 4 * Ca, (M + BM - 1) / BM, 4, st);
 }
 
 // UP: P NHWC (N, SH, SW, Ca) -> out grid (N, 2SH, 2SW) with Bp output channels (pack padding)
