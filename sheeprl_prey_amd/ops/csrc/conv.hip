@@ -722,19 +722,31 @@ __global__ __launch_bounds__(256) void ln_bwd_flat_kernel(const float* __restric
 
 // ConvT forward to a tiny channel count (the decoder's last layer, 3 image channels), on VALU:
 // a workgroup owns a 16x16 tile of small-grid pixels of one image (+1 halo) staged in LDS (NHWC,
-// Ca channels) and produces the 32x32 large-grid outputs; weights [Ca][CO][4][4] in LDS.
+// Ca channels); thread = one small-grid pixel (u, v), producing its 2x2 large-grid outputs (the 4
+// parity classes).  The class / tap loops are workgroup-uniform, so the weights are read as LDS
+// broadcasts ([tap][a][CO padded to 4]: one 16 B read per (tap, a)), one per-lane LDS read of the
+// input channel feeds CO FMAs, and each output row pair is written as float2 (x = 2v, 2v+1).
+// (First version: lanes of one wave mixed parity classes, so every FMA needed its own divergent
+// LDS weight read - LDS-bound at ~180 us for N=1024.)
 // out NCHW [n][co][y][x] = bias[co] + c0 + sum.
 template <int CO, int CA>
 __global__ __launch_bounds__(256) void up_small_kernel(const float* __restrict__ P, const float* __restrict__ W,
                                                        const float* __restrict__ bias, float c0, float* __restrict__ out,
                                                        int lSH, int lSW) {
+  static_assert(CO <= 4, "up_small: CO <= 4");
   constexpr int T = 16, TH = T + 2;
   __shared__ float tile[TH * TH * (CA + 1)];
-  __shared__ float ws[CA * CO * 16];
+  __shared__ f4 ws[16 * CA];  // [kh*4+kw][a] -> (co 0..3)
   const int SH = 1 << lSH, SW = 1 << lSW;
   const int tx = SW / T;
   const int n = blockIdx.y, ty0 = (blockIdx.x / tx) * T, tx0 = (blockIdx.x % tx) * T;
-  for (int i = threadIdx.x; i < CA * CO * 16; i += 256) ws[i] = W[i];
+  for (int i = threadIdx.x; i < 16 * CA; i += 256) {
+    const int tap = i / CA, a = i % CA;
+    f4 w = zero4();
+#pragma unroll
+    for (int c = 0; c < CO; ++c) w[c] = W[(a * CO + c) * 16 + tap];
+    ws[i] = w;
+  }
   for (int i = threadIdx.x; i < TH * TH * (CA / 4); i += 256) {
     const int pixl = i / (CA / 4), aq = i % (CA / 4);
     const int p = ty0 - 1 + pixl / TH, q = tx0 - 1 + pixl % TH;
@@ -748,30 +760,36 @@ __global__ __launch_bounds__(256) void up_small_kernel(const float* __restrict__
   }
   __syncthreads();
   const int LH = 2 * SH, LW = 2 * SW;
-  // 1024 outputs per block (32x32), 4 per thread: thread -> (yy, xx pair)
-  for (int o = threadIdx.x; o < 4 * T * T; o += 256) {
-    const int yy = o / (2 * T), xx = o % (2 * T);
-    const int y = 2 * ty0 + yy, x = 2 * tx0 + xx;
-    const int cy = yy & 1, cx = xx & 1, u = yy >> 1, v = xx >> 1;
-    float s[CO];
+  const int u = threadIdx.x >> 4, v = threadIdx.x & 15;
+  float s[2][2][CO];
 #pragma unroll
-    for (int c = 0; c < CO; ++c) s[c] = 0.f;
+  for (int cy = 0; cy < 2; ++cy)
 #pragma unroll
-    for (int th = 0; th < 2; ++th)
+    for (int cx = 0; cx < 2; ++cx) {
 #pragma unroll
-      for (int tw = 0; tw < 2; ++tw) {
-        const int pl = (u + cy - th + 1) * TH + (v + cx - tw + 1);
-        const int kh = 1 - cy + 2 * th, kw = 1 - cx + 2 * tw;
-        const float* src = tile + pl * (CA + 1);
+      for (int c = 0; c < CO; ++c) s[cy][cx][c] = 0.f;
+#pragma unroll
+      for (int th = 0; th < 2; ++th)
+#pragma unroll
+        for (int tw = 0; tw < 2; ++tw) {
+          const float* src = tile + ((u + cy - th + 1) * TH + (v + cx - tw + 1)) * (CA + 1);
+          const f4* wt = ws + ((1 - cy + 2 * th) * 4 + (1 - cx + 2 * tw)) * CA;
 #pragma unroll 8
-        for (int a = 0; a < CA; ++a) {
-          const float pv = src[a];
+          for (int a = 0; a < CA; ++a) {
+            const float pv = src[a];
+            const f4 w = wt[a];
 #pragma unroll
-          for (int c = 0; c < CO; ++c) s[c] += pv * ws[(a * CO + c) * 16 + kh * 4 + kw];
+            for (int c = 0; c < CO; ++c) s[cy][cx][c] += pv * w[c];
+          }
         }
-      }
+    }
+  const int y0 = 2 * (ty0 + u), x0 = 2 * (tx0 + v);
 #pragma unroll
-    for (int c = 0; c < CO; ++c) out[(((size_t)n * CO + c) * LH + y) * LW + x] = s[c] + (bias ? bias[c] : 0.f) + c0;
+  for (int c = 0; c < CO; ++c) {
+    const float b = (bias ? bias[c] : 0.f) + c0;
+#pragma unroll
+    for (int cy = 0; cy < 2; ++cy)
+      *(float2*)(out + (((size_t)n * CO + c) * LH + y0 + cy) * LW + x0) = make_float2(s[cy][0][c] + b, s[cy][1][c] + b);
   }
 }
 
