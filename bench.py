@@ -47,6 +47,8 @@ def parse():
                    help="per-phase hipGraphs with event timing (diagnostic; adds syncs, not a bench number)")
     p.add_argument("--check-finite", type=int, default=0,
                    help="diagnostic: run N untimed steps, report the first non-finite train output per step")
+    p.add_argument("--host-times", action="store_true",
+                   help="diagnostic: host wall time per part of a bench step (act+readback / sample+launch / env)")
     p.add_argument("overrides", nargs="*")
     return p.parse_args()
 
@@ -153,6 +155,35 @@ def main():
             step_data["is_first"][idx] = 1.0
             player.init_states(idx)
 
+    # pipelined policy step (timed loop): the row's host data is staged in pinned buffers (two, used
+    # alternately) so the replay add, the batch sample and the train-graph launch are all enqueued
+    # right behind the player graph; the host then waits only for the action readback (an event
+    # after the player), steps the env, and the GPU goes from the player straight into training.
+    row_keys = obs_keys + ["rewards", "dones", "is_first"]
+    staging = [{k: torch.empty_like(step_data[k]).pin_memory() for k in row_keys} for _ in range(2)]
+    real_pin = torch.empty((len(actions_dim), cfg.env.num_envs), dtype=torch.int64).pin_memory()
+    act_ev = torch.cuda.Event()
+    slot = [0]
+
+    def act_add_train():
+        # buffer `slot` was last read by copies enqueued before the player of the previous step,
+        # whose readback event this host thread has already waited on
+        b = staging[slot[0]]
+        slot[0] ^= 1
+        for k in row_keys:
+            b[k].copy_(step_data[k])
+        with torch.no_grad():
+            pre = {k: b[k][None].to(device, non_blocking=True) / 255.0 for k in obs_keys}
+            a = player.get_exploration_action(pre, is_continuous)
+            acts = torch.cat(a, -1).view(cfg.env.num_envs, -1)
+            real_pin.copy_(torch.stack([x.argmax(-1) for x in a]).view(len(actions_dim), -1), non_blocking=True)
+            act_ev.record()
+        row = TensorDict({**{k: b[k] for k in row_keys}, "actions": acts}, batch_size=[cfg.env.num_envs])
+        rb.add(row[None, ...])
+        out = train_once()
+        act_ev.synchronize()
+        return real_pin.numpy().copy(), out
+
     grad_steps = 0
     last_batch = [None]
 
@@ -170,19 +201,35 @@ def main():
         env_advance(act_and_add(True))
 
     env_ms = [0.0]
+    host_ms = [0.0, 0.0, 0.0, 0]
 
     def one_step():
         # act (weights W_t) -> store the row -> launch the gradient step (async, W_t -> W_t+1) -> step
         # the env on the CPU while the GPU trains (the env step needs only the action): the same
-        # order of effects as the reference's act / env-step / add / train loop
+        # order of effects as the reference's act / env-step / add / train loop.  Default: the
+        # pipelined act_add_train; --phase-times / --host-times time the serial form of the same step.
         if args.phase_times:
             torch.cuda.synchronize()
             t = time.perf_counter()
             real = act_and_add(False)
             torch.cuda.synchronize()
             env_ms[0] += (time.perf_counter() - t) * 1e3
+        elif args.host_times:
+            t0 = time.perf_counter()
+            real = act_and_add(False)  # player graph + action readback (waits for the previous step)
+            t1 = time.perf_counter()
+            out = train_once()  # replay sample + train-graph launch
+            t2 = time.perf_counter()
+            env_advance(real)  # CPU env step, overlapping the GPU train step
+            t3 = time.perf_counter()
+            for i, d in enumerate((t1 - t0, t2 - t1, t3 - t2)):
+                host_ms[i] += d * 1e3
+            host_ms[3] += 1
+            return out
         else:
-            real = act_and_add(False)
+            real, out = act_add_train()
+            env_advance(real)
+            return out
         out = train_once()
         env_advance(real)
         return out
@@ -221,6 +268,7 @@ def main():
     if args.profile_steps:
         torch.cuda._sleep(1000)  # marker kernel: scripts/trace_window.py aggregates the dispatches after it
         torch.cuda.synchronize()
+    host_ms[:] = [0.0, 0.0, 0.0, 0]
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = one_step()
@@ -229,6 +277,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if args.host_times and rank == 0 and host_ms[3]:
+        n = host_ms[3]
+        print(f"host ms/step: act+readback {host_ms[0] / n:.3f}, sample+launch {host_ms[1] / n:.3f}, "
+              f"env step {host_ms[2] / n:.3f}", file=sys.stderr, flush=True)
     if args.phase_times and rank == 0:
         seg = trainer.seg
         if seg.phase_ms is not None and seg.timed_steps:
