@@ -49,6 +49,8 @@ def parse():
                    help="diagnostic: run N untimed steps, report the first non-finite train output per step")
     p.add_argument("--host-times", action="store_true",
                    help="diagnostic: host wall time per part of a bench step (act+readback / sample+launch / env)")
+    p.add_argument("--gemm-tuning", default=None, choices=["use", "tune", "off"],
+                   help="library-GEMM TunableOp mode (default: fabric.tunable_gemm = use the committed results)")
     p.add_argument("overrides", nargs="*")
     return p.parse_args()
 
@@ -85,7 +87,7 @@ def main():
         "exp=dreamer_v3_100k_ms_pacman", "env=synthetic_atari", "env.sync_env=True",
         "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]", "fabric.accelerator=cuda",
         f"fabric.cuda_graphs={not args.no_graphs}", "metric.log_every=1000000000",
-    ] + list(args.overrides)
+    ] + ([f"fabric.tunable_gemm={args.gemm_tuning}"] if args.gemm_tuning else []) + list(args.overrides)
     cfg = dotdict(compose(overrides))
     cfg.pop("hydra", None)
     runner = Runner(**{k: v for k, v in cfg.fabric.items()})

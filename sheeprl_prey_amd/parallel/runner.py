@@ -90,6 +90,7 @@ class Runner:
         cuda_graphs: bool = False,
         fused_ops: bool = True,
         bucket_mb: int = 32,
+        tunable_gemm: str = "use",
         process_group=None,
         **_unused,
     ) -> None:
@@ -105,9 +106,12 @@ class Runner:
         self.cuda_graphs = bool(cuda_graphs) and self.accelerator == "cuda"
         self.fused_ops = bool(fused_ops)
         self.bucket_mb = int(bucket_mb)
+        # library-GEMM solution choice (parallel/gemm_tuning.py): committed TunableOp results
+        self.tunable_gemm = str(tunable_gemm)
         self._kwargs = dict(
             devices=devices, num_nodes=num_nodes, strategy=strategy, accelerator=accelerator,
             precision=precision, callbacks=callbacks, cuda_graphs=cuda_graphs, fused_ops=fused_ops, bucket_mb=bucket_mb,
+            tunable_gemm=tunable_gemm,
         )
         self.group = process_group  # None == WORLD
         if str(strategy).lower() in ("fsdp",):
@@ -168,6 +172,9 @@ class Runner:
         ws = int(os.environ.get("WORLD_SIZE", "1"))
         if self.accelerator == "cuda":
             torch.cuda.set_device(self.device)
+            from sheeprl_prey_amd.parallel.gemm_tuning import configure
+
+            configure(self.tunable_gemm)
         if ws > 1 and not dist.is_initialized():
             kwargs = dict(backend=self.backend, timeout=datetime.timedelta(minutes=30))
             if self.accelerator == "cuda" and self.backend == "nccl":
@@ -182,6 +189,9 @@ class Runner:
                 self._init_distributed()
             elif self.accelerator == "cuda":
                 torch.cuda.set_device(self.device)
+                from sheeprl_prey_amd.parallel.gemm_tuning import configure
+
+                configure(self.tunable_gemm)
             return fn(self, cfg)
         import torch.multiprocessing as mp
 

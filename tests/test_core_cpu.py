@@ -252,3 +252,18 @@ def test_mask_velocities_requires_known_env():
     assert o[1] == 0 and o[3] == 0
     with pytest.raises(NotImplementedError):
         MaskVelocityWrapper(ContinuousDummyEnv(size=(4,)))
+
+
+def test_gemm_tuning_modes_cpu():
+    """parallel/gemm_tuning: YAML booleans map to modes; without a GPU nothing is enabled; the
+    committed MI355X TunableOp results file exists and carries its validators."""
+    import os
+
+    from sheeprl_prey_amd.parallel import gemm_tuning
+
+    assert gemm_tuning.configure(False) is False
+    assert gemm_tuning.configure("off") is False
+    assert gemm_tuning.configure("use") is False  # no GPU in the CPU suite
+    assert os.path.exists(gemm_tuning.RESULTS)
+    head = open(gemm_tuning.RESULTS).read().splitlines()[:5]
+    assert any(line.startswith("Validator,GCN_ARCH_NAME,gfx950") for line in head)

@@ -42,3 +42,17 @@ def test_segmented_graph_collective_sees_phase_gradients():
     assert len(seen) == 6 and all(s > 0 for s in seen), seen
     # ... and its result (zeros) is what the optimiser applied: no update at all
     torch.testing.assert_close(opt.flat_param, before)
+
+
+def test_gemm_tuning_use_loads_results():
+    import torch.cuda.tunable as tun
+
+    from sheeprl_prey_amd.parallel import gemm_tuning
+
+    try:
+        assert gemm_tuning.configure("use") is True
+        assert tun.is_enabled() and not tun.tuning_is_enabled()
+        a, b = torch.randn(1024, 512, device="cuda"), torch.randn(512, 1536, device="cuda")
+        torch.testing.assert_close(a @ b, (a.double() @ b.double()).float(), rtol=1e-4, atol=1e-3)
+    finally:
+        tun.enable(False)
