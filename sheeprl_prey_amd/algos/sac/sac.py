@@ -57,6 +57,7 @@ class SACTrainer:
         self.critic_params = list(agent.critic.parameters())
         self.actor_params = [p for p in agent.actor.parameters() if p.requires_grad]
         self._st: Dict[str, Tensor] = {}
+        self._ema_w: Dict[Any, Tensor] = {}
         use_graphs = bool(cfg.fabric.get("cuda_graphs", False)) if graphs is None else graphs
         self.critic_step = PhasedStep(runner, [self._critic_fwd_bwd, self._critic_apply], [self._coll_critic],
                                       graphs=use_graphs, name="sac_critic")
@@ -111,7 +112,11 @@ class SACTrainer:
 
     # ------------------------------------------------------------------ API
     def ema_weight(self, do_update: bool, device) -> Tensor:
-        return torch.tensor([self.agent.tau if do_update else 0.0], device=device)
+        # two cached device scalars: no per-step host->device copy (a pageable copy syncs the stream)
+        key = (bool(do_update), str(device))
+        if key not in self._ema_w:
+            self._ema_w[key] = torch.tensor([self.agent.tau if do_update else 0.0], device=device)
+        return self._ema_w[key]
 
     def train(self, data: Dict[str, Tensor], do_ema: bool, aggregator: Optional[MetricAggregator] = None) -> None:
         """One SAC ``train`` call (reference ``sac/sac.py:34-78``) on a minibatch."""
@@ -264,6 +269,23 @@ def run_sac_family(runner, cfg: Dict[str, Any], variant: str = "sac"):
 
     o = envs.reset(seed=cfg.seed)[0]
     obs = obs_to_tensor(o, cfg.mlp_keys.encoder, rb.device, cfg.env.num_envs)
+    # GPU: the player's actor forward is one hipGraph replay, and each env step's row (next obs, real
+    # next obs, actions, reward, done) goes to the device as ONE pinned copy sliced on the device
+    # (instead of five synchronous pageable copies).  The staging buffer is rewritten only after an event
+    # recorded behind its last copy has completed.
+    gpu_row = rb.device.type == "cuda"
+    if gpu_row:
+        from sheeprl_prey_amd.parallel.graphs import GraphedStep
+
+        n_env, act_dim = cfg.env.num_envs, int(np.prod(action_space.shape))
+        stage = torch.empty((n_env, 2 * obs_dim + act_dim + 2), dtype=torch.float32).pin_memory()
+        staged = torch.cuda.Event()  # the last copy out of `stage` (random-action steps have no readback)
+        player = GraphedStep(lambda d: {"a": agent.actor(d["obs"])[0]}, warmup=2, enabled=runner.cuda_graphs,
+                             name="sac_player")
+
+    def host_rows(x: Dict[str, Any]) -> np.ndarray:
+        return np.concatenate([np.asarray(x[k], dtype=np.float32).reshape(cfg.env.num_envs, -1)
+                               for k in cfg.mlp_keys.encoder], -1)
 
     for update in range(start_step, num_updates + 1):
         policy_step += cfg.env.num_envs * world_size
@@ -272,8 +294,11 @@ def run_sac_family(runner, cfg: Dict[str, Any], variant: str = "sac"):
                 actions = envs.action_space.sample()
             else:
                 with torch.no_grad():
-                    actions, _ = agent.actor(obs.to(device))
-                    actions = actions.cpu().numpy()
+                    if gpu_row:
+                        actions = player({"obs": obs})["a"].cpu().numpy()
+                    else:
+                        actions, _ = agent.actor(obs.to(device))
+                        actions = actions.cpu().numpy()
             next_o, rewards, dones, truncated, infos = envs.step(actions.reshape(envs.action_space.shape))
             dones = np.logical_or(dones, truncated)
 
@@ -282,14 +307,32 @@ def run_sac_family(runner, cfg: Dict[str, Any], variant: str = "sac"):
             aggregator.update("Game/ep_len_avg", ep_len)
             runner.print(f"Rank-0: policy_step={policy_step}, reward_env_{i}={ep_rew[-1]}")
 
-        next_obs = obs_to_tensor(next_o, cfg.mlp_keys.encoder, rb.device, cfg.env.num_envs)
-        step_data["dones"] = torch.as_tensor(dones, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
-        step_data["actions"] = torch.as_tensor(actions, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
-        step_data["observations"] = obs
-        if not cfg.buffer.sample_next_obs:
-            step_data["next_observations"] = obs_to_tensor(real_next_obs(next_o, infos), cfg.mlp_keys.encoder,
-                                                           rb.device, cfg.env.num_envs)
-        step_data["rewards"] = torch.as_tensor(rewards, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
+        if gpu_row:
+            staged.synchronize()
+            st = stage.numpy()
+            st[:, :obs_dim] = host_rows(next_o)
+            st[:, obs_dim:2 * obs_dim] = host_rows(real_next_obs(next_o, infos))
+            st[:, 2 * obs_dim:2 * obs_dim + act_dim] = np.asarray(actions, dtype=np.float32).reshape(n_env, -1)
+            st[:, -2] = np.asarray(rewards, dtype=np.float32).reshape(n_env)
+            st[:, -1] = np.asarray(dones, dtype=np.float32).reshape(n_env)
+            row = stage.to(rb.device, non_blocking=True)
+            staged.record()
+            next_obs = row[:, :obs_dim]
+            step_data["dones"] = row[:, -1:]
+            step_data["actions"] = row[:, 2 * obs_dim:2 * obs_dim + act_dim]
+            step_data["observations"] = obs
+            if not cfg.buffer.sample_next_obs:
+                step_data["next_observations"] = row[:, obs_dim:2 * obs_dim]
+            step_data["rewards"] = row[:, -2:-1]
+        else:
+            next_obs = obs_to_tensor(next_o, cfg.mlp_keys.encoder, rb.device, cfg.env.num_envs)
+            step_data["dones"] = torch.as_tensor(dones, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
+            step_data["actions"] = torch.as_tensor(actions, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
+            step_data["observations"] = obs
+            if not cfg.buffer.sample_next_obs:
+                step_data["next_observations"] = obs_to_tensor(real_next_obs(next_o, infos), cfg.mlp_keys.encoder,
+                                                               rb.device, cfg.env.num_envs)
+            step_data["rewards"] = torch.as_tensor(rewards, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
         rb.add(step_data.unsqueeze(0))
         obs = next_obs
 

@@ -160,8 +160,13 @@ class SACAETrainer:
         dev = data["rewards"].device
         do_ema = update % critic_freq == 0
         d = dict(data)
-        d["ema_q"] = torch.tensor([self.agent.tau if do_ema else 0.0], device=dev)
-        d["ema_enc"] = torch.tensor([self.agent.encoder_tau if do_ema else 0.0], device=dev)
+        # cached device scalars: a per-step torch.tensor(device=...) is a synchronous H2D copy
+        cache = self.__dict__.setdefault("_ema_cache", {})
+        key = (bool(do_ema), str(dev))
+        if key not in cache:
+            cache[key] = (torch.tensor([self.agent.tau if do_ema else 0.0], device=dev),
+                          torch.tensor([self.agent.encoder_tau if do_ema else 0.0], device=dev))
+        d["ema_q"], d["ema_enc"] = cache[key]
         out = {}
         out.update(self._run(self.critic_step, d, eager))
         if update % actor_freq == 0:

@@ -19,20 +19,43 @@ class MeanMetric:
         self.sync_on_compute = sync_on_compute
         self.reset()
 
+    SLOTS = 512  # device scalars staged before one NaN-filtered reduction
+
     def reset(self) -> None:
         self._host_sum = 0.0
         self._host_n = 0
         self._dev_sum: Optional[Tensor] = None
         self._dev_n: Optional[Tensor] = None
+        self._slots: Optional[Tensor] = None
+        self._used = 0
+
+    def _flush(self) -> None:
+        if not self._used:
+            return
+        v = self._slots[: self._used]
+        finite = torch.isfinite(v)
+        self._dev_sum += torch.where(finite, v, torch.zeros_like(v)).sum().double()
+        self._dev_n += finite.sum().double()
+        self._used = 0
 
     def update(self, value: Union[float, int, Tensor, Any]) -> None:
         if isinstance(value, Tensor):
             v = value.detach()
             if v.is_cuda:
-                v = v.float().reshape(-1)
                 if self._dev_sum is None:
                     self._dev_sum = torch.zeros((), device=v.device, dtype=torch.float64)
                     self._dev_n = torch.zeros((), device=v.device, dtype=torch.float64)
+                if v.numel() == 1:
+                    # a per-step device scalar (e.g. a graph's static loss output): one copy kernel into
+                    # a staging slot, no host sync; the NaN-filtered sum runs once per SLOTS updates
+                    if self._slots is None:
+                        self._slots = torch.empty(self.SLOTS, device=v.device, dtype=torch.float32)
+                    self._slots[self._used].copy_(v.reshape(()))
+                    self._used += 1
+                    if self._used == self.SLOTS:
+                        self._flush()
+                    return
+                v = v.float().reshape(-1)
                 finite = torch.isfinite(v)
                 self._dev_sum += torch.where(finite, v, torch.zeros_like(v)).sum().double()
                 self._dev_n += finite.sum().double()
@@ -50,6 +73,7 @@ class MeanMetric:
     def compute(self) -> float:
         s, n = self._host_sum, float(self._host_n)
         if self._dev_sum is not None:
+            self._flush()
             s += float(self._dev_sum.item())
             n += float(self._dev_n.item())
         if self.sync_on_compute and torch.distributed.is_available() and torch.distributed.is_initialized():

@@ -26,6 +26,15 @@ def test_sac_gpu():
     _check_ckpt("sac", "g", SAC_KEYS, True)
 
 
+def test_sac_gpu_graphed_player_pendulum():
+    """A short non-dry SAC run on the native Pendulum: random-action steps, then the hipGraph-replayed
+    player and the single pinned row copy per env step (sac.py gpu_row path), several logs."""
+    _run(["env.num_envs=2", "env.sync_env=True", "env.capture_video=False", "exp=sac", "env=gym",
+          "env.id=Pendulum-v1", "total_steps=400", "algo.learning_starts=100", "per_rank_batch_size=32",
+          "metric.log_every=100", "checkpoint.every=0", "root_dir=sac_pend", "run_name=g"])
+    _check_ckpt("sac_pend", "g", SAC_KEYS, False)
+
+
 def test_droq_gpu():
     _run(STD + ["exp=droq", "env=dummy", "env.id=continuous_dummy_vec", "per_rank_batch_size=4", "buffer.size=8",
                 "algo.learning_starts=0", "algo.per_rank_gradient_steps=4", "root_dir=droq", "run_name=g",
