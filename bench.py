@@ -45,6 +45,9 @@ def parse():
                    help="DV3: run N extra eager steps under torch.profiler and print the aten op table (stderr)")
     p.add_argument("--phase-times", action="store_true",
                    help="per-phase hipGraphs with event timing (diagnostic; adds syncs, not a bench number)")
+    p.add_argument("--segmented", action="store_true",
+                   help="use the multi-rank graph mode (one hipGraph per phase, collectives between replays) "
+                        "on any N, to price it against the single-graph step at N=1")
     p.add_argument("--check-finite", type=int, default=0,
                    help="diagnostic: run N untimed steps, report the first non-finite train output per step")
     p.add_argument("--host-times", action="store_true",
@@ -111,7 +114,7 @@ def main():
     moments = Moments(runner, cfg.algo.actor.moments.decay, cfg.algo.actor.moments.max,
                       cfg.algo.actor.moments.percentile.low, cfg.algo.actor.moments.percentile.high).to(device)
     trainer = DreamerV3Trainer(runner, cfg, world_model, actor, critic, target_critic, wopt, aopt, copt, moments,
-                               is_continuous, actions_dim, force_segmented=args.phase_times)
+                               is_continuous, actions_dim, force_segmented=args.phase_times or args.segmented)
     n_params = sum(p.numel() for m in (world_model, actor, critic) for p in m.parameters())
     rb = AsyncReplayBuffer(cfg.buffer.size // (cfg.env.num_envs * world), cfg.env.num_envs, device=device, sequential=True)
     obs_keys = list(cfg.cnn_keys.encoder)
