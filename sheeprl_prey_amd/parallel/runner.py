@@ -28,6 +28,51 @@ import torch.nn as nn
 from torch import Tensor
 
 
+# Fabric precision strings -> autocast dtype of the forward passes of set-up modules (None: plain fp32).
+# "16-mixed" needs a loss scaler the flat-slab optimisers do not implement; "64-true" would need every
+# buffer and env tensor in fp64: both are rejected up front rather than silently run in fp32.
+_PRECISIONS = {"32-true": None, "32": None, "bf16-mixed": torch.bfloat16}
+
+
+def _autocast_dtype(precision: Any) -> Optional[torch.dtype]:
+    key = str(precision)
+    if key not in _PRECISIONS:
+        raise ValueError(f"fabric.precision={precision!r} is not supported; use one of {sorted(_PRECISIONS)}")
+    return _PRECISIONS[key]
+
+
+def _to_fp32(out: Any) -> Any:
+    if isinstance(out, Tensor):
+        return out.float() if out.is_floating_point() and out.dtype != torch.float32 else out
+    if isinstance(out, (tuple, list)):
+        return type(out)(_to_fp32(o) for o in out)
+    if isinstance(out, dict):
+        return {k: _to_fp32(v) for k, v in out.items()}
+    return out
+
+
+class _AutocastHooks:
+    """Forward pre/post hooks that run a module's ``forward`` under ``torch.autocast`` and hand fp32
+    outputs back, like Fabric's mixed-precision ``_FabricModule`` (reference ``fabric.precision``,
+    ``configs/fabric/default.yaml:5``).  Hooks, not a patched ``forward``: a deep-copied module (the
+    target critics) keeps calling its OWN weights.  Our fused ops take fp32 only, so bf16 activations
+    route through the eager reference ops (``ops/__init__.py`` dtype checks)."""
+
+    def __init__(self, device_type: str, dtype: torch.dtype) -> None:
+        self.device_type, self.dtype = device_type, dtype
+        self._stack: List[Any] = []
+
+    def pre(self, module, args):
+        ctx = torch.autocast(self.device_type, dtype=self.dtype)
+        ctx.__enter__()
+        self._stack.append(ctx)
+
+    def post(self, module, args, out):
+        if self._stack:
+            self._stack.pop().__exit__(None, None, None)
+        return _to_fp32(out)
+
+
 def _free_port() -> int:
     with closing(socket.socket(socket.AF_INET, socket.SOCK_STREAM)) as s:
         s.bind(("127.0.0.1", 0))
@@ -101,6 +146,8 @@ class Runner:
         self.num_nodes = int(num_nodes)
         self.strategy = strategy
         self.precision = precision
+        self._amp_dtype = _autocast_dtype(precision)
+        self._amp_hooks: Optional[_AutocastHooks] = None
         self.callbacks = list(callbacks or [])
         self._loggers = list(loggers or [])
         self.cuda_graphs = bool(cuda_graphs) and self.accelerator == "cuda"
@@ -239,8 +286,14 @@ class Runner:
         return x
 
     def setup_module(self, module: nn.Module) -> nn.Module:
-        """Move to device and make every rank start from rank 0's weights."""
+        """Move to device, make every rank start from rank 0's weights and, with
+        ``precision=bf16-mixed``, run the module's forward under autocast."""
         module = module.to(self.device)
+        if self._amp_dtype is not None:
+            if self._amp_hooks is None:
+                self._amp_hooks = _AutocastHooks(self.device.type, self._amp_dtype)
+            module.register_forward_pre_hook(self._amp_hooks.pre)
+            module.register_forward_hook(self._amp_hooks.post, always_call=True)
         if self.world_size > 1:
             with torch.no_grad():
                 tensors = [p.data for p in module.parameters()] + [b for b in module.buffers()]

@@ -270,3 +270,20 @@ def test_p2e_explores_then_switches(algo, env_id):
     keys = set().union(*[r.keys() for r in rows])
     assert {"Loss/ensemble_loss", "Loss/policy_loss_exploration", "Loss/value_loss_exploration",
             "Loss/policy_loss_task", "Rewards/intrinsic"} <= keys, keys
+
+
+@pytest.mark.parametrize("algo", ["ppo", "sac"])
+def test_bf16_mixed_precision(algo):
+    """``fabric.precision=bf16-mixed`` (Fabric's mixed-precision plugin in the reference): set-up
+    modules run their forward under autocast and the run trains and checkpoints as usual."""
+    env = ["env=dummy", "env.id=discrete_dummy"] if algo == "ppo" else ["env.id=Pendulum-v1", "algo.learning_starts=0",
+                                                                       "buffer.size=1", "algo.hidden_size=8"]
+    extra = ["algo.rollout_steps=1"] if algo == "ppo" else ["algo.per_rank_gradient_steps=1"]
+    _run(STD + [f"exp={algo}", "fabric.precision=bf16-mixed", "per_rank_batch_size=1", f"root_dir={algo}_bf16",
+                "run_name=r"] + env + extra, 1)
+    _check_ckpt(f"{algo}_bf16", "r", PPO_KEYS if algo == "ppo" else SAC_KEYS, False)
+
+
+def test_unsupported_precision_rejected():
+    with pytest.raises(ValueError, match="precision"):
+        _run(STD + ["exp=ppo", "env=dummy", "env.id=discrete_dummy", "fabric.precision=16-mixed"], 1)

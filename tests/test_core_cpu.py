@@ -267,3 +267,29 @@ def test_gemm_tuning_modes_cpu():
     assert os.path.exists(gemm_tuning.RESULTS)
     head = open(gemm_tuning.RESULTS).read().splitlines()[:5]
     assert any(line.startswith("Validator,GCN_ARCH_NAME,gfx950") for line in head)
+
+
+def test_bf16_mixed_setup_module_hooks():
+    """bf16-mixed runs the set-up module's forward under autocast, returns fp32, keeps fp32 grads,
+    and a deep copy (target network) keeps using its own weights."""
+    import copy
+
+    from sheeprl_prey_amd.parallel.runner import Runner
+
+    r = Runner(accelerator="cpu", precision="bf16-mixed")
+    torch.manual_seed(0)
+    m = r.setup_module(torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.Tanh(), torch.nn.Linear(16, 3)))
+    x = torch.randn(5, 8)
+    y = m(x)
+    assert y.dtype == torch.float32
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        want = m[2](m[1](m[0](x))).float()
+    torch.testing.assert_close(y, want)
+    y.sum().backward()
+    assert m[0].weight.grad.dtype == torch.float32
+    c = copy.deepcopy(m)
+    with torch.no_grad():
+        m[0].weight.zero_()
+    torch.testing.assert_close(c(x), y.detach())
+    with pytest.raises(ValueError):
+        Runner(precision="64-true")
