@@ -107,7 +107,8 @@ class FusedPPOTrainer:
 
         if (runner.device.type != "cuda" or runner.world_size != 1 or not isinstance(optimizer, FlatAdam)
                 or len(cfg.mlp_keys.encoder) != 1 or len(cfg.cnn_keys.encoder) != 0 or agent.is_continuous
-                or str(cfg.algo.loss_reduction).lower() != "mean" or not ops.native_available()):
+                or str(cfg.algo.loss_reduction).lower() != "mean" or not ops.native_available()
+                or getattr(runner, "_amp_dtype", None) is not None):
             return None
         chains = FusedCartPoleRollout.chains_of(agent)
         if chains is None:

@@ -50,11 +50,13 @@ def set_fused(flag: bool) -> None:
 
 
 def fused_enabled() -> bool:
-    return _FUSED
+    """Fused (fp32-only) HIP paths are on - and no CUDA autocast region (``precision=bf16-mixed``)
+    is active: under autocast the ops run as eager torch code so they compute in bf16 like the rest."""
+    return _FUSED and not torch.is_autocast_enabled("cuda")
 
 
 def _native(t: Tensor) -> bool:
-    if t.is_cuda and _FUSED:
+    if t.is_cuda and fused_enabled():
         _ext()  # loud failure if missing
         return True
     return False
