@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include "scan4.h"
+#include "scanp.h"
 
 // ---- launchers (defined in the .hip translation units)
 void launch_flat_grad_norm(const float*, int64_t, float*, int, float*, float*, float, hipStream_t);
@@ -58,6 +59,12 @@ void launch_scan4_fwd(const srl::scan4::SP&, hipStream_t);
 void launch_scan4_bwd(const srl::scan4::SP&, hipStream_t);
 int scan4_fwd_lds(int, int, int, int);
 int scan4_bwd_lds(int, int, int, int);
+void launch_scanp_fwd(const srl::scanp::PP&, hipStream_t);
+void launch_scanp_bwd(const srl::scanp::PP&, hipStream_t);
+bool scanp_supported(int, int, int, int, int, int);
+int scanp_sync_words();
+int scanp_fwd_grid(int, int, int);
+int scanp_bwd_grid(int, int, int, int);
 
 namespace {
 
@@ -543,6 +550,64 @@ int64_t scan4_lds(int64_t S, int64_t D, int64_t H, int64_t hid) {
   return a > b ? a : b;
 }
 
+// ------------------------------------------------------------------ persistent RSSM posterior scan
+// tensors (fixed order, see ops/rssm.py RSSMPersistFn): 33 forward buffers + the int32 hand-off
+// counter block, then 18 backward ones; an undefined / empty tensor is a null pointer.
+srl::scanp::PP scanp_params(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints,
+                            const std::vector<double>& fl) {
+  TORCH_CHECK(ints.size() == 9 && fl.size() == 4, "scanp: bad scalar arguments");
+  srl::scanp::PP p{};
+  p.T = ints[0]; p.B = ints[1]; p.S = ints[2]; p.D = ints[3]; p.H = ints[4]; p.hid = ints[5]; p.C = ints[6];
+  p.act1 = ints[7]; p.act2 = ints[8];
+  p.alpha = fl[0]; p.eps1 = fl[1]; p.epsg = fl[2]; p.eps2 = fl[3];
+  TORCH_CHECK(scanp_supported(p.B, p.S, p.D, p.H, p.hid, p.C), "scanp: unsupported shape B=", p.B, " S=", p.S, " D=", p.D,
+              " H=", p.H, " hid=", p.hid, " C=", p.C);
+  auto P = [&](size_t i) -> float* {
+    if (i >= ts.size() || !ts[i].defined() || ts[i].numel() == 0) return nullptr;
+    TORCH_CHECK(ts[i].is_cuda() && ts[i].scalar_type() == torch::kFloat32 && ts[i].is_contiguous(),
+                "scanp: tensor ", i, " must be a contiguous float32 GPU tensor");
+    return ts[i].data_ptr<float>();
+  };
+  size_t k = 0;
+  p.P = P(k++); p.first = P(k++); p.uni = P(k++); p.z0 = P(k++); p.Wz = P(k++); p.WzT = P(k++); p.ln1w = P(k++);
+  p.ln1b = P(k++); p.Wg = P(k++); p.lngw = P(k++); p.lngb = P(k++); p.W1 = P(k++); p.ln2w = P(k++); p.ln2b = P(k++);
+  p.W2 = P(k++); p.b2 = P(k++);
+  p.xr = P(k++); p.cat = P(k++); p.zm = P(k++); p.m1 = P(k++); p.r1 = P(k++); p.gx = P(k++); p.gst = P(k++); p.mg = P(k++);
+  p.rg = P(k++); p.hs = P(k++); p.u = P(k++); p.v = P(k++); p.m2 = P(k++); p.r2 = P(k++); p.logits = P(k++);
+  p.mixed = P(k++); p.samples = P(k++);
+  const torch::Tensor& sync = ts.at(k++);
+  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == torch::kInt32 && sync.is_contiguous() &&
+                  sync.numel() >= scanp_sync_words(), "scanp: sync must be int32[", scanp_sync_words(), "] on the GPU");
+  p.sync = (unsigned*)sync.data_ptr<int32_t>();
+  p.W2T = P(k++); p.W1T = P(k++); p.WgT = P(k++); p.dpost = P(k++); p.dmixed = P(k++);
+  p.DH = P(k++); p.dlog = P(k++); p.dv = P(k++); p.du = P(k++); p.dgx = P(k++); p.dcat = P(k++); p.dx = P(k++);
+  p.p1g = P(k++); p.p1b = P(k++); p.pgg = P(k++); p.pgb = P(k++); p.p2g = P(k++); p.p2b = P(k++);
+  return p;
+}
+
+void scanp_fwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints, const std::vector<double>& fl) {
+  TORCH_CHECK(ts.size() == 34, "scanp_fwd: expects 34 tensors");
+  auto p = scanp_params(ts, ints, fl);
+  TORCH_CHECK(p.P && p.first && p.uni && p.z0 && p.WzT && p.Wg && p.W1 && p.W2 && p.xr && p.hs && p.u && p.samples,
+              "scanp_fwd: missing tensors");
+  launch_scanp_fwd(p, cur_stream());
+}
+
+void scanp_bwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints, const std::vector<double>& fl) {
+  TORCH_CHECK(ts.size() == 52, "scanp_bwd: expects 52 tensors");
+  auto p = scanp_params(ts, ints, fl);
+  TORCH_CHECK(p.W2T && p.W1T && p.WgT && p.dmixed && p.DH && p.dlog && p.dv && p.du && p.dgx && p.dcat && p.dx,
+              "scanp_bwd: missing tensors");
+  launch_scanp_bwd(p, cur_stream());
+}
+
+std::vector<int64_t> scanp_info(int64_t B, int64_t S, int64_t D, int64_t H, int64_t hid, int64_t C) {
+  // [supported, sync words, error word index, forward grid, backward grid]
+  const int words = scanp_sync_words();
+  return {scanp_supported(B, S, D, H, hid, C) ? 1 : 0, words, words - 32, scanp_fwd_grid(S, H, hid),
+          scanp_bwd_grid(S, D, H, hid)};
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ strided-output (no-grad) forms
@@ -892,5 +957,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scan4_fwd", &scan4_fwd);
   m.def("scan4_bwd", &scan4_bwd);
   m.def("scan4_lds", &scan4_lds);
+  m.def("scanp_fwd", &scanp_fwd);
+  m.def("scanp_bwd", &scanp_bwd);
+  m.def("scanp_info", &scanp_info);
   m.def("set_scan4_prof", &set_scan4_prof);
 }

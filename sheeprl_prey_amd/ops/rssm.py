@@ -225,6 +225,100 @@ class RSSMScan4Fn(torch.autograd.Function):
                 p2g.sum(0).view(2, hid), p2b.sum(0).view(2, hid), dW2, db2, None)
 
 
+class RSSMPersistFn(torch.autograd.Function):
+    """Posterior path of the scan as ONE persistent launch forward and ONE backward
+    (``csrc/rssm_persist.hip``): every workgroup keeps its weight tile in registers for all T steps
+    and the GEMM -> LayerNorm seams are in-launch hand-offs (write-through stores + arrival
+    counters).  ``W1`` is the h-half of the representation input layer [hid, H], ``ln2_*`` / ``W2`` /
+    ``b2`` the representation head, ``P`` its embedding projection (+ bias), ``uniform`` [T, B*S/C].
+    Returns recurrent states, posterior samples and posterior unimix logits; the prior head runs
+    batched on the returned states (``fused_scan``)."""
+
+    @staticmethod
+    def forward(ctx, a_proj, P, is_first, uniform, z0, Wz, ln1_w, ln1_b, Wg, lng_w, lng_b, W1, ln2_w, ln2_b, W2, b2, meta):
+        from sheeprl_prey_amd.ops import _ext
+
+        C = _ext()
+        T, B, D = a_proj.shape
+        S = Wz.shape[1]
+        H = lng_w.shape[0] // 3
+        hid = W1.shape[0]
+        disc, alpha, eps1, epsg, eps2, act1, act2 = meta
+        dev, f32 = a_proj.device, torch.float32
+        e = lambda *shape: torch.empty(*shape, device=dev, dtype=f32)  # noqa: E731
+        first = is_first.reshape(T, B).contiguous()
+        Wz_c = Wz.contiguous()
+        z0 = z0.reshape(-1).contiguous()
+        # recurrent input before the posterior gathers: action part + z0 Wz^T of reset rows
+        xr = torch.addcmul(a_proj, first.unsqueeze(-1), torch.mv(Wz_c, z0))
+        zm = e(T, B, S)
+        zm[0] = first[0].unsqueeze(-1) * z0
+        ok, words, _, _, _ = C.scanp_info(B, S, D, H, hid, disc)
+        assert ok, "scanp: unsupported shape"
+        sync = torch.empty(words, device=dev, dtype=torch.int32)
+        fwd = [P.contiguous(), first, uniform.contiguous(), z0, Wz_c, Wz_c.t().contiguous(), ln1_w.contiguous(),
+               ln1_b.contiguous(), Wg.contiguous(), lng_w.contiguous(), lng_b.contiguous(), W1.contiguous(),
+               ln2_w.contiguous(), ln2_b.contiguous(), W2.contiguous(), b2.contiguous(),
+               xr, e(T, B, H + D), zm, e(T, B), e(T, B), e(T, B, 3 * H), e(T, 3 * H // 16, 16, 2), e(T, B), e(T, B),
+               e(T, B, H), e(T, B, hid), e(T, B, hid), e(T, B), e(T, B), e(T, B, S), e(T, B, S), e(T, B, S), sync]
+        dims = [T, B, S, D, H, hid, disc, act1, act2]
+        fl = [alpha, eps1, epsg, eps2]
+        C.scanp_fwd(fwd, dims, fl)
+        ctx.save_for_backward(*fwd)
+        ctx.dims, ctx.fl = dims, fl
+        hs, mixed, samples = fwd[25], fwd[31], fwd[32]
+        return hs, samples, mixed
+
+    @staticmethod
+    def backward(ctx, d_hs, d_post, d_post_mixed):
+        from sheeprl_prey_amd.ops import _ext
+
+        C = _ext()
+        fwd = list(ctx.saved_tensors)
+        T, B, S, D, H, hid, disc = ctx.dims[:7]
+        alpha = ctx.fl[0]
+        dev, f32 = fwd[0].device, torch.float32
+        e = lambda *shape: torch.empty(*shape, device=dev, dtype=f32)  # noqa: E731
+        Wz, Wg, W1, W2 = fwd[4], fwd[8], fwd[11], fwd[14]
+        logits = fwd[30]
+        dmixed = d_post_mixed.contiguous() if d_post_mixed is not None else torch.zeros(T, B, S, device=dev, dtype=f32)
+        DH = d_hs.contiguous().clone() if d_hs is not None else torch.zeros(T, B, H, device=dev, dtype=f32)
+        dpost = d_post.contiguous() if d_post is not None else torch.empty(0, device=dev, dtype=f32)
+        dlog = e(T, B, S)
+        # the last step's categorical adjoint has no recurrent term: one launch before the scan
+        C.unimix_sample_bwd_into(logits[T - 1], dmixed[T - 1], dpost[T - 1] if d_post is not None else None, dlog[T - 1],
+                                 disc, alpha)
+        dv, du, dgx, dcat, dx = e(T, B, hid), e(T, B, hid), e(T, B, 3 * H), e(T, B, H + D), e(T, B, D)
+        p1g, p1b, pgg, pgb, p2g, p2b = e(T, D), e(T, D), e(T, 3 * H), e(T, 3 * H), e(T, hid), e(T, hid)
+        bwd = [W2.t().contiguous(), W1.t().contiguous(), Wg.t().contiguous(), dpost, dmixed, DH, dlog, dv, du, dgx, dcat,
+               dx, p1g, p1b, pgg, pgb, p2g, p2b]
+        C.scanp_bwd(fwd + bwd, ctx.dims, ctx.fl)
+        cat, zm, hs, v = fwd[17], fwd[18], fwd[25], fwd[27]
+        TB = T * B
+        dWz = dx.reshape(TB, D).t().mm(zm.reshape(TB, S))
+        dWg = dgx.reshape(TB, 3 * H).t().mm(cat.reshape(TB, H + D))
+        dW1 = du.reshape(TB, hid).t().mm(hs.reshape(TB, H))
+        dlog2 = dlog.reshape(TB, S)
+        dW2 = dlog2.t().mm(v.reshape(TB, hid))
+        db2 = dlog2.sum(0)
+        return (dx, du, None, None, None, dWz, p1g.sum(0), p1b.sum(0), dWg, pgg.sum(0), pgb.sum(0), dW1, p2g.sum(0),
+                p2b.sum(0), dW2, db2, None)
+
+
+def scanp_error(sync: Tensor) -> int:
+    """Error word of a persistent-scan launch (0 = every hand-off completed; else the waiter's code)."""
+    from sheeprl_prey_amd.ops import _ext
+
+    return int(sync[_ext().scanp_info(1, 32, 16, 16, 16, 32)[2]].item())
+
+
+def scanp_supported(B: int, S: int, D: int, H: int, hid: int, classes: int) -> bool:
+    """Shape gate of the persistent scan (register tiles, LDS, one resident workgroup per CU)."""
+    from sheeprl_prey_amd.ops import _ext
+
+    return bool(_ext().scanp_info(B, S, D, H, hid, classes)[0])
+
+
 def scan4_supported(B: int, S: int, D: int, H: int, hid: int, classes: int) -> bool:
     """Shape gate of the 4-launch scan: 16-row tiles, 16/32-column tiles, whole categorical groups
     per 32-column tile, every A operand fits the 160 KiB LDS of one workgroup."""
@@ -278,19 +372,30 @@ def fused_scan(rssm, embedded_obs: Tensor, actions: Tensor, is_first: Tensor, z0
     We = rep[0].weight[:, H:]
     e_proj = torch.nn.functional.linear(embedded_obs, We, rep[0].bias)
     hid = tr[0].out_features
+    meta = (rssm.discrete, float(rssm.unimix), float(rec[1].eps), float(gru.layer_norm.eps), float(tr[1].eps),
+            ACTS[rec[1].act], ACTS[tr[1].act])
+    impl = getattr(rssm, "scan_impl", os.environ.get("SRL_SCAN_IMPL", "persist"))
+    nseg = S // rssm.discrete
+    if impl == "persist" and scanp_supported(B, S, rec_lin.out_features, H, hid, rssm.discrete):
+        # posterior path in one persistent launch; the prior head is off the recurrence: batched
+        uni_post = uniform.view(T, 2, B * nseg)[:, 1] if uniform is not None else torch.rand(
+            T, B * nseg, device=embedded_obs.device)
+        hs, post, post_mixed = RSSMPersistFn.apply(
+            a_proj.contiguous(), e_proj.contiguous(), is_first.contiguous(), uni_post.contiguous(), z0.reshape(-1).contiguous(),
+            Wz, rec[1].weight, rec[1].bias, gru.linear.weight, gru.layer_norm.weight, gru.layer_norm.bias,
+            rep[0].weight[:, :H], rep[1].weight, rep[1].bias, rep[3].weight, rep[3].bias, meta)
+        prior_mixed = rssm._uniform_mix_fused(rssm.transition_model(hs))
+        return hs, post, post_mixed, prior_mixed
+    if uniform is None:
+        uniform = torch.rand(T, 2 * B * nseg, device=embedded_obs.device)
     P = torch.cat((tr[0].bias.expand(T, B, hid), e_proj), -1)
     W1 = torch.cat((tr[0].weight, rep[0].weight[:, :H]), 0)
     ln2_w = torch.stack((tr[1].weight, rep[1].weight))
     ln2_b = torch.stack((tr[1].bias, rep[1].bias))
     W2 = torch.stack((tr[3].weight, rep[3].weight))
     b2 = torch.stack((tr[3].bias, rep[3].bias)).unsqueeze(1)
-    if uniform is None:
-        uniform = torch.rand(T, 2 * B * (S // rssm.discrete), device=embedded_obs.device)
-    meta = (rssm.discrete, float(rssm.unimix), float(rec[1].eps), float(gru.layer_norm.eps), float(tr[1].eps),
-            ACTS[rec[1].act], ACTS[tr[1].act])
     fn = RSSMScanFn
-    if getattr(rssm, "scan_impl", os.environ.get("SRL_SCAN_IMPL", "scan4")) == "scan4" and scan4_supported(B, S, rec_lin.out_features, H, hid,
-                                                                         rssm.discrete):
+    if impl in ("scan4", "persist") and scan4_supported(B, S, rec_lin.out_features, H, hid, rssm.discrete):
         fn = RSSMScan4Fn
     return fn.apply(a_proj.contiguous(), P.contiguous(), is_first.contiguous(), uniform, z0.reshape(-1).contiguous(),
                             Wz, rec[1].weight, rec[1].bias, gru.linear.weight, gru.layer_norm.weight, gru.layer_norm.bias,

@@ -68,11 +68,22 @@ def test_dv3_graph_matches_eager_losses():
     assert abs(la - lb) / abs(la) < 1e-4
 
 
-@pytest.mark.parametrize("impl", ["scan4", "scan9"])
+@pytest.mark.parametrize("impl", ["persist", "scan4", "scan9"])
 @pytest.mark.parametrize("H,D,hid,B,T", [(64, 64, 64, 4, 16), (512, 512, 512, 16, 8), (96, 80, 48, 3, 5)])
 def test_fused_rssm_scan_matches_python_scan(H, D, hid, B, T, impl):
-    """The fused scans (scan4: 4+4 MFMA launches/step; scan9: 9+9 launches/step; batched weight
-    grads) vs the python step loop, same noise."""
+    """The fused scans (persist: one persistent launch per direction; scan4: 4+4 MFMA launches/step;
+    scan9: 9+9 launches/step; batched weight grads) vs the python step loop, same noise."""
+    _check_scan_vs_python(H, D, hid, B, T, impl)
+
+
+@pytest.mark.parametrize("impl", ["persist", "scan4"])
+def test_fused_rssm_scan_full_shape_T64(impl):
+    """Atari-100k shape over the whole sequence (B 16, T 64, H = D = hid = 512): the fast
+    sigmoid/tanh forms and the in-launch hand-offs must hold through 64 recurrent steps, fwd + bwd."""
+    _check_scan_vs_python(512, 512, 512, 16, 64, impl, tol=(5e-3, 5e-4), gtol=(5e-3, 5e-3))
+
+
+def _check_scan_vs_python(H, D, hid, B, T, impl, tol=(2e-3, 2e-4), gtol=(3e-3, 3e-3)):
     import copy
 
     from sheeprl_prey_amd.algos.dreamer_v3.agent import RSSM, RecurrentModel, init_weights
@@ -100,17 +111,22 @@ def test_fused_rssm_scan_matches_python_scan(H, D, hid, B, T, impl):
     e1, e2 = emb.clone().requires_grad_(), emb.clone().requires_grad_()
     out1 = rssm.scan_dynamic(e1, act, first, uniform=uni)
     out2 = rssm_ref.scan_dynamic(e2, act, first, uniform=uni_post)
-    if impl == "scan4":
-        assert type(out1[0].grad_fn).__name__ == "RSSMScan4FnBackward"
+    fn = {"persist": "RSSMPersistFnBackward", "scan4": "RSSMScan4FnBackward", "scan9": "RSSMScanFnBackward"}[impl]
+    assert type(out1[0].grad_fn).__name__ == fn
     names = ["h", "post", "post_logits", "prior_logits"]
     for n, a, b in zip(names, out1, out2):
-        torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-4, msg=lambda m: f"{n}: {m}")
+        torch.testing.assert_close(a, b, rtol=tol[0], atol=tol[1], msg=lambda m: f"{n}: {m}")
+    sync = out1[0].grad_fn.saved_tensors[33] if impl == "persist" else None  # hand-off counters + error word
     gs = [torch.randn_like(o) for o in out1]
     sum((o * g).sum() for o, g in zip(out1, gs)).backward()
     sum((o * g).sum() for o, g in zip(out2, gs)).backward()
-    torch.testing.assert_close(e1.grad, e2.grad, rtol=2e-3, atol=2e-3)
+    if sync is not None:
+        from sheeprl_prey_amd.ops.rssm import scanp_error
+
+        assert scanp_error(sync) == 0, "a persistent-scan hand-off timed out"
+    torch.testing.assert_close(e1.grad, e2.grad, rtol=gtol[0], atol=gtol[1])
     for (n, p1), p2 in zip(rssm.named_parameters(), rssm_ref.parameters()):
-        torch.testing.assert_close(p1.grad, p2.grad, rtol=3e-3, atol=3e-3, msg=lambda m: f"{n}: {m}")
+        torch.testing.assert_close(p1.grad, p2.grad, rtol=gtol[0], atol=gtol[1], msg=lambda m: f"{n}: {m}")
 
 
 def test_dv3_segmented_graph_matches_single_graph():
