@@ -551,8 +551,8 @@ int64_t scan4_lds(int64_t S, int64_t D, int64_t H, int64_t hid) {
 }
 
 // ------------------------------------------------------------------ persistent RSSM posterior scan
-// tensors (fixed order, see ops/rssm.py RSSMPersistFn): 33 forward buffers + the int32 hand-off
-// counter block, then 18 backward ones; an undefined / empty tensor is a null pointer.
+// tensors (fixed order, see ops/rssm.py RSSMPersistFn): 33 forward buffers + the int32 sample table and hand-off
+// counter block, then 20 backward ones; an undefined / empty tensor is a null pointer.
 srl::scanp::PP scanp_params(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints,
                             const std::vector<double>& fl) {
   TORCH_CHECK(ints.size() == 9 && fl.size() == 4, "scanp: bad scalar arguments");
@@ -575,6 +575,10 @@ srl::scanp::PP scanp_params(const std::vector<torch::Tensor>& ts, const std::vec
   p.xr = P(k++); p.cat = P(k++); p.zm = P(k++); p.m1 = P(k++); p.r1 = P(k++); p.gx = P(k++); p.gst = P(k++); p.mg = P(k++);
   p.rg = P(k++); p.hs = P(k++); p.u = P(k++); p.v = P(k++); p.m2 = P(k++); p.r2 = P(k++); p.logits = P(k++);
   p.mixed = P(k++); p.samples = P(k++);
+  const torch::Tensor& sel = ts.at(k++);
+  TORCH_CHECK(sel.is_cuda() && sel.scalar_type() == torch::kInt32 && sel.is_contiguous() && sel.numel() >= p.T * p.B * (p.S / p.C),
+              "scanp: sel must be int32 [T, B, S/C] on the GPU");
+  p.sel = sel.data_ptr<int32_t>();
   const torch::Tensor& sync = ts.at(k++);
   TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == torch::kInt32 && sync.is_contiguous() &&
                   sync.numel() >= scanp_sync_words(), "scanp: sync must be int32[", scanp_sync_words(), "] on the GPU");
@@ -582,21 +586,35 @@ srl::scanp::PP scanp_params(const std::vector<torch::Tensor>& ts, const std::vec
   p.W2T = P(k++); p.W1T = P(k++); p.WgT = P(k++); p.dpost = P(k++); p.dmixed = P(k++);
   p.DH = P(k++); p.dlog = P(k++); p.dv = P(k++); p.du = P(k++); p.dgx = P(k++); p.dcat = P(k++); p.dx = P(k++);
   p.p1g = P(k++); p.p1b = P(k++); p.pgg = P(k++); p.pgb = P(k++); p.p2g = P(k++); p.p2b = P(k++);
+  p.dZ = P(k++); p.sst = P(k++);
   return p;
 }
 
+long long* g_scanp_prof = nullptr;  // debug phase timestamps (set_scanp_prof)
+
+void set_scanp_prof(c10::optional<torch::Tensor> buf) {
+  if (buf.has_value() && buf->defined()) {
+    TORCH_CHECK(buf->scalar_type() == torch::kInt64 && buf->is_cuda(), "prof buffer: int64 [7 * T * 8] on GPU");
+    g_scanp_prof = (long long*)buf->data_ptr<int64_t>();
+  } else {
+    g_scanp_prof = nullptr;
+  }
+}
+
 void scanp_fwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints, const std::vector<double>& fl) {
-  TORCH_CHECK(ts.size() == 34, "scanp_fwd: expects 34 tensors");
+  TORCH_CHECK(ts.size() == 35, "scanp_fwd: expects 35 tensors");
   auto p = scanp_params(ts, ints, fl);
+  p.prof = g_scanp_prof;
   TORCH_CHECK(p.P && p.first && p.uni && p.z0 && p.WzT && p.Wg && p.W1 && p.W2 && p.xr && p.hs && p.u && p.samples,
               "scanp_fwd: missing tensors");
   launch_scanp_fwd(p, cur_stream());
 }
 
 void scanp_bwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints, const std::vector<double>& fl) {
-  TORCH_CHECK(ts.size() == 52, "scanp_bwd: expects 52 tensors");
+  TORCH_CHECK(ts.size() == 55, "scanp_bwd: expects 55 tensors");
   auto p = scanp_params(ts, ints, fl);
-  TORCH_CHECK(p.W2T && p.W1T && p.WgT && p.dmixed && p.DH && p.dlog && p.dv && p.du && p.dgx && p.dcat && p.dx,
+  p.prof = g_scanp_prof;
+  TORCH_CHECK(p.W2T && p.W1T && p.WgT && p.dmixed && p.DH && p.dlog && p.dv && p.du && p.dgx && p.dcat && p.dx && p.dZ && p.sst,
               "scanp_bwd: missing tensors");
   launch_scanp_bwd(p, cur_stream());
 }
@@ -960,5 +978,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scanp_fwd", &scanp_fwd);
   m.def("scanp_bwd", &scanp_bwd);
   m.def("scanp_info", &scanp_info);
+  m.def("set_scanp_prof", &set_scanp_prof);
   m.def("set_scan4_prof", &set_scan4_prof);
 }

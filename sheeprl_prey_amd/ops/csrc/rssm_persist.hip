@@ -55,10 +55,24 @@ constexpr int NCTR = 4;               // counters per direction
 constexpr int ERRW = NCTR * NSH * SHW;  // index of the error word
 constexpr u32 SPIN_MAX = 1u << 20;
 
+// Phase timestamps (s_memrealtime, 100 MHz): 0 step start, 1 hand-off in, 2 operand ready, 3 GEMM done, 4 published.
+// The read is an asm statement with a memory clobber so the compiler can neither move it across the
+// phase's memory operations nor merge it with a neighbour.
+__device__ __forceinline__ long long prof_clock() {
+  long long c;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c)::"memory");
+  return c;
+}
+#define PROF(role, k)                                                                                 \
+  do {                                                                                                \
+    if (p.prof && first_wg && threadIdx.x == 0) p.prof[((role) * p.T + t) * 8 + (k)] = prof_clock(); \
+  } while (0)
+
 // Register tile caps per phase (K chunks of 16 per wave): host gate mirrors them.
 constexpr int UA = 4, UB = 2, UC = 2;           // K = H+D <= 1024, H <= 512, hid <= 512
 constexpr int U1 = 4, U2 = 2, U3 = 6, U4 = 2;   // K = S <= 1024, hid <= 512, 3H <= 1536, D <= 512
 constexpr int GRU_M = 8;                        // H <= 64 * GRU_M
+constexpr int LN_M = 8;                         // D, hid <= 64 * LN_M (row LayerNorms in registers)
 
 // ------------------------------------------------------------------ write-through accesses
 __device__ __forceinline__ float ld_wt(const float* p) {
@@ -217,12 +231,10 @@ __device__ __forceinline__ void gemm_reg(const WTile<NT, U>& wt, const float* As
 // One role per workgroup; each role carves the dynamic LDS its own way (floats).
 __host__ __device__ inline int lds_A(int D, int H) { return 16 * (H + D + 4) + 2 * D + 4096 + 256 + 16; }
 __host__ __device__ inline int lds_B(int H) { return 16 * (H + 4) + 6 * H + 4096 + 256 + 16; }
-__host__ __device__ inline int lds_C(int hid) { return 16 * (hid + 4) + 2 * hid + 8192 + 512 + 16 + 512; }
-__host__ __device__ inline int g3_parts(int H, int D) { return (H + D) / 16; }
-__host__ __device__ inline int g3_nch(int H, int D) { return (3 * H + g3_parts(H, D) - 1) / g3_parts(H, D); }
+__host__ __device__ inline int lds_C(int hid, int S, int C) { return 16 * (hid + 4) + 2 * hid + 8192 + 512 + 16 + 16 * (S / C); }
 __host__ __device__ inline int lds_G1(int S) { return 16 * (S + 4) + 4096 + 256 + 16; }
-__host__ __device__ inline int lds_G2(int hid) { return 32 * (hid + 4) + 2 * hid + 48 + 4096 + 256 + 16; }
-__host__ __device__ inline int lds_G3(int H, int D) { return 16 * (3 * H + 4) + 6 * H + 4096 + 256 + 256 + 32 * g3_nch(H, D) + 16; }
+__host__ __device__ inline int lds_G2(int hid) { return 32 * (hid + 4) + 2 * hid + 48 + 4096 + 256 + 1536 + 1792 + 16; }
+__host__ __device__ inline int lds_G3(int H) { return 16 * (3 * H + 4) + 64 + 4096 + 256 + 16; }
 __host__ __device__ inline int lds_G4(int D) { return 32 * (D + 4) + 2 * D + 48 + 8192 + 512 + 16; }
 
 // ======================================================================= forward roles
@@ -230,6 +242,7 @@ __host__ __device__ inline int lds_G4(int D) { return 32 * (D + 4) + 2 * D + 48 
 
 // A: gx tile = [(1-first) h_{t-1}, act(LN1(xr_t))] Wg^T, plus per-row (mean, M2) of the tile.
 __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
+  const bool first_wg = a == 0;
   const int B = p.B, D = p.D, H = p.H, HD = H + D, N3 = 3 * H, T = p.T;
   const int nA = N3 / 16, nB = p.hid / 16, nC = p.S / 32;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lda = HD + 4;
@@ -247,32 +260,29 @@ __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
   for (int e = threadIdx.x; e < 16 * H; e += NTH) As[(e / H) * lda + e % H] = 0.f;  // h_{-1} = 0
   __syncthreads();
   for (int t = 0; t < T; ++t) {
+    PROF(0, 0);
     if (t > 0) {
       // h_{t-1} is published by B(t-1) before C(t-1) runs: load it while C finishes
       if (!wait_ctr(p.sync, 1, eB, t, 1, flag)) return;
       stage_wt(As, lda, p.hs + (size_t)(t - 1) * B * H, H, B, H, p.first + (size_t)t * B);
       if (!wait_ctr(p.sync, 2, eC, t, 2, flag)) return;
     }
+    PROF(0, 1);
     stage_wt(As + H, lda, p.xr + (size_t)t * B * D, D, B, D);
     __syncthreads();
+    PROF(0, 5);
     if (w < B) {
-      float* r = As + w * lda + H;
       float mu, rs;
-      wave_row_stats(r, D, p.eps1, mu, rs);
-      for (int k = lane; k < D; k += 64) r[k] = f_act((r[k] - mu) * rs * l1w[k] + l1b[k], p.act1);
+      wave_ln_act_row<LN_M>(As + w * lda + H, D, p.eps1, l1w, l1b, p.act1, mu, rs);
       if (a == 0 && lane == 0) {
         p.m1[(size_t)t * B + w] = mu;
         p.r1[(size_t)t * B + w] = rs;
       }
     }
     __syncthreads();
-    {
-      int lo, hi;
-      part_range(B * HD, a, nA, lo, hi);
-      float* cat = p.cat + (size_t)t * B * HD;
-      for (int e = lo + threadIdx.x; e < hi; e += NTH) cat[e] = As[(e / HD) * lda + e % HD];
-    }
+    PROF(0, 2);
     gemm_reg<1, UA>(wt, As, lda, HD, red, ct);
+    PROF(0, 3);
     if (threadIdx.x < 256) {
       const int b = threadIdx.x >> 4, c = threadIdx.x & 15;
       const float x = ct[threadIdx.x];
@@ -284,12 +294,20 @@ __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
       }
     }
     arrive(p.sync + 0 * NSH * SHW);
+    PROF(0, 4);
+    {  // the GRU input of step t, read only by the backward: behind the hand-off
+      int lo, hi;
+      part_range(B * HD, a, nA, lo, hi);
+      float* cat = p.cat + (size_t)t * B * HD;
+      for (int e = lo + threadIdx.x; e < hi; e += NTH) cat[e] = As[(e / HD) * lda + e % HD];
+    }
   }
 }
 
 // B: h_t = LNGRU(gx_t, (1-first) h_{t-1}) (row statistics from A's partials, gates straight from gx);
 // u tile = h_t Wr1^T + P_t.  h stays in this workgroup's LDS from one step to the next.
 __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
+  const bool first_wg = bI == 0;
   const int B = p.B, H = p.H, N3 = 3 * H, T = p.T, hid = p.hid;
   const int nA = N3 / 16, nB = hid / 16;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lda = H + 4;
@@ -307,26 +325,14 @@ __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
   for (int e = threadIdx.x; e < 16 * H; e += NTH) As[(e / H) * lda + e % H] = 0.f;
   __syncthreads();
   for (int t = 0; t < T; ++t) {
+    PROF(1, 0);
+    const int eb = threadIdx.x >> 4, ec = threadIdx.x & 15;
+    const size_t eo = ((size_t)t * B + eb) * hid + bI * 16 + ec;
+    const float pre = (threadIdx.x < 256 && eb < B) ? p.P[eo] : 0.f;  // epilogue input, loaded behind the wait
     if (!wait_ctr(p.sync, 0, eA, t + 1, 3, flag)) return;
+    PROF(1, 1);
     if (w < B) {
-      // row statistics of gx from the nA tile partials (16 columns each): Chan's parallel combine
-      float sm1 = 0.f;
-      float2 pr[2];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int i = lane + 64 * k;
-        pr[k] = i < nA ? ld_wt2(p.gst + (((size_t)t * nA + i) * 16 + w) * 2) : make_float2(0.f, 0.f);
-        sm1 += pr[k].x;
-      }
-      const float mu = wave_sum(sm1) / nA;
-      float q = 0.f;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int i = lane + 64 * k;
-        if (i < nA) q += pr[k].y + 16.f * (pr[k].x - mu) * (pr[k].x - mu);
-      }
-      const float rs = rsqrtf(wave_sum(q) / N3 + p.epsg);
-      const float keep = 1.f - p.first[(size_t)t * B + w];
+      // gate inputs and the nA per-tile (mean, M2) partials, all loads issued before any use
       const float* gxr = p.gx + ((size_t)t * B + w) * N3;
       float x0[GRU_M], x1[GRU_M], x2[GRU_M];
 #pragma unroll
@@ -338,6 +344,22 @@ __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
           x2[m] = ld_wt(gxr + 2 * H + j);
         }
       }
+      float2 pr[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int i = lane + 64 * k;
+        pr[k] = i < nA ? ld_wt2(p.gst + (((size_t)t * nA + i) * 16 + w) * 2) : make_float2(0.f, 0.f);
+      }
+      // row statistics of gx from the tile partials (16 columns each): Chan's parallel combine
+      const float mu = wave_sum(pr[0].x + pr[1].x) / nA;
+      float q = 0.f;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int i = lane + 64 * k;
+        if (i < nA) q += pr[k].y + 16.f * (pr[k].x - mu) * (pr[k].x - mu);
+      }
+      const float rs = rsqrtf(wave_sum(q) / N3 + p.epsg);
+      const float keep = 1.f - p.first[(size_t)t * B + w];
       float* hr = As + w * lda;
 #pragma unroll
       for (int m = 0; m < GRU_M; ++m) {
@@ -358,27 +380,26 @@ __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
       }
     }
     __syncthreads();
+    PROF(1, 5);
     {
       int lo, hi;
       part_range(B * H, bI, nB, lo, hi);
       float* hs = p.hs + (size_t)t * B * H;
       for (int e = lo + threadIdx.x; e < hi; e += NTH) st_wt(hs + e, As[(e / H) * lda + e % H]);
     }
+    PROF(1, 2);
     gemm_reg<1, UB>(wt, As, lda, H, red, ct);
-    if (threadIdx.x < 256) {
-      const int b = threadIdx.x >> 4, c = threadIdx.x & 15;
-      if (b < B) {
-        const size_t o = ((size_t)t * B + b) * hid + bI * 16 + c;
-        st_wt(p.u + o, ct[threadIdx.x] + p.P[o]);
-      }
-    }
+    PROF(1, 3);
+    if (threadIdx.x < 256 && eb < B) st_wt(p.u + eo, ct[threadIdx.x] + pre);
     arrive(p.sync + 1 * NSH * SHW);
+    PROF(1, 4);
   }
 }
 
 // C: logits tile = act(LN2(u_t)) W2^T + b2 over whole categorical groups; unimix + straight-through
 // sample; the sampled one-hot rows of Wz^T are added into xr_{t+1} (device-scope atomics).
 __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
+  const bool first_wg = cI == 0;
   const int B = p.B, S = p.S, D = p.D, H = p.H, hid = p.hid, C = p.C, T = p.T;
   const int nA = 3 * H / 16, nB = hid / 16, nC = S / 32, nseg = S / C;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lda = hid + 4, n0 = cI * 32;
@@ -388,42 +409,40 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
   float* red = l2b + hid;
   float* ct = red + 8192;
   int* flag = (int*)(ct + 512);
-  int* sel = flag + 16;  // [16 rows][32 / C groups]
+  int* selL = flag + 16;  // [B][S / C] sampled rows of the step
   WTile<2, UC> wt;
   wload<2, UC>(wt, p.W2 + (size_t)n0 * hid, hid, hid, w);
   stage_vec(l2w, p.ln2w, hid);
   stage_vec(l2b, p.ln2b, hid);
-  const u32 eB = shard_count(nA, nB);
+  const u32 eB = shard_count(nA, nB), eC = shard_count(nA + nB, nC);
   __syncthreads();
   for (int t = 0; t < T; ++t) {
+    PROF(2, 0);
+    // epilogue inputs, loaded behind the wait: bias and the uniform of this lane's (row, categorical)
+    const int eb = threadIdx.x >> 5, ec = threadIdx.x & 31;
+    const bool evalid = threadIdx.x < 512 && eb < B;
+    const float ebias = threadIdx.x < 512 ? p.b2[n0 + ec] : 0.f;
+    const float euni = evalid ? p.uni[(size_t)t * B * nseg + eb * nseg + (n0 + ec) / C] : 0.f;
     if (!wait_ctr(p.sync, 1, eB, t + 1, 4, flag)) return;
+    PROF(2, 1);
     stage_wt(As, lda, p.u + (size_t)t * B * hid, hid, B, hid);
     __syncthreads();
     if (w < B) {
-      float* r = As + w * lda;
       float mu, rs;
-      wave_row_stats(r, hid, p.eps2, mu, rs);
-      for (int k = lane; k < hid; k += 64) r[k] = f_act((r[k] - mu) * rs * l2w[k] + l2b[k], p.act2);
+      wave_ln_act_row<LN_M>(As + w * lda, hid, p.eps2, l2w, l2b, p.act2, mu, rs);
       if (cI == 0 && lane == 0) {
         p.m2[(size_t)t * B + w] = mu;
         p.r2[(size_t)t * B + w] = rs;
       }
     }
     __syncthreads();
-    {
-      int lo, hi;
-      part_range(B * hid, cI, nC, lo, hi);
-      float* v = p.v + (size_t)t * B * hid;
-      for (int e = lo + threadIdx.x; e < hi; e += NTH) v[e] = As[(e / hid) * lda + e % hid];
-    }
+    PROF(2, 2);
     gemm_reg<2, UC>(wt, As, lda, hid, red, ct);
+    PROF(2, 3);
+    float el = 0.f, em = 0.f, esamp = 0.f;
     if (threadIdx.x < 512) {
-      const size_t base = (size_t)t * B * S;
-      const float* uni = p.uni + (size_t)t * B * nseg;
-      const int idx = threadIdx.x;
-      const int b = idx >> 5, c = idx & 31, k = c % C;
-      const bool valid = b < B;
-      const float l = ct[idx] + p.b2[n0 + c];
+      const int k = ec % C;
+      const float l = ct[threadIdx.x] + ebias;
       float m = l;
       if (p.alpha > 0.f) {
         const float mx = seg_max(l, C);
@@ -441,34 +460,72 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
         const float tt = __shfl_up(cdf, o, C);
         if (k >= o) cdf += tt;
       }
-      const float uu = valid ? uni[b * nseg + (n0 + c) / C] : 0.f;
-      const float below = cdf < uu * seg_max(cdf, C) ? 1.f : 0.f;
+      const float below = cdf < euni * seg_max(cdf, C) ? 1.f : 0.f;
       int pick = (int)seg_sum(below, C);
       if (pick > C - 1) pick = C - 1;
-      if (valid) {
-        const size_t o = base + (size_t)b * S + n0 + c;
-        p.logits[o] = l;
-        p.mixed[o] = m;
-        p.samples[o] = (k == pick) ? 1.f : 0.f;
-      }
-      if (t + 1 < T) {
-        const float f1 = valid ? p.first[(size_t)(t + 1) * B + b] : 1.f;
-        if (valid) p.zm[((size_t)(t + 1) * B + b) * S + n0 + c] = (1.f - f1) * (k == pick ? 1.f : 0.f) + f1 * p.z0[n0 + c];
-        // selected Wz^T row per (row, group); -1: reset row (its z0 Wz^T is already in xr) or padding
-        if (k == 0) sel[b * (32 / C) + c / C] = (valid && f1 == 0.f) ? n0 + c + pick : -1;
+      el = l;
+      em = m;
+      esamp = k == pick ? 1.f : 0.f;
+      // sampled row of Wz^T per (row, categorical) of step t+1's input; -1: reset row (z0 Wz^T is in xr)
+      if (t + 1 < T && k == 0 && evalid) {
+        const float f1 = p.first[(size_t)(t + 1) * B + eb];
+        __hip_atomic_store(p.sel + ((size_t)(t + 1) * B + eb) * nseg + (n0 + ec) / C, f1 == 0.f ? n0 + ec + pick : -1,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+    PROF(2, 5);
     if (t + 1 < T) {
+      // every C workgroup's samples of step t -> xr_{t+1} column tiles (16 columns of D) gathered from Wz^T:
+      // xr = a_proj + first z0 Wz^T (host) + sum over categoricals of the sampled rows.  All 1024 threads
+      // gather (row, column, quarter of the categoricals) so every load of a thread is in flight at once.
+      arrive(p.sync + 3 * NSH * SHW);
+      if (!wait_ctr(p.sync, 3, eC, t + 1, 5, flag)) return;
+      PROF(2, 6);
+      for (int e = threadIdx.x; e < B * nseg; e += NTH)
+        selL[e] = __hip_atomic_load(p.sel + (size_t)(t + 1) * B * nseg + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
-      const int npair = 16 * (32 / C);
       float* xr1 = p.xr + (size_t)(t + 1) * B * D;
-      for (int e = threadIdx.x; e < npair * D; e += NTH) {
-        const int pr = e / D, j = e - pr * D;
-        const int row = sel[pr];
-        if (row >= 0) atomicAdd(xr1 + (size_t)(pr / (32 / C)) * D + j, p.WzT[(size_t)row * D + j]);
+      const int gb = threadIdx.x >> 6, gc = (threadIdx.x >> 2) & 15, gq = threadIdx.x & 3;
+      const int per = (nseg + 3) >> 2;
+      for (int q = cI; q < D / 16; q += nC) {
+        const int col = q * 16 + gc;
+        float x = 0.f;
+        if (gb < B) {
+          const int* sr = selL + gb * nseg;
+#pragma unroll 8
+          for (int g = gq * per; g < min(nseg, gq * per + per); ++g) {
+            const int row = sr[g];
+            if (row >= 0) x += p.WzT[(size_t)row * D + col];
+          }
+        }
+        x += __shfl_xor(x, 1, 64);
+        x += __shfl_xor(x, 2, 64);
+        if (gb < B && gq == 0) {
+          float* d = xr1 + (size_t)gb * D + col;
+          st_wt(d, *d + x);
+        }
       }
+      PROF(2, 7);
     }
     arrive(p.sync + 2 * NSH * SHW);
+    PROF(2, 4);
+    // outputs read only after the launch: issued behind the hand-off
+    if (evalid) {
+      const size_t o = (size_t)t * B * S + (size_t)eb * S + n0 + ec;
+      p.logits[o] = el;
+      p.mixed[o] = em;
+      p.samples[o] = esamp;
+      if (t + 1 < T) {
+        const float f1 = p.first[(size_t)(t + 1) * B + eb];
+        p.zm[o + (size_t)B * S] = (1.f - f1) * esamp + f1 * p.z0[n0 + ec];
+      }
+    }
+    {
+      int lo, hi;
+      part_range(B * hid, cI, nC, lo, hi);
+      float* v = p.v + (size_t)t * B * hid;
+      for (int e = lo + threadIdx.x; e < hi; e += NTH) v[e] = As[(e / hid) * lda + e % hid];
+    }
   }
 }
 
@@ -490,6 +547,7 @@ __global__ void __launch_bounds__(NTH) fwd_kernel(PP p) {
 
 // G1: dv_t = dlog_t W2 (K = S).
 __device__ __forceinline__ void bwd_G1(const PP& p, int i, float* sm) {
+  const bool first_wg = i == 0;
   const int B = p.B, S = p.S, hid = p.hid, T = p.T, H = p.H, D = p.D;
   const int n1 = hid / 16, n2 = H / 16, n3 = (H + D) / 16, n4 = S / 32;
   const int w = threadIdx.x >> 6, lda = S + 4;
@@ -502,21 +560,30 @@ __device__ __forceinline__ void bwd_G1(const PP& p, int i, float* sm) {
   const u32 e4 = shard_count(n1 + n2 + n3, n4);
   __syncthreads();
   for (int t = T - 1; t >= 0; --t) {
+    PROF(3, 0);
     if (t < T - 1 && !wait_ctr(p.sync, 3, e4, T - 1 - t, 11, flag)) return;
+    PROF(3, 1);
     stage_wt(As, lda, p.dlog + (size_t)t * B * S, S, B, S);
     __syncthreads();
+    PROF(3, 2);
     gemm_reg<1, U1>(wt, As, lda, S, red, ct);
+    PROF(3, 3);
     if (threadIdx.x < 256) {
       const int b = threadIdx.x >> 4, c = threadIdx.x & 15;
       if (b < B) st_wt(p.dv + ((size_t)t * B + b) * hid + i * 16 + c, ct[threadIdx.x]);
     }
     arrive(p.sync + 0 * NSH * SHW);
+    PROF(3, 4);
   }
 }
 
-// G2: du_t = LN2'(dv_t) (+ LN2 parameter partials); DH_t += du_t Wr1 (K = hid).
+// G2: du_t = LN2'(dv_t) (+ LN2 parameter partials); DH_t tile = DH_t + du_t Wr1 (K = hid) is final for
+// this workgroup's 16 h columns, so the LN-GRU adjoint of those columns is formed here: dz * gamma of
+// the three gates (handed to G3 with the row partial sums the LayerNorm adjoint needs), the LN-GRU
+// parameter partials, and the gate's direct path into DH_{t-1}.
 __device__ __forceinline__ void bwd_G2(const PP& p, int i, float* sm) {
-  const int B = p.B, H = p.H, hid = p.hid, T = p.T;
+  const bool first_wg = i == 0;
+  const int B = p.B, H = p.H, hid = p.hid, T = p.T, N3 = 3 * H, HD = H + p.D;
   const int n1 = hid / 16, n2 = H / 16;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lda = hid + 4;
   float* As = sm;
@@ -526,157 +593,162 @@ __device__ __forceinline__ void bwd_G2(const PP& p, int i, float* sm) {
   float* st = l2b + hid;
   float* red = st + 48;
   float* ct = red + 4096;
-  int* flag = (int*)(ct + 256);
+  float* gsc = ct + 256;  // [16 rows][6][16 columns]: LN-GRU parameter partial terms
+  float* pre = gsc + 1536;  // [7][256]: forward values of this thread's GRU adjoint element
+  int* flag = (int*)(pre + 1792);
   WTile<1, U2> wt;
   wload<1, U2>(wt, p.W1T + (size_t)i * 16 * hid, hid, hid, w);
   stage_vec(l2w, p.ln2w, hid);
   stage_vec(l2b, p.ln2b, hid);
   const u32 e1 = shard_count(0, n1);
+  // thread -> (row eb, h column j) of the GRU adjoint; gate parameters fixed per thread
+  const int eb = threadIdx.x >> 4, ec = threadIdx.x & 15, j = i * 16 + ec;
+  const bool eok = threadIdx.x < 256;
+  float gw0 = 0.f, gw1 = 0.f, gw2 = 0.f, gb0 = 0.f, gb1 = 0.f, gb2 = 0.f;
+  if (eok) {
+    gw0 = p.lngw[j], gw1 = p.lngw[H + j], gw2 = p.lngw[2 * H + j];
+    gb0 = p.lngb[j], gb1 = p.lngb[H + j], gb2 = p.lngb[2 * H + j];
+  }
   __syncthreads();
   for (int t = T - 1; t >= 0; --t) {
+    PROF(4, 0);
     stage(As, lda, p.u + (size_t)t * B * hid, hid, B, hid);
+    // forward values of the GRU adjoint: loaded behind the wait
+    const bool rv = eok && eb < B;
+    if (eok) {  // parked in LDS, not registers: they are consumed after the LN2 adjoint and the GEMM
+      const size_t gr = ((size_t)t * B + (rv ? eb : 0)) * N3;
+      pre[threadIdx.x] = rv ? p.gx[gr + j] : 0.f;
+      pre[256 + threadIdx.x] = rv ? p.gx[gr + H + j] : 0.f;
+      pre[512 + threadIdx.x] = rv ? p.gx[gr + 2 * H + j] : 0.f;
+      pre[768 + threadIdx.x] = rv ? p.cat[((size_t)t * B + eb) * HD + j] : 0.f;
+      pre[1024 + threadIdx.x] = rv ? p.mg[(size_t)t * B + eb] : 0.f;
+      pre[1280 + threadIdx.x] = rv ? p.rg[(size_t)t * B + eb] : 0.f;
+      pre[1536 + threadIdx.x] = (rv && t > 0) ? 1.f - p.first[(size_t)t * B + eb] : 0.f;
+    }
     if (!wait_ctr(p.sync, 0, e1, T - t, 12, flag)) return;
+    PROF(4, 1);
     stage_wt(R, lda, p.dv + (size_t)t * B * hid, hid, B, hid);
     __syncthreads();
+    float xh[LN_M], dzr[LN_M], s1 = 0.f, s2 = 0.f, rsw = 0.f;
     if (w < B) {
-      const float mu = p.m2[(size_t)t * B + w], rs = p.r2[(size_t)t * B + w];
-      float s1, s2;
-      wave_ln_bwd_prep(As + w * lda, R + w * lda, l2w, l2b, hid, p.act2, mu, rs, s1, s2);
-      if (lane == 0) {
-        st[w] = s1;
-        st[16 + w] = s2;
-        st[32 + w] = rs;
-      }
+      const float m2 = p.m2[(size_t)t * B + w];
+      rsw = p.r2[(size_t)t * B + w];
+      wave_ln_bwd_regs<LN_M>(As + w * lda, R + w * lda, l2w, l2b, hid, p.act2, m2, rsw, xh, dzr, s1, s2);
     }
     __syncthreads();
     int lo, hi;
     part_range(hid, i, n2, lo, hi);
     ln_param_partials(As, lda, R, lda, B, lo, hi, p.p2g + (size_t)t * hid, p.p2b + (size_t)t * hid);
     __syncthreads();
-    if (w < B) {
-      const float s1 = st[w], s2 = st[16 + w], rs = st[32 + w];
-      float* x = As + w * lda;
-      const float* dz = R + w * lda;
-      for (int k = lane; k < hid; k += 64) x[k] = rs * (dz[k] * l2w[k] - s1 - x[k] * s2);
-    }
+    if (w < B) wave_ln_bwd_finish<LN_M>(As + w * lda, l2w, hid, rsw, s1, s2, xh, dzr);
     __syncthreads();
     part_range(B * hid, i, n2, lo, hi);
     float* du = p.du + (size_t)t * B * hid;
     for (int e = lo + threadIdx.x; e < hi; e += NTH) du[e] = As[(e / hid) * lda + e % hid];
+    PROF(4, 2);
     gemm_reg<1, U2>(wt, As, lda, hid, red, ct);
-    if (threadIdx.x < 256) {
-      const int b = threadIdx.x >> 4, c = threadIdx.x & 15;
-      if (b < B) {
-        float* d = p.DH + ((size_t)t * B + b) * H + i * 16 + c;
-        st_wt(d, ld_wt(d) + ct[threadIdx.x]);
-      }
-    }
-    arrive(p.sync + 1 * NSH * SHW);
-  }
-}
-
-// G3: dgx_t = LNGRU'(DH_t) (+ LN-GRU parameter partials); dcat tile = dgx_t Wg (K = 3H); h columns of
-// the tile go straight into DH_{t-1} with the gate's direct path, feature columns are handed to G4.
-__device__ __forceinline__ void bwd_G3(const PP& p, int i3, float* sm) {
-  const int B = p.B, H = p.H, D = p.D, HD = H + D, N3 = 3 * H, T = p.T;
-  const int n2 = H / 16, n3 = HD / 16;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lda = N3 + 4, n0 = i3 * 16;
-  const int nch = g3_nch(H, D);
-  float* As = sm;
-  float* lgw = As + 16 * lda;
-  float* lgb = lgw + N3;
-  float* red = lgb + N3;
-  float* ct = red + 4096;
-  float* dhpL = ct + 256;  // [16][16]: direct h gradient of this tile's columns
-  float* sc = dhpL + 256;  // [2][nch][16] column partial scratch
-  int* flag = (int*)(sc + 32 * nch);
-  WTile<1, U3> wt;
-  wload<1, U3>(wt, p.WgT + (size_t)n0 * N3, N3, N3, w);
-  stage_vec(lgw, p.lngw, N3);
-  stage_vec(lgb, p.lngb, N3);
-  const u32 e2 = shard_count(p.hid / 16, n2);
-  int clo, chi;
-  part_range(N3, i3, n3, clo, chi);
-  const int ncol = chi - clo;
-  const int i = w;
-  const bool row_ok = i < B;
-  __syncthreads();
-  for (int t = T - 1; t >= 0; --t) {
-    stage(As, lda, p.gx + (size_t)t * B * N3, N3, B, N3);
-    if (!wait_ctr(p.sync, 1, e2, T - t, 13, flag)) return;
-    if (row_ok) {
-      const float mu = p.mg[(size_t)t * B + i], rs = p.rg[(size_t)t * B + i];
-      const float* DHr = p.DH + ((size_t)t * B + i) * H;
-      const float* catr = p.cat + ((size_t)t * B + i) * HD;  // (1 - first) h_{t-1}
-      float* x = As + i * lda;
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll 2
-      for (int m = 0; m < GRU_M; ++m) {  // pass 1: gate adjoints, stored as dz*gamma in place
-        const int j = lane + 64 * m;
-        if (j < H) {
-          const float a0 = (x[j] - mu) * rs, a1 = (x[H + j] - mu) * rs, a2 = (x[2 * H + j] - mu) * rs;
-          const float zr = a0 * lgw[j] + lgb[j];
-          const float zc = a1 * lgw[H + j] + lgb[H + j];
-          const float zu = a2 * lgw[2 * H + j] + lgb[2 * H + j];
-          const float r = fsig(zr), c = ftanh(r * zc), u = fsig(zu - 1.f);
-          const float go = ld_wt(DHr + j);
-          const float dua = go * (c - catr[j]);
-          const float da = go * u * (1.f - c * c);
-          const float dz2 = dua * u * (1.f - u);
-          const float dz1 = da * r;
-          const float dz0 = da * zc * r * (1.f - r);
-          const float d0 = dz0 * lgw[j], d1 = dz1 * lgw[H + j], d2 = dz2 * lgw[2 * H + j];
-          x[j] = d0;
-          x[H + j] = d1;
-          x[2 * H + j] = d2;
-          s1 += d0 + d1 + d2;
-          s2 += d0 * a0 + d1 * a1 + d2 * a2;
-          if (j >= clo && j < chi) {
-            sc[(j - clo) * 16 + i] = dz0 * a0;
-            sc[(ncol + j - clo) * 16 + i] = dz0;
-          }
-          if (H + j >= clo && H + j < chi) {
-            sc[(H + j - clo) * 16 + i] = dz1 * a1;
-            sc[(ncol + H + j - clo) * 16 + i] = dz1;
-          }
-          if (2 * H + j >= clo && 2 * H + j < chi) {
-            sc[(2 * H + j - clo) * 16 + i] = dz2 * a2;
-            sc[(ncol + 2 * H + j - clo) * 16 + i] = dz2;
-          }
-          if (j >= n0 && j < n0 + 16) dhpL[i * 16 + j - n0] = go * (1.f - u);
-        }
-      }
-      const float m1 = wave_sum(s1) / N3, m2 = wave_sum(s2) / N3;
-      // pass 2: dgx (the wave owns its row); the normalised inputs are re-read from gx (just staged,
-      // cache-resident) instead of being held in 3 x GRU_M registers across the row reduction
-      const float* gxr = p.gx + ((size_t)t * B + i) * N3;
-#pragma unroll
-      for (int m = 0; m < GRU_M; ++m) {
-        const int j = lane + 64 * m;
-        if (j < H) {
-          x[j] = rs * (x[j] - m1 - (gxr[j] - mu) * rs * m2);
-          x[H + j] = rs * (x[H + j] - m1 - (gxr[H + j] - mu) * rs * m2);
-          x[2 * H + j] = rs * (x[2 * H + j] - m1 - (gxr[2 * H + j] - mu) * rs * m2);
+    PROF(4, 3);
+    if (eok) {
+      const float go = rv ? ld_wt(p.DH + ((size_t)t * B + eb) * H + j) + ct[threadIdx.x] : 0.f;
+      const float x0 = pre[threadIdx.x], x1 = pre[256 + threadIdx.x], x2 = pre[512 + threadIdx.x];
+      const float hp = pre[768 + threadIdx.x], mu = pre[1024 + threadIdx.x], rsg = pre[1280 + threadIdx.x];
+      const float keep = pre[1536 + threadIdx.x];
+      const float a0 = (x0 - mu) * rsg, a1 = (x1 - mu) * rsg, a2 = (x2 - mu) * rsg;
+      const float r = fsig(a0 * gw0 + gb0), zc = a1 * gw1 + gb1, c = ftanh(r * zc), u = fsig(a2 * gw2 + gb2 - 1.f);
+      const float dua = go * (c - hp);
+      const float da = go * u * (1.f - c * c);
+      const float dz2 = dua * u * (1.f - u);
+      const float dz1 = da * r;
+      const float dz0 = da * zc * r * (1.f - r);
+      const float d0 = dz0 * gw0, d1 = dz1 * gw1, d2 = dz2 * gw2;
+      const float s1p = seg_sum(d0 + d1 + d2, 16), s2p = seg_sum(d0 * a0 + d1 * a1 + d2 * a2, 16);
+      float* g = gsc + eb * 96 + ec;
+      g[0] = dz0 * a0;
+      g[16] = dz0;
+      g[32] = dz1 * a1;
+      g[48] = dz1;
+      g[64] = dz2 * a2;
+      g[80] = dz2;
+      if (rv) {
+        float* dZ = p.dZ + ((size_t)t * B + eb) * N3;
+        st_wt(dZ + j, d0);
+        st_wt(dZ + H + j, d1);
+        st_wt(dZ + 2 * H + j, d2);
+        if (ec == 0) st_wt2(p.sst + (((size_t)t * n2 + i) * 16 + eb) * 2, s1p, s2p);
+        if (t > 0) {  // direct path h_{t-1} -> h_t through the update gate
+          float* d = p.DH + ((size_t)(t - 1) * B + eb) * H + j;
+          st_wt(d, ld_wt(d) + keep * go * (1.f - u));
         }
       }
     }
     __syncthreads();
-    for (int col = threadIdx.x; col < ncol; col += NTH) {
-      float ag = 0.f, ab = 0.f;
-      for (int b = 0; b < B; ++b) {
-        ag += sc[col * 16 + b];
-        ab += sc[(ncol + col) * 16 + b];
-      }
-      p.pgg[(size_t)t * N3 + clo + col] = ag;
-      p.pgb[(size_t)t * N3 + clo + col] = ab;
+    if (threadIdx.x < 96) {  // LN-GRU parameter partials of this workgroup's 3 x 16 gate columns
+      const int k = threadIdx.x >> 4, c = threadIdx.x & 15;
+      float a = 0.f;
+      for (int b = 0; b < B; ++b) a += gsc[b * 96 + k * 16 + c];
+      const int col = (k >> 1) * H + i * 16 + c;
+      (k & 1 ? p.pgb : p.pgg)[(size_t)t * N3 + col] = a;
     }
+    arrive(p.sync + 1 * NSH * SHW);
+    PROF(4, 4);
+  }
+}
+
+// G3: dgx_t = rs (dz*gamma - mean(dz*gamma) - xh mean(dz*gamma*xh)) from G2's pieces; dcat tile =
+// dgx_t Wg (K = 3H); h columns of the tile go straight into DH_{t-1}, feature columns to G4.
+__device__ __forceinline__ void bwd_G3(const PP& p, int i3, float* sm) {
+  const bool first_wg = i3 == 0;
+  const int B = p.B, H = p.H, D = p.D, HD = H + D, N3 = 3 * H, T = p.T;
+  const int n2 = H / 16, n3 = HD / 16;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lda = N3 + 4, n0 = i3 * 16;
+  float* As = sm;
+  float* rowst = As + 16 * lda;  // [16][4]: mu, rs, mean(dz*g), mean(dz*g*xh)
+  float* red = rowst + 64;
+  float* ct = red + 4096;
+  int* flag = (int*)(ct + 256);
+  WTile<1, U3> wt;
+  wload<1, U3>(wt, p.WgT + (size_t)n0 * N3, N3, N3, w);
+  const u32 e2 = shard_count(p.hid / 16, n2);
+  __syncthreads();
+  for (int t = T - 1; t >= 0; --t) {
+    PROF(5, 0);
+    stage(As, lda, p.gx + (size_t)t * B * N3, N3, B, N3);
+    if (threadIdx.x < B) {
+      rowst[threadIdx.x * 4] = p.mg[(size_t)t * B + threadIdx.x];
+      rowst[threadIdx.x * 4 + 1] = p.rg[(size_t)t * B + threadIdx.x];
+    }
+    if (!wait_ctr(p.sync, 1, e2, T - t, 13, flag)) return;
+    PROF(5, 1);
+    if (w < B) {
+      const float2 sp = lane < n2 ? ld_wt2(p.sst + (((size_t)t * n2 + lane) * 16 + w) * 2) : make_float2(0.f, 0.f);
+      const float m1 = wave_sum(sp.x) / N3, m2 = wave_sum(sp.y) / N3;
+      if (lane == 0) {
+        rowst[w * 4 + 2] = m1;
+        rowst[w * 4 + 3] = m2;
+      }
+    }
+    __syncthreads();
+    {
+      const int c4 = N3 >> 2, n = B * c4;
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.dZ + (size_t)t * B * N3, (short)0, B * N3 * 4, 0x00020000);
+      for (int e = threadIdx.x; e < n; e += NTH) {
+        const int r = e / c4, k = (e - r * c4) << 2;
+        const f4 d = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (r * N3 + k) * 4, 0, 16));
+        const float mu = rowst[r * 4], rg = rowst[r * 4 + 1], m1 = rowst[r * 4 + 2], m2 = rowst[r * 4 + 3];
+        f4* x = (f4*)(As + r * lda + k);
+        *x = rg * (d - m1 - (*x - mu) * (rg * m2));
+      }
+    }
+    __syncthreads();
     {
       int lo, hi;
       part_range(B * N3, i3, n3, lo, hi);
       float* dgx = p.dgx + (size_t)t * B * N3;
       for (int e = lo + threadIdx.x; e < hi; e += NTH) dgx[e] = As[(e / N3) * lda + e % N3];
     }
+    PROF(5, 2);
     gemm_reg<1, U3>(wt, As, lda, N3, red, ct);
+    PROF(5, 3);
     if (threadIdx.x < 256) {
       const int b = threadIdx.x >> 4, c = threadIdx.x & 15;
       if (b < B) {
@@ -685,17 +757,19 @@ __device__ __forceinline__ void bwd_G3(const PP& p, int i3, float* sm) {
           st_wt(p.dcat + ((size_t)t * B + b) * HD + n0 + c, v);
         } else if (t > 0) {
           float* d = p.DH + ((size_t)(t - 1) * B + b) * H + n0 + c;
-          st_wt(d, ld_wt(d) + (1.f - p.first[(size_t)t * B + b]) * (dhpL[b * 16 + c] + v));
+          st_wt(d, ld_wt(d) + (1.f - p.first[(size_t)t * B + b]) * v);
         }
       }
     }
     arrive(p.sync + 2 * NSH * SHW);
+    PROF(5, 4);
   }
 }
 
 // G4: dx_t = LN1'(dcat_x) (+ LN1 parameter partials); dz = dx_t Wz (K = D);
 // dlog_{t-1} = unimix_ST'(logits_{t-1}; dmixed, d_post + (1-first_t) dz).
 __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
+  const bool first_wg = i4 == 0;
   const int B = p.B, S = p.S, D = p.D, H = p.H, HD = H + D, C = p.C, T = p.T;
   const int n3 = HD / 16, n4 = S / 32;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lda = D + 4, n0 = i4 * 32;
@@ -714,47 +788,41 @@ __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
   const u32 e3 = shard_count(p.hid / 16 + H / 16, n3);
   __syncthreads();
   for (int t = T - 1; t >= 0; --t) {
+    PROF(6, 0);
     stage(As, lda, p.xr + (size_t)t * B * D, D, B, D);
+    // epilogue inputs (forward values / external gradients of step t-1): loaded behind the wait
+    const int eb = threadIdx.x >> 5, ec = threadIdx.x & 31, ebb = eb < B ? eb : 0;
+    const size_t eo = (size_t)(t > 0 ? t - 1 : 0) * B * S + (size_t)ebb * S + n0 + ec;
+    const bool eok = threadIdx.x < 512 && t > 0;
+    const float el = eok ? p.logits[eo] : 0.f, egm = eok ? p.dmixed[eo] : 0.f;
+    const float edp = (eok && p.dpost) ? p.dpost[eo] : 0.f, ekeep = eok ? 1.f - p.first[(size_t)t * B + ebb] : 0.f;
     if (!wait_ctr(p.sync, 2, e3, T - t, 14, flag)) return;
+    PROF(6, 1);
     stage_wt(R, lda, p.dcat + (size_t)t * B * HD + H, HD, B, D);
     __syncthreads();
+    float xh[LN_M], dzr[LN_M], s1 = 0.f, s2 = 0.f, rsw = 0.f;
     if (w < B) {
-      const float mu = p.m1[(size_t)t * B + w], rs = p.r1[(size_t)t * B + w];
-      float s1, s2;
-      wave_ln_bwd_prep(As + w * lda, R + w * lda, l1w, l1b, D, p.act1, mu, rs, s1, s2);
-      if (lane == 0) {
-        st[w] = s1;
-        st[16 + w] = s2;
-        st[32 + w] = rs;
-      }
+      const float mu = p.m1[(size_t)t * B + w];
+      rsw = p.r1[(size_t)t * B + w];
+      wave_ln_bwd_regs<LN_M>(As + w * lda, R + w * lda, l1w, l1b, D, p.act1, mu, rsw, xh, dzr, s1, s2);
     }
     __syncthreads();
     int lo, hi;
     part_range(D, i4, n4, lo, hi);
     ln_param_partials(As, lda, R, lda, B, lo, hi, p.p1g + (size_t)t * D, p.p1b + (size_t)t * D);
     __syncthreads();
-    if (w < B) {
-      const float s1 = st[w], s2 = st[16 + w], rs = st[32 + w];
-      float* x = As + w * lda;
-      const float* dz = R + w * lda;
-      for (int k = lane; k < D; k += 64) x[k] = rs * (dz[k] * l1w[k] - s1 - x[k] * s2);
-    }
+    if (w < B) wave_ln_bwd_finish<LN_M>(As + w * lda, l1w, D, rsw, s1, s2, xh, dzr);
     __syncthreads();
     part_range(B * D, i4, n4, lo, hi);
     float* dx = p.dx + (size_t)t * B * D;
     for (int e = lo + threadIdx.x; e < hi; e += NTH) dx[e] = As[(e / D) * lda + e % D];
     if (t == 0) break;  // no z_{-1} to propagate into
+    PROF(6, 2);
     gemm_reg<2, U4>(wt, As, lda, D, red, ct);
+    PROF(6, 3);
     if (threadIdx.x < 512) {
-      const float* first = p.first + (size_t)t * B;
-      const size_t base = (size_t)(t - 1) * B * S;
-      const int idx = threadIdx.x;
-      const int b = idx >> 5, c = idx & 31;
-      const bool valid = b < B;
-      const int bb = valid ? b : 0;
-      const size_t o = base + (size_t)bb * S + n0 + c;
-      const float ds = (p.dpost ? p.dpost[o] : 0.f) + (1.f - first[bb]) * ct[idx];
-      const float l = p.logits[o];
+      const float ds = edp + ekeep * ct[threadIdx.x];
+      const float l = el;
       float q = 0.f, pm = 0.f, m = l;
       bool clamped = false;
       if (p.alpha > 0.f) {
@@ -765,7 +833,7 @@ __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
         clamped = pm <= FEPS || pm >= 1.f - FEPS;
         m = logf(fminf(fmaxf(pm, FEPS), 1.f - FEPS));
       }
-      float gm = p.dmixed[o];
+      float gm = egm;
       const float mx2 = seg_max(m, C);
       const float e2 = __expf(m - mx2);
       const float pr = e2 / seg_sum(e2, C);
@@ -778,9 +846,10 @@ __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
       } else {
         dl = gm;
       }
-      if (valid) st_wt(p.dlog + o, dl);
+      if (eb < B) st_wt(p.dlog + eo, dl);
     }
     arrive(p.sync + 3 * NSH * SHW);
+    PROF(6, 4);
   }
 }
 
@@ -816,13 +885,12 @@ int scanp_sync_words() { return ERRW + SHW; }
 int scanp_fwd_grid(int S, int H, int hid) { return 3 * H / 16 + hid / 16 + S / 32; }
 int scanp_bwd_grid(int S, int D, int H, int hid) { return hid / 16 + H / 16 + (H + D) / 16 + S / 32; }
 
-int scanp_fwd_lds(int S, int D, int H, int hid) {
-  (void)S;
-  return 4 * std::max(std::max(lds_A(D, H), lds_B(H)), lds_C(hid));
+int scanp_fwd_lds(int S, int D, int H, int hid, int C) {
+  return 4 * std::max(std::max(lds_A(D, H), lds_B(H)), lds_C(hid, S, C));
 }
 
 int scanp_bwd_lds(int S, int D, int H, int hid) {
-  return 4 * std::max(std::max(lds_G1(S), lds_G2(hid)), std::max(lds_G3(H, D), lds_G4(D)));
+  return 4 * std::max(std::max(lds_G1(S), lds_G2(hid)), std::max(lds_G3(H), lds_G4(D)));
 }
 
 // Shape gate (register tile caps, LDS, residency of every workgroup): mirrors the kernels.
@@ -830,9 +898,10 @@ bool scanp_supported(int B, int S, int D, int H, int hid, int C) {
   if (B < 1 || B > 16 || C < 1 || C > 32 || (32 % C) != 0 || S % 32 || D % 16 || H % 16 || hid % 16) return false;
   if (H + D > 16 * 16 * UA || H > 16 * 16 * UB || hid > 16 * 16 * UC) return false;
   if (S > 16 * 16 * U1 || hid > 16 * 16 * U2 || 3 * H > 16 * 16 * U3 || D > 16 * 16 * U4 || H > 64 * GRU_M) return false;
+  if (D > 64 * LN_M || hid > 64 * LN_M) return false;
   if (3 * H / 16 > 128) return false;  // Chan combine: two partials per lane
   const int mx = 160 * 1024;
-  if (scanp_fwd_lds(S, D, H, hid) > mx || scanp_bwd_lds(S, D, H, hid) > mx) return false;
+  if (scanp_fwd_lds(S, D, H, hid, C) > mx || scanp_bwd_lds(S, D, H, hid) > mx) return false;
   int dev = 0, cus = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -846,7 +915,7 @@ void launch_scanp_fwd(const PP& p, hipStream_t st) {
     init = true;
   }
   hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(256), 0, st, p.sync, scanp_sync_words());
-  hipLaunchKernelGGL(fwd_kernel, dim3(scanp_fwd_grid(p.S, p.H, p.hid)), dim3(NTH), scanp_fwd_lds(p.S, p.D, p.H, p.hid), st,
+  hipLaunchKernelGGL(fwd_kernel, dim3(scanp_fwd_grid(p.S, p.H, p.hid)), dim3(NTH), scanp_fwd_lds(p.S, p.D, p.H, p.hid, p.C), st,
                      p);
 }
 

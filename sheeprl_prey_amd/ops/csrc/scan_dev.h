@@ -168,6 +168,82 @@ __device__ __forceinline__ void wave_row_stats(const float* r, int N, float eps,
   rs = rsqrtf(wave_sum(q) / N + eps);
 }
 
+// LayerNorm + activation of one row r[0:N) (N <= 64 * M) by the calling wave, the row held in
+// registers: one LDS read per element, both statistics from registers, one write.
+template <int M>
+__device__ __forceinline__ void wave_ln_act_row(float* r, int N, float eps, const float* gam, const float* bet, int act,
+                                                float& mu, float& rs) {
+  const int s = threadIdx.x & 63;
+  float v[M];
+  float a = 0.f;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int k = s + 64 * m;
+    v[m] = k < N ? r[k] : 0.f;
+    a += v[m];
+  }
+  mu = wave_sum(a) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int k = s + 64 * m;
+    const float d = k < N ? v[m] - mu : 0.f;
+    q += d * d;
+  }
+  rs = rsqrtf(wave_sum(q) / N + eps);
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int k = s + 64 * m;
+    if (k < N) r[k] = f_act((v[m] - mu) * rs * gam[k] + bet[k], act);
+  }
+}
+
+// LayerNorm(+act) adjoint of one row, first pass, with the row in registers (N <= 64 * M): loads x
+// and dy once, leaves xh / dz in registers AND in place (x <- xh, dy <- dz, for ln_param_partials);
+// returns s1 = mean(dz*gamma), s2 = mean(dz*gamma*xh).  Finish with wave_ln_bwd_finish.
+template <int M>
+__device__ __forceinline__ void wave_ln_bwd_regs(float* x, float* dy, const float* gam, const float* bet, int N, int act,
+                                                 float mu, float rs, float (&xh)[M], float (&dz)[M], float& s1, float& s2) {
+  const int s = threadIdx.x & 63;
+  float xv[M], dv[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int k = s + 64 * m;
+    xv[m] = k < N ? x[k] : 0.f;
+    dv[m] = k < N ? dy[k] : 0.f;
+  }
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int k = s + 64 * m;
+    if (k < N) {
+      xh[m] = (xv[m] - mu) * rs;
+      dz[m] = dv[m] * f_act_grad(xh[m] * gam[k] + bet[k], act);
+      const float dxh = dz[m] * gam[k];
+      a += dxh;
+      b += dxh * xh[m];
+      x[k] = xh[m];
+      dy[k] = dz[m];
+    } else {
+      xh[m] = 0.f;
+      dz[m] = 0.f;
+    }
+  }
+  s1 = wave_sum(a) / N;
+  s2 = wave_sum(b) / N;
+}
+
+template <int M>
+__device__ __forceinline__ void wave_ln_bwd_finish(float* x, const float* gam, int N, float rs, float s1, float s2,
+                                                   const float (&xh)[M], const float (&dz)[M]) {
+  const int s = threadIdx.x & 63;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int k = s + 64 * m;
+    if (k < N) x[k] = rs * (dz[m] * gam[k] - s1 - xh[m] * s2);
+  }
+}
+
 // LayerNorm(+act) adjoint, first pass, by the wave owning a row: x <- xh, dy <- dz = dy * act'(z);
 // returns (mean(dz*gamma), mean(dz*gamma*xh)).
 __device__ __forceinline__ void wave_ln_bwd_prep(float* x, float* dy, const float* gam, const float* bet, int N, int act,

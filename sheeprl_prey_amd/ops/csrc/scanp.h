@@ -17,12 +17,17 @@ struct PP {
   const float *P, *first, *uni, *z0, *Wz, *WzT, *ln1w, *ln1b, *Wg, *lngw, *lngb, *W1, *ln2w, *ln2b, *W2, *b2;
   // forward state: xr holds a_proj + first * (z0 Wz^T) on entry and receives the posterior row gathers
   float *xr, *cat, *zm, *m1, *r1, *gx, *gst, *mg, *rg, *hs, *u, *v, *m2, *r2, *logits, *mixed, *samples;
+  int* sel;  // [T][B][S/C] sampled row of Wz^T per (row, categorical), -1 = reset row (hand-off C -> C)
   // backward inputs
   const float *W2T, *W1T, *WgT, *dpost, *dmixed;
   // backward state / outputs: DH holds d_hs on entry, dlog[T-1] is written before the launch
   float *DH, *dlog, *dv, *du, *dgx, *dcat, *dx, *p1g, *p1b, *pgg, *pgb, *p2g, *p2b;
+  // LN-GRU adjoint pieces handed G2 -> G3: dz*gamma per gate column [T][B][3H], row partial sums [T][H/16][16][2]
+  float *dZ, *sst;
   // hand-off counters (zeroed before every launch) and the error word (0 = ok)
   unsigned* sync;
+  // optional phase timestamps (first workgroup of each role, thread 0): prof[(role * T + t) * 8 + k]
+  long long* prof;
 };
 
 }  // namespace scanp

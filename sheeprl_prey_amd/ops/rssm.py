@@ -260,7 +260,8 @@ class RSSMPersistFn(torch.autograd.Function):
                ln1_b.contiguous(), Wg.contiguous(), lng_w.contiguous(), lng_b.contiguous(), W1.contiguous(),
                ln2_w.contiguous(), ln2_b.contiguous(), W2.contiguous(), b2.contiguous(),
                xr, e(T, B, H + D), zm, e(T, B), e(T, B), e(T, B, 3 * H), e(T, 3 * H // 16, 16, 2), e(T, B), e(T, B),
-               e(T, B, H), e(T, B, hid), e(T, B, hid), e(T, B), e(T, B), e(T, B, S), e(T, B, S), e(T, B, S), sync]
+               e(T, B, H), e(T, B, hid), e(T, B, hid), e(T, B), e(T, B), e(T, B, S), e(T, B, S), e(T, B, S),
+               torch.empty(T, B, S // disc, device=dev, dtype=torch.int32), sync]
         dims = [T, B, S, D, H, hid, disc, act1, act2]
         fl = [alpha, eps1, epsg, eps2]
         C.scanp_fwd(fwd, dims, fl)
@@ -291,7 +292,7 @@ class RSSMPersistFn(torch.autograd.Function):
         dv, du, dgx, dcat, dx = e(T, B, hid), e(T, B, hid), e(T, B, 3 * H), e(T, B, H + D), e(T, B, D)
         p1g, p1b, pgg, pgb, p2g, p2b = e(T, D), e(T, D), e(T, 3 * H), e(T, 3 * H), e(T, hid), e(T, hid)
         bwd = [W2.t().contiguous(), W1.t().contiguous(), Wg.t().contiguous(), dpost, dmixed, DH, dlog, dv, du, dgx, dcat,
-               dx, p1g, p1b, pgg, pgb, p2g, p2b]
+               dx, p1g, p1b, pgg, pgb, p2g, p2b, e(T, B, 3 * H), e(T, H // 16, 16, 2)]
         C.scanp_bwd(fwd + bwd, ctx.dims, ctx.fl)
         cat, zm, hs, v = fwd[17], fwd[18], fwd[25], fwd[27]
         TB = T * B

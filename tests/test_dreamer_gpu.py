@@ -116,7 +116,7 @@ def _check_scan_vs_python(H, D, hid, B, T, impl, tol=(2e-3, 2e-4), gtol=(3e-3, 3
     names = ["h", "post", "post_logits", "prior_logits"]
     for n, a, b in zip(names, out1, out2):
         torch.testing.assert_close(a, b, rtol=tol[0], atol=tol[1], msg=lambda m: f"{n}: {m}")
-    sync = out1[0].grad_fn.saved_tensors[33] if impl == "persist" else None  # hand-off counters + error word
+    sync = out1[0].grad_fn.saved_tensors[34] if impl == "persist" else None  # hand-off counters + error word
     gs = [torch.randn_like(o) for o in out1]
     sum((o * g).sum() for o, g in zip(out1, gs)).backward()
     sum((o * g).sum() for o, g in zip(out2, gs)).backward()
