@@ -270,6 +270,7 @@ class RSSM(nn.Module):
         gru = self.recurrent_model.rnn
         rec = list(self.recurrent_model.mlp.model)
         return (isinstance(gru.layer_norm, nn.LayerNorm) and isinstance(rec[0], nn.Linear)
+                and not getattr(self, "_srl_autocast", False) and not getattr(actor, "_srl_autocast", False)
                 and type(actor) is Actor and not actor.is_continuous and ops.native_available() and ops.fused_enabled()
                 and gru.layer_norm.weight is not None and gru.layer_norm.bias is not None)
 
@@ -341,6 +342,9 @@ class RSSM(nn.Module):
         Returns recurrent_states [T,B,H], posteriors [T,B,S,D], posteriors_logits [T,B,S*D],
         priors_logits [T,B,S*D]."""
         T, B = embedded_obs.shape[:2]
+        if getattr(self, "_srl_autocast", False):
+            # bf16-mixed: every sub-model through its own (autocast) forward, as the reference does
+            return self._scan_by_steps(embedded_obs, actions, is_first, uniform)
         if ops._native(embedded_obs) and getattr(self, "fused_scan", True):
             from sheeprl_prey_amd.ops.rssm import fused_scan, fused_scan_supported
 
@@ -395,6 +399,23 @@ class RSSM(nn.Module):
         recurrent_states = torch.stack(hs)
         posteriors = torch.stack(posts).view(T, B, -1, self.discrete)
         return recurrent_states, posteriors, torch.stack(post_logits), torch.stack(prior_logits)
+
+    def _scan_by_steps(self, embedded_obs: Tensor, actions: Tensor, is_first: Tensor, uniform: Optional[Tensor] = None):
+        """``dynamic`` step by step (reference loop ``dreamer_v3.py:122-129``): each sub-model is called
+        through its forward, so set-up hooks (autocast) apply."""
+        T, B = embedded_obs.shape[:2]
+        H = self.recurrent_model.rnn.hidden_size
+        S = self.transition_model.model[-1].out_features
+        h = torch.zeros(B, H, device=embedded_obs.device)
+        z = torch.zeros(B, S // self.discrete, self.discrete, device=embedded_obs.device)
+        hs, posts, post_logits, prior_logits = [], [], [], []
+        for t in range(T):
+            h, z, _, ql, pl = self.dynamic(z, h, actions[t], embedded_obs[t], is_first[t])
+            hs.append(h)
+            posts.append(z)
+            post_logits.append(ql)
+            prior_logits.append(pl)
+        return torch.stack(hs), torch.stack(posts), torch.stack(post_logits), torch.stack(prior_logits)
 
     def _uniform_mix_fused(self, logits: Tensor) -> Tensor:
         """Unimix logits only (no sampling) - the prior in the posterior scan is never sampled."""

@@ -345,6 +345,7 @@ class FusedCartPoleRollout:
         from sheeprl_prey_amd.envs.device import CartPoleDevice
 
         return (isinstance(env, CartPoleDevice) and env.device.type == "cuda" and list(agent.actions_dim) == [2]
+                and not getattr(agent, "_srl_autocast", False)  # bf16-mixed: the agent's autocast forward instead
                 and cls.chains_of(agent) is not None)
 
     @torch.no_grad()

@@ -424,3 +424,59 @@ def squashed_gaussian(mean: Tensor, log_std: Tensor, scale: Tensor, bias: Tensor
         return _SquashedGaussian.apply(mean, log_std, eps, scale.float().contiguous(), bias.float().contiguous(),
                                        int(mode), float(lo), float(hi))
     return ref.squashed_gaussian(mean, log_std, eps, scale, bias, mode, lo, hi)
+
+
+# =============================================================== truncated normal (DreamerV2/V3 continuous actors)
+class _TruncNormRsample(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, loc, scale, lo, hi, u):
+        x = _ext().truncnorm_rsample_fwd(loc, scale, lo, hi, u)
+        ctx.save_for_backward(loc, scale, lo, hi, u)
+        return x
+
+    @staticmethod
+    def backward(ctx, gx):
+        gl, gs = _ext().truncnorm_rsample_bwd(*ctx.saved_tensors, gx.contiguous())
+        return gl, gs, None, None, None
+
+
+class _TruncNormLogProb(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, value, loc, scale, lo, hi):
+        lp = _ext().truncnorm_logprob_fwd(value, loc, scale, lo, hi)
+        ctx.save_for_backward(value, loc, scale, lo, hi)
+        return lp
+
+    @staticmethod
+    def backward(ctx, g):
+        value, loc, scale, lo, hi = ctx.saved_tensors
+        gv, gl, gs = _ext().truncnorm_logprob_bwd(value, loc, scale, lo, hi, g.contiguous())
+        lead = value.numel() // loc.numel()  # broadcast over leading sample dimensions
+        return gv, gl.view(lead, *loc.shape).sum(0), gs.view(lead, *loc.shape).sum(0), None, None
+
+
+def _tn_bound(b: Tensor, like: Tensor) -> Tensor:
+    return b.reshape(1).float() if b.numel() == 1 else b.expand_as(like).float().contiguous()
+
+
+def _tn_native(loc: Tensor, lo: Tensor, hi: Tensor) -> bool:
+    return (_native(loc) and loc.dtype == torch.float32 and not lo.requires_grad and not hi.requires_grad
+            and lo.device == loc.device and hi.device == loc.device)
+
+
+def truncnorm_rsample(loc: Tensor, scale: Tensor, lo: Tensor, hi: Tensor, u: Tensor) -> Tensor:
+    """Reparameterised truncated-normal sample for uniforms ``u`` (one fused launch forward and backward
+    on GPU; ``loc``, ``scale``, ``u`` share one shape, bounds are scalars or that shape)."""
+    if _tn_native(loc, lo, hi) and loc.shape == scale.shape == u.shape:
+        return _TruncNormRsample.apply(loc.contiguous(), scale.contiguous(), _tn_bound(lo, loc), _tn_bound(hi, loc),
+                                       u.contiguous())
+    return ref.truncnorm_rsample(loc, scale, lo, hi, u)
+
+
+def truncnorm_log_prob(value: Tensor, loc: Tensor, scale: Tensor, lo: Tensor, hi: Tensor) -> Tensor:
+    """Truncated-normal log-density; ``value`` is ``[sample..., *loc.shape]``."""
+    if (_tn_native(loc, lo, hi) and loc.shape == scale.shape and value.dtype == torch.float32
+            and value.shape[value.dim() - loc.dim():] == loc.shape):
+        return _TruncNormLogProb.apply(value.contiguous(), loc.contiguous(), scale.contiguous(), _tn_bound(lo, loc),
+                                       _tn_bound(hi, loc))
+    return ref.truncnorm_log_prob(value, loc, scale, lo, hi)

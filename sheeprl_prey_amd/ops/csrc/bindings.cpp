@@ -55,6 +55,15 @@ void launch_squashed_gaussian_fwd(const float*, const float*, const float*, cons
 void launch_squashed_gaussian_bwd(const float*, const float*, const float*, const float*, const float*, const float*, float*,
                                   float*, int, int, int, float, float, hipStream_t);
 
+void launch_truncnorm_rsample_fwd(const float*, const float*, const float*, int, const float*, int, const float*, float*, int,
+                                  hipStream_t);
+void launch_truncnorm_rsample_bwd(const float*, const float*, const float*, int, const float*, int, const float*, const float*,
+                                  float*, float*, int, hipStream_t);
+void launch_truncnorm_logprob_fwd(const float*, const float*, const float*, const float*, int, const float*, int, float*, int,
+                                  int, hipStream_t);
+void launch_truncnorm_logprob_bwd(const float*, const float*, const float*, const float*, int, const float*, int, const float*,
+                                  float*, float*, float*, int, int, hipStream_t);
+
 void launch_scan4_fwd(const srl::scan4::SP&, hipStream_t);
 void launch_scan4_bwd(const srl::scan4::SP&, hipStream_t);
 int scan4_fwd_lds(int, int, int, int);
@@ -619,6 +628,63 @@ void scanp_bwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>&
   launch_scanp_bwd(p, cur_stream());
 }
 
+// ------------------------------------------------------------------ truncated normal (ops.truncnorm_*)
+void tn_check(const torch::Tensor& loc, const torch::Tensor& scale, const torch::Tensor& lo, const torch::Tensor& hi) {
+  check_f32(loc, "loc");
+  check_f32(scale, "scale");
+  check_f32(lo, "lo");
+  check_f32(hi, "hi");
+  TORCH_CHECK(scale.numel() == loc.numel(), "truncnorm: loc / scale sizes differ");
+  TORCH_CHECK(lo.numel() == 1 || lo.numel() == loc.numel(), "truncnorm: lo must be a scalar or loc-shaped");
+  TORCH_CHECK(hi.numel() == 1 || hi.numel() == loc.numel(), "truncnorm: hi must be a scalar or loc-shaped");
+}
+
+torch::Tensor truncnorm_rsample_fwd(torch::Tensor loc, torch::Tensor scale, torch::Tensor lo, torch::Tensor hi, torch::Tensor u) {
+  tn_check(loc, scale, lo, hi);
+  check_f32(u, "u");
+  TORCH_CHECK(u.numel() == loc.numel(), "truncnorm: u must be loc-shaped");
+  auto x = torch::empty_like(loc);
+  launch_truncnorm_rsample_fwd(loc.data_ptr<float>(), scale.data_ptr<float>(), lo.data_ptr<float>(), (int)lo.numel(),
+                               hi.data_ptr<float>(), (int)hi.numel(), u.data_ptr<float>(), x.data_ptr<float>(), (int)loc.numel(),
+                               cur_stream());
+  return x;
+}
+
+std::vector<torch::Tensor> truncnorm_rsample_bwd(torch::Tensor loc, torch::Tensor scale, torch::Tensor lo, torch::Tensor hi,
+                                                 torch::Tensor u, torch::Tensor gx) {
+  tn_check(loc, scale, lo, hi);
+  check_f32(u, "u");
+  check_f32(gx, "gx");
+  auto gl = torch::empty_like(loc), gs = torch::empty_like(loc);
+  launch_truncnorm_rsample_bwd(loc.data_ptr<float>(), scale.data_ptr<float>(), lo.data_ptr<float>(), (int)lo.numel(),
+                               hi.data_ptr<float>(), (int)hi.numel(), u.data_ptr<float>(), gx.data_ptr<float>(),
+                               gl.data_ptr<float>(), gs.data_ptr<float>(), (int)loc.numel(), cur_stream());
+  return {gl, gs};
+}
+
+torch::Tensor truncnorm_logprob_fwd(torch::Tensor v, torch::Tensor loc, torch::Tensor scale, torch::Tensor lo, torch::Tensor hi) {
+  tn_check(loc, scale, lo, hi);
+  check_f32(v, "value");
+  TORCH_CHECK(v.numel() % loc.numel() == 0, "truncnorm: value must be [sample..., *loc.shape]");
+  auto lp = torch::empty_like(v);
+  launch_truncnorm_logprob_fwd(v.data_ptr<float>(), loc.data_ptr<float>(), scale.data_ptr<float>(), lo.data_ptr<float>(),
+                               (int)lo.numel(), hi.data_ptr<float>(), (int)hi.numel(), lp.data_ptr<float>(), (int)v.numel(),
+                               (int)loc.numel(), cur_stream());
+  return lp;
+}
+
+std::vector<torch::Tensor> truncnorm_logprob_bwd(torch::Tensor v, torch::Tensor loc, torch::Tensor scale, torch::Tensor lo,
+                                                 torch::Tensor hi, torch::Tensor g) {
+  tn_check(loc, scale, lo, hi);
+  check_f32(v, "value");
+  check_f32(g, "grad");
+  auto gv = torch::empty_like(v), gl = torch::empty_like(v), gs = torch::empty_like(v);
+  launch_truncnorm_logprob_bwd(v.data_ptr<float>(), loc.data_ptr<float>(), scale.data_ptr<float>(), lo.data_ptr<float>(),
+                               (int)lo.numel(), hi.data_ptr<float>(), (int)hi.numel(), g.data_ptr<float>(), gv.data_ptr<float>(),
+                               gl.data_ptr<float>(), gs.data_ptr<float>(), (int)v.numel(), (int)loc.numel(), cur_stream());
+  return {gv, gl, gs};
+}
+
 std::vector<int64_t> scanp_info(int64_t B, int64_t S, int64_t D, int64_t H, int64_t hid, int64_t C) {
   // [supported, sync words, error word index, forward grid, backward grid]
   const int words = scanp_sync_words();
@@ -978,6 +1044,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scanp_fwd", &scanp_fwd);
   m.def("scanp_bwd", &scanp_bwd);
   m.def("scanp_info", &scanp_info);
+  m.def("truncnorm_rsample_fwd", &truncnorm_rsample_fwd);
+  m.def("truncnorm_rsample_bwd", &truncnorm_rsample_bwd);
+  m.def("truncnorm_logprob_fwd", &truncnorm_logprob_fwd);
+  m.def("truncnorm_logprob_bwd", &truncnorm_logprob_bwd);
   m.def("set_scanp_prof", &set_scanp_prof);
   m.def("set_scan4_prof", &set_scan4_prof);
 }

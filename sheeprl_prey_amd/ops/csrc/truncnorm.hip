@@ -1,0 +1,135 @@
+// Truncated normal N(loc, scale) restricted to [lo, hi]: inverse-CDF reparameterised sample and
+// log-density, forward and backward, one elementwise launch each (reference semantics:
+// sheeprl/utils/distribution.py:25-147 — Z = max(Phi(beta) - Phi(alpha), eps) with eps the float32
+// machine epsilon, the icdf argument Phi(alpha) + u Z is not clamped).
+//
+// With alpha = (lo - loc) / scale, beta = (hi - loc) / scale, xi = Phi(alpha) + u Z, s = Phi^-1(xi):
+//   sample  x = loc + scale s
+//   dx/dloc   = 1 - (dxi/dalpha + dxi/dbeta) / phi(s)
+//   dx/dscale = s - (alpha dxi/dalpha + beta dxi/dbeta) / phi(s)
+//   dxi/dalpha = (1-u) phi(alpha), dxi/dbeta = u phi(beta)   (Z clamped: phi(alpha), 0)
+//   log p(v) = -log(sqrt(2 pi)) - log Z - z^2 / 2 - log scale,  z = (v - loc) / scale
+//   dlogZ/dloc = (phi(alpha) - phi(beta)) / (Z scale), dlogZ/dscale = (alpha phi(alpha) - beta phi(beta)) / (Z scale)
+// Bounds are either one value per element or one scalar (n_lo / n_hi == 1); parameters broadcast over
+// leading sample dimensions (element i uses parameter i % np).
+#include "common.h"
+
+namespace srl {
+namespace tn {
+
+constexpr float INV_SQRT_2PI = 0.3989422804014327f;
+constexpr float INV_SQRT_2 = 0.7071067811865476f;
+constexpr float SQRT_2 = 1.4142135623730951f;
+constexpr float LOG_INV_SQRT_2PI = -0.9189385332046727f;
+constexpr float EPS = 1.1920928955078125e-07f;
+
+__device__ __forceinline__ float pdf(float x) { return isfinite(x) ? INV_SQRT_2PI * __expf(-0.5f * x * x) : 0.f; }
+__device__ __forceinline__ float cdf(float x) { return 0.5f * (1.f + erff(x * INV_SQRT_2)); }
+
+struct Trunc {
+  float alpha, beta, pa, pb, Z;
+  bool clamped;
+};
+
+__device__ __forceinline__ Trunc bounds(float loc, float scale, float lo, float hi) {
+  Trunc t;
+  t.alpha = (lo - loc) / scale;
+  t.beta = (hi - loc) / scale;
+  t.pa = pdf(t.alpha);
+  t.pb = pdf(t.beta);
+  const float z = cdf(t.beta) - cdf(t.alpha);
+  t.clamped = !(z > EPS);
+  t.Z = t.clamped ? EPS : z;
+  return t;
+}
+
+__global__ void rsample_fwd(const float* __restrict__ loc, const float* __restrict__ scale, const float* __restrict__ lo,
+                            int nlo, const float* __restrict__ hi, int nhi, const float* __restrict__ u, float* __restrict__ x,
+                            int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float l = loc[i], s = scale[i];
+    const Trunc t = bounds(l, s, lo[nlo == 1 ? 0 : i], hi[nhi == 1 ? 0 : i]);
+    const float xi = cdf(t.alpha) + u[i] * t.Z;
+    x[i] = l + s * (SQRT_2 * erfinvf(2.f * xi - 1.f));
+  }
+}
+
+__global__ void rsample_bwd(const float* __restrict__ loc, const float* __restrict__ scale, const float* __restrict__ lo,
+                            int nlo, const float* __restrict__ hi, int nhi, const float* __restrict__ u,
+                            const float* __restrict__ gx, float* __restrict__ gloc, float* __restrict__ gscale, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float l = loc[i], sc = scale[i], ui = u[i], g = gx[i];
+    const Trunc t = bounds(l, sc, lo[nlo == 1 ? 0 : i], hi[nhi == 1 ? 0 : i]);
+    const float xi = cdf(t.alpha) + ui * t.Z;
+    const float s = SQRT_2 * erfinvf(2.f * xi - 1.f);
+    const float da = t.clamped ? t.pa : (1.f - ui) * t.pa;
+    const float db = t.clamped ? 0.f : ui * t.pb;
+    const float inv = 1.f / (INV_SQRT_2PI * __expf(-0.5f * s * s));
+    const float wa = isfinite(t.alpha) ? t.alpha * da : 0.f, wb = isfinite(t.beta) ? t.beta * db : 0.f;
+    gloc[i] = g * (1.f - (da + db) * inv);
+    gscale[i] = g * (s - (wa + wb) * inv);
+  }
+}
+
+__global__ void logprob_fwd(const float* __restrict__ v, const float* __restrict__ loc, const float* __restrict__ scale,
+                            const float* __restrict__ lo, int nlo, const float* __restrict__ hi, int nhi, float* __restrict__ lp,
+                            int n, int np) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int k = i % np;
+    const float l = loc[k], s = scale[k];
+    const Trunc t = bounds(l, s, lo[nlo == 1 ? 0 : k], hi[nhi == 1 ? 0 : k]);
+    const float z = (v[i] - l) / s;
+    lp[i] = LOG_INV_SQRT_2PI - __logf(t.Z) - 0.5f * z * z - __logf(s);
+  }
+}
+
+// Per-element parameter gradients (summed over sample dimensions by the caller).
+__global__ void logprob_bwd(const float* __restrict__ v, const float* __restrict__ loc, const float* __restrict__ scale,
+                            const float* __restrict__ lo, int nlo, const float* __restrict__ hi, int nhi,
+                            const float* __restrict__ g, float* __restrict__ gv, float* __restrict__ gloc,
+                            float* __restrict__ gscale, int n, int np) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int k = i % np;
+    const float l = loc[k], s = scale[k], gi = g[i];
+    const Trunc t = bounds(l, s, lo[nlo == 1 ? 0 : k], hi[nhi == 1 ? 0 : k]);
+    const float z = (v[i] - l) / s;
+    float dzl = 0.f, dzs = 0.f;  // dlogZ / dloc, dlogZ / dscale
+    if (!t.clamped) {
+      const float wa = isfinite(t.alpha) ? t.alpha * t.pa : 0.f, wb = isfinite(t.beta) ? t.beta * t.pb : 0.f;
+      dzl = (t.pa - t.pb) / (t.Z * s);
+      dzs = (wa - wb) / (t.Z * s);
+    }
+    gv[i] = -gi * z / s;
+    gloc[i] = gi * (z / s - dzl);
+    gscale[i] = gi * ((z * z - 1.f) / s - dzs);
+  }
+}
+
+inline int grid_for(int n) { return std::max(1, std::min((n + 255) / 256, 2048)); }
+
+}  // namespace tn
+}  // namespace srl
+
+using namespace srl::tn;
+
+void launch_truncnorm_rsample_fwd(const float* loc, const float* scale, const float* lo, int nlo, const float* hi, int nhi,
+                                  const float* u, float* x, int n, hipStream_t st) {
+  hipLaunchKernelGGL(rsample_fwd, dim3(grid_for(n)), dim3(256), 0, st, loc, scale, lo, nlo, hi, nhi, u, x, n);
+}
+
+void launch_truncnorm_rsample_bwd(const float* loc, const float* scale, const float* lo, int nlo, const float* hi, int nhi,
+                                  const float* u, const float* gx, float* gloc, float* gscale, int n, hipStream_t st) {
+  hipLaunchKernelGGL(rsample_bwd, dim3(grid_for(n)), dim3(256), 0, st, loc, scale, lo, nlo, hi, nhi, u, gx, gloc, gscale, n);
+}
+
+void launch_truncnorm_logprob_fwd(const float* v, const float* loc, const float* scale, const float* lo, int nlo,
+                                  const float* hi, int nhi, float* lp, int n, int np, hipStream_t st) {
+  hipLaunchKernelGGL(logprob_fwd, dim3(grid_for(n)), dim3(256), 0, st, v, loc, scale, lo, nlo, hi, nhi, lp, n, np);
+}
+
+void launch_truncnorm_logprob_bwd(const float* v, const float* loc, const float* scale, const float* lo, int nlo,
+                                  const float* hi, int nhi, const float* g, float* gv, float* gloc, float* gscale, int n, int np,
+                                  hipStream_t st) {
+  hipLaunchKernelGGL(logprob_bwd, dim3(grid_for(n)), dim3(256), 0, st, v, loc, scale, lo, nlo, hi, nhi, g, gv, gloc, gscale, n,
+                     np);
+}

@@ -178,3 +178,31 @@ def squashed_gaussian(mean: Tensor, log_std: Tensor, eps: Tensor, scale: Tensor,
     logp = -0.5 * eps.pow(2) - ls - 0.5 * math.log(2 * math.pi)
     logp = logp - torch.log(scale * (1 - y.pow(2)) + 1e-6)
     return action, logp.sum(-1, keepdim=True)
+
+
+# ---------------------------------------------------------------- truncated normal (K16)
+_SQRT2 = math.sqrt(2.0)
+_LOG_INV_SQRT_2PI = -0.5 * math.log(2.0 * math.pi)
+
+
+def truncnorm_terms(loc: Tensor, scale: Tensor, lo: Tensor, hi: Tensor) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """Standardised bounds (alpha, beta), Phi(alpha) and the mass Z = max(Phi(beta) - Phi(alpha), eps)."""
+    alpha = (lo - loc) / scale
+    beta = (hi - loc) / scale
+    cdf_a = 0.5 * (1.0 + torch.erf(alpha / _SQRT2))
+    cdf_b = 0.5 * (1.0 + torch.erf(beta / _SQRT2))
+    Z = (cdf_b - cdf_a).clamp_min(torch.finfo(loc.dtype).eps)
+    return alpha, beta, cdf_a, Z
+
+
+def truncnorm_rsample(loc: Tensor, scale: Tensor, lo: Tensor, hi: Tensor, u: Tensor) -> Tensor:
+    """Inverse-CDF sample loc + scale * Phi^-1(Phi(alpha) + u Z) (reference distribution.py:97-112, 139-140)."""
+    _, _, cdf_a, Z = truncnorm_terms(loc, scale, lo, hi)
+    return loc + scale * (_SQRT2 * torch.erfinv(2.0 * (cdf_a + u * Z) - 1.0))
+
+
+def truncnorm_log_prob(value: Tensor, loc: Tensor, scale: Tensor, lo: Tensor, hi: Tensor) -> Tensor:
+    """-log sqrt(2 pi) - log Z - z^2 / 2 - log scale (reference distribution.py:102-105, 142-143)."""
+    _, _, _, Z = truncnorm_terms(loc, scale, lo, hi)
+    z = (value - loc) / scale
+    return _LOG_INV_SQRT_2PI - Z.log() - 0.5 * z * z - scale.log()

@@ -32,13 +32,30 @@ from torch import Tensor
 # "16-mixed" needs a loss scaler the flat-slab optimisers do not implement; "64-true" would need every
 # buffer and env tensor in fp64: both are rejected up front rather than silently run in fp32.
 _PRECISIONS = {"32-true": None, "32": None, "bf16-mixed": torch.bfloat16}
+# Lightning Fabric's spellings of the same two modes (``fabric.precision=bf16`` / ``32`` in the reference)
+_PRECISION_ALIASES = {"bf16": "bf16-mixed", "32-true": "32-true", "32": "32-true"}
 
 
 def _autocast_dtype(precision: Any) -> Optional[torch.dtype]:
-    key = str(precision)
+    key = str(precision).strip().lower()
+    key = _PRECISION_ALIASES.get(key, key)
     if key not in _PRECISIONS:
-        raise ValueError(f"fabric.precision={precision!r} is not supported; use one of {sorted(_PRECISIONS)}")
+        raise ValueError(f"fabric.precision={precision!r} is not supported; use one of "
+                         f"{sorted(set(_PRECISIONS) | set(_PRECISION_ALIASES))} (16-mixed needs a loss scaler, "
+                         "bf16-true / 64-true a non-fp32 parameter store: neither is implemented)")
     return _PRECISIONS[key]
+
+
+def _autocast_targets(module: nn.Module) -> List[nn.Module]:
+    """The modules whose ``forward`` the algorithms actually call.  A container without a forward of its
+    own (DreamerV3's ``WorldModel`` and ``RSSM``, SAC's agent) is never called itself: its children are
+    (the reference sets each of them up separately, ``dreamer_v3/agent.py:1054-1063``)."""
+    if type(module).forward is not nn.Module.forward:
+        return [module]
+    out: List[nn.Module] = []
+    for child in module.children():
+        out += _autocast_targets(child)
+    return out
 
 
 def _to_fp32(out: Any) -> Any:
@@ -292,8 +309,13 @@ class Runner:
         if self._amp_dtype is not None:
             if self._amp_hooks is None:
                 self._amp_hooks = _AutocastHooks(self.device.type, self._amp_dtype)
-            module.register_forward_pre_hook(self._amp_hooks.pre)
-            module.register_forward_hook(self._amp_hooks.post, always_call=True)
+            for m in _autocast_targets(module):
+                m.register_forward_pre_hook(self._amp_hooks.pre)
+                m.register_forward_hook(self._amp_hooks.post, always_call=True)
+            # fp32-only fast paths that read weights without calling forwards (fused RSSM scan,
+            # buffer-resident imagination, fused PPO rollout/update) check this flag and step aside
+            for m in module.modules():
+                m._srl_autocast = True
         if self.world_size > 1:
             with torch.no_grad():
                 tensors = [p.data for p in module.parameters()] + [b for b in module.buffers()]

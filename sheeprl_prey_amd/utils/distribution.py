@@ -19,133 +19,129 @@ from torch.distributions.utils import broadcast_all
 from sheeprl_prey_amd import ops
 from sheeprl_prey_amd.utils.utils import symexp, symlog
 
-CONST_SQRT_2 = math.sqrt(2)
-CONST_INV_SQRT_2PI = 1 / math.sqrt(2 * math.pi)
-CONST_INV_SQRT_2 = 1 / math.sqrt(2)
-CONST_LOG_INV_SQRT_2PI = math.log(CONST_INV_SQRT_2PI)
-CONST_LOG_SQRT_2PI_E = 0.5 * math.log(2 * math.pi * math.e)
+_LOG_SQRT_2PI_E = 0.5 * math.log(2.0 * math.pi * math.e)
+_INV_SQRT_2PI = 1.0 / math.sqrt(2.0 * math.pi)
 
 
-class TruncatedStandardNormal(Distribution):
-    """Standard normal truncated to [a, b]; rsample by inverse CDF (erfinv)."""
+def _std_pdf(x: Tensor) -> Tensor:
+    return torch.exp(-0.5 * x * x) * _INV_SQRT_2PI
 
-    arg_constraints = {"a": constraints.real, "b": constraints.real}
+
+def _finite_times(x: Tensor, y: Tensor) -> Tensor:
+    """x * y with the x = +-inf, y = 0 products of unbounded tails taken as 0."""
+    return torch.where(torch.isfinite(x), x * y, torch.zeros_like(y))
+
+
+class TruncatedNormal(Distribution):
+    """Normal(loc, scale) restricted to [low, high] (reference ``distribution.py:97-147``).
+
+    Sampling is by inverse CDF: ``loc + scale * Phi^-1(Phi(alpha) + u Z)`` with ``u ~ U(eps, 1-eps)``,
+    ``alpha = (low - loc) / scale``, ``Z = max(Phi(beta) - Phi(alpha), eps)`` (float32 eps), exactly the
+    reference's semantics: the icdf argument is not clamped and samples are not clipped to the bounds.
+    On the GPU ``rsample`` and ``log_prob`` are single fused HIP launches forward and backward
+    (``csrc/truncnorm.hip``); moments, entropy and cdf are closed forms in eager torch.  Unlike the
+    reference, the ``low < high`` check runs only with ``validate_args`` (it is a host sync)."""
+
+    arg_constraints = {"loc": constraints.real, "scale": constraints.positive}
     has_rsample = True
-    eps = 1e-6
 
-    def __init__(self, a, b, validate_args=None):
-        self.a, self.b = broadcast_all(a, b)
-        batch_shape = torch.Size() if isinstance(a, Number) and isinstance(b, Number) else self.a.size()
+    def __init__(self, loc, scale, low, high, validate_args=None):
+        # the un-broadcast bounds go to the kernels (scalar bounds stay scalars)
+        self._low_arg = low if isinstance(low, Tensor) else torch.as_tensor(float(low))
+        self._high_arg = high if isinstance(high, Tensor) else torch.as_tensor(float(high))
+        self.loc, self.scale, self.low, self.high = broadcast_all(loc, scale, low, high)
+        batch_shape = torch.Size() if all(isinstance(v, Number) for v in (loc, scale, low, high)) else self.loc.size()
         super().__init__(batch_shape, validate_args=validate_args)
-        if self.a.dtype != self.b.dtype:
+        if self.low.dtype != self.high.dtype:
             raise ValueError("Truncation bounds types are different")
-        if any((self.a >= self.b).view(-1).tolist()) if validate_args else False:
+        if validate_args and bool((self.low >= self.high).any()):
             raise ValueError("Incorrect truncation range")
-        eps = torch.finfo(self.a.dtype).eps
-        self._dtype_min_gt_0 = eps
-        self._dtype_max_lt_1 = 1 - eps
-        self._little_phi_a = self._little_phi(self.a)
-        self._little_phi_b = self._little_phi(self.b)
-        self._big_phi_a = self._big_phi(self.a)
-        self._big_phi_b = self._big_phi(self.b)
-        self._Z = (self._big_phi_b - self._big_phi_a).clamp(eps, 1 - eps)
-        self._log_Z = self._Z.log()
-        little_phi_coeff_a = torch.nan_to_num(self.a, nan=math.nan)
-        little_phi_coeff_b = torch.nan_to_num(self.b, nan=math.nan)
-        self._lpbb_m_lpaa_d_Z = (self._little_phi_b * little_phi_coeff_b - self._little_phi_a * little_phi_coeff_a) / self._Z
-        self._mean = -(self._little_phi_b - self._little_phi_a) / self._Z
-        self._variance = 1 - self._lpbb_m_lpaa_d_Z - ((self._little_phi_b - self._little_phi_a) / self._Z) ** 2
-        self._entropy = CONST_LOG_SQRT_2PI_E + self._log_Z - 0.5 * self._lpbb_m_lpaa_d_Z
+        self._alpha = (self.low - self.loc) / self.scale
+        self._beta = (self.high - self.loc) / self.scale
+
+    # ---- standardised quantities
+    @property
+    def a(self) -> Tensor:
+        return self._alpha
+
+    @property
+    def b(self) -> Tensor:
+        return self._beta
+
+    def _mass(self) -> Tensor:
+        eps = torch.finfo(self.loc.dtype).eps
+        return (self._phi_cdf(self._beta) - self._phi_cdf(self._alpha)).clamp_min(eps)
+
+    @staticmethod
+    def _phi_cdf(x: Tensor) -> Tensor:
+        return 0.5 * (1.0 + torch.erf(x / math.sqrt(2.0)))
+
+    @property
+    def auc(self) -> Tensor:
+        return self._mass()
 
     @constraints.dependent_property
     def support(self):
-        return constraints.interval(self.a, self.b)
+        return constraints.interval(self.low, self.high)
+
+    # ---- moments / entropy (closed forms of the truncated normal)
+    @property
+    def mean(self) -> Tensor:
+        return self.loc + self.scale * (_std_pdf(self._alpha) - _std_pdf(self._beta)) / self._mass()
 
     @property
-    def mean(self):
-        return self._mean
+    def variance(self) -> Tensor:
+        Z = self._mass()
+        pa, pb = _std_pdf(self._alpha), _std_pdf(self._beta)
+        tail = (_finite_times(self._alpha, pa) - _finite_times(self._beta, pb)) / Z
+        return self.scale**2 * (1.0 + tail - ((pa - pb) / Z) ** 2)
 
-    @property
-    def variance(self):
-        return self._variance
+    def entropy(self) -> Tensor:
+        Z = self._mass()
+        tail = (_finite_times(self._beta, _std_pdf(self._beta)) - _finite_times(self._alpha, _std_pdf(self._alpha))) / Z
+        return _LOG_SQRT_2PI_E + Z.log() - 0.5 * tail + self.scale.log()
 
-    def entropy(self):
-        return self._entropy
-
-    @property
-    def auc(self):
-        return self._Z
-
-    @staticmethod
-    def _little_phi(x):
-        return (-(x**2) * 0.5).exp() * CONST_INV_SQRT_2PI
-
-    @staticmethod
-    def _big_phi(x):
-        phi = 0.5 * (1 + (x * CONST_INV_SQRT_2).erf())
-        return phi.clamp(TruncatedStandardNormal.eps, 1 - TruncatedStandardNormal.eps)
-
-    @staticmethod
-    def _inv_big_phi(x):
-        return CONST_SQRT_2 * (2 * x - 1).erfinv()
-
-    def cdf(self, value):
+    # ---- cdf / icdf / densities / samples
+    def cdf(self, value: Tensor) -> Tensor:
         if self._validate_args:
             self._validate_sample(value)
-        return ((self._big_phi(value) - self._big_phi_a) / self._Z).clamp(0, 1)
+        z = (value - self.loc) / self.scale
+        return ((self._phi_cdf(z) - self._phi_cdf(self._alpha)) / self._mass()).clamp(0, 1)
 
-    def icdf(self, value):
-        y = self._big_phi_a + value * self._Z
-        y = y.clamp(self.eps, 1 - self.eps)
-        return self._inv_big_phi(y)
+    def icdf(self, value: Tensor) -> Tensor:
+        return self.loc + self.scale * (math.sqrt(2.0) * torch.erfinv(2.0 * (self._phi_cdf(self._alpha) + value * self._mass()) - 1.0))
 
-    def log_prob(self, value):
+    def log_prob(self, value: Tensor) -> Tensor:
         if self._validate_args:
             self._validate_sample(value)
-        return CONST_LOG_INV_SQRT_2PI - self._log_Z - (value**2) * 0.5
+        lo, hi = self._bounds_for(value.device)
+        return ops.truncnorm_log_prob(value, self.loc, self.scale, lo, hi)
 
-    def rsample(self, sample_shape=torch.Size()):
+    def rsample(self, sample_shape=torch.Size()) -> Tensor:
         shape = self._extended_shape(sample_shape)
-        p = torch.empty(shape, device=self.a.device).uniform_(self._dtype_min_gt_0, self._dtype_max_lt_1)
-        return self.icdf(p)
+        eps = torch.finfo(self.loc.dtype).eps
+        u = torch.empty(shape, device=self.loc.device, dtype=self.loc.dtype).uniform_(eps, 1.0 - eps)
+        loc, scale = self.loc.expand(shape), self.scale.expand(shape)
+        lo, hi = self._bounds_for(self.loc.device)
+        if lo.numel() != 1:
+            lo, hi = self.low.expand(shape), self.high.expand(shape)
+        return ops.truncnorm_rsample(loc, scale, lo, hi, u)
+
+    def _bounds_for(self, device) -> tuple:
+        lo, hi = self._low_arg, self._high_arg
+        if lo.numel() == 1 and hi.numel() == 1:
+            return lo.to(device=device, dtype=self.loc.dtype), hi.to(device=device, dtype=self.loc.dtype)
+        return self.low, self.high
 
 
-class TruncatedNormal(TruncatedStandardNormal):
-    """Normal(loc, scale) truncated to [a, b] (reference ``distribution.py:97-147``)."""
+class TruncatedStandardNormal(TruncatedNormal):
+    """Standard normal truncated to [a, b] (reference ``distribution.py:25-94``)."""
 
-    has_rsample = True
-
-    def __init__(self, loc, scale, a, b, validate_args=None):
-        self.loc, self.scale, a, b = broadcast_all(loc, scale, a, b)
-        self._non_std_a = a
-        self._non_std_b = b
-        a = (a - self.loc) / self.scale
-        b = (b - self.loc) / self.scale
-        super().__init__(a, b, validate_args=validate_args)
-        self._log_scale = self.scale.log()
-        self._mean = self._mean * self.scale + self.loc
-        self._variance = self._variance * self.scale**2
-        self._entropy = self._entropy + self._log_scale
-
-    def _to_std_rv(self, value):
-        return (value - self.loc) / self.scale
-
-    def _from_std_rv(self, value):
-        return value * self.scale + self.loc
-
-    def cdf(self, value):
-        return super().cdf(self._to_std_rv(value))
-
-    def icdf(self, value):
-        sample = self._from_std_rv(super().icdf(value))
-        clipped = torch.max(torch.min(sample, self._non_std_b), self._non_std_a)
-        return sample + (clipped - sample).detach()
-
-    def log_prob(self, value):
-        value = self._to_std_rv(value)
-        if self._validate_args:
-            self._validate_sample(value)
-        return super().log_prob(value) - self._log_scale
+    def __init__(self, a, b, validate_args=None):
+        a_t = a if isinstance(a, Tensor) else torch.as_tensor(float(a))
+        super().__init__(torch.zeros_like(a_t, dtype=torch.get_default_dtype() if not a_t.is_floating_point() else a_t.dtype),
+                         torch.ones_like(a_t, dtype=torch.get_default_dtype() if not a_t.is_floating_point() else a_t.dtype),
+                         a, b, validate_args=validate_args)
 
 
 class SymlogDistribution:

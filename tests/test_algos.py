@@ -5,6 +5,8 @@ checkpoint key set and the saved ``.hydra/config.yaml``.  ``devices=2`` runs two
 """
 from __future__ import annotations
 
+import collections
+import contextlib
 import os
 from pathlib import Path
 from unittest import mock
@@ -114,11 +116,47 @@ TINY_DREAMER = [
 
 @pytest.mark.timeout(240)
 @pytest.mark.parametrize("devices", [1, 2])
-@pytest.mark.parametrize("env_id", ["discrete_dummy", "continuous_dummy"])
+@pytest.mark.parametrize("env_id", ["discrete_dummy", "multidiscrete_dummy", "continuous_dummy"])
 def test_dreamer_v3(devices, env_id):
     _run(STD + ["exp=dreamer_v3", "env=dummy", f"env.id={env_id}", f"buffer.size={devices}", "root_dir=dv3",
                 f"run_name={env_id}{devices}", "buffer.checkpoint=True"] + TINY_DREAMER, devices)
     _check_ckpt("dv3", f"{env_id}{devices}", DV3_KEYS, True)
+
+
+@pytest.mark.timeout(300)
+def test_resume_dreamer_v3_two_cli_runs():
+    """Checkpoint -> resume through two separate ``python sheeprl.py`` processes (reference
+    ``tests/test_algos/test_cli.py:39-79``): the second run restores world model, actor, critics,
+    optimisers, Moments and the replay buffer, then keeps training and checkpoints again."""
+    import subprocess
+    import sys
+
+    repo = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, LT_ACCELERATOR="cpu", LT_DEVICES="1",
+               PYTHONPATH=os.pathsep.join([str(repo), os.environ.get("PYTHONPATH", "")]))
+    tiny = [a for a in TINY_DREAMER if not a.startswith("per_rank_sequence_length")]
+    first = [sys.executable, str(repo / "sheeprl.py"), "exp=dreamer_v3", "env=dummy", "dry_run=True", "env.capture_video=False",
+             "buffer.size=10", "buffer.checkpoint=True", "per_rank_sequence_length=1", "root_dir=dv3_ckpt",
+             "run_name=a"] + tiny
+    subprocess.run(first, check=True, env=env, timeout=240)
+    ck = sorted(Path("logs", "runs", "dv3_ckpt", "a").rglob("*.ckpt"))[-1]
+    saved = torch.load(ck, map_location="cpu", weights_only=True)
+    assert set(saved) == DV3_KEYS | {"rb"}
+    second = [sys.executable, str(repo / "sheeprl.py"), "exp=dreamer_v3", f"checkpoint.resume_from={ck}", "root_dir=dv3_resume",
+              "run_name=b"]
+    subprocess.run(second, check=True, env=env, timeout=240)
+    resumed = sorted(Path("logs", "runs", "dv3_resume", "b").rglob("*.ckpt"))
+    assert resumed, "the resumed run wrote no checkpoint"
+    state = torch.load(resumed[-1], map_location="cpu", weights_only=True)
+    assert set(state) == DV3_KEYS | {"rb"}
+    assert state["update"] >= saved["update"]
+
+
+def test_sac_default_env_needs_box2d_message():
+    """``exp=sac`` defaults to LunarLanderContinuous-v2 (reference ``configs/exp/sac.yaml:15``); Box2D is not
+    in the image, so the run must stop with an actionable message instead of an unknown-id error."""
+    with pytest.raises(ModuleNotFoundError, match="Box2D"):
+        _run(STD + ["exp=sac"], 1)
 
 
 def test_fsdp_rejected():
@@ -272,16 +310,50 @@ def test_p2e_explores_then_switches(algo, env_id):
             "Loss/policy_loss_task", "Rewards/intrinsic"} <= keys, keys
 
 
+@contextlib.contextmanager
+def record_autocast():
+    """Counts, per module class, the forwards that actually ran inside an enabled autocast region."""
+    from sheeprl_prey_amd.parallel import runner as R
+
+    seen = collections.Counter()
+    orig = R._AutocastHooks.pre
+
+    def pre(self, module, args):
+        orig(self, module, args)
+        if torch.is_autocast_enabled(self.device_type):
+            seen[type(module).__name__] += 1
+
+    with mock.patch.object(R._AutocastHooks, "pre", pre):
+        yield seen
+
+
 @pytest.mark.parametrize("algo", ["ppo", "sac"])
 def test_bf16_mixed_precision(algo):
-    """``fabric.precision=bf16-mixed`` (Fabric's mixed-precision plugin in the reference): set-up
-    modules run their forward under autocast and the run trains and checkpoints as usual."""
+    """``fabric.precision=bf16-mixed`` (Fabric's mixed-precision plugin in the reference): the forwards the
+    algorithm calls run under autocast (for SAC the actor and the critics, children of an agent that has
+    no forward of its own) and the run trains and checkpoints as usual."""
     env = ["env=dummy", "env.id=discrete_dummy"] if algo == "ppo" else ["env.id=Pendulum-v1", "algo.learning_starts=0",
                                                                        "buffer.size=1", "algo.hidden_size=8"]
     extra = ["algo.rollout_steps=1"] if algo == "ppo" else ["algo.per_rank_gradient_steps=1"]
-    _run(STD + [f"exp={algo}", "fabric.precision=bf16-mixed", "per_rank_batch_size=1", f"root_dir={algo}_bf16",
-                "run_name=r"] + env + extra, 1)
+    with record_autocast() as seen:
+        _run(STD + [f"exp={algo}", "fabric.precision=bf16-mixed", "per_rank_batch_size=1", f"root_dir={algo}_bf16",
+                    "run_name=r"] + env + extra, 1)
     _check_ckpt(f"{algo}_bf16", "r", PPO_KEYS if algo == "ppo" else SAC_KEYS, False)
+    want = {"PPOAgent"} if algo == "ppo" else {"SACActor", "SACCriticEnsemble"}
+    assert want <= set(seen), f"forwards run under autocast: {dict(seen)}"
+
+
+@pytest.mark.parametrize("alias,ok", [("bf16", True), ("32", True), ("32-true", True), ("16-mixed", False),
+                                      ("64-true", False), ("bf16-true", False)])
+def test_precision_aliases(alias, ok):
+    from sheeprl_prey_amd.parallel.runner import _autocast_dtype
+
+    if ok:
+        assert _autocast_dtype(alias) in (None, torch.bfloat16)
+        assert (_autocast_dtype(alias) is torch.bfloat16) == alias.startswith("bf16")
+    else:
+        with pytest.raises(ValueError, match="precision"):
+            _autocast_dtype(alias)
 
 
 def test_unsupported_precision_rejected():

@@ -128,11 +128,17 @@ def test_dreamer_v3_continuous_graph_capture():
 def test_bf16_mixed_gpu(algo):
     """``fabric.precision=bf16-mixed`` on the GPU: autocast forwards (fused fp32 kernels step aside),
     hipGraph capture of the train step, checkpoint written."""
-    if algo == "ppo":
-        _run(STD + ["exp=ppo", "env=dummy", "env.id=discrete_dummy", "algo.rollout_steps=4", "per_rank_batch_size=2",
-                    "fabric.precision=bf16-mixed", "root_dir=ppo_bf16", "run_name=g"])
-        _check_ckpt("ppo_bf16", "g", PPO_KEYS, False)
-    else:
-        _run(STD + ["exp=dreamer_v3", "env=dummy", "env.id=discrete_dummy", "buffer.size=4", "root_dir=dv3_bf16",
-                    "run_name=g", "fabric.precision=bf16-mixed"] + TINY_DREAMER)
-        _check_ckpt("dv3_bf16", "g", DV3_KEYS, False)
+    from tests.test_algos import record_autocast
+
+    with record_autocast() as seen:
+        if algo == "ppo":
+            _run(STD + ["exp=ppo", "env=dummy", "env.id=discrete_dummy", "algo.rollout_steps=4", "per_rank_batch_size=2",
+                        "fabric.precision=bf16-mixed", "root_dir=ppo_bf16", "run_name=g"])
+            _check_ckpt("ppo_bf16", "g", PPO_KEYS, False)
+        else:
+            _run(STD + ["exp=dreamer_v3", "env=dummy", "env.id=discrete_dummy", "buffer.size=4", "root_dir=dv3_bf16",
+                        "run_name=g", "fabric.precision=bf16-mixed"] + TINY_DREAMER)
+            _check_ckpt("dv3_bf16", "g", DV3_KEYS, False)
+    # every sub-model the step calls ran its forward under autocast (the world model has no forward of its own)
+    want = {"PPOAgent"} if algo == "ppo" else {"MultiEncoder", "RecurrentModel", "MLP", "MultiDecoder", "Actor"}
+    assert want <= set(seen), f"forwards run under autocast: {dict(seen)}"
