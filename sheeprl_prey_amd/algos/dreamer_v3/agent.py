@@ -14,6 +14,8 @@ hot paths are re-shaped for MI355X:
 """
 from __future__ import annotations
 
+import os
+
 import copy
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -289,6 +291,18 @@ class RSSM(nn.Module):
         M, S = post.shape
         Hd = h.shape[1]
         A = int(sum(actor.actions_dim))
+        disc = self.discrete
+        nh, G = len(actor.actions_dim), S // disc
+        # every uniform of the rollout in one launch: per step nh x M for the actions, G x M for the prior
+        U = torch.rand(horizon + 1, M * (nh + G), device=post.device)
+        # persistent one-launch rollout (imagine.hip): opt-in, it measures 2.27 ms vs 1.85 ms for the
+        # in-graph per-op rollout at the Atari-100k shapes (profiles/r2_imagine_persistent.md)
+        if getattr(self, "fused_imagine", os.environ.get("SRL_IMAGINE_IMPL", "ops") == "persist"):
+            from sheeprl_prey_amd.ops.imagine import fused_imagine
+
+            full = fused_imagine(self, actor, post, h, horizon, U)  # one persistent launch (imagine.hip)
+            if full is not None:
+                return full[:, :, A:], full[:, :, :A]
         buf = post.new_empty(horizon + 1, M, A + S + Hd)
         buf[0, :, A:A + S].copy_(post)
         buf[0, :, A + S:].copy_(h)
@@ -300,10 +314,6 @@ class RSSM(nn.Module):
         Wg = gru.linear.weight  # columns: (h | feat)
         WgT_h, WgT_f = Wg[:, :Hd].t(), Wg[:, Hd:].t()
         ln = gru.layer_norm
-        disc = self.discrete
-        nh, G = len(actor.actions_dim), S // disc
-        # every uniform of the rollout in one launch: per step nh x M for the actions, G x M for the prior
-        U = torch.rand(horizon + 1, M * (nh + G), device=post.device)
         for t in range(horizon + 1):
             out = actor.model(buf[t, :, A:])
             c0 = 0

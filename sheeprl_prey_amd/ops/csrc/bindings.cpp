@@ -994,9 +994,11 @@ void ppo_mlp_train(std::vector<std::vector<int64_t>> layers, std::vector<int64_t
 }
 
 void register_conv(pybind11::module& m);
+void register_ext(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_conv(m);
+  register_ext(m);
   m.def("ln_gru_into", &ln_gru_into);
   m.def("colsum", &colsum);
   m.def("cartpole_step", &cartpole_step);
