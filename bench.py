@@ -445,7 +445,7 @@ def bench_ppo(args):
     optimizer = build_optimizer(cfg.algo.optimizer, agent.parameters())
     player = PPOPlayer(agent, cfg, is_continuous, enabled=runner.cuda_graphs)
     T = cfg.algo.rollout_steps
-    trainer = PPOTrainer(runner, agent, optimizer, cfg, T * ne)
+    trainer = PPOTrainer(runner, agent, optimizer, cfg, T * ne, force_segmented=args.segmented)
     # rollout staging: env-side arrays stay on the host (one H2D per rollout), policy outputs are
     # copied into device rollout tensors; the obs for the next policy step goes H2D from pinned memory
     o = envs.reset(seed=cfg.seed + rank)[0]
@@ -530,6 +530,13 @@ def bench_ppo(args):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    spread = 0.0  # data-parallel consistency: every rank must hold the same weights
+    if world > 1:
+        cs = optimizer.flat_param.double().sum().reshape(1)
+        lo, hi = cs.clone(), cs.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        spread = float((hi - lo).abs().max().item())
     policy_steps = args.steps * cfg.algo.rollout_steps * ne * world
     if rank == 0:
         rec = {
@@ -549,9 +556,10 @@ def bench_ppo(args):
             "config": {"model": "PPO MLP 2x64 tanh (exp=ppo)", "global_batch": cfg.per_rank_batch_size * world,
                        "rollout_steps": cfg.algo.rollout_steps, "num_envs_per_rank": ne,
                        "update_epochs": cfg.algo.update_epochs, "parallelism": f"dp{world}",
-                       "hipgraph": bool(trainer.graphed.enabled), "device_env": bool(args.device_env),
+                       "hipgraph": trainer.mode != "eager", "update_mode": trainer.mode, "device_env": bool(args.device_env),
                        "rollout": type(drollout).__name__ if args.device_env else "host"},
             "mean_episode_return": round(float(np.mean(returns_seen[-20:])), 2) if returns_seen else None,
+            "dp_param_spread": spread,
         }
         print(json.dumps(rec), flush=True)
     envs.close()

@@ -71,9 +71,10 @@ class DreamerV3Trainer:
     all-gather(lambda) | ``actor`` (Moments, actor fwd/bwd) | all-reduce(actor grads) | ``critic`` (actor
     step, critic fwd/bwd) | all-reduce(critic grads) | ``final`` (critic step).
 
-    Execution: one hipGraph for the whole step on a single rank; on N ranks (discrete actions) one
-    hipGraph per phase with the RCCL collectives issued eagerly between replays (collectives stay
-    out of captured graphs); otherwise eager."""
+    Execution: one hipGraph for the whole step on a single rank; on N ranks one hipGraph per phase
+    with the RCCL collectives issued eagerly between replays (collectives stay out of captured
+    graphs; for continuous actors the actor phase's backward runs through the imagination graph the
+    previous capture recorded - both captures share one memory pool); otherwise eager."""
 
     PHASES = ("wm", "imagine", "actor", "critic", "final")
 
@@ -91,7 +92,7 @@ class DreamerV3Trainer:
         self._gather_buf = None
         ws = runner.world_size
         graphs = bool(runner.cuda_graphs)
-        self.segmented = graphs and (force_segmented or (ws > 1 and not is_continuous))
+        self.segmented = graphs and (force_segmented or ws > 1)
         single = graphs and ws == 1 and not self.segmented
         self.graphed = GraphedStep(self._full_step, warmup=2, enabled=single, name="dreamer_v3_train")
         if self.segmented:

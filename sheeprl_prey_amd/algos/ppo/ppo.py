@@ -157,14 +157,114 @@ class FusedPPOTrainer:
                 aggregator.update(k, self.out[i].clone())
 
 
-class PPOTrainer:
-    """All ``update_epochs`` x minibatch steps of one PPO update as ONE hipGraph (single rank, GPU,
-    ``fabric.cuda_graphs``): permutations are drawn on device (``argsort`` of uniform keys), the
-    clip / entropy coefficients are device scalars refreshed before each replay (annealing works),
-    the loss means come back as graph outputs.  Multi-rank or ``anneal_lr`` runs use ``train``
-    (per-minibatch RCCL all-reduce; the flat Adam takes its lr as a launch argument)."""
+class SegmentedPPOUpdate:
+    """The update as hipGraph replays with the gradient all-reduce between them (N ranks, GPU,
+    ``fabric.cuda_graphs``): per minibatch ``fwd+bwd`` graph -> RCCL all-reduce of the flat gradient
+    slab (eager, the reference's DDP averaging, ``ppo.py:41-52``) -> ``clip + Adam`` graph.  The
+    minibatch rows come from a static index buffer refreshed by one device copy per minibatch, so
+    one forward/backward graph serves every minibatch of a size (a ragged tail gets its own)."""
 
-    def __init__(self, runner, agent, optimizer, cfg, n: int):
+    def __init__(self, trainer: "PPOTrainer", warmup: int = 2):
+        self.tr = trainer
+        self.warmup = warmup
+        self.calls = 0
+        self.static = None
+        self.g_fb: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.g_opt = None
+        self.pool = None
+        dev = trainer.runner.device
+        self.sums = torch.zeros(3, device=dev)
+        self.idx_cur = torch.zeros(max(1, int(trainer.cfg.per_rank_batch_size)), dtype=torch.long, device=dev)
+
+    def _fb(self, m: int) -> None:
+        tr, cfg = self.tr, self.tr.cfg
+        sel = self.idx_cur[:m]
+        batch = {k: v.index_select(0, sel) for k, v in self.static.items()}
+        obs = {k: batch[k] / 255 - 0.5 if k in cfg.cnn_keys.encoder else batch[k] for k in tr.obs_keys}
+        _, logprobs, entropy, new_values = tr.agent(obs, torch.split(batch["actions"], tr.agent.actions_dim, dim=-1))
+        adv = batch["advantages"]
+        if cfg.algo.normalize_advantages:
+            adv = normalize_tensor(adv)
+        pg = policy_loss(logprobs, batch["logprobs"], adv, tr.clip_t, cfg.algo.loss_reduction)
+        vl = value_loss(new_values, batch["values"], batch["returns"], tr.clip_t, cfg.algo.clip_vloss, cfg.algo.loss_reduction)
+        el = entropy_loss(entropy, cfg.algo.loss_reduction)
+        loss = pg + cfg.algo.vf_coef * vl + tr.ent_t * el
+        tr.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        tr.optimizer._gather()  # the grads reach the flat slab inside this graph, before the all-reduce
+        self.sums.add_(torch.stack((pg.detach(), vl.detach(), el.detach())))
+
+    def _opt(self) -> None:
+        tr, cfg = self.tr, self.tr.cfg
+        if cfg.algo.max_grad_norm > 0.0:
+            tr.runner.clip_gradients(tr.agent, tr.optimizer, max_norm=cfg.algo.max_grad_norm)
+        tr.optimizer.step()
+
+    def _run(self, key, fn) -> None:
+        """Eager on a side stream while warming up, then capture once and replay."""
+        graphs = self.g_fb if key != "opt" else None
+        g = graphs.get(key) if graphs is not None else self.g_opt
+        if g is not None:
+            g.replay()
+            return
+        if self.calls < self.warmup:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                fn()
+            torch.cuda.current_stream().wait_stream(s)
+            return
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, pool=self.pool):
+            fn()
+        self.pool = g.pool()
+        if graphs is not None:
+            graphs[key] = g
+        else:
+            self.g_opt = g
+        g.replay()  # capture recorded without running
+
+    def __call__(self, data: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        tr, cfg = self.tr, self.tr.cfg
+        n, bs = tr.n, int(cfg.per_rank_batch_size)
+        if self.static is None:
+            self.static = {k: v.detach().clone() for k, v in data.items()}
+        for k, v in data.items():
+            self.static[k].copy_(v, non_blocking=True)
+        dev = self.sums.device
+        self.sums.zero_()
+        steps = 0
+        share = bool(cfg.buffer.share_data) and tr.runner.world_size > 1
+        for epoch in range(cfg.algo.update_epochs):
+            if share:  # DistributedSampler semantics over the gathered rollout (reference ppo.py:41-52)
+                perm = shard_indices(n, tr.runner, True, cfg.seed, epoch).to(dev, non_blocking=True)
+            else:
+                perm = torch.argsort(torch.rand(n, device=dev))
+            for start in range(0, perm.numel(), bs):
+                m = min(bs, perm.numel() - start)
+                self.idx_cur[:m].copy_(perm[start:start + m])
+                self._run(m, lambda m=m: self._fb(m))
+                tr.runner.sync_gradients(tr.optimizer)
+                self._run("opt", self._opt)
+                steps += 1
+        self.calls += 1
+        out = self.sums / max(1, steps)
+        return {"Loss/policy_loss": out[0], "Loss/value_loss": out[1], "Loss/entropy_loss": out[2]}
+
+
+class PPOTrainer:
+    """All ``update_epochs`` x minibatch steps of one PPO update:
+
+    * one rank, GPU, ``fabric.cuda_graphs``: the fused one-launch kernel when the agent fits it
+      (``FusedPPOTrainer``), else ONE hipGraph for the whole update - permutations drawn on device
+      (``argsort`` of uniform keys), clip / entropy coefficients as device scalars refreshed before
+      each replay (annealing works), the loss means as graph outputs;
+    * N ranks (or ``force_segmented``): ``SegmentedPPOUpdate`` - graph replays with the per-minibatch
+      RCCL all-reduce between them;
+    * ``anneal_lr`` (the flat Adam takes its lr as a launch argument) or CPU: eager ``train``."""
+
+    def __init__(self, runner, agent, optimizer, cfg, n: int, force_segmented: bool = False):
         from sheeprl_prey_amd.parallel.graphs import GraphedStep
 
         self.runner, self.agent, self.optimizer, self.cfg, self.n = runner, agent, optimizer, cfg, n
@@ -172,13 +272,22 @@ class PPOTrainer:
         self.obs_keys = list(cfg.mlp_keys.encoder) + list(cfg.cnn_keys.encoder)
         self.clip_t = torch.tensor(float(cfg.algo.clip_coef), device=dev)
         self.ent_t = torch.tensor(float(cfg.algo.ent_coef), device=dev)
-        enabled = (dev.type == "cuda" and bool(getattr(runner, "cuda_graphs", False)) and runner.world_size == 1
-                   and not cfg.algo.anneal_lr)
-        self.graphed = GraphedStep(self._train, warmup=2, enabled=enabled, name="ppo_train")
+        graphs = dev.type == "cuda" and bool(getattr(runner, "cuda_graphs", False)) and not cfg.algo.anneal_lr
+        self.segmented = SegmentedPPOUpdate(self) if graphs and (runner.world_size > 1 or force_segmented) else None
+        self.graphed = GraphedStep(self._train, warmup=2, enabled=graphs and self.segmented is None, name="ppo_train")
         from sheeprl_prey_amd import ops
 
-        plan = FusedPPOTrainer.plan(runner, agent, optimizer, cfg) if cfg.algo.get("fused_update", True) and ops._FUSED else None
+        plan = (FusedPPOTrainer.plan(runner, agent, optimizer, cfg)
+                if cfg.algo.get("fused_update", True) and ops._FUSED and self.segmented is None else None)
         self.fused = FusedPPOTrainer(runner, agent, optimizer, cfg, n, plan) if plan is not None else None
+
+    @property
+    def mode(self) -> str:
+        if self.fused is not None:
+            return "fused"
+        if self.segmented is not None:
+            return "segmented"
+        return "graph" if self.graphed.enabled else "eager"
 
     def _train(self, data: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         cfg = self.cfg
@@ -202,12 +311,13 @@ class PPOTrainer:
         if self.fused is not None:
             self.fused(data, aggregator)
             return
-        if not self.graphed.enabled:
+        if self.segmented is None and not self.graphed.enabled:
             train(self.runner, self.agent, self.optimizer, data, aggregator, self.cfg)
             return
         self.clip_t.fill_(float(self.cfg.algo.clip_coef))
         self.ent_t.fill_(float(self.cfg.algo.ent_coef))
-        out = self.graphed({k: data[k] for k in data.keys()})
+        inputs = {k: data[k] for k in data.keys()}
+        out = self.segmented(inputs) if self.segmented is not None else self.graphed(inputs)
         if aggregator is not None:
             for k, v in out.items():
                 aggregator.update(k, v.clone())

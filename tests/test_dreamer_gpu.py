@@ -5,7 +5,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _build(graphs: bool, seed: int = 0):
+def _build(graphs: bool, seed: int = 0, continuous: bool = False):
     from sheeprl_prey_amd.algos.dreamer_v3.agent import build_models
     from sheeprl_prey_amd.algos.dreamer_v3.dreamer_v3 import DreamerV3Trainer
     from sheeprl_prey_amd.algos.dreamer_v3.utils import Moments
@@ -25,18 +25,20 @@ def _build(graphs: bool, seed: int = 0):
     torch.manual_seed(seed)
     runner = Runner(**dict(cfg.fabric))
     obs_space = spaces.Dict({"rgb": spaces.Box(0, 255, (3, 64, 64), "uint8")})
-    wm, actor, critic, target = build_models(runner, [5], False, cfg, obs_space)
+    adim = [3] if continuous else [5]
+    wm, actor, critic, target = build_models(runner, adim, continuous, cfg, obs_space)
     opts = [build_optimizer(c, m.parameters()) for c, m in
             ((cfg.algo.world_model.optimizer, wm), (cfg.algo.actor.optimizer, actor), (cfg.algo.critic.optimizer, critic))]
-    trainer = DreamerV3Trainer(runner, cfg, wm, actor, critic, target, *opts, Moments(None).cuda(), False, [5])
+    trainer = DreamerV3Trainer(runner, cfg, wm, actor, critic, target, *opts, Moments(None).cuda(), continuous, adim)
     return trainer
 
 
-def _data(T=16, B=4, seed=1):
+def _data(T=16, B=4, seed=1, continuous=False):
     g = torch.Generator(device="cuda").manual_seed(seed)
     return {
         "rgb": torch.randint(0, 255, (T, B, 3, 64, 64), dtype=torch.uint8, device="cuda", generator=g),
-        "actions": torch.nn.functional.one_hot(torch.randint(0, 5, (T, B), device="cuda", generator=g), 5).float(),
+        "actions": (torch.rand(T, B, 3, device="cuda", generator=g) * 2 - 1) if continuous else
+        torch.nn.functional.one_hot(torch.randint(0, 5, (T, B), device="cuda", generator=g), 5).float(),
         "rewards": torch.randn(T, B, 1, device="cuda", generator=g),
         "dones": (torch.rand(T, B, 1, device="cuda", generator=g) < 0.1).float(),
         "is_first": (torch.rand(T, B, 1, device="cuda", generator=g) < 0.1).float(),
@@ -129,16 +131,18 @@ def _check_scan_vs_python(H, D, hid, B, T, impl, tol=(2e-3, 2e-4), gtol=(3e-3, 3
         torch.testing.assert_close(p1.grad, p2.grad, rtol=gtol[0], atol=gtol[1], msg=lambda m: f"{n}: {m}")
 
 
-def test_dv3_segmented_graph_matches_single_graph():
+@pytest.mark.parametrize("continuous", [False, True])
+def test_dv3_segmented_graph_matches_single_graph(continuous):
     """Multi-rank execution mode (one hipGraph per phase, collectives between replays) forced on one
-    rank must reproduce the single-graph step."""
-    a = _build(graphs=True, seed=5)
-    b = _build(graphs=True, seed=5)
+    rank must reproduce the single-graph step - for continuous actors too, whose actor loss
+    back-propagates through the imagination graph recorded in the previous phase's capture."""
+    a = _build(graphs=True, seed=5, continuous=continuous)
+    b = _build(graphs=True, seed=5, continuous=continuous)
     from sheeprl_prey_amd.algos.dreamer_v3.dreamer_v3 import DreamerV3Trainer
 
     b2 = DreamerV3Trainer(b.runner, b.cfg, b.world_model, b.actor, b.critic, b.target_critic, b.world_optimizer,
-                          b.actor_optimizer, b.critic_optimizer, b.moments, False, [5], force_segmented=True)
-    data = _data(seed=9)
+                          b.actor_optimizer, b.critic_optimizer, b.moments, continuous, b.actions_dim, force_segmented=True)
+    data = _data(seed=9, continuous=continuous)
     la, lb = [], []
     for i in range(5):
         torch.manual_seed(100 + i)
@@ -149,6 +153,8 @@ def test_dv3_segmented_graph_matches_single_graph():
     assert la[-1] < la[0] and lb[-1] < lb[0]
     # both executions train (identical math; RNG streams differ once graphs replay)
     assert abs(la[1] - lb[1]) / abs(la[1]) < 1e-3, (la, lb)
+    for k in ("Loss/policy_loss", "Loss/value_loss"):
+        assert torch.isfinite(b2.seg.static_out[k]).all()
 
 
 def test_imagine_discrete_matches_reference_loop(monkeypatch):
