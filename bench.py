@@ -570,3 +570,6 @@ def bench_ppo(args):
 
 if __name__ == "__main__":
     main()
+    if os.environ.get("SRL_DUMP_MAPS"):  # diagnostic: attribute native frames of a crash at exit
+        with open("/proc/self/maps") as f, open(os.environ["SRL_DUMP_MAPS"], "w") as o:
+            o.write(f.read())

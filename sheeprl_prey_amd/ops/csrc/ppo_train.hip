@@ -155,7 +155,7 @@ __device__ void pt_stage(const PTArgs& p, float* lds, int NL) {
   }
 }
 
-// Grid-wide barrier of the nwg co-resident workgroups (cooperative launch): monotonic counter,
+// Grid-wide barrier of the nwg co-resident workgroups (residency checked by the launcher): monotonic counter,
 // producer = every wave drains its stores, lane 0 releases at agent scope and arrives; consumer =
 // relaxed polls, one agent-scope acquire, then the workgroup barrier (MI355X_MICROARCH.md,
 // inter-workgroup visibility).  The poll gives up after ~1 s and flags `err` so a broken launch ends.
@@ -546,8 +546,16 @@ hipError_t launch_ppo_mlp_train(const srl::PTArgs& p, hipStream_t st) {
     hipLaunchKernelGGL(srl::ppo_mlp_train_kernel, dim3(1), dim3(srl::PT_THREADS), 0, st, p);
     return hipGetLastError();
   }
-  // the workgroups meet at grid barriers: a cooperative launch guarantees (and checks) co-residency
-  srl::PTArgs a = p;
-  void* args[] = {(void*)&a};
-  return hipLaunchCooperativeKernel((const void*)srl::ppo_mlp_train_kernel, dim3(p.nwg), dim3(srl::PT_THREADS), args, 0, st);
+  // The workgroups meet at grid barriers, so all nwg must be resident at once.  That is checked here
+  // from the occupancy (nwg is a handful on a 256-CU part) and the barrier itself is bounded (it
+  // flags `err` and moves on).  A plain launch, not hipLaunchCooperativeKernel: the cooperative
+  // launch path creates a queue of its own whose teardown at process exit faults under rocprofv3
+  // kernel tracing (profiles/r2_rocprof_exit_crash.md).
+  int dev = 0, cus = 0, per_cu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)srl::ppo_mlp_train_kernel, srl::PT_THREADS, 0);
+  if (per_cu < 1 || p.nwg > per_cu * cus) return hipErrorCooperativeLaunchTooLarge;
+  hipLaunchKernelGGL(srl::ppo_mlp_train_kernel, dim3(p.nwg), dim3(srl::PT_THREADS), 0, st, p);
+  return hipGetLastError();
 }
