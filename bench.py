@@ -50,8 +50,6 @@ def parse():
                         "on any N, to price it against the single-graph step at N=1")
     p.add_argument("--check-finite", type=int, default=0,
                    help="diagnostic: run N untimed steps, report the first non-finite train output per step")
-    p.add_argument("--host-times", action="store_true",
-                   help="diagnostic: host wall time per part of a bench step (act+readback / sample+launch / env)")
     p.add_argument("--gemm-tuning", default=None, choices=["use", "tune", "off"],
                    help="library-GEMM TunableOp mode (default: fabric.tunable_gemm = use the committed results)")
     p.add_argument("overrides", nargs="*")
@@ -117,77 +115,14 @@ def main():
                                is_continuous, actions_dim, force_segmented=args.phase_times or args.segmented)
     n_params = sum(p.numel() for m in (world_model, actor, critic) for p in m.parameters())
     rb = AsyncReplayBuffer(cfg.buffer.size // (cfg.env.num_envs * world), cfg.env.num_envs, device=device, sequential=True)
-    obs_keys = list(cfg.cnn_keys.encoder)
-    o = envs.reset(seed=cfg.seed + rank)[0]
-    step_data = TensorDict({}, batch_size=[cfg.env.num_envs], device="cpu")
-    for k in obs_keys:
-        step_data[k] = torch.from_numpy(np.asarray(o[k]))
-    step_data["dones"] = torch.zeros(cfg.env.num_envs, 1)
-    step_data["rewards"] = torch.zeros(cfg.env.num_envs, 1)
-    step_data["is_first"] = torch.ones(cfg.env.num_envs, 1)
+    # the env-interaction step of dreamer_v3.main itself (interaction.py): pinned staging ring, H2D on
+    # a side stream, the player graph, the replay add and the train-graph launch enqueued back to back,
+    # the host waits only for the action readback and steps the env while the GPU trains
+    from sheeprl_prey_amd.algos.dreamer_v3.interaction import InteractionLoop
+
+    loop = InteractionLoop(runner, cfg, envs, player, rb, actions_dim, is_continuous)
     player.use_graphs = runner.cuda_graphs
-    player.init_states()
-    obs = {k: step_data[k] for k in obs_keys}
-
-    def act_and_add(random_actions: bool):
-        if random_actions:
-            real = np.array(envs.action_space.sample())
-            acts = np.concatenate([np.eye(d, dtype=np.float32)[a] for a, d in zip(real.reshape(len(actions_dim), -1), actions_dim)], -1)
-        else:
-            with torch.no_grad():
-                pre = {k: v[None].to(device) / 255.0 for k, v in obs.items()}  # pageable source: sync copy
-                a = player.get_exploration_action(pre, is_continuous)
-                acts = torch.cat(a, -1).cpu().numpy()
-                real = np.array([x.argmax(-1).cpu().numpy() for x in a])
-        step_data["actions"] = torch.from_numpy(np.asarray(acts)).view(cfg.env.num_envs, -1).float()
-        rb.add(step_data[None, ...])
-        return real
-
-    def env_advance(real):
-        nonlocal obs
-        o, r, d, tr, infos = envs.step(real.reshape(envs.action_space.shape))
-        d = np.logical_or(d, tr)
-        step_data["is_first"] = torch.zeros(cfg.env.num_envs, 1)
-        for k in obs_keys:
-            step_data[k] = torch.from_numpy(np.asarray(o[k]))
-        obs = {k: step_data[k] for k in obs_keys}
-        step_data["rewards"] = torch.from_numpy(np.asarray(r)).view(-1, 1).float()
-        step_data["dones"] = torch.from_numpy(np.asarray(d)).view(-1, 1).float()
-        idx = np.nonzero(d)[0].tolist()
-        if idx:
-            step_data["dones"][idx] = 0.0
-            step_data["rewards"][idx] = 0.0
-            step_data["is_first"][idx] = 1.0
-            player.init_states(idx)
-
-    # pipelined policy step (timed loop): the row's host data is staged in pinned buffers (two, used
-    # alternately) so the replay add, the batch sample and the train-graph launch are all enqueued
-    # right behind the player graph; the host then waits only for the action readback (an event
-    # after the player), steps the env, and the GPU goes from the player straight into training.
-    row_keys = obs_keys + ["rewards", "dones", "is_first"]
-    staging = [{k: torch.empty_like(step_data[k]).pin_memory() for k in row_keys} for _ in range(2)]
-    real_pin = torch.empty((len(actions_dim), cfg.env.num_envs), dtype=torch.int64).pin_memory()
-    act_ev = torch.cuda.Event()
-    slot = [0]
-
-    def act_add_train():
-        # buffer `slot` was last read by copies enqueued before the player of the previous step,
-        # whose readback event this host thread has already waited on
-        b = staging[slot[0]]
-        slot[0] ^= 1
-        for k in row_keys:
-            b[k].copy_(step_data[k])
-        with torch.no_grad():
-            pre = {k: b[k][None].to(device, non_blocking=True) / 255.0 for k in obs_keys}
-            a = player.get_exploration_action(pre, is_continuous)
-            acts = torch.cat(a, -1).view(cfg.env.num_envs, -1)
-            real_pin.copy_(torch.stack([x.argmax(-1) for x in a]).view(len(actions_dim), -1), non_blocking=True)
-            act_ev.record()
-        row = TensorDict({**{k: b[k] for k in row_keys}, "actions": acts}, batch_size=[cfg.env.num_envs])
-        rb.add(row[None, ...])
-        out = train_once()
-        act_ev.synchronize()
-        return real_pin.numpy().copy(), out
+    loop.reset(cfg.seed + rank)
 
     grad_steps = 0
     last_batch = [None]
@@ -203,41 +138,23 @@ def main():
         return out
 
     for _ in range(max(args.prefill, cfg.per_rank_sequence_length + 1)):
-        env_advance(act_and_add(True))
+        loop.step(True)
 
     env_ms = [0.0]
-    host_ms = [0.0, 0.0, 0.0, 0]
 
     def one_step():
-        # act (weights W_t) -> store the row -> launch the gradient step (async, W_t -> W_t+1) -> step
-        # the env on the CPU while the GPU trains (the env step needs only the action): the same
-        # order of effects as the reference's act / env-step / add / train loop.  Default: the
-        # pipelined act_add_train; --phase-times / --host-times time the serial form of the same step.
+        # act (weights W_t) -> store the row -> launch the gradient step (W_t -> W_t+1) -> env step on
+        # the CPU while the GPU trains.  --phase-times times the serial form of the same step.
         if args.phase_times:
+            loop.pipelined = False
             torch.cuda.synchronize()
             t = time.perf_counter()
-            real = act_and_add(False)
+            loop.step(False, None)
             torch.cuda.synchronize()
             env_ms[0] += (time.perf_counter() - t) * 1e3
-        elif args.host_times:
-            t0 = time.perf_counter()
-            real = act_and_add(False)  # player graph + action readback (waits for the previous step)
-            t1 = time.perf_counter()
-            out = train_once()  # replay sample + train-graph launch
-            t2 = time.perf_counter()
-            env_advance(real)  # CPU env step, overlapping the GPU train step
-            t3 = time.perf_counter()
-            for i, d in enumerate((t1 - t0, t2 - t1, t3 - t2)):
-                host_ms[i] += d * 1e3
-            host_ms[3] += 1
-            return out
-        else:
-            real, out = act_add_train()
-            env_advance(real)
-            return out
-        out = train_once()
-        env_advance(real)
-        return out
+            return train_once()
+        loop.step(False, train_once)
+        return loop.last_train_out
 
     if args.check_finite:
         check_finite_steps(args, trainer, rb, cfg, one_step, lambda: trainer.train_step(last_batch[0]), (world_model, actor, critic),
@@ -273,7 +190,6 @@ def main():
     if args.profile_steps:
         torch.cuda._sleep(1000)  # marker kernel: scripts/trace_window.py aggregates the dispatches after it
         torch.cuda.synchronize()
-    host_ms[:] = [0.0, 0.0, 0.0, 0]
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = one_step()
@@ -282,10 +198,6 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if args.host_times and rank == 0 and host_ms[3]:
-        n = host_ms[3]
-        print(f"host ms/step: act+readback {host_ms[0] / n:.3f}, sample+launch {host_ms[1] / n:.3f}, "
-              f"env step {host_ms[2] / n:.3f}", file=sys.stderr, flush=True)
     if args.phase_times and rank == 0:
         seg = trainer.seg
         if seg.phase_ms is not None and seg.timed_steps:

@@ -18,3 +18,4 @@ t = [r for r in rows if any(k.startswith("Time/") for k in r)]
 print(json.dumps({"dv3_cli_total_policy_steps": steps, "env_steps": steps, "cli_wall_s": round(s1 - s0, 2), "time_metrics": t,
                   "losses_last": {k: v for r in rows for k, v in r.items() if k.startswith("Loss/")}}))
 PY
+rm -rf gpurun_out/dv3cli/run  # logs / checkpoints: too large to copy back

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import copy
 import os
+import time
 import warnings
 from typing import Any, Dict, List, Sequence
 
@@ -38,6 +39,7 @@ from sheeprl_prey_amd.algos.common import (
     warn_log_ckpt_every,
 )
 from sheeprl_prey_amd.algos.dreamer_v3.agent import PlayerDV3, build_models
+from sheeprl_prey_amd.algos.dreamer_v3.interaction import InteractionLoop
 from sheeprl_prey_amd.algos.dreamer_v3.loss import reconstruction_loss
 from sheeprl_prey_amd.algos.dreamer_v3.utils import Moments, compute_lambda_values, test
 from sheeprl_prey_amd.data.buffers import AsyncReplayBuffer
@@ -394,7 +396,6 @@ def main(runner, cfg: Dict[str, Any]):
             rb.load_state_dict(state["rb"])
         else:
             raise RuntimeError(f"Given {len(state['rb'])}, but {world_size} processes are instantiated")
-    step_data = TensorDict({}, batch_size=[cfg.env.num_envs], device="cpu")
     expl_decay_steps = state["expl_decay_steps"] if state else 0
 
     train_step = 0
@@ -415,117 +416,53 @@ def main(runner, cfg: Dict[str, Any]):
                                               final=cfg.algo.player.expl_min, max_decay_steps=max_step_expl_decay)
     warn_log_ckpt_every(cfg, policy_steps_per_update)
 
-    o = envs.reset(seed=cfg.seed)[0]
-    obs = {}
-    for k in obs_keys:
-        t = torch.from_numpy(np.asarray(o[k])).view(cfg.env.num_envs, *np.asarray(o[k]).shape[1:])
-        if k in cfg.mlp_keys.encoder:
-            t = t.float()
-        step_data[k] = t
-        obs[k] = t
-    step_data["dones"] = torch.zeros(cfg.env.num_envs, 1)
-    step_data["rewards"] = torch.zeros(cfg.env.num_envs, 1)
-    step_data["is_first"] = torch.ones_like(step_data["dones"])
+    # env interaction shared with bench.py (interaction.py): pinned staging ring, H2D on a side stream,
+    # the gradient steps launched before the CPU env step so the two overlap
     player.use_graphs = bool(runner.cuda_graphs) and cfg.algo.actor.cls.endswith(".Actor")
-    player.init_states()
+    loop = InteractionLoop(runner, cfg, envs, player, rb, actions_dim, is_continuous, clip_rewards_fn)
+    loop.reset(cfg.seed)
+    train_events = []  # (start, end) GPU events of launched gradient bursts, charged to Time/train_time at log
 
     per_rank_gradient_steps = 0
+
+    def train_burst(n_samples: int) -> None:
+        nonlocal per_rank_gradient_steps
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if device.type == "cuda" else None
+        t0 = time.perf_counter()
+        if ev:
+            ev[0].record()
+        local_data = rb.sample(cfg.per_rank_batch_size, sequence_length=cfg.per_rank_sequence_length, n_samples=n_samples)
+        local_data = local_data.to(device)
+        for i in range(n_samples):
+            if per_rank_gradient_steps % cfg.algo.critic.target_network_update_freq == 0:
+                trainer.update_target(1.0 if per_rank_gradient_steps == 0 else cfg.algo.critic.tau)
+            batch = {k: v[i].float() if v.dtype != torch.uint8 else v[i] for k, v in local_data.items()}
+            metrics = trainer.train_step(batch)
+            for k, v in metrics.items():
+                aggregator.update(k, v)
+            per_rank_gradient_steps += 1
+        if ev:
+            ev[1].record()
+            train_events.append(ev)
+        else:
+            timer.add("Time/train_time", time.perf_counter() - t0)
+
     for update in range(start_step, num_updates + 1):
         policy_step += cfg.env.num_envs * world_size
+        random_actions = update <= learning_starts and state is None and "minedojo" not in cfg.algo.actor.cls.lower()
+        train_now = update >= learning_starts and updates_before_training - 1 <= 0
+        n_samples = (cfg.algo.per_rank_pretrain_steps if update == learning_starts else cfg.algo.per_rank_gradient_steps)
         with timer("Time/env_interaction_time"):
-            if update <= learning_starts and state is None and "minedojo" not in cfg.algo.actor.cls.lower():
-                real_actions = actions = np.array(envs.action_space.sample())
-                if not is_continuous:
-                    actions = np.concatenate(
-                        [np.eye(d, dtype=np.float32)[a] for a, d in
-                         zip(actions.reshape(len(actions_dim), -1), actions_dim)], axis=-1)
-            else:
-                with torch.no_grad():
-                    pre = {}
-                    for k, v in obs.items():
-                        v = v[None].to(device, non_blocking=v.is_pinned())
-                        pre[k] = v / 255.0 if k in cfg.cnn_keys.encoder else v
-                    mask = {k: v for k, v in pre.items() if k.startswith("mask")} or None
-                    real_actions = actions = player.get_exploration_action(pre, is_continuous, mask)
-                    actions = torch.cat(actions, -1).cpu().numpy()
-                    if is_continuous:
-                        real_actions = torch.cat(real_actions, dim=-1).cpu().numpy()
-                    else:
-                        real_actions = np.array([a.cpu().argmax(dim=-1).numpy() for a in real_actions])
-            step_data["actions"] = torch.from_numpy(np.asarray(actions)).view(cfg.env.num_envs, -1).float()
-            rb.add(step_data[None, ...])
-            o, rewards, dones, truncated, infos = envs.step(np.asarray(real_actions).reshape(envs.action_space.shape))
-            dones = np.logical_or(dones, truncated)
-
-        step_data["is_first"] = torch.zeros_like(step_data["dones"])
-        if "restart_on_exception" in infos:
-            for i, roe in enumerate(infos["restart_on_exception"]):
-                if roe and not dones[i]:
-                    b = rb.buffer[i]
-                    last = (b._pos - 1) % b.buffer_size
-                    b["dones"][last] = torch.ones_like(b["dones"][last])
-                    b["is_first"][last] = torch.zeros_like(b["is_first"][last])
-                    step_data["is_first"][i] = torch.ones_like(step_data["is_first"][i])
+            infos = loop.step(random_actions, (lambda: train_burst(n_samples)) if train_now else None)
 
         for i, ep_rew, ep_len in episode_stats(infos):
             aggregator.update("Rewards/rew_avg", ep_rew)
             aggregator.update("Game/ep_len_avg", ep_len)
             runner.print(f"Rank-0: policy_step={policy_step}, reward_env_{i}={ep_rew[-1]}")
 
-        real_next_obs = {k: np.array(v, copy=True) for k, v in o.items()}
-        if "final_observation" in infos:
-            for idx, final_obs in enumerate(infos["final_observation"]):
-                if final_obs is not None:
-                    for k, v in final_obs.items():
-                        real_next_obs[k][idx] = v
-        next_obs = {}
-        for k in obs_keys:
-            t = torch.from_numpy(np.asarray(o[k])).view(cfg.env.num_envs, *np.asarray(o[k]).shape[1:])
-            if k in cfg.mlp_keys.encoder:
-                t = t.float()
-            step_data[k] = t
-            next_obs[k] = t
-        obs = next_obs
-
-        rewards = torch.from_numpy(np.asarray(rewards)).view(cfg.env.num_envs, -1).float()
-        dones_t = torch.from_numpy(np.asarray(dones)).view(cfg.env.num_envs, -1).float()
-        step_data["dones"] = dones_t
-        step_data["rewards"] = clip_rewards_fn(rewards)
-
-        dones_idxes = dones_t.nonzero(as_tuple=True)[0].tolist()
-        if dones_idxes:
-            n = len(dones_idxes)
-            reset_data = TensorDict({}, batch_size=[n], device="cpu")
-            for k in obs_keys:
-                v = torch.from_numpy(real_next_obs[k][dones_idxes])
-                reset_data[k] = v.float() if k in cfg.mlp_keys.encoder else v
-            reset_data["dones"] = torch.ones(n, 1)
-            reset_data["actions"] = torch.zeros(n, int(np.sum(actions_dim)))
-            reset_data["rewards"] = step_data["rewards"][dones_idxes].float()
-            reset_data["is_first"] = torch.zeros_like(reset_data["dones"])
-            rb.add(reset_data[None, ...], dones_idxes)
-            step_data["rewards"][dones_idxes] = 0.0
-            step_data["dones"][dones_idxes] = 0.0
-            step_data["is_first"][dones_idxes] = 1.0
-            player.init_states(dones_idxes)
-
         updates_before_training -= 1
-
-        if update >= learning_starts and updates_before_training <= 0:
-            runner.barrier()
-            n_samples = cfg.algo.per_rank_pretrain_steps if update == learning_starts else cfg.algo.per_rank_gradient_steps
-            local_data = rb.sample(cfg.per_rank_batch_size, sequence_length=cfg.per_rank_sequence_length, n_samples=n_samples)
-            local_data = local_data.to(device)
-            with timer("Time/train_time"):
-                for i in range(n_samples):
-                    if per_rank_gradient_steps % cfg.algo.critic.target_network_update_freq == 0:
-                        trainer.update_target(1.0 if per_rank_gradient_steps == 0 else cfg.algo.critic.tau)
-                    batch = {k: v[i].float() if v.dtype != torch.uint8 else v[i] for k, v in local_data.items()}
-                    metrics = trainer.train_step(batch)
-                    for k, v in metrics.items():
-                        aggregator.update(k, v)
-                    per_rank_gradient_steps += 1
-                train_step += world_size
+        if train_now:
+            train_step += world_size
             updates_before_training = cfg.algo.train_every // policy_steps_per_update
             if cfg.algo.player.expl_decay:
                 expl_decay_steps += 1
@@ -534,6 +471,10 @@ def main(runner, cfg: Dict[str, Any]):
             aggregator.update("Params/exploration_amout", player.expl_amount)
 
         if policy_step - last_log >= cfg.metric.log_every or update == num_updates or cfg.dry_run:
+            for e0, e1 in train_events:
+                e1.synchronize()
+                timer.add("Time/train_time", e0.elapsed_time(e1) / 1e3)
+            train_events.clear()
             runner.log_dict(aggregator.compute(), policy_step)
             aggregator.reset()
             log_throughput(runner, timer.compute(), policy_step, last_log, train_step, last_train, cfg.env.action_repeat)

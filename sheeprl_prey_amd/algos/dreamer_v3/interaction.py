@@ -1,0 +1,188 @@
+"""The env-interaction step of the DreamerV3 loop (reference ``dreamer_v3.py:587-709``), shared by
+``dreamer_v3.main`` and ``bench.py`` so the headline number measures the loop users run.
+
+One step on the GPU, in stream order:
+
+    host: row (obs_t, reward_t, done_t, is_first_t) -> pinned ring slot (two slots, alternating)
+    side stream: pinned slot -> device obs buffer (H2D), event
+    main stream: wait(H2D event) -> player graph (act with W_t) -> action readback into pinned memory,
+                 event -> replay-buffer add of the row (+ action) -> [gradient steps: graph launches]
+    host: wait(readback event) only -> env.step on the CPU while the GPU trains -> bookkeeping
+
+The order of effects is the reference's act / env step / add / train order (the row a gradient step
+samples is added before it, the next action uses the trained weights); the env step needs only the
+action, so it overlaps the training graphs instead of waiting for them.  CPU runs keep the serial form.
+"""
+from __future__ import annotations
+
+from typing import Any, Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from sheeprl_prey_amd.data.tensordict import TensorDict
+
+
+class InteractionLoop:
+    def __init__(self, runner, cfg, envs, player, rb, actions_dim: Sequence[int], is_continuous: bool,
+                 clip_rewards: Optional[Callable] = None):
+        self.runner, self.cfg, self.envs, self.player, self.rb = runner, cfg, envs, player, rb
+        self.actions_dim = list(actions_dim)
+        self.is_continuous = is_continuous
+        self.clip_rewards = clip_rewards or (lambda r: r)
+        self.device = runner.device
+        self.ne = int(cfg.env.num_envs)
+        self.cnn_keys = list(cfg.cnn_keys.encoder)
+        self.mlp_keys = list(cfg.mlp_keys.encoder)
+        self.obs_keys = self.cnn_keys + self.mlp_keys
+        self.row_keys = self.obs_keys + ["rewards", "dones", "is_first"]
+        self.pipelined = self.device.type == "cuda"
+        self.step_data = TensorDict({}, batch_size=[self.ne], device="cpu")
+        self._slot = 0
+        self._ring: List[Dict[str, torch.Tensor]] = []
+
+    # ------------------------------------------------------------------ setup
+    def _obs_tensor(self, k: str, v) -> torch.Tensor:
+        a = np.asarray(v)
+        t = torch.from_numpy(a).view(self.ne, *a.shape[1:])
+        return t.float() if k in self.mlp_keys else t
+
+    def reset(self, seed: int) -> None:
+        o = self.envs.reset(seed=seed)[0]
+        for k in self.obs_keys:
+            self.step_data[k] = self._obs_tensor(k, o[k])
+        self.step_data["dones"] = torch.zeros(self.ne, 1)
+        self.step_data["rewards"] = torch.zeros(self.ne, 1)
+        self.step_data["is_first"] = torch.ones(self.ne, 1)
+        self.player.init_states()
+        if self.pipelined:
+            sd = self.step_data
+            self._ring = [{k: torch.empty_like(sd[k]).pin_memory() for k in self.row_keys} for _ in range(2)]
+            self._dev_obs = {k: torch.empty_like(sd[k], device=self.device) for k in self.obs_keys}
+            width = sum(self.actions_dim) if self.is_continuous else len(self.actions_dim)
+            dtype = torch.float32 if self.is_continuous else torch.int64
+            shape = (self.ne, width) if self.is_continuous else (width, self.ne)
+            self._real_pin = torch.empty(shape, dtype=dtype).pin_memory()
+            self._h2d = torch.cuda.Stream(device=self.device)
+            self._h2d_ev = torch.cuda.Event()
+            self._act_ev = torch.cuda.Event()
+
+    # ------------------------------------------------------------------ acting
+    def _random_actions(self):
+        real = np.array(self.envs.action_space.sample())
+        acts = real
+        if not self.is_continuous:
+            acts = np.concatenate([np.eye(d, dtype=np.float32)[a] for a, d in
+                                   zip(real.reshape(len(self.actions_dim), -1), self.actions_dim)], axis=-1)
+        return real, acts
+
+    def _policy_serial(self):
+        """CPU (or diagnostic) form: pageable copies, blocking readback."""
+        pre = {}
+        for k in self.obs_keys:
+            v = self.step_data[k][None].to(self.device)
+            pre[k] = v / 255.0 if k in self.cnn_keys else v
+        mask = {k: v for k, v in pre.items() if k.startswith("mask")} or None
+        with torch.no_grad():
+            actions = self.player.get_exploration_action(pre, self.is_continuous, mask)
+        acts = torch.cat(actions, -1).cpu().numpy()
+        if self.is_continuous:
+            real = acts
+        else:
+            real = np.array([a.cpu().argmax(dim=-1).numpy() for a in actions])
+        return real, acts
+
+    def _policy_pipelined(self) -> None:
+        """Stage the row, act, enqueue the row's replay add; the action comes back via ``_real_pin``."""
+        b = self._ring[self._slot]
+        self._slot ^= 1
+        for k in self.row_keys:  # slot last read by work enqueued before the previous step's player
+            b[k].copy_(self.step_data[k])
+        # the device obs buffer was last read by the previous player, which the host already waited for
+        # (its readback event): the copy may overlap the previous step's training on the main stream
+        main = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(self._h2d):
+            for k in self.obs_keys:
+                self._dev_obs[k].copy_(b[k], non_blocking=True)
+            self._h2d_ev.record(self._h2d)
+        main.wait_event(self._h2d_ev)
+        with torch.no_grad():
+            pre = {k: (v[None] / 255.0 if k in self.cnn_keys else v[None]) for k, v in self._dev_obs.items()}
+            mask = {k: v for k, v in pre.items() if k.startswith("mask")} or None
+            actions = self.player.get_exploration_action(pre, self.is_continuous, mask)
+            acts = torch.cat(actions, -1).view(self.ne, -1)
+            if self.is_continuous:
+                self._real_pin.copy_(acts, non_blocking=True)
+            else:
+                self._real_pin.copy_(torch.stack([a.argmax(-1) for a in actions]).view(len(self.actions_dim), -1),
+                                     non_blocking=True)
+            self._act_ev.record(main)
+        row = TensorDict({**{k: b[k] for k in self.row_keys}, "actions": acts}, batch_size=[self.ne])
+        self.rb.add(row[None, ...])
+
+    # ------------------------------------------------------------------ one step
+    def step(self, random_actions: bool, train_fn: Optional[Callable[[], Any]] = None) -> Dict[str, Any]:
+        """Act (random or policy), add the row, run ``train_fn`` (launched before the env step on the
+        GPU path), step the envs.  Returns the env ``infos``."""
+        cfg, ne = self.cfg, self.ne
+        if random_actions:
+            real, acts = self._random_actions()
+            self.step_data["actions"] = torch.from_numpy(np.asarray(acts, dtype=np.float32)).view(ne, -1)
+            self.rb.add(self.step_data[None, ...])
+            out = train_fn() if train_fn is not None else None
+        elif self.pipelined:
+            self._policy_pipelined()
+            out = train_fn() if train_fn is not None else None
+            self._act_ev.synchronize()
+            real = self._real_pin.numpy().copy()
+        else:
+            real, acts = self._policy_serial()
+            self.step_data["actions"] = torch.from_numpy(np.asarray(acts, dtype=np.float32)).view(ne, -1)
+            self.rb.add(self.step_data[None, ...])
+            out = train_fn() if train_fn is not None else None
+        self.last_train_out = out
+
+        o, rewards, dones, truncated, infos = self.envs.step(np.asarray(real).reshape(self.envs.action_space.shape))
+        dones = np.logical_or(dones, truncated)
+
+        sd = self.step_data
+        sd["is_first"] = torch.zeros_like(sd["dones"])
+        if "restart_on_exception" in infos:
+            for i, roe in enumerate(infos["restart_on_exception"]):
+                if roe and not dones[i]:
+                    b = self.rb.buffer[i]
+                    last = (b._pos - 1) % b.buffer_size
+                    b["dones"][last] = torch.ones_like(b["dones"][last])
+                    b["is_first"][last] = torch.zeros_like(b["is_first"][last])
+                    sd["is_first"][i] = torch.ones_like(sd["is_first"][i])
+
+        real_next_obs = {k: np.array(v, copy=True) for k, v in o.items()}
+        if "final_observation" in infos:
+            for idx, final_obs in enumerate(infos["final_observation"]):
+                if final_obs is not None:
+                    for k, v in final_obs.items():
+                        real_next_obs[k][idx] = v
+        for k in self.obs_keys:
+            sd[k] = self._obs_tensor(k, o[k])
+        r = torch.from_numpy(np.asarray(rewards)).view(ne, -1).float()
+        d = torch.from_numpy(np.asarray(dones)).view(ne, -1).float()
+        sd["dones"] = d
+        sd["rewards"] = self.clip_rewards(r)
+
+        idxes = d.nonzero(as_tuple=True)[0].tolist()
+        if idxes:
+            n = len(idxes)
+            reset = TensorDict({}, batch_size=[n], device="cpu")
+            for k in self.obs_keys:
+                v = torch.from_numpy(real_next_obs[k][idxes])
+                reset[k] = v.float() if k in self.mlp_keys else v
+            reset["dones"] = torch.ones(n, 1)
+            reset["actions"] = torch.zeros(n, int(np.sum(self.actions_dim)))
+            reset["rewards"] = sd["rewards"][idxes].float()
+            reset["is_first"] = torch.zeros_like(reset["dones"])
+            self.rb.add(reset[None, ...], idxes)
+            sd["rewards"][idxes] = 0.0
+            sd["dones"][idxes] = 0.0
+            sd["is_first"][idxes] = 1.0
+            self.player.init_states(idxes)
+        return infos

@@ -72,6 +72,15 @@ class timer(ContextDecorator):
         return None
 
     @classmethod
+    def add(cls, name: str, seconds: float) -> None:
+        """Charge ``seconds`` measured elsewhere (e.g. GPU event time of asynchronously launched work)."""
+        if cls.disabled:
+            return
+        if name not in cls.timers:
+            cls.timers[name] = SumMetric()
+        cls.timers[name].update(seconds)
+
+    @classmethod
     def reset(cls) -> None:
         for t in cls.timers.values():
             t.reset()
