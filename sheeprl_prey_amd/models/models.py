@@ -168,8 +168,21 @@ class NatureCNN(CNN):
         return self._output_dim
 
     def forward(self, x: Tensor) -> Tensor:
+        if x.is_cuda and x.dtype == torch.float32 and ops.fused_enabled() and not self.training_eager:
+            from sheeprl_prey_amd.ops.natcnn import conv_relu_plan, conv_relu_stack
+
+            if not hasattr(self, "_nc_plan"):
+                self._nc_plan = conv_relu_plan(self.model)
+            if self._nc_plan is not None:
+                # the three conv + ReLU layers on the implicit-GEMM HIP kernels (ops/natcnn.py)
+                lead = x.shape[:-3]
+                y = conv_relu_stack(self._nc_plan, x.reshape(-1, *x.shape[-3:]))
+                x = y.reshape(*lead, -1)
+                return F.relu(self.fc(x)) if self.fc is not None else x
         x = cnn_forward(self.model, x, input_dim=x.shape[-3:], output_dim=(-1,))
         return F.relu(self.fc(x)) if self.fc is not None else x
+
+    training_eager = False  # set True to force the stock conv path (A/B measurements)
 
 
 class LayerNormGRUCell(nn.Module):

@@ -11,6 +11,13 @@ int imagine_sync_words(int nslots);
 int imagine_lds_bytes();
 void launch_imagine(const srl::imag::IP& p, hipStream_t st);
 
+void natcnn_fwd(const float* x, const float* w, const float* b, float* y, int Nb, int H, int W, int Ci, int Co, int KH,
+                int KW, int S, hipStream_t st);
+void natcnn_wgrad(const float* x, const float* dy, const float* y, float* dw, float* db, int Nb, int H, int W, int Ci,
+                  int Co, int KH, int KW, int S, hipStream_t st);
+void natcnn_dgrad(const float* dy, const float* y, const float* w, float* dcol, float* dx, int Nb, int H, int W, int Ci,
+                  int Co, int KH, int KW, int S, hipStream_t st);
+
 namespace {
 
 long long* g_prof = nullptr;  // debug timestamps of block 0 (set_imagine_prof)
@@ -118,7 +125,69 @@ void set_imagine_prof(c10::optional<torch::Tensor> buf) {
   }
 }
 
+// ------------------------------------------------------------------ NatureCNN convolutions (natcnn.hip)
+namespace {
+void nc_check(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.defined() && t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous(), "natcnn: ", name,
+              " must be a contiguous float32 GPU tensor");
+}
+struct NcDims {
+  int Nb, H, W, Ci, Co, OH, OW;
+};
+NcDims nc_dims(const torch::Tensor& x, const torch::Tensor& wp, int64_t KH, int64_t KW, int64_t S) {
+  nc_check(x, "x");
+  nc_check(wp, "w");
+  TORCH_CHECK(x.dim() == 4, "natcnn: x must be NHWC [N, H, W, C]");
+  NcDims d{(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)wp.size(0), 0, 0};
+  TORCH_CHECK(KH >= 1 && KW >= 1 && S >= 1 && d.H >= KH && d.W >= KW, "natcnn: bad kernel/stride for the input");
+  TORCH_CHECK(d.Ci % 4 == 0 && d.Co % 4 == 0, "natcnn: channel counts must be multiples of 4");
+  TORCH_CHECK(wp.dim() == 2 && wp.size(1) == KH * KW * d.Ci, "natcnn: packed weight must be [Co, KH*KW*Ci]");
+  TORCH_CHECK((int64_t)d.Nb * d.H * d.W * d.Ci < (1LL << 31), "natcnn: input too large for 32-bit offsets");
+  d.OH = (int)((d.H - KH) / S + 1);
+  d.OW = (int)((d.W - KW) / S + 1);
+  return d;
+}
+}  // namespace
+
+torch::Tensor nc_conv_fwd(torch::Tensor x, torch::Tensor wp, c10::optional<torch::Tensor> b, int64_t KH, int64_t KW,
+                          int64_t S) {
+  const NcDims d = nc_dims(x, wp, KH, KW, S);
+  const float* bp = nullptr;
+  if (b.has_value() && b->defined()) {
+    nc_check(*b, "b");
+    TORCH_CHECK(b->numel() == d.Co, "natcnn: bias size");
+    bp = b->data_ptr<float>();
+  }
+  auto y = torch::empty({d.Nb, d.OH, d.OW, d.Co}, x.options());
+  natcnn_fwd(x.data_ptr<float>(), wp.data_ptr<float>(), bp, y.data_ptr<float>(), d.Nb, d.H, d.W, d.Ci, d.Co, (int)KH,
+             (int)KW, (int)S, stream());
+  return y;
+}
+
+// {dx (empty unless need_dx), dW packed [Co, K], db [Co]} for y = relu(conv(x) + b)
+std::vector<torch::Tensor> nc_conv_bwd(torch::Tensor x, torch::Tensor y, torch::Tensor dy, torch::Tensor wp, int64_t KH,
+                                       int64_t KW, int64_t S, bool need_dx) {
+  const NcDims d = nc_dims(x, wp, KH, KW, S);
+  nc_check(y, "y");
+  nc_check(dy, "dy");
+  TORCH_CHECK(y.numel() == (int64_t)d.Nb * d.OH * d.OW * d.Co && dy.numel() == y.numel(), "natcnn: y / dy shape");
+  auto dw = torch::zeros_like(wp);
+  auto db = torch::zeros({d.Co}, x.options());
+  natcnn_wgrad(x.data_ptr<float>(), dy.data_ptr<float>(), y.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
+               d.Nb, d.H, d.W, d.Ci, d.Co, (int)KH, (int)KW, (int)S, stream());
+  torch::Tensor dx;
+  if (need_dx) {
+    dx = torch::empty_like(x);
+    auto dcol = torch::empty({(int64_t)d.Nb * d.OH * d.OW, KH * KW * d.Ci}, x.options());
+    natcnn_dgrad(dy.data_ptr<float>(), y.data_ptr<float>(), wp.data_ptr<float>(), dcol.data_ptr<float>(), dx.data_ptr<float>(),
+                 d.Nb, d.H, d.W, d.Ci, d.Co, (int)KH, (int)KW, (int)S, stream());
+  }
+  return {dx, dw, db};
+}
+
 void register_ext(pybind11::module& m) {
+  m.def("nc_conv_fwd", &nc_conv_fwd);
+  m.def("nc_conv_bwd", &nc_conv_bwd);
   m.def("imagine_info", &imagine_info);
   m.def("imagine_rollout", &imagine_rollout);
   m.def("set_imagine_prof", &set_imagine_prof);
