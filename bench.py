@@ -37,6 +37,8 @@ def parse():
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--eager-ops", action="store_true", help="route GPU ops through the eager reference (A/B only)")
     p.add_argument("--profile-steps", type=int, default=0)
+    p.add_argument("--pixel", action="store_true",
+                   help="--algo ppo: 84x84 grayscale 4-frame Atari-shaped pixel PPO (NatureCNN) on a synthetic env")
     p.add_argument("--device-env", action="store_true",
                    help="--algo ppo: step CartPole-v1 on the GPU (envs/device.py) and capture the whole rollout")
     p.add_argument("--no-fused-rollout", action="store_true",
@@ -336,9 +338,17 @@ def bench_ppo(args):
     from sheeprl_prey_amd.utils.env import make_env, make_vector_env
     from sheeprl_prey_amd.utils.utils import dotdict, gae
 
-    overrides = ["exp=ppo", "mlp_keys.encoder=[state]", "env.sync_env=True", "fabric.accelerator=cuda",
-                 f"fabric.cuda_graphs={not args.no_graphs}",
-                 "metric.log_every=1000000000"] + list(args.overrides)
+    if args.pixel:
+        # Atari-shaped pixel PPO (BASELINE config #2 shape): 84x84 grayscale, 4 stacked frames, Pong action
+        # set, NatureCNN encoder; cleanrl-style Atari schedule (8 envs x 128 steps, 4 epochs, minibatch 256)
+        obs_over = ["env=synthetic_atari", "env.id=PongNoFrameskip-v4", "env.screen_size=84", "env.grayscale=True",
+                    "env.frame_stack=4", "cnn_keys.encoder=[rgb]", "mlp_keys.encoder=[]", "env.num_envs=8",
+                    "algo.update_epochs=4", "per_rank_batch_size=256"]
+    else:
+        obs_over = ["mlp_keys.encoder=[state]"]
+    overrides = ["exp=ppo"] + obs_over + ["env.sync_env=True", "fabric.accelerator=cuda",
+                                          f"fabric.cuda_graphs={not args.no_graphs}",
+                                          "metric.log_every=1000000000"] + list(args.overrides)
     cfg = dotdict(compose(overrides))
     cfg.pop("hydra", None)
     runner = Runner(**{k: v for k, v in cfg.fabric.items()})
@@ -360,8 +370,14 @@ def bench_ppo(args):
     trainer = PPOTrainer(runner, agent, optimizer, cfg, T * ne, force_segmented=args.segmented)
     # rollout staging: env-side arrays stay on the host (one H2D per rollout), policy outputs are
     # copied into device rollout tensors; the obs for the next policy step goes H2D from pinned memory
+    cnn_keys = set(cfg.cnn_keys.encoder)
+
+    def prep(o):  # pixel frames: [envs, stack, C, H, W] -> [envs, stack*C, H, W] (as ppo.main does)
+        return {k: (np.asarray(o[k], dtype=np.float32).reshape(ne, -1, *np.asarray(o[k]).shape[-2:]) if k in cnn_keys
+                    else np.asarray(o[k], dtype=np.float32)) for k in obs_keys}
+
     o = envs.reset(seed=cfg.seed + rank)[0]
-    cur = {k: np.asarray(o[k], dtype=np.float32) for k in obs_keys}
+    cur = prep(o)
     obs_host = {k: np.zeros((T, ne) + cur[k].shape[1:], np.float32) for k in obs_keys}
     rew_host = np.zeros((T, ne, 1), np.float32)
     done_host = np.zeros((T, ne, 1), np.float32)
@@ -385,7 +401,7 @@ def bench_ppo(args):
             o, r, d, tr, info = envs.step(real.reshape(envs.action_space.shape))
             rew_host[t, :, 0] = r
             done_host[t, :, 0] = np.logical_or(d, tr)
-            cur = {k: np.asarray(o[k], dtype=np.float32) for k in obs_keys}
+            cur = prep(o)
             if "final_info" in info:
                 for ep in info["final_info"]:
                     if ep is not None and "episode" in ep:
@@ -395,7 +411,8 @@ def bench_ppo(args):
         data["dones"] = torch.from_numpy(done_host).to(device)
         data.update({n: v for n, v in buf.items()})
         with torch.no_grad():
-            nv = agent.get_value({k: torch.from_numpy(cur[k]).to(device) for k in obs_keys})
+            nv = agent.get_value({k: (torch.from_numpy(cur[k]).to(device) / 255 - 0.5 if k in cnn_keys
+                                      else torch.from_numpy(cur[k]).to(device)) for k in obs_keys})
             ret, adv = gae(data["rewards"], data["values"], data["dones"], nv, T, cfg.algo.gamma, cfg.algo.gae_lambda)
         data["returns"], data["advantages"] = ret.float(), adv.float()
         trainer(TensorDict({k: v.reshape(T * ne, *v.shape[2:]) for k, v in data.items()}, batch_size=[T * ne]), None)
@@ -452,7 +469,8 @@ def bench_ppo(args):
     policy_steps = args.steps * cfg.algo.rollout_steps * ne * world
     if rank == 0:
         rec = {
-            "metric": "PPO CartPole-v1 policy steps/sec (whole node)",
+            "metric": ("PPO Atari-shaped 84x84 pixel policy steps/sec (whole node)" if args.pixel
+                       else "PPO CartPole-v1 policy steps/sec (whole node)"),
             "value": round(policy_steps / elapsed, 3),
             "unit": "policy_steps/s (whole job)",
             "n_gpus": world,
@@ -463,9 +481,12 @@ def bench_ppo(args):
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": ("CartPole-v1 dynamics stepped on the GPU (envs/device.py), random-init weights" if args.device_env
+            "data": ("synthetic 84x84 grayscale sprites, 4 stacked frames, Pong action set (envs/synthetic.py), random-init weights"
+                     if args.pixel else
+                     "CartPole-v1 dynamics stepped on the GPU (envs/device.py), random-init weights" if args.device_env
                      else "CartPole-v1 dynamics (native host env), random-init weights"),
-            "config": {"model": "PPO MLP 2x64 tanh (exp=ppo)", "global_batch": cfg.per_rank_batch_size * world,
+            "config": {"model": ("PPO NatureCNN 8s4/4s2/3s1 + fc512 encoder, 2x64 tanh heads" if args.pixel
+                                 else "PPO MLP 2x64 tanh (exp=ppo)"), "global_batch": cfg.per_rank_batch_size * world,
                        "rollout_steps": cfg.algo.rollout_steps, "num_envs_per_rank": ne,
                        "update_epochs": cfg.algo.update_epochs, "parallelism": f"dp{world}",
                        "hipgraph": trainer.mode != "eager", "update_mode": trainer.mode, "device_env": bool(args.device_env),

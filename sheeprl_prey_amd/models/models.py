@@ -5,6 +5,7 @@ passes route through fused HIP ops (LayerNorm+act, LayerNorm-GRU epilogue) on GP
 """
 from __future__ import annotations
 
+import os
 import warnings
 from math import prod
 from typing import Dict, Optional, Sequence, Union, no_type_check
@@ -182,7 +183,7 @@ class NatureCNN(CNN):
         x = cnn_forward(self.model, x, input_dim=x.shape[-3:], output_dim=(-1,))
         return F.relu(self.fc(x)) if self.fc is not None else x
 
-    training_eager = False  # set True to force the stock conv path (A/B measurements)
+    training_eager = os.environ.get("SRL_NATCNN", "1") == "0"  # stock conv path (A/B measurements)
 
 
 class LayerNormGRUCell(nn.Module):
