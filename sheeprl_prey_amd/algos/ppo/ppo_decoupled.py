@@ -279,6 +279,15 @@ def trainer(runner, cfg: Dict[str, Any], comm: DecoupledComm):
 
 @register_algorithm(decoupled=True)
 def main(runner, cfg: Dict[str, Any]):
+    if str(cfg.algo.get("topology", "player_trainers")) == "actor_fleet":
+        # N-1 actor ranks -> 1 learner (ppo_actor_fleet.py); the default is the reference's 1 player +
+        # N-1 trainers split
+        from sheeprl_prey_amd.algos.ppo.ppo_actor_fleet import actor_fleet
+
+        cfg, _ = load_resume(runner, cfg)
+        runner.seed_everything(cfg.seed)
+        _, log_dir = setup_logger(runner, cfg)
+        return actor_fleet(runner, cfg, log_dir)
     comm = DecoupledComm(runner)
     if "minedojo" in str(cfg.env.wrapper.get("_target_", "")).lower():
         raise ValueError("MineDojo is not currently supported by PPO agent, since it does not take into consideration "

@@ -133,8 +133,12 @@ def _spawn_entry(local_rank: int, world_size: int, port: int, fn, cfg, runner_kw
     runner._init_distributed()
     try:
         fn(runner, cfg)
-    finally:
-        runner.teardown()
+    except BaseException:
+        # no final barrier after a failure: the other ranks may sit in another collective; dropping
+        # the process group makes theirs fail too instead of every rank hanging
+        runner.teardown(clean=False)
+        raise
+    runner.teardown()
 
 
 class Runner:
@@ -269,17 +273,18 @@ class Runner:
         )
         return None
 
-    def teardown(self) -> None:
+    def teardown(self, clean: bool = True) -> None:
         for lg in self._loggers:
             try:
-                lg.finalize("success")
+                lg.finalize("success" if clean else "failed")
             except Exception:
                 pass
         if dist.is_available() and dist.is_initialized():
-            try:
-                dist.barrier()
-            except Exception:
-                pass
+            if clean:
+                try:
+                    dist.barrier()
+                except Exception:
+                    pass
             dist.destroy_process_group()
 
     # ------------------------------------------------------------------ utils

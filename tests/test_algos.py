@@ -189,6 +189,18 @@ def test_ppo_decoupled(devices, env_id):
     _check_ckpt("ppo_dec", f"{env_id}{devices}", PPO_KEYS, False)
 
 
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("devices", [2, 3])
+@pytest.mark.parametrize("env_id", ["discrete_dummy", "continuous_dummy"])
+def test_ppo_actor_fleet(devices, env_id):
+    """N-1 actor ranks -> 1 learner over gloo: fixed-shape rollout slabs gathered on the learner, the
+    weights broadcast back; the learner checkpoints with the coupled PPO key set."""
+    _run(STD + ["exp=ppo_decoupled", "algo.topology=actor_fleet", "env=dummy", f"env.id={env_id}", "algo.rollout_steps=4",
+                "per_rank_batch_size=4", "algo.update_epochs=1", "root_dir=ppo_fleet", f"run_name={env_id}{devices}"],
+         devices)
+    _check_ckpt("ppo_fleet", f"{env_id}{devices}", PPO_KEYS, False)
+
+
 @pytest.mark.timeout(180)
 @pytest.mark.parametrize("devices", [1, 2])
 def test_ppo_recurrent(devices):
