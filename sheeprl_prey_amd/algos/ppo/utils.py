@@ -22,6 +22,8 @@ def test(agent, runner, cfg: Dict[str, Any], log_dir: str) -> float:
         obs = {}
         for k in keys:
             t = torch.as_tensor(np.asarray(o[k]), device=runner.device).unsqueeze(0)
+            if k in cfg.cnn_keys.encoder:  # stacked frames x channels -> channels, as the training loop
+                t = t.view(1, -1, *t.shape[-2:])
             obs[k] = t.float() / 255 - 0.5 if k in cfg.cnn_keys.encoder else t.float()
         actions = agent.get_greedy_actions(obs)
         if agent.is_continuous:

@@ -174,7 +174,7 @@ class NatureCNN(CNN):
 
             if not hasattr(self, "_nc_plan"):
                 self._nc_plan = conv_relu_plan(self.model)
-            if self._nc_plan is not None:
+            if self._nc_plan is not None and x.shape[-3] == self._nc_plan[0].in_channels:
                 # the three conv + ReLU layers on the implicit-GEMM HIP kernels (ops/natcnn.py)
                 lead = x.shape[:-3]
                 y = conv_relu_stack(self._nc_plan, x.reshape(-1, *x.shape[-3:]))
