@@ -19,7 +19,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join("sheeprl_prey_amd", "ops", "csrc")
 ARCH = os.environ.get("SRL_OFFLOAD_ARCH", "gfx950")
-HIPCC_FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-ffp-contract=fast", "-munsafe-fp-atomics",
+HIPCC_FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-ffp-contract=fast-honor-pragmas", "-munsafe-fp-atomics",
                "-Wno-unused-result"]
 
 ext_modules = []

@@ -271,6 +271,17 @@ class DreamerV3Trainer:
         lambda_values = st["lambda_values"]
         baseline = st["predicted_values"][:-1]
         offset, invscale = self.moments.update(st["gathered"])
+        if not self.is_continuous:
+            # advantage, log-probs, entropies, discounting and the mean in one kernel (actor_loss.hip)
+            z = torch.cat([p.logits for p in policies], -1) if len(policies) > 1 else policies[0].logits
+            T = z.shape[0]
+            policy_loss = ops.actor_loss_discrete(
+                z, st["imagined_actions"], lambda_values.reshape(T - 1, -1), baseline.reshape(T - 1, -1),
+                st["discount"].detach().reshape(T, -1), offset, invscale, self.actions_dim, cfg.algo.actor.ent_coef)
+            if policy_loss is not None:
+                policy_loss.backward()
+                st["out"]["Loss/policy_loss"] = policy_loss.detach()
+                return
         advantage = (lambda_values - offset) / invscale - (baseline - offset) / invscale
         if self.is_continuous:
             objective = advantage

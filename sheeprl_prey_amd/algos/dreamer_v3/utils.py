@@ -12,6 +12,12 @@ from sheeprl_prey_amd import ops
 from sheeprl_prey_amd.utils.env import make_env
 
 
+def _ranks(n: int, q: float):
+    pos = q * (n - 1)
+    lo = int(np.floor(pos))
+    return lo, min(lo + 1, n - 1), pos - lo
+
+
 def quantile(x: Tensor, q: float) -> Tensor:
     """``torch.quantile(x, q)`` (linear interpolation) built from a sort with host-constant
     indices, so it is hipGraph-capturable."""
@@ -38,11 +44,20 @@ class Moments(torch.nn.Module):
         self._percentile_high = percentile_high
         self.register_buffer("low", torch.zeros((), dtype=torch.float32))
         self.register_buffer("high", torch.zeros((), dtype=torch.float32))
+        self.register_buffer("_invscale", torch.zeros((), dtype=torch.float32), persistent=False)
 
     def gather(self, x: Tensor) -> Tensor:
         return self._runner.all_gather(x.detach()) if self._runner is not None else x.detach()
 
     def update(self, gathered: Tensor):
+        if ops._native(gathered) and gathered.dtype == torch.float32:
+            # one radix-select launch (moments.hip): both percentiles, the EMA and the scale, in place
+            g = gathered.detach().reshape(-1).contiguous()
+            l0, l1, fl = _ranks(g.numel(), self._percentile_low)
+            h0, h1, fh = _ranks(g.numel(), self._percentile_high)
+            ops._ext().moments_update(g, [l0, l1, h0, h1], [fl, fh], float(self._decay), float(self._max), self.low,
+                                      self.high, self._invscale)
+            return self.low.detach(), self._invscale.detach()
         low = quantile(gathered, self._percentile_low)
         high = quantile(gathered, self._percentile_high)
         # in place: the buffers stay the same tensors across hipGraph replays

@@ -480,3 +480,32 @@ def truncnorm_log_prob(value: Tensor, loc: Tensor, scale: Tensor, lo: Tensor, hi
         return _TruncNormLogProb.apply(value.contiguous(), loc.contiguous(), scale.contiguous(), _tn_bound(lo, loc),
                                        _tn_bound(hi, loc))
     return ref.truncnorm_log_prob(value, loc, scale, lo, hi)
+
+
+# =============================================================== DreamerV3 discrete actor objective
+class _ActorLossDiscrete(torch.autograd.Function):
+    """``csrc/actor_loss.hip``: the loss and its gradient w.r.t. the mixed logits in one pass."""
+
+    @staticmethod
+    def forward(ctx, z, actions, lam, base, disc, offset, invscale, heads, ent_coef):
+        loss, dz = _ext().actor_loss_discrete(z.contiguous(), actions.contiguous(), lam.contiguous(), base.contiguous(),
+                                              disc.contiguous(), offset.reshape(1).contiguous(),
+                                              invscale.reshape(1).contiguous(), list(heads), float(ent_coef))
+        ctx.save_for_backward(dz)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dz,) = ctx.saved_tensors
+        return dz * g, None, None, None, None, None, None, None, None
+
+
+def actor_loss_discrete(z: Tensor, actions: Tensor, lam: Tensor, base: Tensor, disc: Tensor, offset: Tensor,
+                        invscale: Tensor, heads, ent_coef: float) -> Optional[Tensor]:
+    """DreamerV3 discrete policy loss (reference ``dreamer_v3.py:258-301``) from the per-head mixed
+    logits ``z`` [T, M, A]; None when the fused kernel does not apply (the caller keeps the eager form)."""
+    if not (_native(z) and z.dim() == 3
+            and all(t.dtype == torch.float32 for t in (z, actions, lam, base, disc, offset, invscale))):
+        return None
+    return _ActorLossDiscrete.apply(z, actions.detach(), lam.detach(), base.detach(), disc.detach(), offset.detach(),
+                                    invscale.detach(), tuple(int(h) for h in heads), float(ent_coef))

@@ -1,0 +1,101 @@
+// DreamerV3 discrete-actor objective (reference: dreamer_v3/dreamer_v3.py:258-301):
+//
+//   adv[t,m]   = (lambda[t,m] - offset) / invscale - (baseline[t,m] - offset) / invscale
+//   obj[t,m]   = sum_h log_softmax(z_h[t,m])[a_h[t,m]] * adv[t,m]
+//   ent[t,m]   = ent_coef * sum_h H(softmax(z_h[t,m]))
+//   loss       = -mean_{t < T-1, m} discount[t,m] * (obj[t,m] + ent[t,m])
+//
+// z = the unimix-mixed logits of every action head [T, M, A]; offset / invscale are the Moments
+// scalars (device pointers, so the launch stays inside a captured graph).  The forward writes
+// d loss / d z as well (the loss is linear in the upstream scalar gradient, the backward only scales
+// it): d/dz_k of log_softmax[a] = a_k - p_k, of H = -p_k (log p_k + H).  One thread per (t, m) row;
+// per-workgroup partial sums, then a fixed-order final reduction (deterministic).
+#include "common.h"
+
+#include <algorithm>
+
+namespace srl {
+namespace aloss {
+
+constexpr int NTH = 256;
+constexpr int MAXH = 8;
+
+struct Heads {
+  int n, size[MAXH];
+};
+
+__global__ __launch_bounds__(NTH) void actor_loss_kernel(const float* __restrict__ z, const float* __restrict__ act,
+                                                         const float* __restrict__ lam, const float* __restrict__ base,
+                                                         const float* __restrict__ disc, const float* __restrict__ offp,
+                                                         const float* __restrict__ invp, Heads hd, int A, int T, int M,
+                                                         float ent_coef, float* __restrict__ dz, float* __restrict__ partial) {
+  __shared__ float red[NTH / 64];
+  const int rows = T * M, last = (T - 1) * M;
+  const float off = *offp, inv = *invp;
+  const float scale = -1.f / (float)last;  // d loss / d (disc * (obj + ent)) per row
+  float acc = 0.f;
+  for (int r = blockIdx.x * NTH + threadIdx.x; r < rows; r += gridDim.x * NTH) {
+    const float* zr = z + (size_t)r * A;
+    const float* ar = act + (size_t)r * A;
+    float* gr = dz + (size_t)r * A;
+    if (r >= last) {  // the last imagined step enters neither the objective nor the entropy term
+      for (int k = 0; k < A; ++k) gr[k] = 0.f;
+      continue;
+    }
+    const float adv = (lam[r] - off) / inv - (base[r] - off) / inv;
+    const float d = disc[r];
+    float lp_sum = 0.f, h_sum = 0.f;
+    int c0 = 0;
+    for (int h = 0; h < hd.n; ++h) {
+      const int C = hd.size[h];
+      float mx = -INFINITY;
+      for (int k = 0; k < C; ++k) mx = fmaxf(mx, zr[c0 + k]);
+      float se = 0.f;
+      for (int k = 0; k < C; ++k) se += __expf(zr[c0 + k] - mx);
+      const float lse = mx + __logf(se);
+      float lp = 0.f, H = 0.f;
+      for (int k = 0; k < C; ++k) {
+        const float l = zr[c0 + k] - lse, p = __expf(l);
+        lp += ar[c0 + k] * l;
+        H -= p * l;
+      }
+      lp_sum += lp;
+      h_sum += H;
+      // gradient of this row's term  scale * d * (lp * adv + ent_coef * H)
+      const float ga = scale * d * adv, ge = scale * d * ent_coef;
+      for (int k = 0; k < C; ++k) {
+        const float l = zr[c0 + k] - lse, p = __expf(l);
+        gr[c0 + k] = ga * (ar[c0 + k] - p) - ge * p * (l + H);
+      }
+      c0 += C;
+    }
+    acc += d * (lp_sum * adv + ent_coef * h_sum);
+  }
+  acc = block_sum<NTH / 64>(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = acc;
+}
+
+__global__ void actor_loss_final(const float* __restrict__ partial, int n, float scale, float* __restrict__ loss) {
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int i = 0; i < n; ++i) s += partial[i];
+    *loss = s * scale;
+  }
+}
+
+}  // namespace aloss
+}  // namespace srl
+
+int actor_loss_blocks(int rows) { return std::min(256, std::max(1, (rows + srl::aloss::NTH - 1) / srl::aloss::NTH)); }
+
+void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
+                       const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
+                       float* dz, float* partial, float* loss, hipStream_t st) {
+  srl::aloss::Heads hd{};
+  hd.n = nh;
+  for (int h = 0; h < nh; ++h) hd.size[h] = heads[h];
+  const int nb = actor_loss_blocks(T * M);
+  hipLaunchKernelGGL(srl::aloss::actor_loss_kernel, dim3(nb), dim3(srl::aloss::NTH), 0, st, z, act, lam, base, disc, offp,
+                     invp, hd, A, T, M, ent_coef, dz, partial);
+  hipLaunchKernelGGL(srl::aloss::actor_loss_final, dim3(1), dim3(64), 0, st, partial, nb, -1.f / (float)((T - 1) * M), loss);
+}

@@ -18,6 +18,14 @@ void natcnn_wgrad(const float* x, const float* dy, const float* y, float* dw, fl
 void natcnn_dgrad(const float* dy, const float* y, const float* w, float* dcol, float* dx, int Nb, int H, int W, int Ci,
                   int Co, int KH, int KW, int S, hipStream_t st);
 
+void launch_moments(const float* x, int n, int r0, int r1, int r2, int r3, float frac_lo, float frac_hi, float decay,
+                    float om, float inv_max, float* low, float* high, float* inv, hipStream_t st);
+
+int actor_loss_blocks(int rows);
+void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
+                       const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
+                       float* dz, float* partial, float* loss, hipStream_t st);
+
 namespace {
 
 long long* g_prof = nullptr;  // debug timestamps of block 0 (set_imagine_prof)
@@ -185,7 +193,58 @@ std::vector<torch::Tensor> nc_conv_bwd(torch::Tensor x, torch::Tensor y, torch::
   return {dx, dw, db};
 }
 
+// ------------------------------------------------------------------ Moments percentile EMA (moments.hip)
+// ranks = order statistics {floor, ceil} of q_low * (n - 1) and of q_high * (n - 1); low / high / inv: fp32 scalars
+void moments_update(torch::Tensor x, std::vector<int64_t> ranks, std::vector<double> fracs, double decay, double max_,
+                    torch::Tensor low, torch::Tensor high, torch::Tensor inv) {
+  nc_check(x, "x");
+  nc_check(low, "low");
+  nc_check(high, "high");
+  nc_check(inv, "inv");
+  TORCH_CHECK(low.numel() == 1 && high.numel() == 1 && inv.numel() == 1, "moments: scalar buffers");
+  TORCH_CHECK(ranks.size() == 4 && fracs.size() == 2, "moments: 4 ranks, 2 fractions");
+  const int64_t n = x.numel();
+  TORCH_CHECK(n >= 1 && n < (1LL << 31), "moments: size");
+  for (auto r : ranks) TORCH_CHECK(r >= 0 && r < n, "moments: rank out of range");
+  launch_moments(x.data_ptr<float>(), (int)n, (int)ranks[0], (int)ranks[1], (int)ranks[2], (int)ranks[3], (float)fracs[0],
+                 (float)fracs[1], (float)decay, (float)(1.0 - decay), (float)(1.0 / max_), low.data_ptr<float>(),
+                 high.data_ptr<float>(), inv.data_ptr<float>(), stream());
+}
+
+// ------------------------------------------------------------------ DreamerV3 discrete actor objective (actor_loss.hip)
+// z, actions [T, M, A]; lam, base [T-1, M]; disc [T, M] (only the first T-1 rows read); offset / invscale
+// scalars.  Returns {loss (0-dim), dloss/dz [T, M, A]}.
+std::vector<torch::Tensor> actor_loss_discrete(torch::Tensor z, torch::Tensor actions, torch::Tensor lam, torch::Tensor base,
+                                               torch::Tensor disc, torch::Tensor offset, torch::Tensor invscale,
+                                               std::vector<int64_t> heads, double ent_coef) {
+  for (auto* t : {&z, &actions, &lam, &base, &disc, &offset, &invscale}) nc_check(*t, "actor_loss operand");
+  TORCH_CHECK(z.dim() == 3 && actions.sizes() == z.sizes(), "actor_loss: z / actions must be [T, M, A]");
+  const int64_t T = z.size(0), M = z.size(1), A = z.size(2);
+  TORCH_CHECK(T >= 2 && lam.numel() == (T - 1) * M && base.numel() == (T - 1) * M && disc.numel() >= (T - 1) * M,
+              "actor_loss: lambda / baseline [T-1, M], discount [T, M]");
+  TORCH_CHECK(offset.numel() == 1 && invscale.numel() == 1, "actor_loss: scalar offset / invscale");
+  TORCH_CHECK(!heads.empty() && heads.size() <= 8, "actor_loss: 1..8 heads");
+  int64_t sum = 0;
+  std::vector<int> hs;
+  for (auto h : heads) {
+    TORCH_CHECK(h >= 1, "actor_loss: head size");
+    sum += h;
+    hs.push_back((int)h);
+  }
+  TORCH_CHECK(sum == A, "actor_loss: head sizes must add up to A");
+  auto dz = torch::empty_like(z);
+  auto loss = torch::empty({}, z.options());
+  auto partial = torch::empty({actor_loss_blocks((int)(T * M))}, z.options());
+  launch_actor_loss(z.data_ptr<float>(), actions.data_ptr<float>(), lam.data_ptr<float>(), base.data_ptr<float>(),
+                    disc.data_ptr<float>(), offset.data_ptr<float>(), invscale.data_ptr<float>(), hs.data(), (int)hs.size(),
+                    (int)A, (int)T, (int)M, (float)ent_coef, dz.data_ptr<float>(), partial.data_ptr<float>(),
+                    loss.data_ptr<float>(), stream());
+  return {loss, dz};
+}
+
 void register_ext(pybind11::module& m) {
+  m.def("actor_loss_discrete", &actor_loss_discrete);
+  m.def("moments_update", &moments_update);
   m.def("nc_conv_fwd", &nc_conv_fwd);
   m.def("nc_conv_bwd", &nc_conv_bwd);
   m.def("imagine_info", &imagine_info);

@@ -1,0 +1,118 @@
+"""DreamerV3 actor-phase kernels vs plain fp32 PyTorch:
+
+* ``moments.hip`` (radix-select percentiles + EMA) vs the sort-based ``quantile`` path
+  (reference ``dreamer_v3/utils.py:16-41``) -- bitwise, over several EMA updates, with ties / negatives.
+* ``actor_loss.hip`` (fused discrete policy objective + its logit gradient) vs the eager
+  distribution formulation (reference ``dreamer_v3/dreamer_v3.py:258-301``).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from sheeprl_prey_amd import ops
+from sheeprl_prey_amd.algos.dreamer_v3.utils import Moments
+
+pytestmark = pytest.mark.gpu
+
+
+def _moments_pair():
+    native, eager = Moments(None), Moments(None)
+    return native.cuda(), eager.cuda()
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 1000, 15 * 1024, 65536 + 3])
+def test_moments_kernel_matches_sort_path(n):
+    torch.manual_seed(n)
+    native, eager = _moments_pair()
+    for it in range(4):
+        if it == 0:
+            x = torch.randn(n, device="cuda") * 5 - 1
+        elif it == 1:  # heavy ties
+            x = torch.randint(-3, 4, (n,), device="cuda").float()
+        elif it == 2:  # signed zeros, tiny and huge magnitudes
+            x = torch.randn(n, device="cuda") * torch.tensor([1e-30, 1e30, 0.0, -0.0], device="cuda").repeat(n // 4 + 1)[:n]
+        else:
+            x = torch.rand(15, max(1, n // 15), device="cuda") * 100
+        lo_n, inv_n = native.update(x)
+        ops.set_fused(False)
+        try:
+            lo_e, inv_e = eager.update(x)
+        finally:
+            ops.set_fused(True)
+        torch.cuda.synchronize()
+        assert torch.equal(native.low, eager.low), (it, native.low.item(), eager.low.item())
+        assert torch.equal(native.high, eager.high), (it, native.high.item(), eager.high.item())
+        assert torch.equal(lo_n, lo_e) and torch.equal(inv_n, inv_e)
+
+
+def _eager_actor_loss(mixed, actions, lam, base, disc, off, inv, heads, ent_coef):
+    adv = (lam - off) / inv - (base - off) / inv  # [T-1, M, 1]
+    lps, ents = [], []
+    for z, a in zip(torch.split(mixed, heads, -1), torch.split(actions, heads, -1)):
+        logp = F.log_softmax(z, -1)
+        lps.append((logp * a).sum(-1, keepdim=True)[:-1])
+        ents.append(-(logp.exp() * logp).sum(-1))
+    obj = torch.stack(lps, -1).sum(-1) * adv
+    ent = ent_coef * torch.stack(ents, -1).sum(-1)
+    return -torch.mean(disc[:-1] * (obj + ent.unsqueeze(-1)[:-1]))
+
+
+@pytest.mark.parametrize("heads,T,M", [((6,), 16, 1024), ((3, 5, 2), 16, 257), ((18,), 4, 64)])
+def test_actor_loss_kernel_matches_eager(heads, T, M):
+    torch.manual_seed(sum(heads) + T + M)
+    A = sum(heads)
+    dev = "cuda"
+    raw = torch.randn(T, M, A, device=dev) * 3
+    mixed = torch.cat([ops.reference.unimix_logits(z, z.shape[-1], 0.01) for z in torch.split(raw, heads, -1)], -1)
+    mixed = mixed.detach().requires_grad_(True)
+    idx = [torch.randint(0, h, (T, M), device=dev) for h in heads]
+    actions = torch.cat([F.one_hot(i, h).float() for i, h in zip(idx, heads)], -1)
+    lam = torch.randn(T - 1, M, 1, device=dev) * 10
+    base = torch.randn(T - 1, M, 1, device=dev) * 10
+    disc = torch.rand(T, M, 1, device=dev)
+    off = torch.tensor(-0.7, device=dev)
+    inv = torch.tensor(3.3, device=dev)
+    ent = 3e-4
+
+    ref = _eager_actor_loss(mixed, actions, lam, base, disc, off, inv, list(heads), ent)
+    (g_ref,) = torch.autograd.grad(ref, mixed)
+
+    z = mixed.detach().requires_grad_(True)
+    got = ops.actor_loss_discrete(z, actions, lam.reshape(T - 1, M), base.reshape(T - 1, M), disc.reshape(T, M), off, inv,
+                                  heads, ent)
+    assert got is not None
+    (got * 2.0).backward()
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(z.grad, 2.0 * g_ref, rtol=1e-4, atol=1e-8)
+    assert torch.all(z.grad[-1] == 0)
+
+
+def test_actor_loss_kernel_graph_capture():
+    T, M, heads = 8, 128, (4,)
+    dev = "cuda"
+    z = torch.randn(T, M, 4, device=dev, requires_grad=True)
+    actions = F.one_hot(torch.randint(0, 4, (T, M), device=dev), 4).float()
+    lam, base, disc = torch.randn(T - 1, M, device=dev), torch.randn(T - 1, M, device=dev), torch.rand(T, M, device=dev)
+    off, inv = torch.tensor(0.1, device=dev), torch.tensor(2.0, device=dev)
+
+    def step():
+        z.grad = None
+        loss = ops.actor_loss_discrete(z, actions, lam, base, disc, off, inv, heads, 1e-3)
+        loss.backward()
+        return loss
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step()
+    torch.cuda.current_stream().wait_stream(s)
+    eager_loss = step().detach().clone()
+    eager_grad = z.grad.clone()
+    z.grad = torch.zeros_like(z)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        loss = ops.actor_loss_discrete(z, actions, lam, base, disc, off, inv, heads, 1e-3)
+        (gz,) = torch.autograd.grad(loss, z)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(loss, eager_loss) and torch.equal(gz, eager_grad)
