@@ -9,7 +9,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tra
 rc=$?
 tail -1 gpurun_out/trace.log
 f=$(find gpurun_out/trace -name "*kernel_trace.csv" | head -1)
-[ -n "$f" ] && python scripts/trace_window.py "$f" $STEPS 45 > gpurun_out/trace_summary.md
+[ -n "$f" ] && python scripts/trace_window.py "$f" $STEPS ${TOP:-45} > gpurun_out/trace_summary.md
 rm -f gpurun_out/trace/*kernel_trace.csv
 head -3 gpurun_out/trace_summary.md
 exit $rc

@@ -7,6 +7,16 @@ import csv
 import sys
 
 
+CATS = [
+    ("rssm scan (persistent)", ["scanp::"]),
+    ("conv (srl igemm/wgrad)", ["srl::conv::"]),
+    ("library GEMM (hipBLASLt/rocBLAS)", ["Cijk_", "gemm"]),
+    ("layernorm / LN-GRU", ["ln_wave", "ln_gru", "layer_norm"]),
+    ("ATen elementwise / reduce / copy", ["at::native", "__amd_rocclr", "zero2_kernel"]),
+    ("srl other", ["srl::"]),
+]
+
+
 def main(path, steps, top=40):
     rows = list(csv.DictReader(open(path)))
     key_s, key_e = "Start_Timestamp", "End_Timestamp"
@@ -24,6 +34,15 @@ def main(path, steps, top=40):
     n = sum(a[1] for a in agg.values())
     print(f"timed window: {steps} steps, wall {(t1 - t0) / 1e6:.2f} ms ({(t1 - t0) / 1e6 / steps:.2f} ms/step), "
           f"kernel busy {busy / 1e6:.2f} ms ({busy / 1e6 / steps:.2f} ms/step), {n / steps:.0f} dispatches/step\n")
+    cats = collections.defaultdict(lambda: [0, 0])
+    for name, (d, c) in agg.items():
+        cat = next((k for k, pat in CATS if any(p in name for p in pat)), "other")
+        cats[cat][0] += d
+        cats[cat][1] += c
+    print("| category | ms/step | calls/step |\n|---|---:|---:|")
+    for k, (d, c) in sorted(cats.items(), key=lambda kv: -kv[1][0]):
+        print(f"| {k} | {d / 1e6 / steps:.3f} | {c / steps:.1f} |")
+    print()
     print("| ms/step | calls/step | avg us | % busy | kernel |\n|---:|---:|---:|---:|---|")
     for name, (d, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:top]:
         print(f"| {d / 1e6 / steps:.3f} | {c / steps:.1f} | {d / c / 1e3:.1f} | {100 * d / busy:.1f} | `{name[:95]}` |")

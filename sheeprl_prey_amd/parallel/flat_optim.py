@@ -140,6 +140,8 @@ class FlatOptimizer:
         computed gradient (AccumulateGrad steals the buffer: no per-parameter accumulate kernel), and
         the slab is rebuilt by ``_gather`` - one memset + multi-tensor copies - before anything reads
         it.  Otherwise the slab is zeroed and grads accumulate into it in place."""
+        if getattr(self, "_ov", None) is not None:
+            self.arm_overlap()
         if set_to_none:
             for p in self.params:
                 p.grad = None
@@ -181,7 +183,129 @@ class FlatOptimizer:
         self._advanced = True
         return norm
 
+    # ------------------------------------------------------------------ overlapped gradient all-reduce
+    def enable_overlap(self, group=None, world_size: int = 1, bucket_mb: float = 32) -> bool:
+        """Bucketed all-reduce overlapped with the backward (eager multi-rank paths).
+
+        The slab is cut into buckets from its tail (parameters are laid out in forward order, so
+        the backward produces the tail first).  A post-accumulate-grad hook per parameter moves its
+        fresh gradient into the slab and, once every parameter of a bucket has reported, launches
+        that bucket's async all-reduce while autograd keeps computing earlier layers.  Buckets are
+        launched strictly in index order, so every rank issues the same collective sequence
+        whatever the hook order.  Hooks act only between ``arm_overlap()`` and the following
+        ``all_reduce_grads`` (``Runner.backward`` / ``Runner.sync_gradients`` pair them), so extra
+        backward passes that accumulate into the same slab never trigger a collective.  Contract: ONE
+        backward between ``zero_grad`` (which arms) and the sync, as every algorithm here does.
+        Reference counterpart: the per-model DDP reducers of ``dreamer_v3/agent.py:1054-1063``."""
+        if world_size <= 1 or getattr(self, "_ov", None) is not None:
+            return getattr(self, "_ov", None) is not None
+        if self.flat_grad._base is not None or any(
+                getattr(p, "_flat_slab", (None,))[0] is not None and p._flat_slab[0]() is not self for p in self.params):
+            return False  # slab shared with another optimiser: keep the plain path
+        cap = max(_ALIGN, int(bucket_mb * (1 << 20) // 4))
+        buckets: List[List[int]] = []  # param indices, tail first
+        cur, size = [], 0
+        for i in reversed(range(len(self.params))):
+            cur.append(i)
+            size += _aligned(self.params[i].numel())
+            if size >= cap:
+                buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            buckets.append(cur)
+        ranges = []
+        for b in buckets:
+            lo = min(self.offsets[i] for i in b)
+            hi = max(self.offsets[i] + _aligned(self.params[i].numel()) for i in b)
+            ranges.append((lo, hi))
+        bucket_of = {}
+        for bi, b in enumerate(buckets):
+            for i in b:
+                bucket_of[i] = bi
+        g = self.flat_grad
+        use_avg = g.is_cuda and dist.get_backend(group) == "nccl"
+        self._ov = dict(group=group, ws=world_size, buckets=buckets, ranges=ranges, bucket_of=bucket_of,
+                        op=dist.ReduceOp.AVG if use_avg else dist.ReduceOp.SUM, avg=use_avg, armed=False,
+                        pending=[], seen=[], works=[], next=0)
+        self._ov_handles = [p.register_post_accumulate_grad_hook(self._make_ov_hook(i)) for i, p in enumerate(self.params)]
+        return True
+
+    def _make_ov_hook(self, i: int):
+        ref = weakref.ref(self)
+
+        def hook(p: Tensor) -> None:
+            self_ = ref()
+            # inside a hipGraph capture (segmented multi-rank graphs) the collectives stay between replays
+            if self_ is not None and self_._ov["armed"] and not (p.is_cuda and torch.cuda.is_current_stream_capturing()):
+                self_._ov_ready(i, p)
+
+        return hook
+
+    def arm_overlap(self) -> None:
+        """Start a new gradient round (``zero_grad`` calls this).  A round that launched buckets and
+        was never synced (no ``all_reduce_grads``) is drained and dropped - every rank does the same."""
+        ov = getattr(self, "_ov", None)
+        if ov is None:
+            return
+        for w in ov["works"]:
+            w.wait()
+        ov.update(armed=True, pending=[len(b) for b in ov["buckets"]], seen=[False] * len(self.params), works=[], next=0)
+
+    def _ov_view(self, i: int) -> Tensor:
+        p = self.params[i]
+        return self.flat_grad[self.offsets[i] : self.offsets[i] + p.numel()].view_as(p)
+
+    def _ov_ready(self, i: int, p: Tensor) -> None:
+        ov = self._ov
+        if ov["seen"][i]:
+            return
+        v = self._ov_view(i)
+        g = p.grad
+        if g is not None and g.data_ptr() != v.data_ptr():
+            v.copy_(g)
+            p.grad = v
+        elif g is None:
+            v.zero_()
+            p.grad = v
+        ov["seen"][i] = True
+        b = ov["bucket_of"][i]
+        ov["pending"][b] -= 1
+        self._ov_launch_ready()
+
+    def _ov_launch_ready(self) -> None:
+        ov = self._ov
+        while ov["next"] < len(ov["buckets"]) and ov["pending"][ov["next"]] == 0:
+            lo, hi = ov["ranges"][ov["next"]]
+            ov["works"].append(dist.all_reduce(self.flat_grad[lo:hi], op=ov["op"], group=ov["group"], async_op=True))
+            ov["next"] += 1
+
+    def _ov_finish(self) -> None:
+        ov = self._ov
+        # parameters that got no gradient in this backward: a zero slab view (set_to_none) or the
+        # accumulated one already there
+        for i, p in enumerate(self.params):
+            if not ov["seen"][i]:
+                v = self._ov_view(i)
+                if self._detached or p.grad is None:
+                    v.zero_()
+                elif p.grad.data_ptr() != v.data_ptr():
+                    v.copy_(p.grad)
+                p.grad = v
+                ov["seen"][i] = True
+                ov["pending"][ov["bucket_of"][i]] -= 1
+        self._detached = False
+        self._ov_launch_ready()
+        for w in ov["works"]:
+            w.wait()
+        ov.update(armed=False, works=[])
+        if not ov["avg"]:
+            self.flat_grad.div_(ov["ws"])
+
     def all_reduce_grads(self, group=None, world_size: int = 1, bucket_mb: int = 32) -> None:
+        ov = getattr(self, "_ov", None)
+        if ov is not None and ov["armed"]:
+            self._ov_finish()
+            return
         self._gather()
         if world_size <= 1:
             return

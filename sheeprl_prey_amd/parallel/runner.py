@@ -155,8 +155,9 @@ class Runner:
         loggers: Optional[Sequence[Any]] = None,
         cuda_graphs: bool = False,
         fused_ops: bool = True,
-        bucket_mb: int = 32,
+        bucket_mb: float = 32,
         tunable_gemm: str = "use",
+        overlap_grad_sync: bool = True,
         process_group=None,
         **_unused,
     ) -> None:
@@ -173,13 +174,15 @@ class Runner:
         self._loggers = list(loggers or [])
         self.cuda_graphs = bool(cuda_graphs) and self.accelerator == "cuda"
         self.fused_ops = bool(fused_ops)
-        self.bucket_mb = int(bucket_mb)
+        self.bucket_mb = float(bucket_mb)
+        # bucketed all-reduce launched from backward hooks (FlatOptimizer.enable_overlap)
+        self.overlap_grad_sync = bool(overlap_grad_sync)
         # library-GEMM solution choice (parallel/gemm_tuning.py): committed TunableOp results
         self.tunable_gemm = str(tunable_gemm)
         self._kwargs = dict(
             devices=devices, num_nodes=num_nodes, strategy=strategy, accelerator=accelerator,
             precision=precision, callbacks=callbacks, cuda_graphs=cuda_graphs, fused_ops=fused_ops, bucket_mb=bucket_mb,
-            tunable_gemm=tunable_gemm,
+            tunable_gemm=tunable_gemm, overlap_grad_sync=overlap_grad_sync,
         )
         self.group = process_group  # None == WORLD
         if str(strategy).lower() in ("fsdp",):
@@ -356,6 +359,9 @@ class Runner:
 
         if isinstance(optimizer, FlatOptimizer):
             optimizer.all_reduce_grads(self.group, self.world_size, bucket_mb=self.bucket_mb)
+            if self.overlap_grad_sync:
+                # from the next zero_grad on, buckets launch from the backward hooks (same call on every rank)
+                optimizer.enable_overlap(self.group, self.world_size, bucket_mb=self.bucket_mb)
             return
         grads = [p.grad for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
         if not grads:

@@ -79,3 +79,56 @@ def test_two_rank_step_equals_full_batch_step(tmp_path):
     low, invscale = m(lam)
     low2, invscale2 = m(lam * 2.0)
     torch.testing.assert_close(r0["moments"], torch.stack([low, invscale, low2, invscale2]))
+
+
+class _WithUnused(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        # never in the loss: head of the slab = the last bucket, completed by the sync itself
+        self.unused = torch.nn.Linear(5, 5)
+        self.body = _model()
+
+    def forward(self, x):
+        return self.body(x)
+
+
+def _overlap_rank_fn(runner: Runner, out_dir: str) -> None:
+    overlap = runner.overlap_grad_sync
+    rank, ws = runner.global_rank, runner.world_size
+    x, y = _data()
+    half = BATCH // ws
+    sl = slice(rank * half, (rank + 1) * half)
+    torch.manual_seed(0)
+    model = _WithUnused()
+    opt = FlatAdam(model.parameters(), lr=1e-2)
+    launched_in_backward = []
+    for s in range(STEPS):
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(model(x[s, sl]), y[s, sl]).backward()
+        ov = getattr(opt, "_ov", None)
+        launched_in_backward.append(ov["next"] if ov is not None and ov["armed"] else 0)
+        runner.sync_gradients(opt)
+        opt.step()
+    params = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    torch.save({"params": params, "launched": torch.tensor(launched_in_backward),
+                "buckets": torch.tensor(len(opt._ov["buckets"]) if getattr(opt, "_ov", None) else 0)},
+               os.path.join(out_dir, f"{'ov' if overlap else 'plain'}{rank}.pt"))
+
+
+@pytest.mark.timeout(300)
+def test_overlapped_bucket_all_reduce_matches_plain(tmp_path):
+    """Bucketed all-reduce launched from post-accumulate-grad hooks during the backward
+    (``FlatOptimizer.enable_overlap``) gives the same replicas as the all-reduce after the backward,
+    including a parameter that never receives a gradient."""
+    for overlap in (False, True):
+        Runner(devices=2, accelerator="cpu", bucket_mb=0.0002, overlap_grad_sync=overlap).launch(
+            _overlap_rank_fn, str(tmp_path))
+    plain = [torch.load(tmp_path / f"plain{r}.pt", weights_only=True) for r in range(2)]
+    ov = [torch.load(tmp_path / f"ov{r}.pt", weights_only=True) for r in range(2)]
+    assert torch.equal(ov[0]["params"], ov[1]["params"])
+    assert torch.equal(ov[0]["params"], plain[0]["params"])
+    # step 0 syncs on the plain path and enables the hooks; later steps launch buckets mid-backward
+    # 52-float buckets: 4 of them, the 3 of the used layers launched before the backward returned
+    assert int(ov[0]["buckets"]) == 4
+    assert ov[0]["launched"].tolist() == [0] + [3] * (STEPS - 1)
+    assert int(plain[0]["buckets"]) == 0
