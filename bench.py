@@ -54,8 +54,19 @@ def parse():
                    help="diagnostic: run N untimed steps, report the first non-finite train output per step")
     p.add_argument("--gemm-tuning", default=None, choices=["use", "tune", "off"],
                    help="library-GEMM TunableOp mode (default: fabric.tunable_gemm = use the committed results)")
+    p.add_argument("--xl", action="store_true",
+                   help="dreamer_v3: the XL model of exp=dreamer_v3_XL_crafter (dense 1024, mlp 5, cnn mult 96, "
+                        "deter 4096, hidden 1024) on the synthetic 64x64 env")
     p.add_argument("overrides", nargs="*")
     return p.parse_args()
+
+
+# model dimensions of the reference's configs/exp/dreamer_v3_XL_crafter.yaml:35-47
+XL_OVERRIDES = [
+    "algo.dense_units=1024", "algo.mlp_layers=5", "algo.world_model.encoder.cnn_channels_multiplier=96",
+    "algo.world_model.recurrent_model.recurrent_state_size=4096", "algo.world_model.transition_model.hidden_size=1024",
+    "algo.world_model.representation_model.hidden_size=1024",
+]
 
 
 def main():
@@ -90,7 +101,8 @@ def main():
         "exp=dreamer_v3_100k_ms_pacman", "env=synthetic_atari", "env.sync_env=True",
         "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]", "fabric.accelerator=cuda",
         f"fabric.cuda_graphs={not args.no_graphs}", "metric.log_every=1000000000",
-    ] + ([f"fabric.tunable_gemm={args.gemm_tuning}"] if args.gemm_tuning else []) + list(args.overrides)
+    ] + ([f"fabric.tunable_gemm={args.gemm_tuning}"] if args.gemm_tuning else []) + (XL_OVERRIDES if args.xl else []) + list(
+        args.overrides)
     cfg = dotdict(compose(overrides))
     cfg.pop("hydra", None)
     runner = Runner(**{k: v for k, v in cfg.fabric.items()})
@@ -225,7 +237,8 @@ def main():
     env_steps_per_s = policy_steps * cfg.env.action_repeat / elapsed
     if rank == 0:
         rec = {
-            "metric": "env-steps/sec (whole node) DreamerV3 Atari-100k 64x64",
+            "metric": ("env-steps/sec (whole node) DreamerV3-XL 64x64" if args.xl
+                       else "env-steps/sec (whole node) DreamerV3 Atari-100k 64x64"),
             "value": round(env_steps_per_s, 3),
             "unit": "env_steps/s (policy steps x action_repeat=4, whole job)",
             "n_gpus": world,
@@ -238,7 +251,9 @@ def main():
             "dtype": "fp32",
             "data": "synthetic (Atari-shaped 64x64x3 uint8 env, MsPacman action set; random-init weights)",
             "config": {
-                "model": "DreamerV3 Atari-100k (dense 512, mlp 2, cnn mult 32, deter 512, stoch 32x32, bins 255)",
+                "model": ("DreamerV3-XL (dense 1024, mlp 5, cnn mult 96, deter 4096, hidden 1024, stoch 32x32, bins 255)"
+                          if args.xl else
+                          "DreamerV3 Atari-100k (dense 512, mlp 2, cnn mult 32, deter 512, stoch 32x32, bins 255)"),
                 "global_batch": cfg.per_rank_batch_size * world,
                 "seq_len": cfg.per_rank_sequence_length,
                 "horizon": cfg.algo.horizon,

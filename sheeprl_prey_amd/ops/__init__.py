@@ -509,3 +509,33 @@ def actor_loss_discrete(z: Tensor, actions: Tensor, lam: Tensor, base: Tensor, d
         return None
     return _ActorLossDiscrete.apply(z, actions.detach(), lam.detach(), base.detach(), disc.detach(), offset.detach(),
                                     invscale.detach(), tuple(int(h) for h in heads), float(ent_coef))
+
+
+# =============================================================== skinny weight-streaming GEMM
+def skinny_ok(A: Tensor, W: Tensor) -> bool:
+    """Shape/alignment gate of ``skinny_nt`` (M <= 16 rows, K % 128, N % 128, 16-byte strides)."""
+    if not (_native(A) and A.dtype == torch.float32 and W.dtype == torch.float32 and A.dim() in (2, 3)
+            and W.dim() == A.dim() and A.stride(-1) == 1 and W.stride(-1) == 1):
+        return False
+    M, K = A.shape[-2:]
+    N = W.shape[-2]
+    if not (1 <= M <= 16 and K % 128 == 0 and N % 128 == 0 and W.shape[-1] == K):
+        return False
+    strides = [A.stride(-2), W.stride(-2)] + ([A.stride(0), W.stride(0)] if A.dim() == 3 else [])
+    return all(s % 4 == 0 for s in strides) and A.data_ptr() % 16 == 0 and W.data_ptr() % 16 == 0
+
+
+def skinny_nt(A: Tensor, W: Tensor, out: Tensor, add: Optional[Tensor] = None) -> bool:
+    """``out = A @ W^T (+ add)`` for a few activation rows against a large weight (``csrc/skinny.hip``:
+    split-K weight streaming at HBM rate).  Batched when A / W / out are 3-D.  Returns False (nothing
+    done) when the shapes are outside the kernel's gate - the caller keeps its library GEMM."""
+    if not skinny_ok(A, W) or out.stride(-1) != 1 or out.data_ptr() % 16 or out.stride(-2) % 4:
+        return False
+    if add is not None and (add.stride(-1) != 1 or add.data_ptr() % 16 or (add.shape[-2] > 1 and add.stride(-2) % 4)):
+        return False
+    C = _ext()
+    Z = A.shape[0] if A.dim() == 3 else 1
+    need = C.skinny_workspace(W.shape[-2], A.shape[-1], Z)
+    part = torch.empty(need, device=A.device, dtype=torch.float32) if need else None
+    C.skinny_nt(A, W, out, add, part)
+    return True

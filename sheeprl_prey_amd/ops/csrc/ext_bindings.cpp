@@ -21,6 +21,9 @@ void natcnn_dgrad(const float* dy, const float* y, const float* w, float* dcol, 
 void launch_moments(const float* x, int n, int r0, int r1, int r2, int r3, float frac_lo, float frac_hi, float decay,
                     float om, float inv_max, float* low, float* high, float* inv, hipStream_t st);
 
+int skinny_plan(int N, int K, int Z, int* kc);
+void launch_skinny_nt(const float* A, long lda, long sA, const float* W, long ldw, long sW, float* out, long ldo, long sO,
+                      const float* add, long ldadd, long sAdd, float* part, int M, int N, int K, int Z, hipStream_t st);
 int actor_loss_blocks(int rows);
 void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
@@ -242,7 +245,70 @@ std::vector<torch::Tensor> actor_loss_discrete(torch::Tensor z, torch::Tensor ac
   return {loss, dz};
 }
 
+// ------------------------------------------------------------------ skinny weight-streaming GEMM (skinny.hip)
+// out[z] = A[z] . W[z]^T (+ add[z]); A [Z, M<=16, K] (row stride free), W [Z, N, K] contiguous rows,
+// out [Z, M, N], add [Z, M or 1 (broadcast), N].  2-D operands are Z = 1.  Returns the workspace size
+// needed (floats) when `part` is undefined and nothing was launched.
+static void skinny_dims(const torch::Tensor& t, int64_t& Z, int64_t& R, int64_t& C, int64_t& ld, int64_t& sz) {
+  TORCH_CHECK(t.dim() == 2 || t.dim() == 3, "skinny_nt: 2-D or 3-D operands");
+  TORCH_CHECK(t.stride(-1) == 1, "skinny_nt: unit stride along the last dim");
+  Z = t.dim() == 3 ? t.size(0) : 1;
+  R = t.size(-2);
+  C = t.size(-1);
+  ld = t.stride(-2);
+  sz = t.dim() == 3 ? t.stride(0) : 0;
+}
+
+int64_t skinny_nt(torch::Tensor A, torch::Tensor W, torch::Tensor out, c10::optional<torch::Tensor> add,
+                  c10::optional<torch::Tensor> part) {
+  int64_t Za, M, K, lda, sA, Zw, N, Kw, ldw, sW, Zo, Mo, No, ldo, sO;
+  skinny_dims(A, Za, M, K, lda, sA);
+  skinny_dims(W, Zw, N, Kw, ldw, sW);
+  skinny_dims(out, Zo, Mo, No, ldo, sO);
+  TORCH_CHECK(Za == Zw && Za == Zo && K == Kw && Mo == M && No == N, "skinny_nt: shape mismatch");
+  TORCH_CHECK(M >= 1 && M <= 16 && K % 128 == 0 && N % 128 == 0, "skinny_nt: M <= 16, K % 128 == 0, N % 128 == 0");
+  for (auto* t : {&A, &W, &out}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32, "skinny_nt: fp32 CUDA operands");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "skinny_nt: 16-byte aligned operands");
+  }
+  TORCH_CHECK(lda % 4 == 0 && ldw % 4 == 0 && ldo % 4 == 0 && sA % 4 == 0 && sW % 4 == 0 && sO % 4 == 0,
+              "skinny_nt: strides must be multiples of 4 floats");
+  const float* addp = nullptr;
+  int64_t ldadd = 0, sAdd = 0;
+  if (add.has_value() && add->defined()) {
+    int64_t Zd, Md, Nd;
+    skinny_dims(*add, Zd, Md, Nd, ldadd, sAdd);
+    TORCH_CHECK(Nd == N && (Md == M || Md == 1) && (Zd == Za || add->dim() == 2), "skinny_nt: addend shape");
+    TORCH_CHECK(add->scalar_type() == torch::kFloat32 && reinterpret_cast<uintptr_t>(add->data_ptr()) % 16 == 0 &&
+                    ldadd % 4 == 0 && sAdd % 4 == 0, "skinny_nt: addend fp32, 16-byte aligned");
+    if (Md == 1) ldadd = 0;
+    addp = add->data_ptr<float>();
+  }
+  int kc = 0;
+  const int splits = skinny_plan((int)N, (int)K, (int)Za, &kc);
+  const int64_t need = splits > 1 ? (int64_t)splits * Za * 16 * N : 0;
+  float* pp = nullptr;
+  if (need) {
+    if (!part.has_value() || !part->defined()) return need;
+    TORCH_CHECK(part->numel() >= need && part->scalar_type() == torch::kFloat32 && part->is_contiguous(),
+                "skinny_nt: workspace too small");
+    pp = part->data_ptr<float>();
+  }
+  launch_skinny_nt(A.data_ptr<float>(), lda, sA, W.data_ptr<float>(), ldw, sW, out.data_ptr<float>(), ldo, sO, addp, ldadd,
+                   sAdd, pp, (int)M, (int)N, (int)K, (int)Za, stream());
+  return 0;
+}
+
+int64_t skinny_workspace(int64_t N, int64_t K, int64_t Z) {
+  int kc = 0;
+  const int splits = skinny_plan((int)N, (int)K, (int)Z, &kc);
+  return splits > 1 ? (int64_t)splits * Z * 16 * N : 0;
+}
+
 void register_ext(pybind11::module& m) {
+  m.def("skinny_nt", &skinny_nt, pybind11::arg("A"), pybind11::arg("W"), pybind11::arg("out"),
+        pybind11::arg("add") = pybind11::none(), pybind11::arg("part") = pybind11::none());
+  m.def("skinny_workspace", &skinny_workspace);
   m.def("actor_loss_discrete", &actor_loss_discrete);
   m.def("moments_update", &moments_update);
   m.def("nc_conv_fwd", &nc_conv_fwd);

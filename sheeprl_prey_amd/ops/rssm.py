@@ -13,6 +13,10 @@ backward, per step (9 launches): the adjoint chain only (activation gradients);
 after the loop every weight gradient is ONE large GEMM over the stacked T*B rows and every LayerNorm
 parameter gradient ONE column reduction over per-step partial slots.
 
+Large recurrent states (XL, deter 4096: ~300 MB of weights per step for 16 rows) route every per-step
+GEMM by size (``_nt``): ``skinny.hip`` split-K streaming for the smaller weights, the library's NT
+kernels for the GRU weight, with transposed weight copies for the adjoint GEMMs.
+
 The step-invariant work (action half of the recurrent input layer, embedding half of the posterior
 layer) is hoisted by the caller (``RSSM.scan_dynamic``) and enters as ``a_proj`` / ``P`` inputs, so
 autograd handles their (large, efficient) GEMM backward.
@@ -26,6 +30,38 @@ import torch
 from torch import Tensor
 
 from sheeprl_prey_amd.ops.reference import ACTS
+
+
+def _use_skinny(B: int, H: int) -> bool:
+    """Large recurrent states (XL: deter 4096): the per-step GEMMs take a weight-streaming route."""
+    return B <= 16 and H >= 1024 and os.environ.get("SRL_SKINNY", "1") != "0"
+
+
+# Measured on MI355X (scripts/skinny_sweep.py, 16 rows): hipBLASLt's NT kernels stream the big GRU
+# weight at ~6.4 TB/s (16x12288x5120: 39 us) against 4.5 TB/s for skinny.hip, while skinny.hip wins
+# below ~16 M weights (16x2048x4096: 13.8 us vs 17.7 us).  Route by size; the adjoint GEMMs use a
+# transposed weight copy so they also run in the fast NT layout (16x5120x12288 A.W: 76 -> 42 us).
+_SKINNY_MAX_WEIGHTS = 16 * 1024 * 1024
+
+
+def _nt(A: Tensor, W: Tensor, out: Tensor, add: Tensor = None) -> None:
+    """out = A @ W^T (+ add) for few rows against a large row-major weight W."""
+    from sheeprl_prey_amd.ops import skinny_nt
+
+    if W.shape[-2] * W.shape[-1] <= _SKINNY_MAX_WEIGHTS and skinny_nt(A, W, out, add):
+        return
+    Wt = W.transpose(-1, -2)
+    if A.dim() == 3:
+        if add is None:
+            torch.bmm(A, Wt, out=out)
+        else:
+            torch.baddbmm(add, A, Wt, out=out)
+    elif add is None:
+        torch.mm(A, Wt, out=out)
+    elif add.data_ptr() == out.data_ptr():
+        out.addmm_(A, Wt)
+    else:
+        torch.addmm(add, A, Wt, out=out)
 
 
 class RSSMScanFn(torch.autograd.Function):
@@ -59,17 +95,32 @@ class RSSMScanFn(torch.autograd.Function):
         mixed = torch.empty(T, 2, B, S, device=dev, dtype=f32)
         samples = torch.empty(T, 2, B, S, device=dev, dtype=f32)
         Wz_t, Wg_t, W1_t, W2_t = Wz.t(), Wg.t(), W1.t(), W2.transpose(1, 2)
+        # XL shapes: split-K weight streaming instead of the library's skinny GEMMs (False -> library)
+        sk = _use_skinny(B, H)
+        Wzc = Wz.contiguous() if sk else None
         h_prev = None
         z_prev = None
         for t in range(T):
             C.rssm_mask_fwd(h_prev, H, z_prev, first[t], z0, cat[t], HD, zm[t], B, H, S)
-            torch.addmm(a_proj[t], zm[t], Wz_t, out=xr[t])
+            if sk:
+                _nt(zm[t], Wzc, xr[t], a_proj[t])
+            else:
+                torch.addmm(a_proj[t], zm[t], Wz_t, out=xr[t])
             C.ln_act_fwd_into(xr[t], D, cat[t, :, H:], HD, ln1_w, ln1_b, m1[t], r1[t], B, D, 1, eps1, act1)
-            torch.mm(cat[t], Wg_t, out=gx[t])
+            if sk:
+                _nt(cat[t], Wg, gx[t])
+            else:
+                torch.mm(cat[t], Wg_t, out=gx[t])
             C.ln_gru_fwd_into(gx[t], cat[t], HD, lng_w, lng_b, hs[t], mg[t], rg[t], B, H, epsg)
-            torch.addmm(P[t], hs[t], W1_t, out=u[t])
+            if sk:
+                _nt(hs[t], W1, u[t], P[t])
+            else:
+                torch.addmm(P[t], hs[t], W1_t, out=u[t])
             C.ln_act_fwd_into(u[t], hid, v[t], hid, ln2_w, ln2_b, m2[t], r2[t], 2 * B, hid, 2, eps2, act2)
-            torch.baddbmm(b2, v[t], W2_t, out=logits[t])
+            if sk:
+                _nt(v[t], W2, logits[t], b2)
+            else:
+                torch.baddbmm(b2, v[t], W2_t, out=logits[t])
             C.unimix_sample_fwd_into(logits[t], uniform[t], mixed[t], samples[t], disc, alpha)
             h_prev = hs[t]
             z_prev = samples[t, 1]
@@ -118,19 +169,35 @@ class RSSMScanFn(torch.autograd.Function):
         p2b = torch.empty_like(p2g)
         pgg = torch.empty(T, gg, 3 * H, device=dev, dtype=f32)
         pgb = torch.empty_like(pgg)
+        sk = _use_skinny(B, H)
+        if sk:  # the adjoint GEMMs stream W^T: one transposed copy of each weight per backward
+            WzT, WgT, W1T, W2T = (Wz.t().contiguous(), Wg.t().contiguous(), W1.t().contiguous(),
+                                  W2.transpose(1, 2).contiguous())
         for t in range(T - 1, -1, -1):
             C.unimix_sample_bwd_into(logits[t], dmixed[t], dsamp[t], dlog[t], disc, alpha)
-            torch.bmm(dlog[t], W2, out=dv[t])
+            if sk:
+                _nt(dlog[t], W2T, dv[t])
+            else:
+                torch.bmm(dlog[t], W2, out=dv[t])
             C.ln_act_bwd_into(u[t], hid, dv[t], hid, du[t], hid, ln2_w, ln2_b, m2[t], r2[t], p2g[t], p2b[t], None, None,
                               2 * B, hid, 2, act2)
-            DH[t].addmm_(du[t], W1)
+            if sk:
+                _nt(du[t], W1T, DH[t], DH[t])
+            else:
+                DH[t].addmm_(du[t], W1)
             C.ln_gru_bwd_into(gx[t], cat[t], HD, lng_w, lng_b, mg[t], rg[t], DH[t], dgx[t], dhp, pgg[t], pgb[t], None, None,
                               B, H)
-            torch.mm(dgx[t], Wg, out=dcat)
+            if sk:
+                _nt(dgx[t], WgT, dcat)
+            else:
+                torch.mm(dgx[t], Wg, out=dcat)
             C.ln_act_bwd_into(xr[t], D, dcat[:, H:], HD, dx[t], D, ln1_w, ln1_b, m1[t], r1[t], p1g[t], p1b[t], None, None,
                               B, D, 1, act1)
             if t > 0:
-                torch.mm(dx[t], Wz, out=dzp)
+                if sk:
+                    _nt(dx[t], WzT, dzp)
+                else:
+                    torch.mm(dx[t], Wz, out=dzp)
                 C.rssm_mask_bwd(dhp, H, dcat, HD, dzp, first[t], DH[t - 1], dsamp[t - 1, 1], B, H, S)
         TB = T * B
         # ---- batched weight gradients: one GEMM / one reduction each

@@ -85,7 +85,14 @@ def test_fused_rssm_scan_full_shape_T64(impl):
     _check_scan_vs_python(512, 512, 512, 16, 64, impl, tol=(5e-3, 5e-4), gtol=(5e-3, 5e-3))
 
 
-def _check_scan_vs_python(H, D, hid, B, T, impl, tol=(2e-3, 2e-4), gtol=(3e-3, 3e-3)):
+def test_fused_rssm_scan_xl_shape():
+    """DreamerV3-XL recurrent shape (deter 4096, dense 1024, hidden 1024; reference
+    ``configs/exp/dreamer_v3_XL_crafter.yaml``): beyond the register/LDS-resident scans, the
+    per-step scan with the skinny split-K weight-streaming GEMMs, fwd + bwd vs the python loop."""
+    _check_scan_vs_python(4096, 1024, 1024, 16, 6, "persist", tol=(5e-3, 5e-4), gtol=(5e-3, 5e-3), expect="scan9")
+
+
+def _check_scan_vs_python(H, D, hid, B, T, impl, tol=(2e-3, 2e-4), gtol=(3e-3, 3e-3), expect=None):
     import copy
 
     from sheeprl_prey_amd.algos.dreamer_v3.agent import RSSM, RecurrentModel, init_weights
@@ -113,12 +120,12 @@ def _check_scan_vs_python(H, D, hid, B, T, impl, tol=(2e-3, 2e-4), gtol=(3e-3, 3
     e1, e2 = emb.clone().requires_grad_(), emb.clone().requires_grad_()
     out1 = rssm.scan_dynamic(e1, act, first, uniform=uni)
     out2 = rssm_ref.scan_dynamic(e2, act, first, uniform=uni_post)
-    fn = {"persist": "RSSMPersistFnBackward", "scan4": "RSSMScan4FnBackward", "scan9": "RSSMScanFnBackward"}[impl]
+    fn = {"persist": "RSSMPersistFnBackward", "scan4": "RSSMScan4FnBackward", "scan9": "RSSMScanFnBackward"}[expect or impl]
     assert type(out1[0].grad_fn).__name__ == fn
     names = ["h", "post", "post_logits", "prior_logits"]
     for n, a, b in zip(names, out1, out2):
         torch.testing.assert_close(a, b, rtol=tol[0], atol=tol[1], msg=lambda m: f"{n}: {m}")
-    sync = out1[0].grad_fn.saved_tensors[34] if impl == "persist" else None  # hand-off counters + error word
+    sync = out1[0].grad_fn.saved_tensors[34] if (expect or impl) == "persist" else None  # hand-off counters + error word
     gs = [torch.randn_like(o) for o in out1]
     sum((o * g).sum() for o, g in zip(out1, gs)).backward()
     sum((o * g).sum() for o, g in zip(out2, gs)).backward()
