@@ -151,6 +151,11 @@ class SACAgent(nn.Module):
     @torch.no_grad()
     def get_next_target_q_values(self, next_obs: Tensor, rewards: Tensor, dones: Tensor, gamma: float) -> Tensor:
         next_actions, next_logp = self.get_actions_and_log_probs(next_obs)
+        # both target critics, the min, the entropy term and the Bellman target: one kernel (K15)
+        y = ops.sac_twin_q_target(self.critic_target.model, next_obs, next_actions, next_logp, rewards, dones,
+                                  self.log_alpha, gamma)
+        if y is not None:
+            return y
         q_next = self.get_target_q_values(next_obs, next_actions)
         min_q = torch.min(q_next, dim=-1, keepdim=True)[0] - self.alpha_t * next_logp
         return rewards + (1 - dones) * gamma * min_q

@@ -539,3 +539,26 @@ def skinny_nt(A: Tensor, W: Tensor, out: Tensor, add: Optional[Tensor] = None) -
     part = torch.empty(need, device=A.device, dtype=torch.float32) if need else None
     C.skinny_nt(A, W, out, add, part)
     return True
+
+
+# =============================================================== SAC twin-Q target (K15)
+def sac_twin_q_target(ens, obs: Tensor, act: Tensor, logp: Tensor, rewards: Tensor, dones: Tensor, log_alpha: Tensor,
+                      gamma: float) -> Optional[Tensor]:
+    """``r + (1 - d) * gamma * (min_c Q'_c(s', a') - alpha * logp)`` for an ``EnsembleMLP`` target critic
+    (2 ReLU hidden layers, scalar head, no dropout / LayerNorm) in one kernel (``csrc/sac_target.hip``).
+    None when the critic or the tensors are outside the kernel's gate (the caller keeps the eager path)."""
+    if not (_native(obs) and obs.dtype == torch.float32 and act.dtype == torch.float32 and obs.dim() == 2):
+        return None
+    if ens.norms is not None or (ens.dropout > 0 and ens.training) or ens.act_name != "relu" or len(ens.layers) != 2:
+        return None
+    if ens.head is None or ens.head.out_features != 1 or ens.layers[0].bias is None or ens.layers[1].bias is None:
+        return None
+    H = ens.layers[0].out_features
+    if not (1 <= ens.n <= 4 and H % 128 == 0 and H <= 512 and ens.layers[1].out_features == H
+            and obs.shape[1] + act.shape[1] <= 1024):
+        return None
+    l1, l2, hd = ens.layers[0], ens.layers[1], ens.head
+    return _ext().sac_twin_q_target(obs.contiguous(), act.contiguous(), logp.reshape(-1).contiguous(),
+                                    rewards.reshape(-1).contiguous().float(), dones.reshape(-1).contiguous().float(),
+                                    log_alpha.detach().reshape(-1), l1.weight.detach(), l1.bias.detach(),
+                                    l2.weight.detach(), l2.bias.detach(), hd.weight.detach(), hd.bias.detach(), float(gamma))

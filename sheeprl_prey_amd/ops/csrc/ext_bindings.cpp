@@ -24,6 +24,10 @@ void launch_moments(const float* x, int n, int r0, int r1, int r2, int r3, float
 int skinny_plan(int N, int K, int Z, int* kc);
 void launch_skinny_nt(const float* A, long lda, long sA, const float* W, long ldw, long sW, float* out, long ldo, long sO,
                       const float* add, long ldadd, long sAdd, float* part, int M, int N, int K, int Z, hipStream_t st);
+void launch_sac_target(const float* obs, const float* act, const float* logp, const float* rew, const float* done,
+                       const float* log_alpha, const float* W1, const float* b1, const float* W2, const float* b2,
+                       const float* W3, const float* b3, float* y, int M, int OD, int AD, int H, int n, float gamma,
+                       hipStream_t st);
 int actor_loss_blocks(int rows);
 void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
@@ -305,7 +309,29 @@ int64_t skinny_workspace(int64_t N, int64_t K, int64_t Z) {
   return splits > 1 ? (int64_t)splits * Z * 16 * N : 0;
 }
 
+// ------------------------------------------------------------------ SAC twin-Q target (sac_target.hip)
+torch::Tensor sac_twin_q_target(torch::Tensor obs, torch::Tensor act, torch::Tensor logp, torch::Tensor rew, torch::Tensor done,
+                                torch::Tensor log_alpha, torch::Tensor W1, torch::Tensor b1, torch::Tensor W2, torch::Tensor b2,
+                                torch::Tensor W3, torch::Tensor b3, double gamma) {
+  for (auto* t : {&obs, &act, &logp, &rew, &done, &log_alpha, &W1, &b1, &W2, &b2, &W3, &b3}) nc_check(*t, "sac_twin_q_target operand");
+  TORCH_CHECK(obs.dim() == 2 && act.dim() == 2 && obs.size(0) == act.size(0), "sac_twin_q_target: obs / act [M, *]");
+  const int64_t M = obs.size(0), OD = obs.size(1), AD = act.size(1);
+  TORCH_CHECK(logp.numel() == M && rew.numel() == M && done.numel() == M && log_alpha.numel() >= 1, "sac_twin_q_target: [M] terms");
+  TORCH_CHECK(W1.dim() == 3 && W1.size(2) == OD + AD, "sac_twin_q_target: W1 [n, H, obs+act]");
+  const int64_t n = W1.size(0), H = W1.size(1);
+  TORCH_CHECK(n >= 1 && n <= 4 && H % 128 == 0 && H <= 512 && OD + AD <= 1024, "sac_twin_q_target: n <= 4, H % 128 == 0, H <= 512");
+  TORCH_CHECK(b1.numel() == n * H && W2.numel() == n * H * H && b2.numel() == n * H && W3.numel() == n * H && b3.numel() == n,
+              "sac_twin_q_target: layer shapes");
+  auto y = torch::empty({M, 1}, obs.options());
+  launch_sac_target(obs.data_ptr<float>(), act.data_ptr<float>(), logp.data_ptr<float>(), rew.data_ptr<float>(),
+                    done.data_ptr<float>(), log_alpha.data_ptr<float>(), W1.data_ptr<float>(), b1.data_ptr<float>(),
+                    W2.data_ptr<float>(), b2.data_ptr<float>(), W3.data_ptr<float>(), b3.data_ptr<float>(), y.data_ptr<float>(),
+                    (int)M, (int)OD, (int)AD, (int)H, (int)n, (float)gamma, stream());
+  return y;
+}
+
 void register_ext(pybind11::module& m) {
+  m.def("sac_twin_q_target", &sac_twin_q_target);
   m.def("skinny_nt", &skinny_nt, pybind11::arg("A"), pybind11::arg("W"), pybind11::arg("out"),
         pybind11::arg("add") = pybind11::none(), pybind11::arg("part") = pybind11::none());
   m.def("skinny_workspace", &skinny_workspace);
