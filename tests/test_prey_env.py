@@ -122,3 +122,25 @@ def test_dreamer_v3_prey_preset_and_evaluate():
     rets = evaluate(str(ck), ["env.env_type=test"], episodes=2, render=True)
     assert len(rets) == 2
     assert list((ck.parent / "eval_videos").glob("*.gif"))
+
+
+def test_observation_and_reward_contract_of_reference_step():
+    """Pins the per-step contract of the reference ``prey_env/envs/gymnasium_env_bins.py:152-232``:
+    obs = [prey x, y, theta, speed, turning, predator x, y, theta (-1, -1, 0 when not visible),
+    3 x (distance, angle) of the nearest occlusions]; reward = -|prey - (1, 0.5)| off the goal."""
+    env = PreyEnv()
+    o, _ = env.reset(seed=3)
+    rng = np.random.default_rng(0)
+    for _ in range(40):
+        a = int(rng.integers(100))
+        o, r, done, trunc, info = env.step(a)
+        speed, turning = env.map_discrete_to_continuous(a)
+        assert o.shape == (14,) and o.dtype == np.float32
+        np.testing.assert_allclose(o[3:5], [speed, turning], atol=1e-6)
+        if o[5] == -1.0 and o[6] == -1.0:
+            assert o[7] == 0.0  # predator not visible
+        assert np.all(o[8::2] >= 0)  # occlusion distances
+        if not done and not trunc:
+            assert abs(r - (-math.hypot(o[0] - 1.0, o[1] - 0.5))) < 1e-5
+        if done or trunc:
+            break
