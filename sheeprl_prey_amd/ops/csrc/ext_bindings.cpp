@@ -28,6 +28,10 @@ void launch_sac_target(const float* obs, const float* act, const float* logp, co
                        const float* log_alpha, const float* W1, const float* b1, const float* W2, const float* b2,
                        const float* W3, const float* b3, float* y, int M, int OD, int AD, int H, int n, float gamma,
                        hipStream_t st);
+void launch_obs_mse_fwd(const float* rec, const void* tgt, bool u8, int rows, int n, float scale, int symlog, float* loss,
+                        hipStream_t st);
+void launch_obs_mse_bwd(const float* rec, const void* tgt, bool u8, int rows, int n, float scale, int symlog, const float* g,
+                        float* drec, hipStream_t st);
 int actor_loss_blocks(int rows);
 void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
@@ -330,7 +334,35 @@ torch::Tensor sac_twin_q_target(torch::Tensor obs, torch::Tensor act, torch::Ten
   return y;
 }
 
+// ------------------------------------------------------------------ observation MSE (obs_loss.hip)
+static void obs_check(const torch::Tensor& rec, const torch::Tensor& tgt, int64_t rows) {
+  nc_check(rec, "obs_mse rec");
+  TORCH_CHECK(tgt.is_cuda() && tgt.is_contiguous() && tgt.numel() == rec.numel(), "obs_mse: target like rec");
+  TORCH_CHECK(tgt.scalar_type() == torch::kUInt8 || tgt.scalar_type() == torch::kFloat32, "obs_mse: uint8 or fp32 target");
+  TORCH_CHECK(rows > 0 && rec.numel() % rows == 0 && (rec.numel() / rows) % 4 == 0, "obs_mse: row length % 4");
+}
+
+torch::Tensor obs_mse_fwd(torch::Tensor rec, torch::Tensor tgt, int64_t rows, double scale, int64_t symlog) {
+  obs_check(rec, tgt, rows);
+  auto loss = torch::empty({rows}, rec.options());
+  launch_obs_mse_fwd(rec.data_ptr<float>(), tgt.data_ptr(), tgt.scalar_type() == torch::kUInt8, (int)rows,
+                     (int)(rec.numel() / rows), (float)scale, (int)symlog, loss.data_ptr<float>(), stream());
+  return loss;
+}
+
+torch::Tensor obs_mse_bwd(torch::Tensor rec, torch::Tensor tgt, int64_t rows, double scale, int64_t symlog, torch::Tensor g) {
+  obs_check(rec, tgt, rows);
+  nc_check(g, "obs_mse grad");
+  TORCH_CHECK(g.numel() == rows, "obs_mse: one upstream gradient per row");
+  auto drec = torch::empty_like(rec);
+  launch_obs_mse_bwd(rec.data_ptr<float>(), tgt.data_ptr(), tgt.scalar_type() == torch::kUInt8, (int)rows,
+                     (int)(rec.numel() / rows), (float)scale, (int)symlog, g.data_ptr<float>(), drec.data_ptr<float>(), stream());
+  return drec;
+}
+
 void register_ext(pybind11::module& m) {
+  m.def("obs_mse_fwd", &obs_mse_fwd);
+  m.def("obs_mse_bwd", &obs_mse_bwd);
   m.def("sac_twin_q_target", &sac_twin_q_target);
   m.def("skinny_nt", &skinny_nt, pybind11::arg("A"), pybind11::arg("W"), pybind11::arg("out"),
         pybind11::arg("add") = pybind11::none(), pybind11::arg("part") = pybind11::none());

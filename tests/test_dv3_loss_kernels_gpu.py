@@ -116,3 +116,29 @@ def test_actor_loss_kernel_graph_capture():
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(loss, eager_loss) and torch.equal(gz, eager_grad)
+
+
+@pytest.mark.parametrize("u8,symlog,shape", [(True, False, (8, 4, 3, 64, 64)), (False, True, (8, 4, 20)),
+                                            (False, False, (5, 3, 1, 16, 16))])
+def test_obs_mse_kernel_matches_eager(u8, symlog, shape):
+    """K6: observation MSE (image: against the raw uint8 frames / 255; vector: symlog MSE with the
+    d < 1e-8 rule) and its gradient vs the reference formulation."""
+    torch.manual_seed(len(shape))
+    rec = torch.randn(*shape, device="cuda", requires_grad=True)
+    if u8:
+        raw = torch.randint(0, 256, shape, device="cuda", dtype=torch.uint8)
+        tgt = raw.float() / 255.0
+    else:
+        raw = tgt = torch.randn(*shape, device="cuda") * 3
+    dims = tuple(range(2, rec.dim()))
+    if symlog:
+        d = (rec - torch.sign(tgt) * torch.log1p(tgt.abs())) ** 2
+        ref = torch.where(d < 1e-8, torch.zeros_like(d), d).sum(dim=dims)
+    else:
+        ref = ((rec - tgt) ** 2).sum(dim=dims)
+    g = torch.rand_like(ref)
+    (gr,) = torch.autograd.grad((ref * g).sum(), rec)
+    got = ops.obs_mse(rec, raw, 1.0 / 255.0 if u8 else 1.0, symlog=symlog)
+    (gg,) = torch.autograd.grad((got * g).sum(), rec)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(gg, gr, rtol=1e-5, atol=1e-5)
