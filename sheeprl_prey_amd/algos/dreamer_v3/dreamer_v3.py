@@ -250,13 +250,12 @@ class DreamerV3Trainer:
                 imagined_actions_t = torch.stack(imagined_actions)
             predicted_values = ops.twohot_mean(critic(imagined_trajectories))
             predicted_rewards = ops.twohot_mean(wm.reward_model(imagined_trajectories))
-            continues = (wm.continue_model(imagined_trajectories) > 0).to(predicted_values.dtype)
-            true_done = (1 - data["dones"]).reshape(1, -1, 1)
-            continues = torch.cat((true_done, continues[1:]))
-            lambda_values = compute_lambda_values(predicted_rewards[1:], predicted_values[1:],
-                                                  continues[1:] * cfg.algo.gamma, lmbda=cfg.algo.lmbda)
-        with torch.no_grad():
-            st["discount"] = torch.cumprod(continues * cfg.algo.gamma, dim=0) / cfg.algo.gamma
+            # continuation flags, their gamma-discounts and the cumulative discount: one kernel (K11)
+            cont_g, discount = ops.imag_discount(wm.continue_model(imagined_trajectories), data["dones"],
+                                                 cfg.algo.gamma)
+            lambda_values = compute_lambda_values(predicted_rewards[1:], predicted_values[1:], cont_g,
+                                                  lmbda=cfg.algo.lmbda)
+        st["discount"] = discount.detach()
         st["imagined_trajectories"] = imagined_trajectories
         st["imagined_actions"] = imagined_actions_t
         st["predicted_values"] = predicted_values

@@ -596,3 +596,14 @@ def obs_mse(rec: Tensor, target: Tensor, scale: float = 1.0, symlog: bool = Fals
         d = torch.where(d < 1e-8, torch.zeros_like(d), d)
         return d.sum(dim=dims)
     return ((rec - tgt) ** 2).sum(dim=dims)
+
+
+def imag_discount(continue_logits: Tensor, dones: Tensor, gamma: float):
+    """``(c[1:] * gamma, cumprod(c * gamma) / gamma)`` with ``c_0 = 1 - done`` and ``c_t = [logit_t > 0]``
+    (reference ``dreamer_v3.py:680-700``), one kernel on GPU; shapes [T, M, 1] / [T+1, M, 1]."""
+    if _native(continue_logits) and continue_logits.dtype == torch.float32 and dones.dtype == torch.float32:
+        cg, disc = _ext().imag_discount(continue_logits.detach().contiguous(), dones.reshape(-1).contiguous(), float(gamma))
+        return cg, disc
+    c = (continue_logits > 0).to(continue_logits.dtype)
+    c = torch.cat(((1 - dones).reshape(1, -1, 1).to(c.dtype), c[1:]))
+    return c[1:] * gamma, torch.cumprod(c * gamma, dim=0) / gamma

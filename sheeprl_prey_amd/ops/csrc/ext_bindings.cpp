@@ -32,6 +32,8 @@ void launch_obs_mse_fwd(const float* rec, const void* tgt, bool u8, int rows, in
                         hipStream_t st);
 void launch_obs_mse_bwd(const float* rec, const void* tgt, bool u8, int rows, int n, float scale, int symlog, const float* g,
                         float* drec, hipStream_t st);
+void launch_imag_discount(const float* clog, const float* dones, int T1, int M, float gamma, float* cont_g, float* discount,
+                          hipStream_t st);
 int actor_loss_blocks(int rows);
 void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
@@ -360,7 +362,21 @@ torch::Tensor obs_mse_bwd(torch::Tensor rec, torch::Tensor tgt, int64_t rows, do
   return drec;
 }
 
+// continue logits [T1, M(, 1)], dones [M] -> {cont_g [T1-1, M, 1], discount [T1, M, 1]}
+std::vector<torch::Tensor> imag_discount(torch::Tensor clog, torch::Tensor dones, double gamma) {
+  nc_check(clog, "imag_discount logits");
+  nc_check(dones, "imag_discount dones");
+  const int64_t T1 = clog.size(0), M = clog.numel() / T1;
+  TORCH_CHECK(T1 >= 2 && dones.numel() == M, "imag_discount: logits [T1, M], dones [M]");
+  auto cg = torch::empty({T1 - 1, M, 1}, clog.options());
+  auto disc = torch::empty({T1, M, 1}, clog.options());
+  launch_imag_discount(clog.data_ptr<float>(), dones.data_ptr<float>(), (int)T1, (int)M, (float)gamma, cg.data_ptr<float>(),
+                       disc.data_ptr<float>(), stream());
+  return {cg, disc};
+}
+
 void register_ext(pybind11::module& m) {
+  m.def("imag_discount", &imag_discount);
   m.def("obs_mse_fwd", &obs_mse_fwd);
   m.def("obs_mse_bwd", &obs_mse_bwd);
   m.def("sac_twin_q_target", &sac_twin_q_target);

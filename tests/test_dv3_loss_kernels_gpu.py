@@ -142,3 +142,16 @@ def test_obs_mse_kernel_matches_eager(u8, symlog, shape):
     (gg,) = torch.autograd.grad((got * g).sum(), rec)
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(gg, gr, rtol=1e-5, atol=1e-5)
+
+
+def test_imag_discount_kernel_matches_torch():
+    """K11: imagined continuation discounts (one kernel) vs the reference torch form, bitwise."""
+    torch.manual_seed(0)
+    T1, M, gamma = 16, 1024, 0.996996996
+    logits = torch.randn(T1, M, 1, device="cuda")
+    dones = (torch.rand(M, device="cuda") < 0.1).float()
+    cg, disc = ops.imag_discount(logits, dones, gamma)
+    c = (logits > 0).float()
+    c = torch.cat(((1 - dones).reshape(1, -1, 1), c[1:]))
+    assert torch.equal(cg, c[1:] * gamma)
+    assert torch.equal(disc, torch.cumprod(c * gamma, dim=0) / gamma)
