@@ -18,6 +18,7 @@ import torch.nn as nn
 from torch import Tensor
 from torch.distributions import Independent, Normal
 
+from sheeprl_prey_amd import ops
 from sheeprl_prey_amd.algos.ppo.agent import CNNEncoder, MLPEncoder, _act
 from sheeprl_prey_amd.models.models import MLP, MultiEncoder
 from sheeprl_prey_amd.utils.distribution import OneHotCategoricalValidateArgs
@@ -45,7 +46,10 @@ class RecurrentModel(nn.Module):
 
     def forward(self, input: Tensor, states: Tuple[Tensor, Tensor], mask: Optional[Tensor] = None):
         x = self._pre_mlp(input)
-        out, states = self._lstm(x, states)
+        if ops.lstm_supported(self._lstm, x):  # persistent HIP LSTM, one launch per direction (K18)
+            out, states = ops.lstm_seq(self._lstm, x, states)
+        else:
+            out, states = self._lstm(x, states)
         shape = out.shape
         return self._post_mlp(out.reshape(-1, shape[-1])).view(*shape[:-1], -1), states
 

@@ -607,3 +607,53 @@ def imag_discount(continue_logits: Tensor, dones: Tensor, gamma: float):
     c = (continue_logits > 0).to(continue_logits.dtype)
     c = torch.cat(((1 - dones).reshape(1, -1, 1).to(c.dtype), c[1:]))
     return c[1:] * gamma, torch.cumprod(c * gamma, dim=0) / gamma
+
+
+# =============================================================== persistent LSTM (K18)
+class _LSTMSeq(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, h0, c0, W_ih, W_hh, b_ih, b_hh):
+        T, B, D = x.shape
+        H = W_hh.shape[1]
+        C = _ext()
+        bias = b_ih + b_hh if b_ih is not None else None
+        x2 = x.reshape(T * B, D)
+        xg = (torch.addmm(bias, x2, W_ih.t()) if bias is not None else x2.mm(W_ih.t())).view(T, B, 4 * H)
+        h0c, c0c = h0.reshape(B, H).contiguous(), c0.reshape(B, H).contiguous()
+        Whh = W_hh.contiguous()
+        out, gates, cs, hT, cT = C.lstm_fwd(xg, Whh, h0c, c0c)
+        ctx.save_for_backward(x, h0c, c0c, W_ih, Whh, out, gates, cs)
+        ctx.has_bias = bias is not None
+        return out, hT.unsqueeze(0), cT.unsqueeze(0)
+
+    @staticmethod
+    def backward(ctx, dout, dhT, dcT):
+        x, h0, c0, W_ih, Whh, out, gates, cs = ctx.saved_tensors
+        T, B, D = x.shape
+        H = Whh.shape[1]
+        dout = dout.contiguous() if dout is not None else torch.zeros_like(out)
+        dg, dh0, dc0 = _ext().lstm_bwd(Whh, c0, gates, cs, dout, dhT.reshape(B, H).contiguous() if dhT is not None else None,
+                                       dcT.reshape(B, H).contiguous() if dcT is not None else None)
+        dg2 = dg.reshape(T * B, 4 * H)
+        h_prev = torch.cat((h0.unsqueeze(0), out[:-1]), 0).reshape(T * B, H)
+        dW_hh = dg2.t().mm(h_prev)
+        dW_ih = dg2.t().mm(x.reshape(T * B, D))
+        dx = dg2.mm(W_ih).view(T, B, D)
+        db = dg2.sum(0) if ctx.has_bias else None
+        return dx, dh0.unsqueeze(0), dc0.unsqueeze(0), dW_ih, dW_hh, db, db
+
+
+def lstm_supported(lstm: torch.nn.LSTM, x: Tensor) -> bool:
+    return (_native(x) and x.dtype == torch.float32 and x.dim() == 3 and lstm.num_layers == 1 and not lstm.batch_first
+            and not lstm.bidirectional and getattr(lstm, "proj_size", 0) == 0 and lstm.hidden_size % 16 == 0
+            and lstm.hidden_size <= 64 and (lstm.dropout == 0 or not lstm.training))
+
+
+def lstm_seq(lstm: torch.nn.LSTM, x: Tensor, states):
+    """``nn.LSTM`` (1 layer, seq-first) over the whole sequence as one persistent launch each way
+    (``csrc/lstm.hip``); same outputs and gradients as the module (reference ppo_recurrent/agent.py:60-73)."""
+    h0, c0 = states
+    return_ = _LSTMSeq.apply(x, h0, c0, lstm.weight_ih_l0, lstm.weight_hh_l0, lstm.bias_ih_l0 if lstm.bias else None,
+                             lstm.bias_hh_l0 if lstm.bias else None)
+    out, hT, cT = return_
+    return out, (hT, cT)

@@ -34,6 +34,10 @@ void launch_obs_mse_bwd(const float* rec, const void* tgt, bool u8, int rows, in
                         float* drec, hipStream_t st);
 void launch_imag_discount(const float* clog, const float* dones, int T1, int M, float gamma, float* cont_g, float* discount,
                           hipStream_t st);
+void launch_lstm_fwd(const float* xg, const float* Whh, const float* h0, const float* c0, float* out, float* gates, float* cs,
+                     float* hT, float* cT, int T, int B, int H, hipStream_t st);
+void launch_lstm_bwd(const float* Whh, const float* c0, const float* gates, const float* cs, const float* dout, const float* dhT,
+                     const float* dcT, float* dgates, float* dh0, float* dc0, int T, int B, int H, hipStream_t st);
 int actor_loss_blocks(int rows);
 void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
@@ -375,7 +379,49 @@ std::vector<torch::Tensor> imag_discount(torch::Tensor clog, torch::Tensor dones
   return {cg, disc};
 }
 
+// ------------------------------------------------------------------ persistent LSTM (lstm.hip)
+// xg [T, B, 4H] (input projection + both biases), Whh [4H, H], h0 / c0 [B, H]
+// -> {out [T, B, H], gates [T, B, 4H], cs [T, B, H], hT, cT}
+std::vector<torch::Tensor> lstm_fwd(torch::Tensor xg, torch::Tensor Whh, torch::Tensor h0, torch::Tensor c0) {
+  for (auto* t : {&xg, &Whh, &h0, &c0}) nc_check(*t, "lstm_fwd operand");
+  TORCH_CHECK(xg.dim() == 3 && Whh.dim() == 2 && Whh.size(0) == 4 * Whh.size(1) && xg.size(2) == Whh.size(0), "lstm_fwd: shapes");
+  const int64_t T = xg.size(0), B = xg.size(1), H = Whh.size(1);
+  TORCH_CHECK(H % 16 == 0 && H <= 64 && h0.numel() == B * H && c0.numel() == B * H, "lstm_fwd: H % 16 == 0, H <= 64");
+  auto o = xg.options();
+  auto out = torch::empty({T, B, H}, o), gates = torch::empty({T, B, 4 * H}, o), cs = torch::empty({T, B, H}, o);
+  auto hT = torch::empty({B, H}, o), cT = torch::empty({B, H}, o);
+  launch_lstm_fwd(xg.data_ptr<float>(), Whh.data_ptr<float>(), h0.data_ptr<float>(), c0.data_ptr<float>(), out.data_ptr<float>(),
+                  gates.data_ptr<float>(), cs.data_ptr<float>(), hT.data_ptr<float>(), cT.data_ptr<float>(), (int)T, (int)B,
+                  (int)H, stream());
+  return {out, gates, cs, hT, cT};
+}
+
+// -> {dgates [T, B, 4H] (pre-activation), dh0, dc0}
+std::vector<torch::Tensor> lstm_bwd(torch::Tensor Whh, torch::Tensor c0, torch::Tensor gates, torch::Tensor cs, torch::Tensor dout,
+                                    c10::optional<torch::Tensor> dhT, c10::optional<torch::Tensor> dcT) {
+  for (auto* t : {&Whh, &c0, &gates, &cs, &dout}) nc_check(*t, "lstm_bwd operand");
+  const int64_t T = gates.size(0), B = gates.size(1), H = Whh.size(1);
+  TORCH_CHECK(dout.numel() == T * B * H && cs.numel() == T * B * H, "lstm_bwd: shapes");
+  const float* dh = nullptr;
+  const float* dc = nullptr;
+  if (dhT.has_value() && dhT->defined()) {
+    nc_check(*dhT, "lstm_bwd dhT");
+    dh = dhT->data_ptr<float>();
+  }
+  if (dcT.has_value() && dcT->defined()) {
+    nc_check(*dcT, "lstm_bwd dcT");
+    dc = dcT->data_ptr<float>();
+  }
+  auto dgates = torch::empty_like(gates), dh0 = torch::empty({B, H}, gates.options()), dc0 = torch::empty({B, H}, gates.options());
+  launch_lstm_bwd(Whh.data_ptr<float>(), c0.data_ptr<float>(), gates.data_ptr<float>(), cs.data_ptr<float>(), dout.data_ptr<float>(),
+                  dh, dc, dgates.data_ptr<float>(), dh0.data_ptr<float>(), dc0.data_ptr<float>(), (int)T, (int)B, (int)H, stream());
+  return {dgates, dh0, dc0};
+}
+
 void register_ext(pybind11::module& m) {
+  m.def("lstm_fwd", &lstm_fwd);
+  m.def("lstm_bwd", &lstm_bwd, pybind11::arg("Whh"), pybind11::arg("c0"), pybind11::arg("gates"), pybind11::arg("cs"),
+        pybind11::arg("dout"), pybind11::arg("dhT") = pybind11::none(), pybind11::arg("dcT") = pybind11::none());
   m.def("imag_discount", &imag_discount);
   m.def("obs_mse_fwd", &obs_mse_fwd);
   m.def("obs_mse_bwd", &obs_mse_bwd);
