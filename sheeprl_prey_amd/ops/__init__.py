@@ -657,3 +657,33 @@ def lstm_seq(lstm: torch.nn.LSTM, x: Tensor, states):
                              lstm.bias_hh_l0 if lstm.bias else None)
     out, hT, cT = return_
     return out, (hT, cT)
+
+
+# =============================================================== plain GRU cell (K19)
+class _GRUCellAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gi, gh, h):
+        hn, rzn = _ext().gru_cell_fwd(gi, gh, h)
+        ctx.save_for_backward(gh, h, rzn)
+        return hn
+
+    @staticmethod
+    def backward(ctx, g):
+        gh, h, rzn = ctx.saved_tensors
+        return tuple(_ext().gru_cell_bwd(gh, h, rzn, g.contiguous()))
+
+
+def gru_step(rnn: torch.nn.GRU, x: Tensor, h: Tensor):
+    """One step of a 1-layer ``nn.GRU`` (``x`` [1, B, D] or [B, D], ``h`` [1, B, H]) with the gate math
+    fused in one kernel each way (``csrc/gru_cell.hip``) and the two input/recurrent projections as
+    library GEMMs; returns ``(out, h')`` like the module.  Falls back to the module off the GPU."""
+    single_step = x.dim() == 3 and x.shape[0] == 1
+    if not (single_step and _native(x) and x.dtype == torch.float32 and rnn.num_layers == 1 and not rnn.batch_first
+            and not rnn.bidirectional and rnn.bias):
+        return rnn(x, h)
+    x2 = x.reshape(-1, x.shape[-1])
+    h2 = h.reshape(-1, rnn.hidden_size)
+    gi = torch.nn.functional.linear(x2, rnn.weight_ih_l0, rnn.bias_ih_l0).contiguous()
+    gh = torch.nn.functional.linear(h2, rnn.weight_hh_l0, rnn.bias_hh_l0).contiguous()
+    hn = _GRUCellAct.apply(gi, gh, h2.contiguous()).view(1, -1, rnn.hidden_size)
+    return hn, hn

@@ -38,6 +38,9 @@ void launch_lstm_fwd(const float* xg, const float* Whh, const float* h0, const f
                      float* hT, float* cT, int T, int B, int H, hipStream_t st);
 void launch_lstm_bwd(const float* Whh, const float* c0, const float* gates, const float* cs, const float* dout, const float* dhT,
                      const float* dcT, float* dgates, float* dh0, float* dc0, int T, int B, int H, hipStream_t st);
+void launch_gru_cell_fwd(const float* gi, const float* gh, const float* h, float* hn, float* rzn, int B, int H, hipStream_t st);
+void launch_gru_cell_bwd(const float* gh, const float* h, const float* rzn, const float* dhn, float* dgi, float* dgh, float* dh,
+                         int B, int H, hipStream_t st);
 int actor_loss_blocks(int rows);
 void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
@@ -418,7 +421,29 @@ std::vector<torch::Tensor> lstm_bwd(torch::Tensor Whh, torch::Tensor c0, torch::
   return {dgates, dh0, dc0};
 }
 
+// ------------------------------------------------------------------ plain GRU cell (gru_cell.hip)
+std::vector<torch::Tensor> gru_cell_fwd(torch::Tensor gi, torch::Tensor gh, torch::Tensor h) {
+  for (auto* t : {&gi, &gh, &h}) nc_check(*t, "gru_cell operand");
+  const int64_t H = h.size(-1), B = h.numel() / H;
+  TORCH_CHECK(gi.numel() == 3 * B * H && gh.numel() == 3 * B * H, "gru_cell: gi / gh [B, 3H]");
+  auto hn = torch::empty_like(h), rzn = torch::empty_like(gi);
+  launch_gru_cell_fwd(gi.data_ptr<float>(), gh.data_ptr<float>(), h.data_ptr<float>(), hn.data_ptr<float>(), rzn.data_ptr<float>(),
+                      (int)B, (int)H, stream());
+  return {hn, rzn};
+}
+
+std::vector<torch::Tensor> gru_cell_bwd(torch::Tensor gh, torch::Tensor h, torch::Tensor rzn, torch::Tensor dhn) {
+  for (auto* t : {&gh, &h, &rzn, &dhn}) nc_check(*t, "gru_cell_bwd operand");
+  const int64_t H = h.size(-1), B = h.numel() / H;
+  auto dgi = torch::empty_like(gh), dgh = torch::empty_like(gh), dh = torch::empty_like(h);
+  launch_gru_cell_bwd(gh.data_ptr<float>(), h.data_ptr<float>(), rzn.data_ptr<float>(), dhn.data_ptr<float>(), dgi.data_ptr<float>(),
+                      dgh.data_ptr<float>(), dh.data_ptr<float>(), (int)B, (int)H, stream());
+  return {dgi, dgh, dh};
+}
+
 void register_ext(pybind11::module& m) {
+  m.def("gru_cell_fwd", &gru_cell_fwd);
+  m.def("gru_cell_bwd", &gru_cell_bwd);
   m.def("lstm_fwd", &lstm_fwd);
   m.def("lstm_bwd", &lstm_bwd, pybind11::arg("Whh"), pybind11::arg("c0"), pybind11::arg("gates"), pybind11::arg("cs"),
         pybind11::arg("dout"), pybind11::arg("dhT") = pybind11::none(), pybind11::arg("dcT") = pybind11::none());

@@ -51,3 +51,25 @@ def test_lstm_kernel_in_recurrent_ppo_agent_module():
         ops.set_fused(True)
     torch.testing.assert_close(out, out2, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(h, h2, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("B,D,H", [(16, 200, 200), (3, 30, 64)])
+def test_gru_cell_kernel_matches_module(B, D, H):
+    """K19: DreamerV1's GRU step with fused gate kernels vs ``nn.GRU`` in fp64 (outputs and all grads)."""
+    torch.manual_seed(B + H)
+    rnn = torch.nn.GRU(D, H).cuda()
+    ref = copy.deepcopy(rnn).double().cpu()
+    x = torch.randn(1, B, D, device="cuda", requires_grad=True)
+    h = torch.randn(1, B, H, device="cuda", requires_grad=True)
+    out, hn = ops.gru_step(rnn, x, h)
+    assert type(hn.grad_fn).__name__ != "CudnnRnnBackward0" and out is hn
+    xr, hr = x.detach().double().cpu().requires_grad_(), h.detach().double().cpu().requires_grad_()
+    outr, hnr = ref(xr, hr)
+    torch.testing.assert_close(hn.double().cpu(), hnr, rtol=1e-5, atol=1e-5)
+    g = torch.randn_like(hn)
+    hn.backward(g)
+    hnr.backward(g.double().cpu())
+    torch.testing.assert_close(x.grad.double().cpu(), xr.grad, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(h.grad.double().cpu(), hr.grad, rtol=1e-4, atol=1e-5)
+    for p, pr in zip(rnn.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.grad.double().cpu(), pr.grad, rtol=1e-4, atol=1e-5)
