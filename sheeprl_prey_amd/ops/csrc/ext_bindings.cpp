@@ -41,6 +41,8 @@ void launch_lstm_bwd(const float* Whh, const float* c0, const float* gates, cons
 void launch_gru_cell_fwd(const float* gi, const float* gh, const float* h, float* hn, float* rzn, int B, int H, hipStream_t st);
 void launch_gru_cell_bwd(const float* gh, const float* h, const float* rzn, const float* dhn, float* dgi, float* dgh, float* dh,
                          int B, int H, hipStream_t st);
+void launch_gather_rows(const void* const* src, void* const* dst, const long* row_bytes, int nk, int n_envs, long cap, int N,
+                        const long* row, const long* env, hipStream_t st);
 int actor_loss_blocks(int rows);
 void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
@@ -441,7 +443,38 @@ std::vector<torch::Tensor> gru_cell_bwd(torch::Tensor gh, torch::Tensor h, torch
   return {dgi, dgh, dh};
 }
 
+// ------------------------------------------------------------------ replay row gather (gather.hip)
+// srcs[k] [capacity, n_envs, ...] contiguous; row / env int64 [N] -> outputs [N, ...] per key
+std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::Tensor row, torch::Tensor env) {
+  TORCH_CHECK(!srcs.empty() && srcs.size() <= 16, "gather_rows: 1..16 keys");
+  TORCH_CHECK(row.is_cuda() && env.is_cuda() && row.scalar_type() == torch::kLong && env.scalar_type() == torch::kLong &&
+                  row.is_contiguous() && env.is_contiguous() && row.numel() == env.numel(),
+              "gather_rows: int64 row / env index vectors");
+  const int64_t N = row.numel();
+  const int64_t n_envs = srcs[0].size(1), cap = srcs[0].size(0);
+  std::vector<const void*> sp;
+  std::vector<void*> dp;
+  std::vector<long> rb;
+  std::vector<torch::Tensor> outs;
+  for (auto& s : srcs) {
+    TORCH_CHECK(s.is_cuda() && s.is_contiguous() && s.dim() >= 2 && s.size(0) == cap && s.size(1) == n_envs,
+                "gather_rows: every key [capacity, n_envs, ...]");
+    std::vector<int64_t> shape{N};
+    for (int d = 2; d < s.dim(); ++d) shape.push_back(s.size(d));
+    auto o = torch::empty(shape, s.options());
+    sp.push_back(s.data_ptr());
+    dp.push_back(o.data_ptr());
+    rb.push_back((long)(s.numel() / (s.size(0) * n_envs) * s.element_size()));
+    outs.push_back(o);
+  }
+  if (N > 0)
+    launch_gather_rows(sp.data(), dp.data(), rb.data(), (int)srcs.size(), (int)n_envs, (long)cap, (int)N, row.data_ptr<int64_t>(),
+                       env.data_ptr<int64_t>(), stream());
+  return outs;
+}
+
 void register_ext(pybind11::module& m) {
+  m.def("gather_rows", &gather_rows);
   m.def("gru_cell_fwd", &gru_cell_fwd);
   m.def("gru_cell_bwd", &gru_cell_bwd);
   m.def("lstm_fwd", &lstm_fwd);
