@@ -138,12 +138,32 @@ class CNN(_ConvStack):
         super().__init__(input_channels, hidden_channels, cnn_layer, **kwargs)
 
 
+class _NativeConvTranspose2d(nn.ConvTranspose2d):
+    """``nn.ConvTranspose2d`` that never dispatches to MIOpen on the GPU.
+
+    MIOpen's transposed-conv forward for the few-channel image output layer (measured: 8 -> 3,
+    k4 s2 p1, N=64 at 32x32 -> 64x64) raised an illegal memory access on MI355X, depending on where
+    its buffers sat in memory (reproduced under AMD_SERIALIZE_KERNEL=3: the fault is in MIOpen's own
+    launch, profiles/r2_gpu_fault_note.md).  This layer runs PyTorch's native col2im transposed
+    convolution instead; forward and backward are the same math, parameter names are unchanged.
+    The DreamerV3 hot path does not use it: its decoder runs on the HIP conv stack (ops/conv.py)."""
+
+    def forward(self, input: Tensor, output_size=None) -> Tensor:
+        if input.is_cuda:
+            with torch.backends.cudnn.flags(enabled=False):
+                return super().forward(input, output_size)
+        return super().forward(input, output_size)
+
+
 class DeCNN(_ConvStack):
     """ConvTranspose2d stack (reference ``models.py:204-284``)."""
 
     def __init__(self, input_channels: int, hidden_channels: Sequence[int] = (), cnn_layer: ModuleType = nn.ConvTranspose2d,
                  **kwargs):
         super().__init__(input_channels, hidden_channels, cnn_layer, **kwargs)
+        for m in self._model.modules():
+            if type(m) is nn.ConvTranspose2d and m.out_channels <= 4:
+                m.__class__ = _NativeConvTranspose2d
 
 
 class NatureCNN(CNN):

@@ -58,7 +58,7 @@ def _stages(seq: nn.Sequential, conv_type) -> Optional[List[Tuple[nn.Module, Opt
     i = 0
     while i < len(mods):
         conv = mods[i]
-        if type(conv) is not conv_type or not _is_k4s2p1(conv):
+        if not isinstance(conv, conv_type) or not _is_k4s2p1(conv):
             return None
         ln = None
         if i + 1 < len(mods) and isinstance(mods[i + 1], LayerNormChannelLast):

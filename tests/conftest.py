@@ -20,3 +20,27 @@ def _chdir_tmp(tmp_path, monkeypatch, request):
     if "no_chdir" not in request.keywords:
         monkeypatch.chdir(tmp_path)
     yield
+
+
+@pytest.fixture(autouse=True)
+def _gpu_teardown(request):
+    """GPU tests: objects of a finished test (trainers hold reference cycles through their graphed
+    step functions, so their captured hipGraphs, graph memory pools and tensors are otherwise freed
+    by the cyclic GC at an arbitrary point of a LATER test) are collected while the device is idle."""
+    yield
+    if "gpu" in request.keywords:
+        import gc
+
+        import torch
+
+        gc.collect()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+
+
+if os.environ.get("SRL_ANOMALY"):
+    # diagnostics (scripts/diag_fault2.sh): a failing backward node reports the forward stack that made it
+    import torch
+
+    torch.autograd.set_detect_anomaly(True)
