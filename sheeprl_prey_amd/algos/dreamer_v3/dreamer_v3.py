@@ -199,7 +199,10 @@ class DreamerV3Trainer:
             continue_logits, continue_targets, wm_cfg.continue_scale_factor,
         )
         self.world_optimizer.zero_grad(set_to_none=True)
-        rec_loss.backward()
+        # decoder weight gradients run on a side stream beside the persistent scan backward (joined
+        # here); not with the overlapped all-reduce, whose grad hooks read each gradient at once
+        with ops.sidework.region(rec_loss.is_cuda and getattr(self.world_optimizer, "_ov", None) is None):
+            rec_loss.backward()
         out["Loss/world_model_loss"] = rec_loss.detach()
         out["Loss/observation_loss"] = observation_loss.detach()
         out["Loss/reward_loss"] = reward_loss.detach()

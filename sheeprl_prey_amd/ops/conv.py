@@ -19,6 +19,8 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 from torch import Tensor, nn
 
+from sheeprl_prey_amd.ops import sidework
+
 _OK_CH = (32, 64, 128, 256)
 ENABLED = True  # A/B switch: False routes the stacks through the per-layer modules (MIOpen + LN kernels)
 # Below this many frames (e.g. the env-interaction player, one frame per env) the deepest stage has
@@ -179,6 +181,20 @@ def encoder_forward(stages, x: Tensor) -> Tensor:
     return EncoderConvFn.apply(x, meta, *params)
 
 
+def _wgrad(C, P: Tensor, Q: Tensor, cb: int, w: Tensor) -> Tensor:
+    """Decoder weight gradient: in line, or - inside ``sidework.region`` - deferred to the side stream
+    that runs beside the persistent scan backward (``ops/sidework.py``).  The output is allocated
+    here, on the calling stream; the queued launch holds a second tensor on the same storage, made
+    with ``set_`` rather than ``view`` (a view keeps its base referenced: AccumulateGrad would then
+    not steal the returned tensor as ``.grad`` but clone it - before the side stream has written it)."""
+    if not sidework.active():
+        return C.conv_wgrad(P, Q, cb)
+    out = torch.empty_like(w)
+    dst = out.new_empty(0).set_(out.untyped_storage(), out.storage_offset(), out.shape, out.stride())
+    sidework.defer(lambda: C.conv_wgrad(P, Q, cb, dst), P, Q)
+    return out
+
+
 # ---------------------------------------------------------------------------------- decoder
 class DecoderConvFn(torch.autograd.Function):
     """h: [N, C0*4*4] (Linear output, C,H,W order) -> image [N, 3, 2^L*4, 2^L*4] NCHW, + c0."""
@@ -230,7 +246,7 @@ class DecoderConvFn(torch.autograd.Function):
         dbias = dout.sum(dim=(0, 2, 3))
         dws: List[Optional[Tensor]] = [None] * (L + 1)
         cout_last = ws[L].shape[1]
-        dws[L] = C.conv_wgrad(p_last, q, cout_last)
+        dws[L] = _wgrad(C, p_last, q, cout_last, ws[L])
         wp = C.conv_pack_down(ws[L], q.shape[3])
         _, zp, mp, rp = acts[4 * (L - 1):4 * L]
         dz = C.conv_gemm(0, q, wp, ws[L].shape[0], 1, gs[L - 1], bs[L - 1], 0.0, act[L - 1], False, zp, mp, rp,
@@ -239,7 +255,7 @@ class DecoderConvFn(torch.autograd.Function):
         for i in range(L - 1, -1, -1):
             p = acts[4 * i]
             cout = ws[i].shape[1]
-            dws[i] = C.conv_wgrad(p, dz, cout)
+            dws[i] = _wgrad(C, p, dz, cout, ws[i])
             wp = C.conv_pack_down(ws[i], cout)
             cin = ws[i].shape[0]
             if i > 0:

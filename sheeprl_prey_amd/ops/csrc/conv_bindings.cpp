@@ -165,7 +165,7 @@ std::vector<torch::Tensor> conv_gemm(int64_t kind, torch::Tensor src, torch::Ten
 }
 
 // dW[a][b][4][4] = sum_m P[m][a] Q[gather(m, tap)][b]; P NHWC small grid [N,SH,SW,Ca], Q NHWC large [N,2SH,2SW,Cbp]
-torch::Tensor conv_wgrad(torch::Tensor P, torch::Tensor Q, int64_t Cb) {
+torch::Tensor conv_wgrad(torch::Tensor P, torch::Tensor Q, int64_t Cb, c10::optional<torch::Tensor> out) {
   chk_nhwc(P, "wgrad P");
   chk_nhwc(Q, "wgrad Q");
   const int64_t N = P.size(0), SH = P.size(1), SW = P.size(2), Ca = P.size(3), Cbp = Q.size(3);
@@ -175,7 +175,15 @@ torch::Tensor conv_wgrad(torch::Tensor P, torch::Tensor Q, int64_t Cb) {
   int S, kper;
   conv_wgrad_plan(N, SH, SW, Ca, Cbp, &S, &kper);
   auto slab = torch::empty({(int64_t)S, Ca, 16 * Cbp}, P.options());
-  auto dw = torch::empty({Ca, Cb, 4, 4}, P.options());
+  torch::Tensor dw;
+  if (out.has_value() && out->defined()) {
+    dw = *out;  // caller-allocated (e.g. on another stream than the one this runs on)
+    TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == torch::kFloat32 && dw.is_contiguous() && dw.dim() == 4 &&
+                    dw.size(0) == Ca && dw.size(1) == Cb && dw.size(2) == 4 && dw.size(3) == 4,
+                "wgrad: out must be a contiguous float32 [Ca, Cb, 4, 4] GPU tensor");
+  } else {
+    dw = torch::empty({Ca, Cb, 4, 4}, P.options());
+  }
   bool ok = launch_conv_wgrad(P.data_ptr<float>(), Q.data_ptr<float>(), slab.data_ptr<float>(), dw.data_ptr<float>(), N,
                               SH, SW, Ca, Cbp, Cb, stream());
   TORCH_CHECK(ok, "wgrad: unsupported configuration");
@@ -229,7 +237,7 @@ void register_conv(pybind11::module& m) {
   m.def("conv_pack_down", &conv_pack_down);
   m.def("conv_pack_up", &conv_pack_up);
   m.def("conv_gemm", &conv_gemm);
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, pybind11::arg("P"), pybind11::arg("Q"), pybind11::arg("Cb"), pybind11::arg("out") = pybind11::none());
   m.def("conv_to_nhwc4", &conv_to_nhwc4);
   m.def("conv_ln_bwd_flat", &conv_ln_bwd_flat);
   m.def("conv_up_small", &conv_up_small);

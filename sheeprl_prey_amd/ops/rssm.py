@@ -360,7 +360,16 @@ class RSSMPersistFn(torch.autograd.Function):
         p1g, p1b, pgg, pgb, p2g, p2b = e(T, D), e(T, D), e(T, 3 * H), e(T, 3 * H), e(T, hid), e(T, hid)
         bwd = [W2.t().contiguous(), W1.t().contiguous(), Wg.t().contiguous(), dpost, dmixed, DH, dlog, dv, du, dgx, dcat,
                dx, p1g, p1b, pgg, pgb, p2g, p2b, e(T, B, 3 * H), e(T, H // 16, 16, 2)]
+        from sheeprl_prey_amd.ops import sidework
+
+        gate = None
+        if sidework.active():
+            # deferred decoder weight gradients start with the scan, on the CUs it leaves free
+            gate = torch.cuda.Event()
+            gate.record()
         C.scanp_bwd(fwd + bwd, ctx.dims, ctx.fl)
+        if gate is not None:
+            sidework.launch(gate)
         cat, zm, hs, v = fwd[17], fwd[18], fwd[25], fwd[27]
         TB = T * B
         dWz = dx.reshape(TB, D).t().mm(zm.reshape(TB, S))

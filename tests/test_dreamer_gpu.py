@@ -5,7 +5,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _build(graphs: bool, seed: int = 0, continuous: bool = False):
+def _build(graphs: bool, seed: int = 0, continuous: bool = False, cnn_mult: int = 8):
     from sheeprl_prey_amd.algos.dreamer_v3.agent import build_models
     from sheeprl_prey_amd.algos.dreamer_v3.dreamer_v3 import DreamerV3Trainer
     from sheeprl_prey_amd.algos.dreamer_v3.utils import Moments
@@ -17,7 +17,7 @@ def _build(graphs: bool, seed: int = 0, continuous: bool = False):
 
     cfg = dotdict(compose([
         "exp=dreamer_v3", "env=dummy", "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]", "algo.dense_units=64",
-        "algo.mlp_layers=2", "algo.world_model.encoder.cnn_channels_multiplier=8",
+        "algo.mlp_layers=2", f"algo.world_model.encoder.cnn_channels_multiplier={cnn_mult}",
         "algo.world_model.recurrent_model.recurrent_state_size=64", "algo.world_model.representation_model.hidden_size=64",
         "algo.world_model.transition_model.hidden_size=64", "algo.horizon=5", "fabric.accelerator=cuda",
         f"fabric.cuda_graphs={graphs}",
@@ -68,6 +68,43 @@ def test_dv3_graph_matches_eager_losses():
     torch.manual_seed(11)
     lb = float(b.train_step(data)["Loss/observation_loss"])
     assert abs(la - lb) / abs(la) < 1e-4
+
+
+def test_side_stream_decoder_wgrad_matches_inline():
+    """Decoder weight gradients deferred to the side stream beside the persistent scan backward
+    (ops/sidework.py) equal the in-line ones; every other world-model gradient is unchanged too."""
+    from sheeprl_prey_amd.ops import sidework
+
+    tr = _build(graphs=False, seed=5, cnn_mult=32)  # channels 32..256: the HIP conv stack + persistent scan
+    data = _data(seed=9)
+    wm = tr.world_model
+    grads = []
+    n0 = sidework.deferred_count()
+    names = [n for n, _ in wm.named_parameters()]
+    default = sidework._ENABLED
+    for on in (False, False, True):  # the first call builds the lazy plans (kept out of the comparison)
+        sidework._ENABLED = on
+        if on:
+            # poison the allocator's free blocks of the weight sizes with NaN: a gradient read before the
+            # side stream wrote it (e.g. cloned by autograd instead of stolen) cannot pass by luck
+            for p in wm.parameters():
+                p.grad = None
+            junk = [torch.full((p.numel(),), float("nan"), device="cuda") for p in wm.parameters() for _ in range(4)]
+            del junk
+        try:
+            torch.manual_seed(123)
+            tr._phase_wm(data)
+            torch.cuda.synchronize()
+            grads.append([None if p.grad is None else p.grad.detach().clone() for p in wm.parameters()])
+        finally:
+            sidework._ENABLED = default
+    assert sidework.deferred_count() - n0 >= 4, "the decoder weight gradients were not deferred"
+    bad = []
+    for n, ga, gb in zip(names, grads[1], grads[2]):
+        assert (ga is None) == (gb is None), n
+        if ga is not None and not torch.allclose(gb, ga, rtol=1e-4, atol=1e-5):
+            bad.append((n, float((gb - ga).abs().max())))
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("impl", ["persist", "scan4", "scan9"])
