@@ -19,6 +19,7 @@ import torch
 import torch.nn as nn
 from torch import Tensor
 
+from sheeprl_prey_amd import ops
 from sheeprl_prey_amd.models.ensemble import EnsembleLinear, EnsembleMLP
 from sheeprl_prey_amd.parallel.flat_optim import flatten_like
 from sheeprl_prey_amd.parallel.graphs import PhasedStep
@@ -129,8 +130,10 @@ class P2EMixin:
         with torch.no_grad():
             x = torch.cat((traj.detach(), acts.detach()), -1)
             lead = x.shape[:-1]
-            pred = self.ensembles(x.reshape(-1, x.shape[-1])).view(self.ensembles.n, *lead, -1)
-            r = pred.var(0).mean(-1, keepdim=True) * self.cfg.algo.intrinsic_reward_multiplier
+            ens = self.ensembles
+            # member head GEMMs + variance over members + mean over features: one kernel on the GPU (K20)
+            r = ops.ensemble_disagreement(ens.hidden(x.reshape(-1, x.shape[-1])), ens.head.weight, ens.head.bias)
+            r = r.view(*lead, 1) * self.cfg.algo.intrinsic_reward_multiplier
         self._st["out"]["Rewards/intrinsic"] = r.mean()
         return r
 

@@ -120,6 +120,17 @@ class EnsembleMLP(nn.Module):
         self.head = EnsembleLinear(n, d, output_dim) if output_dim is not None else None
         self.output_dim = output_dim if output_dim is not None else d
 
+    def hidden(self, x: Tensor) -> Tensor:
+        """Every member's last hidden layer, ``[n, B, hidden]`` (the head's input)."""
+        for i, layer in enumerate(self.layers):
+            x = layer(x)
+            if self.dropout > 0:
+                x = F.dropout(x, self.dropout, self.training)
+            if self.norms is not None:
+                x = self.norms[i](x)
+            x = self._act(x)
+        return x
+
     def forward(self, x: Tensor) -> Tensor:
         """``x``: ``[B, in]`` or ``[n, B, in]`` -> ``[n, B, out]``."""
         for i, layer in enumerate(self.layers):

@@ -541,6 +541,24 @@ def skinny_nt(A: Tensor, W: Tensor, out: Tensor, add: Optional[Tensor] = None) -
     return True
 
 
+# =============================================================== P2E disagreement (K20)
+def ensemble_disagreement(hidden: Tensor, weight: Tensor, bias: Optional[Tensor] = None) -> Tensor:
+    """``mean_c var_i (hidden_i W_i^T + b_i)[m, c]`` per row (unbiased variance over the ``n`` members):
+    the Plan2Explore intrinsic reward before its multiplier (reference ``p2e_dv2/p2e_dv2.py`` /
+    ``p2e_dv1/p2e_dv1.py``).  ``hidden`` [n, M, H], ``weight`` [n, O, H], ``bias`` [n, O] -> [M].
+    On the GPU the member head GEMMs and the variance are one kernel (``csrc/ensemble.hip``): the
+    [n, M, O] predictions are never materialised."""
+    n, M, H = hidden.shape
+    if (_native(hidden) and hidden.dtype == torch.float32 and weight.dtype == torch.float32 and H % 4 == 0
+            and n <= 64 and (bias is None or bias.dtype == torch.float32)):
+        part = _ext().ens_disagreement(hidden.contiguous(), weight.contiguous(),
+                                       bias.contiguous() if bias is not None else None)
+        return part.sum(0) / weight.shape[1]
+    wt = weight.transpose(1, 2)
+    pred = torch.baddbmm(bias.unsqueeze(1), hidden, wt) if bias is not None else torch.bmm(hidden, wt)
+    return pred.var(0).mean(-1)
+
+
 # =============================================================== SAC twin-Q target (K15)
 def sac_twin_q_target(ens, obs: Tensor, act: Tensor, logp: Tensor, rewards: Tensor, dones: Tensor, log_alpha: Tensor,
                       gamma: float) -> Optional[Tensor]:

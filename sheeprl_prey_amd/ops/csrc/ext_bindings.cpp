@@ -28,6 +28,8 @@ void launch_sac_target(const float* obs, const float* act, const float* logp, co
                        const float* log_alpha, const float* W1, const float* b1, const float* W2, const float* b2,
                        const float* W3, const float* b3, float* y, int M, int OD, int AD, int H, int n, float gamma,
                        hipStream_t st);
+bool launch_ens_disagreement(const float* X, const float* W, const float* b, float* part, int n, int M, int O, int H,
+                             hipStream_t st);
 void launch_obs_mse_fwd(const float* rec, const void* tgt, bool u8, int rows, int n, float scale, int symlog, float* loss,
                         hipStream_t st);
 void launch_obs_mse_bwd(const float* rec, const void* tgt, bool u8, int rows, int n, float scale, int symlog, const float* g,
@@ -345,6 +347,29 @@ torch::Tensor sac_twin_q_target(torch::Tensor obs, torch::Tensor act, torch::Ten
   return y;
 }
 
+// ------------------------------------------------------------------ P2E disagreement (ensemble.hip)
+// X [n, M, H] last hidden layer of every member, W [n, O, H], b [n, O] -> partial feature sums of the
+// member variance [ceil(O / 64), M]
+torch::Tensor ens_disagreement(torch::Tensor X, torch::Tensor W, c10::optional<torch::Tensor> b) {
+  nc_check(X, "disagreement X");
+  nc_check(W, "disagreement W");
+  TORCH_CHECK(X.dim() == 3 && W.dim() == 3 && X.size(0) == W.size(0) && X.size(2) == W.size(2),
+              "disagreement: X [n, M, H] and W [n, O, H]");
+  const int64_t n = X.size(0), M = X.size(1), H = X.size(2), O = W.size(1);
+  TORCH_CHECK(H % 4 == 0 && n <= 64 && M < (int64_t(1) << 31) && n * M * H < (int64_t(1) << 40), "disagreement: H % 4, n <= 64");
+  const float* bp = nullptr;
+  if (b.has_value() && b->defined()) {
+    nc_check(*b, "disagreement b");
+    TORCH_CHECK(b->numel() == n * O, "disagreement: b [n, O]");
+    bp = b->data_ptr<float>();
+  }
+  auto part = torch::empty({(O + 63) / 64, M}, X.options());
+  TORCH_CHECK(launch_ens_disagreement(X.data_ptr<float>(), W.data_ptr<float>(), bp, part.data_ptr<float>(), (int)n, (int)M,
+                                      (int)O, (int)H, stream()),
+              "disagreement: unsupported shape");
+  return part;
+}
+
 // ------------------------------------------------------------------ observation MSE (obs_loss.hip)
 static void obs_check(const torch::Tensor& rec, const torch::Tensor& tgt, int64_t rows) {
   nc_check(rec, "obs_mse rec");
@@ -481,6 +506,7 @@ void register_ext(pybind11::module& m) {
   m.def("lstm_bwd", &lstm_bwd, pybind11::arg("Whh"), pybind11::arg("c0"), pybind11::arg("gates"), pybind11::arg("cs"),
         pybind11::arg("dout"), pybind11::arg("dhT") = pybind11::none(), pybind11::arg("dcT") = pybind11::none());
   m.def("imag_discount", &imag_discount);
+  m.def("ens_disagreement", &ens_disagreement);
   m.def("obs_mse_fwd", &obs_mse_fwd);
   m.def("obs_mse_bwd", &obs_mse_bwd);
   m.def("sac_twin_q_target", &sac_twin_q_target);
