@@ -111,14 +111,21 @@ class CNNEncoder(nn.Module):
             self.output_dim = self.model(torch.zeros(1, *self.input_dim)).shape[-1]
 
     def forward(self, obs: Dict[str, Tensor]) -> Tensor:
-        x = torch.cat([obs[k] for k in self.keys], -3)
-        if x.is_cuda and x.dtype == torch.float32 and ops.fused_enabled() and conv_ops.ENABLED:
+        """``obs``: the scaled float frames (reference form), or the raw uint8 frames, which are
+        scaled by 1/255 here (on the fused path inside the NHWC conversion: no float copy of the batch)."""
+        # one key: no concatenation copy (torch.cat of a single tensor still copies it)
+        x = obs[self.keys[0]] if len(self.keys) == 1 else torch.cat([obs[k] for k in self.keys], -3)
+        raw = x.dtype == torch.uint8
+        if x.is_cuda and (raw or x.dtype == torch.float32) and ops.fused_enabled() and conv_ops.ENABLED:
             if not hasattr(self, "_fused_spec"):
                 self._fused_spec = conv_ops.encoder_spec(self.model, tuple(self.input_dim[1:]), self.input_dim[0])
             flat = x.reshape(-1, *x.shape[-3:])
             if self._fused_spec is not None and flat.shape[0] >= conv_ops.MIN_FRAMES:
                 # whole stack as one implicit-GEMM autograd op (ops/conv.py): NHWC, LN+SiLU fused
-                return conv_ops.encoder_forward(self._fused_spec, flat).reshape(*x.shape[:-3], -1)
+                out = conv_ops.encoder_forward(self._fused_spec, flat, 1.0 / 255.0 if raw else 1.0)
+                return out.reshape(*x.shape[:-3], -1)
+        if raw:
+            x = x / 255.0
         return cnn_forward(self.model, x, x.shape[-3:], (-1,))
 
 

@@ -173,7 +173,9 @@ class DreamerV3Trainer:
         wm_cfg = cfg.algo.world_model
         stoch, disc = wm_cfg.stochastic_size, wm_cfg.discrete_size
         out: Dict[str, Tensor] = {}
-        batch_obs = {k: data[k] / 255.0 for k in cfg.cnn_keys.encoder}
+        # image keys go to the encoder as the raw uint8 frames: it scales them by 1/255 itself (inside the
+        # fused conv stack's NHWC conversion), the reference divides here (dreamer_v3.py:169)
+        batch_obs = {k: data[k] if data[k].dtype == torch.uint8 else data[k] / 255.0 for k in cfg.cnn_keys.encoder}
         batch_obs.update({k: data[k] for k in cfg.mlp_keys.encoder})
         is_first = data["is_first"].clone()
         is_first[0] = 1.0
@@ -186,8 +188,8 @@ class DreamerV3Trainer:
         # image MSE against the raw uint8 frames and vector symlog MSE, one fused kernel each way (K6)
         obs_loss = 0
         for k in cfg.cnn_keys.decoder:
-            src = data[k] if data[k].dtype == torch.uint8 and data[k].is_cuda else batch_obs[k]
-            obs_loss = obs_loss + ops.obs_mse(reconstructed[k], src, 1.0 / 255.0 if src is data[k] else 1.0)
+            raw = data[k].dtype == torch.uint8
+            obs_loss = obs_loss + ops.obs_mse(reconstructed[k], data[k] if raw else batch_obs[k], 1.0 / 255.0 if raw else 1.0)
         for k in cfg.mlp_keys.decoder:
             obs_loss = obs_loss + ops.obs_mse(reconstructed[k], batch_obs[k], symlog=True)
         reward_logits = wm.reward_model(latent_states)

@@ -120,7 +120,8 @@ def decoder_spec(model: nn.Module, out_ch: int):
 
 # ---------------------------------------------------------------------------------- encoder
 class EncoderConvFn(torch.autograd.Function):
-    """x: [N, C<=4, H, W] float (already scaled) -> flat features [N, C_L * H_L * W_L] (C,H,W order)."""
+    """x: [N, C<=4, H, W] float (already scaled), or the raw uint8 frames with ``meta["scale"]``
+    (the scaling is folded into the NHWC conversion) -> flat features [N, C_L * H_L * W_L] (C,H,W order)."""
 
     @staticmethod
     def forward(ctx, x: Tensor, meta, *params: Tensor) -> Tensor:
@@ -128,7 +129,7 @@ class EncoderConvFn(torch.autograd.Function):
         L = len(meta["cout"])
         act, eps = meta["act"], meta["eps"]
         ws, gs, bs = params[:L], params[L:2 * L], params[2 * L:3 * L]
-        q = C.conv_to_nhwc4(x.contiguous(), 1.0)
+        q = C.conv_to_nhwc4(x.contiguous(), float(meta.get("scale", 1.0)))
         saved = []
         for i in range(L):
             wp = C.conv_pack_down(ws[i], q.shape[3])
@@ -171,12 +172,13 @@ class EncoderConvFn(torch.autograd.Function):
         return (None, None, *dws, *[d.view_as(g) for d, g in zip(dgs, gs)], *[d.view_as(b) for d, b in zip(dbs, bs)])
 
 
-def encoder_forward(stages, x: Tensor) -> Tensor:
+def encoder_forward(stages, x: Tensor, scale: float = 1.0) -> Tensor:
     from sheeprl_prey_amd.ops import _act_code as act_code
 
     convs = [c for c, _ in stages]
     lns = [ln for _, ln in stages]
-    meta = {"cout": [c.out_channels for c in convs], "act": [act_code(ln.act) for ln in lns], "eps": [float(ln.eps) for ln in lns]}
+    meta = {"cout": [c.out_channels for c in convs], "act": [act_code(ln.act) for ln in lns], "eps": [float(ln.eps) for ln in lns],
+            "scale": float(scale)}
     params = [c.weight for c in convs] + [ln.weight for ln in lns] + [ln.bias for ln in lns]
     return EncoderConvFn.apply(x, meta, *params)
 
