@@ -186,14 +186,50 @@ def main():
             for _ in range(args.torch_profile):
                 one_step()
             torch.cuda.synchronize()
+        if os.environ.get("SRL_PROFILE_SITES"):
+            # every ATen op of one eager step with its framework call site (innermost frame in the package)
+            import collections
+            import traceback
+
+            from torch.utils._python_dispatch import TorchDispatchMode
+
+            skip = {"detach", "view", "_unsafe_view", "reshape", "t", "transpose", "permute", "select", "slice", "unsqueeze",
+                    "squeeze", "expand", "as_strided", "alias", "split", "split_with_sizes", "unbind", "lift_fresh", "empty",
+                    "empty_like", "empty_strided", "is_same_size", "_local_scalar_dense",
+                    "mm", "addmm", "bmm", "baddbmm", "convolution", "miopen_convolution", "record_stream", "set_",
+                    "new_empty", "new_empty_strided", "resize_", "_has_compatible_shallow_copy_type", "numpy_T"}
+
+            class _Sites(TorchDispatchMode):
+                def __init__(self):
+                    super().__init__()
+                    self.c = collections.Counter()
+
+                def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+                    name = func.overloadpacket.__name__
+                    if name not in skip:
+                        fr = [f for f in traceback.extract_stack()[:-1] if "sheeprl_prey_amd" in f.filename]
+                        site = f"{fr[-1].filename.split('sheeprl_prey_amd/')[-1]}:{fr[-1].lineno}" if fr else "<autograd>"
+                        self.c[(name, site)] += 1
+                    return func(*args, **(kwargs or {}))
+
+            trainer.graphed.enabled = False
+            with _Sites() as sm:
+                one_step()
+            torch.cuda.synchronize()
+            for (name, site), n in sm.c.most_common(int(os.environ.get("SRL_PROFILE_TOP", 60))):
+                print(f"SITE {n:4d} {name:28s} {site}", file=sys.stderr, flush=True)
         trainer.graphed.enabled = True
         small = ("aten::cat", "aten::copy_", "aten::fill_", "aten::zero_", "aten::add", "aten::add_", "aten::sum",
                  "aten::mean", "aten::mul", "aten::sub", "aten::rand", "aten::zeros", "aten::clone", "aten::div",
                  "aten::neg", "aten::exp", "aten::where", "aten::stack", "aten::contiguous", "aten::index_select",
                  "aten::lerp_", "aten::_foreach_copy_", "aten::max", "aten::amax", "aten::sort", "aten::quantile")
-        rows = [e for e in prof.key_averages(group_by_stack_n=5) if e.key in small]
+        big = ("aten::mm", "aten::addmm", "aten::bmm", "aten::baddbmm", "aten::linear", "aten::matmul", "aten::convolution",
+               "aten::_convolution", "aten::miopen_convolution", "aten::conv2d", "aten::conv_transpose2d")
+        rows = [e for e in prof.key_averages(group_by_stack_n=5)
+                if e.key in small or (os.environ.get("SRL_PROFILE_ALL") and e.key.startswith("aten::") and e.key not in big
+                                      and getattr(e, "self_device_time_total", 0) > 0)]
         rows.sort(key=lambda e: -e.count)
-        for e in rows[:60]:
+        for e in rows[:int(os.environ.get('SRL_PROFILE_TOP', 60))]:
             stack = " <- ".join(f.split("/")[-1] for f in e.stack[:5])
             print(f"{e.key:24s} n={e.count / args.torch_profile:6.1f}/step  {stack}", file=sys.stderr, flush=True)
     if world > 1:

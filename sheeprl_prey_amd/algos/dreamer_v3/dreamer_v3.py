@@ -61,11 +61,6 @@ METRIC_KEYS = (
 )
 
 
-def _entropy_categorical(logits: Tensor) -> Tensor:
-    lp = logits.log_softmax(-1)
-    return -(lp.exp() * lp).sum(-1)
-
-
 class DreamerV3Trainer:
     """One DreamerV3 gradient step as five phases separated by the collectives they need:
 
@@ -195,10 +190,11 @@ class DreamerV3Trainer:
         reward_logits = wm.reward_model(latent_states)
         continue_logits = wm.continue_model(latent_states)
         continue_targets = 1 - data["dones"]
+        ents: List[Tensor] = []  # posterior / prior entropies: a by-product of the KL kernel
         rec_loss, kl, state_loss, reward_loss, observation_loss, continue_loss = reconstruction_loss(
             obs_loss, reward_logits, data["rewards"], priors_logits, posteriors_logits, stoch, disc,
             wm_cfg.kl_dynamic, wm_cfg.kl_representation, wm_cfg.kl_free_nats, wm_cfg.kl_regularizer,
-            continue_logits, continue_targets, wm_cfg.continue_scale_factor,
+            continue_logits, continue_targets, wm_cfg.continue_scale_factor, entropies=ents,
         )
         self.world_optimizer.zero_grad(set_to_none=True)
         # decoder weight gradients run on a side stream beside the persistent scan backward (joined
@@ -212,10 +208,8 @@ class DreamerV3Trainer:
         out["Loss/continue_loss"] = continue_loss.detach()
         out["State/kl"] = kl.detach()
         with torch.no_grad():
-            pl = posteriors_logits.detach().view(T, B, stoch, disc)
-            ql = priors_logits.detach().view(T, B, stoch, disc)
-            out["State/post_entropy"] = _entropy_categorical(pl).sum(-1).mean()
-            out["State/prior_entropy"] = _entropy_categorical(ql).sum(-1).mean()
+            out["State/post_entropy"] = ents[0].mean()
+            out["State/prior_entropy"] = ents[1].mean()
         st["out"] = out
         st["posteriors"] = posteriors.detach()
         st["recurrent_states"] = recurrent_states.detach()

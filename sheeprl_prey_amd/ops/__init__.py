@@ -282,16 +282,16 @@ class _KLBalance(torch.autograd.Function):
     def forward(ctx, post, prior, groups, classes, dyn, rep, free):
         a = post.contiguous()
         b = prior.contiguous()
-        kl, loss = _ext().kl_fwd(a, b, groups, classes, dyn, rep, free)
+        kl, loss, ea, eb = _ext().kl_fwd(a, b, groups, classes, dyn, rep, free)
         ctx.save_for_backward(a, b, kl)
         ctx.cfg = (groups, classes, dyn, rep, free)
-        ctx.mark_non_differentiable(kl)
+        ctx.mark_non_differentiable(kl, ea, eb)
         shape = post.shape[:-1] if post.shape[-1] == groups * classes else post.shape[:-2]
         ctx.shape = post.shape
-        return loss.view(shape), kl.view(shape)
+        return loss.view(shape), kl.view(shape), ea.view(shape), eb.view(shape)
 
     @staticmethod
-    def backward(ctx, gl, _gkl):
+    def backward(ctx, gl, _gkl, _gea, _geb):
         a, b, kl = ctx.saved_tensors
         groups, classes, dyn, rep, free = ctx.cfg
         da, db = _ext().kl_bwd(a, b, kl, gl.contiguous().view(-1), groups, classes, dyn, rep, free)
@@ -300,12 +300,23 @@ class _KLBalance(torch.autograd.Function):
 
 def kl_balance(
     post_logits: Tensor, prior_logits: Tensor, groups: int, classes: int, dyn: float = 0.5, rep: float = 0.1,
-    free_nats: float = 1.0,
+    free_nats: float = 1.0, entropies: Optional[list] = None,
 ) -> Tuple[Tensor, Tensor]:
     """DreamerV3 KL loss per row: ``dyn*max(KL(sg(post)||prior),free) + rep*max(KL(post||sg(prior)),free)``.
-    Returns (loss, kl)."""
+    Returns (loss, kl).  ``entropies`` (a list): receives the per-row summed categorical entropies of the
+    posterior and the prior (detached) - on the GPU a by-product of the KL kernel's log-softmaxes."""
     if _native(post_logits) and post_logits.dtype == torch.float32 and classes <= 64:
-        return _KLBalance.apply(post_logits, prior_logits, int(groups), int(classes), float(dyn), float(rep), float(free_nats))
+        loss, kl, ea, eb = _KLBalance.apply(post_logits, prior_logits, int(groups), int(classes), float(dyn), float(rep),
+                                            float(free_nats))
+        if entropies is not None:
+            entropies.extend((ea, eb))
+        return loss, kl
+    if entropies is not None:
+        with torch.no_grad():
+            for lg in (post_logits, prior_logits):
+                lp = lg.detach().reshape(-1, groups, classes).log_softmax(-1)
+                entropies.append(-(lp.exp() * lp).sum((-1, -2)).view(lg.shape[:-1] if lg.shape[-1] == groups * classes
+                                                                          else lg.shape[:-2]))
     return ref.kl_balance(post_logits, prior_logits, groups, classes, dyn, rep, free_nats)
 
 

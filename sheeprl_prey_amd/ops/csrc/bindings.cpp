@@ -43,7 +43,7 @@ bool launch_twohot_nll_fwd(const float*, const float*, const float*, float*, int
 bool launch_twohot_nll_bwd(const float*, const float*, const float*, const float*, float*, int, int, hipStream_t);
 bool launch_twohot_mean_fwd(const float*, const float*, float*, float*, int, int, hipStream_t);
 bool launch_twohot_mean_bwd(const float*, const float*, const float*, const float*, float*, int, int, hipStream_t);
-bool launch_kl_fwd(const float*, const float*, float*, float*, int, int, int, float, float, float, hipStream_t);
+bool launch_kl_fwd(const float*, const float*, float*, float*, float*, float*, int, int, int, float, float, float, hipStream_t);
 bool launch_kl_bwd(const float*, const float*, const float*, const float*, float*, float*, int, int, int, float, float, float,
                    hipStream_t);
 void launch_lambda_fwd(const float*, const float*, const float*, float*, int, int, float, hipStream_t);
@@ -360,10 +360,13 @@ std::vector<torch::Tensor> kl_fwd(torch::Tensor a, torch::Tensor b, int64_t G, i
   const int R = a.numel() / (G * C);
   auto kl = torch::empty({R}, a.options());
   auto loss = torch::empty({R}, a.options());
-  bool ok = launch_kl_fwd(a.data_ptr<float>(), b.data_ptr<float>(), kl.data_ptr<float>(), loss.data_ptr<float>(), R,
-                          (int)G, (int)C, (float)dyn, (float)rep, (float)free_nats, cur_stream());
+  auto ea = torch::empty({R}, a.options());  // per-row summed categorical entropies of a and b
+  auto eb = torch::empty({R}, a.options());
+  bool ok = launch_kl_fwd(a.data_ptr<float>(), b.data_ptr<float>(), kl.data_ptr<float>(), loss.data_ptr<float>(),
+                          ea.data_ptr<float>(), eb.data_ptr<float>(), R, (int)G, (int)C, (float)dyn, (float)rep,
+                          (float)free_nats, cur_stream());
   TORCH_CHECK(ok, "kl: too many classes ", C);
-  return {kl, loss};
+  return {kl, loss, ea, eb};
 }
 
 std::vector<torch::Tensor> kl_bwd(torch::Tensor a, torch::Tensor b, torch::Tensor kl, torch::Tensor gl, int64_t G,

@@ -288,15 +288,18 @@ __global__ void __launch_bounds__(256) twohot_mean_bwd_kernel(const float* __res
 
 // ---------------------------------------------------------------- categorical KL(post || prior)
 // one block per row; row holds G groups of C classes; loss = (dyn + rep) * max(kl, free)
+// also the row's summed categorical entropies of a and b (the posterior / prior entropy metrics of
+// reference dreamer_v3.py:512-515) when ent_a / ent_b are given: they reuse the log-softmaxes.
 __global__ void __launch_bounds__(256) kl_fwd_kernel(const float* __restrict__ a, const float* __restrict__ b,
-                                                     float* __restrict__ kl_out, float* __restrict__ loss_out, int R, int G,
+                                                     float* __restrict__ kl_out, float* __restrict__ loss_out,
+                                                     float* __restrict__ ent_a, float* __restrict__ ent_b, int R, int G,
                                                      int C, int W, float dyn, float rep, float free_nats) {
   __shared__ float red[4];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int spw = 64 / W;
   const int k = lane % W;
   const int r = blockIdx.x;
-  float acc = 0.f;
+  float acc = 0.f, hA = 0.f, hB = 0.f;
   for (int g0 = 0; g0 < G; g0 += 4 * spw) {
     const int g = g0 + wid * spw + lane / W;
     const bool valid = g < G && k < C;
@@ -308,11 +311,23 @@ __global__ void __launch_bounds__(256) kl_fwd_kernel(const float* __restrict__ a
     float lpa = av - la, lpb = bv - lb;
     float p = valid ? __expf(lpa) : 0.f;
     acc += valid ? p * (lpa - lpb) : 0.f;
+    if (ent_a) {
+      hA -= valid ? p * lpa : 0.f;
+      hB -= valid ? __expf(lpb) * lpb : 0.f;
+    }
   }
   float kl = block_sum<4>(acc, red);
+  if (ent_a) {
+    hA = block_sum<4>(hA, red);
+    hB = block_sum<4>(hB, red);
+  }
   if (threadIdx.x == 0) {
     kl_out[r] = kl;
     loss_out[r] = (dyn + rep) * fmaxf(kl, free_nats);
+    if (ent_a) {
+      ent_a[r] = hA;
+      ent_b[r] = hB;
+    }
   }
 }
 
@@ -408,10 +423,11 @@ bool launch_twohot_mean_bwd(const float* logits, const float* bins, const float*
   return true;
 }
 
-bool launch_kl_fwd(const float* a, const float* b, float* kl, float* loss, int R, int G, int C, float dyn, float rep,
-                   float free_nats, hipStream_t st) {
+bool launch_kl_fwd(const float* a, const float* b, float* kl, float* loss, float* ent_a, float* ent_b, int R, int G, int C,
+                   float dyn, float rep, float free_nats, hipStream_t st) {
   if (C > 64) return false;
-  hipLaunchKernelGGL(kl_fwd_kernel, dim3(R), dim3(256), 0, st, a, b, kl, loss, R, G, C, next_pow2(C), dyn, rep, free_nats);
+  hipLaunchKernelGGL(kl_fwd_kernel, dim3(R), dim3(256), 0, st, a, b, kl, loss, ent_a, ent_b, R, G, C, next_pow2(C), dyn,
+                     rep, free_nats);
   return true;
 }
 bool launch_kl_bwd(const float* a, const float* b, const float* kl, const float* gl, float* da, float* db, int R, int G,

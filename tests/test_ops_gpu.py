@@ -141,6 +141,12 @@ def test_kl_balance(G, C):
     _close(l1, l2, rtol=1e-4, atol=1e-4)
     for x, y in zip(g1, g2):
         _close(x, y, rtol=1e-3, atol=1e-5)
+    # the kernel's by-product: per-row summed categorical entropies of both distributions
+    ents = []
+    ops.kl_balance(a, b, G, C, 0.5, 0.1, 1.0, entropies=ents)
+    for e, x in zip(ents, (a, b)):
+        lp = x.double().view(-1, G, C).log_softmax(-1)
+        _close(e.double(), -(lp.exp() * lp).sum((-1, -2)), rtol=1e-4, atol=1e-4)
 
 
 def test_lambda_returns():
