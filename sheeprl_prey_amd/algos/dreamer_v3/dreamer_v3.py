@@ -189,12 +189,11 @@ class DreamerV3Trainer:
             obs_loss = obs_loss + ops.obs_mse(reconstructed[k], batch_obs[k], symlog=True)
         reward_logits = wm.reward_model(latent_states)
         continue_logits = wm.continue_model(latent_states)
-        continue_targets = 1 - data["dones"]
         ents: List[Tensor] = []  # posterior / prior entropies: a by-product of the KL kernel
         rec_loss, kl, state_loss, reward_loss, observation_loss, continue_loss = reconstruction_loss(
             obs_loss, reward_logits, data["rewards"], priors_logits, posteriors_logits, stoch, disc,
             wm_cfg.kl_dynamic, wm_cfg.kl_representation, wm_cfg.kl_free_nats, wm_cfg.kl_regularizer,
-            continue_logits, continue_targets, wm_cfg.continue_scale_factor, entropies=ents,
+            continue_logits, None, wm_cfg.continue_scale_factor, entropies=ents, dones=data["dones"],
         )
         self.world_optimizer.zero_grad(set_to_none=True)
         # decoder weight gradients run on a side stream beside the persistent scan backward (joined

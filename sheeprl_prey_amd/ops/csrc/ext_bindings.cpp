@@ -28,6 +28,10 @@ void launch_sac_target(const float* obs, const float* act, const float* logp, co
                        const float* log_alpha, const float* W1, const float* b1, const float* W2, const float* b2,
                        const float* W3, const float* b3, float* y, int M, int OD, int AD, int H, int n, float gamma,
                        hipStream_t st);
+void launch_wm_loss_fwd(const float* kl_loss, const float* obs, const float* rew, const float* logit, const float* done,
+                        const float* kl, int R, float kl_reg, float scale, float* total, float* means, hipStream_t st);
+void launch_wm_loss_bwd(const float* logit, const float* done, const float* g, int R, float kl_reg, float scale, float* d_kll,
+                        float* d_obs, float* d_rew, float* d_logit, hipStream_t st);
 bool launch_ens_disagreement(const float* X, const float* W, const float* b, float* part, int n, int M, int O, int H,
                              hipStream_t st);
 void launch_obs_mse_fwd(const float* rec, const void* tgt, bool u8, int rows, int n, float scale, int symlog, float* loss,
@@ -347,6 +351,54 @@ torch::Tensor sac_twin_q_target(torch::Tensor obs, torch::Tensor act, torch::Ten
   return y;
 }
 
+// ------------------------------------------------------------------ DV3 world-model loss assembly (wm_loss.hip)
+static void row_check(const torch::Tensor& t, int64_t R, const char* name) {
+  nc_check(t, name);
+  TORCH_CHECK(t.numel() == R, "wm_loss: ", name, " must hold one value per row");
+}
+
+// -> {total (0-dim), [mean kl, mean kl_loss, mean reward loss, mean obs loss, mean continue loss]}
+std::vector<torch::Tensor> wm_loss_fwd(torch::Tensor kl_loss, torch::Tensor obs, torch::Tensor rew, c10::optional<torch::Tensor> logit,
+                          c10::optional<torch::Tensor> done, torch::Tensor kl, double kl_reg, double scale) {
+  const int64_t R = kl_loss.numel();
+  TORCH_CHECK(R > 0 && R < (int64_t(1) << 31), "wm_loss: rows");
+  row_check(kl_loss, R, "kl_loss");
+  row_check(obs, R, "obs");
+  row_check(rew, R, "rew");
+  row_check(kl, R, "kl");
+  const bool has_c = logit.has_value() && logit->defined();
+  if (has_c) {
+    row_check(*logit, R, "continue logits");
+    TORCH_CHECK(done.has_value() && done->defined(), "wm_loss: dones needed with continue logits");
+    row_check(*done, R, "dones");
+  }
+  auto total = torch::empty({}, kl_loss.options());
+  auto means = torch::empty({5}, kl_loss.options());
+  launch_wm_loss_fwd(kl_loss.data_ptr<float>(), obs.data_ptr<float>(), rew.data_ptr<float>(),
+                     has_c ? logit->data_ptr<float>() : nullptr, has_c ? done->data_ptr<float>() : nullptr,
+                     kl.data_ptr<float>(), (int)R, (float)kl_reg, (float)scale, total.data_ptr<float>(), means.data_ptr<float>(),
+                     stream());
+  return {total, means};
+}
+
+std::vector<torch::Tensor> wm_loss_bwd(c10::optional<torch::Tensor> logit, c10::optional<torch::Tensor> done, torch::Tensor g,
+                                       int64_t R, double kl_reg, double scale) {
+  nc_check(g, "wm_loss grad");
+  TORCH_CHECK(g.numel() == 1, "wm_loss: scalar upstream gradient");
+  const bool has_c = logit.has_value() && logit->defined();
+  if (has_c) {
+    row_check(*logit, R, "continue logits");
+    row_check(*done, R, "dones");
+  }
+  auto opts = g.options();
+  auto d_kll = torch::empty({R}, opts), d_obs = torch::empty({R}, opts), d_rew = torch::empty({R}, opts);
+  auto d_logit = has_c ? torch::empty({R}, opts) : torch::Tensor();
+  launch_wm_loss_bwd(has_c ? logit->data_ptr<float>() : nullptr, has_c ? done->data_ptr<float>() : nullptr, g.data_ptr<float>(),
+                     (int)R, (float)kl_reg, (float)scale, d_kll.data_ptr<float>(), d_obs.data_ptr<float>(),
+                     d_rew.data_ptr<float>(), has_c ? d_logit.data_ptr<float>() : nullptr, stream());
+  return {d_kll, d_obs, d_rew, d_logit};
+}
+
 // ------------------------------------------------------------------ P2E disagreement (ensemble.hip)
 // X [n, M, H] last hidden layer of every member, W [n, O, H], b [n, O] -> partial feature sums of the
 // member variance [ceil(O / 64), M]
@@ -507,6 +559,8 @@ void register_ext(pybind11::module& m) {
         pybind11::arg("dout"), pybind11::arg("dhT") = pybind11::none(), pybind11::arg("dcT") = pybind11::none());
   m.def("imag_discount", &imag_discount);
   m.def("ens_disagreement", &ens_disagreement);
+  m.def("wm_loss_fwd", &wm_loss_fwd);
+  m.def("wm_loss_bwd", &wm_loss_bwd);
   m.def("obs_mse_fwd", &obs_mse_fwd);
   m.def("obs_mse_bwd", &obs_mse_bwd);
   m.def("sac_twin_q_target", &sac_twin_q_target);

@@ -155,3 +155,30 @@ def test_imag_discount_kernel_matches_torch():
     c = torch.cat(((1 - dones).reshape(1, -1, 1), c[1:]))
     assert torch.equal(cg, c[1:] * gamma)
     assert torch.equal(disc, torch.cumprod(c * gamma, dim=0) / gamma)
+
+
+def test_wm_loss_assembly_matches_eager():
+    """The fused loss assembly (wm_loss.hip: continue BCE, weighted sum, mean, metric means) vs the
+    eager formulation, forward values and the gradients reaching every per-row input."""
+    from sheeprl_prey_amd import ops
+    from sheeprl_prey_amd.algos.dreamer_v3.loss import reconstruction_loss
+
+    torch.manual_seed(0)
+    T, B, S, C, K = 16, 8, 32, 32, 255
+    mk = lambda *s: torch.randn(*s, device="cuda", requires_grad=True)  # noqa: E731
+    obs, rl, post, prior, cl = mk(T, B), mk(T, B, K), mk(T, B, S * C), mk(T, B, S * C), mk(T, B, 1)
+    rew = torch.randn(T, B, 1, device="cuda")
+    dones = (torch.rand(T, B, 1, device="cuda") < 0.2).float()
+    args = (rew, prior, post, S, C, 0.5, 0.1, 1.0, 1.0)
+    fused = reconstruction_loss(obs, rl, *args, cl, None, 1.0, dones=dones)
+    g_f = torch.autograd.grad(fused[0], (obs, rl, post, prior, cl))
+    ops._FUSED = False
+    try:
+        eager = reconstruction_loss(obs, rl, *args, cl, 1 - dones, 1.0)
+        g_e = torch.autograd.grad(eager[0], (obs, rl, post, prior, cl))
+    finally:
+        ops._FUSED = True
+    for a, b in zip(fused, eager):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+    for a, b in zip(g_f, g_e):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-6)
