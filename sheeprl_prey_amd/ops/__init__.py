@@ -8,6 +8,7 @@ explicitly routes GPU tensors through the eager reference (for A/B measurements 
 from __future__ import annotations
 
 import importlib
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -70,6 +71,23 @@ def _act_code(act: str) -> int:
 
 
 # =============================================================== Linear (library GEMMs, column-sum bias grad)
+_LIN2D = os.environ.get("SRL_LIN2D", "1") != "0"  # A/B switch
+
+
+def _lin2d(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
+    """``F.linear`` with >2-D inputs flattened to one GEMM when the leading dims fold into a row stride
+    (e.g. row-strided views into the imagination buffer): the bias then rides in the GEMM epilogue
+    (addmm) instead of a separate broadcast add over the whole output."""
+    if x.dim() > 2 and _LIN2D:
+        try:
+            x2 = x.view(-1, x.shape[-1])
+        except RuntimeError:
+            return torch.nn.functional.linear(x, weight, bias)
+        y = torch.addmm(bias, x2, weight.t()) if bias is not None else x2.mm(weight.t())
+        return y.view(*x.shape[:-1], weight.shape[0])
+    return torch.nn.functional.linear(x, weight, bias)
+
+
 class _Linear(torch.autograd.Function):
     """``F.linear`` whose backward takes the bias gradient with a row-split column-sum kernel
     (``norm.hip: colsum1``): torch's dim-0 sum of a [15360, 255] two-hot head gradient ran 165 us on
@@ -80,7 +98,7 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
-        return torch.nn.functional.linear(x, weight, bias)
+        return _lin2d(x, weight, bias)
 
     @staticmethod
     def backward(ctx, gy):
@@ -99,6 +117,8 @@ class _Linear(torch.autograd.Function):
 def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None) -> Tensor:
     if _native(x) and x.dtype == torch.float32 and x.dim() >= 2 and torch.is_grad_enabled():
         return _Linear.apply(x, weight, bias)
+    if _native(x) and x.dtype == torch.float32:
+        return _lin2d(x, weight, bias)
     return torch.nn.functional.linear(x, weight, bias)
 
 
