@@ -432,6 +432,33 @@ def fused_scan_supported(rssm) -> bool:
     return bool(ok)
 
 
+class _SplitCols(torch.autograd.Function):
+    """``W[:, :k], W[:, k:]`` whose backward assembles the full-weight gradient with ONE concatenation
+    (autograd's slice backward zero-fills the full weight for each part, copies the part in and adds
+    the two: five launches per split weight per step)."""
+
+    @staticmethod
+    def forward(ctx, W: Tensor, k: int):
+        ctx.k, ctx.n, ctx.m = k, W.shape[0], W.shape[1]
+        return W[:, :k], W[:, k:]
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        k, n, m = ctx.k, ctx.n, ctx.m
+        ref = g1 if g1 is not None else g2
+        if g1 is None:
+            g1 = torch.zeros(n, k, device=ref.device, dtype=ref.dtype)
+        if g2 is None:
+            g2 = torch.zeros(n, m - k, device=ref.device, dtype=ref.dtype)
+        return torch.cat((g1, g2), 1), None
+
+
+def _split_cols(W: Tensor, k: int):
+    if W.requires_grad and torch.is_grad_enabled():
+        return _SplitCols.apply(W, k)
+    return W[:, :k], W[:, k:]
+
+
 def fused_scan(rssm, embedded_obs: Tensor, actions: Tensor, is_first: Tensor, z0: Tensor,
                uniform: Tensor = None) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """Returns recurrent_states [T,B,H], posteriors [T,B,S], posteriors_logits [T,B,S], priors_logits [T,B,S]."""
@@ -443,10 +470,9 @@ def fused_scan(rssm, embedded_obs: Tensor, actions: Tensor, is_first: Tensor, z0
     H = gru.hidden_size
     S = tr[3].out_features
     rec_lin = rec[0]
-    Wz = rec_lin.weight[:, :S]
-    Wa = rec_lin.weight[:, S:]
+    Wz, Wa = _split_cols(rec_lin.weight, S)
     a_proj = torch.nn.functional.linear((1 - is_first) * actions, Wa)
-    We = rep[0].weight[:, H:]
+    Wh_rep, We = _split_cols(rep[0].weight, H)
     e_proj = torch.nn.functional.linear(embedded_obs, We, rep[0].bias)
     hid = tr[0].out_features
     meta = (rssm.discrete, float(rssm.unimix), float(rec[1].eps), float(gru.layer_norm.eps), float(tr[1].eps),
@@ -460,13 +486,13 @@ def fused_scan(rssm, embedded_obs: Tensor, actions: Tensor, is_first: Tensor, z0
         hs, post, post_mixed = RSSMPersistFn.apply(
             a_proj.contiguous(), e_proj.contiguous(), is_first.contiguous(), uni_post.contiguous(), z0.reshape(-1).contiguous(),
             Wz, rec[1].weight, rec[1].bias, gru.linear.weight, gru.layer_norm.weight, gru.layer_norm.bias,
-            rep[0].weight[:, :H], rep[1].weight, rep[1].bias, rep[3].weight, rep[3].bias, meta)
+            Wh_rep, rep[1].weight, rep[1].bias, rep[3].weight, rep[3].bias, meta)
         prior_mixed = rssm._uniform_mix_fused(rssm.transition_model(hs))
         return hs, post, post_mixed, prior_mixed
     if uniform is None:
         uniform = torch.rand(T, 2 * B * nseg, device=embedded_obs.device)
     P = torch.cat((tr[0].bias.expand(T, B, hid), e_proj), -1)
-    W1 = torch.cat((tr[0].weight, rep[0].weight[:, :H]), 0)
+    W1 = torch.cat((tr[0].weight, Wh_rep), 0)
     ln2_w = torch.stack((tr[1].weight, rep[1].weight))
     ln2_b = torch.stack((tr[1].bias, rep[1].bias))
     W2 = torch.stack((tr[3].weight, rep[3].weight))
