@@ -15,11 +15,13 @@
 // sums the O/64 partials (fixed order, deterministic).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace srl {
 namespace ens {
 
 constexpr int NTH = 256;
-constexpr int BM = 128, BN = 64, KC = 64, LDK = KC + 4;
+constexpr int BM = 128, BN = 64, KC = 64;
 constexpr int NA = BM * KC / 4 / NTH, NB = BN * KC / 4 / NTH;  // float4 per thread per chunk: 8, 4
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -47,7 +49,7 @@ __device__ __forceinline__ void fetch(float4* reg, const float* src, int nrows, 
   }
 }
 
-template <int NV>
+template <int NV, int LDK>
 __device__ __forceinline__ void put(float* dst, const float4* reg) {
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
@@ -56,6 +58,7 @@ __device__ __forceinline__ void put(float* dst, const float4* reg) {
   }
 }
 
+template <int LDK>
 __global__ __launch_bounds__(NTH) void disagreement_kernel(EP p) {
   __shared__ float As[BM * LDK];
   __shared__ float Bs[BN * LDK];
@@ -83,8 +86,8 @@ __global__ __launch_bounds__(NTH) void disagreement_kernel(EP p) {
       for (int t = 0; t < 4; ++t) acc[rt][t] = floatx4{0.f, 0.f, 0.f, 0.f};
     for (int kc = 0; kc < nk; ++kc) {
       __syncthreads();  // previous chunk's readers are done
-      put<NA>(As, ra);
-      put<NB>(Bs, rb);
+      put<NA, LDK>(As, ra);
+      put<NB, LDK>(Bs, rb);
       __syncthreads();
       // prefetch the next chunk (this member's next K chunk, or the next member's first) behind the MFMAs
       {
@@ -156,6 +159,19 @@ bool launch_ens_disagreement(const float* X, const float* W, const float* b, flo
   if (n < 1 || M < 1 || O < 1 || H < 4 || (H & 3)) return false;
   srl::ens::EP p{X, W, b, part, n, M, O, H};
   dim3 grid((M + srl::ens::BM - 1) / srl::ens::BM, (O + srl::ens::BN - 1) / srl::ens::BN);
-  hipLaunchKernelGGL(srl::ens::disagreement_kernel, grid, dim3(srl::ens::NTH), 0, st, p);
+  // LDS row stride in floats (64-wide K chunk + padding); 72 measured fastest (1479 us vs 1518 at 68 and 1514 at
+  // 80 for the DV2-P2E shape); SRL_ENS_LDK=68/80 for A/B runs
+  static const int ldk = [] {
+    const char* e = std::getenv("SRL_ENS_LDK");
+    return e ? std::atoi(e) : 72;
+  }();
+  if (ldk == 72)
+    hipLaunchKernelGGL(srl::ens::disagreement_kernel<72>, grid, dim3(srl::ens::NTH), 0, st, p);
+  else if (ldk == 80)
+    hipLaunchKernelGGL(srl::ens::disagreement_kernel<80>, grid, dim3(srl::ens::NTH), 0, st, p);
+  else if (ldk == 68)
+    hipLaunchKernelGGL(srl::ens::disagreement_kernel<68>, grid, dim3(srl::ens::NTH), 0, st, p);
+  else
+    hipLaunchKernelGGL(srl::ens::disagreement_kernel<72>, grid, dim3(srl::ens::NTH), 0, st, p);
   return true;
 }
