@@ -295,7 +295,7 @@ def main():
                 "horizon": cfg.algo.horizon,
                 "parallelism": f"dp{world}",
                 "params": n_params,
-                "hipgraph": bool(trainer.uses_graphs), "graph_mode": "segmented" if trainer.segmented else ("single" if trainer.graphed.enabled else "eager"),
+                "hipgraph": bool(trainer.uses_graphs), "graph_mode": trainer.graph_mode,
                 "fused_ops": ops.fused_enabled(),
             },
             "policy_steps_per_s": round(policy_steps / elapsed, 3),

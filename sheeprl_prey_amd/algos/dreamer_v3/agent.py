@@ -284,7 +284,7 @@ class RSSM(nn.Module):
                 and gru.layer_norm.weight is not None and gru.layer_norm.bias is not None)
 
     @torch.no_grad()
-    def imagine_discrete(self, post: Tensor, h: Tensor, actor: "Actor", horizon: int) -> Tuple[Tensor, Tensor]:
+    def imagine_discrete(self, post: Tensor, h: Tensor, actor: "Actor", horizon: int, record: bool = False):
         """Imagination rollout for discrete actors without autograd (reference loop: ``dreamer_v3.py:
         235-257`` over ``RSSM.imagination`` + ``Actor.forward``; the discrete objective back-propagates
         only through log-probs of detached actions, so no graph is needed).
@@ -293,7 +293,13 @@ class RSSM(nn.Module):
         h): the LN-GRU and unimix-sample kernels store into row-strided slices of it, the recurrent
         GEMM reads (action | prior) in place (weight columns permuted once), the GRU input projection
         is two GEMMs (feat, then h accumulated) instead of a concat.  No per-step concatenations and no
-        final stacks: the trajectories ``[H+1, M, S + Hd]`` and actions ``[H+1, M, A]`` are views."""
+        final stacks: the trajectories ``[H+1, M, S + Hd]`` and actions ``[H+1, M, A]`` are views.
+
+        ``record``: the actor trunk's activations of every step are kept (``ops.mlp_trunk``) and a third
+        value is returned, the ``TrunkRecord`` the actor loss back-propagates through instead of running
+        the actor forward over the trajectories a second time."""
+        from sheeprl_prey_amd.ops.mlp_trunk import TrunkRecord, trunk_layers
+
         C = ops._ext()
         M, S = post.shape
         Hd = h.shape[1]
@@ -304,12 +310,14 @@ class RSSM(nn.Module):
         U = torch.rand(horizon + 1, M * (nh + G), device=post.device)
         # persistent one-launch rollout (imagine.hip): opt-in, it measures 2.27 ms vs 1.85 ms for the
         # in-graph per-op rollout at the Atari-100k shapes (profiles/r2_imagine_persistent.md)
-        if getattr(self, "fused_imagine", os.environ.get("SRL_IMAGINE_IMPL", "ops") == "persist"):
+        layers = trunk_layers(actor.model) if record else None
+        rec = TrunkRecord(layers, horizon + 1, M, post.device) if layers is not None else None
+        if rec is None and getattr(self, "fused_imagine", os.environ.get("SRL_IMAGINE_IMPL", "ops") == "persist"):
             from sheeprl_prey_amd.ops.imagine import fused_imagine
 
             full = fused_imagine(self, actor, post, h, horizon, U)  # one persistent launch (imagine.hip)
             if full is not None:
-                return full[:, :, A:], full[:, :, :A]
+                return (full[:, :, A:], full[:, :, :A]) + ((None,) if record else ())
         buf = post.new_empty(horizon + 1, M, A + S + Hd)
         buf[0, :, A:A + S].copy_(post)
         buf[0, :, A + S:].copy_(h)
@@ -322,7 +330,7 @@ class RSSM(nn.Module):
         WgT_h, WgT_f = Wg[:, :Hd].t(), Wg[:, Hd:].t()
         ln = gru.layer_norm
         for t in range(horizon + 1):
-            out = actor.model(buf[t, :, A:])
+            out = rec.step(t, buf[t, :, A:]) if rec is not None else actor.model(buf[t, :, A:])
             c0 = 0
             for i, (head, a) in enumerate(zip(actor.mlp_heads, actor.actions_dim)):
                 C.unimix_sample_into(head(out), U[t, i * M:(i + 1) * M], int(a), float(actor._unimix), buf[t, :, c0:c0 + a])
@@ -341,7 +349,7 @@ class RSSM(nn.Module):
             C.ln_gru_into(gx, buf[t, :, A + S:], ln.weight, ln.bias, float(ln.eps), buf[t + 1, :, A + S:])
             logits = self.transition_model(buf[t + 1, :, A + S:])
             C.unimix_sample_into(logits.contiguous(), U[t, nh * M:], disc, float(self.unimix), buf[t + 1, :, A:A + S])
-        return buf[:, :, A:], buf[:, :, :A]
+        return (buf[:, :, A:], buf[:, :, :A]) + ((rec,) if record else ())
 
     # ---- MI355X scan: T-step posterior rollout with hoisted GEMMs --------------------
     def _mlp_head(self, mlp: MLP, x_pre: Tensor) -> Tensor:

@@ -65,13 +65,23 @@ class DreamerV3Trainer:
     """One DreamerV3 gradient step as five phases separated by the collectives they need:
 
     ``wm`` (world-model fwd/bwd) | all-reduce(wm grads) | ``imagine`` (wm step, imagination, lambda) |
-    all-gather(lambda) | ``actor`` (Moments, actor fwd/bwd) | all-reduce(actor grads) | ``critic`` (actor
-    step, critic fwd/bwd) | all-reduce(critic grads) | ``final`` (critic step).
+    all-gather(lambda) | ``actor`` (Moments, actor fwd/bwd) | all-reduce(actor grads) | ``critic`` (critic
+    fwd/bwd) | all-reduce(critic grads) | ``final`` (actor step, critic step).
 
-    Execution: one hipGraph for the whole step on a single rank; on N ranks one hipGraph per phase
-    with the RCCL collectives issued eagerly between replays (collectives stay out of captured
-    graphs; for continuous actors the actor phase's backward runs through the imagination graph the
-    previous capture recorded - both captures share one memory pool); otherwise eager."""
+    The critic loss reads neither the actor's weights nor its gradients, so the actor's all-reduce is
+    left in flight across the critic phase and joined by the actor's clip/step in ``final`` (the
+    reference steps the actor before the critic forward, ``dreamer_v3.py:319-327``: same values).
+
+    Execution:
+    * one rank, graphs: ONE hipGraph for the whole step;
+    * N ranks over RCCL, graphs (``fabric.graph_collectives``, default): still ONE hipGraph per rank -
+      the collectives are captured in it; the world-model buckets launch from the backward hooks and
+      overlap the rest of the world-model backward, the actor all-reduce overlaps the critic phase;
+    * N ranks otherwise (gloo, or ``graph_collectives=False``): one hipGraph per phase with the
+      collectives issued eagerly between replays (for continuous actors the actor phase's backward
+      then runs through the imagination graph the previous capture recorded; both captures share one
+      memory pool);
+    * no graphs: eager."""
 
     PHASES = ("wm", "imagine", "actor", "critic", "final")
 
@@ -85,12 +95,19 @@ class DreamerV3Trainer:
         self.is_continuous = is_continuous
         self.actions_dim = list(actions_dim)
         self.target_flat = flatten_like(target_critic, critic_optimizer)
+        # discrete fast path: record the rollout's actor forward and keep the imagination critic forward's
+        # graph, so the actor / critic losses skip their second forwards (A/B switch SRL_REUSE_FWD=0)
+        self.reuse_forwards = os.environ.get("SRL_REUSE_FWD", "1") != "0"
         self._st: Dict[str, Any] = {}
         self._gather_buf = None
         ws = runner.world_size
         graphs = bool(runner.cuda_graphs)
-        self.segmented = graphs and (force_segmented or ws > 1)
-        single = graphs and ws == 1 and not self.segmented
+        capture_coll = ws > 1 and getattr(runner, "capture_collectives", False)
+        self.segmented = graphs and (force_segmented or (ws > 1 and not capture_coll))
+        single = graphs and not self.segmented
+        self.graph_mode = "segmented" if self.segmented else (("single+rccl" if ws > 1 else "single") if single else "eager")
+        # the actor all-reduce overlaps the critic phase wherever the step is not cut between phases
+        self.defer_actor_sync = not self.segmented
         self.graphed = GraphedStep(self._full_step, warmup=2, enabled=single, name="dreamer_v3_train")
         if self.segmented:
             from sheeprl_prey_amd.parallel.graphs import SegmentedGraph
@@ -134,7 +151,7 @@ class DreamerV3Trainer:
 
     def _coll_actor(self, dry: bool = False) -> None:
         if not dry:
-            self.runner.sync_gradients(self.actor_optimizer)
+            self.runner.sync_gradients(self.actor_optimizer, wait=not self.defer_actor_sync)
 
     def _coll_critic(self, dry: bool = False) -> None:
         if not dry:
@@ -231,7 +248,10 @@ class DreamerV3Trainer:
             h = st["recurrent_states"].reshape(-1, H)
             fast = (not self.is_continuous and prior.is_cuda and wm.rssm.imagine_fast_ok(actor))
             if fast:
-                imagined_trajectories, imagined_actions_t = wm.rssm.imagine_discrete(prior, h, actor, cfg.algo.horizon)
+                res = wm.rssm.imagine_discrete(prior, h, actor, cfg.algo.horizon, record=self.reuse_forwards)
+                imagined_trajectories, imagined_actions_t = res[0], res[1]
+                if len(res) > 2 and res[2] is not None:
+                    st["actor_rec"] = res[2]
             else:
                 latent = torch.cat((prior, h), -1)
                 trajectories: List[Tensor] = [latent]
@@ -246,7 +266,15 @@ class DreamerV3Trainer:
                     imagined_actions.append(actions)
                 imagined_trajectories = torch.stack(trajectories)
                 imagined_actions_t = torch.stack(imagined_actions)
-            predicted_values = ops.twohot_mean(critic(imagined_trajectories))
+            if fast and self.reuse_forwards:
+                # the critic's forward over the trajectories, WITH its graph: the critic loss of this step
+                # (same weights - the critic steps in the final phase - same detached inputs) reuses it
+                # instead of running the critic forward a second time (reference dreamer_v3.py:260, :327)
+                with torch.enable_grad():
+                    st["critic_logits"] = critic(imagined_trajectories)
+                predicted_values = ops.twohot_mean(st["critic_logits"].detach())
+            else:
+                predicted_values = ops.twohot_mean(critic(imagined_trajectories))
             predicted_rewards = ops.twohot_mean(wm.reward_model(imagined_trajectories))
             # continuation flags, their gamma-discounts and the cumulative discount: one kernel (K11)
             cont_g, discount = ops.imag_discount(wm.continue_model(imagined_trajectories), data["dones"],
@@ -262,13 +290,23 @@ class DreamerV3Trainer:
     def _phase_actor(self, data: Dict[str, Tensor]) -> None:
         cfg, st = self.cfg, self._st
         self.actor_optimizer.zero_grad(set_to_none=True)
-        policies = self.actor(st["imagined_trajectories"].detach())[1]
+        rec = st.pop("actor_rec", None)
+        if rec is not None:
+            # the rollout recorded the actor trunk: heads + unimix over its output, backward through the
+            # recorded activations (ops/mlp_trunk.py) - no second actor forward
+            trunk = rec.output(st["imagined_trajectories"].detach())
+            mixed = [ops.unimix_sample(head(trunk), int(a), float(self.actor._unimix), sample=False)[0]
+                     for head, a in zip(self.actor.mlp_heads, self.actions_dim)]
+            policies = None  # built from ``mixed`` only if the eager objective below is needed
+        else:
+            policies = self.actor(st["imagined_trajectories"].detach())[1]
+            mixed = None if self.is_continuous else [p.logits for p in policies]
         lambda_values = st["lambda_values"]
         baseline = st["predicted_values"][:-1]
         offset, invscale = self.moments.update(st["gathered"])
         if not self.is_continuous:
             # advantage, log-probs, entropies, discounting and the mean in one kernel (actor_loss.hip)
-            z = torch.cat([p.logits for p in policies], -1) if len(policies) > 1 else policies[0].logits
+            z = torch.cat(mixed, -1) if len(mixed) > 1 else mixed[0]
             T = z.shape[0]
             policy_loss = ops.actor_loss_discrete(
                 z, st["imagined_actions"], lambda_values.reshape(T - 1, -1), baseline.reshape(T - 1, -1),
@@ -277,6 +315,8 @@ class DreamerV3Trainer:
                 policy_loss.backward()
                 st["out"]["Loss/policy_loss"] = policy_loss.detach()
                 return
+        if policies is None:
+            policies = [OneHotCategoricalValidateArgs(logits=m, validate_args=False) for m in mixed]
         advantage = (lambda_values - offset) / invscale - (baseline - offset) / invscale
         if self.is_continuous:
             objective = advantage
@@ -295,14 +335,9 @@ class DreamerV3Trainer:
 
     def _phase_critic(self, data: Dict[str, Tensor]) -> None:
         cfg, st = self.cfg, self._st
-        clip = cfg.algo.actor.clip_gradients
-        if clip is not None and clip > 0:
-            st["out"]["Grads/actor"] = self.runner.clip_gradients(self.actor, self.actor_optimizer, max_norm=clip).detach()
-        else:
-            st["out"]["Grads/actor"] = torch.zeros((), device=data["rewards"].device)
-        self.actor_optimizer.step()
         traj = st["imagined_trajectories"].detach()[:-1]
-        qv_logits = self.critic(traj)
+        qv_full = st.pop("critic_logits", None)
+        qv_logits = qv_full[:-1] if qv_full is not None else self.critic(traj)
         with torch.no_grad():
             target_values = ops.twohot_mean(self.target_critic(traj))
         self.critic_optimizer.zero_grad(set_to_none=True)
@@ -313,15 +348,28 @@ class DreamerV3Trainer:
 
     def _phase_final(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:
         cfg, st = self.cfg, self._st
+        clip = cfg.algo.actor.clip_gradients
+        # joins the actor all-reduce left in flight across the critic phase
+        if clip is not None and clip > 0:
+            st["out"]["Grads/actor"] = self.runner.clip_gradients(self.actor, self.actor_optimizer, max_norm=clip).detach()
+        else:
+            st["out"]["Grads/actor"] = torch.zeros((), device=data["rewards"].device)
+        self.actor_optimizer.step()
         clip = cfg.algo.critic.clip_gradients
         if clip is not None and clip > 0:
             st["out"]["Grads/critic"] = self.runner.clip_gradients(self.critic, self.critic_optimizer, max_norm=clip).detach()
         else:
             st["out"]["Grads/critic"] = torch.zeros((), device=data["rewards"].device)
         self.critic_optimizer.step()
-        self.actor_optimizer.zero_grad(set_to_none=True)
-        self.critic_optimizer.zero_grad(set_to_none=True)
-        self.world_optimizer.zero_grad(set_to_none=True)
+        # clean-up zeros (not armed: the next backward reaching these parameters may belong to another
+        # loss, e.g. the continuous actor loss flowing into the critic), and drop every autograd-carrying
+        # hand-off so no graph of this step outlives it
+        self.actor_optimizer.zero_grad(set_to_none=True, arm=False)
+        self.critic_optimizer.zero_grad(set_to_none=True, arm=False)
+        self.world_optimizer.zero_grad(set_to_none=True, arm=False)
+        for k, v in list(st.items()):
+            if torch.is_tensor(v) and v.grad_fn is not None:
+                st[k] = v.detach()  # same storage (the segmented collectives re-read it), no graph
         return dict(st["out"])
 
 
@@ -458,8 +506,10 @@ def main(runner, cfg: Dict[str, Any]):
         random_actions = update <= learning_starts and state is None and "minedojo" not in cfg.algo.actor.cls.lower()
         train_now = update >= learning_starts and updates_before_training - 1 <= 0
         n_samples = (cfg.algo.per_rank_pretrain_steps if update == learning_starts else cfg.algo.per_rank_gradient_steps)
-        with timer("Time/env_interaction_time"):
-            infos = loop.step(random_actions, (lambda: train_burst(n_samples)) if train_now else None)
+        t_int = time.perf_counter()
+        infos = loop.step(random_actions, (lambda: train_burst(n_samples)) if train_now else None)
+        # the gradient steps launched inside the interaction step are charged to Time/train_time only
+        timer.add("Time/env_interaction_time", time.perf_counter() - t_int - loop.last_train_host_s)
 
         for i, ep_rew, ep_len in episode_stats(infos):
             aggregator.update("Rewards/rew_avg", ep_rew)
@@ -481,6 +531,7 @@ def main(runner, cfg: Dict[str, Any]):
                 e1.synchronize()
                 timer.add("Time/train_time", e0.elapsed_time(e1) / 1e3)
             train_events.clear()
+            rb.check_gather_error()
             runner.log_dict(aggregator.compute(), policy_step)
             aggregator.reset()
             log_throughput(runner, timer.compute(), policy_step, last_log, train_step, last_train, cfg.env.action_repeat)

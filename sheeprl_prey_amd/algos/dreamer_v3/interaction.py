@@ -9,12 +9,20 @@ One step on the GPU, in stream order:
                  event -> replay-buffer add of the row (+ action) -> [gradient steps: graph launches]
     host: wait(readback event) only -> env.step on the CPU while the GPU trains -> bookkeeping
 
-The order of effects is the reference's act / env step / add / train order (the row a gradient step
-samples is added before it, the next action uses the trained weights); the env step needs only the
-action, so it overlaps the training graphs instead of waiting for them.  CPU runs keep the serial form.
+Order of effects vs the reference (act / add / env step / add reset rows / train,
+``dreamer_v3.py:609-709``): the row a gradient step samples is added before it and the next action
+uses the trained weights, as there; the gradient steps are launched BEFORE the env step so the CPU
+env step overlaps them.  Divergence: the reset rows (final obs, ``done=1``) of episodes that end at
+this env step are added after this step's gradient launch, so they reach training one step later
+than in the reference.  CPU runs keep the same order in serial form.
+
+``last_train_host_s`` is the host time spent inside ``train_fn`` during the last ``step``; callers
+timing the env interaction subtract it (the reference times interaction and training separately,
+``dreamer_v3.py:592`` vs ``:711``).
 """
 from __future__ import annotations
 
+import time
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
 import numpy as np
@@ -40,6 +48,7 @@ class InteractionLoop:
         self.step_data = TensorDict({}, batch_size=[self.ne], device="cpu")
         self._slot = 0
         self._ring: List[Dict[str, torch.Tensor]] = []
+        self.last_train_host_s = 0.0
 
     # ------------------------------------------------------------------ setup
     def _obs_tensor(self, k: str, v) -> torch.Tensor:
@@ -121,10 +130,25 @@ class InteractionLoop:
         self.rb.add(row[None, ...])
 
     # ------------------------------------------------------------------ one step
+    def _timed(self, fn: Optional[Callable[[], Any]]):
+        if fn is None:
+            return None
+
+        def run():
+            t0 = time.perf_counter()
+            try:
+                return fn()
+            finally:
+                self.last_train_host_s += time.perf_counter() - t0
+
+        return run
+
     def step(self, random_actions: bool, train_fn: Optional[Callable[[], Any]] = None) -> Dict[str, Any]:
         """Act (random or policy), add the row, run ``train_fn`` (launched before the env step on the
         GPU path), step the envs.  Returns the env ``infos``."""
         cfg, ne = self.cfg, self.ne
+        train_fn = self._timed(train_fn)
+        self.last_train_host_s = 0.0
         if random_actions:
             real, acts = self._random_actions()
             self.step_data["actions"] = torch.from_numpy(np.asarray(acts, dtype=np.float32)).view(ne, -1)

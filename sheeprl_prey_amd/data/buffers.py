@@ -304,11 +304,24 @@ class SequentialReplayBuffer(ReplayBuffer):
         keys = list(self._buf.keys())
         if batch_idxes.is_cuda and 0 < len(keys) <= 16 and ops.fused_enabled() and all(
                 self._buf[k].is_cuda and self._buf[k].is_contiguous() for k in keys):
-            # every key's sequence rows in one gather launch (ops/csrc/gather.hip)
+            # every key's sequence rows in one gather launch (ops/csrc/gather.hip); an out-of-range index
+            # zero-fills its row and raises the device error word read by ``check_gather_error``
+            err = getattr(self, "_gather_err", None)
+            if err is None or err.device != batch_idxes.device:
+                err = self._gather_err = torch.zeros(1, dtype=torch.int32, device=batch_idxes.device)
             outs = ops._ext().gather_rows([self._buf[k] for k in keys], batch_idxes.reshape(-1).contiguous(),
-                                          env_idxes.reshape(-1).contiguous())
+                                          env_idxes.reshape(-1).contiguous(), err)
             return TensorDict(dict(zip(keys, outs)), batch_size=[batch_idxes.numel()], device=self._buf.device).view(*shape)
         return self._buf[batch_idxes.reshape(-1), env_idxes.reshape(-1)].view(*shape)
+
+
+    def check_gather_error(self) -> None:
+        """Host check of the gather kernel's error word (off the hot path: log / checkpoint time)."""
+        err = getattr(self, "_gather_err", None)
+        if err is not None and int(err.item()) != 0:
+            err.zero_()
+            raise RuntimeError("SequentialReplayBuffer: a sampled (row, env) index was outside the store; "
+                               "the affected sample rows were zero-filled")
 
 
 class EpisodeBuffer:
@@ -515,6 +528,12 @@ class AsyncReplayBuffer:
 
     def __len__(self) -> int:
         return self.buffer_size
+
+    def check_gather_error(self) -> None:
+        """Raise if any per-env sequential buffer's gather kernel saw an out-of-range index."""
+        for b in self._buf or ():
+            if isinstance(b, SequentialReplayBuffer):
+                b.check_gather_error()
 
     def _init(self) -> None:
         cls = SequentialReplayBuffer if self._sequential else ReplayBuffer

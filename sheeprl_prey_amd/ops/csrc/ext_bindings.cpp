@@ -48,7 +48,7 @@ void launch_gru_cell_fwd(const float* gi, const float* gh, const float* h, float
 void launch_gru_cell_bwd(const float* gh, const float* h, const float* rzn, const float* dhn, float* dgi, float* dgh, float* dh,
                          int B, int H, hipStream_t st);
 void launch_gather_rows(const void* const* src, void* const* dst, const long* row_bytes, int nk, int n_envs, long cap, int N,
-                        const long* row, const long* env, hipStream_t st);
+                        const long* row, const long* env, int* err, hipStream_t st);
 int actor_loss_blocks(int rows);
 void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
@@ -521,8 +521,10 @@ std::vector<torch::Tensor> gru_cell_bwd(torch::Tensor gh, torch::Tensor h, torch
 }
 
 // ------------------------------------------------------------------ replay row gather (gather.hip)
-// srcs[k] [capacity, n_envs, ...] contiguous; row / env int64 [N] -> outputs [N, ...] per key
-std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::Tensor row, torch::Tensor env) {
+// srcs[k] [capacity, n_envs, ...] contiguous; row / env int64 [N] -> outputs [N, ...] per key.  ``err``
+// (optional int32 [1]) is or-ed with 1 when an index is out of range; that row comes back zero-filled.
+std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::Tensor row, torch::Tensor env,
+                                       c10::optional<torch::Tensor> err) {
   TORCH_CHECK(!srcs.empty() && srcs.size() <= 16, "gather_rows: 1..16 keys");
   TORCH_CHECK(row.is_cuda() && env.is_cuda() && row.scalar_type() == torch::kLong && env.scalar_type() == torch::kLong &&
                   row.is_contiguous() && env.is_contiguous() && row.numel() == env.numel(),
@@ -544,14 +546,20 @@ std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::T
     rb.push_back((long)(s.numel() / (s.size(0) * n_envs) * s.element_size()));
     outs.push_back(o);
   }
+  int* errp = nullptr;
+  if (err.has_value() && err->defined()) {
+    TORCH_CHECK(err->is_cuda() && err->scalar_type() == torch::kInt && err->numel() >= 1, "gather_rows: err int32 [1]");
+    errp = err->data_ptr<int>();
+  }
   if (N > 0)
     launch_gather_rows(sp.data(), dp.data(), rb.data(), (int)srcs.size(), (int)n_envs, (long)cap, (int)N, row.data_ptr<int64_t>(),
-                       env.data_ptr<int64_t>(), stream());
+                       env.data_ptr<int64_t>(), errp, stream());
   return outs;
 }
 
 void register_ext(pybind11::module& m) {
-  m.def("gather_rows", &gather_rows);
+  m.def("gather_rows", &gather_rows, pybind11::arg("srcs"), pybind11::arg("row"), pybind11::arg("env"),
+        pybind11::arg("err") = pybind11::none());
   m.def("gru_cell_fwd", &gru_cell_fwd);
   m.def("gru_cell_bwd", &gru_cell_bwd);
   m.def("lstm_fwd", &lstm_fwd);

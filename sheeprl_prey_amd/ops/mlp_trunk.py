@@ -1,0 +1,120 @@
+"""Recorded MLP trunks: run an ``[Linear -> LayerNorm(+act)] * L`` stack step by step inside a rollout,
+keep every step's activations in ``[R, M, N]`` slabs, and back-propagate through ALL R steps later as
+one batch of ``R*M`` rows.
+
+Why (DreamerV3 discrete imagination, reference ``dreamer_v3.py:235-301``): the reference runs the actor
+on each imagined latent during the H=15 rollout (to pick the next action) and then AGAIN over the
+stacked trajectories ``[H+1, B*T, latent]`` to build the policy loss - the same weights on the same
+inputs.  Recording the rollout's forward (pre-LayerNorm GEMM outputs, row statistics, activations)
+removes the second forward entirely (~35 GFLOP, 3 GEMMs + 2 LayerNorms at the Atari-100k shapes); the
+backward is the usual per-layer chain at ``M = (H+1)*B*T`` rows: ``ln_act_bwd`` (HIP), ``dW = dpre^T x``
+and ``dx = dpre W`` (library GEMMs), bias gradients by the column-sum kernel.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+from torch import Tensor, nn
+
+from sheeprl_prey_amd import ops
+
+
+def trunk_layers(mlp: nn.Module) -> Optional[List[Tuple[nn.Linear, nn.Module]]]:
+    """``[(Linear, fused LayerNorm)]`` of an MLP built as ``[Linear, LayerNorm(act), Identity] * L``
+    (``models.MLP`` after ``fuse_norm_act``); None for any other layout (dropout, no norm, ...)."""
+    from sheeprl_prey_amd.utils.model import LayerNorm
+
+    seq = getattr(mlp, "model", mlp)
+    if getattr(mlp, "flatten_dim", None) is not None:
+        return None
+    mods = list(seq)
+    if len(mods) % 3:
+        return None
+    out = []
+    for i in range(0, len(mods), 3):
+        lin, ln, ident = mods[i : i + 3]
+        if not (isinstance(lin, nn.Linear) and type(ln) is LayerNorm and isinstance(ident, nn.Identity)):
+            return None
+        if len(ln.normalized_shape) != 1 or ln.weight is None or ln.bias is None or ln.normalized_shape[0] != lin.out_features:
+            return None
+        out.append((lin, ln))
+    return out or None
+
+
+class TrunkRecord:
+    """Activation slabs of one recorded rollout: ``rows`` steps of ``M`` rows through ``layers``."""
+
+    def __init__(self, layers: Sequence[Tuple[nn.Linear, nn.Module]], rows: int, M: int, device) -> None:
+        self.layers = list(layers)
+        self.R, self.M = rows, M
+        self.pre = [torch.empty(rows, M, lin.out_features, device=device) for lin, _ in self.layers]
+        self.y = [torch.empty(rows, M, lin.out_features, device=device) for lin, _ in self.layers]
+        self.mean = [torch.empty(rows, M, device=device) for _ in self.layers]
+        self.rstd = [torch.empty(rows, M, device=device) for _ in self.layers]
+        self.inp: Optional[Tensor] = None  # [R, M, K0] (may be a row-strided view)
+
+    @torch.no_grad()
+    def step(self, t: int, x: Tensor) -> Tensor:
+        """Forward of step ``t`` on ``x`` [M, K0] (row stride allowed); returns the trunk output [M, N]."""
+        C = ops._ext()
+        M = self.M
+        for i, (lin, ln) in enumerate(self.layers):
+            pre = self.pre[i][t]
+            if lin.bias is not None:
+                torch.addmm(lin.bias, x, lin.weight.t(), out=pre)
+            else:
+                torch.mm(x, lin.weight.t(), out=pre)
+            N = pre.shape[-1]
+            C.ln_act_fwd_into(pre, N, self.y[i][t], N, ln.weight, ln.bias, self.mean[i][t], self.rstd[i][t], M, N, 1,
+                              float(ln.eps), ops._act_code(ln.act))
+            x = self.y[i][t]
+        return x
+
+    def output(self, inputs: Tensor) -> Tensor:
+        """The recorded trunk output ``[R, M, N]`` as a tensor whose backward runs the batched chain.
+        ``inputs`` [R, M, K0]: the rollout's trunk inputs (their gradient is not computed: the DV3
+        actor reads detached latents)."""
+        self.inp = inputs
+        params = []
+        for lin, ln in self.layers:
+            params += [lin.weight, lin.bias if lin.bias is not None else _NONE, ln.weight, ln.bias]
+        return _RecordedTrunk.apply(self, *params)
+
+
+_NONE = torch.empty(0)
+
+
+class _RecordedTrunk(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, rec: TrunkRecord, *params):
+        ctx.rec = rec
+        # a fresh alias of the last activation slab: autograd owns the returned tensor's grad_fn
+        return rec.y[-1].view_as(rec.y[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        rec: TrunkRecord = ctx.rec
+        C = ops._ext()
+        RM = rec.R * rec.M
+        L = len(rec.layers)
+        grads: List[Optional[Tensor]] = [None] * (4 * L)
+        dy = dy.reshape(RM, -1)
+        if dy.stride(-1) != 1 or dy.stride(0) != dy.shape[-1]:
+            dy = dy.contiguous()
+        for i in reversed(range(L)):
+            lin, ln = rec.layers[i]
+            N = lin.out_features
+            pre = rec.pre[i].view(RM, N)
+            dpre, dg, db = C.ln_act_bwd(pre, dy, ln.weight, ln.bias, rec.mean[i].view(RM), rec.rstd[i].view(RM),
+                                        ops._act_code(ln.act))
+            x = rec.y[i - 1].view(RM, -1) if i > 0 else rec.inp.reshape(RM, rec.inp.shape[-1])
+            grads[4 * i] = dpre.t().mm(x) if lin.weight.requires_grad else None
+            if lin.bias is not None and lin.bias.requires_grad:
+                grads[4 * i + 1] = C.colsum(dpre)
+            grads[4 * i + 2] = dg if ln.weight.requires_grad else None
+            grads[4 * i + 3] = db if ln.bias.requires_grad else None
+            if i > 0:
+                dy = dpre.mm(lin.weight)
+        ctx.rec = None
+        return (None, *grads)

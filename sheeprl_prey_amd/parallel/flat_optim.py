@@ -135,13 +135,24 @@ class FlatOptimizer:
             if p.grad is None or p.grad.data_ptr() != self.flat_grad[off:].data_ptr():
                 p.grad = self.flat_grad[off : off + p.numel()].view_as(p)
 
-    def zero_grad(self, set_to_none: bool = True) -> None:
+    def zero_grad(self, set_to_none: bool = True, arm: bool = True) -> None:
         """``set_to_none`` (default): the next backward lets autograd hand each parameter its freshly
         computed gradient (AccumulateGrad steals the buffer: no per-parameter accumulate kernel), and
         the slab is rebuilt by ``_gather`` - one memset + multi-tensor copies - before anything reads
-        it.  Otherwise the slab is zeroed and grads accumulate into it in place."""
-        if getattr(self, "_ov", None) is not None:
-            self.arm_overlap()
+        it.  Otherwise the slab is zeroed and grads accumulate into it in place.
+
+        ``arm`` starts an overlapped all-reduce round (``enable_overlap``): pass ``False`` for a
+        clean-up zero that is not followed by the backward its sync belongs to - a backward of another
+        loss reaching these parameters must not launch collectives."""
+        self.wait_grads()
+        ov = getattr(self, "_ov", None)
+        if ov is not None:
+            if arm:
+                self.arm_overlap()
+            else:
+                for w in ov["works"]:
+                    w.wait()
+                ov.update(armed=False, works=[])
         if set_to_none:
             for p in self.params:
                 p.grad = None
@@ -178,13 +189,14 @@ class FlatOptimizer:
     def clip_grad_norm_(self, max_norm: float) -> Tensor:
         from sheeprl_prey_amd import ops
 
+        self.wait_grads()
         self._gather()
         norm = ops.flat_grad_norm(self.flat_grad, self.scalars, float(max_norm))
         self._advanced = True
         return norm
 
     # ------------------------------------------------------------------ overlapped gradient all-reduce
-    def enable_overlap(self, group=None, world_size: int = 1, bucket_mb: float = 32) -> bool:
+    def enable_overlap(self, group=None, world_size: int = 1, bucket_mb: float = 32, in_capture: bool = False) -> bool:
         """Bucketed all-reduce overlapped with the backward (eager multi-rank paths).
 
         The slab is cut into buckets from its tail (parameters are laid out in forward order, so
@@ -196,9 +208,16 @@ class FlatOptimizer:
         ``all_reduce_grads`` (``Runner.backward`` / ``Runner.sync_gradients`` pair them), so extra
         backward passes that accumulate into the same slab never trigger a collective.  Contract: ONE
         backward between ``zero_grad`` (which arms) and the sync, as every algorithm here does.
-        Reference counterpart: the per-model DDP reducers of ``dreamer_v3/agent.py:1054-1063``."""
+        Reference counterpart: the per-model DDP reducers of ``dreamer_v3/agent.py:1054-1063``.
+
+        ``in_capture``: the hooks also launch their buckets while a hipGraph is being captured (RCCL
+        collectives are stream-capturable), so a graph-captured multi-rank step overlaps the gradient
+        all-reduce with the rest of its backward exactly like the eager path."""
         if world_size <= 1 or getattr(self, "_ov", None) is not None:
-            return getattr(self, "_ov", None) is not None
+            ov = getattr(self, "_ov", None)
+            if ov is not None:
+                ov["in_capture"] = ov["in_capture"] or in_capture
+            return ov is not None
         if self.flat_grad._base is not None or any(
                 getattr(p, "_flat_slab", (None,))[0] is not None and p._flat_slab[0]() is not self for p in self.params):
             return False  # slab shared with another optimiser: keep the plain path
@@ -226,7 +245,7 @@ class FlatOptimizer:
         use_avg = g.is_cuda and dist.get_backend(group) == "nccl"
         self._ov = dict(group=group, ws=world_size, buckets=buckets, ranges=ranges, bucket_of=bucket_of,
                         op=dist.ReduceOp.AVG if use_avg else dist.ReduceOp.SUM, avg=use_avg, armed=False,
-                        pending=[], seen=[], works=[], next=0)
+                        pending=[], seen=[], works=[], next=0, in_capture=bool(in_capture))
         self._ov_handles = [p.register_post_accumulate_grad_hook(self._make_ov_hook(i)) for i, p in enumerate(self.params)]
         return True
 
@@ -235,9 +254,13 @@ class FlatOptimizer:
 
         def hook(p: Tensor) -> None:
             self_ = ref()
-            # inside a hipGraph capture (segmented multi-rank graphs) the collectives stay between replays
-            if self_ is not None and self_._ov["armed"] and not (p.is_cuda and torch.cuda.is_current_stream_capturing()):
-                self_._ov_ready(i, p)
+            # inside a hipGraph capture the collectives are captured too only in the single-graph RCCL mode
+            # (``in_capture``); the segmented mode keeps them between replays
+            if self_ is None or not self_._ov["armed"]:
+                return
+            if p.is_cuda and torch.cuda.is_current_stream_capturing() and not self_._ov["in_capture"]:
+                return
+            self_._ov_ready(i, p)
 
         return hook
 
@@ -279,7 +302,7 @@ class FlatOptimizer:
             ov["works"].append(dist.all_reduce(self.flat_grad[lo:hi], op=ov["op"], group=ov["group"], async_op=True))
             ov["next"] += 1
 
-    def _ov_finish(self) -> None:
+    def _ov_finish(self, wait: bool = True) -> None:
         ov = self._ov
         # parameters that got no gradient in this backward: a zero slab view (set_to_none) or the
         # accumulated one already there
@@ -295,16 +318,20 @@ class FlatOptimizer:
                 ov["pending"][ov["bucket_of"][i]] -= 1
         self._detached = False
         self._ov_launch_ready()
-        for w in ov["works"]:
-            w.wait()
+        works = ov["works"]
         ov.update(armed=False, works=[])
-        if not ov["avg"]:
-            self.flat_grad.div_(ov["ws"])
+        self._pending = (works, None if ov["avg"] else ov["ws"])
+        if wait:
+            self.wait_grads()
 
-    def all_reduce_grads(self, group=None, world_size: int = 1, bucket_mb: int = 32) -> None:
+    def all_reduce_grads(self, group=None, world_size: int = 1, bucket_mb: int = 32, wait: bool = True) -> None:
+        """Average the gradient slab over ``group`` (bucketed for xGMI).  ``wait=False`` leaves the
+        collectives in flight: ``wait_grads`` - called by ``clip_grad_norm_`` / ``step`` before they read
+        the slab - joins them, so the caller may run independent work meanwhile (on a graph-captured
+        step the join is a stream dependency, the overlap is recorded in the graph)."""
         ov = getattr(self, "_ov", None)
         if ov is not None and ov["armed"]:
-            self._ov_finish()
+            self._ov_finish(wait)
             return
         self._gather()
         if world_size <= 1:
@@ -313,19 +340,28 @@ class FlatOptimizer:
         use_avg = g.is_cuda and dist.get_backend(group) == "nccl"
         op = dist.ReduceOp.AVG if use_avg else dist.ReduceOp.SUM
         bucket = max(1, int(bucket_mb * (1 << 20) // 4))
-        if g.numel() <= bucket:
-            dist.all_reduce(g, op=op, group=group)
-        else:
-            works = [dist.all_reduce(g[i : i + bucket], op=op, group=group, async_op=True) for i in range(0, g.numel(), bucket)]
-            for w in works:
-                w.wait()
-        if not use_avg:
-            g.div_(world_size)
+        works = [dist.all_reduce(g[i : i + bucket], op=op, group=group, async_op=True) for i in range(0, g.numel(), bucket)]
+        self._pending = (works, None if use_avg else world_size)
+        if wait:
+            self.wait_grads()
+
+    def wait_grads(self) -> None:
+        """Join the gradient collectives ``all_reduce_grads(wait=False)`` left in flight."""
+        pending = getattr(self, "_pending", None)
+        if pending is None:
+            return
+        self._pending = None
+        works, div = pending
+        for w in works:
+            w.wait()
+        if div is not None:
+            self.flat_grad.div_(div)
 
     @torch.no_grad()
     def step(self, closure=None):
         from sheeprl_prey_amd import ops
 
+        self.wait_grads()
         self._gather()
         if not self._advanced:
             ops.flat_advance(self.scalars)

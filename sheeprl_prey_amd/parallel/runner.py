@@ -158,6 +158,7 @@ class Runner:
         bucket_mb: float = 32,
         tunable_gemm: str = "use",
         overlap_grad_sync: bool = True,
+        graph_collectives: bool = True,
         process_group=None,
         **_unused,
     ) -> None:
@@ -177,12 +178,15 @@ class Runner:
         self.bucket_mb = float(bucket_mb)
         # bucketed all-reduce launched from backward hooks (FlatOptimizer.enable_overlap)
         self.overlap_grad_sync = bool(overlap_grad_sync)
+        # multi-rank hipGraph steps: capture the RCCL collectives INSIDE the one step graph (N ranks replay
+        # one graph each, like N=1) instead of per-phase graphs with eager collectives in between
+        self.graph_collectives = bool(graph_collectives)
         # library-GEMM solution choice (parallel/gemm_tuning.py): committed TunableOp results
         self.tunable_gemm = str(tunable_gemm)
         self._kwargs = dict(
             devices=devices, num_nodes=num_nodes, strategy=strategy, accelerator=accelerator,
             precision=precision, callbacks=callbacks, cuda_graphs=cuda_graphs, fused_ops=fused_ops, bucket_mb=bucket_mb,
-            tunable_gemm=tunable_gemm, overlap_grad_sync=overlap_grad_sync,
+            tunable_gemm=tunable_gemm, overlap_grad_sync=overlap_grad_sync, graph_collectives=graph_collectives,
         )
         self.group = process_group  # None == WORLD
         if str(strategy).lower() in ("fsdp",):
@@ -229,6 +233,11 @@ class Runner:
         if forced:
             return forced
         return "nccl" if self.accelerator == "cuda" else "gloo"
+
+    @property
+    def capture_collectives(self) -> bool:
+        """Graph-captured steps may record their gradient collectives (RCCL only: gloo is host-side)."""
+        return self.cuda_graphs and self.graph_collectives and self.backend == "nccl" and self.accelerator == "cuda"
 
     @property
     def logger(self):
@@ -352,16 +361,19 @@ class Runner:
         if optimizer is not None:
             self.sync_gradients(optimizer)
 
-    def sync_gradients(self, optimizer) -> None:
+    def sync_gradients(self, optimizer, wait: bool = True) -> None:
+        """Average ``optimizer``'s gradients over the ranks.  ``wait=False`` (flat optimisers): the
+        collectives stay in flight until the optimiser's next ``clip_grad_norm_`` / ``step`` joins them."""
         if self.world_size <= 1:
             return
         from sheeprl_prey_amd.parallel.flat_optim import FlatOptimizer
 
         if isinstance(optimizer, FlatOptimizer):
-            optimizer.all_reduce_grads(self.group, self.world_size, bucket_mb=self.bucket_mb)
+            optimizer.all_reduce_grads(self.group, self.world_size, bucket_mb=self.bucket_mb, wait=wait)
             if self.overlap_grad_sync:
                 # from the next zero_grad on, buckets launch from the backward hooks (same call on every rank)
-                optimizer.enable_overlap(self.group, self.world_size, bucket_mb=self.bucket_mb)
+                optimizer.enable_overlap(self.group, self.world_size, bucket_mb=self.bucket_mb,
+                                         in_capture=self.capture_collectives)
             return
         grads = [p.grad for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
         if not grads:

@@ -273,3 +273,39 @@ def test_player_graphed_steps_and_resets():
     player.init_states()
     assert player.recurrent_state.data_ptr() == buf_ptr
     torch.testing.assert_close(player.recurrent_state, h0)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_dv3_forward_reuse_matches_recompute(graphs):
+    """Recorded actor trunk + reused critic forward (``reuse_forwards``) vs the reference-shaped second
+    forwards: same losses and the same updated weights after one step from the same state/RNG."""
+    import copy
+
+    tr = _build(graphs=False)
+    data = _data()
+    tr.train_step(data)  # move off the initial state (Moments, Adam moments)
+    torch.cuda.synchronize()
+    opts = (tr.world_optimizer, tr.actor_optimizer, tr.critic_optimizer)
+    snap = [(o.flat_param.clone(), o.exp_avg.clone(), o.exp_avg_sq.clone(), o.scalars.clone()) for o in opts]
+    msnap = copy.deepcopy(tr.moments.state_dict())
+    results = []
+    for reuse in (False, True):
+        for o, (p, m, v, sc) in zip(opts, snap):
+            o.flat_param.copy_(p); o.exp_avg.copy_(m); o.exp_avg_sq.copy_(v); o.scalars.copy_(sc)
+        tr.moments.load_state_dict(msnap)
+        tr.reuse_forwards = reuse
+        tr.graphed.enabled = graphs
+        tr.graphed.graph = None
+        tr.graphed._calls = 0
+        torch.manual_seed(123)
+        torch.cuda.manual_seed(123)
+        if graphs:
+            tr.graphed.warmup = 0
+        out = tr.train_step(data)
+        torch.cuda.synchronize()
+        results.append(({k: float(v) for k, v in out.items()}, [o.flat_param.clone() for o in opts]))
+    (o0, p0), (o1, p1) = results
+    for k in ("Loss/policy_loss", "Loss/value_loss", "Grads/actor", "Grads/critic"):
+        assert abs(o0[k] - o1[k]) <= 1e-4 * max(1.0, abs(o0[k])), (k, o0[k], o1[k])
+    for a, b in zip(p0, p1):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
