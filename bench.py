@@ -248,6 +248,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # loud failure if any persistent-scan hand-off of the run timed out (outside the timed region)
+    from sheeprl_prey_amd.ops.rssm import check_scan_health
+
+    check_scan_health()
     if args.phase_times and rank == 0:
         seg = trainer.seg
         if seg.phase_ms is not None and seg.timed_steps:

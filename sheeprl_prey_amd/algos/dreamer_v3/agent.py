@@ -308,16 +308,8 @@ class RSSM(nn.Module):
         nh, G = len(actor.actions_dim), S // disc
         # every uniform of the rollout in one launch: per step nh x M for the actions, G x M for the prior
         U = torch.rand(horizon + 1, M * (nh + G), device=post.device)
-        # persistent one-launch rollout (imagine.hip): opt-in, it measures 2.27 ms vs 1.85 ms for the
-        # in-graph per-op rollout at the Atari-100k shapes (profiles/r2_imagine_persistent.md)
         layers = trunk_layers(actor.model) if record else None
-        rec = TrunkRecord(layers, horizon + 1, M, post.device) if layers is not None else None
-        if rec is None and getattr(self, "fused_imagine", os.environ.get("SRL_IMAGINE_IMPL", "ops") == "persist"):
-            from sheeprl_prey_amd.ops.imagine import fused_imagine
-
-            full = fused_imagine(self, actor, post, h, horizon, U)  # one persistent launch (imagine.hip)
-            if full is not None:
-                return (full[:, :, A:], full[:, :, :A]) + ((None,) if record else ())
+        trunk_rec = TrunkRecord(layers, horizon + 1, M, post.device) if layers is not None else None
         buf = post.new_empty(horizon + 1, M, A + S + Hd)
         buf[0, :, A:A + S].copy_(post)
         buf[0, :, A + S:].copy_(h)
@@ -330,7 +322,7 @@ class RSSM(nn.Module):
         WgT_h, WgT_f = Wg[:, :Hd].t(), Wg[:, Hd:].t()
         ln = gru.layer_norm
         for t in range(horizon + 1):
-            out = rec.step(t, buf[t, :, A:]) if rec is not None else actor.model(buf[t, :, A:])
+            out = trunk_rec.step(t, buf[t, :, A:]) if trunk_rec is not None else actor.model(buf[t, :, A:])
             c0 = 0
             for i, (head, a) in enumerate(zip(actor.mlp_heads, actor.actions_dim)):
                 C.unimix_sample_into(head(out), U[t, i * M:(i + 1) * M], int(a), float(actor._unimix), buf[t, :, c0:c0 + a])
@@ -349,7 +341,7 @@ class RSSM(nn.Module):
             C.ln_gru_into(gx, buf[t, :, A + S:], ln.weight, ln.bias, float(ln.eps), buf[t + 1, :, A + S:])
             logits = self.transition_model(buf[t + 1, :, A + S:])
             C.unimix_sample_into(logits.contiguous(), U[t, nh * M:], disc, float(self.unimix), buf[t + 1, :, A:A + S])
-        return (buf[:, :, A:], buf[:, :, :A]) + ((rec,) if record else ())
+        return (buf[:, :, A:], buf[:, :, :A]) + ((trunk_rec,) if record else ())
 
     # ---- MI355X scan: T-step posterior rollout with hoisted GEMMs --------------------
     def _mlp_head(self, mlp: MLP, x_pre: Tensor) -> Tensor:

@@ -44,6 +44,7 @@ from sheeprl_prey_amd.algos.dreamer_v3.loss import reconstruction_loss
 from sheeprl_prey_amd.algos.dreamer_v3.utils import Moments, compute_lambda_values, test
 from sheeprl_prey_amd.data.buffers import AsyncReplayBuffer
 from sheeprl_prey_amd.data.tensordict import TensorDict
+from sheeprl_prey_amd.ops.rssm import check_scan_health
 from sheeprl_prey_amd.parallel.flat_optim import flatten_like, build_optimizer
 from sheeprl_prey_amd.parallel.graphs import GraphedStep
 from sheeprl_prey_amd.utils.distribution import OneHotCategoricalValidateArgs
@@ -213,10 +214,7 @@ class DreamerV3Trainer:
             continue_logits, None, wm_cfg.continue_scale_factor, entropies=ents, dones=data["dones"],
         )
         self.world_optimizer.zero_grad(set_to_none=True)
-        # decoder weight gradients run on a side stream beside the persistent scan backward (joined
-        # here); not with the overlapped all-reduce, whose grad hooks read each gradient at once
-        with ops.sidework.region(rec_loss.is_cuda and getattr(self.world_optimizer, "_ov", None) is None):
-            rec_loss.backward()
+        rec_loss.backward()
         out["Loss/world_model_loss"] = rec_loss.detach()
         out["Loss/observation_loss"] = observation_loss.detach()
         out["Loss/reward_loss"] = reward_loss.detach()
@@ -532,6 +530,7 @@ def main(runner, cfg: Dict[str, Any]):
                 timer.add("Time/train_time", e0.elapsed_time(e1) / 1e3)
             train_events.clear()
             rb.check_gather_error()
+            check_scan_health()
             runner.log_dict(aggregator.compute(), policy_step)
             aggregator.reset()
             log_throughput(runner, timer.compute(), policy_step, last_log, train_step, last_train, cfg.env.action_repeat)

@@ -736,4 +736,3 @@ def gru_step(rnn: torch.nn.GRU, x: Tensor, h: Tensor):
     gh = torch.nn.functional.linear(h2, rnn.weight_hh_l0, rnn.bias_hh_l0).contiguous()
     hn = _GRUCellAct.apply(gi, gh, h2.contiguous()).view(1, -1, rnn.hidden_size)
     return hn, hn
-from sheeprl_prey_amd.ops import sidework  # noqa: E402,F401  (side-stream weight gradients)

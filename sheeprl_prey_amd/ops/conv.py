@@ -19,8 +19,6 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 from torch import Tensor, nn
 
-from sheeprl_prey_amd.ops import sidework
-
 _OK_CH = (32, 64, 128, 256)
 ENABLED = True  # A/B switch: False routes the stacks through the per-layer modules (MIOpen + LN kernels)
 # Below this many frames (e.g. the env-interaction player, one frame per env) the deepest stage has
@@ -184,17 +182,8 @@ def encoder_forward(stages, x: Tensor, scale: float = 1.0) -> Tensor:
 
 
 def _wgrad(C, P: Tensor, Q: Tensor, cb: int, w: Tensor) -> Tensor:
-    """Decoder weight gradient: in line, or - inside ``sidework.region`` - deferred to the side stream
-    that runs beside the persistent scan backward (``ops/sidework.py``).  The output is allocated
-    here, on the calling stream; the queued launch holds a second tensor on the same storage, made
-    with ``set_`` rather than ``view`` (a view keeps its base referenced: AccumulateGrad would then
-    not steal the returned tensor as ``.grad`` but clone it - before the side stream has written it)."""
-    if not sidework.active():
-        return C.conv_wgrad(P, Q, cb)
-    out = torch.empty_like(w)
-    dst = out.new_empty(0).set_(out.untyped_storage(), out.storage_offset(), out.shape, out.stride())
-    sidework.defer(lambda: C.conv_wgrad(P, Q, cb, dst), P, Q)
-    return out
+    """Decoder weight gradient (in line)."""
+    return C.conv_wgrad(P, Q, cb)
 
 
 # ---------------------------------------------------------------------------------- decoder

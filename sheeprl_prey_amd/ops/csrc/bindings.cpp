@@ -603,6 +603,18 @@ srl::scanp::PP scanp_params(const std::vector<torch::Tensor>& ts, const std::vec
 }
 
 long long* g_scanp_prof = nullptr;  // debug phase timestamps (set_scanp_prof)
+unsigned* g_scanp_health = nullptr;  // sticky timeout word shared by every launch (set_scanp_health)
+unsigned g_scanp_spin = 0;           // spin bound of the hand-off waits (0 = kernel default; tests force timeouts)
+
+void set_scanp_health(c10::optional<torch::Tensor> buf, int64_t spin_max) {
+  if (buf.has_value() && buf->defined()) {
+    TORCH_CHECK(buf->scalar_type() == torch::kInt32 && buf->is_cuda() && buf->numel() >= 1, "health word: int32 [1] on GPU");
+    g_scanp_health = (unsigned*)buf->data_ptr<int32_t>();
+  } else {
+    g_scanp_health = nullptr;
+  }
+  g_scanp_spin = (unsigned)std::max<int64_t>(0, spin_max);
+}
 
 void set_scanp_prof(c10::optional<torch::Tensor> buf) {
   if (buf.has_value() && buf->defined()) {
@@ -617,6 +629,8 @@ void scanp_fwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>&
   TORCH_CHECK(ts.size() == 35, "scanp_fwd: expects 35 tensors");
   auto p = scanp_params(ts, ints, fl);
   p.prof = g_scanp_prof;
+  p.health = g_scanp_health;
+  p.spin_max = g_scanp_spin;
   TORCH_CHECK(p.P && p.first && p.uni && p.z0 && p.WzT && p.Wg && p.W1 && p.W2 && p.xr && p.hs && p.u && p.samples,
               "scanp_fwd: missing tensors");
   launch_scanp_fwd(p, cur_stream());
@@ -626,6 +640,8 @@ void scanp_bwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>&
   TORCH_CHECK(ts.size() == 55, "scanp_bwd: expects 55 tensors");
   auto p = scanp_params(ts, ints, fl);
   p.prof = g_scanp_prof;
+  p.health = g_scanp_health;
+  p.spin_max = g_scanp_spin;
   TORCH_CHECK(p.W2T && p.W1T && p.WgT && p.dmixed && p.DH && p.dlog && p.dv && p.du && p.dgx && p.dcat && p.dx && p.dZ && p.sst,
               "scanp_bwd: missing tensors");
   launch_scanp_bwd(p, cur_stream());
@@ -1054,5 +1070,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("truncnorm_logprob_fwd", &truncnorm_logprob_fwd);
   m.def("truncnorm_logprob_bwd", &truncnorm_logprob_bwd);
   m.def("set_scanp_prof", &set_scanp_prof);
+  m.def("set_scanp_health", &set_scanp_health);
   m.def("set_scan4_prof", &set_scan4_prof);
 }

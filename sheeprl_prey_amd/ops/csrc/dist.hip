@@ -81,82 +81,6 @@ __global__ void __launch_bounds__(256) unimix_sample_fwd_kernel(const float* __r
   }
 }
 
-// Same op, one lane per categorical (C <= CW): the whole segment lives in the lane's registers, so the
-// unimix softmax, the CDF and the inverse-CDF pick are sequential per-lane loops instead of ~7
-// segmented shuffle reductions per element (the imagination's transition head: 32 categoricals of 32
-// classes for each of the 1024 rows, 15 times per step).  Same arithmetic as above except the CDF is
-// accumulated left to right (the segmented form sums in a tree).
-template <int CW>
-__global__ void __launch_bounds__(256) unimix_lane_fwd_kernel(const float* __restrict__ logits,
-                                                              const float* __restrict__ uniform, float* __restrict__ mixed,
-                                                              float* __restrict__ sample, int R, int C, float alpha, int G,
-                                                              int lds) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= R) return;
-  const float* lr = logits + (int64_t)r * C;
-  float m[CW];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int k = 0; k < CW; ++k) {
-    m[k] = k < C ? lr[k] : -INFINITY;
-    mx = fmaxf(mx, m[k]);
-  }
-  if (alpha > 0.f) {
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < CW; ++k) {
-      m[k] = k < C ? __expf(m[k] - mx) : 0.f;
-      s += m[k];
-    }
-    const float inv = 1.f / s, a0 = alpha / C;
-    mx = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < CW; ++k) {
-      float pm = (1.f - alpha) * (m[k] * inv) + a0;
-      pm = fminf(fmaxf(pm, FEPS), 1.f - FEPS);
-      m[k] = k < C ? logf(pm) : -INFINITY;
-      mx = fmaxf(mx, m[k]);
-    }
-  }
-  if (mixed) {
-#pragma unroll
-    for (int k = 0; k < CW; ++k)
-      if (k < C) mixed[(int64_t)r * C + k] = m[k];
-  }
-  // probabilities of Categorical(logits=m), then the pick
-  float e[CW], s2 = 0.f;
-#pragma unroll
-  for (int k = 0; k < CW; ++k) {
-    e[k] = k < C ? __expf(m[k] - mx) : 0.f;
-    s2 += e[k];
-  }
-  int pick = 0;
-  if (uniform != nullptr) {
-    float cdf[CW], c = 0.f;
-#pragma unroll
-    for (int k = 0; k < CW; ++k) {
-      c += e[k] / s2;
-      cdf[k] = c;
-    }
-    const float thr = uniform[r] * c;
-#pragma unroll
-    for (int k = 0; k < CW; ++k) pick += (k < C && cdf[k] < thr) ? 1 : 0;
-    if (pick > C - 1) pick = C - 1;
-  } else {
-    float best = -1.f;
-#pragma unroll
-    for (int k = 0; k < CW; ++k)
-      if (k < C && e[k] > best) {
-        best = e[k];
-        pick = k;
-      }
-  }
-  float* so = sample + (int64_t)(r / G) * lds + (int64_t)(r % G) * C;
-#pragma unroll
-  for (int k = 0; k < CW; ++k)
-    if (k < C) so[k] = k == pick ? 1.f : 0.f;
-}
-
 // d(loss)/d(logits) given g_mixed (may be null) and g_sample (straight-through path, may be null)
 __global__ void __launch_bounds__(256) unimix_sample_bwd_kernel(const float* __restrict__ logits,
                                                                 const float* __restrict__ g_mixed,
@@ -453,22 +377,6 @@ bool launch_unimix_sample_fwd(const float* logits, const float* uniform, float* 
   if (G <= 0) {
     G = 1;
     lds = C;
-  }
-  // lane-per-categorical form for C <= 32: opt-in (SRL_UNIMIX_LANE=1).  Measured slower in the DV3 step
-  // (same-box A/B, 120 steps x 2: 266.2-268.1 vs 269.6-270.0 env-steps/s for the segmented form): one
-  // lane per row makes every load / store instruction touch 64 different cache lines.
-  static const bool lane_on = [] {
-    const char* e = std::getenv("SRL_UNIMIX_LANE");
-    return e != nullptr && e[0] == '1';
-  }();
-  if (C <= 32 && lane_on) {
-    if (C <= 16)
-      hipLaunchKernelGGL(unimix_lane_fwd_kernel<16>, dim3(cdiv(R, 256)), dim3(256), 0, st, logits, uniform, mixed, sample, R,
-                         C, alpha, G, lds);
-    else
-      hipLaunchKernelGGL(unimix_lane_fwd_kernel<32>, dim3(cdiv(R, 256)), dim3(256), 0, st, logits, uniform, mixed, sample, R,
-                         C, alpha, G, lds);
-    return true;
   }
   int W = next_pow2(C);
   int segs_per_block = 4 * (64 / W);

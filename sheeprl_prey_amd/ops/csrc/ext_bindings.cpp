@@ -1,15 +1,9 @@
-// Torch bindings of the round-2 kernels (persistent imagination rollout, ...).  Registered into the
+// Torch bindings of the round-2+ kernels (replay gather, LSTM, GRU cell, NatureCNN, ...).  Registered into the
 // same extension module as bindings.cpp (register_ext).  Every launch validates the shapes of all
 // operands on the host against the dimensions the kernel indexes with.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
-#include "imag.h"
-
-void imagine_plan(int M, int S, int Hd, int D, int Da, int Ht, int A, int nh, int disc, int La, int& NB, int& nslots);
-int imagine_sync_words(int nslots);
-int imagine_lds_bytes();
-void launch_imagine(const srl::imag::IP& p, hipStream_t st);
 
 void natcnn_fwd(const float* x, const float* w, const float* b, float* y, int Nb, int H, int W, int Ci, int Co, int KH,
                 int KW, int S, hipStream_t st);
@@ -56,110 +50,10 @@ void launch_actor_loss(const float* z, const float* act, const float* lam, const
 
 namespace {
 
-long long* g_prof = nullptr;  // debug timestamps of block 0 (set_imagine_prof)
-
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
-
-const float* fptr(const torch::Tensor& t, const char* name, int64_t numel, bool optional = false) {
-  if (optional && (!t.defined() || t.numel() == 0)) return nullptr;
-  TORCH_CHECK(t.defined() && t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.is_contiguous(), "imagine: ", name,
-              " must be a contiguous float32 GPU tensor");
-  TORCH_CHECK(t.numel() == numel, "imagine: ", name, " has ", t.numel(), " elements, expected ", numel);
-  return t.data_ptr<float>();
-}
 
 }  // namespace
 
-// [NB, nslots, sync words, LDS bytes]; NB == 0: shape unsupported
-std::vector<int64_t> imagine_info(int64_t M, int64_t S, int64_t Hd, int64_t D, int64_t Da, int64_t Ht, int64_t A,
-                                  int64_t nh, int64_t disc, int64_t La) {
-  int NB = 0, nslots = 0;
-  imagine_plan(M, S, Hd, D, Da, Ht, A, nh, disc, La, NB, nslots);
-  return {NB, nslots, NB ? imagine_sync_words(nslots) : 0, imagine_lds_bytes()};
-}
-
-// ts: WaT, Wh [Ap, Da], bh [Ap] (Ap = A rounded up to 16, zero rows), WrT, br, lnrw, lnrb, Wg, bg, lngw, lngb, Wt1, bt1, lntw, lntb, Wt2, bt2, U, buf, Y, part,
-//     idx (int32), sync (int32), then La x (Wa, ba, lnaw, lnab).  Empty tensors = absent biases.
-// ints: M, horizon, S, Hd, D, Da, La, Ht, disc, act_a, act_r, act_t, heads...
-// fl: alpha_a, alpha_s, eps_a, eps_r, eps_g, eps_t
-void imagine_rollout(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints, const std::vector<double>& fl) {
-  using srl::imag::IP;
-  TORCH_CHECK(ints.size() >= 13 && fl.size() == 6, "imagine: bad scalar arguments");
-  IP p{};
-  p.M = ints[0]; p.horizon = ints[1]; p.S = ints[2]; p.Hd = ints[3]; p.D = ints[4]; p.Da = ints[5]; p.La = ints[6];
-  p.Ht = ints[7]; p.disc = ints[8]; p.act_a = ints[9]; p.act_r = ints[10]; p.act_t = ints[11];
-  p.nh = (int)ints.size() - 12;
-  TORCH_CHECK(p.nh >= 1 && p.nh <= srl::imag::MAXH, "imagine: 1..", srl::imag::MAXH, " action heads");
-  TORCH_CHECK(p.La >= 1 && p.La <= srl::imag::MAXL, "imagine: 1..", srl::imag::MAXL, " actor layers");
-  TORCH_CHECK(p.disc >= 1 && p.S % p.disc == 0 && p.horizon >= 0, "imagine: bad discrete/horizon");
-  p.A = 0;
-  for (int h = 0; h < p.nh; ++h) {
-    p.head[h] = (int)ints[12 + h];
-    TORCH_CHECK(p.head[h] >= 1 && p.head[h] <= 32, "imagine: head sizes must be in [1, 32]");
-    p.A += p.head[h];
-  }
-  p.G = p.S / p.disc;
-  p.alpha_a = fl[0]; p.alpha_s = fl[1]; p.eps_a = fl[2]; p.eps_r = fl[3]; p.eps_g = fl[4]; p.eps_t = fl[5];
-  int NB = 0, nslots = 0;
-  imagine_plan(p.M, p.S, p.Hd, p.D, p.Da, p.Ht, p.A, p.nh, p.disc, p.La, NB, nslots);
-  TORCH_CHECK(NB > 0, "imagine: unsupported shape");
-  p.NB = NB;
-  p.nslots = nslots;
-  p.RB = p.M / 64;
-  TORCH_CHECK(ts.size() == 23 + 4 * (size_t)p.La, "imagine: expected ", 23 + 4 * p.La, " tensors");
-  const int64_t M = p.M, S = p.S, Hd = p.Hd, D = p.D, Da = p.Da, Ht = p.Ht, A = p.A, H1 = p.horizon + 1;
-  const int64_t YLD = std::max(Da, std::max(D, Ht));
-  size_t k = 0;
-  p.WaT = fptr(ts[k++], "WaT", S * Da);
-  const int64_t Ap = (A + 15) / 16 * 16;  // heads zero-padded to whole 16-row tiles
-  p.Wh = fptr(ts[k++], "Wh", Ap * Da);
-  p.bh = fptr(ts[k++], "bh", Ap, true);
-  p.WrT = fptr(ts[k++], "WrT", (S + A) * D);
-  p.br = fptr(ts[k++], "br", D, true);
-  p.lnrw = fptr(ts[k++], "lnrw", D);
-  p.lnrb = fptr(ts[k++], "lnrb", D);
-  p.Wg = fptr(ts[k++], "Wg", 3 * Hd * (Hd + D));
-  p.bg = fptr(ts[k++], "bg", 3 * Hd, true);
-  p.lngw = fptr(ts[k++], "lngw", 3 * Hd);
-  p.lngb = fptr(ts[k++], "lngb", 3 * Hd);
-  p.Wt1 = fptr(ts[k++], "Wt1", Ht * Hd);
-  p.bt1 = fptr(ts[k++], "bt1", Ht, true);
-  p.lntw = fptr(ts[k++], "lntw", Ht);
-  p.lntb = fptr(ts[k++], "lntb", Ht);
-  p.Wt2 = fptr(ts[k++], "Wt2", S * Ht);
-  p.bt2 = fptr(ts[k++], "bt2", S, true);
-  p.U = fptr(ts[k++], "U", H1 * M * (p.nh + p.G));
-  p.buf = const_cast<float*>(fptr(ts[k++], "buf", H1 * M * (A + S + Hd)));
-  p.Y = const_cast<float*>(fptr(ts[k++], "Y", 2 * M * YLD));
-  p.part = const_cast<float*>(fptr(ts[k++], "part", 2 * M * NB * 2));
-  const torch::Tensor& idx = ts[k++];
-  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == torch::kInt32 && idx.is_contiguous() && idx.numel() == M * p.G,
-              "imagine: idx must be int32 [M, G] on the GPU");
-  p.idx = idx.data_ptr<int32_t>();
-  const torch::Tensor& sync = ts[k++];
-  TORCH_CHECK(sync.is_cuda() && sync.scalar_type() == torch::kInt32 && sync.is_contiguous() &&
-                  sync.numel() >= imagine_sync_words(nslots),
-              "imagine: sync must be int32[", imagine_sync_words(nslots), "] on the GPU");
-  p.sync = (unsigned*)sync.data_ptr<int32_t>();
-  for (int l = 0; l < p.La; ++l) {
-    const int64_t in = l == 0 ? S + Hd : Da;
-    p.Wa[l] = fptr(ts[k++], "Wa", Da * in);
-    p.ba[l] = fptr(ts[k++], "ba", Da, true);
-    p.lnaw[l] = fptr(ts[k++], "lnaw", Da);
-    p.lnab[l] = fptr(ts[k++], "lnab", Da);
-  }
-  p.prof = g_prof;
-  launch_imagine(p, stream());
-}
-
-void set_imagine_prof(c10::optional<torch::Tensor> buf) {
-  if (buf.has_value() && buf->defined()) {
-    TORCH_CHECK(buf->scalar_type() == torch::kInt64 && buf->is_cuda(), "prof buffer: int64 on GPU");
-    g_prof = (long long*)buf->data_ptr<int64_t>();
-  } else {
-    g_prof = nullptr;
-  }
-}
 
 // ------------------------------------------------------------------ NatureCNN convolutions (natcnn.hip)
 namespace {
@@ -579,7 +473,4 @@ void register_ext(pybind11::module& m) {
   m.def("moments_update", &moments_update);
   m.def("nc_conv_fwd", &nc_conv_fwd);
   m.def("nc_conv_bwd", &nc_conv_bwd);
-  m.def("imagine_info", &imagine_info);
-  m.def("imagine_rollout", &imagine_rollout);
-  m.def("set_imagine_prof", &set_imagine_prof);
 }

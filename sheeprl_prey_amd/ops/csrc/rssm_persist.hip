@@ -142,7 +142,9 @@ __device__ __forceinline__ u32 shard_count(int p0, int np) {
 
 // Wave 0 polls until every shard holds rounds x its producer count; the workgroup then joins.
 // Returns false (uniformly) when the launch is aborting.
-__device__ __forceinline__ bool wait_ctr(u32* sync, int ctr, u32 cnt, u32 rounds, int code, int* flag) {
+__device__ __forceinline__ bool wait_ctr(const PP& p, int ctr, u32 cnt, u32 rounds, int code, int* flag) {
+  u32* sync = p.sync;
+  const u32 spin_max = p.spin_max ? p.spin_max : SPIN_MAX;
   if (threadIdx.x < 64) {
     const int s = threadIdx.x;
     const u32 need = cnt * rounds;
@@ -157,14 +159,17 @@ __device__ __forceinline__ bool wait_ctr(u32* sync, int ctr, u32 cnt, u32 rounds
         break;
       }
       if (__all(s >= NSH || v >= need)) break;
-      if (spins >= SPIN_MAX) {
+      if (spins >= spin_max) {
         bad = 2;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
     if (s == 0) {
-      if (bad == 2) __hip_atomic_store(err, (u32)code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (bad == 2) {
+        __hip_atomic_store(err, (u32)code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p.health) __hip_atomic_fetch_or(p.health, 1u << (code & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       *flag = bad;
     }
   }
@@ -263,9 +268,9 @@ __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
     PROF(0, 0);
     if (t > 0) {
       // h_{t-1} is published by B(t-1) before C(t-1) runs: load it while C finishes
-      if (!wait_ctr(p.sync, 1, eB, t, 1, flag)) return;
+      if (!wait_ctr(p, 1, eB, t, 1, flag)) return;
       stage_wt(As, lda, p.hs + (size_t)(t - 1) * B * H, H, B, H, p.first + (size_t)t * B);
-      if (!wait_ctr(p.sync, 2, eC, t, 2, flag)) return;
+      if (!wait_ctr(p, 2, eC, t, 2, flag)) return;
     }
     PROF(0, 1);
     stage_wt(As + H, lda, p.xr + (size_t)t * B * D, D, B, D);
@@ -329,7 +334,7 @@ __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
     const int eb = threadIdx.x >> 4, ec = threadIdx.x & 15;
     const size_t eo = ((size_t)t * B + eb) * hid + bI * 16 + ec;
     const float pre = (threadIdx.x < 256 && eb < B) ? p.P[eo] : 0.f;  // epilogue input, loaded behind the wait
-    if (!wait_ctr(p.sync, 0, eA, t + 1, 3, flag)) return;
+    if (!wait_ctr(p, 0, eA, t + 1, 3, flag)) return;
     PROF(1, 1);
     if (w < B) {
       // gate inputs and the nA per-tile (mean, M2) partials, all loads issued before any use
@@ -423,7 +428,7 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
     const bool evalid = threadIdx.x < 512 && eb < B;
     const float ebias = threadIdx.x < 512 ? p.b2[n0 + ec] : 0.f;
     const float euni = evalid ? p.uni[(size_t)t * B * nseg + eb * nseg + (n0 + ec) / C] : 0.f;
-    if (!wait_ctr(p.sync, 1, eB, t + 1, 4, flag)) return;
+    if (!wait_ctr(p, 1, eB, t + 1, 4, flag)) return;
     PROF(2, 1);
     stage_wt(As, lda, p.u + (size_t)t * B * hid, hid, B, hid);
     __syncthreads();
@@ -479,7 +484,7 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
       // xr = a_proj + first z0 Wz^T (host) + sum over categoricals of the sampled rows.  All 1024 threads
       // gather (row, column, quarter of the categoricals) so every load of a thread is in flight at once.
       arrive(p.sync + 3 * NSH * SHW);
-      if (!wait_ctr(p.sync, 3, eC, t + 1, 5, flag)) return;
+      if (!wait_ctr(p, 3, eC, t + 1, 5, flag)) return;
       PROF(2, 6);
       for (int e = threadIdx.x; e < B * nseg; e += NTH)
         selL[e] = __hip_atomic_load(p.sel + (size_t)(t + 1) * B * nseg + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -561,7 +566,7 @@ __device__ __forceinline__ void bwd_G1(const PP& p, int i, float* sm) {
   __syncthreads();
   for (int t = T - 1; t >= 0; --t) {
     PROF(3, 0);
-    if (t < T - 1 && !wait_ctr(p.sync, 3, e4, T - 1 - t, 11, flag)) return;
+    if (t < T - 1 && !wait_ctr(p, 3, e4, T - 1 - t, 11, flag)) return;
     PROF(3, 1);
     stage_wt(As, lda, p.dlog + (size_t)t * B * S, S, B, S);
     __syncthreads();
@@ -625,7 +630,7 @@ __device__ __forceinline__ void bwd_G2(const PP& p, int i, float* sm) {
       pre[1280 + threadIdx.x] = rv ? p.rg[(size_t)t * B + eb] : 0.f;
       pre[1536 + threadIdx.x] = (rv && t > 0) ? 1.f - p.first[(size_t)t * B + eb] : 0.f;
     }
-    if (!wait_ctr(p.sync, 0, e1, T - t, 12, flag)) return;
+    if (!wait_ctr(p, 0, e1, T - t, 12, flag)) return;
     PROF(4, 1);
     stage_wt(R, lda, p.dv + (size_t)t * B * hid, hid, B, hid);
     __syncthreads();
@@ -717,7 +722,7 @@ __device__ __forceinline__ void bwd_G3(const PP& p, int i3, float* sm) {
       rowst[threadIdx.x * 4] = p.mg[(size_t)t * B + threadIdx.x];
       rowst[threadIdx.x * 4 + 1] = p.rg[(size_t)t * B + threadIdx.x];
     }
-    if (!wait_ctr(p.sync, 1, e2, T - t, 13, flag)) return;
+    if (!wait_ctr(p, 1, e2, T - t, 13, flag)) return;
     PROF(5, 1);
     if (w < B) {
       const float2 sp = lane < n2 ? ld_wt2(p.sst + (((size_t)t * n2 + lane) * 16 + w) * 2) : make_float2(0.f, 0.f);
@@ -796,7 +801,7 @@ __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
     const bool eok = threadIdx.x < 512 && t > 0;
     const float el = eok ? p.logits[eo] : 0.f, egm = eok ? p.dmixed[eo] : 0.f;
     const float edp = (eok && p.dpost) ? p.dpost[eo] : 0.f, ekeep = eok ? 1.f - p.first[(size_t)t * B + ebb] : 0.f;
-    if (!wait_ctr(p.sync, 2, e3, T - t, 14, flag)) return;
+    if (!wait_ctr(p, 2, e3, T - t, 14, flag)) return;
     PROF(6, 1);
     stage_wt(R, lda, p.dcat + (size_t)t * B * HD + H, HD, B, D);
     __syncthreads();

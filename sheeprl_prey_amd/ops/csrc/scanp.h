@@ -26,6 +26,10 @@ struct PP {
   float *dZ, *sst;
   // hand-off counters (zeroed before every launch) and the error word (0 = ok)
   unsigned* sync;
+  // sticky health word across launches (or-ed with 1 << code on a hand-off timeout; read by the host off
+  // the hot path: ops.rssm.check_scan_health) and the spin bound of every wait (0 = default)
+  unsigned* health;
+  unsigned spin_max;
   // optional phase timestamps (first workgroup of each role, thread 0): prof[(role * T + t) * 8 + k]
   long long* prof;
 };

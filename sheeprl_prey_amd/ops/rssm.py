@@ -323,6 +323,7 @@ class RSSMPersistFn(torch.autograd.Function):
         ok, words, _, _, _ = C.scanp_info(B, S, D, H, hid, disc)
         assert ok, "scanp: unsupported shape"
         sync = torch.empty(words, device=dev, dtype=torch.int32)
+        _scan_health_word(dev)
         fwd = [P.contiguous(), first, uniform.contiguous(), z0, Wz_c, Wz_c.t().contiguous(), ln1_w.contiguous(),
                ln1_b.contiguous(), Wg.contiguous(), lng_w.contiguous(), lng_b.contiguous(), W1.contiguous(),
                ln2_w.contiguous(), ln2_b.contiguous(), W2.contiguous(), b2.contiguous(),
@@ -360,16 +361,8 @@ class RSSMPersistFn(torch.autograd.Function):
         p1g, p1b, pgg, pgb, p2g, p2b = e(T, D), e(T, D), e(T, 3 * H), e(T, 3 * H), e(T, hid), e(T, hid)
         bwd = [W2.t().contiguous(), W1.t().contiguous(), Wg.t().contiguous(), dpost, dmixed, DH, dlog, dv, du, dgx, dcat,
                dx, p1g, p1b, pgg, pgb, p2g, p2b, e(T, B, 3 * H), e(T, H // 16, 16, 2)]
-        from sheeprl_prey_amd.ops import sidework
-
-        gate = None
-        if sidework.active():
-            # deferred decoder weight gradients start with the scan, on the CUs it leaves free
-            gate = torch.cuda.Event()
-            gate.record()
+        _scan_health_word(dev)
         C.scanp_bwd(fwd + bwd, ctx.dims, ctx.fl)
-        if gate is not None:
-            sidework.launch(gate)
         cat, zm, hs, v = fwd[17], fwd[18], fwd[25], fwd[27]
         TB = T * B
         dWz = dx.reshape(TB, D).t().mm(zm.reshape(TB, S))
@@ -387,6 +380,58 @@ def scanp_error(sync: Tensor) -> int:
     from sheeprl_prey_amd.ops import _ext
 
     return int(sync[_ext().scanp_info(1, 32, 16, 16, 16, 32)[2]].item())
+
+
+# ---------------------------------------------------------------- persistent-scan health
+# Every hand-off wait of the persistent scan is bounded; a wait that times out (a starved / not
+# co-resident workgroup) makes the whole grid drain and or-s ``1 << code`` into this sticky device word,
+# which every launch shares.  The host reads it off the hot path (log / checkpoint time, end of a bench)
+# and raises, so a starved scan can never silently produce garbage gradients.
+SCAN_WAIT_CODES = {
+    1: "fwd A waits h_{t-1} (B)", 2: "fwd A waits x_{t} (C gathers)", 3: "fwd B waits gx (A)", 4: "fwd C waits u (B)",
+    5: "fwd C waits every C sample", 11: "bwd G1 waits dlog (G4)", 12: "bwd G2 waits dv (G1)", 13: "bwd G3 waits dZ (G2)",
+    14: "bwd G4 waits dcat (G3)",
+}
+_HEALTH: dict = {}
+_SPIN_MAX = 0  # 0 = kernel default; tests force tiny bounds to exercise the timeout path
+
+
+def _scan_health_word(device) -> Tensor:
+    from sheeprl_prey_amd.ops import _ext
+
+    key = str(device)
+    w = _HEALTH.get(key)
+    if w is None:
+        w = _HEALTH[key] = torch.zeros(1, dtype=torch.int32, device=device)
+    _ext().set_scanp_health(w, _SPIN_MAX)
+    return w
+
+
+def set_scan_spin_max(n: int) -> None:
+    """Debug: bound every persistent-scan hand-off wait to ``n`` polls (0 = the kernel default)."""
+    global _SPIN_MAX
+    _SPIN_MAX = int(n)
+    for w in _HEALTH.values():
+        from sheeprl_prey_amd.ops import _ext
+
+        _ext().set_scanp_health(w, _SPIN_MAX)
+
+
+def check_scan_health(raise_error: bool = True) -> int:
+    """Host check of the sticky persistent-scan health word (syncs the device).  Returns the bit mask of
+    the wait codes that timed out since the last check (0 = healthy) and raises when it is non-zero."""
+    bad = 0
+    for w in _HEALTH.values():
+        v = int(w.item())
+        if v:
+            w.zero_()
+            bad |= v
+    if bad and raise_error:
+        names = [f"{c}: {n}" for c, n in SCAN_WAIT_CODES.items() if bad & (1 << c)]
+        raise RuntimeError("persistent RSSM scan: a hand-off wait timed out (workgroups starved or not co-resident); "
+                           f"the affected steps' outputs are invalid. Timed-out waits: {names or hex(bad)}. "
+                           "SRL_SCAN_IMPL=scan4 selects the multi-launch scan.")
+    return bad
 
 
 def scanp_supported(B: int, S: int, D: int, H: int, hid: int, classes: int) -> bool:

@@ -70,43 +70,6 @@ def test_dv3_graph_matches_eager_losses():
     assert abs(la - lb) / abs(la) < 1e-4
 
 
-def test_side_stream_decoder_wgrad_matches_inline():
-    """Decoder weight gradients deferred to the side stream beside the persistent scan backward
-    (ops/sidework.py) equal the in-line ones; every other world-model gradient is unchanged too."""
-    from sheeprl_prey_amd.ops import sidework
-
-    tr = _build(graphs=False, seed=5, cnn_mult=32)  # channels 32..256: the HIP conv stack + persistent scan
-    data = _data(seed=9)
-    wm = tr.world_model
-    grads = []
-    n0 = sidework.deferred_count()
-    names = [n for n, _ in wm.named_parameters()]
-    default = sidework._ENABLED
-    for on in (False, False, True):  # the first call builds the lazy plans (kept out of the comparison)
-        sidework._ENABLED = on
-        if on:
-            # poison the allocator's free blocks of the weight sizes with NaN: a gradient read before the
-            # side stream wrote it (e.g. cloned by autograd instead of stolen) cannot pass by luck
-            for p in wm.parameters():
-                p.grad = None
-            junk = [torch.full((p.numel(),), float("nan"), device="cuda") for p in wm.parameters() for _ in range(4)]
-            del junk
-        try:
-            torch.manual_seed(123)
-            tr._phase_wm(data)
-            torch.cuda.synchronize()
-            grads.append([None if p.grad is None else p.grad.detach().clone() for p in wm.parameters()])
-        finally:
-            sidework._ENABLED = default
-    assert sidework.deferred_count() - n0 >= 4, "the decoder weight gradients were not deferred"
-    bad = []
-    for n, ga, gb in zip(names, grads[1], grads[2]):
-        assert (ga is None) == (gb is None), n
-        if ga is not None and not torch.allclose(gb, ga, rtol=1e-4, atol=1e-5):
-            bad.append((n, float((gb - ga).abs().max())))
-    assert not bad, bad
-
-
 @pytest.mark.parametrize("impl", ["persist", "scan4", "scan9"])
 @pytest.mark.parametrize("H,D,hid,B,T", [(64, 64, 64, 4, 16), (512, 512, 512, 16, 8), (96, 80, 48, 3, 5)])
 def test_fused_rssm_scan_matches_python_scan(H, D, hid, B, T, impl):
@@ -309,3 +272,28 @@ def test_dv3_forward_reuse_matches_recompute(graphs):
         assert abs(o0[k] - o1[k]) <= 1e-4 * max(1.0, abs(o0[k])), (k, o0[k], o1[k])
     for a, b in zip(p0, p1):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5)
+
+
+def test_persistent_scan_timeout_is_loud():
+    """A starved hand-off must not pass silently: with every wait bounded to one poll the persistent
+    scan's waits time out, the grid drains, the sticky health word records the waits and the host check
+    raises; with the default bound a step is healthy again."""
+    from sheeprl_prey_amd.ops import rssm as R
+
+    tr = _build(graphs=False)
+    data = _data()
+    tr.train_step(data)
+    torch.cuda.synchronize()
+    assert R.check_scan_health() == 0
+    try:
+        R.set_scan_spin_max(1)
+        tr.train_step(data)
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match="hand-off wait timed out"):
+            R.check_scan_health()
+    finally:
+        R.set_scan_spin_max(0)
+    assert R.check_scan_health() == 0  # the check cleared the word
+    tr.train_step(data)
+    torch.cuda.synchronize()
+    assert R.check_scan_health() == 0
