@@ -29,8 +29,9 @@ import torch.distributed as dist
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--algo", default="dreamer_v3", choices=["dreamer_v3", "ppo"],
-                   help="dreamer_v3: the headline DV3 Atari-100k bench; ppo: PPO CartPole-v1 (exp=ppo) steps/sec")
+    p.add_argument("--algo", default="dreamer_v3", choices=["dreamer_v3", "ppo", "sac"],
+                   help="dreamer_v3: the headline DV3 Atari-100k bench; ppo: PPO CartPole-v1 (exp=ppo) steps/sec; "
+                        "sac: SAC on a dm_control walker_walk-shaped synthetic env (BASELINE config #3)")
     p.add_argument("--steps", type=int, default=40)
     p.add_argument("--warmup", type=int, default=8)
     p.add_argument("--prefill", type=int, default=1024, help="random-action steps before training (learning_starts)")
@@ -57,6 +58,9 @@ def parse():
     p.add_argument("--xl", action="store_true",
                    help="dreamer_v3: the XL model of exp=dreamer_v3_XL_crafter (dense 1024, mlp 5, cnn mult 96, "
                         "deter 4096, hidden 1024) on the synthetic 64x64 env")
+    p.add_argument("--continuous", action="store_true",
+                   help="dreamer_v3: exp=dreamer_v3_dmc_walker_walk (continuous 6-dim actions, TruncatedNormal actor, "
+                        "64x64 pixels + 24-dim state, train_every 2) on the walker_walk-shaped synthetic env")
     p.add_argument("overrides", nargs="*")
     return p.parse_args()
 
@@ -81,6 +85,8 @@ def main():
         sys.exit(subprocess.call(cmd))
     if args.algo == "ppo":
         return bench_ppo(args)
+    if args.algo == "sac":
+        return bench_sac(args)
 
     from sheeprl_prey_amd import ops
     from sheeprl_prey_amd.algos.common import action_info
@@ -97,10 +103,16 @@ def main():
 
     if args.eager_ops:
         ops.set_fused(False)
-    overrides = [
-        "exp=dreamer_v3_100k_ms_pacman", "env=synthetic_atari", "env.sync_env=True",
-        "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]", "fabric.accelerator=cuda",
-        f"fabric.cuda_graphs={not args.no_graphs}", "metric.log_every=1000000000",
+    if args.continuous:
+        # reference configs/exp/dreamer_v3_dmc_walker_walk.yaml on the walker_walk-shaped synthetic env
+        base = ["exp=dreamer_v3_dmc_walker_walk", "env=gym", "env.id=walker_walk_synthetic", "env.sync_env=True",
+                "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]", "mlp_keys.encoder=[state]", "mlp_keys.decoder=[state]",
+                "buffer.memmap=False", "checkpoint.every=1000000000"]
+    else:
+        base = ["exp=dreamer_v3_100k_ms_pacman", "env=synthetic_atari", "env.sync_env=True",
+                "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]"]
+    overrides = base + [
+        "fabric.accelerator=cuda", f"fabric.cuda_graphs={not args.no_graphs}", "metric.log_every=1000000000",
     ] + ([f"fabric.tunable_gemm={args.gemm_tuning}"] if args.gemm_tuning else []) + (XL_OVERRIDES if args.xl else []) + list(
         args.overrides)
     cfg = dotdict(compose(overrides))
@@ -156,9 +168,15 @@ def main():
 
     env_ms = [0.0]
 
+    # one bench step = train_every policy steps of every rank's env + the gradient steps they trigger
+    # (the Atari-100k recipe: train_every 1; the DMC walker recipe: train_every 2)
+    policy_per_step = max(1, int(cfg.algo.train_every) // (cfg.env.num_envs * world))
+
     def one_step():
         # act (weights W_t) -> store the row -> launch the gradient step (W_t -> W_t+1) -> env step on
         # the CPU while the GPU trains.  --phase-times times the serial form of the same step.
+        for _ in range(policy_per_step - 1):
+            loop.step(False, None)
         if args.phase_times:
             loop.pipelined = False
             torch.cuda.synchronize()
@@ -273,14 +291,15 @@ def main():
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         spread = float((hi - lo).abs().max().item())
     ms_per_step = elapsed / args.steps * 1e3
-    policy_steps = args.steps * cfg.env.num_envs * world
+    policy_steps = args.steps * policy_per_step * cfg.env.num_envs * world
     env_steps_per_s = policy_steps * cfg.env.action_repeat / elapsed
     if rank == 0:
         rec = {
             "metric": ("env-steps/sec (whole node) DreamerV3-XL 64x64" if args.xl
+                       else "env-steps/sec (whole node) DreamerV3 DMC walker_walk 64x64 (continuous)" if args.continuous
                        else "env-steps/sec (whole node) DreamerV3 Atari-100k 64x64"),
             "value": round(env_steps_per_s, 3),
-            "unit": "env_steps/s (policy steps x action_repeat=4, whole job)",
+            "unit": f"env_steps/s (policy steps x action_repeat={cfg.env.action_repeat}, whole job)",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -289,10 +308,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (Atari-shaped 64x64x3 uint8 env, MsPacman action set; random-init weights)",
+            "data": ("synthetic walker_walk-shaped env (64x64x3 uint8 render + 24-dim state, 6-dim continuous action; "
+                     "random-init weights)" if args.continuous else
+                     "synthetic (Atari-shaped 64x64x3 uint8 env, MsPacman action set; random-init weights)"),
             "config": {
                 "model": ("DreamerV3-XL (dense 1024, mlp 5, cnn mult 96, deter 4096, hidden 1024, stoch 32x32, bins 255)"
                           if args.xl else
+                          "DreamerV3 DMC walker (dense 512, mlp 2, cnn mult 32, deter 512, stoch 32x32, TruncatedNormal actor, "
+                          "train_every 2)" if args.continuous else
                           "DreamerV3 Atari-100k (dense 512, mlp 2, cnn mult 32, deter 512, stoch 32x32, bins 255)"),
                 "global_batch": cfg.per_rank_batch_size * world,
                 "seq_len": cfg.per_rank_sequence_length,
@@ -550,6 +573,106 @@ def bench_ppo(args):
             "dp_param_spread": spread,
         }
         print(json.dumps(rec), flush=True)
+    envs.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def bench_sac(args):
+    """SAC coupled (``exp=sac``: per-rank batch 256, 2 critics, hidden 256, 1 gradient step per env step,
+    target EMA every step) on ``walker_walk_synthetic``: dm_control walker_walk's 24-dim state and 6-dim
+    action (BASELINE config #3).  One bench step = one env step of every rank (actor forward, env step,
+    replay add) + one full SAC gradient step (replay sample, all-gather + re-shard across ranks, twin-Q
+    critic update + target EMA, actor + alpha update) - the loop of ``sac.main`` (``SACInteraction`` +
+    ``sac_train_update``).  value = whole-job env steps/s."""
+    from sheeprl_prey_amd.algos.sac.agent import build_agent
+    from sheeprl_prey_amd.algos.sac.sac import SACInteraction, SACTrainer, make_aggregator, sac_train_update
+    from sheeprl_prey_amd.config.compose import compose
+    from sheeprl_prey_amd.data.buffers import ReplayBuffer
+    from sheeprl_prey_amd.parallel.flat_optim import build_optimizer
+    from sheeprl_prey_amd.parallel.runner import Runner
+    from sheeprl_prey_amd.utils.env import make_env, make_vector_env
+    from sheeprl_prey_amd.utils.utils import dotdict
+
+    overrides = ["exp=sac", "env=gym", "env.id=walker_walk_synthetic", "mlp_keys.encoder=[state]", "env.sync_env=True",
+                 "fabric.accelerator=cuda", f"fabric.cuda_graphs={not args.no_graphs}", "metric.log_every=1000000000",
+                 "buffer.size=1000000"] + list(args.overrides)
+    cfg = dotdict(compose(overrides))
+    cfg.pop("hydra", None)
+    runner = Runner(**{k: v for k, v in cfg.fabric.items()})
+    runner._init_distributed()
+    rank, world = runner.global_rank, runner.world_size
+    device = runner.device
+    runner.seed_everything(cfg.seed + rank)
+    ne = cfg.env.num_envs
+    envs = make_vector_env(cfg, [make_env(cfg, cfg.seed + rank * ne + i, rank * ne, None, "train", i) for i in range(ne)])
+    obs_space = envs.single_observation_space
+    obs_dim = int(sum(int(np.prod(obs_space[k].shape)) for k in cfg.mlp_keys.encoder))
+    agent = build_agent(runner, cfg, obs_dim, envs.single_action_space)
+    qf_opt = build_optimizer(cfg.algo.critic.optimizer, agent.critic.parameters())
+    actor_opt = build_optimizer(cfg.algo.actor.optimizer, agent.actor.parameters())
+    alpha_opt = build_optimizer(cfg.algo.alpha.optimizer, [agent.log_alpha])
+    trainer = SACTrainer(runner, cfg, agent, actor_opt, qf_opt, alpha_opt)
+    aggregator = make_aggregator(cfg)
+    rb = ReplayBuffer(cfg.buffer.size // (ne * world), ne, device=device)
+    loop = SACInteraction(runner, cfg, envs, agent, rb, obs_dim)
+    loop.reset(cfg.seed + rank)
+    learning_starts = max(int(cfg.algo.learning_starts) // (ne * world), 1)
+    ema_every = cfg.algo.critic.target_network_frequency // (ne * world) + 1
+    update = [0]
+    sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
+
+    def one_step():
+        update[0] += 1
+        loop.act_and_step(update[0] <= learning_starts)
+        loop.store()
+        sac_train_update(trainer, runner, cfg, rb, update[0], learning_starts, ema_every, aggregator)
+
+    for _ in range(max(args.prefill, learning_starts + 1)):
+        one_step()
+    for _ in range(args.warmup):
+        one_step()
+    sync()
+    if args.profile_steps and device.type == "cuda":
+        torch.cuda._sleep(1000)  # marker kernel for scripts/trace_window.py
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    spread = 0.0
+    if world > 1:
+        cs = torch.stack([o.flat_param.double().sum() for o in (qf_opt, actor_opt, alpha_opt)])
+        lo, hi = cs.clone(), cs.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        spread = float((hi - lo).abs().max().item())
+    env_steps = args.steps * ne * world * cfg.env.action_repeat
+    if rank == 0:
+        print(json.dumps({
+            "metric": "SAC walker_walk-shaped env-steps/sec (whole node)",
+            "value": round(env_steps / elapsed, 3),
+            "unit": "env_steps/s (policy steps x action_repeat, whole job)",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic walker_walk-shaped control env (24-dim state, 6-dim action; envs/synthetic.py), random-init weights",
+            "config": {"model": "SAC actor 2x256 + 2 critics 2x256 (exp=sac)", "global_batch": cfg.per_rank_batch_size * world,
+                       "num_envs_per_rank": ne, "gradient_steps_per_env_step": cfg.algo.per_rank_gradient_steps,
+                       "parallelism": f"dp{world}", "update_mode": trainer.critic_step.mode},
+            "dp_param_spread": spread,
+        }), flush=True)
     envs.close()
     if world > 1:
         dist.barrier()

@@ -176,7 +176,7 @@ class CNNDecoder(nn.Module):
             ),
         )
 
-    def forward(self, latent_states: Tensor) -> Dict[str, Tensor]:
+    def forward(self, latent_states: Tensor, onehot=None) -> Dict[str, Tensor]:
         out = None
         if latent_states.is_cuda and latent_states.dtype == torch.float32 and ops.fused_enabled() and conv_ops.ENABLED:
             if not hasattr(self, "_fused_spec"):
@@ -184,7 +184,15 @@ class CNNDecoder(nn.Module):
             x = latent_states.reshape(-1, latent_states.shape[-1])
             if self._fused_spec is not None and x.shape[0] >= conv_ops.MIN_FRAMES:
                 lin, stages = self._fused_spec
-                out = conv_ops.decoder_forward(stages, lin(x), 0.5)
+                from sheeprl_prey_amd.ops import onehot as oh
+
+                if onehot is not None and oh.layer_supported(lin, onehot[3]):
+                    # the posterior columns of the Linear gathered from its transposed weight (ops/onehot.py)
+                    idx, G, off, n1 = onehot
+                    h = oh.first_layer(x, idx.reshape(-1, idx.shape[-1]), G, off, lin, None, n1)
+                else:
+                    h = lin(x)
+                out = conv_ops.decoder_forward(stages, h, 0.5)
                 out = out.reshape(*latent_states.shape[:-1], *self.output_dim)
         if out is None:
             out = cnn_forward(self.model, latent_states, (latent_states.shape[-1],), self.output_dim) + 0.5
@@ -204,8 +212,14 @@ class MLPDecoder(nn.Module):
         )
         self.heads = nn.ModuleList([Linear(dense_units, d) for d in self.output_dims])
 
-    def forward(self, latent_states: Tensor) -> Dict[str, Tensor]:
-        x = self.model(latent_states)
+    def forward(self, latent_states: Tensor, onehot=None) -> Dict[str, Tensor]:
+        x = None
+        if onehot is not None:
+            from sheeprl_prey_amd.ops.onehot import mlp_forward
+
+            x = mlp_forward(self.model, latent_states, *onehot)
+        if x is None:
+            x = self.model(latent_states)
         return {k: h(x) for k, h in zip(self.keys, self.heads)}
 
 
@@ -284,20 +298,26 @@ class RSSM(nn.Module):
                 and gru.layer_norm.weight is not None and gru.layer_norm.bias is not None)
 
     @torch.no_grad()
-    def imagine_discrete(self, post: Tensor, h: Tensor, actor: "Actor", horizon: int, record: bool = False):
+    def imagine_discrete(self, post: Tensor, h: Tensor, actor: "Actor", horizon: int, record: bool = False,
+                         indices: bool = False, gather: bool = True):
         """Imagination rollout for discrete actors without autograd (reference loop: ``dreamer_v3.py:
         235-257`` over ``RSSM.imagination`` + ``Actor.forward``; the discrete objective back-propagates
         only through log-probs of detached actions, so no graph is needed).
 
-        Every step writes straight into one buffer ``[H+1, M, A + S + Hd]`` holding (action | prior |
-        h): the LN-GRU and unimix-sample kernels store into row-strided slices of it, the recurrent
-        GEMM reads (action | prior) in place (weight columns permuted once), the GRU input projection
-        is two GEMMs (feat, then h accumulated) instead of a concat.  No per-step concatenations and no
-        final stacks: the trajectories ``[H+1, M, S + Hd]`` and actions ``[H+1, M, A]`` are views.
+        Every step writes straight into one buffer ``[H+1, M, A + S + Hd + D]`` holding (action | prior |
+        h | x), x = the recurrent MLP's output of the step: the sampling, LayerNorm and LN-GRU kernels
+        store into row-strided slices of it, so the GRU input projection is ONE GEMM over (h | x)
+        (K = Hd + D) and the trajectories ``[H+1, M, S + Hd]`` / actions ``[H+1, M, A]`` are views.
 
-        ``record``: the actor trunk's activations of every step are kept (``ops.mlp_trunk``) and a third
-        value is returned, the ``TrunkRecord`` the actor loss back-propagates through instead of running
-        the actor forward over the trajectories a second time."""
+        One-hot gathers (``ops/onehot.py``): actions and priors are exact one-hots, so the samplers also
+        emit their hot columns (``IDX [H+1, M, nh + G]``: action columns, then A + prior column) and
+        the recurrent MLP's [action | prior] layer is a row gather of its transposed weight + LayerNorm
+        + act in one kernel (no GEMM), the actor trunk's first layer a K = Hd GEMM + gather.
+
+        ``record``: the actor trunk's activations of every step are kept (``ops.mlp_trunk``) and
+        returned, the ``TrunkRecord`` the actor loss back-propagates through instead of running the
+        actor forward over the trajectories a second time.  ``indices``: also return ``IDX``."""
+        from sheeprl_prey_amd.ops import onehot as oh
         from sheeprl_prey_amd.ops.mlp_trunk import TrunkRecord, trunk_layers
 
         C = ops._ext()
@@ -306,42 +326,74 @@ class RSSM(nn.Module):
         A = int(sum(actor.actions_dim))
         disc = self.discrete
         nh, G = len(actor.actions_dim), S // disc
+        dev = post.device
         # every uniform of the rollout in one launch: per step nh x M for the actions, G x M for the prior
-        U = torch.rand(horizon + 1, M * (nh + G), device=post.device)
-        layers = trunk_layers(actor.model) if record else None
-        trunk_rec = TrunkRecord(layers, horizon + 1, M, post.device) if layers is not None else None
-        buf = post.new_empty(horizon + 1, M, A + S + Hd)
-        buf[0, :, A:A + S].copy_(post)
-        buf[0, :, A + S:].copy_(h)
-        rec = list(self.recurrent_model.mlp.model)
-        rec_lin, rec_rest = rec[0], rec[1:]
-        W = rec_lin.weight  # columns: (prior | action)
-        Wp = torch.cat((W[:, S:], W[:, :S]), 1)  # columns: (action | prior)
+        U = torch.rand(horizon + 1, M * (nh + G), device=dev)
+        layers = trunk_layers(actor.model)
+        trunk_rec = TrunkRecord(layers, horizon + 1, M, dev) if (record and layers is not None) else None
+        rec_sp = oh.mlp_split(self.recurrent_model.mlp)
+        rec_lin = list(self.recurrent_model.mlp.model)[0]
+        rec_ln = rec_sp[1] if rec_sp is not None else None
+        D = rec_lin.out_features
+        use_gather = (gather and rec_sp is not None and rec_ln is not None and not rec_sp[2] and oh.layer_supported(rec_lin, A + S)
+                      and rec_lin.bias is None and all(a <= 64 for a in actor.actions_dim))
         gru = self.recurrent_model.rnn
         Wg = gru.linear.weight  # columns: (h | feat)
-        WgT_h, WgT_f = Wg[:, :Hd].t(), Wg[:, Hd:].t()
         ln = gru.layer_norm
+        Wd = A + S + Hd + D
+        buf = post.new_empty(horizon + 1, M, Wd)
+        buf[0, :, A:A + S].copy_(post)
+        buf[0, :, A + S:A + S + Hd].copy_(h)
+        IDX = torch.empty(horizon + 1, M, nh + G, dtype=torch.int32, device=dev)
+        oh.onehot_index(post, disc, IDX[0, :, nh:], A)
+        W = rec_lin.weight  # columns: (prior | action)
+        Wp = torch.cat((W[:, S:], W[:, :S]), 1)  # columns: (action | prior)
+        rec_table = Wp.t().contiguous() if use_gather else None  # [A + S, D]: row = hot column of (action | prior)
+        # the actor trunk's first layer: prior columns gathered from its transposed weight, h by a GEMM
+        a0 = layers[0][0] if layers is not None else None
+        a_table = a0.weight[:, :S].t().contiguous() if (gather and layers is not None and oh.layer_supported(a0, S)) else None
+        act_scratch = None
         for t in range(horizon + 1):
-            out = trunk_rec.step(t, buf[t, :, A:]) if trunk_rec is not None else actor.model(buf[t, :, A:])
+            traj_t = buf[t, :, A:A + S + Hd]
+            if trunk_rec is not None:
+                out = trunk_rec.step(t, traj_t, gather=(IDX[t, :, nh:], G, A, S, a_table) if a_table is not None else None)
+            elif layers is not None and a_table is not None:
+                if act_scratch is None:
+                    act_scratch = TrunkRecord(layers, 1, M, dev)
+                out = act_scratch.step(0, traj_t, gather=(IDX[t, :, nh:], G, A, S, a_table))
+            else:
+                out = actor.model(traj_t)
             c0 = 0
             for i, (head, a) in enumerate(zip(actor.mlp_heads, actor.actions_dim)):
-                C.unimix_sample_into(head(out), U[t, i * M:(i + 1) * M], int(a), float(actor._unimix), buf[t, :, c0:c0 + a])
+                C.unimix_sample_into(head(out), U[t, i * M:(i + 1) * M], int(a), float(actor._unimix), buf[t, :, c0:c0 + a],
+                                     IDX[t, :, i:i + 1], c0)
                 c0 += a
             if t == horizon:
                 break
-            x = torch.mm(buf[t, :, :A + S], Wp.t())
-            if rec_lin.bias is not None:
-                x = x + rec_lin.bias
-            for m in rec_rest:
-                x = m(x)
-            gx = torch.mm(x, WgT_f)
-            gx.addmm_(buf[t, :, A + S:], WgT_h)
+            xs = buf[t, :, A + S + Hd:]
+            if use_gather:
+                oh.gather_first_layer(buf[t, :, :A + S], IDX[t], nh + G, 0, rec_lin, rec_ln, A + S, table=rec_table,
+                                      y_out=xs)
+            else:
+                x = torch.mm(buf[t, :, :A + S], Wp.t())
+                if rec_lin.bias is not None:
+                    x = x + rec_lin.bias
+                for m in list(self.recurrent_model.mlp.model)[1:]:
+                    x = m(x)
+                xs.copy_(x)
+            gx = torch.mm(buf[t, :, A + S:], Wg.t())  # (h | x) in one GEMM
             if gru.linear.bias is not None:
                 gx = gx + gru.linear.bias
-            C.ln_gru_into(gx, buf[t, :, A + S:], ln.weight, ln.bias, float(ln.eps), buf[t + 1, :, A + S:])
-            logits = self.transition_model(buf[t + 1, :, A + S:])
-            C.unimix_sample_into(logits.contiguous(), U[t, nh * M:], disc, float(self.unimix), buf[t + 1, :, A:A + S])
-        return (buf[:, :, A:], buf[:, :, :A]) + ((trunk_rec,) if record else ())
+            C.ln_gru_into(gx, buf[t, :, A + S:A + S + Hd], ln.weight, ln.bias, float(ln.eps), buf[t + 1, :, A + S:A + S + Hd])
+            logits = self.transition_model(buf[t + 1, :, A + S:A + S + Hd])
+            C.unimix_sample_into(logits.contiguous(), U[t, nh * M:], disc, float(self.unimix), buf[t + 1, :, A:A + S],
+                                 IDX[t + 1, :, nh:], A)
+        out = (buf[:, :, A:A + S + Hd], buf[:, :, :A])
+        if record:
+            out = out + (trunk_rec,)
+        if indices:
+            out = out + (IDX,)
+        return out
 
     # ---- MI355X scan: T-step posterior rollout with hoisted GEMMs --------------------
     def _mlp_head(self, mlp: MLP, x_pre: Tensor) -> Tensor:

@@ -99,6 +99,8 @@ class DreamerV3Trainer:
         # discrete fast path: record the rollout's actor forward and keep the imagination critic forward's
         # graph, so the actor / critic losses skip their second forwards (A/B switch SRL_REUSE_FWD=0)
         self.reuse_forwards = os.environ.get("SRL_REUSE_FWD", "1") != "0"
+        # first layers over the one-hot posteriors / priors as row gathers (ops/onehot.py; A/B switch SRL_ONEHOT=0)
+        self.onehot_heads = os.environ.get("SRL_ONEHOT", "1") != "0"
         self._st: Dict[str, Any] = {}
         self._gather_buf = None
         ws = runner.world_size
@@ -177,6 +179,19 @@ class DreamerV3Trainer:
             dist.all_gather(list(self._gather_buf.unbind(0)), lam.detach().contiguous(), group=self.runner.group)
         self._st["gathered"] = self._gather_buf
 
+    @staticmethod
+    def _head(mlp, x: Tensor, onehot) -> Tensor:
+        """``mlp(x)``; with ``onehot = (idx, G, off, S)`` the first layer's one-hot prior columns are row
+        gathers (``ops/onehot.py``) instead of GEMM columns."""
+        if onehot is not None:
+            from sheeprl_prey_amd.ops.onehot import mlp_forward
+
+            idx, G, off, S = onehot
+            y = mlp_forward(mlp, x, idx, G, off, S)
+            if y is not None:
+                return y
+        return mlp(x)
+
     # ------------------------------------------------------------------ phases
     def _phase_wm(self, data: Dict[str, Tensor]) -> None:
         cfg = self.cfg
@@ -197,7 +212,16 @@ class DreamerV3Trainer:
         recurrent_states, posteriors, posteriors_logits, priors_logits = wm.rssm.scan_dynamic(
             embedded_obs, batch_actions, is_first)
         latent_states = torch.cat((posteriors.view(T, B, -1), recurrent_states), -1)
-        reconstructed = wm.observation_model(latent_states)
+        # the posteriors are exact one-hots: the heads' first layers gather those columns (ops/onehot.py)
+        oh = None
+        if latent_states.is_cuda and ops.fused_enabled() and self.onehot_heads:
+            from sheeprl_prey_amd.ops.onehot import onehot_index
+
+            G = stoch
+            idx = onehot_index(posteriors.reshape(T * B, stoch * disc), disc,
+                               torch.empty(T * B, G, dtype=torch.int32, device=latent_states.device))
+            oh = (idx.view(T, B, G), G, 0, stoch * disc)
+        reconstructed = wm.observation_model(latent_states, onehot=oh) if oh is not None else wm.observation_model(latent_states)
         # image MSE against the raw uint8 frames and vector symlog MSE, one fused kernel each way (K6)
         obs_loss = 0
         for k in cfg.cnn_keys.decoder:
@@ -205,8 +229,8 @@ class DreamerV3Trainer:
             obs_loss = obs_loss + ops.obs_mse(reconstructed[k], data[k] if raw else batch_obs[k], 1.0 / 255.0 if raw else 1.0)
         for k in cfg.mlp_keys.decoder:
             obs_loss = obs_loss + ops.obs_mse(reconstructed[k], batch_obs[k], symlog=True)
-        reward_logits = wm.reward_model(latent_states)
-        continue_logits = wm.continue_model(latent_states)
+        reward_logits = self._head(wm.reward_model, latent_states, oh)
+        continue_logits = self._head(wm.continue_model, latent_states, oh)
         ents: List[Tensor] = []  # posterior / prior entropies: a by-product of the KL kernel
         rec_loss, kl, state_loss, reward_loss, observation_loss, continue_loss = reconstruction_loss(
             obs_loss, reward_logits, data["rewards"], priors_logits, posteriors_logits, stoch, disc,
@@ -241,15 +265,41 @@ class DreamerV3Trainer:
             st["out"]["Grads/world_model"] = torch.zeros((), device=data["rewards"].device)
         self.world_optimizer.step()
         grad_ctx = torch.enable_grad() if self.is_continuous else torch.no_grad()
+        # continuous actors back-propagate the policy loss through the imagined dynamics and the critic: only
+        # the DATA gradients through the world model and the critic are needed - their parameter gradients
+        # from that loss are discarded (the reference zeroes them before the next world-model / critic
+        # backward, dreamer_v3.py:179 / :336) - so the rollout's graph is built with those parameters frozen:
+        # no weight-gradient GEMMs for them in the actor backward
+        frozen = [p for m in (wm, critic) for p in m.parameters() if p.requires_grad] if self.is_continuous else []
+        for p in frozen:
+            p.requires_grad_(False)
+        try:
+            self._imagine(data, grad_ctx)
+        finally:
+            for p in frozen:
+                p.requires_grad_(True)
+
+    def _imagine(self, data: Dict[str, Tensor], grad_ctx) -> None:
+        cfg, st = self.cfg, self._st
+        wm, actor, critic = self.world_model, self.actor, self.critic
+        wm_cfg = cfg.algo.world_model
+        S = wm_cfg.stochastic_size * wm_cfg.discrete_size
+        H = wm_cfg.recurrent_model.recurrent_state_size
         with grad_ctx:
             prior = st["posteriors"].reshape(-1, S)
             h = st["recurrent_states"].reshape(-1, H)
             fast = (not self.is_continuous and prior.is_cuda and wm.rssm.imagine_fast_ok(actor))
             if fast:
-                res = wm.rssm.imagine_discrete(prior, h, actor, cfg.algo.horizon, record=self.reuse_forwards)
+                res = wm.rssm.imagine_discrete(prior, h, actor, cfg.algo.horizon, record=self.reuse_forwards,
+                                               indices=True, gather=self.onehot_heads)
                 imagined_trajectories, imagined_actions_t = res[0], res[1]
-                if len(res) > 2 and res[2] is not None:
+                if self.reuse_forwards and res[2] is not None:
                     st["actor_rec"] = res[2]
+                # hot columns of the trajectories' one-hot priors (offset: the actions' columns), for the
+                # heads' first layers as row gathers (ops/onehot.py)
+                A = imagined_actions_t.shape[-1]
+                if self.onehot_heads:
+                    st["traj_onehot"] = (res[-1][:, :, len(self.actions_dim):], S // wm_cfg.discrete_size, A, S)
             else:
                 latent = torch.cat((prior, h), -1)
                 trajectories: List[Tensor] = [latent]
@@ -264,18 +314,19 @@ class DreamerV3Trainer:
                     imagined_actions.append(actions)
                 imagined_trajectories = torch.stack(trajectories)
                 imagined_actions_t = torch.stack(imagined_actions)
+            oh = st.get("traj_onehot")
             if fast and self.reuse_forwards:
                 # the critic's forward over the trajectories, WITH its graph: the critic loss of this step
                 # (same weights - the critic steps in the final phase - same detached inputs) reuses it
                 # instead of running the critic forward a second time (reference dreamer_v3.py:260, :327)
                 with torch.enable_grad():
-                    st["critic_logits"] = critic(imagined_trajectories)
+                    st["critic_logits"] = self._head(critic, imagined_trajectories, oh)
                 predicted_values = ops.twohot_mean(st["critic_logits"].detach())
             else:
-                predicted_values = ops.twohot_mean(critic(imagined_trajectories))
-            predicted_rewards = ops.twohot_mean(wm.reward_model(imagined_trajectories))
+                predicted_values = ops.twohot_mean(self._head(critic, imagined_trajectories, oh))
+            predicted_rewards = ops.twohot_mean(self._head(wm.reward_model, imagined_trajectories, oh))
             # continuation flags, their gamma-discounts and the cumulative discount: one kernel (K11)
-            cont_g, discount = ops.imag_discount(wm.continue_model(imagined_trajectories), data["dones"],
+            cont_g, discount = ops.imag_discount(self._head(wm.continue_model, imagined_trajectories, oh), data["dones"],
                                                  cfg.algo.gamma)
             lambda_values = compute_lambda_values(predicted_rewards[1:], predicted_values[1:], cont_g,
                                                   lmbda=cfg.algo.lmbda)
@@ -337,7 +388,8 @@ class DreamerV3Trainer:
         qv_full = st.pop("critic_logits", None)
         qv_logits = qv_full[:-1] if qv_full is not None else self.critic(traj)
         with torch.no_grad():
-            target_values = ops.twohot_mean(self.target_critic(traj))
+            oh = st.get("traj_onehot")
+            target_values = ops.twohot_mean(self._head(self.target_critic, traj, (oh[0][:-1],) + oh[1:] if oh else None))
         self.critic_optimizer.zero_grad(set_to_none=True)
         value_loss = ops.twohot_nll(qv_logits, st["lambda_values"].detach()) + ops.twohot_nll(qv_logits, target_values)
         value_loss = torch.mean(value_loss * st["discount"][:-1].squeeze(-1))

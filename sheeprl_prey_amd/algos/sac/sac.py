@@ -209,6 +209,89 @@ def sac_train_update(trainer: SACTrainer, runner, cfg, rb, update: int, learning
     return True
 
 
+class SACInteraction:
+    """One env-interaction step of the SAC family (reference ``sac/sac.py:270-305``), shared by
+    ``run_sac_family`` and ``bench.py --algo sac``: act (random before ``learning_starts``, else the
+    actor - one hipGraph replay on GPU), step the envs, and store the transition row.
+
+    GPU: each env step's row (next obs, real next obs, actions, reward, done) goes to the device as ONE
+    pinned copy sliced on the device (instead of five synchronous pageable copies); the staging buffer
+    is rewritten only after an event recorded behind its last copy has completed."""
+
+    def __init__(self, runner, cfg, envs, agent, rb, obs_dim: int):
+        self.runner, self.cfg, self.envs, self.agent, self.rb = runner, cfg, envs, agent, rb
+        self.obs_dim = obs_dim
+        self.n_env = int(cfg.env.num_envs)
+        self.act_dim = int(np.prod(envs.single_action_space.shape))
+        self.step_data = TensorDict({}, batch_size=[self.n_env], device=rb.device)
+        self.gpu_row = rb.device.type == "cuda"
+        if self.gpu_row:
+            from sheeprl_prey_amd.parallel.graphs import GraphedStep
+
+            self.stage = torch.empty((self.n_env, 2 * obs_dim + self.act_dim + 2), dtype=torch.float32).pin_memory()
+            self.staged = torch.cuda.Event()  # the last copy out of `stage` (random-action steps have no readback)
+            self.player = GraphedStep(lambda d: {"a": agent.actor(d["obs"])[0]}, warmup=2, enabled=runner.cuda_graphs,
+                                      name="sac_player")
+        self._last = None
+
+    def reset(self, seed: int) -> None:
+        o = self.envs.reset(seed=seed)[0]
+        self.obs = obs_to_tensor(o, self.cfg.mlp_keys.encoder, self.rb.device, self.n_env)
+
+    def _host_rows(self, x: Dict[str, Any]) -> np.ndarray:
+        return np.concatenate([np.asarray(x[k], dtype=np.float32).reshape(self.n_env, -1)
+                               for k in self.cfg.mlp_keys.encoder], -1)
+
+    def act_and_step(self, random_actions: bool):
+        """Act and step the envs; returns the env ``infos`` (``store`` adds the row afterwards)."""
+        if random_actions:
+            actions = self.envs.action_space.sample()
+        else:
+            with torch.no_grad():
+                if self.gpu_row:
+                    actions = self.player({"obs": self.obs})["a"].cpu().numpy()
+                else:
+                    actions, _ = self.agent.actor(self.obs.to(self.runner.device))
+                    actions = actions.cpu().numpy()
+        next_o, rewards, dones, truncated, infos = self.envs.step(actions.reshape(self.envs.action_space.shape))
+        self._last = (actions, next_o, rewards, np.logical_or(dones, truncated), infos)
+        return infos
+
+    def store(self) -> None:
+        """Add the last step's transition to the replay buffer and advance the observation."""
+        cfg, rb, n_env, obs_dim, act_dim = self.cfg, self.rb, self.n_env, self.obs_dim, self.act_dim
+        actions, next_o, rewards, dones, infos = self._last
+        sd = self.step_data
+        if self.gpu_row:
+            self.staged.synchronize()
+            st = self.stage.numpy()
+            st[:, :obs_dim] = self._host_rows(next_o)
+            st[:, obs_dim:2 * obs_dim] = self._host_rows(real_next_obs(next_o, infos))
+            st[:, 2 * obs_dim:2 * obs_dim + act_dim] = np.asarray(actions, dtype=np.float32).reshape(n_env, -1)
+            st[:, -2] = np.asarray(rewards, dtype=np.float32).reshape(n_env)
+            st[:, -1] = np.asarray(dones, dtype=np.float32).reshape(n_env)
+            row = self.stage.to(rb.device, non_blocking=True)
+            self.staged.record()
+            next_obs = row[:, :obs_dim]
+            sd["dones"] = row[:, -1:]
+            sd["actions"] = row[:, 2 * obs_dim:2 * obs_dim + act_dim]
+            sd["observations"] = self.obs
+            if not cfg.buffer.sample_next_obs:
+                sd["next_observations"] = row[:, obs_dim:2 * obs_dim]
+            sd["rewards"] = row[:, -2:-1]
+        else:
+            next_obs = obs_to_tensor(next_o, cfg.mlp_keys.encoder, rb.device, n_env)
+            sd["dones"] = torch.as_tensor(dones, dtype=torch.float32).view(n_env, -1).to(rb.device)
+            sd["actions"] = torch.as_tensor(actions, dtype=torch.float32).view(n_env, -1).to(rb.device)
+            sd["observations"] = self.obs
+            if not cfg.buffer.sample_next_obs:
+                sd["next_observations"] = obs_to_tensor(real_next_obs(next_o, infos), cfg.mlp_keys.encoder,
+                                                        rb.device, n_env)
+            sd["rewards"] = torch.as_tensor(rewards, dtype=torch.float32).view(n_env, -1).to(rb.device)
+        rb.add(sd.unsqueeze(0))
+        self.obs = next_obs
+
+
 def run_sac_family(runner, cfg: Dict[str, Any], variant: str = "sac"):
     """Shared coupled main loop of SAC (``sac/sac.py:81-406``) and DroQ (``droq/droq.py:128-416``)."""
     cfg, state = load_resume(runner, cfg)
@@ -251,7 +334,6 @@ def run_sac_family(runner, cfg: Dict[str, Any], variant: str = "sac"):
                       memmap_dir=os.path.join(log_dir, "memmap_buffer", f"rank_{rank}"))
     if state and cfg.buffer.checkpoint and "rb" in state:
         restore_replay_buffer(rb, state["rb"], runner)
-    step_data = TensorDict({}, batch_size=[cfg.env.num_envs], device=rb.device)
 
     last_train = 0
     train_step = 0
@@ -267,74 +349,20 @@ def run_sac_family(runner, cfg: Dict[str, Any], variant: str = "sac"):
     warn_log_ckpt_every(cfg, policy_steps_per_update)
     ema_every = cfg.algo.critic.target_network_frequency // policy_steps_per_update + 1
 
-    o = envs.reset(seed=cfg.seed)[0]
-    obs = obs_to_tensor(o, cfg.mlp_keys.encoder, rb.device, cfg.env.num_envs)
-    # GPU: the player's actor forward is one hipGraph replay, and each env step's row (next obs, real
-    # next obs, actions, reward, done) goes to the device as ONE pinned copy sliced on the device
-    # (instead of five synchronous pageable copies).  The staging buffer is rewritten only after an event
-    # recorded behind its last copy has completed.
-    gpu_row = rb.device.type == "cuda"
-    if gpu_row:
-        from sheeprl_prey_amd.parallel.graphs import GraphedStep
-
-        n_env, act_dim = cfg.env.num_envs, int(np.prod(action_space.shape))
-        stage = torch.empty((n_env, 2 * obs_dim + act_dim + 2), dtype=torch.float32).pin_memory()
-        staged = torch.cuda.Event()  # the last copy out of `stage` (random-action steps have no readback)
-        player = GraphedStep(lambda d: {"a": agent.actor(d["obs"])[0]}, warmup=2, enabled=runner.cuda_graphs,
-                             name="sac_player")
-
-    def host_rows(x: Dict[str, Any]) -> np.ndarray:
-        return np.concatenate([np.asarray(x[k], dtype=np.float32).reshape(cfg.env.num_envs, -1)
-                               for k in cfg.mlp_keys.encoder], -1)
+    loop = SACInteraction(runner, cfg, envs, agent, rb, obs_dim)
+    loop.reset(cfg.seed)
 
     for update in range(start_step, num_updates + 1):
         policy_step += cfg.env.num_envs * world_size
         with timer("Time/env_interaction_time"):
-            if update <= learning_starts:
-                actions = envs.action_space.sample()
-            else:
-                with torch.no_grad():
-                    if gpu_row:
-                        actions = player({"obs": obs})["a"].cpu().numpy()
-                    else:
-                        actions, _ = agent.actor(obs.to(device))
-                        actions = actions.cpu().numpy()
-            next_o, rewards, dones, truncated, infos = envs.step(actions.reshape(envs.action_space.shape))
-            dones = np.logical_or(dones, truncated)
+            infos = loop.act_and_step(update <= learning_starts)
 
         for i, ep_rew, ep_len in episode_stats(infos):
             aggregator.update("Rewards/rew_avg", ep_rew)
             aggregator.update("Game/ep_len_avg", ep_len)
             runner.print(f"Rank-0: policy_step={policy_step}, reward_env_{i}={ep_rew[-1]}")
 
-        if gpu_row:
-            staged.synchronize()
-            st = stage.numpy()
-            st[:, :obs_dim] = host_rows(next_o)
-            st[:, obs_dim:2 * obs_dim] = host_rows(real_next_obs(next_o, infos))
-            st[:, 2 * obs_dim:2 * obs_dim + act_dim] = np.asarray(actions, dtype=np.float32).reshape(n_env, -1)
-            st[:, -2] = np.asarray(rewards, dtype=np.float32).reshape(n_env)
-            st[:, -1] = np.asarray(dones, dtype=np.float32).reshape(n_env)
-            row = stage.to(rb.device, non_blocking=True)
-            staged.record()
-            next_obs = row[:, :obs_dim]
-            step_data["dones"] = row[:, -1:]
-            step_data["actions"] = row[:, 2 * obs_dim:2 * obs_dim + act_dim]
-            step_data["observations"] = obs
-            if not cfg.buffer.sample_next_obs:
-                step_data["next_observations"] = row[:, obs_dim:2 * obs_dim]
-            step_data["rewards"] = row[:, -2:-1]
-        else:
-            next_obs = obs_to_tensor(next_o, cfg.mlp_keys.encoder, rb.device, cfg.env.num_envs)
-            step_data["dones"] = torch.as_tensor(dones, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
-            step_data["actions"] = torch.as_tensor(actions, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
-            step_data["observations"] = obs
-            if not cfg.buffer.sample_next_obs:
-                step_data["next_observations"] = obs_to_tensor(real_next_obs(next_o, infos), cfg.mlp_keys.encoder,
-                                                               rb.device, cfg.env.num_envs)
-            step_data["rewards"] = torch.as_tensor(rewards, dtype=torch.float32).view(cfg.env.num_envs, -1).to(rb.device)
-        rb.add(step_data.unsqueeze(0))
-        obs = next_obs
+        loop.store()
 
         if droq:
             from sheeprl_prey_amd.algos.droq.droq import droq_train_update

@@ -58,3 +58,6 @@ register("Pendulum-v1", "sheeprl_prey_amd.envs.classic:PendulumEnv", max_episode
 register("MountainCar-v0", "sheeprl_prey_amd.envs.classic:MountainCarEnv", max_episode_steps=200)
 register("MountainCarContinuous-v0", "sheeprl_prey_amd.envs.classic:MountainCarContinuousEnv", max_episode_steps=999)
 register("prey_d_1", "sheeprl_prey_amd.envs.prey.env:PreyEnv", max_episode_steps=None)
+# dm_control walker_walk-shaped synthetic control (24-dim state, 6-dim action): bench.py --algo sac
+register("walker_walk_synthetic", "sheeprl_prey_amd.envs.synthetic:SyntheticControl", max_episode_steps=1000,
+         obs_dim=24, act_dim=6)

@@ -104,3 +104,63 @@ class SyntheticAtari(Env):
             return None
         f = self._frame
         return np.repeat(f, 3, axis=-1) if f.shape[-1] == 1 else f
+
+
+class SyntheticControl(Env):
+    """Synthetic continuous-control env with the dm_control ``walker_walk`` interface (no MuJoCo /
+    dm_control in the image): a ``Box(obs_dim)`` float32 ``state`` vector, ``Box(-1, 1, act_dim)``
+    actions, 1000-step episodes.  The state follows a fixed random stable linear system driven by the
+    action through a tanh, and the reward is a smooth function of state and action in [0, 1] (walker's
+    upright x speed reward shape), so an agent has something learnable; a step costs a few
+    microseconds of host time, so benchmarks measure the learner.  With ``from_pixels`` the
+    observation is the dict ``{"rgb": CHW uint8 render, "state": ...}`` of the DMC adapter."""
+
+    metadata = {"render_modes": ["rgb_array"], "render_fps": 30}
+
+    def __init__(self, id: str = "walker_walk", obs_dim: int = 24, act_dim: int = 6, episode_length: int = 1000,
+                 render_mode: Optional[str] = "rgb_array", seed: Optional[int] = None, screen_size: int = 64,
+                 from_pixels: bool = True, from_vectors: bool = True):
+        # from_pixels / from_vectors: accepted for DMC-config compatibility; the env factory adds the rendered
+        # pixels (PixelObservationWrapper) when cnn keys are requested
+        self.id = id
+        self.obs_dim, self.act_dim = int(obs_dim), int(act_dim)
+        self.episode_length = int(episode_length)
+        self.render_mode = render_mode
+        self.size = int(screen_size)
+        self.action_space = spaces.Box(-1.0, 1.0, (self.act_dim,), np.float32)
+        self.observation_space = spaces.Box(-np.inf, np.inf, (self.obs_dim,), np.float32)
+        self.spec = EnvSpec(id, entry_point="sheeprl_prey_amd.envs.synthetic:SyntheticControl")
+        g = np.random.default_rng(1234 + self.obs_dim * 31 + self.act_dim)  # the system itself is fixed
+        q, _ = np.linalg.qr(g.standard_normal((self.obs_dim, self.obs_dim)))
+        self._A = (0.97 * q).astype(np.float32)
+        self._B = (0.3 * g.standard_normal((self.obs_dim, self.act_dim))).astype(np.float32)
+        self._w = g.standard_normal(self.obs_dim).astype(np.float32) / np.sqrt(self.obs_dim)
+        self._rng = np.random.default_rng(seed)
+        self._x = np.zeros(self.obs_dim, np.float32)
+        self._t = 0
+
+    def reset(self, *, seed: Optional[int] = None, options=None):
+        if seed is not None:
+            self._rng = np.random.default_rng(seed)
+        self._t = 0
+        self._x = self._rng.normal(0.0, 0.1, self.obs_dim).astype(np.float32)
+        return self._x.copy(), {}
+
+    def step(self, action):
+        a = np.clip(np.asarray(action, dtype=np.float32).reshape(self.act_dim), -1.0, 1.0)
+        self._x = np.tanh(self._A @ self._x + self._B @ a) + self._rng.normal(0.0, 0.01, self.obs_dim).astype(np.float32)
+        speed = float(self._w @ self._x)
+        reward = float(0.5 * (1.0 + np.tanh(speed)) * (1.0 - 0.1 * float(np.mean(a * a))))
+        self._t += 1
+        return self._x.copy(), reward, False, self._t >= self.episode_length, {}
+
+    def render(self):
+        """A 'stick figure' of the state: 8 segments whose endpoints follow pairs of state coordinates,
+        drawn over a tiled floor (64x64x3 uint8 by default)."""
+        s = self.size
+        yy, xx = np.mgrid[0:s, 0:s]
+        img = np.repeat((((xx // 8 + yy // 8) % 2) * 30 + 40).astype(np.uint8)[..., None], 3, axis=-1)
+        pts = np.clip((np.tanh(self._x[:16].reshape(8, 2)) * 0.45 + 0.5) * (s - 1), 0, s - 1).astype(np.int64)
+        for i, (x, y) in enumerate(pts):
+            img[max(y - 2, 0):y + 2, max(x - 2, 0):x + 2] = (200, 60 + 20 * i, 255 - 25 * i)
+        return img

@@ -305,10 +305,13 @@ class MultiDecoder(nn.Module):
         self.cnn_decoder = cnn_decoder
         self.mlp_decoder = mlp_decoder
 
-    def forward(self, x: Tensor) -> Dict[str, Tensor]:
+    def forward(self, x: Tensor, onehot=None) -> Dict[str, Tensor]:
+        """``onehot`` (optional ``(idx, G, off, n_onehot)``): the first ``n_onehot`` latent columns are
+        one-hot (DreamerV3 posteriors); decoders that support it gather them (``ops/onehot.py``)."""
         reconstructed_obs = {}
+        kw = {"onehot": onehot} if onehot is not None else {}
         if self.cnn_decoder is not None:
-            reconstructed_obs.update(self.cnn_decoder(x))
+            reconstructed_obs.update(self.cnn_decoder(x, **kw))
         if self.mlp_decoder is not None:
-            reconstructed_obs.update(self.mlp_decoder(x))
+            reconstructed_obs.update(self.mlp_decoder(x, **kw))
         return reconstructed_obs

@@ -37,7 +37,7 @@ int ln_gru_bwd_grid(int);
 bool launch_ln_gru_bwd(const float*, const float*, int, const float*, const float*, const float*, const float*, const float*,
                        float*, float*, float*, float*, float*, float*, int, int, hipStream_t);
 bool launch_unimix_sample_fwd(const float*, const float*, float*, float*, int, int, float, hipStream_t, int G = 0,
-                              int lds = 0);
+                              int lds = 0, int* idx = nullptr, int ldi = 0, int ioff = 0);
 bool launch_unimix_sample_bwd(const float*, const float*, const float*, float*, int, int, float, hipStream_t);
 bool launch_twohot_nll_fwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
 bool launch_twohot_nll_bwd(const float*, const float*, const float*, const float*, float*, int, int, hipStream_t);
@@ -732,15 +732,26 @@ void ln_gru_into(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::T
   TORCH_CHECK(ok, "ln_gru_into: unsupported hidden size ", H);
 }
 
+// ``idx`` (optional int32 [M, >= N / C] row-strided view): the hot column of each sampled categorical,
+// ``idx_off + g * C + pick`` (the one-hot gather consumers of ops/csrc/onehot.hip read it).
 void unimix_sample_into(torch::Tensor logits, c10::optional<torch::Tensor> uniform, int64_t classes, double alpha,
-                        torch::Tensor out) {
+                        torch::Tensor out, c10::optional<torch::Tensor> idx, int64_t idx_off) {
   check_f32(logits, "logits");
   TORCH_CHECK(out.is_cuda() && out.dim() == 2 && out.stride(1) == 1, "unimix_sample_into: out must be a row-strided 2-D view");
   const int C = classes, N = out.size(1), M = out.size(0);
   TORCH_CHECK(N % C == 0 && logits.numel() == (int64_t)M * N, "unimix_sample_into: shapes");
   const int R = M * (N / C);
+  int* ip = nullptr;
+  int ldi = 0;
+  if (idx.has_value() && idx->defined()) {
+    TORCH_CHECK(idx->is_cuda() && idx->scalar_type() == torch::kInt && idx->dim() == 2 && idx->stride(1) == 1 &&
+                    idx->size(0) == M && idx->size(1) >= N / C,
+                "unimix_sample_into: idx must be an int32 [M, >= G] row-strided view");
+    ip = idx->data_ptr<int>();
+    ldi = idx->stride(0);
+  }
   bool ok = launch_unimix_sample_fwd(logits.data_ptr<float>(), opt_ptr(uniform), nullptr, out.data_ptr<float>(), R, C,
-                                     (float)alpha, cur_stream(), N / C, out.stride(0));
+                                     (float)alpha, cur_stream(), N / C, out.stride(0), ip, ldi, (int)idx_off);
   TORCH_CHECK(ok, "unimix_sample_into: classes must be <= 64");
 }
 
@@ -1024,7 +1035,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ppo_cartpole_rollout", &ppo_cartpole_rollout);
   m.def("ppo_mlp_train_fits", &ppo_mlp_train_fits);
   m.def("ppo_mlp_train", &ppo_mlp_train);
-  m.def("unimix_sample_into", &unimix_sample_into);
+  m.def("unimix_sample_into", &unimix_sample_into, pybind11::arg("logits"), pybind11::arg("uniform"), pybind11::arg("classes"),
+        pybind11::arg("alpha"), pybind11::arg("out"), pybind11::arg("idx") = pybind11::none(), pybind11::arg("idx_off") = 0);
   m.doc() = "sheeprl_prey_amd HIP kernels (gfx950)";
   m.def("flat_grad_norm", &flat_grad_norm);
   m.def("flat_advance", &flat_advance);

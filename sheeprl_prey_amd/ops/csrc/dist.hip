@@ -38,7 +38,8 @@ __device__ __forceinline__ int seg_argmax(float v, int idx, int width) {
 __global__ void __launch_bounds__(256) unimix_sample_fwd_kernel(const float* __restrict__ logits,
                                                                 const float* __restrict__ uniform,
                                                                 float* __restrict__ mixed, float* __restrict__ sample,
-                                                                int R, int C, int W, float alpha, int G, int lds) {
+                                                                int R, int C, int W, float alpha, int G, int lds,
+                                                                int* __restrict__ idx, int ldi, int ioff) {
   const int lane = threadIdx.x & 63;
   const int seg_per_wave = 64 / W;
   const int gwave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -78,6 +79,8 @@ __global__ void __launch_bounds__(256) unimix_sample_fwd_kernel(const float* __r
     // sample rows may be strided: G categoricals per row, row stride lds (G*C when contiguous)
     const int64_t so = (int64_t)(r / G) * lds + (int64_t)(r % G) * C + k;
     sample[so] = (k == pick) ? 1.f : 0.f;
+    // optional hot-column index of the sample (ops/csrc/onehot.hip consumers): ioff + g * C + pick
+    if (idx != nullptr && k == 0) idx[(int64_t)(r / G) * ldi + (r % G)] = ioff + (r % G) * C + pick;
   }
 }
 
@@ -372,7 +375,7 @@ static int next_pow2(int c) {
 }
 
 bool launch_unimix_sample_fwd(const float* logits, const float* uniform, float* mixed, float* sample, int R, int C,
-                              float alpha, hipStream_t st, int G, int lds) {
+                              float alpha, hipStream_t st, int G, int lds, int* idx, int ldi, int ioff) {
   if (C > 64) return false;
   if (G <= 0) {
     G = 1;
@@ -381,7 +384,7 @@ bool launch_unimix_sample_fwd(const float* logits, const float* uniform, float* 
   int W = next_pow2(C);
   int segs_per_block = 4 * (64 / W);
   hipLaunchKernelGGL(unimix_sample_fwd_kernel, dim3(cdiv(R, segs_per_block)), dim3(256), 0, st, logits, uniform, mixed,
-                     sample, R, C, W, alpha, G, lds);
+                     sample, R, C, W, alpha, G, lds, idx, ldi, ioff);
   return true;
 }
 

@@ -48,11 +48,77 @@ void launch_actor_loss(const float* z, const float* act, const float* lam, const
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
                        float* dz, float* partial, float* loss, hipStream_t st);
 
+void launch_onehot_index(const float* x, int ldx, int M, int G, int C, int* idx, int ldi, int off, hipStream_t st);
+bool launch_onehot_gather_ln(const float* Y, int ldy, const int* idx, int ldi, int G, int off, const float* T, int K,
+                             const float* bias, const float* gamma, const float* beta, float eps, int act, int ln,
+                             float* z_out, int ldz, float* y_out, int ldo, float* mean, float* rstd, int M, int N, int* err,
+                             hipStream_t st);
+
 namespace {
 
 hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
+const float* optf(const c10::optional<torch::Tensor>& t, const char* name, int64_t numel) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32 && t->is_contiguous() && t->numel() == numel, "onehot: ",
+              name, " must be a contiguous float32 GPU tensor of ", numel, " elements");
+  return t->data_ptr<float>();
+}
+
+void rowview(const torch::Tensor& t, const char* name, int64_t M, int64_t N, torch::ScalarType dt) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == dt && t.dim() == 2 && t.size(0) == M && t.size(1) >= N && t.stride(1) == 1 &&
+                  t.stride(0) >= t.size(1),
+              "onehot: ", name, " must be a row-strided 2-D [", M, ", >=", N, "] view of the right dtype");
+}
+
 }  // namespace
+
+// ------------------------------------------------------------------ one-hot row gathers (onehot.hip)
+// x [M, G*C] one-hot rows (row-strided) -> idx [M, >= G] int32 (row-strided): off + g*C + hot class.
+void onehot_index(torch::Tensor x, int64_t C, torch::Tensor idx, int64_t off) {
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % C == 0, "onehot_index: x [M, G*C]");
+  const int64_t M = x.size(0), G = x.size(1) / C;
+  rowview(x, "x", M, G * C, torch::kFloat32);
+  rowview(idx, "idx", M, G, torch::kInt);
+  launch_onehot_index(x.data_ptr<float>(), x.stride(0), M, G, C, idx.data_ptr<int>(), idx.stride(0), off, stream());
+}
+
+// y = act(LN(Y + sum_j table[idx_j - off] + bias)) per row (LN when gamma/beta given or ln=true); writes z (pre-norm),
+// mean/rstd when given.  table [K, N] contiguous; Y / z / y row-strided [M, N]; idx row-strided [M, >= G].
+bool onehot_gather_ln(c10::optional<torch::Tensor> Y, torch::Tensor idx, int64_t G, int64_t off, torch::Tensor table,
+                      c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta,
+                      double eps, int64_t act, bool ln, c10::optional<torch::Tensor> z_out, torch::Tensor y_out,
+                      c10::optional<torch::Tensor> mean, c10::optional<torch::Tensor> rstd, c10::optional<torch::Tensor> err) {
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == torch::kFloat32 && table.dim() == 2 && table.is_contiguous(),
+              "onehot_gather_ln: table [K, N] contiguous float32");
+  const int64_t K = table.size(0), N = table.size(1), M = y_out.size(0);
+  rowview(y_out, "y_out", M, N, torch::kFloat32);
+  rowview(idx, "idx", M, G, torch::kInt);
+  const float* yp = nullptr;
+  int64_t ldy = 0;
+  if (Y.has_value() && Y->defined()) {
+    rowview(*Y, "Y", M, N, torch::kFloat32);
+    yp = Y->data_ptr<float>();
+    ldy = Y->stride(0);
+  }
+  float* zp = nullptr;
+  int64_t ldz = 0;
+  if (z_out.has_value() && z_out->defined()) {
+    rowview(*z_out, "z_out", M, N, torch::kFloat32);
+    zp = z_out->data_ptr<float>();
+    ldz = z_out->stride(0);
+  }
+  int* ep = nullptr;
+  if (err.has_value() && err->defined()) {
+    TORCH_CHECK(err->is_cuda() && err->scalar_type() == torch::kInt && err->numel() >= 1, "onehot_gather_ln: err int32 [1]");
+    ep = err->data_ptr<int>();
+  }
+  float* mp_ = mean.has_value() && mean->defined() ? const_cast<float*>(optf(mean, "mean", M)) : nullptr;
+  float* rp_ = rstd.has_value() && rstd->defined() ? const_cast<float*>(optf(rstd, "rstd", M)) : nullptr;
+  return launch_onehot_gather_ln(yp, ldy, idx.data_ptr<int>(), idx.stride(0), G, off, table.data_ptr<float>(), K,
+                                 optf(bias, "bias", N), optf(gamma, "gamma", N), optf(beta, "beta", N), (float)eps, act,
+                                 ln ? 1 : 0, zp, ldz, y_out.data_ptr<float>(), y_out.stride(0), mp_, rp_, M, N, ep, stream());
+}
 
 
 // ------------------------------------------------------------------ NatureCNN convolutions (natcnn.hip)
@@ -454,6 +520,11 @@ std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::T
 void register_ext(pybind11::module& m) {
   m.def("gather_rows", &gather_rows, pybind11::arg("srcs"), pybind11::arg("row"), pybind11::arg("env"),
         pybind11::arg("err") = pybind11::none());
+  m.def("onehot_index", &onehot_index);
+  m.def("onehot_gather_ln", &onehot_gather_ln, pybind11::arg("Y"), pybind11::arg("idx"), pybind11::arg("G"), pybind11::arg("off"),
+        pybind11::arg("table"), pybind11::arg("bias"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("eps"),
+        pybind11::arg("act"), pybind11::arg("ln"), pybind11::arg("z_out"), pybind11::arg("y_out"), pybind11::arg("mean"),
+        pybind11::arg("rstd"), pybind11::arg("err") = pybind11::none());
   m.def("gru_cell_fwd", &gru_cell_fwd);
   m.def("gru_cell_bwd", &gru_cell_bwd);
   m.def("lstm_fwd", &lstm_fwd);

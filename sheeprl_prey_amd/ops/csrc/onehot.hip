@@ -1,0 +1,157 @@
+// One-hot input columns as row gathers (DreamerV3 latents, reference dreamer_v3/agent.py:312-455, 602-828).
+//
+// Every DreamerV3 latent is [z | h] with z the straight-through sample of 32 categoricals x 32 classes:
+// its forward value is EXACTLY one-hot (32 ones among 1024 columns).  The first Linear of every MLP that
+// reads a latent (actor trunk, critic, target critic, reward, continue, the decoder's Linear, the
+// recurrent model's [z | a] input) therefore computes, for its z columns,
+//     z W_z^T = sum over the 32 groups g of  W_z^T[g*32 + k_g]        (k_g = the hot class of group g)
+// i.e. 32 row reads of the transposed weight instead of a K = 1024 GEMM slice: 2/3 of the K = 1536
+// GEMM of a 512-unit layer.  The dense h columns stay a library GEMM (K = 512); this kernel adds the
+// gathered rows to it and applies the layer's LayerNorm + activation in the same pass (one wave per row,
+// the whole row in registers), writing the pre-norm value (for the backward), the row statistics and
+// the activation.  Summation order differs from the dense GEMM only by fp32 rounding.
+//
+//   onehot_index_kernel   : one-hot rows (row-strided) -> int32 hot column per group (+ offset)
+//   onehot_gather_ln_kernel: y = act(LN(Y + sum_j T[idx_j - off] + bias)) per row (LN optional)
+#include "common.h"
+
+namespace srl {
+namespace onehot {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
+
+// idx[r * ldi + g] = off + g * C + argmax_k x[r * ldx + g * C + k]   (one lane per (row, group))
+__global__ void __launch_bounds__(256) onehot_index_kernel(const float* __restrict__ x, int ldx, int M, int G, int C,
+                                                           int* __restrict__ idx, int ldi, int off) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= M * G) return;
+  const int r = t / G, g = t - r * G;
+  const float* p = x + (int64_t)r * ldx + g * C;
+  int best = 0;
+  float bv = p[0];
+  for (int k = 1; k < C; ++k) {
+    const float v = p[k];
+    if (v > bv) {
+      bv = v;
+      best = k;
+    }
+  }
+  idx[(int64_t)r * ldi + g] = off + g * C + best;
+}
+
+// One wave per row; lane l owns float4 columns l, l + 64, ... (NV4 of them: N <= 256 * NV4).
+template <int NV4>
+__global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
+    const float* __restrict__ Y, int ldy, const int* __restrict__ idx, int ldi, int G, int off,
+    const float* __restrict__ T, int K, const float* __restrict__ bias, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, int act, int ln, float* __restrict__ z_out, int ldz,
+    float* __restrict__ y_out, int ldo, float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, int N,
+    int* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= M) return;
+  const int N4 = N >> 2;
+  f4 acc[NV4];
+#pragma unroll
+  for (int v = 0; v < NV4; ++v) {
+    const int i4 = lane + 64 * v;
+    acc[v] = (Y != nullptr && i4 < N4) ? reinterpret_cast<const f4*>(Y + (int64_t)r * ldy)[i4] : zero4();
+    if (bias != nullptr && i4 < N4) acc[v] += reinterpret_cast<const f4*>(bias)[i4];
+  }
+  const int* ir = idx + (int64_t)r * ldi;
+  // the row's hot indices: lanes < G load one each, then broadcast (wave-uniform loop below)
+  int my = lane < G ? ir[lane] - off : 0;
+  if (lane < G && (my < 0 || my >= K)) {  // a caller bug: skip the row read, report it
+    if (err) atomicOr(err, 1);
+    my = -1;
+  }
+  // QB table rows in flight per lane at a time (QB * NV4 = 16 float4 temporaries)
+  constexpr int QB = NV4 <= 2 ? 8 : 16 / NV4;
+  for (int j = 0; j < G; j += QB) {
+    f4 t[QB][NV4];
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int row = __shfl(my, j + q, 64);
+      const bool ok = (j + q < G) && row >= 0;
+      const f4* src = reinterpret_cast<const f4*>(T + (int64_t)(ok ? row : 0) * N);
+#pragma unroll
+      for (int v = 0; v < NV4; ++v) {
+        const int i4 = lane + 64 * v;
+        t[q][v] = (ok && i4 < N4) ? src[i4] : zero4();
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q)
+#pragma unroll
+      for (int v = 0; v < NV4; ++v) acc[v] += t[q][v];
+  }
+  if (z_out != nullptr) {
+#pragma unroll
+    for (int v = 0; v < NV4; ++v) {
+      const int i4 = lane + 64 * v;
+      if (i4 < N4) reinterpret_cast<f4*>(z_out + (int64_t)r * ldz)[i4] = acc[v];
+    }
+  }
+  float mu = 0.f, rs = 1.f;
+  if (ln) {
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV4; ++v) s += (acc[v][0] + acc[v][1]) + (acc[v][2] + acc[v][3]);
+    mu = wave_sum(s) / N;
+    float q = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV4; ++v) {
+      if (lane + 64 * v < N4) {
+        const f4 d = acc[v] - mu;
+        q += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+      }
+    }
+    rs = rsqrtf(wave_sum(q) / N + eps);
+    if (lane == 0) {
+      if (mean_out) mean_out[r] = mu;
+      if (rstd_out) rstd_out[r] = rs;
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < NV4; ++v) {
+    const int i4 = lane + 64 * v;
+    if (i4 < N4) {
+      f4 o = acc[v];
+      if (ln) {
+        const f4 g = gamma ? reinterpret_cast<const f4*>(gamma)[i4] : f4{1.f, 1.f, 1.f, 1.f};
+        const f4 b = beta ? reinterpret_cast<const f4*>(beta)[i4] : zero4();
+        o = (o - mu) * rs * g + b;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = act_fwd(o[e], act);
+      reinterpret_cast<f4*>(y_out + (int64_t)r * ldo)[i4] = o;
+    }
+  }
+}
+
+}  // namespace onehot
+}  // namespace srl
+
+void launch_onehot_index(const float* x, int ldx, int M, int G, int C, int* idx, int ldi, int off, hipStream_t st) {
+  const int n = M * G;
+  if (n > 0) hipLaunchKernelGGL(srl::onehot::onehot_index_kernel, dim3((n + 255) / 256), dim3(256), 0, st, x, ldx, M, G, C, idx, ldi, off);
+}
+
+bool launch_onehot_gather_ln(const float* Y, int ldy, const int* idx, int ldi, int G, int off, const float* T, int K,
+                             const float* bias, const float* gamma, const float* beta, float eps, int act, int ln,
+                             float* z_out, int ldz, float* y_out, int ldo, float* mean, float* rstd, int M, int N, int* err,
+                             hipStream_t st) {
+  if (N % 4 != 0 || N > 4096 || G > 64 || M <= 0) return false;
+  const int nv = (N + 255) / 256;
+  const dim3 grid((M + 3) / 4), block(256);
+#define OG(NV)                                                                                                          \
+  if (nv <= NV) {                                                                                                       \
+    hipLaunchKernelGGL(srl::onehot::onehot_gather_ln_kernel<NV>, grid, block, 0, st, Y, ldy, idx, ldi, G, off, T, K,     \
+                       bias, gamma, beta, eps, act, ln, z_out, ldz, y_out, ldo, mean, rstd, M, N, err);                   \
+    return true;                                                                                                        \
+  }
+  OG(1) OG(2) OG(4) OG(8) OG(16)
+#undef OG
+  return false;
+}

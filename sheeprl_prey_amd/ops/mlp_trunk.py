@@ -55,12 +55,23 @@ class TrunkRecord:
         self.inp: Optional[Tensor] = None  # [R, M, K0] (may be a row-strided view)
 
     @torch.no_grad()
-    def step(self, t: int, x: Tensor) -> Tensor:
-        """Forward of step ``t`` on ``x`` [M, K0] (row stride allowed); returns the trunk output [M, N]."""
+    def step(self, t: int, x: Tensor, gather=None) -> Tensor:
+        """Forward of step ``t`` on ``x`` [M, K0] (row stride allowed); returns the trunk output [M, N].
+        ``gather`` = (idx, G, off, n_onehot, table): the first ``n_onehot`` input columns are one-hot with hot
+        columns ``idx - off`` - the first layer is then a GEMM over the dense columns plus a row gather of
+        ``table`` (its transposed one-hot weight columns) with the LayerNorm fused (``ops/onehot.py``)."""
         C = ops._ext()
         M = self.M
         for i, (lin, ln) in enumerate(self.layers):
             pre = self.pre[i][t]
+            if i == 0 and gather is not None:
+                from sheeprl_prey_amd.ops.onehot import gather_first_layer
+
+                idx, G, off, n1, table = gather
+                gather_first_layer(x, idx, G, off, lin, ln, n1, table=table, y_out=self.y[0][t], z_out=pre,
+                                   mean=self.mean[0][t], rstd=self.rstd[0][t])
+                x = self.y[0][t]
+                continue
             if lin.bias is not None:
                 torch.addmm(lin.bias, x, lin.weight.t(), out=pre)
             else:

@@ -162,7 +162,10 @@ class PhasedStep:
     """A training step given as ``phases`` separated by ``colls`` (gradient all-reduces etc.).
 
     * ``graphs`` and one rank: the whole step (phases + the no-op collectives) is ONE hipGraph;
-    * ``graphs`` and N ranks: ``SegmentedGraph`` (per-phase graphs, RCCL eagerly in between);
+    * ``graphs`` and N ranks over RCCL (``runner.capture_collectives``): still ONE hipGraph per rank,
+      the collectives captured in it (``single+rccl``);
+    * ``graphs`` and N ranks otherwise (gloo): ``SegmentedGraph`` (per-phase graphs, collectives eagerly
+      in between);
     * otherwise eager.
     Phase/collective contract as in ``SegmentedGraph``."""
 
@@ -173,6 +176,9 @@ class PhasedStep:
         use = bool(graphs) and torch.cuda.is_available() and runner.device.type == "cuda"
         if not use:
             self.mode = "eager"
+        elif runner.world_size > 1 and not force_segmented and getattr(runner, "capture_collectives", False):
+            self.mode = "single+rccl"
+            self._impl = GraphedStep(self._run, warmup=warmup, enabled=True, name=name)
         elif runner.world_size > 1 or force_segmented:
             self.mode = "segmented"
             self._impl = SegmentedGraph(self.phases, self.colls, warmup=warmup)
