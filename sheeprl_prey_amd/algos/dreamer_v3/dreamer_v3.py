@@ -285,6 +285,7 @@ class DreamerV3Trainer:
         wm_cfg = cfg.algo.world_model
         S = wm_cfg.stochastic_size * wm_cfg.discrete_size
         H = wm_cfg.recurrent_model.recurrent_state_size
+        st.pop("traj_onehot", None)  # set again below by this step's rollout (never a previous step's indices)
         with grad_ctx:
             prior = st["posteriors"].reshape(-1, S)
             h = st["recurrent_states"].reshape(-1, H)
@@ -417,6 +418,7 @@ class DreamerV3Trainer:
         self.actor_optimizer.zero_grad(set_to_none=True, arm=False)
         self.critic_optimizer.zero_grad(set_to_none=True, arm=False)
         self.world_optimizer.zero_grad(set_to_none=True, arm=False)
+        st.pop("traj_onehot", None)
         for k, v in list(st.items()):
             if torch.is_tensor(v) and v.grad_fn is not None:
                 st[k] = v.detach()  # same storage (the segmented collectives re-read it), no graph

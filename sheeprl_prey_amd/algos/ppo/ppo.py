@@ -273,8 +273,17 @@ class PPOTrainer:
         self.clip_t = torch.tensor(float(cfg.algo.clip_coef), device=dev)
         self.ent_t = torch.tensor(float(cfg.algo.ent_coef), device=dev)
         graphs = dev.type == "cuda" and bool(getattr(runner, "cuda_graphs", False)) and not cfg.algo.anneal_lr
-        self.segmented = SegmentedPPOUpdate(self) if graphs and (runner.world_size > 1 or force_segmented) else None
+        ws = runner.world_size
+        # N ranks over RCCL: the per-minibatch gradient all-reduces are captured inside the ONE update graph
+        self.capture_coll = graphs and ws > 1 and not force_segmented and bool(getattr(runner, "capture_collectives", False))
+        self.segmented = (SegmentedPPOUpdate(self) if graphs and (ws > 1 or force_segmented) and not self.capture_coll
+                          else None)
         self.graphed = GraphedStep(self._train, warmup=2, enabled=graphs and self.segmented is None, name="ppo_train")
+        # DistributedSampler permutations of the shared rollout (seeded per epoch, the same every update as in
+        # the reference's sampler.set_epoch(epoch) loop): built once, static inputs of the captured update
+        self._share_perms = None
+        if bool(cfg.buffer.share_data) and ws > 1:
+            self._share_perms = [shard_indices(n, runner, True, cfg.seed, e).to(dev) for e in range(cfg.algo.update_epochs)]
         from sheeprl_prey_amd import ops
 
         plan = (FusedPPOTrainer.plan(runner, agent, optimizer, cfg)
@@ -287,7 +296,9 @@ class PPOTrainer:
             return "fused"
         if self.segmented is not None:
             return "segmented"
-        return "graph" if self.graphed.enabled else "eager"
+        if self.graphed.enabled:
+            return "graph+rccl" if self.capture_coll else "graph"
+        return "eager"
 
     def _train(self, data: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         cfg = self.cfg
@@ -295,9 +306,9 @@ class PPOTrainer:
         dev = data["rewards"].device
         sums = torch.zeros(3, device=dev)
         steps = 0
-        for _ in range(cfg.algo.update_epochs):
-            idx = torch.argsort(torch.rand(n, device=dev))
-            for start in range(0, n, bs):
+        for epoch in range(cfg.algo.update_epochs):
+            idx = self._share_perms[epoch] if self._share_perms is not None else torch.argsort(torch.rand(n, device=dev))
+            for start in range(0, idx.numel(), bs):
                 sel = idx[start : start + bs]
                 batch = {k: v.index_select(0, sel) for k, v in data.items()}
                 pg, vl, el = _minibatch_step(self.runner, self.agent, self.optimizer, batch, self.obs_keys, cfg,

@@ -236,7 +236,16 @@ __device__ __forceinline__ void gemm_reg(const WTile<NT, U>& wt, const float* As
 // One role per workgroup; each role carves the dynamic LDS its own way (floats).
 __host__ __device__ inline int lds_A(int D, int H) { return 16 * (H + D + 4) + 2 * D + 4096 + 256 + 16; }
 __host__ __device__ inline int lds_B(int H) { return 16 * (H + 4) + 6 * H + 4096 + 256 + 16; }
-__host__ __device__ inline int lds_C(int hid, int S, int C) { return 16 * (hid + 4) + 2 * hid + 8192 + 512 + 16 + 16 * (S / C); }
+__host__ __device__ inline int lds_C_base(int hid, int S, int C) { return 16 * (hid + 4) + 2 * hid + 8192 + 512 + 16 + 16 * (S / C); }
+// C also keeps its Wz^T column tiles (S rows x 16 columns each, ceil(D/16 / nC) of them) in LDS when they fit:
+// the per-step posterior gather then reads LDS instead of L2
+__host__ __device__ inline int wz_tiles(int D, int S) { return (D / 16 + S / 32 - 1) / (S / 32); }
+__host__ __device__ inline bool wz_in_lds(int hid, int S, int C, int D) {
+  return 4 * (lds_C_base(hid, S, C) + wz_tiles(D, S) * S * 16) <= 160 * 1024;
+}
+__host__ __device__ inline int lds_C(int hid, int S, int C, int D) {
+  return lds_C_base(hid, S, C) + (wz_in_lds(hid, S, C, D) ? wz_tiles(D, S) * S * 16 : 0);
+}
 __host__ __device__ inline int lds_G1(int S) { return 16 * (S + 4) + 4096 + 256 + 16; }
 __host__ __device__ inline int lds_G2(int hid) { return 32 * (hid + 4) + 2 * hid + 48 + 4096 + 256 + 1536 + 1792 + 16; }
 __host__ __device__ inline int lds_G3(int H) { return 16 * (3 * H + 4) + 64 + 4096 + 256 + 16; }
@@ -337,16 +346,19 @@ __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
     if (!wait_ctr(p, 0, eA, t + 1, 3, flag)) return;
     PROF(1, 1);
     if (w < B) {
-      // gate inputs and the nA per-tile (mean, M2) partials, all loads issued before any use
+      // gate inputs and the nA per-tile (mean, M2) partials, all loads issued before any use: 16-byte
+      // write-through (sc1) buffer loads, lane l owning columns 4l..4l+3 (+256 m) of each gate
       const float* gxr = p.gx + ((size_t)t * B + w) * N3;
-      float x0[GRU_M], x1[GRU_M], x2[GRU_M];
+      const auto grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gxr), (short)0, N3 * 4, 0x00020000);
+      constexpr int GV = GRU_M / 4;
+      f4 x0[GV], x1[GV], x2[GV];
 #pragma unroll
-      for (int m = 0; m < GRU_M; ++m) {
-        const int j = lane + 64 * m;
+      for (int m = 0; m < GV; ++m) {
+        const int j = 4 * lane + 256 * m;
         if (j < H) {
-          x0[m] = ld_wt(gxr + j);
-          x1[m] = ld_wt(gxr + H + j);
-          x2[m] = ld_wt(gxr + 2 * H + j);
+          x0[m] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(grs, j * 4, 0, 16));
+          x1[m] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(grs, (H + j) * 4, 0, 16));
+          x2[m] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(grs, (2 * H + j) * 4, 0, 16));
         }
       }
       float2 pr[2];
@@ -367,16 +379,21 @@ __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
       const float keep = 1.f - p.first[(size_t)t * B + w];
       float* hr = As + w * lda;
 #pragma unroll
-      for (int m = 0; m < GRU_M; ++m) {
-        const int j = lane + 64 * m;
+      for (int m = 0; m < GV; ++m) {
+        const int j = 4 * lane + 256 * m;
         if (j < H) {
-          const float zr = (x0[m] - mu) * rs * lgw[j] + lgb[j];
-          const float zc = (x1[m] - mu) * rs * lgw[H + j] + lgb[H + j];
-          const float zu = (x2[m] - mu) * rs * lgw[2 * H + j] + lgb[2 * H + j];
-          const float r = fsig(zr);
-          const float c = ftanh(r * zc);
-          const float uu = fsig(zu - 1.f);
-          hr[j] = uu * c + (1.f - uu) * (keep * hr[j]);
+          const f4 zr = (x0[m] - mu) * rs * *(const f4*)(lgw + j) + *(const f4*)(lgb + j);
+          const f4 zc = (x1[m] - mu) * rs * *(const f4*)(lgw + H + j) + *(const f4*)(lgb + H + j);
+          const f4 zu = (x2[m] - mu) * rs * *(const f4*)(lgw + 2 * H + j) + *(const f4*)(lgb + 2 * H + j);
+          f4 hv = *(f4*)(hr + j);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float r = fsig(zr[e]);
+            const float c = ftanh(r * zc[e]);
+            const float uu = fsig(zu[e] - 1.f);
+            hv[e] = uu * c + (1.f - uu) * (keep * hv[e]);
+          }
+          *(f4*)(hr + j) = hv;
         }
       }
       if (bI == 0 && lane == 0) {
@@ -415,6 +432,17 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
   float* ct = red + 8192;
   int* flag = (int*)(ct + 512);
   int* selL = flag + 16;  // [B][S / C] sampled rows of the step
+  // this workgroup's Wz^T column tiles q = cI, cI + nC, ... ([S][16] each), resident for all T steps
+  const bool wzl = wz_in_lds(hid, S, C, D);
+  float* wzt = (float*)(selL + 16 * nseg);
+  if (wzl) {
+    int lt = 0;
+    for (int q = cI; q < D / 16; q += nC, ++lt)
+      for (int e = threadIdx.x; e < S * 4; e += NTH) {  // float4 per (row, quarter tile)
+        const int row = e >> 2, c4 = (e & 3) * 4;
+        *(f4*)(wzt + ((size_t)lt * S + row) * 16 + c4) = *(const f4*)(p.WzT + (size_t)row * D + q * 16 + c4);
+      }
+  }
   WTile<2, UC> wt;
   wload<2, UC>(wt, p.W2 + (size_t)n0 * hid, hid, hid, w);
   stage_vec(l2w, p.ln2w, hid);
@@ -492,15 +520,24 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
       float* xr1 = p.xr + (size_t)(t + 1) * B * D;
       const int gb = threadIdx.x >> 6, gc = (threadIdx.x >> 2) & 15, gq = threadIdx.x & 3;
       const int per = (nseg + 3) >> 2;
-      for (int q = cI; q < D / 16; q += nC) {
+      for (int q = cI, lt = 0; q < D / 16; q += nC, ++lt) {
         const int col = q * 16 + gc;
         float x = 0.f;
         if (gb < B) {
           const int* sr = selL + gb * nseg;
+          if (wzl) {
+            const float* tile = wzt + (size_t)lt * S * 16 + gc;
 #pragma unroll 8
-          for (int g = gq * per; g < min(nseg, gq * per + per); ++g) {
-            const int row = sr[g];
-            if (row >= 0) x += p.WzT[(size_t)row * D + col];
+            for (int g = gq * per; g < min(nseg, gq * per + per); ++g) {
+              const int row = sr[g];
+              if (row >= 0) x += tile[row * 16];
+            }
+          } else {
+#pragma unroll 8
+            for (int g = gq * per; g < min(nseg, gq * per + per); ++g) {
+              const int row = sr[g];
+              if (row >= 0) x += p.WzT[(size_t)row * D + col];
+            }
           }
         }
         x += __shfl_xor(x, 1, 64);
@@ -891,7 +928,7 @@ int scanp_fwd_grid(int S, int H, int hid) { return 3 * H / 16 + hid / 16 + S / 3
 int scanp_bwd_grid(int S, int D, int H, int hid) { return hid / 16 + H / 16 + (H + D) / 16 + S / 32; }
 
 int scanp_fwd_lds(int S, int D, int H, int hid, int C) {
-  return 4 * std::max(std::max(lds_A(D, H), lds_B(H)), lds_C(hid, S, C));
+  return 4 * std::max(std::max(lds_A(D, H), lds_B(H)), lds_C(hid, S, C, D));
 }
 
 int scanp_bwd_lds(int S, int D, int H, int hid) {

@@ -207,19 +207,15 @@ void launch_skinny_nt(const float* A, long lda, long sA, const float* W, long ld
   p.Z = Z;
   p.splits = skinny_plan(N, K, Z, &p.kc);
   const size_t lds = sizeof(float) * 16 * (size_t)(p.kc + 4);
-  static const bool nt = env_int("SRL_SKINNY_NT", 0) != 0;  // non-temporal weight loads (experiment)
+  // weight loads use the default cache policy: the non-temporal variant measured no better (round 2)
   static bool attr = false;  // > 64 KiB dynamic LDS needs the opt-in once per process
   if (!attr) {
-    for (const void* f : {reinterpret_cast<const void*>(srl::skinny::skinny_nt_kernel<true>),
-                          reinterpret_cast<const void*>(srl::skinny::skinny_nt_kernel<false>)})
-      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(float) * 16 * (2048 + 4)));
+    hipFuncSetAttribute(reinterpret_cast<const void*>(srl::skinny::skinny_nt_kernel<false>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)(sizeof(float) * 16 * (2048 + 4)));
     attr = true;
   }
   const dim3 grid(N / srl::skinny::WG_ROWS, p.splits, Z);
-  if (nt)
-    hipLaunchKernelGGL(srl::skinny::skinny_nt_kernel<true>, grid, dim3(srl::skinny::NTH), lds, st, p);
-  else
-    hipLaunchKernelGGL(srl::skinny::skinny_nt_kernel<false>, grid, dim3(srl::skinny::NTH), lds, st, p);
+  hipLaunchKernelGGL(srl::skinny::skinny_nt_kernel<false>, grid, dim3(srl::skinny::NTH), lds, st, p);
   if (p.splits > 1)
     hipLaunchKernelGGL(srl::skinny::skinny_reduce_kernel, dim3((N / 4 + 63) / 64, M, Z), dim3(srl::skinny::NTH), 0, st, p);
 }
