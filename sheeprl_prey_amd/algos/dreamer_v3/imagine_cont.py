@@ -1,0 +1,263 @@
+"""DreamerV3 imagination for continuous (trunc_normal) actors as ONE autograd node.
+
+Reference (``dreamer_v3.py:235-301``, ``agent.py:440-455, 685-700``): the continuous policy loss is the
+lambda-return itself, so it back-propagates through the whole H = 15 step imagined rollout - critic,
+reward and continue heads -> trajectories -> transition MLP -> straight-through prior samples -> LN-GRU
+-> recurrent MLP -> the reparameterised actions -> the actor.  The reference builds that as a Python
+loop of ~40 autograd nodes per step (the actor twice: once in the rollout, once more over the stacked
+trajectories for the entropy) and replays it op by op.
+
+Here the rollout is a buffer-resident no-grad forward (the same hand-offs as the discrete
+``RSSM.imagine_discrete``: one ``[H+1, M, S + Hd + D]`` buffer of (prior | h | x), one-hot priors as
+row gathers, the GRU input projection as one GEMM over (h | x), the actor trunk recorded by
+``ops.mlp_trunk.TrunkRecord``, the actor head + truncated-normal sample in one kernel) and the backward
+is hand-written:
+
+* reverse-time chain over the dynamics only (the actor reads detached latents, reference
+  ``dreamer_v3.py:240``): per step the unimix straight-through backward, two transition GEMMs + the
+  fused LayerNorm backward, the LN-GRU backward, the (h | x) GEMM, the recurrent LayerNorm backward and
+  its input GEMM - data gradients only: the world model and the critic are frozen during imagination
+  (``DreamerV3Trainer._phase_imagine``), their parameter gradients from this loss are discarded by the
+  reference anyway;
+* ONE batched actor backward over all ``(H+1) M`` rows: the head + rsample backward kernel (with the
+  entropy's gradient on the head output folded in), the head GEMMs, the recorded trunk's chain.
+
+Outputs: trajectories ``[H+1, M, S + Hd]``, actions ``[H+1, M, A]`` and the actor head outputs
+``pre [H+1, M, 2A]`` (the policy distributions for the entropy are built from ``pre`` - no second
+actor forward).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor, nn
+
+from sheeprl_prey_amd import ops
+
+_EPS = float(torch.finfo(torch.float32).eps)
+
+
+def supported(rssm: nn.Module, actor: nn.Module) -> bool:
+    """Layouts the fused rollout covers: DV3 RSSM with LayerNorm'ed recurrent / transition MLPs and a
+    LayerNorm'ed trunc_normal actor with one head; anything else runs the eager loop."""
+    from sheeprl_prey_amd.algos.dreamer_v3.agent import Actor
+    from sheeprl_prey_amd.ops import onehot as oh
+    from sheeprl_prey_amd.ops.mlp_trunk import trunk_layers
+    from sheeprl_prey_amd.utils.model import LayerNorm
+
+    if not (type(actor) is Actor and actor.is_continuous and actor.distribution == "trunc_normal"
+            and len(actor.mlp_heads) == 1 and ops.native_available() and ops.fused_enabled()):
+        return False
+    if getattr(rssm, "_srl_autocast", False) or getattr(actor, "_srl_autocast", False):
+        return False
+    layers = trunk_layers(actor.model)
+    if layers is None or not oh.layer_supported(layers[0][0], rssm.transition_model.model[-1].out_features):
+        return False
+    rec = oh.mlp_split(rssm.recurrent_model.mlp)
+    if rec is None or rec[1] is None or rec[2] or rec[0].bias is not None:
+        return False
+    if not oh.layer_supported(rec[0], rssm.transition_model.model[-1].out_features):
+        return False
+    tr = list(rssm.transition_model.model)
+    if not (len(tr) == 4 and isinstance(tr[0], nn.Linear) and type(tr[1]) is LayerNorm and isinstance(tr[2], nn.Identity)
+            and isinstance(tr[3], nn.Linear) and tr[1].weight is not None and tr[1].bias is not None):
+        return False
+    gru = rssm.recurrent_model.rnn
+    return (isinstance(gru.layer_norm, nn.LayerNorm) and gru.layer_norm.weight is not None
+            and gru.layer_norm.bias is not None and rssm.discrete <= 64)
+
+
+class ContinuousRollout:
+    """Forward state of one imagined rollout (buffers sized once per call)."""
+
+    def __init__(self, rssm: nn.Module, actor: nn.Module, post: Tensor, h: Tensor, horizon: int) -> None:
+        from sheeprl_prey_amd.ops import onehot as oh
+        from sheeprl_prey_amd.ops.mlp_trunk import TrunkRecord, trunk_layers
+
+        self.rssm, self.actor, self.H = rssm, actor, horizon
+        M, S = post.shape
+        Hd = h.shape[1]
+        dev = post.device
+        self.M, self.S, self.Hd = M, S, Hd
+        self.disc = rssm.discrete
+        self.G = S // self.disc
+        self.A = int(sum(actor.actions_dim))
+        rec_lin, rec_ln, _ = oh.mlp_split(rssm.recurrent_model.mlp)
+        self.rec_lin, self.rec_ln = rec_lin, rec_ln
+        self.D = D = rec_lin.out_features
+        tr = list(rssm.transition_model.model)
+        self.tr1, self.tr_ln, self.tr2 = tr[0], tr[1], tr[3]
+        self.gru = rssm.recurrent_model.rnn
+        self.layers = trunk_layers(actor.model)
+        self.head = actor.mlp_heads[0]
+        R = horizon + 1
+        self.trunk = TrunkRecord(self.layers, R, M, dev)
+        self.buf = post.new_empty(R, M, S + Hd + D)  # (prior | h | x)
+        self.IDX = torch.empty(R, M, self.G, dtype=torch.int32, device=dev)
+        self.pre = post.new_empty(R, M, 2 * self.A)
+        self.acts = post.new_empty(R, M, self.A)
+        self.loc = post.new_empty(R, M, self.A)
+        self.scale = post.new_empty(R, M, self.A)
+        self.u_act = post.new_empty(R, M, self.A).uniform_(_EPS, 1.0 - _EPS)
+        self.u_prior = torch.rand(horizon, M * self.G, device=dev)
+        hid = self.tr1.out_features
+        self.rec_z = post.new_empty(horizon, M, D)
+        self.rec_mean = post.new_empty(horizon, M)
+        self.rec_rstd = post.new_empty(horizon, M)
+        self.gx = post.new_empty(horizon, M, 3 * Hd)
+        self.g_mean = post.new_empty(horizon, M)
+        self.g_rstd = post.new_empty(horizon, M)
+        self.tr_pre = post.new_empty(horizon, M, hid)
+        self.tr_y = post.new_empty(horizon, M, hid)
+        self.tr_mean = post.new_empty(horizon, M)
+        self.tr_rstd = post.new_empty(horizon, M)
+        self.logits = post.new_empty(horizon, M, S)
+        W = rec_lin.weight  # columns: (prior | action)
+        self.rec_table = W[:, :S].t().contiguous()
+        self.a_table = self.layers[0][0].weight[:, :S].t().contiguous()
+        self.buf[0, :, :S].copy_(post)
+        self.buf[0, :, S:S + Hd].copy_(h)
+        oh.onehot_index(post, self.disc, self.IDX[0], 0)
+
+    @torch.no_grad()
+    def forward(self) -> None:
+        from sheeprl_prey_amd.ops.onehot import _err_word
+
+        C = ops._ext()
+        M, S, Hd, A, G = self.M, self.S, self.Hd, self.A, self.G
+        actor, buf = self.actor, self.buf
+        init_std, min_std = float(actor.init_std), float(actor.min_std)
+        Wr = self.rec_lin.weight
+        Wr_a = Wr[:, S:]
+        Wg = self.gru.linear.weight  # columns: (h | feat)
+        gln = self.gru.layer_norm
+        rln, tln = self.rec_ln, self.tr_ln
+        err = _err_word(buf.device)
+        for t in range(self.H + 1):
+            out = self.trunk.step(t, buf[t, :, :S + Hd], gather=(self.IDX[t], G, 0, S, self.a_table))
+            torch.addmm(self.head.bias, out, self.head.weight.t(), out=self.pre[t])
+            C.tn_head_sample_fwd(self.pre[t], self.u_act[t], init_std, min_std, -1.0, 1.0, self.loc[t], self.scale[t],
+                                 self.acts[t])
+            if t == self.H:
+                break
+            # recurrent MLP: action columns by a K = A GEMM, prior columns gathered, LayerNorm + act fused
+            Y = torch.mm(self.acts[t], Wr_a.t())
+            ok = C.onehot_gather_ln(Y, self.IDX[t], G, 0, self.rec_table, None, rln.weight, rln.bias, float(rln.eps),
+                                    ops._act_code(rln.act), True, self.rec_z[t], buf[t, :, S + Hd:], self.rec_mean[t],
+                                    self.rec_rstd[t], err)
+            if not ok:
+                raise RuntimeError("onehot_gather_ln: unsupported recurrent layer width")
+            gx = self.gx[t]
+            torch.mm(buf[t, :, S:], Wg.t(), out=gx)  # (h | x) in one GEMM
+            if self.gru.linear.bias is not None:
+                gx += self.gru.linear.bias
+            C.ln_gru_into(gx, buf[t, :, S:S + Hd], gln.weight, gln.bias, float(gln.eps), buf[t + 1, :, S:S + Hd],
+                          self.g_mean[t], self.g_rstd[t])
+            hid = self.tr_pre.shape[-1]
+            if self.tr1.bias is not None:
+                torch.addmm(self.tr1.bias, buf[t + 1, :, S:S + Hd], self.tr1.weight.t(), out=self.tr_pre[t])
+            else:
+                torch.mm(buf[t + 1, :, S:S + Hd], self.tr1.weight.t(), out=self.tr_pre[t])
+            C.ln_act_fwd_into(self.tr_pre[t], hid, self.tr_y[t], hid, tln.weight, tln.bias, self.tr_mean[t],
+                              self.tr_rstd[t], M, hid, 1, float(tln.eps), ops._act_code(tln.act))
+            if self.tr2.bias is not None:
+                torch.addmm(self.tr2.bias, self.tr_y[t], self.tr2.weight.t(), out=self.logits[t])
+            else:
+                torch.mm(self.tr_y[t], self.tr2.weight.t(), out=self.logits[t])
+            C.unimix_sample_into(self.logits[t], self.u_prior[t], self.disc, float(self.rssm.unimix), buf[t + 1, :, :S],
+                                 self.IDX[t + 1], 0)
+        self.trunk.inp = buf[:, :, :S + Hd]
+
+    def backward(self, d_traj: Optional[Tensor], d_acts: Optional[Tensor], d_pre: Optional[Tensor]):
+        """Gradients of the actor parameters (trunk ``[W, b, gamma, beta] * L`` then head ``W, b``)."""
+        C = ops._ext()
+        M, S, Hd, A, H = self.M, self.S, self.Hd, self.A, self.H
+        buf = self.buf
+        dev = buf.device
+        Wr = self.rec_lin.weight
+        Wg = self.gru.linear.weight
+        gln, rln, tln = self.gru.layer_norm, self.rec_ln, self.tr_ln
+        d_a = torch.zeros(H + 1, M, A, device=dev) if d_acts is None else d_acts.contiguous().clone()
+        if d_traj is not None:
+            d_traj = d_traj.reshape(H + 1, M, S + Hd)
+            dh = d_traj[H, :, S:].contiguous()
+            dp = d_traj[H, :, :S].contiguous()
+        else:
+            dh = torch.zeros(M, Hd, device=dev)
+            dp = torch.zeros(M, S, device=dev)
+        gcols = 3 * Hd
+        grid = C.ln_gru_bwd_grid(M)
+        pdg = torch.empty(grid, gcols, device=dev)
+        pdb = torch.empty(grid, gcols, device=dev)
+        dgx = torch.empty(M, gcols, device=dev)
+        dh_prev = torch.empty(M, Hd, device=dev)
+        hid = self.tr_pre.shape[-1]
+        dtr = torch.empty(M, hid, device=dev)
+        D = self.D
+        dz = torch.empty(M, D, device=dev)
+        t_act, r_act = ops._act_code(tln.act), ops._act_code(rln.act)
+        for t in range(H, 0, -1):
+            s = t - 1  # the step that produced (prior_t, h_t)
+            # prior_t = straight-through unimix sample of logits[s]
+            dlog = C.unimix_sample_bwd(self.logits[s], None, dp, self.disc, float(self.rssm.unimix))
+            du = torch.mm(dlog, self.tr2.weight)
+            C.ln_act_bwd_into(self.tr_pre[s], hid, du, hid, dtr, hid, tln.weight, tln.bias, self.tr_mean[s], self.tr_rstd[s],
+                              None, None, None, None, M, hid, 1, t_act)
+            dh.addmm_(dtr, self.tr1.weight)
+            # h_t = LN-GRU(gx[s], h_s)
+            C.ln_gru_bwd_into(self.gx[s], buf[s, :, S:S + Hd], buf.stride(1), gln.weight, gln.bias, self.g_mean[s],
+                              self.g_rstd[s], dh, dgx, dh_prev, pdg, pdb, None, None, M, Hd)
+            dcat = torch.mm(dgx, Wg)  # [M, Hd + D]: (h | x)
+            # x_s = act(LN([prior_s | a_s] Wr^T)) (no bias)
+            C.ln_act_bwd_into(self.rec_z[s], D, dcat[:, Hd:], Hd + D, dz, D, rln.weight, rln.bias, self.rec_mean[s],
+                              self.rec_rstd[s], None, None, None, None, M, D, 1, r_act)
+            d_a[s].addmm_(dz, Wr[:, S:])
+            if s == 0:
+                break  # (prior_0, h_0) are the detached posteriors
+            dp = torch.mm(dz, Wr[:, :S])
+            dh = dh_prev + dcat[:, :Hd]
+            if d_traj is not None:
+                dp += d_traj[s, :, :S]
+                dh += d_traj[s, :, S:]
+        # one batched actor backward over all (H+1) M rows
+        R = (H + 1) * M
+        dpre = C.tn_head_sample_bwd(self.loc.view(R, A), self.scale.view(R, A), self.u_act.view(R, A), d_a.view(R, A),
+                                    d_pre.reshape(R, 2 * A).contiguous() if d_pre is not None else None,
+                                    float(self.actor.min_std), -1.0, 1.0)
+        out = self.trunk.y[-1].view(R, -1)
+        head_w = dpre.t().mm(out) if self.head.weight.requires_grad else None
+        head_b = C.colsum(dpre) if (self.head.bias is not None and self.head.bias.requires_grad) else None
+        grads = self.trunk.backward(dpre.mm(self.head.weight).view(H + 1, M, -1))
+        return grads + [head_w, head_b]
+
+    def params(self):
+        return self.trunk.params() + [self.head.weight, self.head.bias]
+
+
+class _ImagineContinuous(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, roll: ContinuousRollout, *params):
+        roll.forward()
+        ctx.roll = roll
+        ctx.set_materialize_grads(False)
+        S, Hd = roll.S, roll.Hd
+        traj = roll.buf[:, :, :S + Hd]
+        return traj.view_as(traj), roll.acts.view_as(roll.acts), roll.pre.view_as(roll.pre)
+
+    @staticmethod
+    def backward(ctx, d_traj, d_acts, d_pre):
+        roll: ContinuousRollout = ctx.roll
+        ctx.roll = None
+        grads = roll.backward(d_traj, d_acts, d_pre)
+        return (None, *grads)
+
+
+def imagine_continuous(rssm: nn.Module, actor: nn.Module, post: Tensor, h: Tensor,
+                       horizon: int) -> Tuple[Tensor, Tensor, Tensor, ContinuousRollout]:
+    """(trajectories [H+1, M, S + Hd], actions [H+1, M, A], actor head outputs [H+1, M, 2A], rollout).
+    The three outputs share one autograd node whose backward is ``ContinuousRollout.backward``; the
+    rollout also holds the trajectories' one-hot prior indices (``roll.IDX``) for the heads' gathers."""
+    roll = ContinuousRollout(rssm, actor, post.detach().contiguous(), h.detach().contiguous(), horizon)
+    traj, acts, pre = _ImagineContinuous.apply(roll, *roll.params())
+    return traj, acts, pre, roll

@@ -63,6 +63,10 @@ void launch_truncnorm_logprob_fwd(const float*, const float*, const float*, cons
                                   int, hipStream_t);
 void launch_truncnorm_logprob_bwd(const float*, const float*, const float*, const float*, int, const float*, int, const float*,
                                   float*, float*, float*, int, int, hipStream_t);
+void launch_tn_head_sample_fwd(const float*, int, const float*, float, float, float, float, float*, float*, float*, int, int, int,
+                               hipStream_t);
+void launch_tn_head_sample_bwd(const float*, const float*, const float*, const float*, const float*, float, float, float, float*,
+                               int, int, hipStream_t);
 
 void launch_scan4_fwd(const srl::scan4::SP&, hipStream_t);
 void launch_scan4_bwd(const srl::scan4::SP&, hipStream_t);
@@ -704,6 +708,39 @@ std::vector<torch::Tensor> truncnorm_logprob_bwd(torch::Tensor v, torch::Tensor 
   return {gv, gl, gs};
 }
 
+// DreamerV3 trunc_normal actor head: pre [M, 2A] (row-strided) -> loc, scale [M, A] and the sample into x
+// (row-strided [M, A] view); uniforms u [M, A].
+void tn_head_sample_fwd(torch::Tensor pre, torch::Tensor u, double init_std, double min_std, double lo, double hi,
+                        torch::Tensor loc, torch::Tensor scale, torch::Tensor x) {
+  check_f32(pre, "pre");
+  check_f32(u, "u");
+  TORCH_CHECK(pre.dim() == 2 && pre.stride(1) == 1 && x.dim() == 2 && x.stride(1) == 1, "tn_head_sample: 2-D row-strided views");
+  const int M = pre.size(0), A = pre.size(1) / 2;
+  TORCH_CHECK(pre.size(1) == 2 * A && x.size(0) == M && x.size(1) == A && u.numel() == (int64_t)M * A &&
+                  loc.numel() == (int64_t)M * A && scale.numel() == (int64_t)M * A && loc.is_contiguous() && scale.is_contiguous() &&
+                  u.is_contiguous(),
+              "tn_head_sample_fwd: shapes");
+  launch_tn_head_sample_fwd(fp(pre), pre.stride(0), fp(u), (float)init_std, (float)min_std, (float)lo, (float)hi, mp(loc),
+                            mp(scale), mp(x), x.stride(0), M, A, cur_stream());
+}
+
+// d pre [M, 2A] of the head + sample above: gx = d sample (optional), dpre_in = a gradient reaching pre directly
+// (optional, [M, 2A] contiguous).
+torch::Tensor tn_head_sample_bwd(torch::Tensor loc, torch::Tensor scale, torch::Tensor u, c10::optional<torch::Tensor> gx,
+                                 c10::optional<torch::Tensor> dpre_in, double min_std, double lo, double hi) {
+  const int A = loc.size(-1);
+  const int M = loc.numel() / A;
+  TORCH_CHECK(loc.is_contiguous() && scale.is_contiguous() && u.is_contiguous() && scale.numel() == loc.numel() &&
+                  u.numel() == loc.numel(), "tn_head_sample_bwd: loc/scale/u must be contiguous [M, A]");
+  if (gx.has_value() && gx->defined()) TORCH_CHECK(gx->is_contiguous() && gx->numel() == loc.numel(), "tn_head_sample_bwd: gx");
+  if (dpre_in.has_value() && dpre_in->defined())
+    TORCH_CHECK(dpre_in->is_contiguous() && dpre_in->numel() == 2 * loc.numel(), "tn_head_sample_bwd: dpre_in");
+  auto dpre = torch::empty({M, 2 * A}, loc.options());
+  launch_tn_head_sample_bwd(fp(loc), fp(scale), fp(u), ofp(gx), ofp(dpre_in), (float)min_std, (float)lo, (float)hi, mp(dpre), M,
+                            A, cur_stream());
+  return dpre;
+}
+
 std::vector<int64_t> scanp_info(int64_t B, int64_t S, int64_t D, int64_t H, int64_t hid, int64_t C) {
   // [supported, sync words, error word index, forward grid, backward grid]
   const int words = scanp_sync_words();
@@ -716,7 +753,9 @@ std::vector<int64_t> scanp_info(int64_t B, int64_t S, int64_t D, int64_t H, int6
 // ------------------------------------------------------------------ strided-output (no-grad) forms
 // Write into a caller-owned row-strided view (e.g. a slice of an imagination trajectory buffer):
 // out must have unit stride in its last dim; rows may be strided.
-void ln_gru_into(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::Tensor beta, double eps, torch::Tensor out) {
+// ``mean`` / ``rstd`` (optional [M]): keep the LayerNorm row statistics (for a later ln_gru_bwd_into).
+void ln_gru_into(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::Tensor beta, double eps, torch::Tensor out,
+                 c10::optional<torch::Tensor> mean_out, c10::optional<torch::Tensor> rstd_out) {
   check_f32(x, "x");
   check_f32(gamma, "gamma");
   check_f32(beta, "beta");
@@ -724,8 +763,10 @@ void ln_gru_into(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::T
               "ln_gru_into: h/out must be row-strided 2-D views");
   const int H = h.size(1), M = h.size(0);
   TORCH_CHECK(x.numel() == (int64_t)M * 3 * H && out.size(0) == M && out.size(1) == H, "ln_gru_into: shapes");
-  auto mean = torch::empty({M}, x.options());
-  auto rstd = torch::empty({M}, x.options());
+  const bool keep = mean_out.has_value() && mean_out->defined() && rstd_out.has_value() && rstd_out->defined();
+  if (keep) TORCH_CHECK(mean_out->numel() == M && rstd_out->numel() == M, "ln_gru_into: mean/rstd must hold M rows");
+  auto mean = keep ? *mean_out : torch::empty({M}, x.options());
+  auto rstd = keep ? *rstd_out : torch::empty({M}, x.options());
   bool ok = launch_ln_gru_fwd(x.data_ptr<float>(), h.data_ptr<float>(), h.stride(0), gamma.data_ptr<float>(),
                               beta.data_ptr<float>(), out.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                               M, H, (float)eps, cur_stream(), out.stride(0));
@@ -1029,7 +1070,9 @@ void register_ext(pybind11::module& m);
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_conv(m);
   register_ext(m);
-  m.def("ln_gru_into", &ln_gru_into);
+  m.def("ln_gru_into", &ln_gru_into, pybind11::arg("x"), pybind11::arg("h"), pybind11::arg("gamma"), pybind11::arg("beta"),
+        pybind11::arg("eps"), pybind11::arg("out"), pybind11::arg("mean") = pybind11::none(),
+        pybind11::arg("rstd") = pybind11::none());
   m.def("colsum", &colsum);
   m.def("cartpole_step", &cartpole_step);
   m.def("ppo_cartpole_rollout", &ppo_cartpole_rollout);
@@ -1081,6 +1124,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("truncnorm_rsample_bwd", &truncnorm_rsample_bwd);
   m.def("truncnorm_logprob_fwd", &truncnorm_logprob_fwd);
   m.def("truncnorm_logprob_bwd", &truncnorm_logprob_bwd);
+  m.def("tn_head_sample_fwd", &tn_head_sample_fwd);
+  m.def("tn_head_sample_bwd", &tn_head_sample_bwd);
   m.def("set_scanp_prof", &set_scanp_prof);
   m.def("set_scanp_health", &set_scanp_health);
   m.def("set_scan4_prof", &set_scan4_prof);

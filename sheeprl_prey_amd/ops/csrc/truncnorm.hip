@@ -105,6 +105,60 @@ __global__ void logprob_bwd(const float* __restrict__ v, const float* __restrict
   }
 }
 
+// DreamerV3 continuous actor head + sample in one pass (reference agent.py:685-700, trunc_normal):
+//   loc = tanh(pre[:, a]),  scale = 2 sigmoid((pre[:, A + a] + init_std) / 2) + min_std,  x ~ TN(loc, scale, lo, hi)
+// pre [M, 2A] with row stride ldp, u [M, A]; loc / scale [M, A] kept for the backward, x row-strided (ldx).
+__global__ void head_sample_fwd(const float* __restrict__ pre, int ldp, const float* __restrict__ u, float init_std,
+                                float min_std, float lo, float hi, float* __restrict__ loc_out, float* __restrict__ scale_out,
+                                float* __restrict__ x, int ldx, int M, int A) {
+  const int n = M * A;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int r = i / A, a = i - r * A;
+    const float l = tanhf(pre[(int64_t)r * ldp + a]);
+    const float sg = 1.f / (1.f + __expf(-0.5f * (pre[(int64_t)r * ldp + A + a] + init_std)));
+    const float s = 2.f * sg + min_std;
+    const Trunc t = bounds(l, s, lo, hi);
+    const float xi = cdf(t.alpha) + u[i] * t.Z;
+    loc_out[i] = l;
+    scale_out[i] = s;
+    x[(int64_t)r * ldx + a] = l + s * (SQRT_2 * erfinvf(2.f * xi - 1.f));
+  }
+}
+
+// d pre [M, 2A] = (d loc * (1 - loc^2) | d scale * sg (1 - sg)) (+ dpre_in), with (d loc, d scale) the
+// rsample backward of gx (gx may be null: only dpre_in), sg = (scale - min_std) / 2.
+__global__ void head_sample_bwd(const float* __restrict__ loc, const float* __restrict__ scale, const float* __restrict__ u,
+                                const float* __restrict__ gx, const float* __restrict__ dpre_in, float min_std, float lo,
+                                float hi, float* __restrict__ dpre, int M, int A) {
+  const int n = M * A;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int r = i / A, a = i - r * A;
+    const float l = loc[i], sc = scale[i];
+    float gl = 0.f, gs = 0.f;
+    if (gx != nullptr) {
+      const float ui = u[i], g = gx[i];
+      const Trunc t = bounds(l, sc, lo, hi);
+      const float xi = cdf(t.alpha) + ui * t.Z;
+      const float s = SQRT_2 * erfinvf(2.f * xi - 1.f);
+      const float da = t.clamped ? t.pa : (1.f - ui) * t.pa;
+      const float db = t.clamped ? 0.f : ui * t.pb;
+      const float inv = 1.f / (INV_SQRT_2PI * __expf(-0.5f * s * s));
+      const float wa = isfinite(t.alpha) ? t.alpha * da : 0.f, wb = isfinite(t.beta) ? t.beta * db : 0.f;
+      gl = g * (1.f - (da + db) * inv);
+      gs = g * (s - (wa + wb) * inv);
+    }
+    const float sg = 0.5f * (sc - min_std);
+    const int64_t o = (int64_t)r * 2 * A + a;
+    float dm = gl * (1.f - l * l), ds = gs * sg * (1.f - sg);
+    if (dpre_in != nullptr) {
+      dm += dpre_in[o];
+      ds += dpre_in[o + A];
+    }
+    dpre[o] = dm;
+    dpre[o + A] = ds;
+  }
+}
+
 inline int grid_for(int n) { return std::max(1, std::min((n + 255) / 256, 2048)); }
 
 }  // namespace tn
@@ -132,4 +186,18 @@ void launch_truncnorm_logprob_bwd(const float* v, const float* loc, const float*
                                   hipStream_t st) {
   hipLaunchKernelGGL(logprob_bwd, dim3(grid_for(n)), dim3(256), 0, st, v, loc, scale, lo, nlo, hi, nhi, g, gv, gloc, gscale, n,
                      np);
+}
+
+void launch_tn_head_sample_fwd(const float* pre, int ldp, const float* u, float init_std, float min_std, float lo, float hi,
+                               float* loc, float* scale, float* x, int ldx, int M, int A, hipStream_t st) {
+  if (M * A > 0)
+    hipLaunchKernelGGL(head_sample_fwd, dim3(grid_for(M * A)), dim3(256), 0, st, pre, ldp, u, init_std, min_std, lo, hi, loc,
+                       scale, x, ldx, M, A);
+}
+
+void launch_tn_head_sample_bwd(const float* loc, const float* scale, const float* u, const float* gx, const float* dpre_in,
+                               float min_std, float lo, float hi, float* dpre, int M, int A, hipStream_t st) {
+  if (M * A > 0)
+    hipLaunchKernelGGL(head_sample_bwd, dim3(grid_for(M * A)), dim3(256), 0, st, loc, scale, u, gx, dpre_in, min_std, lo, hi,
+                       dpre, M, A);
 }

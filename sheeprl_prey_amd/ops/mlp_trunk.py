@@ -82,15 +82,45 @@ class TrunkRecord:
             x = self.y[i][t]
         return x
 
+    def backward(self, dy: Tensor) -> List[Optional[Tensor]]:
+        """Parameter gradients ``[W, b, gamma, beta] * L`` (None where not required) of the recorded
+        trunk for the output gradient ``dy`` [R, M, N] (``self.inp`` must hold the trunk inputs)."""
+        C = ops._ext()
+        RM = self.R * self.M
+        L = len(self.layers)
+        grads: List[Optional[Tensor]] = [None] * (4 * L)
+        dy = dy.reshape(RM, -1)
+        if dy.stride(-1) != 1 or dy.stride(0) != dy.shape[-1]:
+            dy = dy.contiguous()
+        for i in reversed(range(L)):
+            lin, ln = self.layers[i]
+            N = lin.out_features
+            pre = self.pre[i].view(RM, N)
+            dpre, dg, db = C.ln_act_bwd(pre, dy, ln.weight, ln.bias, self.mean[i].view(RM), self.rstd[i].view(RM),
+                                        ops._act_code(ln.act))
+            x = self.y[i - 1].view(RM, -1) if i > 0 else self.inp.reshape(RM, self.inp.shape[-1])
+            grads[4 * i] = dpre.t().mm(x) if lin.weight.requires_grad else None
+            if lin.bias is not None and lin.bias.requires_grad:
+                grads[4 * i + 1] = C.colsum(dpre)
+            grads[4 * i + 2] = dg if ln.weight.requires_grad else None
+            grads[4 * i + 3] = db if ln.bias.requires_grad else None
+            if i > 0:
+                dy = dpre.mm(lin.weight)
+        return grads
+
+    def params(self) -> List[Tensor]:
+        """The trunk's parameters in ``backward``'s gradient order (a missing bias as an empty tensor)."""
+        out = []
+        for lin, ln in self.layers:
+            out += [lin.weight, lin.bias if lin.bias is not None else _NONE, ln.weight, ln.bias]
+        return out
+
     def output(self, inputs: Tensor) -> Tensor:
         """The recorded trunk output ``[R, M, N]`` as a tensor whose backward runs the batched chain.
         ``inputs`` [R, M, K0]: the rollout's trunk inputs (their gradient is not computed: the DV3
         actor reads detached latents)."""
         self.inp = inputs
-        params = []
-        for lin, ln in self.layers:
-            params += [lin.weight, lin.bias if lin.bias is not None else _NONE, ln.weight, ln.bias]
-        return _RecordedTrunk.apply(self, *params)
+        return _RecordedTrunk.apply(self, *self.params())
 
 
 _NONE = torch.empty(0)
@@ -106,26 +136,5 @@ class _RecordedTrunk(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         rec: TrunkRecord = ctx.rec
-        C = ops._ext()
-        RM = rec.R * rec.M
-        L = len(rec.layers)
-        grads: List[Optional[Tensor]] = [None] * (4 * L)
-        dy = dy.reshape(RM, -1)
-        if dy.stride(-1) != 1 or dy.stride(0) != dy.shape[-1]:
-            dy = dy.contiguous()
-        for i in reversed(range(L)):
-            lin, ln = rec.layers[i]
-            N = lin.out_features
-            pre = rec.pre[i].view(RM, N)
-            dpre, dg, db = C.ln_act_bwd(pre, dy, ln.weight, ln.bias, rec.mean[i].view(RM), rec.rstd[i].view(RM),
-                                        ops._act_code(ln.act))
-            x = rec.y[i - 1].view(RM, -1) if i > 0 else rec.inp.reshape(RM, rec.inp.shape[-1])
-            grads[4 * i] = dpre.t().mm(x) if lin.weight.requires_grad else None
-            if lin.bias is not None and lin.bias.requires_grad:
-                grads[4 * i + 1] = C.colsum(dpre)
-            grads[4 * i + 2] = dg if ln.weight.requires_grad else None
-            grads[4 * i + 3] = db if ln.bias.requires_grad else None
-            if i > 0:
-                dy = dpre.mm(lin.weight)
         ctx.rec = None
-        return (None, *grads)
+        return (None, *rec.backward(dy))
