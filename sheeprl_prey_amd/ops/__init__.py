@@ -613,6 +613,42 @@ def sac_twin_q_target(ens, obs: Tensor, act: Tensor, logp: Tensor, rewards: Tens
                                     l2.weight.detach(), l2.bias.detach(), hd.weight.detach(), hd.bias.detach(), float(gamma))
 
 
+class _SACCriticLoss(torch.autograd.Function):
+    """``csrc/sac_critic.hip``: forward + loss + data backward in one launch, weight gradients in one."""
+
+    @staticmethod
+    def forward(ctx, obs, act, y, W1, b1, W2, b2, W3, b3):
+        lossp, q, *saved = _ext().sac_critic_fwd(obs, act, y, W1, b1, W2, b2, W3, b3)
+        ctx.save_for_backward(*saved)
+        ctx.IN = W1.shape[2]
+        ctx.mark_non_differentiable(q)
+        return lossp.sum(), q
+
+    @staticmethod
+    def backward(ctx, g, _gq):
+        grads = _ext().sac_critic_wgrad(*ctx.saved_tensors, g.reshape(1).contiguous(), ctx.IN)
+        return (None, None, None, *grads)
+
+
+def sac_critic_loss(ens, obs: Tensor, act: Tensor, y: Tensor) -> Optional[Tuple[Tensor, Tensor]]:
+    """(``sum_c mean_b (Q_c(s, a) - y)^2``, q [B, n]) for an ``EnsembleMLP`` critic (2 ReLU hidden layers,
+    scalar head, no dropout / LayerNorm) as two kernels (K15, ``csrc/sac_critic.hip``) whose backward gives
+    every critic parameter's gradient; None outside the kernels' gate (the caller keeps the eager path)."""
+    if not (_native(obs) and obs.dtype == torch.float32 and act.dtype == torch.float32 and obs.dim() == 2):
+        return None
+    if ens.norms is not None or (ens.dropout > 0 and ens.training) or ens.act_name != "relu" or len(ens.layers) != 2:
+        return None
+    if ens.head is None or ens.head.out_features != 1 or ens.layers[0].bias is None or ens.layers[1].bias is None:
+        return None
+    H = ens.layers[0].out_features
+    if not (1 <= ens.n <= 8 and H % 128 == 0 and H <= 512 and ens.layers[1].out_features == H
+            and obs.shape[1] + act.shape[1] <= 1024):
+        return None
+    l1, l2, hd = ens.layers[0], ens.layers[1], ens.head
+    return _SACCriticLoss.apply(obs.contiguous(), act.contiguous(), y.detach().reshape(-1).contiguous().float(), l1.weight,
+                                l1.bias, l2.weight, l2.bias, hd.weight, hd.bias)
+
+
 # =============================================================== DreamerV3 observation loss (K6)
 class _ObsMSE(torch.autograd.Function):
     @staticmethod

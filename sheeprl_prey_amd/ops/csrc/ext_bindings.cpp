@@ -22,6 +22,15 @@ void launch_sac_target(const float* obs, const float* act, const float* logp, co
                        const float* log_alpha, const float* W1, const float* b1, const float* W2, const float* b2,
                        const float* W3, const float* b3, float* y, int M, int OD, int AD, int H, int n, float gamma,
                        hipStream_t st);
+size_t sac_critic_fwd_lds(int INp, int H);
+int sac_critic_blocks(int M);
+void launch_sac_critic_fwd(const float* obs, const float* act, const float* y, const float* W1, const float* b1,
+                           const float* W2, const float* b2, const float* W3, const float* b3, float* X, float* H1, float* H2,
+                           float* DH1, float* DH2, float* DQ, float* Q, float* lossp, int M, int OD, int AD, int H, int n,
+                           hipStream_t st);
+void launch_sac_critic_wgrad(const float* X, const float* H1, const float* H2, const float* DH1, const float* DH2,
+                             const float* DQ, const float* g, float* dW1, float* db1, float* dW2, float* db2, float* dW3,
+                             float* db3, int M, int IN, int H, int n, hipStream_t st);
 void launch_wm_loss_fwd(const float* kl_loss, const float* obs, const float* rew, const float* logit, const float* done,
                         const float* kl, int R, float kl_reg, float scale, float* total, float* means, hipStream_t st);
 void launch_wm_loss_bwd(const float* logit, const float* done, const float* g, int R, float kl_reg, float scale, float* d_kll,
@@ -311,6 +320,54 @@ torch::Tensor sac_twin_q_target(torch::Tensor obs, torch::Tensor act, torch::Ten
   return y;
 }
 
+// ------------------------------------------------------------------ SAC twin-Q critic update (sac_critic.hip)
+// -> {loss partials [n * blocks], q [M, n], saved: X, H1, H2, DH1, DH2, DQ}
+std::vector<torch::Tensor> sac_critic_fwd(torch::Tensor obs, torch::Tensor act, torch::Tensor y, torch::Tensor W1,
+                                          torch::Tensor b1, torch::Tensor W2, torch::Tensor b2, torch::Tensor W3, torch::Tensor b3) {
+  for (auto* t : {&obs, &act, &y, &W1, &b1, &W2, &b2, &W3, &b3}) nc_check(*t, "sac_critic operand");
+  TORCH_CHECK(obs.dim() == 2 && act.dim() == 2 && obs.size(0) == act.size(0), "sac_critic: obs / act [M, *]");
+  const int64_t M = obs.size(0), OD = obs.size(1), AD = act.size(1), IN = OD + AD;
+  TORCH_CHECK(M >= 1 && y.numel() == M, "sac_critic: y holds one target per row");
+  TORCH_CHECK(W1.dim() == 3 && W1.size(2) == IN, "sac_critic: W1 [n, H, obs+act]");
+  const int64_t n = W1.size(0), H = W1.size(1), INp = (IN + 15) / 16 * 16;
+  TORCH_CHECK(n >= 1 && n <= 8 && H % 128 == 0 && H <= 512 && IN <= 1024, "sac_critic: n <= 8, H % 128 == 0, H <= 512");
+  TORCH_CHECK(b1.numel() == n * H && W2.numel() == n * H * H && b2.numel() == n * H && W3.numel() == n * H && b3.numel() == n,
+              "sac_critic: layer shapes");
+  auto o = obs.options();
+  const int64_t blocks = sac_critic_blocks((int)M);
+  auto lossp = torch::empty({n * blocks}, o);
+  auto q = torch::empty({M, n}, o);
+  auto X = torch::empty({M, INp}, o);
+  auto H1 = torch::empty({n, M, H}, o), H2 = torch::empty({n, M, H}, o);
+  auto DH1 = torch::empty({n, M, H}, o), DH2 = torch::empty({n, M, H}, o);
+  auto DQ = torch::empty({n, M}, o);
+  launch_sac_critic_fwd(obs.data_ptr<float>(), act.data_ptr<float>(), y.data_ptr<float>(), W1.data_ptr<float>(),
+                        b1.data_ptr<float>(), W2.data_ptr<float>(), b2.data_ptr<float>(), W3.data_ptr<float>(), b3.data_ptr<float>(),
+                        X.data_ptr<float>(), H1.data_ptr<float>(), H2.data_ptr<float>(), DH1.data_ptr<float>(), DH2.data_ptr<float>(),
+                        DQ.data_ptr<float>(), q.data_ptr<float>(), lossp.data_ptr<float>(), (int)M, (int)OD, (int)AD, (int)H, (int)n,
+                        stream());
+  return {lossp, q, X, H1, H2, DH1, DH2, DQ};
+}
+
+// -> {dW1 [n, H, IN], db1 [n, H], dW2 [n, H, H], db2 [n, H], dW3 [n, 1, H], db3 [n, 1]}, scaled by g (device scalar)
+std::vector<torch::Tensor> sac_critic_wgrad(torch::Tensor X, torch::Tensor H1, torch::Tensor H2, torch::Tensor DH1,
+                                            torch::Tensor DH2, torch::Tensor DQ, torch::Tensor g, int64_t IN) {
+  for (auto* t : {&X, &H1, &H2, &DH1, &DH2, &DQ, &g}) nc_check(*t, "sac_critic_wgrad operand");
+  TORCH_CHECK(H1.dim() == 3, "sac_critic_wgrad: H1 [n, M, H]");
+  const int64_t n = H1.size(0), M = H1.size(1), H = H1.size(2), INp = (IN + 15) / 16 * 16;
+  TORCH_CHECK(X.numel() == M * INp && H2.sizes() == H1.sizes() && DH1.sizes() == H1.sizes() && DH2.sizes() == H1.sizes() &&
+                  DQ.numel() == n * M && g.numel() >= 1 && H % 128 == 0,
+              "sac_critic_wgrad: saved shapes");
+  auto o = H1.options();
+  auto dW1 = torch::empty({n, H, IN}, o), db1 = torch::empty({n, H}, o), dW2 = torch::empty({n, H, H}, o);
+  auto db2 = torch::empty({n, H}, o), dW3 = torch::empty({n, 1, H}, o), db3 = torch::empty({n, 1}, o);
+  launch_sac_critic_wgrad(X.data_ptr<float>(), H1.data_ptr<float>(), H2.data_ptr<float>(), DH1.data_ptr<float>(),
+                          DH2.data_ptr<float>(), DQ.data_ptr<float>(), g.data_ptr<float>(), dW1.data_ptr<float>(),
+                          db1.data_ptr<float>(), dW2.data_ptr<float>(), db2.data_ptr<float>(), dW3.data_ptr<float>(),
+                          db3.data_ptr<float>(), (int)M, (int)IN, (int)H, (int)n, stream());
+  return {dW1, db1, dW2, db2, dW3, db3};
+}
+
 // ------------------------------------------------------------------ DV3 world-model loss assembly (wm_loss.hip)
 static void row_check(const torch::Tensor& t, int64_t R, const char* name) {
   nc_check(t, name);
@@ -518,6 +575,8 @@ std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::T
 }
 
 void register_ext(pybind11::module& m) {
+  m.def("sac_critic_fwd", &sac_critic_fwd);
+  m.def("sac_critic_wgrad", &sac_critic_wgrad);
   m.def("gather_rows", &gather_rows, pybind11::arg("srcs"), pybind11::arg("row"), pybind11::arg("env"),
         pybind11::arg("err") = pybind11::none());
   m.def("onehot_index", &onehot_index);

@@ -947,7 +947,19 @@ bool scanp_supported(int B, int S, int D, int H, int hid, int C) {
   int dev = 0, cus = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  return scanp_fwd_grid(S, H, hid) <= cus && scanp_bwd_grid(S, D, H, hid) <= cus;
+  // co-residency: every workgroup must be resident at once (they hand off to each other), so the grid
+  // must fit the occupancy the compiler/runtime report for these kernels at their LDS size - not just
+  // the CU count.  Another process or stream sharing the CUs can still starve a wave: the bounded
+  // waits + the sticky health word (check_scan_health on the host) catch that at run time.
+  set_lds((const void*)fwd_kernel, 160 * 1024);
+  set_lds((const void*)bwd_kernel, 160 * 1024);
+  int occ_f = 0, occ_b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, (const void*)fwd_kernel, NTH, scanp_fwd_lds(S, D, H, hid, C)) !=
+          hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_b, (const void*)bwd_kernel, NTH, scanp_bwd_lds(S, D, H, hid)) !=
+          hipSuccess)
+    return false;
+  return scanp_fwd_grid(S, H, hid) <= cus * occ_f && scanp_bwd_grid(S, D, H, hid) <= cus * occ_b;
 }
 
 void launch_scanp_fwd(const PP& p, hipStream_t st) {

@@ -128,3 +128,32 @@ def test_sac_twin_q_target_kernel_matches_eager(n, H, obs_dim, act_dim, M):
         got = ops.sac_twin_q_target(crit.model, obs, act, logp, rew, done, log_alpha, gamma)
     assert got is not None and got.shape == ref.shape
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("n,H,obs_dim,act_dim,M", [(2, 256, 24, 6, 256), (2, 128, 17, 8, 100), (3, 512, 3, 1, 64),
+                                                   (2, 256, 10, 6, 33)])
+def test_sac_critic_fused_loss_and_grads_match_eager(n, H, obs_dim, act_dim, M):
+    """K15: the fused twin-Q critic update (forward + MSE loss + backward, csrc/sac_critic.hip) vs the
+    eager ensemble + ``critic_loss`` autograd (reference sac/agent.py:256-275, sac/loss.py:15-20)."""
+    from sheeprl_prey_amd import ops
+    from sheeprl_prey_amd.algos.sac.agent import SACCriticEnsemble
+    from sheeprl_prey_amd.algos.sac.loss import critic_loss
+
+    torch.manual_seed(7 * n + H + M)
+    crit = SACCriticEnsemble(obs_dim + act_dim, n=n, hidden_size=H).cuda()
+    obs = torch.randn(M, obs_dim, device="cuda")
+    act = torch.rand(M, act_dim, device="cuda") * 2 - 1
+    y = torch.randn(M, 1, device="cuda")
+    params = list(crit.parameters())
+    q_ref = crit(obs, act)
+    loss_ref = critic_loss(q_ref, y, n)
+    g_ref = torch.autograd.grad(loss_ref * 0.7, params)
+    res = ops.sac_critic_loss(crit.model, obs, act, y)
+    assert res is not None
+    loss, q = res
+    torch.testing.assert_close(q, q_ref.detach(), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(loss, loss_ref.detach(), rtol=1e-4, atol=1e-5)
+    g = torch.autograd.grad(loss * 0.7, params)
+    names = [nm for nm, _ in crit.named_parameters()]
+    for nm, a, b in zip(names, g, g_ref):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-5, msg=lambda m, nm=nm: f"{nm}: {m}")
