@@ -9,8 +9,9 @@ channel LayerNorm + activation into the epilogue of the convolution that produce
 each LayerNorm/activation backward into the epilogue of the data-gradient convolution that produces
 its input gradient (backward).  The stack's weights stay in the reference's ``state_dict`` layout;
 they are re-packed (one tiny kernel per layer) at use.  Eligibility (``encoder_spec`` /
-``decoder_spec``): k4 s2 p1 convolutions, channel counts in {32, 64, 128, 256}, at most 4 image
-channels, power-of-two image size; anything else runs the eager modules (MIOpen).
+``decoder_spec``): k4 s2 p1 convolutions, channel counts in ``_OK_CH`` (every preset's multiplier:
+32 / 64 / 96 x 2^k, i.e. Atari-100k, L, XL and the 128 px 5-stage stacks), 1-4 image channels (RGB or
+grayscale), power-of-two image size of at least 32; anything else runs the eager modules (MIOpen).
 """
 from __future__ import annotations
 
@@ -19,7 +20,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 from torch import Tensor, nn
 
-_OK_CH = (32, 64, 128, 256)
+_OK_CH = (32, 64, 96, 128, 192, 256, 384, 512, 768, 1024)  # conv.hip tile table
 ENABLED = True  # A/B switch: False routes the stacks through the per-layer modules (MIOpen + LN kernels)
 # Below this many frames (e.g. the env-interaction player, one frame per env) the deepest stage has
 # too few output rows to fill the chip (E4: 16 rows per frame) and a single workgroup walks all of K:
@@ -78,7 +79,7 @@ def encoder_spec(model: nn.Module, image_hw: Tuple[int, int], in_ch: int):
     except (AttributeError, IndexError, TypeError):
         return None
     st = _stages(seq, nn.Conv2d)
-    if not st or in_ch > 4 or not (_pow2(image_hw[0]) and _pow2(image_hw[1])):
+    if not st or in_ch > 4 or not (_pow2(image_hw[0]) and _pow2(image_hw[1])) or min(image_hw) < 32:
         return None
     h, w = image_hw
     for conv, ln in st:
@@ -89,8 +90,6 @@ def encoder_spec(model: nn.Module, image_hw: Tuple[int, int], in_ch: int):
         h, w = h // 2, w // 2
         if h < 1 or w < 1:
             return None
-    if st[-1][0].out_channels < 64:
-        return None
     return st
 
 
@@ -103,7 +102,7 @@ def decoder_spec(model: nn.Module, out_ch: int):
     if not isinstance(lin, nn.Linear) or not isinstance(unflat, nn.Unflatten):
         return None
     st = _stages(decnn.model, nn.ConvTranspose2d)
-    if not st or len(st) < 2:
+    if not st or len(st) < 3:  # the last layer's input grid (4 * 2^(stages-1)) must be a multiple of 16
         return None
     for conv, ln in st[:-1]:
         if ln is None or conv.bias is not None or conv.in_channels not in _OK_CH or conv.out_channels not in _OK_CH:
@@ -111,7 +110,9 @@ def decoder_spec(model: nn.Module, out_ch: int):
         if ln.weight is None or ln.bias is None or ln.normalized_shape[0] != conv.out_channels:
             return None
     last, ln_last = st[-1]
-    if ln_last is not None or last.bias is None or last.in_channels != 32 or last.out_channels != 3 or out_ch != 3:
+    if ln_last is not None or last.bias is None or last.in_channels % 32 or not 1 <= last.out_channels <= 4:
+        return None
+    if out_ch != last.out_channels:
         return None
     return lin, st
 

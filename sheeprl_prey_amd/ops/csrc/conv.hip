@@ -19,7 +19,8 @@
 //   LN_ACT : z = acc; y = act(LN(z)) (+ per-pixel mean/rstd)        (forward of conv -> LN -> act)
 //   LN_BWD : acc = dy of the NEXT-lower layer's output; dz = LN/act backward, dgamma/dbeta atomics
 //   PLAIN  : out = acc + bias + c0, NHWC or NCHW (for the 3-channel image / the flat Linear seam)
-// All spatial sizes and channel counts on this path are powers of two (host-checked).
+// Spatial sizes are powers of two; channel counts are multiples of 32 up to 1024 (the 4-channel image
+// side: a power of two below 32); all host-checked.
 #include "common.h"
 #include "conv.h"
 
@@ -71,11 +72,14 @@ __device__ __forceinline__ float cact_grad(float z, int act) {
 // stage's latency hides behind the current stage's MFMAs), store() writes them to LDS.
 
 // DOWN gather: rows = small-grid pixels m=(n,p,q), k = tap*Cb + b; Q is NHWC on the large grid.
+// Cb is either a multiple of 32 (every BK = 32 chunk of K lies inside one tap: the tap is a per-stage
+// scalar) or a power of two below 32 (the 4-channel image input: taps change inside a chunk).
 template <int ROWS, int NTH>
 struct DownGather {
-  static constexpr int NV = ROWS * BK / 4 / NTH;
+  static constexpr int NV = (ROWS * BK / 4 + NTH - 1) / NTH;  // a 32-row tile under 512 threads: half a slot
+  static constexpr bool FULL = ROWS * BK / 4 % NTH == 0;
   const float* Q;
-  int lCb, lSH, lSW, M;
+  int Cb, lCb, lSH, lSW, M;
   int pix[NV], py[NV], px[NV];  // per slot: n*LH*LW, 2p-1, 2q-1 (pix = -1: row out of range)
   __device__ void init(int m0, int) {
     const int LH = 2 << lSH, LW = 2 << lSW;
@@ -83,13 +87,26 @@ struct DownGather {
     for (int v = 0; v < NV; ++v) {
       const int idx = threadIdx.x + NTH * v, m = m0 + (idx >> 3);
       const int n = m >> (lSH + lSW), p = (m >> lSW) & ((1 << lSH) - 1), q = m & ((1 << lSW) - 1);
-      pix[v] = m < M ? n * LH * LW : -1;
+      pix[v] = (m < M && (FULL || idx < ROWS * BK / 4)) ? n * LH * LW : -1;
       py[v] = 2 * p - 1;
       px[v] = 2 * q - 1;
     }
   }
   __device__ void load(int k0, f4* r) const {
-    const int LH = 2 << lSH, LW = 2 << lSW, Cb = 1 << lCb;
+    const int LH = 2 << lSH, LW = 2 << lSW;
+    if (Cb >= BK) {
+      const int tap = k0 / Cb, b0 = k0 - tap * Cb, dy = tap >> 2, dx = tap & 3;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int b = b0 + 4 * ((threadIdx.x + NTH * v) & 7);
+        const int iy = py[v] + dy, ix = px[v] + dx;
+        f4 val = zero4();
+        if (pix[v] >= 0 && iy >= 0 && iy < LH && ix >= 0 && ix < LW)
+          val = *(const f4*)(Q + ((pix[v] + iy * LW + ix) * Cb + b));  // < 2^31 (host-checked)
+        r[v] = val;
+      }
+      return;
+    }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int k = k0 + 4 * ((threadIdx.x + NTH * v) & 7);
@@ -105,18 +122,20 @@ struct DownGather {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int idx = threadIdx.x + NTH * v;
-      *(f4*)(s + (idx >> 3) * LDK + 4 * (idx & 7)) = r[v];
+      if (FULL || idx < ROWS * BK / 4) *(f4*)(s + (idx >> 3) * LDK + 4 * (idx & 7)) = r[v];
     }
   }
 };
 
 // UP gather: rows = large-grid pixels of parity class (cy,cx) (blockIdx.z), m=(n,u,v) -> (2u+cy, 2v+cx);
 // k = t*Ca + a with t = (th,tw) in 2x2; source pixel (u+cy-th, v+cx-tw) of P (NHWC, small grid).
+// Ca is a multiple of 32, so a BK chunk lies inside one tap t.
 template <int ROWS, int NTH>
 struct UpGather {
-  static constexpr int NV = ROWS * BK / 4 / NTH;
+  static constexpr int NV = (ROWS * BK / 4 + NTH - 1) / NTH;  // a 32-row tile under 512 threads: half a slot
+  static constexpr bool FULL = ROWS * BK / 4 % NTH == 0;
   const float* P;
-  int lCa, lSH, lSW, M;
+  int Ca, lSH, lSW, M;
   int pix[NV], pu[NV], pv[NV];
   __device__ void init(int m0, int cls) {
     const int cy = cls >> 1, cx = cls & 1;
@@ -124,21 +143,21 @@ struct UpGather {
     for (int v = 0; v < NV; ++v) {
       const int idx = threadIdx.x + NTH * v, m = m0 + (idx >> 3);
       const int n = m >> (lSH + lSW), u = (m >> lSW) & ((1 << lSH) - 1), w = m & ((1 << lSW) - 1);
-      pix[v] = m < M ? n << (lSH + lSW) : -1;
+      pix[v] = (m < M && (FULL || idx < ROWS * BK / 4)) ? n << (lSH + lSW) : -1;
       pu[v] = u + cy;
       pv[v] = w + cx;
     }
   }
   __device__ void load(int k0, f4* r) const {
-    const int SH = 1 << lSH, SW = 1 << lSW, Ca = 1 << lCa;
+    const int SH = 1 << lSH, SW = 1 << lSW;
+    const int t = k0 / Ca, a0 = k0 - t * Ca, dy = t >> 1, dx = t & 1;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const int k = k0 + 4 * ((threadIdx.x + NTH * v) & 7);
-      const int t = k >> lCa, a = k & (Ca - 1);
-      const int p = pu[v] - (t >> 1), q = pv[v] - (t & 1);
+      const int a = a0 + 4 * ((threadIdx.x + NTH * v) & 7);
+      const int p = pu[v] - dy, q = pv[v] - dx;
       f4 val = zero4();
       if (pix[v] >= 0 && p >= 0 && p < SH && q >= 0 && q < SW)
-        val = *(const f4*)(P + ((size_t)(pix[v] + p * SW + q) << lCa) + a);
+        val = *(const f4*)(P + ((pix[v] + p * SW + q) * Ca + a));  // < 2^31 (host-checked)
       r[v] = val;
     }
   }
@@ -146,7 +165,7 @@ struct UpGather {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int idx = threadIdx.x + NTH * v;
-      *(f4*)(s + (idx >> 3) * LDK + 4 * (idx & 7)) = r[v];
+      if (FULL || idx < ROWS * BK / 4) *(f4*)(s + (idx >> 3) * LDK + 4 * (idx & 7)) = r[v];
     }
   }
 };
@@ -182,14 +201,14 @@ template <int ROWS, int NTH>
 struct WgP {
   static constexpr int NV = ROWS * BK / 4 / NTH;
   const float* P;
-  int lCa, M, a0;
+  int Ca, M, a0;
   __device__ void init(int r0) { a0 = r0; }
   __device__ void load(int k0, f4* r) const {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int idx = threadIdx.x + NTH * v;
       const int m = k0 + (idx & 31), a = a0 + 4 * (idx >> 5);
-      r[v] = m < M ? *(const f4*)(P + ((size_t)m << lCa) + a) : zero4();
+      r[v] = m < M ? *(const f4*)(P + (m * Ca + a)) : zero4();
     }
   }
   __device__ void store(const f4* r, float* s) const {
@@ -206,24 +225,34 @@ struct WgP {
 };
 
 // WGRAD operand B: rows j = tap*Cb + b, k = small-grid pixels m=(n,p,q); value Q[n, 2p-1+kh, 2q-1+kw, b].
+// A thread's rows are fixed for the whole launch: their (tap, b) split is done once in init.
 template <int ROWS, int NTH>
 struct WgQ {
   static constexpr int NV = ROWS * BK / 4 / NTH;
   const float* Q;
-  int lCb, lSH, lSW, M, j0;
-  __device__ void init(int r0) { j0 = r0; }
+  int Cb, lSH, lSW, M;
+  int dy[NV], dx[NV], bo[NV];
+  __device__ void init(int j0) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int j = j0 + 4 * ((threadIdx.x + NTH * v) >> 5);
+      const int tap = j / Cb;
+      dy[v] = (tap >> 2) - 1;
+      dx[v] = (tap & 3) - 1;
+      bo[v] = j - tap * Cb;
+    }
+  }
   __device__ void load(int k0, f4* r) const {
-    const int LH = 2 << lSH, LW = 2 << lSW, Cb = 1 << lCb;
+    const int LH = 2 << lSH, LW = 2 << lSW;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int idx = threadIdx.x + NTH * v;
-      const int m = k0 + (idx & 31), j = j0 + 4 * (idx >> 5);
-      const int tap = j >> lCb, b = j & (Cb - 1);
+      const int m = k0 + (idx & 31);
       const int n = m >> (lSH + lSW), p = (m >> lSW) & ((1 << lSH) - 1), q = m & ((1 << lSW) - 1);
-      const int iy = 2 * p - 1 + (tap >> 2), ix = 2 * q - 1 + (tap & 3);
+      const int iy = 2 * p + dy[v], ix = 2 * q + dx[v];
       f4 val = zero4();
       if (m < M && iy >= 0 && iy < LH && ix >= 0 && ix < LW)
-        val = *(const f4*)(Q + ((size_t)((n * LH + iy) * LW + ix) << lCb) + b);
+        val = *(const f4*)(Q + (((n * LH + iy) * LW + ix) * Cb + bo[v]));
       r[v] = val;
     }
   }
@@ -269,17 +298,21 @@ struct Frag {
 // processed by LPR lanes (CPL contiguous channels each: vector loads/stores, row reductions by xor
 // shuffles inside the LPR-lane segment).  This keeps the epilogue's register footprint small, so
 // the MFMA main loop keeps its occupancy.
-// Four channels per lane (16 B vector LDS reads / global stores; a row of 32 channels is 8 lanes, so a
-// row reduction is 3 xor levels and a wave covers 8 rows per pass).  One channel per lane (the first
-// version, 32/64 lanes per row) made the LN epilogue of the narrow E1 / D4 layers (K = 64: two
-// main-loop stages) dominate their kernels: 14% MFMA busy, 57% of wave cycles parked.
+// Four channels per lane up to 256 channels (16 B vector LDS reads / global stores; a row of 32
+// channels is 8 lanes, so a row reduction is 3 xor levels and a wave covers 8 rows per pass); wider
+// rows use all 64 lanes (8 / 12 / 16 channels per lane at 512 / 768 / 1024), and the 3 x 2^k widths
+// (96, 192, 384, 768: the XL multiplier) take 3 / 6 / 12 channels per lane.  One channel per lane
+// (the first version, 32/64 lanes per row) made the LN epilogue of the narrow E1 / D4 layers
+// (K = 64: two main-loop stages) dominate their kernels: 14% MFMA busy, 57% of wave cycles parked.
+__host__ __device__ constexpr int pow2_part(int v) { return v & -v; }
 template <int BN>
 struct RowGeo {
-  static constexpr int CPL = 4;                  // channels per lane
-  static constexpr int LPR = BN / CPL;           // lanes per row
-  static constexpr int RPW = 64 / LPR;           // rows per wave pass
-  static constexpr int PITCH = BN + 4;           // LDS row pitch (floats)
-  static_assert(LPR >= 1 && LPR <= 64 && BN % CPL == 0, "RowGeo: BN must be 4..256");
+  static constexpr int P2 = pow2_part(BN);
+  static constexpr int LPR = (BN == P2 ? (BN / 4 < 64 ? BN / 4 : 64) : (P2 < 64 ? P2 : 64));  // lanes per row
+  static constexpr int CPL = BN / LPR;                                                    // channels per lane
+  static constexpr int RPW = 64 / LPR;                                                    // rows per wave pass
+  static constexpr int PITCH = BN + 4;                                                    // LDS row pitch (floats)
+  static_assert(LPR >= 1 && LPR <= 64 && (LPR & (LPR - 1)) == 0 && CPL * LPR == BN && CPL <= 16, "RowGeo: BN");
 };
 
 template <int TM, int TN, int WN>
@@ -299,14 +332,21 @@ __device__ __forceinline__ float lseg_sum(float v) {
   return v;
 }
 
+// CPL contiguous floats at p (16-B aligned when CPL % 4 == 0, 8-B when CPL % 2 == 0)
 template <int CPL>
 __device__ __forceinline__ void ld_cpl(const float* p, float (&v)[CPL]) {
-  if constexpr (CPL == 4) {
-    const f4 t = *(const f4*)p;
-    v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
-  } else if constexpr (CPL == 2) {
-    const float2 t = *(const float2*)p;
-    v[0] = t.x; v[1] = t.y;
+  if constexpr (CPL % 4 == 0) {
+#pragma unroll
+    for (int e = 0; e < CPL; e += 4) {
+      const f4 t = *(const f4*)(p + e);
+      v[e] = t[0]; v[e + 1] = t[1]; v[e + 2] = t[2]; v[e + 3] = t[3];
+    }
+  } else if constexpr (CPL % 2 == 0) {
+#pragma unroll
+    for (int e = 0; e < CPL; e += 2) {
+      const float2 t = *(const float2*)(p + e);
+      v[e] = t.x; v[e + 1] = t.y;
+    }
   } else {
 #pragma unroll
     for (int e = 0; e < CPL; ++e) v[e] = p[e];
@@ -314,10 +354,12 @@ __device__ __forceinline__ void ld_cpl(const float* p, float (&v)[CPL]) {
 }
 template <int CPL>
 __device__ __forceinline__ void st_cpl(float* p, const float (&v)[CPL]) {
-  if constexpr (CPL == 4) {
-    *(f4*)p = f4{v[0], v[1], v[2], v[3]};
-  } else if constexpr (CPL == 2) {
-    *(float2*)p = make_float2(v[0], v[1]);
+  if constexpr (CPL % 4 == 0) {
+#pragma unroll
+    for (int e = 0; e < CPL; e += 4) *(f4*)(p + e) = f4{v[e], v[e + 1], v[e + 2], v[e + 3]};
+  } else if constexpr (CPL % 2 == 0) {
+#pragma unroll
+    for (int e = 0; e < CPL; e += 2) *(float2*)(p + e) = make_float2(v[e], v[e + 1]);
   } else {
 #pragma unroll
     for (int e = 0; e < CPL; ++e) p[e] = v[e];
@@ -325,11 +367,12 @@ __device__ __forceinline__ void st_cpl(float* p, const float (&v)[CPL]) {
 }
 
 // ------------------------------------------------------------------------------------ epilogues
+// NW = waves of the workgroup (WM x WN); the tile rows of one staged chunk are R = WM * 32.
 struct EpiLNAct : EpiLNActP {  // z = acc (NHWC), y = act(LN_c(z)) (NHWC or NCHW-flat), mean/rstd per pixel
-  template <int BM, int BN, int TM, int TN, int WN, class RM>
+  template <int BM, int BN, int TM, int TN, int WM, int WN, class RM>
   __device__ void run(f16v (&acc)[TM][TN], const Frag<TM, TN, WN>& f, int m0, float* lds, const RM& rm) {
     using G = RowGeo<BN>;
-    constexpr int WM = 4 / WN, R = WM * 32, CPL = G::CPL, LPR = G::LPR;
+    constexpr int NW = WM * WN, R = WM * 32, CPL = G::CPL, LPR = G::LPR;
     const int w = threadIdx.x >> 6, lr = f.lane / LPR, lc = f.lane % LPR, c0 = lc * CPL;
     float gam[CPL], bet[CPL];
 #pragma unroll
@@ -342,7 +385,7 @@ struct EpiLNAct : EpiLNActP {  // z = acc (NHWC), y = act(LN_c(z)) (NHWC or NCHW
       __syncthreads();
       stage_chunk<TM, TN, WN>(acc, i, f, lds, G::PITCH);
       __syncthreads();
-      for (int q0 = w * G::RPW; q0 < R; q0 += 4 * G::RPW) {
+      for (int q0 = w * G::RPW; q0 < R; q0 += NW * G::RPW) {
         const int q = q0 + lr;
         const int m = m0 + (q >> 5) * TM * 32 + i * 32 + (q & 31);
         float v[CPL];
@@ -379,10 +422,10 @@ struct EpiLNAct : EpiLNActP {  // z = acc (NHWC), y = act(LN_c(z)) (NHWC or NCHW
 };
 
 struct EpiLNBwd : EpiLNBwdP {  // acc = dy (grad of y = act(LN(z))); dz = d/dz; dgamma/dbeta += column sums
-  template <int BM, int BN, int TM, int TN, int WN, class RM>
+  template <int BM, int BN, int TM, int TN, int WM, int WN, class RM>
   __device__ void run(f16v (&acc)[TM][TN], const Frag<TM, TN, WN>& f, int m0, float* lds, const RM& rm) {
     using G = RowGeo<BN>;
-    constexpr int WM = 4 / WN, R = WM * 32, CPL = G::CPL, LPR = G::LPR;
+    constexpr int NW = WM * WN, NTH = 64 * NW, R = WM * 32, CPL = G::CPL, LPR = G::LPR;
     const int w = threadIdx.x >> 6, lr = f.lane / LPR, lc = f.lane % LPR, c0 = lc * CPL;
     float gam[CPL], bet[CPL], cg[CPL], cb[CPL];
 #pragma unroll
@@ -397,7 +440,7 @@ struct EpiLNBwd : EpiLNBwdP {  // acc = dy (grad of y = act(LN(z))); dz = d/dz; 
       __syncthreads();
       stage_chunk<TM, TN, WN>(acc, i, f, lds, G::PITCH);
       __syncthreads();
-      for (int q0 = w * G::RPW; q0 < R; q0 += 4 * G::RPW) {
+      for (int q0 = w * G::RPW; q0 < R; q0 += NW * G::RPW) {
         const int q = q0 + lr;
         const int m = m0 + (q >> 5) * TM * 32 + i * 32 + (q & 31);
         const bool ok = m < M;
@@ -433,7 +476,7 @@ struct EpiLNBwd : EpiLNBwdP {  // acc = dy (grad of y = act(LN(z))); dz = d/dz; 
       }
     }
     if (dgamma || dbeta) {
-      // rows of a wave pass share columns: fold the RPW row groups, then the 4 waves through LDS
+      // rows of a wave pass share columns: fold the RPW row groups, then the NW waves through LDS
 #pragma unroll
       for (int e = 0; e < CPL; ++e)
 #pragma unroll
@@ -446,13 +489,17 @@ struct EpiLNBwd : EpiLNBwdP {  // acc = dy (grad of y = act(LN(z))); dz = d/dz; 
 #pragma unroll
         for (int e = 0; e < CPL; ++e) {
           lds[w * BN + c0 + e] = cg[e];
-          lds[4 * BN + w * BN + c0 + e] = cb[e];
+          lds[NW * BN + w * BN + c0 + e] = cb[e];
         }
       }
       __syncthreads();
-      for (int c = threadIdx.x; c < BN; c += 256) {
-        const float sg = lds[c] + lds[BN + c] + lds[2 * BN + c] + lds[3 * BN + c];
-        const float sb = lds[4 * BN + c] + lds[5 * BN + c] + lds[6 * BN + c] + lds[7 * BN + c];
+      for (int c = threadIdx.x; c < BN; c += NTH) {
+        float sg = 0.f, sb = 0.f;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+          sg += lds[q * BN + c];
+          sb += lds[NW * BN + q * BN + c];
+        }
         if (dgamma) atomicAdd(dgamma + c, sg);
         if (dbeta) atomicAdd(dbeta + c, sb);
       }
@@ -461,7 +508,7 @@ struct EpiLNBwd : EpiLNBwdP {  // acc = dy (grad of y = act(LN(z))); dz = d/dz; 
 };
 
 struct EpiPlain : EpiPlainP {  // out = acc + bias[c] + c0 for c < Nreal; NHWC (ld = Nreal) or NCHW-flat
-  template <int BM, int BN, int TM, int TN, int WN, class RM>
+  template <int BM, int BN, int TM, int TN, int WM, int WN, class RM>
   __device__ void run(f16v (&acc)[TM][TN], const Frag<TM, TN, WN>& f, int m0, float*, const RM& rm) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -494,7 +541,7 @@ __global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep,
   constexpr int NTH = 64 * WM * WN, TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(TM >= 1 && TN >= 1 && TM * WM * 32 == BM && TN * WN * 32 == BN, "bad tile");
   constexpr int LDS_MAIN = (BM + BN) * LDK;
-  constexpr int LDS_EPI = (4 / WN) * 32 * (BN + 4) > 8 * BN ? (4 / WN) * 32 * (BN + 4) : 8 * BN;
+  constexpr int LDS_EPI = WM * 32 * (BN + 4) > 2 * WM * WN * BN ? WM * 32 * (BN + 4) : 2 * WM * WN * BN;
   __shared__ float lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
   float* As = lds;
   float* Bs = lds + BM * LDK;
@@ -554,7 +601,7 @@ __global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep,
     }
   }
   __syncthreads();
-  ep.template run<BM, BN, TM, TN, WN>(acc, f, m0, lds, rm);
+  ep.template run<BM, BN, TM, TN, WM, WN>(acc, f, m0, lds, rm);
 }
 
 // WGRAD: rows a (Ca), cols (tap,b) (16 Cb), K = pixel range of split blockIdx.z; writes the partial slab.
@@ -675,17 +722,17 @@ __global__ void to_nhwc4_kernel(const T* __restrict__ x, f4* __restrict__ out, i
 }
 
 // Row LayerNorm+act backward with dy in NCHW-flat order (the encoder's last stage feeds the flat
-// embedding); z NHWC [M][C]; one wave per pixel row, C/64 channels per lane; column partials per
-// block, one atomic per channel per block.
+// embedding); z NHWC [M][C]; one wave per pixel row, channel c = lane + 64 e (e < CPL, c < C); column
+// partials per block, one atomic per channel per block.
 template <int CPL>
 __global__ __launch_bounds__(256) void ln_bwd_flat_kernel(const float* __restrict__ dy, const float* __restrict__ z,
                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                          float* __restrict__ dz, float* dgamma, float* dbeta, int M,
+                                                          float* __restrict__ dz, float* dgamma, float* dbeta, int M, int C,
                                                           int lHW, int act, int rows_per_block) {
-  constexpr int C = 64 * CPL;
-  __shared__ float cr[2][4][C];
+  __shared__ float cr[2][4][64 * CPL];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float invC = 1.f / (float)C;
   float cg[CPL], cb[CPL];
 #pragma unroll
   for (int e = 0; e < CPL; ++e) cg[e] = cb[e] = 0.f;
@@ -697,20 +744,24 @@ __global__ __launch_bounds__(256) void ln_bwd_flat_kernel(const float* __restric
 #pragma unroll
     for (int e = 0; e < CPL; ++e) {
       const int c = lane + 64 * e;
-      const float g = gamma ? gamma[c] : 1.f;
-      xh[e] = (z[(size_t)m * C + c] - mu) * rs;
-      const float a = xh[e] * g + (beta ? beta[c] : 0.f);
-      const float da = dy[(((size_t)n * C + c) << lHW) + hw] * cact_grad(a, act);
-      cg[e] += da * xh[e];
-      cb[e] += da;
-      dxh[e] = da * g;
+      xh[e] = dxh[e] = 0.f;
+      if (c < C) {
+        const float g = gamma ? gamma[c] : 1.f;
+        xh[e] = (z[(size_t)m * C + c] - mu) * rs;
+        const float a = xh[e] * g + (beta ? beta[c] : 0.f);
+        const float da = dy[(((size_t)n * C + c) << lHW) + hw] * cact_grad(a, act);
+        cg[e] += da * xh[e];
+        cb[e] += da;
+        dxh[e] = da * g;
+      }
       s1 += dxh[e];
       s2 += dxh[e] * xh[e];
     }
-    s1 = wave_sum(s1) * (1.f / C);
-    s2 = wave_sum(s2) * (1.f / C);
+    s1 = wave_sum(s1) * invC;
+    s2 = wave_sum(s2) * invC;
 #pragma unroll
-    for (int e = 0; e < CPL; ++e) dz[(size_t)m * C + lane + 64 * e] = rs * (dxh[e] - s1 - xh[e] * s2);
+    for (int e = 0; e < CPL; ++e)
+      if (lane + 64 * e < C) dz[(size_t)m * C + lane + 64 * e] = rs * (dxh[e] - s1 - xh[e] * s2);
   }
 #pragma unroll
   for (int e = 0; e < CPL; ++e) {
@@ -726,69 +777,75 @@ __global__ __launch_bounds__(256) void ln_bwd_flat_kernel(const float* __restric
   }
 }
 
-// ConvT forward to a tiny channel count (the decoder's last layer, 3 image channels), on VALU:
+// ConvT forward to a tiny channel count (the decoder's last layer: 1 or 3 image channels), on VALU:
 // a workgroup owns a 16x16 tile of small-grid pixels of one image (+1 halo) staged in LDS (NHWC,
-// Ca channels); thread = one small-grid pixel (u, v), producing its 2x2 large-grid outputs (the 4
-// parity classes).  The class / tap loops are workgroup-uniform, so the weights are read as LDS
-// broadcasts ([tap][a][CO padded to 4]: one 16 B read per (tap, a)), one per-lane LDS read of the
-// input channel feeds CO FMAs, and each output row pair is written as float2 (x = 2v, 2v+1).
-// (First version: lanes of one wave mixed parity classes, so every FMA needed its own divergent
-// LDS weight read - LDS-bound at ~180 us for N=1024.)
+// 32 input channels per pass, CA / 32 passes); thread = one small-grid pixel (u, v), producing its 2x2
+// large-grid outputs (the 4 parity classes).  The class / tap loops are workgroup-uniform, so the
+// weights are read as LDS broadcasts ([tap][a][CO padded to 4]: one 16 B read per (tap, a)), one
+// per-lane LDS read of the input channel feeds CO FMAs, and each output row pair is written as float2
+// (x = 2v, 2v+1).  (First version: lanes of one wave mixed parity classes, so every FMA needed its own
+// divergent LDS weight read - LDS-bound at ~180 us for N=1024.)
 // out NCHW [n][co][y][x] = bias[co] + c0 + sum.
-template <int CO, int CA>
+template <int CO>
 __global__ __launch_bounds__(256) void up_small_kernel(const float* __restrict__ P, const float* __restrict__ W,
                                                        const float* __restrict__ bias, float c0, float* __restrict__ out,
-                                                       int lSH, int lSW) {
-  static_assert(CO <= 4, "up_small: CO <= 4");
-  constexpr int T = 16, TH = T + 2;
-  __shared__ float tile[TH * TH * (CA + 1)];
-  __shared__ f4 ws[16 * CA];  // [kh*4+kw][a] -> (co 0..3)
+                                                       int lSH, int lSW, int CA) {
+  static_assert(CO >= 1 && CO <= 4, "up_small: CO <= 4");
+  constexpr int T = 16, TH = T + 2, CC = 32;
+  __shared__ float tile[TH * TH * (CC + 1)];
+  __shared__ f4 ws[16 * CC];  // [kh*4+kw][a] -> (co 0..3)
   const int SH = 1 << lSH, SW = 1 << lSW;
   const int tx = SW / T;
   const int n = blockIdx.y, ty0 = (blockIdx.x / tx) * T, tx0 = (blockIdx.x % tx) * T;
-  for (int i = threadIdx.x; i < 16 * CA; i += 256) {
-    const int tap = i / CA, a = i % CA;
-    f4 w = zero4();
-#pragma unroll
-    for (int c = 0; c < CO; ++c) w[c] = W[(a * CO + c) * 16 + tap];
-    ws[i] = w;
-  }
-  for (int i = threadIdx.x; i < TH * TH * (CA / 4); i += 256) {
-    const int pixl = i / (CA / 4), aq = i % (CA / 4);
-    const int p = ty0 - 1 + pixl / TH, q = tx0 - 1 + pixl % TH;
-    f4 v = zero4();
-    if (p >= 0 && p < SH && q >= 0 && q < SW) v = *(const f4*)(P + ((((size_t)n * SH + p) * SW + q) * CA) + 4 * aq);
-    float* d = tile + pixl * (CA + 1) + 4 * aq;
-    d[0] = v[0];
-    d[1] = v[1];
-    d[2] = v[2];
-    d[3] = v[3];
-  }
-  __syncthreads();
-  const int LH = 2 * SH, LW = 2 * SW;
   const int u = threadIdx.x >> 4, v = threadIdx.x & 15;
   float s[2][2][CO];
 #pragma unroll
   for (int cy = 0; cy < 2; ++cy)
 #pragma unroll
-    for (int cx = 0; cx < 2; ++cx) {
+    for (int cx = 0; cx < 2; ++cx)
 #pragma unroll
       for (int c = 0; c < CO; ++c) s[cy][cx][c] = 0.f;
+  for (int a0 = 0; a0 < CA; a0 += CC) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 16 * CC; i += 256) {
+      const int tap = i / CC, a = i % CC;
+      f4 w = zero4();
 #pragma unroll
-      for (int th = 0; th < 2; ++th)
-#pragma unroll
-        for (int tw = 0; tw < 2; ++tw) {
-          const float* src = tile + ((u + cy - th + 1) * TH + (v + cx - tw + 1)) * (CA + 1);
-          const f4* wt = ws + ((1 - cy + 2 * th) * 4 + (1 - cx + 2 * tw)) * CA;
-#pragma unroll 8
-          for (int a = 0; a < CA; ++a) {
-            const float pv = src[a];
-            const f4 w = wt[a];
-#pragma unroll
-            for (int c = 0; c < CO; ++c) s[cy][cx][c] += pv * w[c];
-          }
-        }
+      for (int c = 0; c < CO; ++c) w[c] = W[((a0 + a) * CO + c) * 16 + tap];
+      ws[i] = w;
     }
+    for (int i = threadIdx.x; i < TH * TH * (CC / 4); i += 256) {
+      const int pixl = i / (CC / 4), aq = i % (CC / 4);
+      const int p = ty0 - 1 + pixl / TH, q = tx0 - 1 + pixl % TH;
+      f4 val = zero4();
+      if (p >= 0 && p < SH && q >= 0 && q < SW) val = *(const f4*)(P + ((((size_t)n * SH + p) * SW + q) * CA) + a0 + 4 * aq);
+      float* d = tile + pixl * (CC + 1) + 4 * aq;
+      d[0] = val[0];
+      d[1] = val[1];
+      d[2] = val[2];
+      d[3] = val[3];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int cy = 0; cy < 2; ++cy)
+#pragma unroll
+      for (int cx = 0; cx < 2; ++cx)
+#pragma unroll
+        for (int th = 0; th < 2; ++th)
+#pragma unroll
+          for (int tw = 0; tw < 2; ++tw) {
+            const float* src = tile + ((u + cy - th + 1) * TH + (v + cx - tw + 1)) * (CC + 1);
+            const f4* wt = ws + ((1 - cy + 2 * th) * 4 + (1 - cx + 2 * tw)) * CC;
+#pragma unroll 8
+            for (int a = 0; a < CC; ++a) {
+              const float pv = src[a];
+              const f4 w = wt[a];
+#pragma unroll
+              for (int c = 0; c < CO; ++c) s[cy][cx][c] += pv * w[c];
+            }
+          }
+  }
+  const int LH = 2 * SH, LW = 2 * SW;
   const int y0 = 2 * (ty0 + u), x0 = 2 * (tx0 + v);
 #pragma unroll
   for (int c = 0; c < CO; ++c) {
@@ -848,13 +905,52 @@ static int narrow_tiles() {
   return v;
 }
 
-// DOWN: out grid (N, SH, SW) with Nc output channels (32..256, pow2), input Q NHWC (N, 2SH, 2SW, Cb)
+// Output-channel tiles: the workgroup tile spans the whole channel row (the LayerNorm epilogues need
+// it), so the tile width is the layer's channel count:
+//   32 / 64     256 (or 128) x C, 4 x 1 (or 2 x 2) waves         (Atari-100k E1 / D3)
+//   96          128 x 96,   4 x 1 waves (TN 3)                     (XL E1)
+//   128 / 192   128 x C,    2 x 2 waves (TM 2, TN 2 / 3)
+//   256 / 384   64 x C,     1 x 4 waves (TM 2, TN 2 / 3)
+//   512 / 768   64 x C, 1 x 8 waves (TM 2, TN 2 / 3; 512 threads keep the B-tile prefetch at 8 / 12
+//               float4 per thread; LDS 83 / 120 KB)
+//   1024        32 x C, 1 x 8 waves (TM 1, TN 4: no register spill; LDS 152 KB)
+#define SRL_CONV_TILES(X, ...)                                                                     \
+  switch (Nc) {                                                                                     \
+    case 32:                                                                                        \
+      if (narrow_tiles() & 2) X<128, 32, 4, 1>(__VA_ARGS__);                                        \
+      else X<256, 32, 4, 1>(__VA_ARGS__);                                                           \
+      return true;                                                                                  \
+    case 64:                                                                                        \
+      if (narrow_tiles() & 1) X<128, 64, 2, 2>(__VA_ARGS__);                                        \
+      else X<256, 64, 4, 1>(__VA_ARGS__);                                                           \
+      return true;                                                                                  \
+    case 96: X<128, 96, 4, 1>(__VA_ARGS__); return true;                                            \
+    case 128: X<128, 128, 2, 2>(__VA_ARGS__); return true;                                          \
+    case 192: X<128, 192, 2, 2>(__VA_ARGS__); return true;                                          \
+    case 256: X<64, 256, 1, 4>(__VA_ARGS__); return true;                                           \
+    case 384: X<64, 384, 1, 4>(__VA_ARGS__); return true;                                           \
+    case 512: X<64, 512, 1, 8>(__VA_ARGS__); return true;                                           \
+    case 768: X<64, 768, 1, 8>(__VA_ARGS__); return true;                                           \
+    case 1024: X<32, 1024, 1, 8>(__VA_ARGS__); return true;                                         \
+    default: return false;                                                                          \
+  }
+
+bool conv_channels_supported(int Nc) {
+  switch (Nc) {
+    case 32: case 64: case 96: case 128: case 192: case 256: case 384: case 512: case 768: case 1024: return true;
+    default: return false;
+  }
+}
+
+// DOWN: out grid (N, SH, SW) with Nc output channels, input Q NHWC (N, 2SH, 2SW, Cb); Cb is a
+// multiple of 32 or a power of two below 32
 template <int BM, int BN, int WM, int WN>
 static void down_cfg(const float* Q, const float* Wp, int N, int SH, int SW, int Cb, const ConvEpi& e, hipStream_t st) {
   constexpr int NTH = 64 * WM * WN;
   const int M = N * SH * SW;
   DownGather<BM, NTH> la;
   la.Q = Q;
+  la.Cb = Cb;
   la.lCb = ilog2(Cb);
   la.lSH = ilog2(SH);
   la.lSW = ilog2(SW);
@@ -868,19 +964,8 @@ static void down_cfg(const float* Q, const float* Wp, int N, int SH, int SW, int
 
 bool launch_conv_down(const float* Q, const float* Wp, int N, int SH, int SW, int Cb, int Nc, const ConvEpi& e,
                       hipStream_t st) {
-  switch (Nc) {
-    case 256: down_cfg<64, 256, 1, 4>(Q, Wp, N, SH, SW, Cb, e, st); return true;
-    case 128: down_cfg<128, 128, 2, 2>(Q, Wp, N, SH, SW, Cb, e, st); return true;
-    case 64:
-      if (narrow_tiles() & 1) down_cfg<128, 64, 2, 2>(Q, Wp, N, SH, SW, Cb, e, st);
-      else down_cfg<256, 64, 4, 1>(Q, Wp, N, SH, SW, Cb, e, st);
-      return true;
-    case 32:
-      if (narrow_tiles() & 2) down_cfg<128, 32, 4, 1>(Q, Wp, N, SH, SW, Cb, e, st);
-      else down_cfg<256, 32, 4, 1>(Q, Wp, N, SH, SW, Cb, e, st);
-      return true;
-    default: return false;
-  }
+  if (!(Cb % 32 == 0 || (Cb >= 4 && Cb < 32 && (Cb & (Cb - 1)) == 0))) return false;
+  SRL_CONV_TILES(down_cfg, Q, Wp, N, SH, SW, Cb, e, st)
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -889,7 +974,7 @@ static void up_cfg(const float* P, const float* Wp, int N, int SH, int SW, int C
   const int M = N * SH * SW;
   UpGather<BM, NTH> la;
   la.P = P;
-  la.lCa = ilog2(Ca);
+  la.Ca = Ca;
   la.lSH = ilog2(SH);
   la.lSW = ilog2(SW);
   la.M = M;
@@ -904,19 +989,9 @@ static void up_cfg(const float* P, const float* Wp, int N, int SH, int SW, int C
 // UP: P NHWC (N, SH, SW, Ca) -> out grid (N, 2SH, 2SW) with Bp output channels (pack padding)
 bool launch_conv_up(const float* P, const float* Wp, int N, int SH, int SW, int Ca, int Bp, const ConvEpi& e,
                     hipStream_t st) {
-  switch (Bp) {
-    case 256: up_cfg<64, 256, 1, 4>(P, Wp, N, SH, SW, Ca, Bp, e, st); return true;
-    case 128: up_cfg<128, 128, 2, 2>(P, Wp, N, SH, SW, Ca, Bp, e, st); return true;
-    case 64:
-      if (narrow_tiles() & 1) up_cfg<128, 64, 2, 2>(P, Wp, N, SH, SW, Ca, Bp, e, st);
-      else up_cfg<256, 64, 4, 1>(P, Wp, N, SH, SW, Ca, Bp, e, st);
-      return true;
-    case 32:
-      if (narrow_tiles() & 2) up_cfg<128, 32, 4, 1>(P, Wp, N, SH, SW, Ca, Bp, e, st);
-      else up_cfg<256, 32, 4, 1>(P, Wp, N, SH, SW, Ca, Bp, e, st);
-      return true;
-    default: return false;
-  }
+  if (Ca % 32 != 0) return false;
+  const int Nc = Bp;
+  SRL_CONV_TILES(up_cfg, P, Wp, N, SH, SW, Ca, Bp, e, st)
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -926,11 +1001,11 @@ static void wgrad_cfg(const float* P, const float* Q, float* slab, int S, int kp
   const int M = N * SH * SW;
   WgP<BM, NTH> la;
   la.P = P;
-  la.lCa = ilog2(Ca);
+  la.Ca = Ca;
   la.M = M;
   WgQ<BN, NTH> lb;
   lb.Q = Q;
-  lb.lCb = ilog2(Cbp);
+  lb.Cb = Cbp;
   lb.lSH = ilog2(SH);
   lb.lSW = ilog2(SW);
   lb.M = M;
@@ -938,10 +1013,18 @@ static void wgrad_cfg(const float* P, const float* Q, float* slab, int S, int kp
   hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN>), grid, dim3(NTH), 0, st, la, lb, slab, 16 * Cbp, Ca, kper);
 }
 
+// WGRAD tile: rows = Ca (the largest of 128 / 64 / 32 dividing it), columns = 16 * Cbp (128, or 64 for
+// the 4-channel image side)
+static void wgrad_tile(int Ca, int Cbp, int* BM, int* BN) {
+  *BM = Ca % 128 == 0 ? 128 : (Ca % 64 == 0 ? 64 : 32);
+  *BN = (16 * Cbp) % 128 == 0 ? 128 : 64;
+}
+
 // number of K splits (and pixels per split) for a WGRAD problem; slab = S * Ca * 16 * Cbp floats
 void conv_wgrad_plan(int N, int SH, int SW, int Ca, int Cbp, int* S, int* kper) {
   const int M = N * SH * SW;
-  const int BM = Ca >= 128 ? 128 : Ca, BN = 128 < 16 * Cbp ? 128 : 16 * Cbp;
+  int BM, BN;
+  wgrad_tile(Ca, Cbp, &BM, &BN);
   const int tiles = (Ca / BM) * (16 * Cbp / BN);
   // ~512 workgroups (2 per CU); 1024 for a single-tile problem (E1 / D4: 2K outputs, 1M pixels)
   int want = tiles == 1 ? 1024 : (512 + tiles - 1) / tiles;
@@ -954,22 +1037,19 @@ void conv_wgrad_plan(int N, int SH, int SW, int Ca, int Cbp, int* S, int* kper) 
 
 bool launch_conv_wgrad(const float* P, const float* Q, float* slab, float* dw, int N, int SH, int SW, int Ca, int Cbp, int Cb,
                        hipStream_t st) {
-  int S, kper;
+  if (Ca % 32 != 0 || (16 * Cbp) % 64 != 0) return false;
+  int S, kper, BM, BN;
   conv_wgrad_plan(N, SH, SW, Ca, Cbp, &S, &kper);
-  if (Ca >= 128 && 16 * Cbp >= 128)
-    wgrad_cfg<128, 128, 2, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
-  else if (Ca == 64 && 16 * Cbp >= 128)
-    wgrad_cfg<64, 128, 1, 4>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
-  else if (Ca == 32 && 16 * Cbp >= 128)
-    wgrad_cfg<32, 128, 1, 4>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
-  else if (Ca == 32 && 16 * Cbp == 64)
-    wgrad_cfg<32, 64, 1, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
-  else if (Ca == 64 && 16 * Cbp == 64)
-    wgrad_cfg<64, 64, 1, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
-  else if (Ca >= 128 && 16 * Cbp == 64)
-    wgrad_cfg<128, 64, 2, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
-  else
-    return false;
+  wgrad_tile(Ca, Cbp, &BM, &BN);
+  if (BN == 128) {
+    if (BM == 128) wgrad_cfg<128, 128, 2, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+    else if (BM == 64) wgrad_cfg<64, 128, 1, 4>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+    else wgrad_cfg<32, 128, 1, 4>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+  } else {
+    if (BM == 128) wgrad_cfg<128, 64, 2, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+    else if (BM == 64) wgrad_cfg<64, 64, 1, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+    else wgrad_cfg<32, 64, 1, 2>(P, Q, slab, S, kper, N, SH, SW, Ca, Cbp, st);
+  }
   const int tot = Ca * 16 * Cbp;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((tot + 63) / 64), dim3(256), 0, st, slab, dw, S, Ca, Cbp, Cb);
   return true;
@@ -998,21 +1078,35 @@ void launch_to_nhwc4(const void* x, bool u8, float* out, int N, int C, int HW, f
 bool launch_ln_bwd_flat(const float* dy, const float* z, const float* mean, const float* rstd, const float* gamma,
                         const float* beta, float* dz, float* dgamma, float* dbeta, int M, int C, int HW, int act,
                         hipStream_t st) {
+  if (C % 32 != 0 || C > 1024) return false;
   const int rpb = 64;
   dim3 grid((M + rpb - 1) / rpb);
   const int lHW = ilog2(HW);
-  switch (C) {
-    case 64: hipLaunchKernelGGL(ln_bwd_flat_kernel<1>, grid, dim3(256), 0, st, dy, z, mean, rstd, gamma, beta, dz, dgamma, dbeta, M, lHW, act, rpb); return true;
-    case 128: hipLaunchKernelGGL(ln_bwd_flat_kernel<2>, grid, dim3(256), 0, st, dy, z, mean, rstd, gamma, beta, dz, dgamma, dbeta, M, lHW, act, rpb); return true;
-    case 256: hipLaunchKernelGGL(ln_bwd_flat_kernel<4>, grid, dim3(256), 0, st, dy, z, mean, rstd, gamma, beta, dz, dgamma, dbeta, M, lHW, act, rpb); return true;
-    default: return false;
+#define SRL_LNBF(K) hipLaunchKernelGGL(ln_bwd_flat_kernel<K>, grid, dim3(256), 0, st, dy, z, mean, rstd, gamma, beta, dz, \
+                                       dgamma, dbeta, M, C, lHW, act, rpb)
+  switch ((C + 63) / 64) {
+    case 1: SRL_LNBF(1); return true;
+    case 2: SRL_LNBF(2); return true;
+    case 3: SRL_LNBF(3); return true;
+    case 4: SRL_LNBF(4); return true;
+    case 5: case 6: SRL_LNBF(6); return true;
+    case 7: case 8: SRL_LNBF(8); return true;
+    case 9: case 10: case 11: case 12: SRL_LNBF(12); return true;
+    default: SRL_LNBF(16); return true;
   }
+#undef SRL_LNBF
 }
 
 bool launch_up_small(const float* P, const float* W, const float* bias, float c0, float* out, int N, int SH, int SW, int Ca,
                      int CO, hipStream_t st) {
-  if (SH % 16 || SW % 16 || CO != 3 || Ca != 32) return false;
+  if (SH % 16 || SW % 16 || CO < 1 || CO > 4 || Ca % 32 != 0) return false;
   dim3 grid((SH / 16) * (SW / 16), N);
-  hipLaunchKernelGGL((up_small_kernel<3, 32>), grid, dim3(256), 0, st, P, W, bias, c0, out, ilog2(SH), ilog2(SW));
+  const int lSH = ilog2(SH), lSW = ilog2(SW);
+  switch (CO) {
+    case 1: hipLaunchKernelGGL((up_small_kernel<1>), grid, dim3(256), 0, st, P, W, bias, c0, out, lSH, lSW, Ca); break;
+    case 2: hipLaunchKernelGGL((up_small_kernel<2>), grid, dim3(256), 0, st, P, W, bias, c0, out, lSH, lSW, Ca); break;
+    case 3: hipLaunchKernelGGL((up_small_kernel<3>), grid, dim3(256), 0, st, P, W, bias, c0, out, lSH, lSW, Ca); break;
+    default: hipLaunchKernelGGL((up_small_kernel<4>), grid, dim3(256), 0, st, P, W, bias, c0, out, lSH, lSW, Ca); break;
+  }
   return true;
 }

@@ -1,5 +1,6 @@
 // Torch bindings of the implicit-GEMM k4 s2 p1 convolutions (conv.hip).  Shapes are checked here,
-// before any launch: every kernel assumes power-of-two grids / channel counts and NHWC inputs.
+// before any launch: every kernel assumes power-of-two grids, NHWC inputs, channel counts that are
+// multiples of 32 (or a power of two below 32 on the image side) and 32-bit element offsets.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 
@@ -19,6 +20,7 @@ void launch_to_nhwc4(const void*, bool, float*, int, int, int, float, hipStream_
 bool launch_ln_bwd_flat(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
                         float*, int, int, int, int, hipStream_t);
 bool launch_up_small(const float*, const float*, const float*, float, float*, int, int, int, int, int, hipStream_t);
+bool conv_channels_supported(int);
 
 namespace {
 
@@ -41,8 +43,10 @@ float* optw(const c10::optional<torch::Tensor>& t) { return const_cast<float*>(o
 void chk_nhwc(const torch::Tensor& x, const char* name) {
   chk(x, name);
   TORCH_CHECK(x.dim() == 4, name, " must be NHWC [N,H,W,C]");
-  TORCH_CHECK(pow2(x.size(1)) && pow2(x.size(2)) && pow2(x.size(3)) && x.size(3) >= 4, name,
-              ": H, W and C must be powers of two (C >= 4)");
+  const int64_t C = x.size(3);
+  TORCH_CHECK(pow2(x.size(1)) && pow2(x.size(2)) && (C % 32 == 0 || (pow2(C) && C >= 4 && C < 32)), name,
+              ": H and W must be powers of two, C a multiple of 32 (or 4, 8, 16)");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 31), name, ": too large for 32-bit element offsets");
 }
 
 ConvEpi make_epi(int64_t mode, int64_t M, int64_t Nc, const torch::Tensor& out0, const c10::optional<torch::Tensor>& gamma,
@@ -104,7 +108,7 @@ std::vector<torch::Tensor> conv_gemm(int64_t kind, torch::Tensor src, torch::Ten
   chk(Wp, "packed weight");
   const bool down = kind == 0;
   const int64_t N = src.size(0), H = src.size(1), W = src.size(2), C = src.size(3);
-  TORCH_CHECK(Nc == 32 || Nc == 64 || Nc == 128 || Nc == 256, "conv: output channel tile must be 32..256");
+  TORCH_CHECK(conv_channels_supported((int)Nc), "conv: output channels must be 32, 64, 96, 128, 192, 256, 384, 512, 768 or 1024");
   int64_t OH, OW, M;
   if (down) {
     TORCH_CHECK(H >= 2 && W >= 2, "conv down: input too small");
@@ -113,7 +117,7 @@ std::vector<torch::Tensor> conv_gemm(int64_t kind, torch::Tensor src, torch::Ten
     M = N * OH * OW;
     TORCH_CHECK(Wp.numel() == Nc * 16 * C, "conv down: packed weight has the wrong size");
   } else {
-    TORCH_CHECK(C >= 32, "conv up: input channels must be >= 32");
+    TORCH_CHECK(C % 32 == 0, "conv up: input channels must be a multiple of 32");
     OH = 2 * H;
     OW = 2 * W;
     M = N * H * W;  // per parity class
@@ -170,7 +174,7 @@ torch::Tensor conv_wgrad(torch::Tensor P, torch::Tensor Q, int64_t Cb, c10::opti
   chk_nhwc(Q, "wgrad Q");
   const int64_t N = P.size(0), SH = P.size(1), SW = P.size(2), Ca = P.size(3), Cbp = Q.size(3);
   TORCH_CHECK(Q.size(0) == N && Q.size(1) == 2 * SH && Q.size(2) == 2 * SW, "wgrad: P/Q grids do not match");
-  TORCH_CHECK(Ca >= 32 && Ca <= 4096 && Cb <= Cbp, "wgrad: channel counts");
+  TORCH_CHECK(Ca % 32 == 0 && Ca <= 4096 && Cb <= Cbp && (16 * Cbp) % 64 == 0, "wgrad: channel counts");
   TORCH_CHECK(N * SH * SW < (int64_t(1) << 31), "wgrad: too many pixels");
   int S, kper;
   conv_wgrad_plan(N, SH, SW, Ca, Cbp, &S, &kper);
@@ -215,11 +219,11 @@ torch::Tensor conv_ln_bwd_flat(torch::Tensor dy, torch::Tensor z, torch::Tensor 
   bool ok = launch_ln_bwd_flat(dy.data_ptr<float>(), z.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                                optp(gamma), optp(beta), dz.data_ptr<float>(), optw(dgamma), optw(dbeta), N * HW, C, HW,
                                (int)act, stream());
-  TORCH_CHECK(ok, "ln_bwd_flat: channel count must be 64, 128 or 256");
+  TORCH_CHECK(ok, "ln_bwd_flat: channel count must be a multiple of 32 up to 1024");
   return dz;
 }
 
-// ConvT forward to 3 channels (VALU kernel): P NHWC [N,SH,SW,32], W [32,3,4,4] -> NCHW [N,3,2SH,2SW]
+// ConvT forward to CO <= 4 channels (VALU kernel): P NHWC [N,SH,SW,Ca], W [Ca,CO,4,4] -> NCHW [N,CO,2SH,2SW]
 torch::Tensor conv_up_small(torch::Tensor P, torch::Tensor W, c10::optional<torch::Tensor> bias, double c0) {
   chk_nhwc(P, "P");
   chk(W, "W");
@@ -229,7 +233,7 @@ torch::Tensor conv_up_small(torch::Tensor P, torch::Tensor W, c10::optional<torc
   auto out = torch::empty({N, CO, 2 * SH, 2 * SW}, P.options());
   bool ok = launch_up_small(P.data_ptr<float>(), W.data_ptr<float>(), optp(bias), (float)c0, out.data_ptr<float>(), N, SH,
                             SW, Ca, CO, stream());
-  TORCH_CHECK(ok, "up_small: needs Ca = 32, 3 outputs and a grid multiple of 16");
+  TORCH_CHECK(ok, "up_small: needs Ca % 32 == 0, 1..4 outputs and a grid multiple of 16");
   return out;
 }
 

@@ -1,6 +1,9 @@
 """Implicit-GEMM k4 s2 p1 convolutions (ops/csrc/conv.hip) against fp32 PyTorch references:
 each GEMM form on its own (DOWN = Conv2d fwd / ConvT data-grad, UP = ConvT fwd / Conv2d data-grad,
-WGRAD) and the whole DreamerV3 encoder / decoder stacks, forward and every parameter gradient."""
+WGRAD) and the whole DreamerV3 encoder / decoder stacks, forward and every parameter gradient, at the
+Atari-100k shapes (mult 32, 64 px RGB) and at the L / XL presets' (reference
+configs/exp/dreamer_v3_XL_crafter.yaml:40-46 mult 96, dreamer_v3_L_doapp_128px_gray_combo_discrete.yaml
+mult 64 at 128 px grayscale: 5 stages, 1024 channels)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -21,7 +24,9 @@ def _nhwc(x):
     return x.permute(0, 2, 3, 1).contiguous()
 
 
-@pytest.mark.parametrize("cin,cout,hw,n", [(4, 32, 64, 3), (32, 64, 32, 2), (64, 128, 16, 5), (128, 256, 8, 4)])
+@pytest.mark.parametrize("cin,cout,hw,n", [(4, 32, 64, 3), (32, 64, 32, 2), (64, 128, 16, 5), (128, 256, 8, 4),
+                                            (4, 96, 64, 2), (96, 192, 32, 2), (192, 384, 16, 2), (384, 768, 8, 3),
+                                            (256, 512, 8, 2), (512, 1024, 8, 3), (4, 64, 128, 1), (96, 96, 8, 2)])
 def test_down_plain_matches_conv2d(cin, cout, hw, n):
     C = ops._ext()
     torch.manual_seed(0)
@@ -33,7 +38,9 @@ def test_down_plain_matches_conv2d(cin, cout, hw, n):
     _close(out, ref)
 
 
-@pytest.mark.parametrize("cin,cout,hw,n", [(256, 128, 4, 3), (128, 64, 8, 2), (64, 32, 16, 5), (64, 256, 4, 2)])
+@pytest.mark.parametrize("cin,cout,hw,n", [(256, 128, 4, 3), (128, 64, 8, 2), (64, 32, 16, 5), (64, 256, 4, 2),
+                                            (768, 384, 4, 3), (384, 192, 8, 2), (192, 96, 16, 2), (1024, 512, 4, 2),
+                                            (512, 256, 8, 2), (96, 768, 4, 2), (32, 1024, 4, 2)])
 def test_up_plain_matches_conv_transpose(cin, cout, hw, n):
     C = ops._ext()
     torch.manual_seed(0)
@@ -46,7 +53,9 @@ def test_up_plain_matches_conv_transpose(cin, cout, hw, n):
     _close(out, ref)
 
 
-@pytest.mark.parametrize("cin,cout,hw,n", [(4, 32, 64, 3), (32, 64, 32, 2), (64, 128, 16, 3), (128, 256, 8, 4)])
+@pytest.mark.parametrize("cin,cout,hw,n", [(4, 32, 64, 3), (32, 64, 32, 2), (64, 128, 16, 3), (128, 256, 8, 4),
+                                            (4, 96, 64, 2), (96, 192, 32, 2), (192, 384, 16, 2), (384, 768, 8, 2),
+                                            (512, 1024, 8, 2), (4, 64, 128, 1), (768, 96, 8, 2), (1024, 64, 8, 2)])
 def test_wgrad_matches_autograd(cin, cout, hw, n):
     C = ops._ext()
     torch.manual_seed(0)
@@ -59,23 +68,25 @@ def test_wgrad_matches_autograd(cin, cout, hw, n):
     _close(dw, w.grad, rtol=5e-4, atol=5e-4)
 
 
-def test_up_small_matches_conv_transpose():
+@pytest.mark.parametrize("ca,co,hw", [(32, 3, 32), (96, 3, 32), (64, 1, 64), (128, 4, 16), (64, 2, 32)])
+def test_up_small_matches_conv_transpose(ca, co, hw):
     C = ops._ext()
     torch.manual_seed(0)
-    x = torch.randn(2, 32, 32, 32, device=DEV)
-    w = torch.randn(32, 3, 4, 4, device=DEV) * 0.1
-    b = torch.randn(3, device=DEV)
+    x = torch.randn(2, ca, hw, hw, device=DEV)
+    w = torch.randn(ca, co, 4, 4, device=DEV) * 0.1
+    b = torch.randn(co, device=DEV)
     ref = F.conv_transpose2d(x, w, b, stride=2, padding=1) + 0.5
     out = C.conv_up_small(_nhwc(x), w, b, 0.5)
     _close(out, ref)
 
 
-def _encoder_decoder(mult=32):
+def _encoder_decoder(mult=32, hw=64, ch=3):
     from sheeprl_prey_amd.algos.dreamer_v3.agent import CNNDecoder, CNNEncoder
 
     torch.manual_seed(0)
-    enc = CNNEncoder(["rgb"], [3], (64, 64), mult).to(DEV)
-    dec = CNNDecoder(["rgb"], [3], mult, 96, enc.output_dim, (64, 64)).to(DEV)
+    stages = hw.bit_length() - 3  # reference: log2(screen_size) - log2(4)
+    enc = CNNEncoder(["rgb"], [ch], (hw, hw), mult, stages=stages).to(DEV)
+    dec = CNNDecoder(["rgb"], [ch], mult, 96, enc.output_dim, (hw, hw), stages=stages).to(DEV)
     with torch.no_grad():  # non-trivial LN affine parameters
         for m in list(enc.modules()) + list(dec.modules()):
             if isinstance(m, torch.nn.LayerNorm):
@@ -99,16 +110,17 @@ def _run(enc, dec, x, lat, g_e, g_d, fused):
         ops.set_fused(True)
 
 
-@pytest.mark.parametrize("lead", [(6,), (3, 2), (66,)])
-def test_encoder_decoder_stacks_match_eager(lead, monkeypatch):
+@pytest.mark.parametrize("lead,mult,hw,ch", [((6,), 32, 64, 3), ((3, 2), 32, 64, 3), ((66,), 32, 64, 3),
+                                             ((5,), 96, 64, 3), ((3,), 64, 128, 1), ((4,), 64, 64, 3)])
+def test_encoder_decoder_stacks_match_eager(lead, mult, hw, ch, monkeypatch):
     monkeypatch.setattr(conv_ops, "MIN_FRAMES", 1)  # small batches normally go to MIOpen
-    enc, dec = _encoder_decoder()
-    assert conv_ops.encoder_spec(enc.model, (64, 64), 3) is not None
-    assert conv_ops.decoder_spec(dec.model, 3) is not None
-    x = torch.rand(*lead, 3, 64, 64, device=DEV)
+    enc, dec = _encoder_decoder(mult, hw, ch)
+    assert conv_ops.encoder_spec(enc.model, (hw, hw), ch) is not None
+    assert conv_ops.decoder_spec(dec.model, ch) is not None
+    x = torch.rand(*lead, ch, hw, hw, device=DEV)
     lat = torch.randn(*lead, 96, device=DEV)
     g_e = torch.randn(*lead, enc.output_dim, device=DEV)
-    g_d = torch.randn(*lead, 3, 64, 64, device=DEV)
+    g_d = torch.randn(*lead, ch, hw, hw, device=DEV)
     e1, r1, dl1, gr1 = _run(enc, dec, x, lat, g_e, g_d, True)
     e0, r0, dl0, gr0 = _run(enc, dec, x, lat, g_e, g_d, False)
     _close(e1, e0)
