@@ -446,51 +446,20 @@ def bench_ppo(args):
     player = PPOPlayer(agent, cfg, is_continuous, enabled=runner.cuda_graphs)
     T = cfg.algo.rollout_steps
     trainer = PPOTrainer(runner, agent, optimizer, cfg, T * ne, force_segmented=args.segmented)
-    # rollout staging: env-side arrays stay on the host (one H2D per rollout), policy outputs are
-    # copied into device rollout tensors; the obs for the next policy step goes H2D from pinned memory
+    # the CLI's host-env rollout engine (ppo.HostRollout: graphed policy step, pinned staging, device buffers;
+    # image frames stay uint8)
+    from sheeprl_prey_amd.algos.ppo.ppo import HostRollout
+
     cnn_keys = set(cfg.cnn_keys.encoder)
-
-    def prep(o):  # pixel frames: [envs, stack, C, H, W] -> [envs, stack*C, H, W] (as ppo.main does)
-        return {k: (np.asarray(o[k], dtype=np.float32).reshape(ne, -1, *np.asarray(o[k]).shape[-2:]) if k in cnn_keys
-                    else np.asarray(o[k], dtype=np.float32)) for k in obs_keys}
-
-    o = envs.reset(seed=cfg.seed + rank)[0]
-    cur = prep(o)
-    obs_host = {k: np.zeros((T, ne) + cur[k].shape[1:], np.float32) for k in obs_keys}
-    rew_host = np.zeros((T, ne, 1), np.float32)
-    done_host = np.zeros((T, ne, 1), np.float32)
-    pinned = {k: torch.empty(cur[k].shape, dtype=torch.float32).pin_memory() for k in obs_keys}
-    obs_dev = {k: torch.empty(cur[k].shape, dtype=torch.float32, device=device) for k in obs_keys}
-    buf = {n: torch.zeros(T, ne, d, device=device) for n, d in (("actions", sum(actions_dim) if not is_continuous
-                                                                    else actions_dim[0]), ("logprobs", 1), ("values", 1))}
     returns_seen = []
+    hroll = None if args.device_env else HostRollout(agent, envs, cfg, player, device, obs_keys,
+                                                     envs.reset(seed=cfg.seed + rank)[0])
 
     def update():
-        nonlocal cur
-        for t in range(T):
-            for k in obs_keys:
-                obs_host[k][t] = cur[k]
-                pinned[k].numpy()[...] = cur[k]
-                obs_dev[k].copy_(pinned[k], non_blocking=True)
-            pout = player(obs_dev)
-            for n in buf:
-                buf[n][t].copy_(pout[n])
-            real = pout["real"].cpu().numpy()
-            o, r, d, tr, info = envs.step(real.reshape(envs.action_space.shape))
-            rew_host[t, :, 0] = r
-            done_host[t, :, 0] = np.logical_or(d, tr)
-            cur = prep(o)
-            if "final_info" in info:
-                for ep in info["final_info"]:
-                    if ep is not None and "episode" in ep:
-                        returns_seen.append(float(np.asarray(ep["episode"]["r"]).reshape(-1)[0]))
-        data = {k: torch.from_numpy(obs_host[k]).to(device) for k in obs_keys}
-        data["rewards"] = torch.from_numpy(rew_host).to(device)
-        data["dones"] = torch.from_numpy(done_host).to(device)
-        data.update({n: v for n, v in buf.items()})
+        data = dict(hroll())
+        returns_seen.extend(r for r, _ in hroll.episodes)
         with torch.no_grad():
-            nv = agent.get_value({k: (torch.from_numpy(cur[k]).to(device) / 255 - 0.5 if k in cnn_keys
-                                      else torch.from_numpy(cur[k]).to(device)) for k in obs_keys})
+            nv = agent.get_value({k: (hroll.obs[k] / 255 - 0.5 if k in cnn_keys else hroll.obs[k]) for k in obs_keys})
             ret, adv = gae(data["rewards"], data["values"], data["dones"], nv, T, cfg.algo.gamma, cfg.algo.gae_lambda)
         data["returns"], data["advantages"] = ret.float(), adv.float()
         trainer(TensorDict({k: v.reshape(T * ne, *v.shape[2:]) for k, v in data.items()}, batch_size=[T * ne]), None)

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import copy
 import os
+import time
 from typing import Any, Dict, List, Tuple
 
 import numpy as np
@@ -37,7 +38,7 @@ from sheeprl_prey_amd.utils.timer import timer
 from sheeprl_prey_amd.utils.utils import gae, polynomial_decay
 
 LEARNER = 0
-N_STATS = 3  # per actor and update: sum of finished-episode returns, their count, sum of their lengths
+N_STATS = 6  # per actor and update: finished-episode return sum, count, length sum; rollout, gather-wait, broadcast-wait s
 
 
 class _LocalRunner:
@@ -132,71 +133,76 @@ def actor_fleet(runner, cfg: Dict[str, Any], log_dir: str) -> None:
         return
 
     # ------------------------------------------------------------------ actor
-    def to_obs(o):
-        out = {}
-        for k in obs_keys:
-            t = torch.as_tensor(np.asarray(o[k]), device=device)
-            out[k] = t.view(ne, -1, *t.shape[-2:]) if k in cfg.cnn_keys.encoder else t.float()
-        return out
+    # rollout engine: device-resident envs -> the whole rollout as one launch / one graph replay; host envs ->
+    # graphed policy step with pinned staging into device [T, ne] buffers (ppo.HostRollout)
+    from sheeprl_prey_amd.algos.ppo.ppo import DeviceRollout, FusedCartPoleRollout, HostRollout, PPOPlayer
 
-    next_obs = to_obs(envs.reset(seed=cfg.seed + rank)[0])
+    graphs = device.type == "cuda" and bool(getattr(runner, "cuda_graphs", False))
+    denv = None
+    if cfg.env.get("device", False):
+        from sheeprl_prey_amd.envs.device import make_device_env
+
+        if device.type != "cuda" or obs_keys != ["state"]:
+            raise ValueError("env.device=True needs a GPU run with mlp_keys.encoder=[state] and no cnn keys")
+        envs.close()
+        denv = make_device_env(cfg.env.id, ne, device, seed=cfg.seed + rank * ne, max_episode_steps=cfg.env.max_episode_steps)
+        denv.reset()
+        roll_fn = (FusedCartPoleRollout(agent, denv, cfg, seed=cfg.seed + rank) if FusedCartPoleRollout.supported(agent, denv)
+                   else DeviceRollout(agent, denv, cfg, enabled=graphs))
+    else:
+        player = PPOPlayer(agent, cfg, is_continuous, enabled=graphs)
+        roll_fn = HostRollout(agent, envs, cfg, player, device, obs_keys, envs.reset(seed=cfg.seed + rank)[0])
     u8 = torch.zeros(max(1, n_u8), dtype=torch.uint8, device=wire)
     f32 = torch.zeros(n_f32, dtype=torch.float32, device=wire)
+    # the slabs are packed on the compute device, then moved to the wire device in one copy each
+    u8_dev = u8 if wire == device else torch.zeros_like(u8, device=device)
+    f32_dev = f32 if wire == device else torch.zeros_like(f32, device=device)
+    t_gather = t_bcast = 0.0
     for update in range(1, num_updates + 1):
-        buf: Dict[str, List[Tensor]] = {k: [] for k in obs_keys + ["actions", "logprobs", "values", "rewards", "dones"]}
-        ep = [0.0, 0.0, 0.0]
-        with timer("Time/env_interaction_time"):
-            for _ in range(T):
-                with torch.no_grad():
-                    actions, logprobs, _, values = agent(_norm(next_obs, cfg.cnn_keys.encoder, obs_keys))
-                real = (torch.cat(actions, -1).cpu().numpy() if is_continuous
-                        else np.stack([a.argmax(-1).cpu().numpy() for a in actions], -1))
-                o, rewards, dones, truncated, info = envs.step(real.reshape(envs.action_space.shape))
-                trunc = np.nonzero(truncated)[0]
-                if len(trunc) > 0:  # truncation bootstrap r += gamma-free V(final obs), as the reference
-                    final = {k: torch.as_tensor(np.stack([np.asarray(info["final_observation"][e][k]) for e in trunc]),
-                                                dtype=torch.float32, device=device) for k in obs_keys}
-                    for k in cfg.cnn_keys.encoder:
-                        final[k] = final[k].view(len(trunc), -1, *final[k].shape[-2:]) / 255.0 - 0.5
-                    with torch.no_grad():
-                        v = agent.get_value(final).cpu().numpy()
-                    rewards[trunc] += v.reshape(rewards[trunc].shape)
-                for k in obs_keys:
-                    buf[k].append(next_obs[k])
-                buf["actions"].append(torch.cat(actions, -1))
-                buf["logprobs"].append(logprobs)
-                buf["values"].append(values)
-                buf["rewards"].append(torch.as_tensor(rewards, dtype=torch.float32, device=device).view(ne, 1))
-                buf["dones"].append(torch.as_tensor(np.logical_or(dones, truncated), dtype=torch.float32,
-                                                    device=device).view(ne, 1))
-                next_obs = to_obs(o)
-                for _, ep_rew, ep_len in episode_stats(info):
-                    ep[0] += float(np.sum(ep_rew))
-                    ep[1] += float(np.size(ep_rew))
-                    ep[2] += float(np.sum(ep_len))
-        roll = {k: torch.stack(v) for k, v in buf.items()}
+        t0 = time.perf_counter()
+        roll = dict(roll_fn())
+        if denv is not None:
+            next_obs = {"state": denv.obs}
+            rets, lens = roll_fn.finished_episodes()
+            ep = [float(sum(rets)), float(len(rets)), float(sum(lens))]
+        else:
+            next_obs = roll_fn.obs
+            ep = [float(sum(r for r, _ in roll_fn.episodes)), float(len(roll_fn.episodes)),
+                  float(sum(n_ for _, n_ in roll_fn.episodes))]
         with torch.no_grad():
             nv = agent.get_value(_norm(next_obs, cfg.cnn_keys.encoder, obs_keys))
             ret, adv = gae(roll["rewards"], roll["values"], roll["dones"], nv, T, cfg.algo.gamma, cfg.algo.gae_lambda)
         roll["returns"], roll["advantages"] = ret.float(), adv.float()
-        # pack the two fixed-shape slabs
+        # pack the two fixed-shape slabs (on the device: one copy per field, no host round trip)
         off = 0
-        for k, s in u8_fields:
-            m = n * int(np.prod(s))
-            u8[off:off + m].copy_(roll[k].reshape(-1).to(torch.uint8))
+        for k, sh in u8_fields:
+            m = n * int(np.prod(sh))
+            u8_dev[off:off + m].copy_(roll[k].reshape(-1))
             off += m
         off = 0
-        for k, s in f32_fields:
-            m = n * int(np.prod(s))
-            f32[off:off + m].copy_(roll[k].reshape(-1).float())
+        for k, sh in f32_fields:
+            m = n * int(np.prod(sh))
+            f32_dev[off:off + m].copy_(roll[k].reshape(-1))
             off += m
-        f32[off:off + N_STATS].copy_(torch.tensor(ep, dtype=torch.float32))
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        t_roll = time.perf_counter() - t0
+        # per-actor stats travel with the rollout: episode sums + this actor's rollout / wait seconds
+        f32_dev[off:off + N_STATS].copy_(torch.tensor(ep + [t_roll, t_gather, t_bcast], dtype=torch.float32))
+        if u8_dev is not u8:
+            u8.copy_(u8_dev)
+        if f32_dev is not f32:
+            f32.copy_(f32_dev)
+        t1 = time.perf_counter()
         if n_u8:
             dist.gather(u8, None, dst=LEARNER)
         dist.gather(f32, None, dst=LEARNER)
+        t2 = time.perf_counter()
         dist.broadcast(flat, src=LEARNER)
         vector_to_params(flat.to(device), params)
-    envs.close()
+        t_gather, t_bcast = t2 - t1, time.perf_counter() - t2
+    if denv is None:
+        envs.close()
 
 
 def _learner(runner, cfg, agent, flat, wire, u8_fields, f32_fields, n_u8, n_f32, num_updates, log_dir) -> None:
@@ -217,10 +223,17 @@ def _learner(runner, cfg, agent, flat, wire, u8_fields, f32_fields, n_u8, n_f32,
     f32_all = [torch.empty(n_f32, dtype=torch.float32, device=wire) for _ in range(world)]
     initial_ent, initial_clip = copy.deepcopy(cfg.algo.ent_coef), copy.deepcopy(cfg.algo.clip_coef)
     policy_step = last_log = last_checkpoint = train_step = last_train = 0
+    # per-update breakdown (seconds, summed between logs): learner gather wait / unpack / update / broadcast,
+    # and the actors' own rollout, gather-wait and broadcast-wait times (their means over actors)
+    brk = {k: 0.0 for k in ("gather", "unpack", "update", "broadcast", "actor_rollout", "actor_gather_wait",
+                            "actor_broadcast_wait")}
+    n_brk = 0
     for update in range(1, num_updates + 1):
+        t0 = time.perf_counter()
         if n_u8:
             dist.gather(u8_all[LEARNER], u8_all, dst=LEARNER)
         dist.gather(f32_all[LEARNER], f32_all, dst=LEARNER)
+        t1 = time.perf_counter()
         policy_step += n * n_actors
         parts: Dict[str, List[Tensor]] = {}
         for a in range(1, world):
@@ -232,13 +245,28 @@ def _learner(runner, cfg, agent, flat, wire, u8_fields, f32_fields, n_u8, n_f32,
             if st[1] > 0:
                 aggregator.update("Rewards/rew_avg", st[0] / st[1])
                 aggregator.update("Game/ep_len_avg", st[2] / st[1])
+            brk["actor_rollout"] += st[3] / n_actors
+            brk["actor_gather_wait"] += st[4] / n_actors
+            brk["actor_broadcast_wait"] += st[5] / n_actors
         data = TensorDict({k: (torch.cat(v).float() if k in cfg.cnn_keys.encoder else torch.cat(v))
                            for k, v in parts.items()}, batch_size=[n * n_actors])
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        t2 = time.perf_counter()
         with timer("Time/train_time"):
             trainer(data, aggregator)
         train_step += 1
         flat.copy_(params_to_vector(agent.parameters()).to(wire))
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        t3 = time.perf_counter()
         dist.broadcast(flat, src=LEARNER)
+        t4 = time.perf_counter()
+        brk["gather"] += t1 - t0
+        brk["unpack"] += t2 - t1
+        brk["update"] += t3 - t2
+        brk["broadcast"] += t4 - t3
+        n_brk += 1
         if scheduler is not None:
             scheduler.step()
         if cfg.algo.anneal_clip_coef:
@@ -254,6 +282,11 @@ def _learner(runner, cfg, agent, flat, wire, u8_fields, f32_fields, n_u8, n_f32,
             if tm.get("Time/train_time", 0) > 0:
                 metrics["Time/sps_train"] = (train_step - last_train) / tm["Time/train_time"]
             timer.reset()
+            if n_brk:
+                metrics.update({f"Time/fleet_{k}_ms": 1e3 * v / n_brk for k, v in brk.items()})
+                runner.print("actor fleet per update (ms): " + ", ".join(f"{k} {1e3 * v / n_brk:.2f}" for k, v in brk.items()))
+                brk = dict.fromkeys(brk, 0.0)
+                n_brk = 0
             runner.log_dict(metrics, policy_step)
             last_log, last_train = policy_step, train_step
         if (cfg.checkpoint.every > 0 and policy_step - last_checkpoint >= cfg.checkpoint.every) or cfg.dry_run \
