@@ -57,7 +57,11 @@ def main(H=512, D=512, hid=512, B=16, T=64, E=4096, A=9):
         v = [p[cons, t + shift, 1] - p[prod, t, 4] for t in range(T) if 0 <= t + shift < T and p[prod, t, 4] > 0 and p[cons, t + shift, 1] > 0]
         return sum(v) / max(len(v), 1)
     sub = {0: ("xr staged", [(0, 1, 5), (0, 5, 2)]), 1: ("GRU rows done", [(1, 1, 5), (1, 5, 2)]),
-           2: ("sampled / C->C in / gathered", [(2, 3, 5), (2, 5, 6), (2, 6, 7), (2, 7, 4)])}
+           2: ("sampled / C->C in / gathered", [(2, 3, 5), (2, 5, 6), (2, 6, 7), (2, 7, 4)]),
+           4: ("dv staged / LN2' regs / partials / finish+du", [(4, 1, 5), (4, 5, 6), (4, 6, 7), (4, 7, 2)]),
+           5: ("row stats / dgx / dgx stores", [(5, 1, 5), (5, 5, 6), (5, 6, 2)]),
+           6: ("dcat staged / LN1' regs / rest of prep / unimix' / arrive",
+               [(6, 1, 5), (6, 5, 6), (6, 6, 2), (6, 3, 7), (6, 7, 4)])}
     for r, (label, pairs) in sub.items():
         vals = []
         for role, k0, k1 in pairs:

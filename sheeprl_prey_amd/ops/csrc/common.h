@@ -77,6 +77,40 @@ __device__ __forceinline__ float act_grad(float z, int act) {
   }
 }
 
+// Activation with a compile-time code (ACTC >= 0) or the runtime code `act` (ACTC < 0).  Hot loops branch
+// ONCE on the (wave-uniform) runtime code and instantiate the SiLU body on its own (SRL_ACT_SPECIALIZE): a
+// runtime switch inside an unrolled per-element loop is if-converted into selects that evaluate every
+// activation's transcendentals for every element (5 v_exp/v_rcp per element where SiLU needs 2; measured in
+// the persistent scan's LayerNorm prologues: ~850 instructions for an 8-element row chunk).
+template <int ACTC>
+__device__ __forceinline__ float act_fwd_c(float z, int act) {
+  if constexpr (ACTC == ACT_SILU) return z * sigmoidf_(z);
+  else if constexpr (ACTC == ACT_NONE) return z;
+  else return act_fwd(z, act);
+}
+template <int ACTC>
+__device__ __forceinline__ float act_grad_c(float z, int act) {
+  if constexpr (ACTC == ACT_SILU) {
+    const float s = sigmoidf_(z);
+    return s * (1.f + z * (1.f - s));
+  } else if constexpr (ACTC == ACT_NONE) {
+    return 1.f;
+  } else {
+    return act_grad(z, act);
+  }
+}
+// Runs the statement(s) with `constexpr int ACTC` = ACT_SILU when act is SiLU, -1 (runtime switch) otherwise.
+#define SRL_ACT_SPECIALIZE(act, ...)      \
+  do {                                    \
+    if ((act) == ACT_SILU) {              \
+      constexpr int ACTC = ACT_SILU;      \
+      __VA_ARGS__;                        \
+    } else {                              \
+      constexpr int ACTC = -1;            \
+      __VA_ARGS__;                        \
+    }                                     \
+  } while (0)
+
 __host__ __device__ inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 }  // namespace srl

@@ -65,6 +65,21 @@ __device__ __forceinline__ float cact_grad(float z, int act) {
     default: return 1.f;
   }
 }
+// compile-time activation forms for the epilogue loops (common.h SRL_ACT_SPECIALIZE)
+template <int ACTC>
+__device__ __forceinline__ float cact_c(float z, int act) {
+  if constexpr (ACTC == ACT_SILU) return z * fsig(z);
+  else return cact(z, act);
+}
+template <int ACTC>
+__device__ __forceinline__ float cact_grad_c(float z, int act) {
+  if constexpr (ACTC == ACT_SILU) {
+    const float s = fsig(z);
+    return s * (1.f + z * (1.f - s));
+  } else {
+    return cact_grad(z, act);
+  }
+}
 
 // ------------------------------------------------------------------------------------- loaders
 // A loader fills a ROWS x BK tile (row-major, k contiguous, stride LDK) of LDS from one K stage.
@@ -371,6 +386,10 @@ __device__ __forceinline__ void st_cpl(float* p, const float (&v)[CPL]) {
 struct EpiLNAct : EpiLNActP {  // z = acc (NHWC), y = act(LN_c(z)) (NHWC or NCHW-flat), mean/rstd per pixel
   template <int BM, int BN, int TM, int TN, int WM, int WN, class RM>
   __device__ void run(f16v (&acc)[TM][TN], const Frag<TM, TN, WN>& f, int m0, float* lds, const RM& rm) {
+    SRL_ACT_SPECIALIZE(act, (run_t<BM, BN, TM, TN, WM, WN, RM, ACTC>(acc, f, m0, lds, rm)));
+  }
+  template <int BM, int BN, int TM, int TN, int WM, int WN, class RM, int ACTC>
+  __device__ void run_t(f16v (&acc)[TM][TN], const Frag<TM, TN, WN>& f, int m0, float* lds, const RM& rm) {
     using G = RowGeo<BN>;
     constexpr int NW = WM * WN, R = WM * 32, CPL = G::CPL, LPR = G::LPR;
     const int w = threadIdx.x >> 6, lr = f.lane / LPR, lc = f.lane % LPR, c0 = lc * CPL;
@@ -403,7 +422,7 @@ struct EpiLNAct : EpiLNActP {  // z = acc (NHWC), y = act(LN_c(z)) (NHWC or NCHW
           st_cpl<CPL>(z + (size_t)pix * BN + c0, v);
           float yv[CPL];
 #pragma unroll
-          for (int e = 0; e < CPL; ++e) yv[e] = cact((v[e] - mu) * rs * gam[e] + bet[e], act);
+          for (int e = 0; e < CPL; ++e) yv[e] = cact_c<ACTC>((v[e] - mu) * rs * gam[e] + bet[e], act);
           if (y_nchw) {
             const int n = pix >> lHW, hw = pix & ((1 << lHW) - 1);
 #pragma unroll
@@ -424,6 +443,10 @@ struct EpiLNAct : EpiLNActP {  // z = acc (NHWC), y = act(LN_c(z)) (NHWC or NCHW
 struct EpiLNBwd : EpiLNBwdP {  // acc = dy (grad of y = act(LN(z))); dz = d/dz; dgamma/dbeta += column sums
   template <int BM, int BN, int TM, int TN, int WM, int WN, class RM>
   __device__ void run(f16v (&acc)[TM][TN], const Frag<TM, TN, WN>& f, int m0, float* lds, const RM& rm) {
+    SRL_ACT_SPECIALIZE(act, (run_t<BM, BN, TM, TN, WM, WN, RM, ACTC>(acc, f, m0, lds, rm)));
+  }
+  template <int BM, int BN, int TM, int TN, int WM, int WN, class RM, int ACTC>
+  __device__ void run_t(f16v (&acc)[TM][TN], const Frag<TM, TN, WN>& f, int m0, float* lds, const RM& rm) {
     using G = RowGeo<BN>;
     constexpr int NW = WM * WN, NTH = 64 * NW, R = WM * 32, CPL = G::CPL, LPR = G::LPR;
     const int w = threadIdx.x >> 6, lr = f.lane / LPR, lc = f.lane % LPR, c0 = lc * CPL;
@@ -458,7 +481,7 @@ struct EpiLNBwd : EpiLNBwdP {  // acc = dy (grad of y = act(LN(z))); dz = d/dz; 
 #pragma unroll
         for (int e = 0; e < CPL; ++e) {
           x[e] = (zz[e] - mu) * rs;
-          const float da = ok ? dy[e] * cact_grad(x[e] * gam[e] + bet[e], act) : 0.f;
+          const float da = ok ? dy[e] * cact_grad_c<ACTC>(x[e] * gam[e] + bet[e], act) : 0.f;
           cg[e] += da * x[e];
           cb[e] += da;
           dx[e] = da * gam[e];
@@ -724,7 +747,7 @@ __global__ void to_nhwc4_kernel(const T* __restrict__ x, f4* __restrict__ out, i
 // Row LayerNorm+act backward with dy in NCHW-flat order (the encoder's last stage feeds the flat
 // embedding); z NHWC [M][C]; one wave per pixel row, channel c = lane + 64 e (e < CPL, c < C); column
 // partials per block, one atomic per channel per block.
-template <int CPL>
+template <int CPL, int ACTC>
 __global__ __launch_bounds__(256) void ln_bwd_flat_kernel(const float* __restrict__ dy, const float* __restrict__ z,
                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
                                                           const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -749,7 +772,7 @@ __global__ __launch_bounds__(256) void ln_bwd_flat_kernel(const float* __restric
         const float g = gamma ? gamma[c] : 1.f;
         xh[e] = (z[(size_t)m * C + c] - mu) * rs;
         const float a = xh[e] * g + (beta ? beta[c] : 0.f);
-        const float da = dy[(((size_t)n * C + c) << lHW) + hw] * cact_grad(a, act);
+        const float da = dy[(((size_t)n * C + c) << lHW) + hw] * cact_grad_c<ACTC>(a, act);
         cg[e] += da * xh[e];
         cb[e] += da;
         dxh[e] = da * g;
@@ -1082,8 +1105,15 @@ bool launch_ln_bwd_flat(const float* dy, const float* z, const float* mean, cons
   const int rpb = 64;
   dim3 grid((M + rpb - 1) / rpb);
   const int lHW = ilog2(HW);
-#define SRL_LNBF(K) hipLaunchKernelGGL(ln_bwd_flat_kernel<K>, grid, dim3(256), 0, st, dy, z, mean, rstd, gamma, beta, dz, \
-                                       dgamma, dbeta, M, C, lHW, act, rpb)
+#define SRL_LNBF(K)                                                                                                    \
+  do {                                                                                                                 \
+    if (act == srl::ACT_SILU)                                                                                          \
+      hipLaunchKernelGGL((ln_bwd_flat_kernel<K, srl::ACT_SILU>), grid, dim3(256), 0, st, dy, z, mean, rstd, gamma, beta, dz, \
+                         dgamma, dbeta, M, C, lHW, act, rpb);                                                          \
+    else                                                                                                               \
+      hipLaunchKernelGGL((ln_bwd_flat_kernel<K, -1>), grid, dim3(256), 0, st, dy, z, mean, rstd, gamma, beta, dz,       \
+                         dgamma, dbeta, M, C, lHW, act, rpb);                                                          \
+  } while (0)
   switch ((C + 63) / 64) {
     case 1: SRL_LNBF(1); return true;
     case 2: SRL_LNBF(2); return true;

@@ -15,7 +15,6 @@
 // sums the O/64 partials (fixed order, deterministic).
 #include "common.h"
 
-#include <cstdlib>
 
 namespace srl {
 namespace ens {
@@ -159,19 +158,8 @@ bool launch_ens_disagreement(const float* X, const float* W, const float* b, flo
   if (n < 1 || M < 1 || O < 1 || H < 4 || (H & 3)) return false;
   srl::ens::EP p{X, W, b, part, n, M, O, H};
   dim3 grid((M + srl::ens::BM - 1) / srl::ens::BM, (O + srl::ens::BN - 1) / srl::ens::BN);
-  // LDS row stride in floats (64-wide K chunk + padding); 72 measured fastest (1479 us vs 1518 at 68 and 1514 at
-  // 80 for the DV2-P2E shape); SRL_ENS_LDK=68/80 for A/B runs
-  static const int ldk = [] {
-    const char* e = std::getenv("SRL_ENS_LDK");
-    return e ? std::atoi(e) : 72;
-  }();
-  if (ldk == 72)
-    hipLaunchKernelGGL(srl::ens::disagreement_kernel<72>, grid, dim3(srl::ens::NTH), 0, st, p);
-  else if (ldk == 80)
-    hipLaunchKernelGGL(srl::ens::disagreement_kernel<80>, grid, dim3(srl::ens::NTH), 0, st, p);
-  else if (ldk == 68)
-    hipLaunchKernelGGL(srl::ens::disagreement_kernel<68>, grid, dim3(srl::ens::NTH), 0, st, p);
-  else
-    hipLaunchKernelGGL(srl::ens::disagreement_kernel<72>, grid, dim3(srl::ens::NTH), 0, st, p);
+  // LDS row stride 72 floats (64-wide K chunk + padding): measured fastest for the DV2-P2E shape (1479 us vs
+  // 1518 at 68 and 1514 at 80, profiles/r2_p2e_disagreement.md)
+  hipLaunchKernelGGL(srl::ens::disagreement_kernel<72>, grid, dim3(srl::ens::NTH), 0, st, p);
   return true;
 }

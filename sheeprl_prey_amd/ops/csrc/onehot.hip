@@ -40,34 +40,60 @@ __global__ void __launch_bounds__(256) onehot_index_kernel(const float* __restri
   idx[(int64_t)r * ldi + g] = off + g * C + best;
 }
 
-// One wave per row; lane l owns float4 columns l, l + 64, ... (NV4 of them: N <= 256 * NV4).
-template <int NV4>
+// y = act(LN(acc)) for one wave's float4 columns c4 + lane + 64 v (ACTC: common.h SRL_ACT_SPECIALIZE)
+template <int NV4, int ACTC>
+__device__ __forceinline__ void store_rows(const f4 (&acc)[NV4], int c4, int lane, int N4, int ln, float mu, float rs,
+                                           const float* gamma, const float* beta, int act, float* yrow) {
+#pragma unroll
+  for (int v = 0; v < NV4; ++v) {
+    const int i4 = c4 + lane + 64 * v;
+    if (i4 < N4) {
+      f4 o = acc[v];
+      if (ln) {
+        const f4 g = gamma ? reinterpret_cast<const f4*>(gamma)[i4] : f4{1.f, 1.f, 1.f, 1.f};
+        const f4 b = beta ? reinterpret_cast<const f4*>(beta)[i4] : zero4();
+        o = (o - mu) * rs * g + b;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = act_fwd_c<ACTC>(o[e], act);
+      reinterpret_cast<f4*>(yrow)[i4] = o;
+    }
+  }
+}
+
+// WPR waves per row (4 / WPR rows per 256-thread block); wave part p of a row owns float4 columns
+// p * 64 * NV4 + l + 64 v (v < NV4): N <= 256 * NV4 * WPR.  WPR = 2 at the 512-wide rollout layers (M = B*T =
+// 1024 rows): each lane keeps 16 table rows in flight instead of 8, so the 32 gathers of a row take two L2 round
+// trips instead of four (this kernel is latency-bound at that size: ~10 us per call with one wave per row).
+template <int NV4, int WPR>
 __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
     const float* __restrict__ Y, int ldy, const int* __restrict__ idx, int ldi, int G, int off,
     const float* __restrict__ T, int K, const float* __restrict__ bias, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, int act, int ln, float* __restrict__ z_out, int ldz,
     float* __restrict__ y_out, int ldo, float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, int N,
     int* __restrict__ err) {
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= M) return;
-  const int N4 = N >> 2;
+  static_assert(WPR == 1 || WPR == 2, "onehot_gather_ln: 1 or 2 waves per row");
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, part = wave % WPR;
+  const int r = blockIdx.x * (4 / WPR) + wave / WPR;
+  const bool live = r < M;  // (no early return: the WPR = 2 row reduction joins the block)
+  const int N4 = N >> 2, c4 = part * 64 * NV4;
   f4 acc[NV4];
 #pragma unroll
   for (int v = 0; v < NV4; ++v) {
-    const int i4 = lane + 64 * v;
-    acc[v] = (Y != nullptr && i4 < N4) ? reinterpret_cast<const f4*>(Y + (int64_t)r * ldy)[i4] : zero4();
-    if (bias != nullptr && i4 < N4) acc[v] += reinterpret_cast<const f4*>(bias)[i4];
+    const int i4 = c4 + lane + 64 * v;
+    acc[v] = (live && Y != nullptr && i4 < N4) ? reinterpret_cast<const f4*>(Y + (int64_t)r * ldy)[i4] : zero4();
+    if (live && bias != nullptr && i4 < N4) acc[v] += reinterpret_cast<const f4*>(bias)[i4];
   }
-  const int* ir = idx + (int64_t)r * ldi;
+  const int* ir = idx + (int64_t)(live ? r : 0) * ldi;
   // the row's hot indices: lanes < G load one each, then broadcast (wave-uniform loop below)
-  int my = lane < G ? ir[lane] - off : 0;
-  if (lane < G && (my < 0 || my >= K)) {  // a caller bug: skip the row read, report it
+  int my = (live && lane < G) ? ir[lane] - off : -1;
+  if (live && lane < G && (my < 0 || my >= K)) {  // a caller bug: skip the row read, report it
     if (err) atomicOr(err, 1);
     my = -1;
   }
   // QB table rows in flight per lane at a time (QB * NV4 = 16 float4 temporaries)
-  constexpr int QB = NV4 <= 2 ? 8 : 16 / NV4;
+  constexpr int QB = NV4 <= 1 ? 16 : (NV4 <= 2 ? 8 : 16 / NV4);
   for (int j = 0; j < G; j += QB) {
     f4 t[QB][NV4];
 #pragma unroll
@@ -77,7 +103,7 @@ __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
       const f4* src = reinterpret_cast<const f4*>(T + (int64_t)(ok ? row : 0) * N);
 #pragma unroll
       for (int v = 0; v < NV4; ++v) {
-        const int i4 = lane + 64 * v;
+        const int i4 = c4 + lane + 64 * v;
         t[q][v] = (ok && i4 < N4) ? src[i4] : zero4();
       }
     }
@@ -86,48 +112,47 @@ __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
 #pragma unroll
       for (int v = 0; v < NV4; ++v) acc[v] += t[q][v];
   }
-  if (z_out != nullptr) {
+  if (live && z_out != nullptr) {
 #pragma unroll
     for (int v = 0; v < NV4; ++v) {
-      const int i4 = lane + 64 * v;
+      const int i4 = c4 + lane + 64 * v;
       if (i4 < N4) reinterpret_cast<f4*>(z_out + (int64_t)r * ldz)[i4] = acc[v];
     }
   }
   float mu = 0.f, rs = 1.f;
-  if (ln) {
+  if (ln) {  // (ln is a kernel argument: uniform over the block)
     float s = 0.f;
 #pragma unroll
     for (int v = 0; v < NV4; ++v) s += (acc[v][0] + acc[v][1]) + (acc[v][2] + acc[v][3]);
-    mu = wave_sum(s) / N;
+    s = wave_sum(s);
+    if (WPR == 2) {
+      if (lane == 0) red[0][wave] = s;
+      __syncthreads();
+      s = red[0][wave & ~1] + red[0][wave | 1];
+    }
+    mu = s / N;
     float q = 0.f;
 #pragma unroll
     for (int v = 0; v < NV4; ++v) {
-      if (lane + 64 * v < N4) {
+      if (c4 + lane + 64 * v < N4) {
         const f4 d = acc[v] - mu;
         q += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
       }
     }
-    rs = rsqrtf(wave_sum(q) / N + eps);
-    if (lane == 0) {
+    q = wave_sum(q);
+    if (WPR == 2) {
+      if (lane == 0) red[1][wave] = q;
+      __syncthreads();
+      q = red[1][wave & ~1] + red[1][wave | 1];
+    }
+    rs = rsqrtf(q / N + eps);
+    if (live && lane == 0 && part == 0) {
       if (mean_out) mean_out[r] = mu;
       if (rstd_out) rstd_out[r] = rs;
     }
   }
-#pragma unroll
-  for (int v = 0; v < NV4; ++v) {
-    const int i4 = lane + 64 * v;
-    if (i4 < N4) {
-      f4 o = acc[v];
-      if (ln) {
-        const f4 g = gamma ? reinterpret_cast<const f4*>(gamma)[i4] : f4{1.f, 1.f, 1.f, 1.f};
-        const f4 b = beta ? reinterpret_cast<const f4*>(beta)[i4] : zero4();
-        o = (o - mu) * rs * g + b;
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = act_fwd(o[e], act);
-      reinterpret_cast<f4*>(y_out + (int64_t)r * ldo)[i4] = o;
-    }
-  }
+  if (!live) return;
+  SRL_ACT_SPECIALIZE(act, store_rows<NV4, ACTC>(acc, c4, lane, N4, ln, mu, rs, gamma, beta, act, y_out + (int64_t)r * ldo));
 }
 
 }  // namespace onehot
@@ -144,10 +169,16 @@ bool launch_onehot_gather_ln(const float* Y, int ldy, const int* idx, int ldi, i
                              hipStream_t st) {
   if (N % 4 != 0 || N > 4096 || G > 64 || M <= 0) return false;
   const int nv = (N + 255) / 256;
-  const dim3 grid((M + 3) / 4), block(256);
+  const dim3 block(256);
+  if (nv == 2 && M <= 4096) {  // latency-bound rollout sizes: two waves per 512-wide row
+    hipLaunchKernelGGL((srl::onehot::onehot_gather_ln_kernel<1, 2>), dim3((M + 1) / 2), block, 0, st, Y, ldy, idx, ldi, G, off,
+                       T, K, bias, gamma, beta, eps, act, ln, z_out, ldz, y_out, ldo, mean, rstd, M, N, err);
+    return true;
+  }
+  const dim3 grid((M + 3) / 4);
 #define OG(NV)                                                                                                          \
   if (nv <= NV) {                                                                                                       \
-    hipLaunchKernelGGL(srl::onehot::onehot_gather_ln_kernel<NV>, grid, block, 0, st, Y, ldy, idx, ldi, G, off, T, K,     \
+    hipLaunchKernelGGL((srl::onehot::onehot_gather_ln_kernel<NV, 1>), grid, block, 0, st, Y, ldy, idx, ldi, G, off, T, K, \
                        bias, gamma, beta, eps, act, ln, z_out, ldz, y_out, ldo, mean, rstd, M, N, err);                   \
     return true;                                                                                                        \
   }

@@ -234,9 +234,9 @@ __device__ __forceinline__ void gemm_reg(const WTile<NT, U>& wt, const float* As
 
 // ======================================================================= LDS layouts
 // One role per workgroup; each role carves the dynamic LDS its own way (floats).
-__host__ __device__ inline int lds_A(int D, int H) { return 16 * (H + D + 4) + 2 * D + 4096 + 256 + 16; }
-__host__ __device__ inline int lds_B(int H) { return 16 * (H + 4) + 6 * H + 4096 + 256 + 16; }
-__host__ __device__ inline int lds_C_base(int hid, int S, int C) { return 16 * (hid + 4) + 2 * hid + 8192 + 512 + 16 + 16 * (S / C); }
+__host__ __device__ inline int lds_A(int D, int H) { return 16 * (H + D + 4) + 2 * D + 4096 + 256 + 32 + 16; }
+__host__ __device__ inline int lds_B(int H) { return 16 * (H + 4) + 6 * H + 4096 + 256 + 32 + 16; }
+__host__ __device__ inline int lds_C_base(int hid, int S, int C) { return 16 * (hid + 4) + 2 * hid + 8192 + 512 + 16 + 16 * (S / C) + 32 + 1024 + 512; }
 // C also keeps its Wz^T column tiles (S rows x 16 columns each, ceil(D/16 / nC) of them) in LDS when they fit:
 // the per-step posterior gather then reads LDS instead of L2
 __host__ __device__ inline int wz_tiles(int D, int S) { return (D / 16 + S / 32 - 1) / (S / 32); }
@@ -247,9 +247,9 @@ __host__ __device__ inline int lds_C(int hid, int S, int C, int D) {
   return lds_C_base(hid, S, C) + (wz_in_lds(hid, S, C, D) ? wz_tiles(D, S) * S * 16 : 0);
 }
 __host__ __device__ inline int lds_G1(int S) { return 16 * (S + 4) + 4096 + 256 + 16; }
-__host__ __device__ inline int lds_G2(int hid) { return 32 * (hid + 4) + 2 * hid + 48 + 4096 + 256 + 1536 + 1792 + 16; }
+__host__ __device__ inline int lds_G2(int hid) { return 48 * (hid + 4) + 2 * hid + 48 + 4096 + 256 + 1536 + 1792 + 16; }
 __host__ __device__ inline int lds_G3(int H) { return 16 * (3 * H + 4) + 64 + 4096 + 256 + 16; }
-__host__ __device__ inline int lds_G4(int D) { return 32 * (D + 4) + 2 * D + 48 + 8192 + 512 + 16; }
+__host__ __device__ inline int lds_G4(int D) { return 48 * (D + 4) + 2 * D + 48 + 8192 + 512 + 16 + 7 * 512 + 32; }
 
 // ======================================================================= forward roles
 // Block ids: A = [0, nA), B = [nA, nA + nB), C = [nA + nB, nA + nB + nC).  Counters: 0 = A, 1 = B, 2 = C.
@@ -264,8 +264,8 @@ __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
   float* l1w = As + 16 * lda;
   float* l1b = l1w + D;
   float* red = l1b + D;
-  float* ct = red + 4096;
-  int* flag = (int*)(ct + 256);
+  float* ct = red + 4096;         // [256] GEMM tile + [32] this step's LN1 row statistics (workgroup 0)
+  int* flag = (int*)(ct + 256 + 32);
   WTile<1, UA> wt;
   wload<1, UA>(wt, p.Wg + (size_t)a * 16 * HD, HD, HD, w);
   stage_vec(l1w, p.ln1w, D);
@@ -288,9 +288,9 @@ __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
     if (w < B) {
       float mu, rs;
       wave_ln_act_row<LN_M>(As + w * lda + H, D, p.eps1, l1w, l1b, p.act1, mu, rs);
-      if (a == 0 && lane == 0) {
-        p.m1[(size_t)t * B + w] = mu;
-        p.r1[(size_t)t * B + w] = rs;
+      if (a == 0 && lane == 0) {  // stored after the hand-off: a global store before a barrier would be drained there
+        ct[256 + w] = mu;
+        ct[272 + w] = rs;
       }
     }
     __syncthreads();
@@ -309,6 +309,10 @@ __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
     }
     arrive(p.sync + 0 * NSH * SHW);
     PROF(0, 4);
+    if (a == 0 && threadIdx.x < B) {
+      p.m1[(size_t)t * B + threadIdx.x] = ct[256 + threadIdx.x];
+      p.r1[(size_t)t * B + threadIdx.x] = ct[272 + threadIdx.x];
+    }
     {  // the GRU input of step t, read only by the backward: behind the hand-off
       int lo, hi;
       part_range(B * HD, a, nA, lo, hi);
@@ -329,8 +333,8 @@ __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
   float* lgw = As + 16 * lda;
   float* lgb = lgw + N3;
   float* red = lgb + N3;
-  float* ct = red + 4096;
-  int* flag = (int*)(ct + 256);
+  float* ct = red + 4096;  // [256] GEMM tile + [32] LN-GRU row statistics (workgroup 0)
+  int* flag = (int*)(ct + 256 + 32);
   WTile<1, UB> wt;
   wload<1, UB>(wt, p.W1 + (size_t)bI * 16 * H, H, H, w);
   stage_vec(lgw, p.lngw, N3);
@@ -396,9 +400,9 @@ __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
           *(f4*)(hr + j) = hv;
         }
       }
-      if (bI == 0 && lane == 0) {
-        p.mg[(size_t)t * B + w] = mu;
-        p.rg[(size_t)t * B + w] = rs;
+      if (bI == 0 && lane == 0) {  // stored after the hand-off (see fwd_A)
+        ct[256 + w] = mu;
+        ct[272 + w] = rs;
       }
     }
     __syncthreads();
@@ -415,6 +419,10 @@ __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
     if (threadIdx.x < 256 && eb < B) st_wt(p.u + eo, ct[threadIdx.x] + pre);
     arrive(p.sync + 1 * NSH * SHW);
     PROF(1, 4);
+    if (bI == 0 && threadIdx.x < B) {
+      p.mg[(size_t)t * B + threadIdx.x] = ct[256 + threadIdx.x];
+      p.rg[(size_t)t * B + threadIdx.x] = ct[272 + threadIdx.x];
+    }
   }
 }
 
@@ -432,9 +440,12 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
   float* ct = red + 8192;
   int* flag = (int*)(ct + 512);
   int* selL = flag + 16;  // [B][S / C] sampled rows of the step
+  float* cst = (float*)(selL + 16 * nseg);  // [32]: this step's LN2 row statistics (workgroup 0), stored after the hand-off
+  float* xr0s = cst + 32;                    // [NTH]: prefetched xr_{t+1} base values (gather threads)
+  float* ef1s = xr0s + NTH;                  // [512]: prefetched first_{t+1} flags (epilogue threads)
   // this workgroup's Wz^T column tiles q = cI, cI + nC, ... ([S][16] each), resident for all T steps
   const bool wzl = wz_in_lds(hid, S, C, D);
-  float* wzt = (float*)(selL + 16 * nseg);
+  float* wzt = ef1s + 512;
   if (wzl) {
     int lt = 0;
     for (int q = cI; q < D / 16; q += nC, ++lt)
@@ -456,6 +467,14 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
     const bool evalid = threadIdx.x < 512 && eb < B;
     const float ebias = threadIdx.x < 512 ? p.b2[n0 + ec] : 0.f;
     const float euni = evalid ? p.uni[(size_t)t * B * nseg + eb * nseg + (n0 + ec) / C] : 0.f;
+    // first_{t+1} and this workgroup's xr_{t+1} columns before the posterior rows are added (a_proj + z0
+    // part, written by the host; only this workgroup adds into them): loaded here, off the critical path,
+    // parked in LDS (each thread reads back its own entries)
+    if (threadIdx.x < 512) ef1s[threadIdx.x] = (evalid && t + 1 < T) ? p.first[(size_t)(t + 1) * B + eb] : 0.f;
+    {
+      const int gb = threadIdx.x >> 6, gc = (threadIdx.x >> 2) & 15, gq = threadIdx.x & 3;
+      xr0s[threadIdx.x] = (t + 1 < T && gb < B && gq == 0 && cI < D / 16) ? p.xr[((size_t)(t + 1) * B + gb) * D + cI * 16 + gc] : 0.f;
+    }
     if (!wait_ctr(p, 1, eB, t + 1, 4, flag)) return;
     PROF(2, 1);
     stage_wt(As, lda, p.u + (size_t)t * B * hid, hid, B, hid);
@@ -464,8 +483,8 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
       float mu, rs;
       wave_ln_act_row<LN_M>(As + w * lda, hid, p.eps2, l2w, l2b, p.act2, mu, rs);
       if (cI == 0 && lane == 0) {
-        p.m2[(size_t)t * B + w] = mu;
-        p.r2[(size_t)t * B + w] = rs;
+        cst[w] = mu;
+        cst[16 + w] = rs;
       }
     }
     __syncthreads();
@@ -501,8 +520,7 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
       esamp = k == pick ? 1.f : 0.f;
       // sampled row of Wz^T per (row, categorical) of step t+1's input; -1: reset row (z0 Wz^T is in xr)
       if (t + 1 < T && k == 0 && evalid) {
-        const float f1 = p.first[(size_t)(t + 1) * B + eb];
-        __hip_atomic_store(p.sel + ((size_t)(t + 1) * B + eb) * nseg + (n0 + ec) / C, f1 == 0.f ? n0 + ec + pick : -1,
+        __hip_atomic_store(p.sel + ((size_t)(t + 1) * B + eb) * nseg + (n0 + ec) / C, ef1s[threadIdx.x] == 0.f ? n0 + ec + pick : -1,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -544,13 +562,17 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
         x += __shfl_xor(x, 2, 64);
         if (gb < B && gq == 0) {
           float* d = xr1 + (size_t)gb * D + col;
-          st_wt(d, *d + x);
+          st_wt(d, (lt == 0 ? xr0s[threadIdx.x] : *d) + x);
         }
       }
       PROF(2, 7);
     }
     arrive(p.sync + 2 * NSH * SHW);
     PROF(2, 4);
+    if (cI == 0 && threadIdx.x < B) {
+      p.m2[(size_t)t * B + threadIdx.x] = cst[threadIdx.x];
+      p.r2[(size_t)t * B + threadIdx.x] = cst[16 + threadIdx.x];
+    }
     // outputs read only after the launch: issued behind the hand-off
     if (evalid) {
       const size_t o = (size_t)t * B * S + (size_t)eb * S + n0 + ec;
@@ -558,7 +580,7 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
       p.mixed[o] = em;
       p.samples[o] = esamp;
       if (t + 1 < T) {
-        const float f1 = p.first[(size_t)(t + 1) * B + eb];
+        const float f1 = ef1s[threadIdx.x];
         p.zm[o + (size_t)B * S] = (1.f - f1) * esamp + f1 * p.z0[n0 + ec];
       }
     }
@@ -638,6 +660,7 @@ __device__ __forceinline__ void bwd_G2(const PP& p, int i, float* sm) {
   float* gsc = ct + 256;  // [16 rows][6][16 columns]: LN-GRU parameter partial terms
   float* pre = gsc + 1536;  // [7][256]: forward values of this thread's GRU adjoint element
   int* flag = (int*)(pre + 1792);
+  float* X2 = (float*)(flag + 16);  // [16][hid + 4]: du (As keeps xh for the LN2 parameter partials)
   WTile<1, U2> wt;
   wload<1, U2>(wt, p.W1T + (size_t)i * 16 * hid, hid, hid, w);
   stage_vec(l2w, p.ln2w, hid);
@@ -667,28 +690,29 @@ __device__ __forceinline__ void bwd_G2(const PP& p, int i, float* sm) {
       pre[1280 + threadIdx.x] = rv ? p.rg[(size_t)t * B + eb] : 0.f;
       pre[1536 + threadIdx.x] = (rv && t > 0) ? 1.f - p.first[(size_t)t * B + eb] : 0.f;
     }
+    if (threadIdx.x < B) {  // LN2 row statistics of the forward (read after the wait from LDS)
+      st[threadIdx.x] = p.m2[(size_t)t * B + threadIdx.x];
+      st[16 + threadIdx.x] = p.r2[(size_t)t * B + threadIdx.x];
+    }
     if (!wait_ctr(p, 0, e1, T - t, 12, flag)) return;
     PROF(4, 1);
     stage_wt(R, lda, p.dv + (size_t)t * B * hid, hid, B, hid);
     __syncthreads();
+    PROF(4, 5);
     float xh[LN_M], dzr[LN_M], s1 = 0.f, s2 = 0.f, rsw = 0.f;
     if (w < B) {
-      const float m2 = p.m2[(size_t)t * B + w];
-      rsw = p.r2[(size_t)t * B + w];
+      const float m2 = st[w];
+      rsw = st[16 + w];
       wave_ln_bwd_regs<LN_M>(As + w * lda, R + w * lda, l2w, l2b, hid, p.act2, m2, rsw, xh, dzr, s1, s2);
     }
+    PROF(4, 6);
+    // du into X2 (As keeps xh, R keeps dz): the LN2 parameter partials and the du stores (weight-gradient
+    // inputs only) run after this step's hand-off
+    if (w < B) wave_ln_bwd_finish<LN_M>(X2 + w * lda, l2w, hid, rsw, s1, s2, xh, dzr);
     __syncthreads();
-    int lo, hi;
-    part_range(hid, i, n2, lo, hi);
-    ln_param_partials(As, lda, R, lda, B, lo, hi, p.p2g + (size_t)t * hid, p.p2b + (size_t)t * hid);
-    __syncthreads();
-    if (w < B) wave_ln_bwd_finish<LN_M>(As + w * lda, l2w, hid, rsw, s1, s2, xh, dzr);
-    __syncthreads();
-    part_range(B * hid, i, n2, lo, hi);
-    float* du = p.du + (size_t)t * B * hid;
-    for (int e = lo + threadIdx.x; e < hi; e += NTH) du[e] = As[(e / hid) * lda + e % hid];
+    PROF(4, 7);
     PROF(4, 2);
-    gemm_reg<1, U2>(wt, As, lda, hid, red, ct);
+    gemm_reg<1, U2>(wt, X2, lda, hid, red, ct);
     PROF(4, 3);
     if (eok) {
       const float go = rv ? ld_wt(p.DH + ((size_t)t * B + eb) * H + j) + ct[threadIdx.x] : 0.f;
@@ -723,7 +747,8 @@ __device__ __forceinline__ void bwd_G2(const PP& p, int i, float* sm) {
         }
       }
     }
-    __syncthreads();
+    arrive(p.sync + 1 * NSH * SHW);  // (its barrier also orders the gsc writes before the reads below)
+    PROF(4, 4);
     if (threadIdx.x < 96) {  // LN-GRU parameter partials of this workgroup's 3 x 16 gate columns
       const int k = threadIdx.x >> 4, c = threadIdx.x & 15;
       float a = 0.f;
@@ -731,8 +756,15 @@ __device__ __forceinline__ void bwd_G2(const PP& p, int i, float* sm) {
       const int col = (k >> 1) * H + i * 16 + c;
       (k & 1 ? p.pgb : p.pgg)[(size_t)t * N3 + col] = a;
     }
-    arrive(p.sync + 1 * NSH * SHW);
-    PROF(4, 4);
+    {  // behind the hand-off: LN2 parameter partials and du (weight-gradient inputs)
+      int lo, hi;
+      part_range(hid, i, n2, lo, hi);
+      ln_param_partials(As, lda, R, lda, B, lo, hi, p.p2g + (size_t)t * hid, p.p2b + (size_t)t * hid);
+      part_range(B * hid, i, n2, lo, hi);
+      float* du = p.du + (size_t)t * B * hid;
+      for (int e = lo + threadIdx.x; e < hi; e += NTH) du[e] = X2[(e / hid) * lda + e % hid];
+      __syncthreads();  // As / R / X2 are rewritten by the next step
+    }
   }
 }
 
@@ -770,6 +802,7 @@ __device__ __forceinline__ void bwd_G3(const PP& p, int i3, float* sm) {
       }
     }
     __syncthreads();
+    PROF(5, 5);
     {
       const int c4 = N3 >> 2, n = B * c4;
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.dZ + (size_t)t * B * N3, (short)0, B * N3 * 4, 0x00020000);
@@ -782,12 +815,7 @@ __device__ __forceinline__ void bwd_G3(const PP& p, int i3, float* sm) {
       }
     }
     __syncthreads();
-    {
-      int lo, hi;
-      part_range(B * N3, i3, n3, lo, hi);
-      float* dgx = p.dgx + (size_t)t * B * N3;
-      for (int e = lo + threadIdx.x; e < hi; e += NTH) dgx[e] = As[(e / N3) * lda + e % N3];
-    }
+    PROF(5, 6);
     PROF(5, 2);
     gemm_reg<1, U3>(wt, As, lda, N3, red, ct);
     PROF(5, 3);
@@ -805,6 +833,13 @@ __device__ __forceinline__ void bwd_G3(const PP& p, int i3, float* sm) {
     }
     arrive(p.sync + 2 * NSH * SHW);
     PROF(5, 4);
+    {  // behind the hand-off: dgx (weight-gradient input)
+      int lo, hi;
+      part_range(B * N3, i3, n3, lo, hi);
+      float* dgx = p.dgx + (size_t)t * B * N3;
+      for (int e = lo + threadIdx.x; e < hi; e += NTH) dgx[e] = As[(e / N3) * lda + e % N3];
+      __syncthreads();  // As is restaged by the next step
+    }
   }
 }
 
@@ -823,11 +858,20 @@ __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
   float* red = st + 48;
   float* ct = red + 8192;
   int* flag = (int*)(ct + 512);
+  // [7][512]: the unimix adjoint's forward-only terms q, pm, pr, clamped and its epilogue inputs dmixed,
+  // d_post, keep (parked in LDS: the kernel is at the 128-VGPR cap); [32]: LN1 row statistics
+  float* fpre = (float*)(flag + 16);
+  float* X2 = fpre + 7 * 512 + 32;     // [16][D + 4]: dx (As keeps xh for the LN1 parameter partials)
   WTile<2, U4> wt;
   wload<2, U4>(wt, p.WzT + (size_t)n0 * D, D, D, w);
   stage_vec(l1w, p.ln1w, D);
   stage_vec(l1b, p.ln1b, D);
   const u32 e3 = shard_count(p.hid / 16 + H / 16, n3);
+  // LN1 row statistics of the forward, one step ahead (loaded at the end of the previous step, into LDS)
+  if (threadIdx.x < B) {
+    fpre[3584 + threadIdx.x] = p.m1[(size_t)(T - 1) * B + threadIdx.x];
+    fpre[3600 + threadIdx.x] = p.r1[(size_t)(T - 1) * B + threadIdx.x];
+  }
   __syncthreads();
   for (int t = T - 1; t >= 0; --t) {
     PROF(6, 0);
@@ -836,49 +880,68 @@ __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
     const int eb = threadIdx.x >> 5, ec = threadIdx.x & 31, ebb = eb < B ? eb : 0;
     const size_t eo = (size_t)(t > 0 ? t - 1 : 0) * B * S + (size_t)ebb * S + n0 + ec;
     const bool eok = threadIdx.x < 512 && t > 0;
-    const float el = eok ? p.logits[eo] : 0.f, egm = eok ? p.dmixed[eo] : 0.f;
-    const float edp = (eok && p.dpost) ? p.dpost[eo] : 0.f, ekeep = eok ? 1.f - p.first[(size_t)t * B + ebb] : 0.f;
+    const float el = eok ? p.logits[eo] : 0.f;
+    if (threadIdx.x < 512) {
+      fpre[2048 + threadIdx.x] = eok ? p.dmixed[eo] : 0.f;
+      fpre[2560 + threadIdx.x] = (eok && p.dpost) ? p.dpost[eo] : 0.f;
+      fpre[3072 + threadIdx.x] = eok ? 1.f - p.first[(size_t)t * B + ebb] : 0.f;
+    }
+    if (threadIdx.x < 512 && t > 0) {
+      // the unimix / straight-through adjoint's terms that depend on the forward logits only, computed
+      // before the wait (off the G3 -> G4 -> G1 critical path) and parked in LDS
+      float q = 0.f, pm = 0.f, m = el, cl = 0.f;
+      if (p.alpha > 0.f) {
+        const float mx = seg_max(el, C);
+        const float e = __expf(el - mx);
+        q = e / seg_sum(e, C);
+        pm = (1.f - p.alpha) * q + p.alpha / C;
+        cl = (pm <= FEPS || pm >= 1.f - FEPS) ? 1.f : 0.f;
+        m = logf(fminf(fmaxf(pm, FEPS), 1.f - FEPS));
+      }
+      const float mx2 = seg_max(m, C);
+      const float e2 = __expf(m - mx2);
+      fpre[threadIdx.x] = q;
+      fpre[512 + threadIdx.x] = pm;
+      fpre[1024 + threadIdx.x] = e2 / seg_sum(e2, C);
+      fpre[1536 + threadIdx.x] = cl;
+    }
     if (!wait_ctr(p, 2, e3, T - t, 14, flag)) return;
     PROF(6, 1);
     stage_wt(R, lda, p.dcat + (size_t)t * B * HD + H, HD, B, D);
     __syncthreads();
+    PROF(6, 5);
     float xh[LN_M], dzr[LN_M], s1 = 0.f, s2 = 0.f, rsw = 0.f;
     if (w < B) {
-      const float mu = p.m1[(size_t)t * B + w];
-      rsw = p.r1[(size_t)t * B + w];
+      const float mu = fpre[3584 + w];
+      rsw = fpre[3600 + w];
       wave_ln_bwd_regs<LN_M>(As + w * lda, R + w * lda, l1w, l1b, D, p.act1, mu, rsw, xh, dzr, s1, s2);
     }
+    PROF(6, 6);
+    // dx into X2 (As keeps xh, R keeps dz): the LN1 parameter partials and the dx stores (weight-gradient
+    // inputs only) run after this step's hand-off
+    if (w < B) wave_ln_bwd_finish<LN_M>(X2 + w * lda, l1w, D, rsw, s1, s2, xh, dzr);
     __syncthreads();
-    int lo, hi;
-    part_range(D, i4, n4, lo, hi);
-    ln_param_partials(As, lda, R, lda, B, lo, hi, p.p1g + (size_t)t * D, p.p1b + (size_t)t * D);
-    __syncthreads();
-    if (w < B) wave_ln_bwd_finish<LN_M>(As + w * lda, l1w, D, rsw, s1, s2, xh, dzr);
-    __syncthreads();
-    part_range(B * D, i4, n4, lo, hi);
-    float* dx = p.dx + (size_t)t * B * D;
-    for (int e = lo + threadIdx.x; e < hi; e += NTH) dx[e] = As[(e / D) * lda + e % D];
-    if (t == 0) break;  // no z_{-1} to propagate into
+    auto tail = [&]() {
+      int lo, hi;
+      part_range(D, i4, n4, lo, hi);
+      ln_param_partials(As, lda, R, lda, B, lo, hi, p.p1g + (size_t)t * D, p.p1b + (size_t)t * D);
+      part_range(B * D, i4, n4, lo, hi);
+      float* dx = p.dx + (size_t)t * B * D;
+      for (int e = lo + threadIdx.x; e < hi; e += NTH) dx[e] = X2[(e / D) * lda + e % D];
+      __syncthreads();  // As / R / X2 are rewritten by the next step
+    };
+    if (t == 0) {  // no z_{-1} to propagate into
+      tail();
+      break;
+    }
     PROF(6, 2);
-    gemm_reg<2, U4>(wt, As, lda, D, red, ct);
+    gemm_reg<2, U4>(wt, X2, lda, D, red, ct);
     PROF(6, 3);
     if (threadIdx.x < 512) {
-      const float ds = edp + ekeep * ct[threadIdx.x];
-      const float l = el;
-      float q = 0.f, pm = 0.f, m = l;
-      bool clamped = false;
-      if (p.alpha > 0.f) {
-        const float mx = seg_max(l, C);
-        const float e = __expf(l - mx);
-        q = e / seg_sum(e, C);
-        pm = (1.f - p.alpha) * q + p.alpha / C;
-        clamped = pm <= FEPS || pm >= 1.f - FEPS;
-        m = logf(fminf(fmaxf(pm, FEPS), 1.f - FEPS));
-      }
-      float gm = egm;
-      const float mx2 = seg_max(m, C);
-      const float e2 = __expf(m - mx2);
-      const float pr = e2 / seg_sum(e2, C);
+      const float ds = fpre[2560 + threadIdx.x] + fpre[3072 + threadIdx.x] * ct[threadIdx.x];
+      const float q = fpre[threadIdx.x], pm = fpre[512 + threadIdx.x], pr = fpre[1024 + threadIdx.x];
+      const bool clamped = fpre[1536 + threadIdx.x] != 0.f;
+      float gm = fpre[2048 + threadIdx.x];
       const float dot = seg_sum(pr * ds, C);
       gm += pr * (ds - dot);
       float dl;
@@ -890,8 +953,14 @@ __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
       }
       if (eb < B) st_wt(p.dlog + eo, dl);
     }
+    PROF(6, 7);
     arrive(p.sync + 3 * NSH * SHW);
     PROF(6, 4);
+    tail();
+    if (threadIdx.x < B) {  // the next (earlier) step's LN1 row statistics
+      fpre[3584 + threadIdx.x] = p.m1[(size_t)(t - 1) * B + threadIdx.x];
+      fpre[3600 + threadIdx.x] = p.r1[(size_t)(t - 1) * B + threadIdx.x];
+    }
   }
 }
 

@@ -49,17 +49,32 @@ struct FP {
 
 __device__ __forceinline__ float comp(const float4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
 
+// The weight operands stream from L2: each helper issues a chunk of KC K-steps of loads before the
+// MFMAs that consume them (one load latency per chunk, not per K-step: the first version waited on
+// every 16-wide K step and spent ~30 us in the forward at M = 256, H = 256).
+constexpr int KC = 8;
+
 // acc (16 rows x 16 cols from weight row n0) += act[16][K] . W[n0.., K]^T ; act in LDS (stride lda), W row-major.
 __device__ __forceinline__ floatx4 tile_gemm_nt(const float* act, int lda, const float* W, int ldw, int n0, int K, int lane) {
   const int j = lane & 15, q = lane >> 4;
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   const float* wr = W + (long)(n0 + j) * ldw + 4 * q;
   const float* ar = act + j * lda + 4 * q;
-  for (int k0 = 0; k0 < K; k0 += 16) {
-    const float4 w = *reinterpret_cast<const float4*>(wr + k0);
-    const float4 a = *reinterpret_cast<const float4*>(ar + k0);
+  for (int kb = 0; kb < K; kb += 16 * KC) {
+    float4 w[KC], a[KC];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a, e), comp(w, e), acc, 0, 0, 0);
+    for (int u = 0; u < KC; ++u)
+      if (kb + 16 * u < K) w[u] = *reinterpret_cast<const float4*>(wr + kb + 16 * u);
+#pragma unroll
+    for (int u = 0; u < KC; ++u)
+      if (kb + 16 * u < K) a[u] = *reinterpret_cast<const float4*>(ar + kb + 16 * u);
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+      if (kb + 16 * u < K) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a[u], e), comp(w[u], e), acc, 0, 0, 0);
+      }
+    }
   }
   return acc;
 }
@@ -70,13 +85,20 @@ __device__ __forceinline__ floatx4 tile_gemm_nn(const float* act, int lda, const
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   const float* wc = W + n0 + j;
   const float* ar = act + j * lda + 4 * q;
-  for (int k0 = 0; k0 < K; k0 += 16) {
-    const float4 a = *reinterpret_cast<const float4*>(ar + k0);
-    float w[4];
+  for (int kb = 0; kb < K; kb += 16 * KC) {
+    float w[KC][4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) w[e] = wc[(long)(k0 + 4 * q + e) * ldw];
+    for (int u = 0; u < KC; ++u)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a, e), w[e], acc, 0, 0, 0);
+      for (int e = 0; e < 4; ++e) w[u][e] = kb + 16 * u < K ? wc[(long)(kb + 16 * u + 4 * q + e) * ldw] : 0.f;
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+      if (kb + 16 * u < K) {
+        const float4 a = *reinterpret_cast<const float4*>(ar + kb + 16 * u);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a, e), w[u][e], acc, 0, 0, 0);
+      }
+    }
   }
   return acc;
 }
@@ -209,23 +231,29 @@ struct GP {
   int nb2, nb1;    // workgroups of the dW2 / dW1 roles
 };
 
-// out tile (16 x 16) = sum_r G[r][i0 + i] * A[r][j0 + jj]  (both row-major, row strides ldg / lda)
+// out tile (16 x 16) = sum_r G[r][i0 + i] * A[r][j0 + jj]  (both row-major, row strides ldg / lda); KC/2
+// row steps of loads in flight per chunk
 __device__ __forceinline__ floatx4 tile_wgrad(const float* G, int ldg, const float* A, int lda, int i0, int j0, int M,
                                               int lane) {
   const int j = lane & 15, q = lane >> 4;
+  constexpr int RC = KC / 2;
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   const float* gc = G + i0 + j;
   const float* ac = A + j0 + j;
-  for (int k0 = 0; k0 < M; k0 += 16) {
-    float a[4], b[4];
+  for (int kb = 0; kb < M; kb += 16 * RC) {
+    float a[RC][4], b[RC][4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int r = k0 + 4 * q + e;
-      a[e] = r < M ? gc[(long)r * ldg] : 0.f;
-      b[e] = r < M ? ac[(long)r * lda] : 0.f;
-    }
+    for (int u = 0; u < RC; ++u)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], b[e], acc, 0, 0, 0);
+      for (int e = 0; e < 4; ++e) {
+        const int r = kb + 16 * u + 4 * q + e;
+        a[u][e] = r < M ? gc[(long)r * ldg] : 0.f;
+        b[u][e] = r < M ? ac[(long)r * lda] : 0.f;
+      }
+#pragma unroll
+    for (int u = 0; u < RC; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][e], b[u][e], acc, 0, 0, 0);
   }
   return acc;
 }

@@ -45,17 +45,27 @@ struct TP {
 __device__ __forceinline__ float comp(const float4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
 
 // acc (16 rows x 16 cols of tile starting at weight row n0) += act[16][K] . W[n0.., K]^T
-// act: LDS, row stride lda (floats); W global row-major with row stride ldw.  K % 16 == 0.
+// act: LDS, row stride lda (floats); W global row-major with row stride ldw.  K % 16 == 0.  The weight
+// loads of KC K-steps are issued before the MFMAs that use them (one L2 latency per chunk).
+constexpr int KC = 8;
 __device__ __forceinline__ floatx4 tile_gemm(const float* act, int lda, const float* W, int ldw, int n0, int K, int lane) {
   const int j = lane & 15, q = lane >> 4;
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   const float* wr = W + (long)(n0 + j) * ldw + 4 * q;
   const float* ar = act + j * lda + 4 * q;
-  for (int k0 = 0; k0 < K; k0 += 16) {
-    const float4 w = *reinterpret_cast<const float4*>(wr + k0);
-    const float4 a = *reinterpret_cast<const float4*>(ar + k0);
+  for (int kb = 0; kb < K; kb += 16 * KC) {
+    float4 w[KC];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a, e), comp(w, e), acc, 0, 0, 0);
+    for (int u = 0; u < KC; ++u)
+      if (kb + 16 * u < K) w[u] = *reinterpret_cast<const float4*>(wr + kb + 16 * u);
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+      if (kb + 16 * u < K) {
+        const float4 a = *reinterpret_cast<const float4*>(ar + kb + 16 * u);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a, e), comp(w[u], e), acc, 0, 0, 0);
+      }
+    }
   }
   return acc;
 }

@@ -51,6 +51,21 @@ __device__ __forceinline__ float f_act_grad(float z, int act) {
     default: return 1.f;
   }
 }
+// compile-time activation forms (common.h SRL_ACT_SPECIALIZE)
+template <int ACTC>
+__device__ __forceinline__ float f_act_c(float z, int act) {
+  if constexpr (ACTC == ACT_SILU) return z * fsig(z);
+  else return f_act(z, act);
+}
+template <int ACTC>
+__device__ __forceinline__ float f_act_grad_c(float z, int act) {
+  if constexpr (ACTC == ACT_SILU) {
+    const float sg = fsig(z);
+    return sg * (1.f + z * (1.f - sg));
+  } else {
+    return f_act_grad(z, act);
+  }
+}
 
 // ---------------------------------------------------------------------------------- GEMM core
 // Weight fragments of one batch of k chunks, loaded at kernel entry so their latency hides behind
@@ -170,9 +185,9 @@ __device__ __forceinline__ void wave_row_stats(const float* r, int N, float eps,
 
 // LayerNorm + activation of one row r[0:N) (N <= 64 * M) by the calling wave, the row held in
 // registers: one LDS read per element, both statistics from registers, one write.
-template <int M>
-__device__ __forceinline__ void wave_ln_act_row(float* r, int N, float eps, const float* gam, const float* bet, int act,
-                                                float& mu, float& rs) {
+template <int M, int ACTC>
+__device__ __forceinline__ void wave_ln_act_row_t(float* r, int N, float eps, const float* gam, const float* bet, int act,
+                                                  float& mu, float& rs) {
   const int s = threadIdx.x & 63;
   float v[M];
   float a = 0.f;
@@ -194,16 +209,21 @@ __device__ __forceinline__ void wave_ln_act_row(float* r, int N, float eps, cons
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const int k = s + 64 * m;
-    if (k < N) r[k] = f_act((v[m] - mu) * rs * gam[k] + bet[k], act);
+    if (k < N) r[k] = f_act_c<ACTC>((v[m] - mu) * rs * gam[k] + bet[k], act);
   }
+}
+template <int M>
+__device__ __forceinline__ void wave_ln_act_row(float* r, int N, float eps, const float* gam, const float* bet, int act,
+                                                float& mu, float& rs) {
+  SRL_ACT_SPECIALIZE(act, wave_ln_act_row_t<M, ACTC>(r, N, eps, gam, bet, act, mu, rs));
 }
 
 // LayerNorm(+act) adjoint of one row, first pass, with the row in registers (N <= 64 * M): loads x
 // and dy once, leaves xh / dz in registers AND in place (x <- xh, dy <- dz, for ln_param_partials);
 // returns s1 = mean(dz*gamma), s2 = mean(dz*gamma*xh).  Finish with wave_ln_bwd_finish.
-template <int M>
-__device__ __forceinline__ void wave_ln_bwd_regs(float* x, float* dy, const float* gam, const float* bet, int N, int act,
-                                                 float mu, float rs, float (&xh)[M], float (&dz)[M], float& s1, float& s2) {
+template <int M, int ACTC>
+__device__ __forceinline__ void wave_ln_bwd_regs_t(float* x, float* dy, const float* gam, const float* bet, int N, int act,
+                                                   float mu, float rs, float (&xh)[M], float (&dz)[M], float& s1, float& s2) {
   const int s = threadIdx.x & 63;
   float xv[M], dv[M];
 #pragma unroll
@@ -218,7 +238,7 @@ __device__ __forceinline__ void wave_ln_bwd_regs(float* x, float* dy, const floa
     const int k = s + 64 * m;
     if (k < N) {
       xh[m] = (xv[m] - mu) * rs;
-      dz[m] = dv[m] * f_act_grad(xh[m] * gam[k] + bet[k], act);
+      dz[m] = dv[m] * f_act_grad_c<ACTC>(xh[m] * gam[k] + bet[k], act);
       const float dxh = dz[m] * gam[k];
       a += dxh;
       b += dxh * xh[m];
@@ -231,6 +251,11 @@ __device__ __forceinline__ void wave_ln_bwd_regs(float* x, float* dy, const floa
   }
   s1 = wave_sum(a) / N;
   s2 = wave_sum(b) / N;
+}
+template <int M>
+__device__ __forceinline__ void wave_ln_bwd_regs(float* x, float* dy, const float* gam, const float* bet, int N, int act,
+                                                 float mu, float rs, float (&xh)[M], float (&dz)[M], float& s1, float& s2) {
+  SRL_ACT_SPECIALIZE(act, wave_ln_bwd_regs_t<M, ACTC>(x, dy, gam, bet, N, act, mu, rs, xh, dz, s1, s2));
 }
 
 template <int M>
@@ -246,13 +271,14 @@ __device__ __forceinline__ void wave_ln_bwd_finish(float* x, const float* gam, i
 
 // LayerNorm(+act) adjoint, first pass, by the wave owning a row: x <- xh, dy <- dz = dy * act'(z);
 // returns (mean(dz*gamma), mean(dz*gamma*xh)).
-__device__ __forceinline__ void wave_ln_bwd_prep(float* x, float* dy, const float* gam, const float* bet, int N, int act,
-                                                 float mu, float rs, float& s1, float& s2) {
+template <int ACTC>
+__device__ __forceinline__ void wave_ln_bwd_prep_t(float* x, float* dy, const float* gam, const float* bet, int N, int act,
+                                                   float mu, float rs, float& s1, float& s2) {
   const int s = threadIdx.x & 63;
   float a = 0.f, b = 0.f;
   for (int k = s; k < N; k += 64) {
     const float xh = (x[k] - mu) * rs;
-    const float dz = dy[k] * f_act_grad(xh * gam[k] + bet[k], act);
+    const float dz = dy[k] * f_act_grad_c<ACTC>(xh * gam[k] + bet[k], act);
     x[k] = xh;
     dy[k] = dz;
     const float dxh = dz * gam[k];
@@ -261,6 +287,10 @@ __device__ __forceinline__ void wave_ln_bwd_prep(float* x, float* dy, const floa
   }
   s1 = wave_sum(a) / N;
   s2 = wave_sum(b) / N;
+}
+__device__ __forceinline__ void wave_ln_bwd_prep(float* x, float* dy, const float* gam, const float* bet, int N, int act,
+                                                 float mu, float rs, float& s1, float& s2) {
+  SRL_ACT_SPECIALIZE(act, wave_ln_bwd_prep_t<ACTC>(x, dy, gam, bet, N, act, mu, rs, s1, s2));
 }
 
 // Column sums over the B rows of dz*xh and dz (after wave_ln_bwd_prep) for columns [lo, hi):
