@@ -30,6 +30,78 @@ __device__ __forceinline__ float seg_max(float v, int width) {
   return v;
 }
 
+// ---------------------------------------------------------------- DPP reductions
+// Cross-lane reductions on latency-critical paths (persistent scan, samplers), without the LDS crossbar: __shfl_xor
+// lowers to ds_bpermute_b32 (an LDS-pipe round trip per level, 6 dependent ones per 64-lane sum); these use
+// DPP row ops (quad butterflies, row rotations / shifts / broadcasts: plain VALU operand modifiers) and
+// v_readlane for the cross-row step.  Summation order differs from the butterfly: fp32 rounding only.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xF, false));
+}
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+// every lane of each 16-lane row gets the row's sum / max
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x124>(v);  // row_ror:4
+  v += dpp_f<0x128>(v);  // row_ror:8
+  return v;
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x124>(v));
+  v = fmaxf(v, dpp_f<0x128>(v));
+  return v;
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = row16_sum(v);
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+}
+// segments of 32 lanes (lanes 0-31, 32-63): every lane gets its segment's sum / max
+__device__ __forceinline__ float seg32_sum(float v) {
+  v = row16_sum(v);
+  const float a = lane_f(v, 0) + lane_f(v, 16), b = lane_f(v, 32) + lane_f(v, 48);
+  return (threadIdx.x & 32) ? b : a;
+}
+__device__ __forceinline__ float seg32_max(float v) {
+  v = row16_max(v);
+  const float a = fmaxf(lane_f(v, 0), lane_f(v, 16)), b = fmaxf(lane_f(v, 32), lane_f(v, 48));
+  return (threadIdx.x & 32) ? b : a;
+}
+// inclusive prefix sum inside each 32-lane segment (Hillis-Steele row shifts, then row 1 / 3 add row 0 / 2's total)
+__device__ __forceinline__ float seg32_scan(float v) {
+  v += dpp_f<0x111>(v);       // row_shr:1
+  v += dpp_f<0x112>(v);       // row_shr:2
+  v += dpp_f<0x114>(v);       // row_shr:4
+  v += dpp_f<0x118>(v);       // row_shr:8
+  v += dpp_f<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
+  return v;
+}
+// inclusive prefix sum inside each 16-lane row
+__device__ __forceinline__ float row16_scan(float v) {
+  v += dpp_f<0x111>(v);
+  v += dpp_f<0x112>(v);
+  v += dpp_f<0x114>(v);
+  v += dpp_f<0x118>(v);
+  return v;
+}
+// width-generic forms: DPP for the widths above, the xor-shuffle butterfly otherwise
+__device__ __forceinline__ float seg_sum_f(float v, int width) {
+  if (width == 32) return seg32_sum(v);
+  if (width == 16) return row16_sum(v);
+  if (width == 64) return wave_sum_dpp(v);
+  return seg_sum(v, width);
+}
+__device__ __forceinline__ float seg_max_f(float v, int width) {
+  if (width == 32) return seg32_max(v);
+  if (width == 16) return row16_max(v);
+  return seg_max(v, width);
+}
+
 // Block-wide sum for blockDim.x = 64 * NW. `red` must hold NW floats (LDS).
 template <int NW>
 __device__ __forceinline__ float block_sum(float v, float* red) {

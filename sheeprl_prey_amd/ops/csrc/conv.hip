@@ -340,10 +340,21 @@ __device__ __forceinline__ void stage_chunk(const f16v (&acc)[TM][TN], int i, co
       s[(f.wm * 32 + 8 * (r >> 2) + 4 * (f.lane >> 5) + (r & 3)) * pitch + f.col(j)] = acc[i][j][r];
 }
 
+// sum over aligned segments of LPR lanes, every lane of the segment gets it: DPP quad butterflies, half-row /
+// row mirrors (8 / 16 lanes), readlanes across rows (32 / 64) - no LDS-crossbar shuffles (common.h)
 template <int LPR>
 __device__ __forceinline__ float lseg_sum(float v) {
-#pragma unroll
-  for (int o = 1; o < LPR; o <<= 1) v += __shfl_xor(v, o, 64);
+  static_assert(LPR == 1 || LPR == 2 || LPR == 4 || LPR == 8 || LPR == 16 || LPR == 32 || LPR == 64, "lseg_sum: LPR");
+  if constexpr (LPR >= 2) v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  if constexpr (LPR >= 4) v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  if constexpr (LPR >= 8) v += dpp_f<0x141>(v);  // row_half_mirror
+  if constexpr (LPR >= 16) v += dpp_f<0x140>(v); // row_mirror
+  if constexpr (LPR == 32) {
+    const float a = lane_f(v, 0) + lane_f(v, 16), b = lane_f(v, 32) + lane_f(v, 48);
+    v = (threadIdx.x & 32) ? b : a;
+  } else if constexpr (LPR == 64) {
+    v = (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+  }
   return v;
 }
 

@@ -12,6 +12,8 @@
 namespace srl {
 
 __device__ __forceinline__ float seg_prefix_sum(float v, int width, int lane_in_seg) {
+  if (width == 32) return seg32_scan(v);  // DPP forms (common.h): no LDS-crossbar round trips
+  if (width == 16) return row16_scan(v);
   for (int o = 1; o < width; o <<= 1) {
     float t = __shfl_up(v, o, width);
     if (lane_in_seg >= o) v += t;
@@ -51,25 +53,28 @@ __global__ void __launch_bounds__(256) unimix_sample_fwd_kernel(const float* __r
   float l = valid ? logits[off] : -INFINITY;
   float m = l;
   if (alpha > 0.f) {
-    float mx = seg_max(l, W);
+    float mx = seg_max_f(l, W);
     float e = valid ? __expf(l - mx) : 0.f;
-    float s = seg_sum(e, W);
+    float s = seg_sum_f(e, W);
     float q = e / s;
     float pm = (1.f - alpha) * q + alpha / C;
     pm = fminf(fmaxf(pm, FEPS), 1.f - FEPS);
     m = valid ? logf(pm) : -INFINITY;
   }
   // probabilities of Categorical(logits=m)
-  float mx2 = seg_max(m, W);
+  float mx2 = seg_max_f(m, W);
   float e2 = valid ? __expf(m - mx2) : 0.f;
-  float s2 = seg_sum(e2, W);
+  float s2 = seg_sum_f(e2, W);
   float p = e2 / s2;
   int pick;
   if (uniform != nullptr) {
     float cdf = seg_prefix_sum(p, W, k);
     float u = row_ok ? uniform[r] : 0.f;
-    float below = (valid && cdf < u * seg_max(cdf, W)) ? 1.f : 0.f;
-    pick = (int)seg_sum(below, W);
+    // every cross-lane reduction runs with the whole wave active: a DPP operand from a lane masked off by
+    // a divergent branch (e.g. the short-circuit of `valid && ...`) reads 0, not the lane's value
+    const float cmax = seg_max_f(cdf, W);
+    float below = (valid && cdf < u * cmax) ? 1.f : 0.f;
+    pick = (int)seg_sum_f(below, W);
     if (pick > C - 1) pick = C - 1;
   } else {
     pick = seg_argmax(valid ? p : -1.f, k, W);
@@ -101,9 +106,9 @@ __global__ void __launch_bounds__(256) unimix_sample_bwd_kernel(const float* __r
   float q = 0.f, pm = 0.f, m = l;
   bool clamped = false;
   if (alpha > 0.f) {
-    float mx = seg_max(l, W);
+    float mx = seg_max_f(l, W);
     float e = valid ? __expf(l - mx) : 0.f;
-    float s = seg_sum(e, W);
+    float s = seg_sum_f(e, W);
     q = e / s;
     pm = (1.f - alpha) * q + alpha / C;
     clamped = pm <= FEPS || pm >= 1.f - FEPS;
@@ -111,17 +116,17 @@ __global__ void __launch_bounds__(256) unimix_sample_bwd_kernel(const float* __r
   }
   float gm = (valid && g_mixed) ? g_mixed[off] : 0.f;
   if (g_sample) {
-    float mx2 = seg_max(m, W);
+    float mx2 = seg_max_f(m, W);
     float e2 = valid ? __expf(m - mx2) : 0.f;
-    float p = e2 / seg_sum(e2, W);
+    float p = e2 / seg_sum_f(e2, W);
     float gs = valid ? g_sample[off] : 0.f;
-    float dot = seg_sum(p * gs, W);
+    float dot = seg_sum_f(p * gs, W);
     gm += p * (gs - dot);
   }
   float dl;
   if (alpha > 0.f) {
     float w = (valid && !clamped) ? (1.f - alpha) * gm / pm : 0.f;
-    float dot = seg_sum(q * w, W);
+    float dot = seg_sum_f(q * w, W);
     dl = q * (w - dot);
   } else {
     dl = gm;

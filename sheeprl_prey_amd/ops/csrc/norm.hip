@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(256) ln_wave_fwd_kernel(const float* __restric
       v[k] = idx < N ? xr[idx] : 0.f;
       s += v[k];
     }
-    const float mu = wave_sum(s) / N;
+    const float mu = wave_sum_dpp(s) / N;
     float q = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(256) ln_wave_fwd_kernel(const float* __restric
       float d = idx < N ? v[k] - mu : 0.f;
       q += d * d;
     }
-    const float rs = rsqrtf(wave_sum(q) / N + eps);
+    const float rs = rsqrtf(wave_sum_dpp(q) / N + eps);
     const int ro = (G == 1) ? r : g * Bn + b;
     float* yr = y + (int64_t)ro * ldy;
 #pragma unroll
@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(256) ln_wave4_fwd_kernel(const float* __restri
       v[k] = i4 < N4 ? xr[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
       s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
     }
-    const float mu = wave_sum(s) / N;
+    const float mu = wave_sum_dpp(s) / N;
     float q = 0.f;
 #pragma unroll
     for (int k = 0; k < NV4; ++k) {
@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(256) ln_wave4_fwd_kernel(const float* __restri
         q += (a * a + b * b) + (c * c + d * d);
       }
     }
-    const float rs = rsqrtf(wave_sum(q) / N + eps);
+    const float rs = rsqrtf(wave_sum_dpp(q) / N + eps);
     float4* yr = reinterpret_cast<float4*>(y + (int64_t)r * ldy);
 #pragma unroll
     for (int k = 0; k < NV4; ++k) {
@@ -169,8 +169,8 @@ __global__ void __launch_bounds__(256) ln_wave_bwd_kernel(const float* __restric
         s2 += dxh[k] * h;
       }
     }
-    const float m1 = wave_sum(s1) / N;
-    const float m2 = wave_sum(s2) / N;
+    const float m1 = wave_sum_dpp(s1) / N;
+    const float m2 = wave_sum_dpp(s2) / N;
     float* dxr = dx + (int64_t)r * lddx;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {

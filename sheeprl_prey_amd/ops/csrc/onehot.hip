@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
     float s = 0.f;
 #pragma unroll
     for (int v = 0; v < NV4; ++v) s += (acc[v][0] + acc[v][1]) + (acc[v][2] + acc[v][3]);
-    s = wave_sum(s);
+    s = wave_sum_dpp(s);
     if (WPR == 2) {
       if (lane == 0) red[0][wave] = s;
       __syncthreads();
@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
         q += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
       }
     }
-    q = wave_sum(q);
+    q = wave_sum_dpp(q);
     if (WPR == 2) {
       if (lane == 0) red[1][wave] = q;
       __syncthreads();

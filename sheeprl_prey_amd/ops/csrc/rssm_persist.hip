@@ -300,8 +300,8 @@ __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
     if (threadIdx.x < 256) {
       const int b = threadIdx.x >> 4, c = threadIdx.x & 15;
       const float x = ct[threadIdx.x];
-      const float m = seg_sum(x, 16) * (1.f / 16.f);
-      const float q = seg_sum((x - m) * (x - m), 16);
+      const float m = row16_sum(x) * (1.f / 16.f);
+      const float q = row16_sum((x - m) * (x - m));
       if (b < B) {
         st_wt(p.gx + ((size_t)t * B + b) * N3 + a * 16 + c, x);
         if (c == 0) st_wt2(p.gst + (((size_t)t * nA + a) * 16 + b) * 2, m, q);
@@ -372,14 +372,14 @@ __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
         pr[k] = i < nA ? ld_wt2(p.gst + (((size_t)t * nA + i) * 16 + w) * 2) : make_float2(0.f, 0.f);
       }
       // row statistics of gx from the tile partials (16 columns each): Chan's parallel combine
-      const float mu = wave_sum(pr[0].x + pr[1].x) / nA;
+      const float mu = wave_sum_dpp(pr[0].x + pr[1].x) / nA;
       float q = 0.f;
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int i = lane + 64 * k;
         if (i < nA) q += pr[k].y + 16.f * (pr[k].x - mu) * (pr[k].x - mu);
       }
-      const float rs = rsqrtf(wave_sum(q) / N3 + p.epsg);
+      const float rs = rsqrtf(wave_sum_dpp(q) / N3 + p.epsg);
       const float keep = 1.f - p.first[(size_t)t * B + w];
       float* hr = As + w * lda;
 #pragma unroll
@@ -497,23 +497,27 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
       const float l = ct[threadIdx.x] + ebias;
       float m = l;
       if (p.alpha > 0.f) {
-        const float mx = seg_max(l, C);
+        const float mx = seg_max_f(l, C);
         const float e = __expf(l - mx);
-        const float q = e / seg_sum(e, C);
+        const float q = e / seg_sum_f(e, C);
         float pm = (1.f - p.alpha) * q + p.alpha / C;
         pm = fminf(fmaxf(pm, FEPS), 1.f - FEPS);
         m = logf(pm);
       }
-      const float mx2 = seg_max(m, C);
+      const float mx2 = seg_max_f(m, C);
       const float e2 = __expf(m - mx2);
-      const float pr = e2 / seg_sum(e2, C);
+      const float pr = e2 / seg_sum_f(e2, C);
       float cdf = pr;  // inclusive prefix sum inside the segment
-      for (int o = 1; o < C; o <<= 1) {
-        const float tt = __shfl_up(cdf, o, C);
-        if (k >= o) cdf += tt;
+      if (C == 32) {
+        cdf = seg32_scan(cdf);
+      } else {
+        for (int o = 1; o < C; o <<= 1) {
+          const float tt = __shfl_up(cdf, o, C);
+          if (k >= o) cdf += tt;
+        }
       }
-      const float below = cdf < euni * seg_max(cdf, C) ? 1.f : 0.f;
-      int pick = (int)seg_sum(below, C);
+      const float below = cdf < euni * seg_max_f(cdf, C) ? 1.f : 0.f;
+      int pick = (int)seg_sum_f(below, C);
       if (pick > C - 1) pick = C - 1;
       el = l;
       em = m;
@@ -558,8 +562,8 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
             }
           }
         }
-        x += __shfl_xor(x, 1, 64);
-        x += __shfl_xor(x, 2, 64);
+        x += dpp_f<0xB1>(x);  // quad sum (quad_perm [1,0,3,2], [2,3,0,1])
+        x += dpp_f<0x4E>(x);
         if (gb < B && gq == 0) {
           float* d = xr1 + (size_t)gb * D + col;
           st_wt(d, (lt == 0 ? xr0s[threadIdx.x] : *d) + x);
@@ -727,7 +731,7 @@ __device__ __forceinline__ void bwd_G2(const PP& p, int i, float* sm) {
       const float dz1 = da * r;
       const float dz0 = da * zc * r * (1.f - r);
       const float d0 = dz0 * gw0, d1 = dz1 * gw1, d2 = dz2 * gw2;
-      const float s1p = seg_sum(d0 + d1 + d2, 16), s2p = seg_sum(d0 * a0 + d1 * a1 + d2 * a2, 16);
+      const float s1p = row16_sum(d0 + d1 + d2), s2p = row16_sum(d0 * a0 + d1 * a1 + d2 * a2);
       float* g = gsc + eb * 96 + ec;
       g[0] = dz0 * a0;
       g[16] = dz0;
@@ -795,7 +799,7 @@ __device__ __forceinline__ void bwd_G3(const PP& p, int i3, float* sm) {
     PROF(5, 1);
     if (w < B) {
       const float2 sp = lane < n2 ? ld_wt2(p.sst + (((size_t)t * n2 + lane) * 16 + w) * 2) : make_float2(0.f, 0.f);
-      const float m1 = wave_sum(sp.x) / N3, m2 = wave_sum(sp.y) / N3;
+      const float m1 = wave_sum_dpp(sp.x) / N3, m2 = wave_sum_dpp(sp.y) / N3;
       if (lane == 0) {
         rowst[w * 4 + 2] = m1;
         rowst[w * 4 + 3] = m2;
@@ -891,18 +895,18 @@ __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
       // before the wait (off the G3 -> G4 -> G1 critical path) and parked in LDS
       float q = 0.f, pm = 0.f, m = el, cl = 0.f;
       if (p.alpha > 0.f) {
-        const float mx = seg_max(el, C);
+        const float mx = seg_max_f(el, C);
         const float e = __expf(el - mx);
-        q = e / seg_sum(e, C);
+        q = e / seg_sum_f(e, C);
         pm = (1.f - p.alpha) * q + p.alpha / C;
         cl = (pm <= FEPS || pm >= 1.f - FEPS) ? 1.f : 0.f;
         m = logf(fminf(fmaxf(pm, FEPS), 1.f - FEPS));
       }
-      const float mx2 = seg_max(m, C);
+      const float mx2 = seg_max_f(m, C);
       const float e2 = __expf(m - mx2);
       fpre[threadIdx.x] = q;
       fpre[512 + threadIdx.x] = pm;
-      fpre[1024 + threadIdx.x] = e2 / seg_sum(e2, C);
+      fpre[1024 + threadIdx.x] = e2 / seg_sum_f(e2, C);
       fpre[1536 + threadIdx.x] = cl;
     }
     if (!wait_ctr(p, 2, e3, T - t, 14, flag)) return;
@@ -942,12 +946,12 @@ __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
       const float q = fpre[threadIdx.x], pm = fpre[512 + threadIdx.x], pr = fpre[1024 + threadIdx.x];
       const bool clamped = fpre[1536 + threadIdx.x] != 0.f;
       float gm = fpre[2048 + threadIdx.x];
-      const float dot = seg_sum(pr * ds, C);
+      const float dot = seg_sum_f(pr * ds, C);
       gm += pr * (ds - dot);
       float dl;
       if (p.alpha > 0.f) {
         const float wv = clamped ? 0.f : (1.f - p.alpha) * gm / pm;
-        dl = q * (wv - seg_sum(q * wv, C));
+        dl = q * (wv - seg_sum_f(q * wv, C));
       } else {
         dl = gm;
       }

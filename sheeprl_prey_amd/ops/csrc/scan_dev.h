@@ -197,7 +197,7 @@ __device__ __forceinline__ void wave_ln_act_row_t(float* r, int N, float eps, co
     v[m] = k < N ? r[k] : 0.f;
     a += v[m];
   }
-  mu = wave_sum(a) / N;
+  mu = wave_sum_dpp(a) / N;
   float q = 0.f;
 #pragma unroll
   for (int m = 0; m < M; ++m) {
@@ -205,7 +205,7 @@ __device__ __forceinline__ void wave_ln_act_row_t(float* r, int N, float eps, co
     const float d = k < N ? v[m] - mu : 0.f;
     q += d * d;
   }
-  rs = rsqrtf(wave_sum(q) / N + eps);
+  rs = rsqrtf(wave_sum_dpp(q) / N + eps);
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const int k = s + 64 * m;
@@ -249,8 +249,8 @@ __device__ __forceinline__ void wave_ln_bwd_regs_t(float* x, float* dy, const fl
       dz[m] = 0.f;
     }
   }
-  s1 = wave_sum(a) / N;
-  s2 = wave_sum(b) / N;
+  s1 = wave_sum_dpp(a) / N;
+  s2 = wave_sum_dpp(b) / N;
 }
 template <int M>
 __device__ __forceinline__ void wave_ln_bwd_regs(float* x, float* dy, const float* gam, const float* bet, int N, int act,
