@@ -304,7 +304,7 @@ class RSSM(nn.Module):
         235-257`` over ``RSSM.imagination`` + ``Actor.forward``; the discrete objective back-propagates
         only through log-probs of detached actions, so no graph is needed).
 
-        Every step writes straight into one buffer ``[H+1, M, A + S + Hd + D]`` holding (action | prior |
+        Every step writes straight into one buffer ``[H+1, M, Ap + S + Hd + D]`` holding (action | pad | prior |
         h | x), x = the recurrent MLP's output of the step: the sampling, LayerNorm and LN-GRU kernels
         store into row-strided slices of it, so the GRU input projection is ONE GEMM over (h | x)
         (K = Hd + D) and the trajectories ``[H+1, M, S + Hd]`` / actions ``[H+1, M, A]`` are views.
@@ -340,10 +340,16 @@ class RSSM(nn.Module):
         gru = self.recurrent_model.rnn
         Wg = gru.linear.weight  # columns: (h | feat)
         ln = gru.layer_norm
-        Wd = A + S + Hd + D
+        # prior columns start at Ap >= A: with the gathered recurrent layer the buffer's (action | prior) block is
+        # never read as a dense operand, so the actions are padded to put h (the dense part of every head's first
+        # layer) on a 16-byte boundary with a row stride % 4 == 0 - the heads' weight-gradient kernels then stage
+        # it with 16-byte loads (ops.wgrad)
+        Ap = A + ((-(A + S)) % 4) if use_gather else A
+        Wd = Ap + S + Hd + D
+        Wd += (-Wd) % 4
         buf = post.new_empty(horizon + 1, M, Wd)
-        buf[0, :, A:A + S].copy_(post)
-        buf[0, :, A + S:A + S + Hd].copy_(h)
+        buf[0, :, Ap:Ap + S].copy_(post)
+        buf[0, :, Ap + S:Ap + S + Hd].copy_(h)
         IDX = torch.empty(horizon + 1, M, nh + G, dtype=torch.int32, device=dev)
         oh.onehot_index(post, disc, IDX[0, :, nh:], A)
         W = rec_lin.weight  # columns: (prior | action)
@@ -353,8 +359,10 @@ class RSSM(nn.Module):
         a0 = layers[0][0] if layers is not None else None
         a_table = a0.weight[:, :S].t().contiguous() if (gather and layers is not None and oh.layer_supported(a0, S)) else None
         act_scratch = None
+        if trunk_rec is not None and a_table is not None:
+            trunk_rec.onehot = (IDX[:, :, nh:], G, A, S)  # the trunk backward scatters the prior columns' dW
         for t in range(horizon + 1):
-            traj_t = buf[t, :, A:A + S + Hd]
+            traj_t = buf[t, :, Ap:Ap + S + Hd]
             if trunk_rec is not None:
                 out = trunk_rec.step(t, traj_t, gather=(IDX[t, :, nh:], G, A, S, a_table) if a_table is not None else None)
             elif layers is not None and a_table is not None:
@@ -370,7 +378,7 @@ class RSSM(nn.Module):
                 c0 += a
             if t == horizon:
                 break
-            xs = buf[t, :, A + S + Hd:]
+            xs = buf[t, :, Ap + S + Hd:Ap + S + Hd + D]
             if use_gather:
                 oh.gather_first_layer(buf[t, :, :A + S], IDX[t], nh + G, 0, rec_lin, rec_ln, A + S, table=rec_table,
                                       y_out=xs)
@@ -381,14 +389,14 @@ class RSSM(nn.Module):
                 for m in list(self.recurrent_model.mlp.model)[1:]:
                     x = m(x)
                 xs.copy_(x)
-            gx = torch.mm(buf[t, :, A + S:], Wg.t())  # (h | x) in one GEMM
+            gx = torch.mm(buf[t, :, Ap + S:Ap + S + Hd + D], Wg.t())  # (h | x) in one GEMM
             if gru.linear.bias is not None:
                 gx = gx + gru.linear.bias
-            C.ln_gru_into(gx, buf[t, :, A + S:A + S + Hd], ln.weight, ln.bias, float(ln.eps), buf[t + 1, :, A + S:A + S + Hd])
-            logits = self.transition_model(buf[t + 1, :, A + S:A + S + Hd])
-            C.unimix_sample_into(logits.contiguous(), U[t, nh * M:], disc, float(self.unimix), buf[t + 1, :, A:A + S],
+            C.ln_gru_into(gx, buf[t, :, Ap + S:Ap + S + Hd], ln.weight, ln.bias, float(ln.eps), buf[t + 1, :, Ap + S:Ap + S + Hd])
+            logits = self.transition_model(buf[t + 1, :, Ap + S:Ap + S + Hd])
+            C.unimix_sample_into(logits.contiguous(), U[t, nh * M:], disc, float(self.unimix), buf[t + 1, :, Ap:Ap + S],
                                  IDX[t + 1, :, nh:], A)
-        out = (buf[:, :, A:A + S + Hd], buf[:, :, :A])
+        out = (buf[:, :, Ap:Ap + S + Hd], buf[:, :, :A])
         if record:
             out = out + (trunk_rec,)
         if indices:

@@ -88,6 +88,56 @@ def _lin2d(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
     return torch.nn.functional.linear(x, weight, bias)
 
 
+# =============================================================== tall-layer weight gradients (wgrad.hip)
+WGRAD_MIN_ROWS = int(os.environ.get("SRL_WGRAD_MIN_ROWS", "4096"))  # 0 disables (A/B switch)
+
+
+def _rows2d(t: Tensor) -> Tensor:
+    """``t`` as a row-strided 2-D [rows, last] view (no copy when the leading dims fold into one stride)."""
+    if t.dim() == 2 and t.stride(-1) == 1:
+        return t
+    try:
+        v = t.view(-1, t.shape[-1])
+    except RuntimeError:
+        v = t.reshape(-1, t.shape[-1])
+    return v if v.stride(-1) == 1 else v.contiguous()
+
+
+def wgrad_ok(dz: Tensor) -> bool:
+    """The split-K kernel is used for the weight gradients of layers over >= WGRAD_MIN_ROWS rows (the
+    imagination heads: 15-16k rows), where the library GEMM runs its M reduction in a handful of tiles."""
+    rows = dz.numel() // max(1, dz.shape[-1])
+    return WGRAD_MIN_ROWS > 0 and rows >= WGRAD_MIN_ROWS and _native(dz) and dz.dtype == torch.float32
+
+
+def wgrad_onehot_ok(dz: Tensor, G: int, n_onehot: int) -> bool:
+    """The one-hot scatter covers <= 32 classes per group and 16-byte aligned dZ rows of N % 4 == 0."""
+    C = n_onehot // max(1, G)
+    return (C * G == n_onehot and C <= 32 and dz.shape[-1] % 4 == 0 and dz.stride(-2) % 4 == 0 and dz.stride(-1) == 1
+            and dz.data_ptr() % 16 == 0)
+
+
+def wgrad(dz: Tensor, x: Optional[Tensor] = None, onehot=None, bias: bool = False):
+    """``(dW, db)`` of a linear layer ``z = [onehot | x] W^T + b`` from ``dz`` = dL/dz over M rows:
+    ``dW [N, Kone + Kd] = [onehot | x]^T dz``, ``db = dz.sum(0)`` (None unless ``bias``; needs ``x``).
+    ``onehot = (idx, G, off, n_onehot)``: the first ``n_onehot = G*C`` input columns are exact one-hots whose hot
+    column is ``idx[m, g] - off`` (idx row-strided int32 [M, >= G]); they are scattered, not multiplied."""
+    dz2 = _rows2d(dz)
+    M, N = dz2.shape
+    x2 = _rows2d(x) if x is not None else None
+    idx2 = None
+    G = C = off = 0
+    if onehot is not None:
+        idx, G, off, n1 = onehot
+        idx2 = _rows2d(idx)
+        C = n1 // G
+    Kd = x2.shape[1] if x2 is not None else 0
+    dW = torch.empty(N, G * C + Kd, device=dz.device, dtype=torch.float32)
+    db = torch.empty(N, device=dz.device, dtype=torch.float32) if bias else None
+    _ext().wgrad(dz2, x2, idx2, int(G), int(C), int(off), dW, db, False)
+    return dW, db
+
+
 class _Linear(torch.autograd.Function):
     """``F.linear`` whose backward takes the bias gradient with a row-split column-sum kernel
     (``norm.hip: colsum1``): torch's dim-0 sum of a [15360, 255] two-hot head gradient ran 165 us on
@@ -107,6 +157,9 @@ class _Linear(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = (g2 @ w).view(*gy.shape[:-1], w.shape[1])
+        if ctx.needs_input_grad[1] and wgrad_ok(g2):
+            dw, db = wgrad(g2, x, bias=ctx.has_bias and ctx.needs_input_grad[2])
+            return dx, dw, db
         if ctx.needs_input_grad[1]:
             dw = g2.t() @ x.reshape(-1, x.shape[-1])
         if ctx.has_bias and ctx.needs_input_grad[2]:

@@ -57,6 +57,15 @@ void launch_actor_loss(const float* z, const float* act, const float* lam, const
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
                        float* dz, float* partial, float* loss, hipStream_t st);
 
+int wgrad_dense_chunks(int M, int N, int K);
+void launch_wgrad_dense(const float* dz, long ldz, const float* x, long ldx, float* part, float* bpart, int M, int N, int K,
+                        int S, hipStream_t st);
+int wgrad_onehot_chunks(int M, int N, int G, int C);
+bool launch_wgrad_onehot(const float* dz, long ldz, const int* idx, long ldi, int off, float* part, int M, int N, int G, int C,
+                         int S, hipStream_t st);
+void launch_wgrad_reduce(const float* part, int S, int N, int K, float* out, long ldo, int coff, bool accumulate,
+                         hipStream_t st);
+
 void launch_onehot_index(const float* x, int ldx, int M, int G, int C, int* idx, int ldi, int off, hipStream_t st);
 bool launch_onehot_gather_ln(const float* Y, int ldy, const int* idx, int ldi, int G, int off, const float* T, int K,
                              const float* bias, const float* gamma, const float* beta, float eps, int act, int ln,
@@ -574,12 +583,67 @@ std::vector<torch::Tensor> gather_rows(std::vector<torch::Tensor> srcs, torch::T
   return outs;
 }
 
+// ------------------------------------------------------------------ tall-layer weight gradients (wgrad.hip)
+// dW[N, Kone + Kd] = [onehot(idx) | x]^T dz over M rows, db[N] = colsum(dz).  dz [M, N] and x [M, Kd] row-strided;
+// idx [M, >= G] int32 row-strided with table rows idx - off in [0, G*C) (the first Kone = G*C columns of W);
+// dW / db written (or added, accumulate=true) into the given contiguous outputs.
+void wgrad(torch::Tensor dz, c10::optional<torch::Tensor> x, c10::optional<torch::Tensor> idx, int64_t G, int64_t C,
+           int64_t off, torch::Tensor dW, c10::optional<torch::Tensor> db, bool accumulate) {
+  TORCH_CHECK(dz.is_cuda() && dz.scalar_type() == torch::kFloat32 && dz.dim() == 2 && dz.stride(1) == 1 &&
+                  dz.stride(0) >= dz.size(1),
+              "wgrad: dz must be a row-strided float32 [M, N] GPU tensor");
+  const int64_t M = dz.size(0), N = dz.size(1);
+  const bool has_x = x.has_value() && x->defined();
+  const bool has_i = idx.has_value() && idx->defined();
+  TORCH_CHECK(has_x || has_i, "wgrad: need x and/or idx");
+  const int64_t Kone = has_i ? G * C : 0;
+  const int64_t Kd = has_x ? x->size(1) : 0;
+  TORCH_CHECK(dW.is_cuda() && dW.scalar_type() == torch::kFloat32 && dW.is_contiguous() && dW.dim() == 2 && dW.size(0) == N &&
+                  dW.size(1) == Kone + Kd,
+              "wgrad: dW must be a contiguous float32 [N, Kone + Kd] GPU tensor");
+  TORCH_CHECK(M > 0 && M < (1LL << 31) && N * (Kone + Kd) < (1LL << 31), "wgrad: sizes out of range");
+  const bool has_b = db.has_value() && db->defined();
+  if (has_b)
+    TORCH_CHECK(db->is_cuda() && db->scalar_type() == torch::kFloat32 && db->is_contiguous() && db->numel() == N,
+                "wgrad: db must be a contiguous float32 [N] GPU tensor");
+  TORCH_CHECK(!has_b || has_x, "wgrad: the bias column sum rides on the dense part (x required)");
+  auto opts = dz.options();
+  hipStream_t st = stream();
+  if (has_x) {
+    TORCH_CHECK(x->is_cuda() && x->scalar_type() == torch::kFloat32 && x->dim() == 2 && x->size(0) == M && x->stride(1) == 1 &&
+                    x->stride(0) >= x->size(1),
+                "wgrad: x must be a row-strided float32 [M, Kd] GPU tensor");
+    const int S = wgrad_dense_chunks((int)M, (int)N, (int)Kd);
+    auto part = torch::empty({(int64_t)S * N * Kd}, opts);
+    torch::Tensor bpart;
+    if (has_b) bpart = torch::empty({(int64_t)S * N}, opts);
+    launch_wgrad_dense(dz.data_ptr<float>(), dz.stride(0), x->data_ptr<float>(), x->stride(0), part.data_ptr<float>(),
+                       has_b ? bpart.data_ptr<float>() : nullptr, (int)M, (int)N, (int)Kd, S, st);
+    launch_wgrad_reduce(part.data_ptr<float>(), S, (int)N, (int)Kd, dW.data_ptr<float>(), Kone + Kd, (int)Kone, accumulate, st);
+    if (has_b) launch_wgrad_reduce(bpart.data_ptr<float>(), S, 1, (int)N, db->data_ptr<float>(), N, 0, accumulate, st);
+  }
+  if (has_i) {
+    TORCH_CHECK(idx->is_cuda() && idx->scalar_type() == torch::kInt && idx->dim() == 2 && idx->size(0) == M &&
+                    idx->size(1) >= G && idx->stride(1) == 1 && idx->stride(0) >= G,
+                "wgrad: idx must be a row-strided int32 [M, >= G] GPU tensor");
+    const int S = wgrad_onehot_chunks((int)M, (int)N, (int)G, (int)C);
+    TORCH_CHECK(S > 0, "wgrad: one-hot group of ", C, " classes does not fit the LDS accumulator");
+    auto part = torch::empty({(int64_t)S * N * Kone}, opts);
+    TORCH_CHECK(launch_wgrad_onehot(dz.data_ptr<float>(), dz.stride(0), idx->data_ptr<int>(), idx->stride(0), (int)off,
+                                    part.data_ptr<float>(), (int)M, (int)N, (int)G, (int)C, S, st),
+                "wgrad: one-hot launch failed");
+    launch_wgrad_reduce(part.data_ptr<float>(), S, (int)N, (int)Kone, dW.data_ptr<float>(), Kone + Kd, 0, accumulate, st);
+  }
+}
+
 void register_ext(pybind11::module& m) {
   m.def("sac_critic_fwd", &sac_critic_fwd);
   m.def("sac_critic_wgrad", &sac_critic_wgrad);
   m.def("gather_rows", &gather_rows, pybind11::arg("srcs"), pybind11::arg("row"), pybind11::arg("env"),
         pybind11::arg("err") = pybind11::none());
   m.def("onehot_index", &onehot_index);
+  m.def("wgrad", &wgrad, pybind11::arg("dz"), pybind11::arg("x"), pybind11::arg("idx"), pybind11::arg("G"), pybind11::arg("C"),
+        pybind11::arg("off"), pybind11::arg("dW"), pybind11::arg("db"), pybind11::arg("accumulate") = false);
   m.def("onehot_gather_ln", &onehot_gather_ln, pybind11::arg("Y"), pybind11::arg("idx"), pybind11::arg("G"), pybind11::arg("off"),
         pybind11::arg("table"), pybind11::arg("bias"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("eps"),
         pybind11::arg("act"), pybind11::arg("ln"), pybind11::arg("z_out"), pybind11::arg("y_out"), pybind11::arg("mean"),

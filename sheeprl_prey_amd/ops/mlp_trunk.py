@@ -53,6 +53,9 @@ class TrunkRecord:
         self.mean = [torch.empty(rows, M, device=device) for _ in self.layers]
         self.rstd = [torch.empty(rows, M, device=device) for _ in self.layers]
         self.inp: Optional[Tensor] = None  # [R, M, K0] (may be a row-strided view)
+        # (idx [R, M, >= G], G, off, n_onehot) when the first layer's leading inputs are one-hots (gathered
+        # forward): its weight gradient then scatters those columns instead of multiplying them (ops.wgrad)
+        self.onehot = None
 
     @torch.no_grad()
     def step(self, t: int, x: Tensor, gather=None) -> Tensor:
@@ -99,9 +102,17 @@ class TrunkRecord:
             dpre, dg, db = C.ln_act_bwd(pre, dy, ln.weight, ln.bias, self.mean[i].view(RM), self.rstd[i].view(RM),
                                         ops._act_code(ln.act))
             x = self.y[i - 1].view(RM, -1) if i > 0 else self.inp.reshape(RM, self.inp.shape[-1])
-            grads[4 * i] = dpre.t().mm(x) if lin.weight.requires_grad else None
-            if lin.bias is not None and lin.bias.requires_grad:
-                grads[4 * i + 1] = C.colsum(dpre)
+            want_b = lin.bias is not None and lin.bias.requires_grad
+            if lin.weight.requires_grad and ops.wgrad_ok(dpre):
+                oh = self.onehot if i == 0 else None
+                if oh is not None and x.shape[1] > oh[3] and ops.wgrad_onehot_ok(dpre, oh[1], oh[3]):
+                    grads[4 * i], grads[4 * i + 1] = ops.wgrad(dpre, x[:, oh[3]:], onehot=oh, bias=want_b)
+                else:
+                    grads[4 * i], grads[4 * i + 1] = ops.wgrad(dpre, x, bias=want_b)
+            else:
+                grads[4 * i] = dpre.t().mm(x) if lin.weight.requires_grad else None
+                if want_b:
+                    grads[4 * i + 1] = C.colsum(dpre)
             grads[4 * i + 2] = dg if ln.weight.requires_grad else None
             grads[4 * i + 3] = db if ln.bias.requires_grad else None
             if i > 0:

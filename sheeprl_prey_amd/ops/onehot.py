@@ -100,14 +100,14 @@ class _GatherFirstLayer(torch.autograd.Function):
                                 mean, rstd, _err_word(x.device))
         if not ok:
             raise RuntimeError(f"onehot_gather_ln: unsupported layer width {N}")
-        ctx.save_for_backward(x2, W, gamma, beta, z, mean, rstd)
-        ctx.meta = (act, use_ln, bias is not None, x.shape)
+        ctx.save_for_backward(x2, idx2, W, gamma, beta, z, mean, rstd)
+        ctx.meta = (act, use_ln, bias is not None, x.shape, int(G), int(off), int(n_onehot))
         return y.view(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, W, gamma, beta, z, mean, rstd = ctx.saved_tensors
-        act, use_ln, has_bias, xshape = ctx.meta
+        x2, idx2, W, gamma, beta, z, mean, rstd = ctx.saved_tensors
+        act, use_ln, has_bias, xshape, G, off, n_onehot = ctx.meta
         C = ops._ext()
         N = W.shape[0]
         dy2 = dy.reshape(-1, N).contiguous()
@@ -124,9 +124,16 @@ class _GatherFirstLayer(torch.autograd.Function):
         dx = dW = dbias = None
         if ctx.needs_input_grad[0]:
             dx = dz.mm(W).view(xshape)
-        if ctx.needs_input_grad[2]:
+        if ctx.needs_input_grad[2] and ops.wgrad_ok(dz):
+            # one-hot columns scattered, the dense tail by the split-K kernel, the bias sum on the side (wgrad.hip)
+            want_b = has_bias and ctx.needs_input_grad[3]
+            if x2.shape[1] > n_onehot and ops.wgrad_onehot_ok(dz, G, n_onehot):
+                dW, dbias = ops.wgrad(dz, x2[:, n_onehot:], onehot=(idx2, G, off, n_onehot), bias=want_b)
+            else:
+                dW, dbias = ops.wgrad(dz, x2, bias=want_b)
+        elif ctx.needs_input_grad[2]:
             dW = dz.t().mm(x2)  # x2 may be row-strided (a view into the trajectory buffer): mm takes the stride
-        if has_bias and ctx.needs_input_grad[3]:
+        if has_bias and ctx.needs_input_grad[3] and dbias is None:
             dbias = C.colsum(dz)
         return (dx, None, dW, dbias, dg if ctx.needs_input_grad[4] else None, db if ctx.needs_input_grad[5] else None,
                 None, None, None, None, None, None)

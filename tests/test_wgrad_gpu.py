@@ -1,0 +1,119 @@
+"""Tall-layer weight gradients (csrc/wgrad.hip, ops.wgrad) vs fp64 ``dz^T [onehot | x]`` / ``dz.sum(0)``, and
+the 16-byte LayerNorm backward (norm.hip ln_wave4_bwd) vs fp64 autograd - at the DreamerV3 imagination-head
+shapes (16384 / 15360 rows) and at ragged ones."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, scale, tol=2e-6):
+    err = (a.double() - b).abs().max().item()
+    assert err <= tol * scale, f"max err {err:.3e} > {tol * scale:.3e}"
+
+
+@pytest.mark.parametrize("M,N,K,bias,strided", [(16384, 512, 512, True, True), (15360, 255, 512, True, False),
+                                                (16384, 9, 512, True, True), (5003, 100, 70, True, False),
+                                                (4096, 1024, 1536, False, True)])
+def test_wgrad_dense(M, N, K, bias, strided):
+    from sheeprl_prey_amd import ops
+
+    g = torch.Generator(device="cuda").manual_seed(1)
+    dz = torch.randn(M, N, device="cuda", generator=g)
+    if strided:  # a row-strided view, as the trajectory-buffer slices the heads read
+        xb = torch.randn(M, K + 13, device="cuda", generator=g)
+        x = xb[:, 5:5 + K]
+    else:
+        x = torch.randn(M, K, device="cuda", generator=g)
+    dW, db = ops.wgrad(dz, x, bias=bias)
+    ref = dz.double().t() @ x.double()
+    # |error| of an fp32 k-ordered FMA chain ~ 1e-7 * sum|a b| ~ 1e-7 * M (unit-normal operands)
+    _close(dW, ref, M ** 0.5 * 4, tol=2e-6)
+    if bias:
+        _close(db, dz.double().sum(0), M ** 0.5 * 4, tol=2e-6)
+    else:
+        assert db is None
+
+
+@pytest.mark.parametrize("M,N,G,C,Kd,off", [(16384, 512, 32, 32, 512, 9), (15360, 512, 32, 32, 512, 0),
+                                             (3000, 200, 8, 16, 40, 3)])
+def test_wgrad_onehot(M, N, G, C, Kd, off):
+    from sheeprl_prey_amd import ops
+
+    gen = torch.Generator(device="cuda").manual_seed(2)
+    k = torch.randint(0, C, (M, G), device="cuda", generator=gen)
+    z = F.one_hot(k, C).double().view(M, G * C)
+    idx_buf = torch.zeros(M, G + 5, dtype=torch.int32, device="cuda")
+    idx = idx_buf[:, 5:]  # row-strided, as the rollout's IDX[..., nh:] slice
+    idx.copy_((k + torch.arange(G, device="cuda") * C + off).int())
+    x = torch.randn(M, Kd, device="cuda", generator=gen)
+    dz = torch.randn(M, N, device="cuda", generator=gen)
+    dW, db = ops.wgrad(dz, x, onehot=(idx, G, off, G * C), bias=True)
+    ref = dz.double().t() @ torch.cat((z, x.double()), 1)
+    _close(dW, ref, M ** 0.5 * 4, tol=2e-6)
+    _close(db, dz.double().sum(0), M ** 0.5 * 4, tol=2e-6)
+
+
+def test_linear_backward_uses_wgrad_and_matches_torch():
+    from sheeprl_prey_amd import ops
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(16, 1024, 512, device="cuda", generator=g, requires_grad=True)
+    w = torch.randn(255, 512, device="cuda", generator=g, requires_grad=True)
+    b = torch.randn(255, device="cuda", generator=g, requires_grad=True)
+    gy = torch.randn(16, 1024, 255, device="cuda", generator=g)
+    assert ops.wgrad_ok(gy)
+    ops.linear(x, w, b).backward(gy)
+    xd, wd, bd = (t.detach().double().requires_grad_(True) for t in (x, w, b))
+    F.linear(xd, wd, bd).backward(gy.double())
+    _close(w.grad, wd.grad, 128 * 4)
+    _close(b.grad, bd.grad, 128 * 4)
+    _close(x.grad, xd.grad, 16 * 4, tol=5e-6)
+
+
+def test_gather_first_layer_backward_tall():
+    """The one-hot first layer's weight gradient at 16384 rows goes through the scatter + split-K kernels."""
+    from sheeprl_prey_amd.ops import onehot as oh
+    from sheeprl_prey_amd.utils.model import LayerNorm
+
+    gen = torch.Generator(device="cuda").manual_seed(4)
+    M, G, C, Kd, N = 16384, 32, 32, 512, 512
+    S = G * C
+    k = torch.randint(0, C, (M, G), device="cuda", generator=gen)
+    z = F.one_hot(k, C).float().view(M, S)
+    h = torch.randn(M, Kd, device="cuda", generator=gen)
+    x = torch.cat((z, h), 1)
+    lin = torch.nn.Linear(S + Kd, N, bias=True).cuda()
+    norm = LayerNorm(N, eps=1e-3, act="silu").cuda()
+    idx = torch.empty(M, G, dtype=torch.int32, device="cuda")
+    oh.onehot_index(z, C, idx, 0)
+    dy = torch.randn(M, N, device="cuda", generator=gen)
+    y = oh.first_layer(x, idx, G, 0, lin, norm, S)
+    y.backward(dy)
+    W = lin.weight.detach().double().requires_grad_(True)
+    B = lin.bias.detach().double().requires_grad_(True)
+    ref = F.silu(F.layer_norm(F.linear(x.double(), W, B), (N,), norm.weight.double(), norm.bias.double(), 1e-3))
+    ref.backward(dy.double())
+    _close(lin.weight.grad, W.grad, 128 * 4, tol=1e-5)
+    _close(lin.bias.grad, B.grad, 128 * 4, tol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,act", [(16384, 512, "silu"), (1000, 256, "tanh"), (777, 1024, "none"), (300, 36, "silu")])
+def test_ln_act_backward_vec(M, N, act):
+    from sheeprl_prey_amd import ops
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(M, N, device="cuda", generator=g) * 2 + 0.5
+    w = 1 + 0.1 * torch.randn(N, device="cuda", generator=g)
+    b = 0.1 * torch.randn(N, device="cuda", generator=g)
+    dy = torch.randn(M, N, device="cuda", generator=g)
+    xs, ws, bs = (t.clone().requires_grad_(True) for t in (x, w, b))
+    ops.ln_act(xs, ws, bs, 1e-3, act).backward(dy)
+    xd, wd, bd = (t.double().requires_grad_(True) for t in (x, w, b))
+    y = F.layer_norm(xd, (N,), wd, bd, 1e-3)
+    y = {"silu": F.silu, "tanh": torch.tanh, "none": lambda v: v}[act](y)
+    y.backward(dy.double())
+    _close(xs.grad, xd.grad, 1.0, tol=2e-5)
+    _close(ws.grad, wd.grad, M ** 0.5 * 4, tol=5e-6)
+    _close(bs.grad, bd.grad, M ** 0.5 * 4, tol=5e-6)
