@@ -40,6 +40,13 @@ constexpr int BK = 32;        // K per LDS stage
 constexpr int LDK = BK + 4;   // LDS row stride (floats): conflict-free float4 fragment reads
 
 __device__ __forceinline__ f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
+
+// Out-of-range (padding) taps read this zero vector instead of being skipped: the operand loads are then
+// unconditional - an exec-masked load under a branch, or a select on the loaded value, made the wait-count
+// pass put vmcnt(0) in front of the NEXT K stage's loads, so every stage paid a full memory latency before
+// its MFMAs (the prefetch into registers did not overlap anything).
+__device__ __attribute__((aligned(16))) float g_zero16[4];
+__device__ __forceinline__ const float* zsrc(bool ok, const float* p) { return ok ? p : g_zero16; }
 __device__ __forceinline__ float fsig(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float cact(float z, int act) {
   switch (act) {
@@ -115,10 +122,8 @@ struct DownGather {
       for (int v = 0; v < NV; ++v) {
         const int b = b0 + 4 * ((threadIdx.x + NTH * v) & 7);
         const int iy = py[v] + dy, ix = px[v] + dx;
-        f4 val = zero4();
-        if (pix[v] >= 0 && iy >= 0 && iy < LH && ix >= 0 && ix < LW)
-          val = *(const f4*)(Q + ((pix[v] + iy * LW + ix) * Cb + b));  // < 2^31 (host-checked)
-        r[v] = val;
+        const bool ok = pix[v] >= 0 && iy >= 0 && iy < LH && ix >= 0 && ix < LW;
+        r[v] = *(const f4*)zsrc(ok, Q + ((pix[v] + iy * LW + ix) * Cb + b));  // < 2^31 (host-checked)
       }
       return;
     }
@@ -127,10 +132,8 @@ struct DownGather {
       const int k = k0 + 4 * ((threadIdx.x + NTH * v) & 7);
       const int tap = k >> lCb, b = k & (Cb - 1);
       const int iy = py[v] + (tap >> 2), ix = px[v] + (tap & 3);
-      f4 val = zero4();
-      if (pix[v] >= 0 && iy >= 0 && iy < LH && ix >= 0 && ix < LW)
-        val = *(const f4*)(Q + ((size_t)(pix[v] + iy * LW + ix) << lCb) + b);
-      r[v] = val;
+      const bool ok = pix[v] >= 0 && iy >= 0 && iy < LH && ix >= 0 && ix < LW;
+      r[v] = *(const f4*)zsrc(ok, Q + ((size_t)(pix[v] + iy * LW + ix) << lCb) + b);
     }
   }
   __device__ void store(const f4* r, float* s) const {
@@ -170,10 +173,8 @@ struct UpGather {
     for (int v = 0; v < NV; ++v) {
       const int a = a0 + 4 * ((threadIdx.x + NTH * v) & 7);
       const int p = pu[v] - dy, q = pv[v] - dx;
-      f4 val = zero4();
-      if (pix[v] >= 0 && p >= 0 && p < SH && q >= 0 && q < SW)
-        val = *(const f4*)(P + ((pix[v] + p * SW + q) * Ca + a));  // < 2^31 (host-checked)
-      r[v] = val;
+      const bool ok = pix[v] >= 0 && p >= 0 && p < SH && q >= 0 && q < SW;
+      r[v] = *(const f4*)zsrc(ok, P + ((pix[v] + p * SW + q) * Ca + a));  // < 2^31 (host-checked)
     }
   }
   __device__ void store(const f4* r, float* s) const {
@@ -223,7 +224,7 @@ struct WgP {
     for (int v = 0; v < NV; ++v) {
       const int idx = threadIdx.x + NTH * v;
       const int m = k0 + (idx & 31), a = a0 + 4 * (idx >> 5);
-      r[v] = m < M ? *(const f4*)(P + (m * Ca + a)) : zero4();
+      r[v] = *(const f4*)zsrc(m < M, P + (m * Ca + a));
     }
   }
   __device__ void store(const f4* r, float* s) const {
@@ -265,10 +266,8 @@ struct WgQ {
       const int m = k0 + (idx & 31);
       const int n = m >> (lSH + lSW), p = (m >> lSW) & ((1 << lSH) - 1), q = m & ((1 << lSW) - 1);
       const int iy = 2 * p + dy[v], ix = 2 * q + dx[v];
-      f4 val = zero4();
-      if (m < M && iy >= 0 && iy < LH && ix >= 0 && ix < LW)
-        val = *(const f4*)(Q + (((n * LH + iy) * LW + ix) * Cb + bo[v]));
-      r[v] = val;
+      const bool ok = m < M && iy >= 0 && iy < LH && ix >= 0 && ix < LW;
+      r[v] = *(const f4*)zsrc(ok, Q + (((n * LH + iy) * LW + ix) * Cb + bo[v]));
     }
   }
   __device__ void store(const f4* r, float* s) const {

@@ -28,6 +28,13 @@ constexpr int NV = 64 * BK / 4 / NTH;  // float4 slots per thread per operand st
 
 __device__ __forceinline__ f4 z4() { return f4{0.f, 0.f, 0.f, 0.f}; }
 
+// Out-of-range operand slots load this zero vector (unconditional loads, values not selected after the load:
+// either made the wait-count pass wait for the next K stage's loads before the current stage's MFMAs).
+// The ReLU masks are applied when the registers are written to LDS, after the wait that store needs anyway.
+__device__ __attribute__((aligned(16))) float nc_zero16[4];
+__device__ __forceinline__ const float* zsrc(bool ok, const float* p) { return ok ? p : nc_zero16; }
+__device__ __attribute__((aligned(16))) float nc_one16[4] = {1.f, 0.f, 0.f, 0.f};  // the wgrad bias row's first float4
+
 // Conv geometry: x NHWC [Nb][H][W][Ci] -> y NHWC [Nb][OH][OW][Co], kernel KH x KW, stride S.
 struct Geo {
   int Nb, H, W, Ci, OH, OW, Co, KH, KW, S;
@@ -84,7 +91,7 @@ struct LIm2col {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int k = k0 + 4 * ((threadIdx.x + NTH * v) & 7);
-      r[v] = (b[v] >= 0 && k < K) ? *(const f4*)(x + b[v] + g.tap(k)) : z4();
+      r[v] = *(const f4*)zsrc(b[v] >= 0 && k < K, x + b[v] + g.tap(k));
     }
   }
   __device__ void store(const f4* r, float* s) const { store_rows(r, s); }
@@ -101,23 +108,28 @@ struct LRows {
 #pragma unroll
     for (int v = 0; v < NV; ++v) row[v] = r0 + ((threadIdx.x + NTH * v) >> 3);
   }
+  mutable f4 mk[NV];
   __device__ void load(int k0, f4* r) const {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int k = k0 + 4 * ((threadIdx.x + NTH * v) & 7);
-      f4 val = z4();
-      if (row[v] < R && k < K) {
-        val = *(const f4*)(p + (size_t)row[v] * ld + k);
-        if (mask) {
-          const f4 y = *(const f4*)(mask + (size_t)row[v] * ld + k);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) val[e] = y[e] > 0.f ? val[e] : 0.f;
-        }
-      }
-      r[v] = val;
+      const bool ok = row[v] < R && k < K;
+      r[v] = *(const f4*)zsrc(ok, p + (size_t)row[v] * ld + k);
+      if (mask) mk[v] = *(const f4*)zsrc(ok, mask + (size_t)row[v] * ld + k);
     }
   }
-  __device__ void store(const f4* r, float* s) const { store_rows(r, s); }
+  __device__ void store(const f4* r, float* s) const {
+    if (!mask) {
+      store_rows(r, s);
+      return;
+    }
+    f4 m[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[v][e] = mk[v][e] > 0.f ? r[v][e] : 0.f;
+    store_rows(m, s);
+  }
 };
 
 // Transposed dense: GEMM rows j come from columns of p [Kdim][ld] (float4 along j), k-dim = rows of p.
@@ -128,24 +140,29 @@ struct LCols {
   int R, Kd, ld;  // R = GEMM rows (columns of p), Kd = rows of p
   int j0;
   __device__ void init(int r0) { j0 = r0; }
+  mutable f4 mk[NV];
   __device__ void load(int k0, f4* r) const {
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int idx = threadIdx.x + NTH * v;
       const int kk = k0 + (idx & 31), j = j0 + 4 * (idx >> 5);
-      f4 val = z4();
-      if (kk < Kd && j < R) {
-        val = *(const f4*)(p + (size_t)kk * ld + j);
-        if (mask) {
-          const f4 y = *(const f4*)(mask + (size_t)kk * ld + j);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) val[e] = y[e] > 0.f ? val[e] : 0.f;
-        }
-      }
-      r[v] = val;
+      const bool ok = kk < Kd && j < R;
+      r[v] = *(const f4*)zsrc(ok, p + (size_t)kk * ld + j);
+      if (mask) mk[v] = *(const f4*)zsrc(ok, mask + (size_t)kk * ld + j);
     }
   }
-  __device__ void store(const f4* r, float* s) const { store_trans(r, s); }
+  __device__ void store(const f4* r, float* s) const {
+    if (!mask) {
+      store_trans(r, s);
+      return;
+    }
+    f4 m[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[v][e] = mk[v][e] > 0.f ? r[v][e] : 0.f;
+    store_trans(m, s);
+  }
 };
 
 // WGRAD B: GEMM rows j = (kh, kw, ci) (plus row K = the bias: all ones), k-dim = output pixels m;
@@ -160,15 +177,9 @@ struct LIm2colT {
     for (int v = 0; v < NV; ++v) {
       const int idx = threadIdx.x + NTH * v;
       const int m = k0 + (idx & 31), j = j0 + 4 * (idx >> 5);
-      f4 val = z4();
-      if (m < M) {
-        if (j < K) {
-          val = *(const f4*)(x + g.base(m) + g.tap(j));
-        } else if (j == K) {
-          val[0] = 1.f;  // bias row (K % 4 == 0, so j == K starts a float4)
-        }
-      }
-      r[v] = val;
+      // bias row (K % 4 == 0, so j == K starts a float4): (1, 0, 0, 0); past it / past M: zeros
+      const float* src = (m < M && j < K) ? x + g.base(m) + g.tap(j) : ((m < M && j == K) ? nc_one16 : nc_zero16);
+      r[v] = *(const f4*)src;
     }
   }
   __device__ void store(const f4* r, float* s) const { store_trans(r, s); }
