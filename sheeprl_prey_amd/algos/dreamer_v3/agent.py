@@ -289,6 +289,8 @@ class RSSM(nn.Module):
         return imagined_prior, recurrent_state
 
     # ---- MI355X imagination: buffer-resident no-grad rollout ---------------------------
+    _actor_tail_ok = os.environ.get("SRL_ACTOR_TAIL", "1") != "0"  # A/B switch of the fused rollout actor tail
+
     def imagine_fast_ok(self, actor) -> bool:
         gru = self.recurrent_model.rnn
         rec = list(self.recurrent_model.mlp.model)
@@ -361,18 +363,25 @@ class RSSM(nn.Module):
         act_scratch = None
         if trunk_rec is not None and a_table is not None:
             trunk_rec.onehot = (IDX[:, :, nh:], G, A, S)  # the trunk backward scatters the prior columns' dW
+        one_head = nh == 1 and self._actor_tail_ok
         for t in range(horizon + 1):
             traj_t = buf[t, :, Ap:Ap + S + Hd]
+            # single-head actors: last LayerNorm + head + unimix sample in one kernel (TrunkRecord.step tail)
+            tail = ((actor.mlp_heads[0], U[t, :M], float(actor._unimix), buf[t, :, :A], IDX[t, :, :1], 0)
+                    if one_head else None)
             if trunk_rec is not None:
-                out = trunk_rec.step(t, traj_t, gather=(IDX[t, :, nh:], G, A, S, a_table) if a_table is not None else None)
+                out = trunk_rec.step(t, traj_t, gather=(IDX[t, :, nh:], G, A, S, a_table) if a_table is not None else None,
+                                     tail=tail)
             elif layers is not None and a_table is not None:
                 if act_scratch is None:
                     act_scratch = TrunkRecord(layers, 1, M, dev)
-                out = act_scratch.step(0, traj_t, gather=(IDX[t, :, nh:], G, A, S, a_table))
+                out = act_scratch.step(0, traj_t, gather=(IDX[t, :, nh:], G, A, S, a_table), tail=tail)
             else:
                 out = actor.model(traj_t)
             c0 = 0
             for i, (head, a) in enumerate(zip(actor.mlp_heads, actor.actions_dim)):
+                if out is None:
+                    break  # sampled by the fused tail
                 C.unimix_sample_into(head(out), U[t, i * M:(i + 1) * M], int(a), float(actor._unimix), buf[t, :, c0:c0 + a],
                                      IDX[t, :, i:i + 1], c0)
                 c0 += a

@@ -90,6 +90,7 @@ def _lin2d(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
 
 # =============================================================== tall-layer weight gradients (wgrad.hip)
 WGRAD_MIN_ROWS = int(os.environ.get("SRL_WGRAD_MIN_ROWS", "4096"))  # 0 disables (A/B switch)
+WGRAD_MAX_TILES = 32  # dense parts with more 128 x 128 output tiles go to the library GEMM
 
 
 def _rows2d(t: Tensor) -> Tensor:
@@ -132,6 +133,16 @@ def wgrad(dz: Tensor, x: Optional[Tensor] = None, onehot=None, bias: bool = Fals
         idx2 = _rows2d(idx)
         C = n1 // G
     Kd = x2.shape[1] if x2 is not None else 0
+    if x2 is not None and ((N + 127) // 128) * ((Kd + 127) // 128) > WGRAD_MAX_TILES:
+        # a wide output fills the chip with library tiles (XL: 1024 x 1024 over 16384 rows, hipBLASLt 292 us vs
+        # 342 us split-K; 1024 x 4096: 900 vs 1194 us) - the split-K kernel only wins on small N x K
+        dense = dz2.t().mm(x2)
+        db = _ext().colsum(dz2 if dz2.stride(-1) == 1 else dz2.contiguous()) if bias else None
+        if idx2 is None:
+            return dense, db
+        dWo = torch.empty(N, G * C, device=dz.device, dtype=torch.float32)
+        _ext().wgrad(dz2, None, idx2, int(G), int(C), int(off), dWo, None, False)
+        return torch.cat((dWo, dense), 1), db
     dW = torch.empty(N, G * C + Kd, device=dz.device, dtype=torch.float32)
     db = torch.empty(N, device=dz.device, dtype=torch.float32) if bias else None
     _ext().wgrad(dz2, x2, idx2, int(G), int(C), int(off), dW, db, False)

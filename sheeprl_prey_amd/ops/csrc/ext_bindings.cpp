@@ -66,6 +66,11 @@ bool launch_wgrad_onehot(const float* dz, long ldz, const int* idx, long ldi, in
 void launch_wgrad_reduce(const float* part, int S, int N, int K, float* out, long ldo, int coff, bool accumulate,
                          hipStream_t st);
 
+bool launch_actor_tail(const float* pre, long ldp, float* y, long ldy, const float* gamma, const float* beta, float* mean,
+                       float* rstd, float eps, int act, const float* Wh, const float* bh, int A, const float* uniform,
+                       float alpha, float* sample, long lds, int* idx, long ldi, int ioff, float* logits, int M, int N,
+                       hipStream_t st);
+
 void launch_onehot_index(const float* x, int ldx, int M, int G, int C, int* idx, int ldi, int off, hipStream_t st);
 bool launch_onehot_gather_ln(const float* Y, int ldy, const int* idx, int ldi, int G, int off, const float* T, int K,
                              const float* bias, const float* gamma, const float* beta, float eps, int act, int ln,
@@ -636,12 +641,50 @@ void wgrad(torch::Tensor dz, c10::optional<torch::Tensor> x, c10::optional<torch
   }
 }
 
+// ------------------------------------------------------------------ rollout actor tail (actor_tail.hip)
+// y = act(LN(pre)) (+ mean / rstd), logits = y Wh^T + bh, one-hot sample (unimix) into `sample` [M, >= A] and its
+// column (ioff + pick) into idx [M, >= 1]; pre / y / sample / idx row-strided.  false: shape not covered.
+bool actor_tail(torch::Tensor pre, torch::Tensor y, c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta,
+                torch::Tensor mean, torch::Tensor rstd, double eps, int64_t act, torch::Tensor Wh,
+                c10::optional<torch::Tensor> bh, c10::optional<torch::Tensor> uniform, double alpha, torch::Tensor sample,
+                c10::optional<torch::Tensor> idx, int64_t ioff, c10::optional<torch::Tensor> logits) {
+  const int64_t M = pre.size(0), N = pre.size(1), A = Wh.size(0);
+  rowview(pre, "pre", M, N, torch::kFloat32);
+  rowview(y, "y", M, N, torch::kFloat32);
+  rowview(sample, "sample", M, A, torch::kFloat32);
+  TORCH_CHECK(Wh.is_cuda() && Wh.scalar_type() == torch::kFloat32 && Wh.is_contiguous() && Wh.dim() == 2 && Wh.size(1) == N,
+              "actor_tail: Wh [A, N] contiguous float32");
+  TORCH_CHECK(mean.is_cuda() && mean.numel() == M && rstd.is_cuda() && rstd.numel() == M && mean.is_contiguous() &&
+                  rstd.is_contiguous(),
+              "actor_tail: mean / rstd [M]");
+  const float* gp = optf(gamma, "gamma", N);
+  const float* bp = optf(beta, "beta", N);
+  const float* hp = optf(bh, "bh", A);
+  const float* up = optf(uniform, "uniform", M);
+  float* lp = logits.has_value() && logits->defined() ? const_cast<float*>(optf(logits, "logits", M * A)) : nullptr;
+  int* ip = nullptr;
+  int64_t ldi = 0;
+  if (idx.has_value() && idx->defined()) {
+    rowview(*idx, "idx", M, 1, torch::kInt);
+    ip = idx->data_ptr<int>();
+    ldi = idx->stride(0);
+  }
+  return launch_actor_tail(pre.data_ptr<float>(), pre.stride(0), y.data_ptr<float>(), y.stride(0), gp, bp,
+                           mean.data_ptr<float>(), rstd.data_ptr<float>(), (float)eps, (int)act, Wh.data_ptr<float>(), hp,
+                           (int)A, up, (float)alpha, sample.data_ptr<float>(), sample.stride(0), ip, ldi, (int)ioff, lp,
+                           (int)M, (int)N, stream());
+}
+
 void register_ext(pybind11::module& m) {
   m.def("sac_critic_fwd", &sac_critic_fwd);
   m.def("sac_critic_wgrad", &sac_critic_wgrad);
   m.def("gather_rows", &gather_rows, pybind11::arg("srcs"), pybind11::arg("row"), pybind11::arg("env"),
         pybind11::arg("err") = pybind11::none());
   m.def("onehot_index", &onehot_index);
+  m.def("actor_tail", &actor_tail, pybind11::arg("pre"), pybind11::arg("y"), pybind11::arg("gamma"), pybind11::arg("beta"),
+        pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("eps"), pybind11::arg("act"), pybind11::arg("Wh"),
+        pybind11::arg("bh"), pybind11::arg("uniform"), pybind11::arg("alpha"), pybind11::arg("sample"), pybind11::arg("idx"),
+        pybind11::arg("ioff"), pybind11::arg("logits") = pybind11::none());
   m.def("wgrad", &wgrad, pybind11::arg("dz"), pybind11::arg("x"), pybind11::arg("idx"), pybind11::arg("G"), pybind11::arg("C"),
         pybind11::arg("off"), pybind11::arg("dW"), pybind11::arg("db"), pybind11::arg("accumulate") = false);
   m.def("onehot_gather_ln", &onehot_gather_ln, pybind11::arg("Y"), pybind11::arg("idx"), pybind11::arg("G"), pybind11::arg("off"),

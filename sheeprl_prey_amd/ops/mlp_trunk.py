@@ -58,11 +58,14 @@ class TrunkRecord:
         self.onehot = None
 
     @torch.no_grad()
-    def step(self, t: int, x: Tensor, gather=None) -> Tensor:
+    def step(self, t: int, x: Tensor, gather=None, tail=None) -> Optional[Tensor]:
         """Forward of step ``t`` on ``x`` [M, K0] (row stride allowed); returns the trunk output [M, N].
         ``gather`` = (idx, G, off, n_onehot, table): the first ``n_onehot`` input columns are one-hot with hot
         columns ``idx - off`` - the first layer is then a GEMM over the dense columns plus a row gather of
-        ``table`` (its transposed one-hot weight columns) with the LayerNorm fused (``ops/onehot.py``)."""
+        ``table`` (its transposed one-hot weight columns) with the LayerNorm fused (``ops/onehot.py``).
+        ``tail`` = (head Linear, uniforms [M], unimix, sample_out, idx_out, idx_off): the last LayerNorm, the head
+        and the unimix one-hot sample run as one kernel (``csrc/actor_tail.hip``); returns None when it did (the
+        sample is in ``sample_out``), else the trunk output as without ``tail``."""
         C = ops._ext()
         M = self.M
         for i, (lin, ln) in enumerate(self.layers):
@@ -80,6 +83,13 @@ class TrunkRecord:
             else:
                 torch.mm(x, lin.weight.t(), out=pre)
             N = pre.shape[-1]
+            if tail is not None and i == len(self.layers) - 1:
+                # the last LayerNorm + the actor head + the unimix sample as one launch (csrc/actor_tail.hip)
+                head, uni, alpha, sample_out, idx_out, ioff = tail
+                if C.actor_tail(pre, self.y[i][t], ln.weight, ln.bias, self.mean[i][t], self.rstd[i][t], float(ln.eps),
+                                ops._act_code(ln.act), head.weight, head.bias, uni, float(alpha), sample_out, idx_out,
+                                int(ioff)):
+                    return None
             C.ln_act_fwd_into(pre, N, self.y[i][t], N, ln.weight, ln.bias, self.mean[i][t], self.rstd[i][t], M, N, 1,
                               float(ln.eps), ops._act_code(ln.act))
             x = self.y[i][t]

@@ -28,8 +28,9 @@ def test_wgrad_dense(M, N, K, bias, strided):
         x = torch.randn(M, K, device="cuda", generator=g)
     dW, db = ops.wgrad(dz, x, bias=bias)
     ref = dz.double().t() @ x.double()
-    # |error| of an fp32 k-ordered FMA chain ~ 1e-7 * sum|a b| ~ 1e-7 * M (unit-normal operands)
-    _close(dW, ref, M ** 0.5 * 4, tol=2e-6)
+    # |error| of an fp32 k-ordered FMA chain <~ 1.5e-7 * sum|a b| ~ 1e-7 * M (unit-normal operands): the split-K
+    # kernel's chunked sums stay well inside; the wide shapes go to the library (one chain over M)
+    _close(dW, ref, M, tol=3e-7)
     if bias:
         _close(db, dz.double().sum(0), M ** 0.5 * 4, tol=2e-6)
     else:
@@ -51,7 +52,7 @@ def test_wgrad_onehot(M, N, G, C, Kd, off):
     dz = torch.randn(M, N, device="cuda", generator=gen)
     dW, db = ops.wgrad(dz, x, onehot=(idx, G, off, G * C), bias=True)
     ref = dz.double().t() @ torch.cat((z, x.double()), 1)
-    _close(dW, ref, M ** 0.5 * 4, tol=2e-6)
+    _close(dW, ref, M, tol=3e-7)
     _close(db, dz.double().sum(0), M ** 0.5 * 4, tol=2e-6)
 
 
@@ -117,3 +118,21 @@ def test_ln_act_backward_vec(M, N, act):
     _close(xs.grad, xd.grad, 1.0, tol=2e-5)
     _close(ws.grad, wd.grad, M ** 0.5 * 4, tol=5e-6)
     _close(bs.grad, bd.grad, M ** 0.5 * 4, tol=5e-6)
+
+
+def test_wgrad_wide_dense_goes_to_library_with_onehot():
+    """XL-like widths: the dense part takes the library path, the one-hot part the scatter kernel."""
+    from sheeprl_prey_amd import ops
+
+    gen = torch.Generator(device="cuda").manual_seed(6)
+    M, N, G, C, Kd = 4096, 1024, 32, 32, 2048
+    k = torch.randint(0, C, (M, G), device="cuda", generator=gen)
+    z = F.one_hot(k, C).double().view(M, G * C)
+    idx = (k + torch.arange(G, device="cuda") * C).int()
+    x = torch.randn(M, Kd, device="cuda", generator=gen)
+    dz = torch.randn(M, N, device="cuda", generator=gen)
+    assert ((N + 127) // 128) * ((Kd + 127) // 128) > ops.WGRAD_MAX_TILES
+    dW, db = ops.wgrad(dz, x, onehot=(idx, G, 0, G * C), bias=True)
+    ref = dz.double().t() @ torch.cat((z, x.double()), 1)
+    _close(dW, ref, M, tol=3e-7)
+    _close(db, dz.double().sum(0), M ** 0.5 * 4, tol=2e-6)
