@@ -35,12 +35,22 @@ struct TP {
   float eps, alpha;
 };
 
-template <int NV4, int ACTC>
+template <int NV4, int AMAX, int ACTC>
 __global__ void __launch_bounds__(256) tail_kernel(TP p) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= p.M) return;  // whole wave
   const int N4 = p.N >> 2;
+  // the head rows are requested first (unconditional loads, rows past A clamped to A - 1: their dot products are
+  // dropped), so their latency overlaps the row's load and the LayerNorm instead of 9 serial round trips (the
+  // first version waited on each head row in turn: 11.8 us per step at M = 1024)
+  float4 wv[AMAX][NV4];
+#pragma unroll
+  for (int a = 0; a < AMAX; ++a) {
+    const float4* wr = reinterpret_cast<const float4*>(p.Wh + (long)min(a, p.A - 1) * p.N);
+#pragma unroll
+    for (int k = 0; k < NV4; ++k) wv[a][k] = wr[min(lane + 64 * k, N4 - 1)];
+  }
   const float4* xr = reinterpret_cast<const float4*>(p.pre + (long)r * p.ldp);
   float4 v[NV4];
   float s = 0.f;
@@ -82,19 +92,20 @@ __global__ void __launch_bounds__(256) tail_kernel(TP p) {
   }
   // head: lane a (< A) ends up holding l[a]
   float la = -INFINITY;
-  for (int a = 0; a < p.A; ++a) {
-    const float4* wr = reinterpret_cast<const float4*>(p.Wh + (long)a * p.N);
-    float d = 0.f;
 #pragma unroll
-    for (int k = 0; k < NV4; ++k) {
-      const int i4 = lane + 64 * k;
-      if (i4 < N4) {
-        const float4 w = wr[i4];
-        d += (v[k].x * w.x + v[k].y * w.y) + (v[k].z * w.z + v[k].w * w.w);
+  for (int a = 0; a < AMAX; ++a) {
+    if (a < p.A) {  // wave-uniform
+      float d = 0.f;
+#pragma unroll
+      for (int k = 0; k < NV4; ++k) {
+        if (lane + 64 * k < N4) {
+          const float4 w = wv[a][k];
+          d += (v[k].x * w.x + v[k].y * w.y) + (v[k].z * w.z + v[k].w * w.w);
+        }
       }
+      const float l = wave_sum_dpp(d) + (p.bh ? p.bh[a] : 0.f);
+      if (lane == a) la = l;
     }
-    const float l = wave_sum_dpp(d) + (p.bh ? p.bh[a] : 0.f);
-    if (lane == a) la = l;
   }
   // unimix sample on lanes 0..15 (segment width 16 >= A): dist.hip unimix_sample_fwd_kernel's arithmetic
   constexpr int W = 16;
@@ -182,12 +193,12 @@ bool launch_actor_tail(const float* pre, long ldp, float* y, long ldy, const flo
   p.alpha = alpha;
   const int nv4 = cdiv(N / 4, 64);
   const dim3 grid(cdiv(M, 4));
-#define F(NV)                                                                                              \
-  if (nv4 <= NV) {                                                                                         \
-    SRL_ACT_SPECIALIZE(act, hipLaunchKernelGGL((atail::tail_kernel<NV, ACTC>), grid, dim3(256), 0, st, p)); \
-    return true;                                                                                           \
+#define F(NV, AM)                                                                                              \
+  if (nv4 <= NV && A <= AM) {                                                                                  \
+    SRL_ACT_SPECIALIZE(act, hipLaunchKernelGGL((atail::tail_kernel<NV, AM, ACTC>), grid, dim3(256), 0, st, p)); \
+    return true;                                                                                               \
   }
-  F(1) F(2) F(4)
+  F(1, 8) F(1, 16) F(2, 8) F(2, 16) F(4, 4) F(4, 8)  // N > 512 with A > 8: too many head registers
 #undef F
   return false;
 }

@@ -7,7 +7,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("M,N,A,sample", [(1024, 512, 9, True), (300, 256, 16, True), (77, 1024, 4, False)])
+@pytest.mark.parametrize("M,N,A,sample", [(1024, 512, 9, True), (300, 256, 16, True), (77, 1024, 4, False), (64, 512, 16, True)])
 def test_actor_tail_matches_unfused(M, N, A, sample):
     from sheeprl_prey_amd import ops
 
