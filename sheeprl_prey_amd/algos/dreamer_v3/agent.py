@@ -585,6 +585,15 @@ class Actor(nn.Module):
             actions.append(st)
         return tuple(actions), tuple(dists)
 
+    def sample_actions(self, state: Tensor, is_training: bool = True) -> Tuple[Tensor, ...]:
+        """The actions of ``forward`` without building the distributions (discrete: their logits normalisation
+        is ~10 kernels per env step the player never reads)."""
+        if self.is_continuous:
+            return self.forward(state, is_training)[0]
+        out = self.model(state)
+        return tuple(ops.unimix_sample(head(out), head.out_features, self._unimix, sample=is_training)[1]
+                     for head in self.mlp_heads)
+
     def _uniform_mix(self, logits: Tensor) -> Tensor:
         return ops.reference.unimix_logits(logits, logits.shape[-1], self._unimix)
 
@@ -664,21 +673,40 @@ class PlayerDV3(nn.Module):
 
     def get_exploration_action(self, obs: Dict[str, Tensor], is_continuous: bool, mask=None) -> Tuple[Tensor, ...]:
         if self.use_graphs and mask is None and torch.cuda.is_available() and self.actions.is_cuda:
+            # two captures: with the exploration ops (amount > 0: a device scalar the graph reads, so a decaying
+            # amount needs no re-capture) and without them (amount == 0, the DreamerV3 default: the random
+            # one-hot / where kernels would be identities)
+            explore = float(self.expl_amount) > 0.0
             if self._graphed is None:
+                self._graphed = {}
+            if explore not in self._graphed:
                 from sheeprl_prey_amd.parallel.graphs import GraphedStep
 
                 self._is_continuous = is_continuous
-                self._expl_t = torch.zeros((), device=self.actions.device)
-                self._graphed = GraphedStep(self._graph_step, warmup=2, enabled=True, name="dv3_player")
-            self._expl_t.fill_(float(self.expl_amount))  # decayed amount: a device scalar the graph reads
-            out = self._graphed(obs)
+                if not hasattr(self, "_expl_t"):
+                    self._expl_t = torch.zeros((), device=self.actions.device)
+                fn = self._graph_step if explore else self._graph_step_greedy
+                self._graphed[explore] = GraphedStep(fn, warmup=2, enabled=True,
+                                                     name="dv3_player" if explore else "dv3_player_greedy")
+            if explore:
+                self._expl_t.fill_(float(self.expl_amount))
+            out = self._graphed[explore](obs)
             return tuple(out[f"a{i}"] for i in range(len(out)))
         return self._exploration_action(obs, is_continuous, mask)
 
     @torch.no_grad()
-    def _graph_step(self, obs: Dict[str, Tensor]) -> Dict[str, Tensor]:
+    def _graph_step_greedy(self, obs: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        return self._graph_step(obs, explore=False)
+
+    @torch.no_grad()
+    def _graph_step(self, obs: Dict[str, Tensor], explore: bool = True) -> Dict[str, Tensor]:
         bufs = (self.actions, self.recurrent_state, self.stochastic_state)
-        acts = self._exploration_action(obs, self._is_continuous, None, expl=self._expl_t)
+        if explore:
+            acts = self._exploration_action(obs, self._is_continuous, None, expl=self._expl_t)
+        else:
+            acts = self.get_greedy_action(obs)
+            if self._is_continuous:
+                acts = (torch.cat(acts, -1),)
         for b, new in zip(bufs, (self.actions, self.recurrent_state, self.stochastic_state)):
             b.copy_(new)
         self.actions, self.recurrent_state, self.stochastic_state = bufs
@@ -711,7 +739,11 @@ class PlayerDV3(nn.Module):
         self.recurrent_state = self.rssm.recurrent_model(torch.cat((self.stochastic_state, self.actions), -1), self.recurrent_state)
         _, self.stochastic_state = self.rssm._representation(self.recurrent_state, embedded_obs)
         self.stochastic_state = self.stochastic_state.view(*self.stochastic_state.shape[:-2], self.stochastic_size * self.discrete_size)
-        actions, _ = self.actor(torch.cat((self.stochastic_state, self.recurrent_state), -1), is_training, mask)
+        latent = torch.cat((self.stochastic_state, self.recurrent_state), -1)
+        if type(self.actor) is Actor and mask is None:
+            actions = self.actor.sample_actions(latent, is_training)
+        else:
+            actions, _ = self.actor(latent, is_training, mask)
         self.actions = torch.cat(actions, -1)
         return actions
 

@@ -226,8 +226,18 @@ def test_player_graphed_steps_and_resets():
         a = acts[0]
         assert a.shape == (1, 3, 5)
         assert torch.all(a.sum(-1) == 1)
-    assert player._graphed is not None and player._graphed.graph is not None
+    # expl_amount 0: the capture without the exploration ops
+    assert set(player._graphed) == {False} and player._graphed[False].graph is not None
     assert player.recurrent_state.data_ptr() == buf_ptr, "state must stay in the captured buffers"
+    # a nonzero amount switches to the exploring capture over the same state buffers
+    player.expl_amount = 0.5
+    for _ in range(4):
+        obs = {"rgb": torch.rand(1, 3, 3, 64, 64, device="cuda")}
+        a = player.get_exploration_action(obs, False)[0]
+        assert a.shape == (1, 3, 5) and torch.all(a.sum(-1) == 1)
+    assert set(player._graphed) == {False, True} and player._graphed[True].graph is not None
+    assert player.recurrent_state.data_ptr() == buf_ptr
+    player.expl_amount = 0.0
     assert not torch.equal(player.recurrent_state, h0)
     player.init_states([1])
     torch.testing.assert_close(player.recurrent_state[:, 1], h0[:, 1])
