@@ -155,8 +155,14 @@ def main():
 
     def train_once():
         nonlocal grad_steps
-        data = rb.sample(cfg.per_rank_batch_size, sequence_length=cfg.per_rank_sequence_length, n_samples=1)
         trainer.update_target(1.0 if grad_steps == 0 else cfg.algo.critic.tau)
+        if not args.eager_ops and not args.check_finite:
+            # captured step: the sample is drawn into the graph's inputs by one launch (dreamer_v3.main does the same)
+            out = trainer.train_step_sampled(rb, cfg.per_rank_batch_size, cfg.per_rank_sequence_length)
+            if out is not None:
+                grad_steps += 1
+                return out
+        data = rb.sample(cfg.per_rank_batch_size, sequence_length=cfg.per_rank_sequence_length, n_samples=1)
         batch = {k: (v[0] if v.dtype == torch.uint8 else v[0].float()) for k, v in data.items()}
         last_batch[0] = batch
         out = trainer.train_step(batch)

@@ -139,6 +139,18 @@ class DreamerV3Trainer:
             return self.seg(data)
         return self.graphed(data)
 
+    def train_step_sampled(self, rb, batch_size: int, sequence_length: int):
+        """Once the single-graph step is captured: the replay sample is drawn straight into the graph's static
+        inputs by one device launch (``sample_into``) and the step replayed - None (caller samples + calls
+        ``train_step``) otherwise."""
+        g = self.graphed
+        if (self.segmented or g.graph is None or g.static_in is None or not hasattr(rb, "sample_into")
+                or os.environ.get("SRL_FUSED_SAMPLE", "1") == "0"):
+            return None
+        if not rb.sample_into(g.static_in, batch_size, sequence_length):
+            return None
+        return g.replay_static()
+
     def _full_step(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:
         self._phase_wm(data)
         self._coll_wm()
@@ -553,10 +565,26 @@ def main(runner, cfg: Dict[str, Any]):
         t0 = time.perf_counter()
         if ev:
             ev[0].record()
+        if n_samples == 1 and device.type == "cuda":
+            if per_rank_gradient_steps % cfg.algo.critic.target_network_update_freq == 0:
+                trainer.update_target(1.0 if per_rank_gradient_steps == 0 else cfg.algo.critic.tau)
+            metrics = trainer.train_step_sampled(rb, cfg.per_rank_batch_size, cfg.per_rank_sequence_length)
+            if metrics is not None:
+                for k, v in metrics.items():
+                    aggregator.update(k, v)
+                per_rank_gradient_steps += 1
+                if ev:
+                    ev[1].record()
+                    train_events.append(ev)
+                return
+            # not captured yet: the target update above already ran for this step
+            n_target_done = 1
+        else:
+            n_target_done = 0
         local_data = rb.sample(cfg.per_rank_batch_size, sequence_length=cfg.per_rank_sequence_length, n_samples=n_samples)
         local_data = local_data.to(device)
         for i in range(n_samples):
-            if per_rank_gradient_steps % cfg.algo.critic.target_network_update_freq == 0:
+            if per_rank_gradient_steps % cfg.algo.critic.target_network_update_freq == 0 and not (i == 0 and n_target_done):
                 trainer.update_target(1.0 if per_rank_gradient_steps == 0 else cfg.algo.critic.tau)
             batch = {k: v[i].float() if v.dtype != torch.uint8 else v[i] for k, v in local_data.items()}
             metrics = trainer.train_step(batch)

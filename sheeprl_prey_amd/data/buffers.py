@@ -298,6 +298,34 @@ class SequentialReplayBuffer(ReplayBuffer):
         sample = self._get_samples(idxes).reshape(n_samples, batch_size, sequence_length).permute(0, 2, 1)
         return sample.clone() if clone else sample
 
+    def sample_into(self, out: Dict[str, Tensor], batch_size: int, sequence_length: int) -> bool:
+        """``sample(batch_size, sequence_length=...)[0]`` written straight into the preallocated contiguous
+        ``out[k]`` [sequence_length, batch_size, ...] (e.g. a graphed train step's static inputs) by ONE device
+        launch (``gather.hip`` seq_sample_kernel): the start rows and envs are drawn on the device - same
+        distribution as ``sample``, a counter-based generator seeded from torch's - so the host does not issue the
+        ~15 small ops of the index draw, gather and copy-in.  False (nothing written) when not applicable."""
+        if self._buf is None or not ops.fused_enabled() or set(out) != set(self._buf.keys()):
+            return False
+        dev = self._first_device()
+        if dev.type != "cuda" or sequence_length < 1:
+            return False
+        if not self._full and self._pos - sequence_length + 1 < 1:
+            raise ValueError(f"too long sequence length ({sequence_length})")
+        if self._full:
+            first_end = self._pos - sequence_length + 1
+            second_end = self.buffer_size if first_end >= 0 else self.buffer_size + first_end
+            n1, start2, n2 = max(first_end, 0), self._pos, max(second_end - self._pos, 0)
+        else:
+            n1, start2, n2 = self._pos - sequence_length + 1, 0, 0
+        if not hasattr(self, "_draw_seed"):
+            self._draw_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            self._draw_counter = 0
+        keys = list(self._buf.keys())
+        self._draw_counter += 1
+        return bool(ops._ext().seq_sample_into([self._buf[k] for k in keys], [out[k] for k in keys], int(batch_size),
+                                               int(sequence_length), int(n1), int(start2), int(n2), self._draw_seed,
+                                               self._draw_counter))
+
     def _get_samples(self, batch_idxes: Tensor, sample_next_obs: bool = False) -> TensorDict:
         shape = batch_idxes.shape
         env_idxes = torch.randint(0, self.n_envs, size=(shape[0],), device=batch_idxes.device).view(-1, 1).expand(shape)
@@ -577,6 +605,12 @@ class AsyncReplayBuffer:
         if len(samples) == 1:  # one env buffer drew everything: no concatenation copy
             return samples[0]
         return cat(samples, dim=2 if self._sequential else 0)
+
+    def sample_into(self, out: Dict[str, Tensor], batch_size: int, sequence_length: int) -> bool:
+        """One env buffer: its fused device-side sample into ``out`` (``SequentialReplayBuffer.sample_into``)."""
+        if self._buf is None or self._n_envs != 1 or not self._sequential:
+            return False
+        return self._buf[0].sample_into(out, batch_size, sequence_length)
 
     def state_dict(self) -> Dict:
         return {"buffers": [] if self._buf is None else [b.state_dict() for b in self._buf], "n_envs": self._n_envs,

@@ -71,6 +71,10 @@ bool launch_actor_tail(const float* pre, long ldp, float* y, long ldy, const flo
                        float alpha, float* sample, long lds, int* idx, long ldi, int ioff, float* logits, int M, int N,
                        hipStream_t st);
 
+bool launch_seq_sample(const void* const* src, void* const* dst, const long* row_bytes, int nk, int n_envs, long cap, int B,
+                       int L, long n1, long start2, long n2, unsigned long long seed, unsigned long long counter,
+                       hipStream_t st);
+
 void launch_onehot_index(const float* x, int ldx, int M, int G, int C, int* idx, int ldi, int off, hipStream_t st);
 bool launch_onehot_gather_ln(const float* Y, int ldy, const int* idx, int ldi, int G, int off, const float* T, int K,
                              const float* bias, const float* gamma, const float* beta, float eps, int act, int ln,
@@ -675,12 +679,39 @@ bool actor_tail(torch::Tensor pre, torch::Tensor y, c10::optional<torch::Tensor>
                            (int)M, (int)N, stream());
 }
 
+// Fused replay sequence sample into preallocated [L, B, ...] outputs (gather.hip seq_sample_kernel): srcs are
+// the store's keys [cap, n_envs, ...]; starts uniform over [0, n1) U [start2, start2 + n2), envs uniform.
+bool seq_sample_into(std::vector<torch::Tensor> srcs, std::vector<torch::Tensor> dsts, int64_t B, int64_t L, int64_t n1,
+                     int64_t start2, int64_t n2, int64_t seed, int64_t counter) {
+  TORCH_CHECK(srcs.size() == dsts.size() && !srcs.empty() && srcs.size() <= 16, "seq_sample_into: 1..16 matching keys");
+  const int64_t cap = srcs[0].size(0), n_envs = srcs[0].size(1);
+  std::vector<const void*> sp;
+  std::vector<void*> dp;
+  std::vector<long> rb;
+  for (size_t k = 0; k < srcs.size(); ++k) {
+    const auto& s = srcs[k];
+    const auto& d = dsts[k];
+    TORCH_CHECK(s.is_cuda() && s.is_contiguous() && s.dim() >= 2 && s.size(0) == cap && s.size(1) == n_envs,
+                "seq_sample_into: every store key [cap, n_envs, ...] contiguous");
+    TORCH_CHECK(d.is_cuda() && d.is_contiguous() && d.dim() == s.dim() && d.size(0) == L && d.size(1) == B &&
+                    d.scalar_type() == s.scalar_type(),
+                "seq_sample_into: every output [L, B, ...] contiguous with the store's dtype");
+    for (int64_t i = 2; i < s.dim(); ++i) TORCH_CHECK(d.size(i) == s.size(i), "seq_sample_into: feature dims differ");
+    sp.push_back(s.data_ptr());
+    dp.push_back(d.data_ptr());
+    rb.push_back((long)(s.numel() / (cap * n_envs) * s.element_size()));
+  }
+  return launch_seq_sample(sp.data(), dp.data(), rb.data(), (int)srcs.size(), (int)n_envs, (long)cap, (int)B, (int)L,
+                           (long)n1, (long)start2, (long)n2, (unsigned long long)seed, (unsigned long long)counter, stream());
+}
+
 void register_ext(pybind11::module& m) {
   m.def("sac_critic_fwd", &sac_critic_fwd);
   m.def("sac_critic_wgrad", &sac_critic_wgrad);
   m.def("gather_rows", &gather_rows, pybind11::arg("srcs"), pybind11::arg("row"), pybind11::arg("env"),
         pybind11::arg("err") = pybind11::none());
   m.def("onehot_index", &onehot_index);
+  m.def("seq_sample_into", &seq_sample_into);
   m.def("actor_tail", &actor_tail, pybind11::arg("pre"), pybind11::arg("y"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("eps"), pybind11::arg("act"), pybind11::arg("Wh"),
         pybind11::arg("bh"), pybind11::arg("uniform"), pybind11::arg("alpha"), pybind11::arg("sample"), pybind11::arg("idx"),

@@ -47,8 +47,86 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GP p) {
   }
 }
 
+// Fused sequence sample (SequentialReplayBuffer.sample + the copy into a graph's static inputs): the start
+// row of sample b is drawn on the device - uniform over the valid starts [0, n1) U [start2, start2 + n2) - and
+// its env uniform over [0, n_envs), from a counter-based hash (splitmix64 of seed, call counter, b), so the
+// host issues ONE launch per gradient step instead of ~15 small ATen ops (index draw, arange, modulo, gather,
+// copy-in) - the host, not the GPU, bounds that part of the env-interaction step.  Output row (t, b) lands at
+// dst[k] + (t * B + b) * row_bytes: the [T, B] layout the train step reads.
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ long uniform_below(unsigned long long h, long n) {
+  // 53 random bits -> [0, n)
+  const double u = (double)(h >> 11) * (1.0 / 9007199254740992.0);
+  long v = (long)(u * (double)n);
+  return v < n ? v : n - 1;
+}
+
+struct SP {
+  const unsigned char* src[MAXK];
+  unsigned char* dst[MAXK];
+  long row_bytes[MAXK];
+  int nk, n_envs, B, L;
+  long cap, n1, start2, n2;
+  unsigned long long seed, counter;
+};
+
+__global__ __launch_bounds__(256) void seq_sample_kernel(SP p) {
+  const int n = blockIdx.x, k = blockIdx.y;
+  if (k >= p.nk || n >= p.B * p.L) return;
+  const int t = n / p.B, b = n - t * p.B;
+  const unsigned long long h0 = splitmix64(p.seed ^ splitmix64(p.counter * 0x100000001B3ull + (unsigned long long)b));
+  const long kk = uniform_below(h0, p.n1 + p.n2);
+  const long start = kk < p.n1 ? kk : p.start2 + (kk - p.n1);
+  const long ei = p.n_envs > 1 ? uniform_below(splitmix64(h0), p.n_envs) : 0;
+  long ri = (start + t) % p.cap;
+  const long rb = p.row_bytes[k];
+  const unsigned char* s = p.src[k] + (ri * p.n_envs + ei) * rb;
+  unsigned char* d = p.dst[k] + (long)n * rb;
+  if ((rb & 15) == 0 && (reinterpret_cast<uintptr_t>(s) & 15) == 0 && (reinterpret_cast<uintptr_t>(d) & 15) == 0) {
+    const long n16 = rb >> 4;
+    for (long i = threadIdx.x; i < n16; i += 256) reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
+  } else if ((rb & 3) == 0 && (reinterpret_cast<uintptr_t>(s) & 3) == 0 && (reinterpret_cast<uintptr_t>(d) & 3) == 0) {
+    const long n4 = rb >> 2;
+    for (long i = threadIdx.x; i < n4; i += 256) reinterpret_cast<unsigned*>(d)[i] = reinterpret_cast<const unsigned*>(s)[i];
+  } else {
+    for (long i = threadIdx.x; i < rb; i += 256) d[i] = s[i];
+  }
+}
+
 }  // namespace gather
 }  // namespace srl
+
+bool launch_seq_sample(const void* const* src, void* const* dst, const long* row_bytes, int nk, int n_envs, long cap, int B,
+                       int L, long n1, long start2, long n2, unsigned long long seed, unsigned long long counter,
+                       hipStream_t st) {
+  if (nk < 1 || nk > srl::gather::MAXK || B < 1 || L < 1 || n1 + n2 < 1 || n1 < 0 || n2 < 0 || start2 < 0 ||
+      start2 + n2 > cap || n1 > cap)
+    return false;
+  srl::gather::SP p{};
+  p.nk = nk;
+  for (int k = 0; k < nk; ++k) {
+    p.src[k] = static_cast<const unsigned char*>(src[k]);
+    p.dst[k] = static_cast<unsigned char*>(dst[k]);
+    p.row_bytes[k] = row_bytes[k];
+  }
+  p.n_envs = n_envs;
+  p.cap = cap;
+  p.B = B;
+  p.L = L;
+  p.n1 = n1;
+  p.start2 = start2;
+  p.n2 = n2;
+  p.seed = seed;
+  p.counter = counter;
+  hipLaunchKernelGGL(srl::gather::seq_sample_kernel, dim3(B * L, nk), dim3(256), 0, st, p);
+  return true;
+}
 
 void launch_gather_rows(const void* const* src, void* const* dst, const long* row_bytes, int nk, int n_envs, long cap, int N,
                         const long* row, const long* env, int* err, hipStream_t st) {

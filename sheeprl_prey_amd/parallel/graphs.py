@@ -34,6 +34,14 @@ class GraphedStep:
         for k, v in data.items():
             self.static_in[k].copy_(v, non_blocking=v.device.type != "cpu" or v.is_pinned())
 
+    def replay_static(self) -> Optional[Dict[str, Tensor]]:
+        """Replay the captured step on whatever the caller wrote into ``static_in`` (no copy-in); None before
+        the capture."""
+        if self.graph is None:
+            return None
+        self.graph.replay()
+        return self.static_out
+
     def __call__(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:
         if not self.enabled:
             return self.fn(data)
