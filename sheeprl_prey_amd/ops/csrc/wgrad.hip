@@ -16,6 +16,8 @@
 //    owns one group and 256 output rows and adds every dZ row into the register of its hot class.
 //  * both write per-chunk partials [S, N, Kpart]; a reduce kernel sums them in chunk order into the output
 //    (deterministic: fixed chunk split, fixed in-chunk order).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace srl {
@@ -471,9 +473,15 @@ using namespace srl;
 
 // Chunks for the dense split: ~2 workgroups per CU over the output tiles, chunks of >= 256 rows, a
 // multiple of 16 rows (one register batch).
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
 int wgrad_dense_chunks(int M, int N, int K) {
   const int tiles = cdiv(N, wgrad::BT) * cdiv(K, wgrad::BT);
-  int S = cdiv(512, tiles);
+  static const int target = env_int("SRL_WGRAD_WGS", 512);  // tuning knob (scripts/wgrad_timing.py)
+  int S = cdiv(target, tiles);
   const int maxS = cdiv(M, 256);
   if (S > maxS) S = maxS;
   if (S < 1) S = 1;
@@ -522,7 +530,8 @@ void launch_wgrad_dense(const float* dz, long ldz, const float* x, long ldx, flo
 int wgrad_onehot_chunks(int M, int N, int G, int C) {
   if (C > wgrad::OH_CMAX || C < 1 || (N & 1)) return 0;
   const int blocks = cdiv(N, wgrad::OH_COLS) * cdiv(G, wgrad::OH_WAVES);
-  int S = cdiv(256, blocks);  // one 133 KB-LDS workgroup per CU
+  static const int target = env_int("SRL_WGRAD_OH_WGS", 256);  // tuning knob
+  int S = cdiv(target, blocks);  // one 133 KB-LDS workgroup per CU
   const int maxS = cdiv(M, 256);
   if (S > maxS) S = maxS;
   if (S < 1) S = 1;
