@@ -13,7 +13,7 @@
 //  * one-hot part: the first-layer inputs of the heads are [z | h] with z the exact one-hot sample of G
 //    categoricals; their dW columns are sums of dZ rows (dW[:, t] = sum_{m : t hot in row m} dZ[m, :]).  As a
 //    dense GEMM that is 2/3 of the layer's weight-gradient FLOPs (K 1536 of which 1024 one-hot); here each wave
-//    owns one group and 256 output rows and adds every dZ row into the register of its hot class.
+//    owns one group and 128 output rows and adds every dZ row into the LDS table row of its hot class.
 //  * both write per-chunk partials [S, N, Kpart]; a reduce kernel sums them in chunk order into the output
 //    (deterministic: fixed chunk split, fixed in-chunk order).
 #include <stdlib.h>
@@ -337,6 +337,27 @@ struct OP {
   int KO;  // = G * C
 };
 
+// write-out of a wave's table, transposed: part[s][nb + j][g*C + c], c fastest (float4 over 4 classes when C % 4 == 0)
+__device__ __forceinline__ void oh_writeout(const float* T, const OP& p, int s, int g, int nb, int lane) {
+  float* out = p.part + (long)s * p.N * p.KO + (long)g * p.C;
+  if ((p.C & 3) == 0 && (p.KO & 3) == 0) {
+    const int q4 = p.C >> 2;
+    for (int i = lane; i < OH_COLS * q4; i += 64) {
+      const int j = i / q4, c4 = (i - j * q4) * 4;
+      if (nb + j < p.N) {
+        const float4 o = make_float4(T[(c4 + 0) * OH_LDS + j], T[(c4 + 1) * OH_LDS + j], T[(c4 + 2) * OH_LDS + j],
+                                     T[(c4 + 3) * OH_LDS + j]);
+        *reinterpret_cast<float4*>(out + (long)(nb + j) * p.KO + c4) = o;
+      }
+    }
+  } else {
+    for (int i = lane; i < OH_COLS * p.C; i += 64) {
+      const int j = i / p.C, c = i - j * p.C;
+      if (nb + j < p.N) out[(long)(nb + j) * p.KO + c] = T[c * OH_LDS + j];
+    }
+  }
+}
+
 __global__ void __launch_bounds__(OH_WAVES * 64) onehot_kernel(OP p) {
   __shared__ float tab[OH_WAVES][OH_CMAX + 1][OH_LDS];  // + the junk row
   const int lane = threadIdx.x & 63;
@@ -415,24 +436,102 @@ __global__ void __launch_bounds__(OH_WAVES * 64) onehot_kernel(OP p) {
     const float2 o = T2[c * LD2];
     T2[c * LD2] = make_float2(o.x + x.x, o.y + x.y);
   }
-  // write-out transposed: part[s][nb + j][g*C + c], c fastest (float4 over 4 classes when C % 4 == 0)
-  float* out = p.part + (long)s * p.N * p.KO + (long)g * p.C;
-  if ((p.C & 3) == 0 && (p.KO & 3) == 0) {
-    const int q4 = p.C >> 2;
-    for (int i = lane; i < OH_COLS * q4; i += 64) {
-      const int j = i / q4, c4 = (i - j * q4) * 4;
-      if (nb + j < p.N) {
-        const float4 o = make_float4(T[(c4 + 0) * OH_LDS + j], T[(c4 + 1) * OH_LDS + j], T[(c4 + 2) * OH_LDS + j],
-                                     T[(c4 + 3) * OH_LDS + j]);
-        *reinterpret_cast<float4*>(out + (long)(nb + j) * p.KO + c4) = o;
-      }
-    }
-  } else {
-    for (int i = lane; i < OH_COLS * p.C; i += 64) {
-      const int j = i / p.C, c = i - j * p.C;
-      if (nb + j < p.N) out[(long)(nb + j) * p.KO + c] = T[c * OH_LDS + j];
+  oh_writeout(T, p, s, g, nb, lane);
+}
+
+// Same scatter with the dZ rows and hot classes staged ONCE per workgroup in LDS (the version above has each of
+// the 8 waves load the same 512-byte row slices itself: 8x the TA / L1 work, and only one 8-row batch - 4 KB
+// per CU - in flight, so at 16384 x 512 x 32 groups it sat at ~103 us, latency-bound on the dZ stream).  Units of
+// OS_RU = 16 rows: every thread loads one float4 of dZ (row tid / 32, 4 columns), threads 0-127 one hot index
+// (row tid / 8, group tid % 8) mapped to its class (OH_CMAX = junk row for rows past the chunk), all loads
+// issued two units ahead (32 KB in flight per CU) into named registers, then parked in a double-buffered LDS
+// stage; one barrier per unit.  The per-wave table update is the batch fold above on 4 rows at a time.
+constexpr int OS_RU = 16;
+
+__global__ void __launch_bounds__(OH_WAVES * 64) onehot_stg_kernel(OP p) {
+  __shared__ float tab[OH_WAVES][OH_CMAX + 1][OH_LDS];
+  __shared__ float4 stg[2][OS_RU][OH_COLS / 4];
+  __shared__ int4 cls[2][OH_WAVES][OS_RU / 4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = blockIdx.y * OH_WAVES + wave;  // >= G: the wave computes junk and writes nothing
+  const int s = blockIdx.z;
+  const int nb = blockIdx.x * OH_COLS;
+  float* T = &tab[wave][0][0];
+  for (int i = lane; i < (OH_CMAX + 1) * OH_LDS; i += 64) T[i] = 0.f;
+  const int m0 = s * p.rows, m1 = min(p.M, m0 + p.rows);
+  const int nu = (max(m1 - m0, 0) + OS_RU - 1) / OS_RU;
+  // staging roles (all loads unconditional, from clamped addresses)
+  const int lq = tid >> 5, lc4 = tid & 31;
+  const int iq = (tid >> 3) & (OS_RU - 1), iw = tid & 7;
+  const bool has_i = tid < OS_RU * OH_WAVES;
+  const int ig = min(blockIdx.y * OH_WAVES + iw, p.G - 1);
+  const float* dzp = p.dz + min(nb + 4 * lc4, p.N - 4);
+  const int* ipp = p.idx + ig;
+  const int ibase = ig * p.C + p.off;
+  int* clsw = reinterpret_cast<int*>(&cls[0][0][0]) + iw * OS_RU + iq;
+  const float2* S2 = reinterpret_cast<const float2*>(&stg[0][0][0]) + lane;
+  float2* T2 = reinterpret_cast<float2*>(T) + lane;
+  constexpr int LD2 = OH_LDS / 2;
+#define OS_LOAD(u, rv, ri)                                                             \
+  do {                                                                                 \
+    rv = *reinterpret_cast<const float4*>(dzp + (long)min(m0 + (u) * OS_RU + lq, m1 - 1) * p.ldz); \
+    ri = ipp[(long)min(m0 + (u) * OS_RU + iq, m1 - 1) * p.ldi];                        \
+  } while (0)
+#define OS_STORE(u, b, rv, ri)                                                                          \
+  do {                                                                                                  \
+    stg[b][lq][lc4] = rv;                                                                               \
+    if (has_i) clsw[(b) * OH_WAVES * OS_RU] = m0 + (u) * OS_RU + iq < m1 ? ((ri - ibase) & (OH_CMAX - 1)) : OH_CMAX; \
+  } while (0)
+  // 4 rows (q0..q0+3 of stage b) into the table: repeats folded into the last row of their class (see above)
+  auto quad = [&](int b, int q0, int4 cc) {
+    const int c0 = __builtin_amdgcn_readfirstlane(cc.x), c1 = __builtin_amdgcn_readfirstlane(cc.y);
+    const int c2 = __builtin_amdgcn_readfirstlane(cc.z), c3 = __builtin_amdgcn_readfirstlane(cc.w);
+    const float2* sv = S2 + (b * OS_RU + q0) * (OH_COLS / 2);
+    const float2 v0 = sv[0], v1 = sv[OH_COLS / 2], v2 = sv[OH_COLS], v3 = sv[3 * OH_COLS / 2];
+    const bool e01 = c0 == c1, e02 = c0 == c2, e03 = c0 == c3, e12 = c1 == c2, e13 = c1 == c3, e23 = c2 == c3;
+    const float2 s1 = make_float2(v1.x + (e01 ? v0.x : 0.f), v1.y + (e01 ? v0.y : 0.f));
+    const float2 s2 = make_float2(v2.x + (e02 ? v0.x : 0.f) + (e12 ? v1.x : 0.f), v2.y + (e02 ? v0.y : 0.f) + (e12 ? v1.y : 0.f));
+    const float2 s3 = make_float2(v3.x + (e03 ? v0.x : 0.f) + (e13 ? v1.x : 0.f) + (e23 ? v2.x : 0.f),
+                                  v3.y + (e03 ? v0.y : 0.f) + (e13 ? v1.y : 0.f) + (e23 ? v2.y : 0.f));
+    const int a0 = (e01 || e02 || e03) ? OH_CMAX : c0;
+    const int a1 = (e12 || e13) ? OH_CMAX : c1;
+    const int a2 = e23 ? OH_CMAX : c2;
+    const float2 o0 = T2[a0 * LD2], o1 = T2[a1 * LD2], o2 = T2[a2 * LD2], o3 = T2[c3 * LD2];
+    T2[a0 * LD2] = make_float2(o0.x + v0.x, o0.y + v0.y);
+    T2[a1 * LD2] = make_float2(o1.x + s1.x, o1.y + s1.y);
+    T2[a2 * LD2] = make_float2(o2.x + s2.x, o2.y + s2.y);
+    T2[c3 * LD2] = make_float2(o3.x + s3.x, o3.y + s3.y);
+  };
+  auto unit = [&](int b) {
+    const int4 k0 = cls[b][wave][0], k1 = cls[b][wave][1], k2 = cls[b][wave][2], k3 = cls[b][wave][3];
+    quad(b, 0, k0);
+    quad(b, 4, k1);
+    quad(b, 8, k2);
+    quad(b, 12, k3);
+  };
+  if (nu > 0) {
+    float4 ra, rb;
+    int ia, ib;
+    OS_LOAD(0, ra, ia);
+    OS_LOAD(min(1, nu - 1), rb, ib);
+    OS_STORE(0, 0, ra, ia);
+    __syncthreads();
+    for (int u = 0; u < nu; u += 2) {
+      OS_LOAD(min(u + 2, nu - 1), ra, ia);
+      unit(0);
+      OS_STORE(u + 1, 1, rb, ib);  // past the last unit: every row junk, never read
+      __syncthreads();
+      if (u + 1 >= nu) break;
+      OS_LOAD(min(u + 3, nu - 1), rb, ib);
+      unit(1);
+      OS_STORE(u + 2, 0, ra, ia);
+      __syncthreads();
     }
   }
+#undef OS_LOAD
+#undef OS_STORE
+  if (g < p.G) oh_writeout(T, p, s, g, nb, lane);
 }
 
 // ------------------------------------------------------------------ partial-sum reduction
@@ -553,10 +652,16 @@ bool launch_wgrad_onehot(const float* dz, long ldz, const int* idx, long ldi, in
   p.C = C;
   p.off = off;
   p.S = S;
-  p.rows = cdiv(cdiv(M, S), wgrad::OH_RB) * wgrad::OH_RB;
   p.KO = G * C;
-  hipLaunchKernelGGL(wgrad::onehot_kernel, dim3(cdiv(N, wgrad::OH_COLS), cdiv(G, wgrad::OH_WAVES), S),
-                     dim3(wgrad::OH_WAVES * 64), 0, st, p);
+  const dim3 grid(cdiv(N, wgrad::OH_COLS), cdiv(G, wgrad::OH_WAVES), S);
+  static const bool staged = env_int("SRL_WGRAD_OH_STAGED", 1) != 0;  // A/B switch
+  if (staged && (N & 3) == 0 && (ldz & 3) == 0 && ((uintptr_t)dz & 15) == 0) {
+    p.rows = cdiv(cdiv(M, S), wgrad::OS_RU) * wgrad::OS_RU;
+    hipLaunchKernelGGL(wgrad::onehot_stg_kernel, grid, dim3(wgrad::OH_WAVES * 64), 0, st, p);
+    return true;
+  }
+  p.rows = cdiv(cdiv(M, S), wgrad::OH_RB) * wgrad::OH_RB;
+  hipLaunchKernelGGL(wgrad::onehot_kernel, grid, dim3(wgrad::OH_WAVES * 64), 0, st, p);
   return true;
 }
 

@@ -38,7 +38,8 @@ def test_wgrad_dense(M, N, K, bias, strided):
 
 
 @pytest.mark.parametrize("M,N,G,C,Kd,off", [(16384, 512, 32, 32, 512, 9), (15360, 512, 32, 32, 512, 0),
-                                             (3000, 200, 8, 16, 40, 3)])
+                                             (3000, 200, 8, 16, 40, 3), (2000, 100, 5, 20, 24, 1),
+                                             (999, 64, 9, 7, 8, 2)])
 def test_wgrad_onehot(M, N, G, C, Kd, off):
     from sheeprl_prey_amd import ops
 
