@@ -124,6 +124,10 @@ class CNNEncoder(nn.Module):
                 # whole stack as one implicit-GEMM autograd op (ops/conv.py): NHWC, LN+SiLU fused
                 out = conv_ops.encoder_forward(self._fused_spec, flat, 1.0 / 255.0 if raw else 1.0)
                 return out.reshape(*x.shape[:-3], -1)
+            if self._fused_spec is not None and conv_ops.SMALL_ENABLED and not torch.is_grad_enabled():
+                # the player's few frames: split-K small-batch stack (csrc/conv_small.hip)
+                out = conv_ops.encoder_small(self._fused_spec, flat, 1.0 / 255.0 if raw else 1.0)
+                return out.reshape(*x.shape[:-3], -1)
         if raw:
             x = x / 255.0
         return cnn_forward(self.model, x, x.shape[-3:], (-1,))

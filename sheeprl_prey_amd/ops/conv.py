@@ -15,6 +15,7 @@ grayscale), power-of-two image size of at least 32; anything else runs the eager
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -24,8 +25,9 @@ _OK_CH = (32, 64, 96, 128, 192, 256, 384, 512, 768, 1024)  # conv.hip tile table
 ENABLED = True  # A/B switch: False routes the stacks through the per-layer modules (MIOpen + LN kernels)
 # Below this many frames (e.g. the env-interaction player, one frame per env) the deepest stage has
 # too few output rows to fill the chip (E4: 16 rows per frame) and a single workgroup walks all of K:
-# MIOpen's per-layer kernels are faster there.
+# no-grad calls there take the split-K small-batch stack (csrc/conv_small.hip, ``encoder_small``).
 MIN_FRAMES = 64
+SMALL_ENABLED = os.environ.get("SRL_SMALL_ENCODER", "1") != "0"  # A/B switch: False sends the small no-grad batches to the per-layer modules (MIOpen)
 
 
 def _C():
@@ -180,6 +182,18 @@ def encoder_forward(stages, x: Tensor, scale: float = 1.0) -> Tensor:
             "scale": float(scale)}
     params = [c.weight for c in convs] + [ln.weight for ln in lns] + [ln.bias for ln in lns]
     return EncoderConvFn.apply(x, meta, *params)
+
+
+def encoder_small(stages, x: Tensor, scale: float = 1.0) -> Tensor:
+    """No-grad encoder stack for a few frames (the player): [N, C, H, W] float / uint8 -> flat features, two
+    launches per stage (split-K MFMA conv + slice-sum / LayerNorm / activation), NCHW between stages."""
+    from sheeprl_prey_amd.ops import _act_code as act_code
+
+    convs = [c for c, _ in stages]
+    lns = [ln for _, ln in stages]
+    return _C().conv_small_encoder(x.contiguous(), [c.weight for c in convs], [ln.weight for ln in lns],
+                                   [ln.bias for ln in lns], [float(ln.eps) for ln in lns],
+                                   [act_code(ln.act) for ln in lns], float(scale))
 
 
 def _wgrad(C, P: Tensor, Q: Tensor, cb: int, w: Tensor) -> Tensor:

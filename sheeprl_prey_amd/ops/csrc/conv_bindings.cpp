@@ -237,6 +237,61 @@ torch::Tensor conv_up_small(torch::Tensor P, torch::Tensor W, c10::optional<torc
   return out;
 }
 
+bool launch_small_conv_stage(const void* x, bool u8, float scale, const float* w, const float* gamma, const float* beta,
+                             float eps, int act, float* part, float* y, int N, int Cin, int Hi, int Wi, int Cout,
+                             hipStream_t st);
+int small_conv_slices(int M, int Cout, int Cin);
+
+// Small-batch encoder stack (conv_small.hip): x [N, C, H, W] float or uint8 (scaled by `scale`), stages of
+// k4 s2 p1 conv (no bias) + LayerNormChannelLast + activation -> flat [N, C_L * H_L * W_L] (C, H, W order).
+torch::Tensor conv_small_encoder(torch::Tensor x, std::vector<torch::Tensor> ws, std::vector<torch::Tensor> gs,
+                                 std::vector<torch::Tensor> bs, std::vector<double> eps, std::vector<int64_t> act,
+                                 double scale) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous() &&
+                  (x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kUInt8),
+              "small encoder: x must be a contiguous NCHW float32 / uint8 CUDA tensor");
+  const size_t L = ws.size();
+  TORCH_CHECK(L >= 1 && gs.size() == L && bs.size() == L && eps.size() == L && act.size() == L, "small encoder: stage lists");
+  const int N = (int)x.size(0);
+  int C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  int64_t work = 0;
+  {
+    int c = C, h = H, w = W;
+    for (size_t i = 0; i < L; ++i) {
+      chk(ws[i], "small encoder weight");
+      chk(gs[i], "small encoder LN weight");
+      chk(bs[i], "small encoder LN bias");
+      const int co = (int)ws[i].size(0);
+      TORCH_CHECK(ws[i].dim() == 4 && ws[i].size(1) == c && ws[i].size(2) == 4 && ws[i].size(3) == 4,
+                  "small encoder: weight ", i, " must be [Cout, ", c, ", 4, 4]");
+      TORCH_CHECK(gs[i].numel() == co && bs[i].numel() == co, "small encoder: LN parameters of stage ", i);
+      TORCH_CHECK(h % 2 == 0 && w % 2 == 0 && h >= 2 && w >= 2, "small encoder: odd input size at stage ", i);
+      h /= 2;
+      w /= 2;
+      const int M = N * h * w;
+      work = std::max<int64_t>(work, (int64_t)small_conv_slices(M, co, c) * M * co);
+      c = co;
+    }
+  }
+  auto opt = x.options().dtype(torch::kFloat32);
+  torch::Tensor part = torch::empty({work}, opt);
+  torch::Tensor cur = x;
+  for (size_t i = 0; i < L; ++i) {
+    const int co = (int)ws[i].size(0);
+    torch::Tensor y = torch::empty({N, co, H / 2, W / 2}, opt);
+    const bool u8 = cur.scalar_type() == torch::kUInt8;
+    const bool ok = launch_small_conv_stage(cur.data_ptr(), u8, i == 0 ? (float)scale : 1.f, ws[i].data_ptr<float>(),
+                                            gs[i].data_ptr<float>(), bs[i].data_ptr<float>(), (float)eps[i], (int)act[i],
+                                            part.data_ptr<float>(), y.data_ptr<float>(), N, C, H, W, co, stream());
+    TORCH_CHECK(ok, "small encoder: unsupported stage ", i, " (Cout % 16, Cout <= 1024, even sizes, aligned)");
+    cur = y;
+    C = co;
+    H /= 2;
+    W /= 2;
+  }
+  return cur.reshape({N, -1});
+}
+
 void register_conv(pybind11::module& m) {
   m.def("conv_pack_down", &conv_pack_down);
   m.def("conv_pack_up", &conv_pack_up);
@@ -245,4 +300,5 @@ void register_conv(pybind11::module& m) {
   m.def("conv_to_nhwc4", &conv_to_nhwc4);
   m.def("conv_ln_bwd_flat", &conv_ln_bwd_flat);
   m.def("conv_up_small", &conv_up_small);
+  m.def("conv_small_encoder", &conv_small_encoder);
 }
