@@ -359,11 +359,25 @@ class RSSM(nn.Module):
         IDX = torch.empty(horizon + 1, M, nh + G, dtype=torch.int32, device=dev)
         oh.onehot_index(post, disc, IDX[0, :, nh:], A)
         W = rec_lin.weight  # columns: (prior | action)
-        Wp = torch.cat((W[:, S:], W[:, :S]), 1)  # columns: (action | prior)
-        rec_table = Wp.t().contiguous() if use_gather else None  # [A + S, D]: row = hot column of (action | prior)
         # the actor trunk's first layer: prior columns gathered from its transposed weight, h by a GEMM
         a0 = layers[0][0] if layers is not None else None
-        a_table = a0.weight[:, :S].t().contiguous() if (gather and layers is not None and oh.layer_supported(a0, S)) else None
+        want_a = gather and layers is not None and oh.layer_supported(a0, S)
+        rec_table = a_table = Wp = None
+        if use_gather:
+            # [A + S, D]: row = hot column of (action | prior); both tables transposed in one launch
+            na = W.shape[1] - S
+            rec_table = W.new_empty(W.shape[1], W.shape[0])
+            srcs, outs = [W[:, S:], W[:, :S]], [rec_table[:na], rec_table[na:]]
+            if want_a:
+                srcs.append(a0.weight[:, :S])
+                outs.append(None)
+            with torch.no_grad():
+                tabs = ops.transpose_many(srcs, outs)
+            a_table = tabs[2] if want_a else None
+        else:
+            Wp = torch.cat((W[:, S:], W[:, :S]), 1)  # columns: (action | prior)
+            if want_a:
+                a_table = a0.weight[:, :S].t().contiguous()
         act_scratch = None
         if trunk_rec is not None and a_table is not None:
             trunk_rec.onehot = (IDX[:, :, nh:], G, A, S)  # the trunk backward scatters the prior columns' dW

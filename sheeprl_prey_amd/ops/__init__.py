@@ -118,6 +118,24 @@ def wgrad_onehot_ok(dz: Tensor, G: int, n_onehot: int) -> bool:
             and dz.data_ptr() % 16 == 0)
 
 
+def transpose_many(xs, outs=None):
+    """Contiguous transposes of up to 8 fp32 matrices (2-D, unit column stride; column slices of weights are
+    fine) in ONE launch (csrc/transpose.hip); ``outs`` optionally names contiguous [cols, rows] destinations
+    (None entries allocate).  No autograd: for weight tables the HIP kernels read.  CPU: ``.t().contiguous()``."""
+    xs = list(xs)
+    if xs[0].is_cuda:
+        return _ext().transpose_many(xs, outs)
+    res = []
+    for j, x in enumerate(xs):
+        o = outs[j] if outs is not None and j < len(outs) else None
+        if o is None:
+            res.append(x.detach().t().contiguous())
+        else:
+            o.copy_(x.detach().t())
+            res.append(o)
+    return res
+
+
 def wgrad(dz: Tensor, x: Optional[Tensor] = None, onehot=None, bias: bool = False):
     """``(dW, db)`` of a linear layer ``z = [onehot | x] W^T + b`` from ``dz`` = dL/dz over M rows:
     ``dW [N, Kone + Kd] = [onehot | x]^T dz``, ``db = dz.sum(0)`` (None unless ``bias``; needs ``x``).

@@ -601,7 +601,20 @@ srl::scanp::PP scanp_params(const std::vector<torch::Tensor>& ts, const std::vec
   p.sync = (unsigned*)sync.data_ptr<int32_t>();
   p.W2T = P(k++); p.W1T = P(k++); p.WgT = P(k++); p.dpost = P(k++); p.dmixed = P(k++);
   p.DH = P(k++); p.dlog = P(k++); p.dv = P(k++); p.du = P(k++); p.dgx = P(k++); p.dcat = P(k++); p.dx = P(k++);
-  p.p1g = P(k++); p.p1b = P(k++); p.pgg = P(k++); p.pgb = P(k++); p.p2g = P(k++); p.p2b = P(k++);
+  // the LayerNorm parameter partials: [T, n] column slices (unit column stride) of one buffer, so the host
+  // reduces all six with ONE column sum
+  p.ldp = 0;
+  auto PL = [&](size_t i, int64_t n) -> float* {
+    if (i >= ts.size() || !ts[i].defined() || ts[i].numel() == 0) return nullptr;
+    const torch::Tensor& t = ts[i];
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kFloat32 && t.dim() == 2 && t.size(0) == p.T && t.size(1) == n &&
+                    t.stride(1) == 1, "scanp: LN partial ", i, " must be a float32 [T, ", n, "] GPU view with unit column stride");
+    TORCH_CHECK(p.ldp == 0 || p.ldp == t.stride(0), "scanp: the LN partials must share one row stride");
+    p.ldp = t.stride(0);
+    return t.data_ptr<float>();
+  };
+  p.p1g = PL(k++, p.D); p.p1b = PL(k++, p.D); p.pgg = PL(k++, 3 * p.H); p.pgb = PL(k++, 3 * p.H);
+  p.p2g = PL(k++, p.hid); p.p2b = PL(k++, p.hid);
   p.dZ = P(k++); p.sst = P(k++);
   return p;
 }

@@ -705,6 +705,42 @@ bool seq_sample_into(std::vector<torch::Tensor> srcs, std::vector<torch::Tensor>
                            (long)n1, (long)start2, (long)n2, (unsigned long long)seed, (unsigned long long)counter, stream());
 }
 
+bool launch_transpose_many(int nj, const float* const* src, const long* lds, const int* rows, const int* cols,
+                           float* const* dst, hipStream_t st);
+
+// contiguous transposes of up to 8 row-strided fp32 matrices (unit column stride) in one launch
+// (outs: optional contiguous [cols, rows] destinations, e.g. row blocks of one table; None entries allocate)
+std::vector<torch::Tensor> transpose_many(std::vector<torch::Tensor> xs, c10::optional<std::vector<c10::optional<torch::Tensor>>> outs) {
+  TORCH_CHECK(!xs.empty() && xs.size() <= 8, "transpose_many: 1..8 matrices");
+  std::vector<torch::Tensor> out;
+  const float* src[8];
+  float* dst[8];
+  long lds[8];
+  int rows[8], cols[8];
+  for (size_t j = 0; j < xs.size(); ++j) {
+    const torch::Tensor& x = xs[j];
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.dim() == 2 && (x.stride(1) == 1 || x.size(1) <= 1),
+                "transpose_many: fp32 2-D GPU matrices with unit column stride");
+    TORCH_CHECK(x.size(0) < (1 << 30) && x.size(1) < (1 << 30), "transpose_many: too large");
+    torch::Tensor y;
+    if (outs.has_value() && j < outs->size() && (*outs)[j].has_value() && (*outs)[j]->defined()) {
+      y = *(*outs)[j];
+      TORCH_CHECK(y.is_cuda() && y.scalar_type() == torch::kFloat32 && y.is_contiguous() && y.dim() == 2 &&
+                      y.size(0) == x.size(1) && y.size(1) == x.size(0), "transpose_many: out ", j, " must be contiguous [cols, rows]");
+    } else {
+      y = torch::empty({x.size(1), x.size(0)}, x.options());
+    }
+    src[j] = x.data_ptr<float>();
+    dst[j] = y.data_ptr<float>();
+    lds[j] = x.size(0) > 1 ? (long)x.stride(0) : (long)x.size(1);
+    rows[j] = (int)x.size(0);
+    cols[j] = (int)x.size(1);
+    out.push_back(y);
+  }
+  TORCH_CHECK(launch_transpose_many((int)xs.size(), src, lds, rows, cols, dst, stream()), "transpose_many: launch");
+  return out;
+}
+
 void register_ext(pybind11::module& m) {
   m.def("sac_critic_fwd", &sac_critic_fwd);
   m.def("sac_critic_wgrad", &sac_critic_wgrad);
@@ -712,6 +748,7 @@ void register_ext(pybind11::module& m) {
         pybind11::arg("err") = pybind11::none());
   m.def("onehot_index", &onehot_index);
   m.def("seq_sample_into", &seq_sample_into);
+  m.def("transpose_many", &transpose_many, pybind11::arg("xs"), pybind11::arg("outs") = pybind11::none());
   m.def("actor_tail", &actor_tail, pybind11::arg("pre"), pybind11::arg("y"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("eps"), pybind11::arg("act"), pybind11::arg("Wh"),
         pybind11::arg("bh"), pybind11::arg("uniform"), pybind11::arg("alpha"), pybind11::arg("sample"), pybind11::arg("idx"),

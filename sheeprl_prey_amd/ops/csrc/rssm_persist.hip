@@ -758,12 +758,12 @@ __device__ __forceinline__ void bwd_G2(const PP& p, int i, float* sm) {
       float a = 0.f;
       for (int b = 0; b < B; ++b) a += gsc[b * 96 + k * 16 + c];
       const int col = (k >> 1) * H + i * 16 + c;
-      (k & 1 ? p.pgb : p.pgg)[(size_t)t * N3 + col] = a;
+      (k & 1 ? p.pgb : p.pgg)[(size_t)t * p.ldp + col] = a;
     }
     {  // behind the hand-off: LN2 parameter partials and du (weight-gradient inputs)
       int lo, hi;
       part_range(hid, i, n2, lo, hi);
-      ln_param_partials(As, lda, R, lda, B, lo, hi, p.p2g + (size_t)t * hid, p.p2b + (size_t)t * hid);
+      ln_param_partials(As, lda, R, lda, B, lo, hi, p.p2g + (size_t)t * p.ldp, p.p2b + (size_t)t * p.ldp);
       part_range(B * hid, i, n2, lo, hi);
       float* du = p.du + (size_t)t * B * hid;
       for (int e = lo + threadIdx.x; e < hi; e += NTH) du[e] = X2[(e / hid) * lda + e % hid];
@@ -928,7 +928,7 @@ __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
     auto tail = [&]() {
       int lo, hi;
       part_range(D, i4, n4, lo, hi);
-      ln_param_partials(As, lda, R, lda, B, lo, hi, p.p1g + (size_t)t * D, p.p1b + (size_t)t * D);
+      ln_param_partials(As, lda, R, lda, B, lo, hi, p.p1g + (size_t)t * p.ldp, p.p1b + (size_t)t * p.ldp);
       part_range(B * D, i4, n4, lo, hi);
       float* dx = p.dx + (size_t)t * B * D;
       for (int e = lo + threadIdx.x; e < hi; e += NTH) dx[e] = X2[(e / D) * lda + e % D];

@@ -22,6 +22,7 @@ struct PP {
   const float *W2T, *W1T, *WgT, *dpost, *dmixed;
   // backward state / outputs: DH holds d_hs on entry, dlog[T-1] is written before the launch
   float *DH, *dlog, *dv, *du, *dgx, *dcat, *dx, *p1g, *p1b, *pgg, *pgb, *p2g, *p2b;
+  long ldp;  // row stride of the six LayerNorm parameter partial arrays (column slices of one [T, 2D + 6H + 2hid] buffer)
   // LN-GRU adjoint pieces handed G2 -> G3: dz*gamma per gate column [T][B][3H], row partial sums [T][H/16][16][2]
   float *dZ, *sst;
   // hand-off counters (zeroed before every launch) and the error word (0 = ok)

@@ -67,7 +67,7 @@ def gather_first_layer(x: Tensor, idx: Tensor, G: int, off: int, lin: nn.Linear,
     W = lin.weight
     M, N = x.shape[0], W.shape[0]
     if table is None:
-        table = W[:, :n_onehot].t().contiguous()
+        table = ops.transpose_many([W[:, :n_onehot]])[0]
     Y = None
     if x.shape[1] > n_onehot:
         Y = torch.mm(x[:, n_onehot:], W[:, n_onehot:].t())
@@ -90,7 +90,7 @@ class _GatherFirstLayer(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         idx2 = idx.reshape(-1, idx.shape[-1])
         M, N = x2.shape[0], W.shape[0]
-        table = W[:, :n_onehot].t().contiguous()
+        table = ops.transpose_many([W[:, :n_onehot]])[0]
         Y = torch.mm(x2[:, n_onehot:], W[:, n_onehot:].t()) if x2.shape[1] > n_onehot else None
         z = torch.empty(M, N, device=x.device, dtype=x.dtype)
         y = torch.empty(M, N, device=x.device, dtype=x.dtype)

@@ -324,16 +324,22 @@ class RSSMPersistFn(torch.autograd.Function):
         assert ok, "scanp: unsupported shape"
         sync = torch.empty(words, device=dev, dtype=torch.int32)
         _scan_health_word(dev)
-        fwd = [P.contiguous(), first, uniform.contiguous(), z0, Wz_c, Wz_c.t().contiguous(), ln1_w.contiguous(),
-               ln1_b.contiguous(), Wg.contiguous(), lng_w.contiguous(), lng_b.contiguous(), W1.contiguous(),
-               ln2_w.contiguous(), ln2_b.contiguous(), W2.contiguous(), b2.contiguous(),
+        # every transposed weight the scan needs (forward Wz^T; backward W2^T, W1^T, Wg^T) in one launch
+        from sheeprl_prey_amd.ops import transpose_many
+
+        train = any(ctx.needs_input_grad)
+        W2c, W1c, Wgc = W2.contiguous(), W1.contiguous(), Wg.contiguous()
+        trs = transpose_many([Wz_c, W2c, W1c, Wgc] if train else [Wz_c])
+        fwd = [P.contiguous(), first, uniform.contiguous(), z0, Wz_c, trs[0], ln1_w.contiguous(),
+               ln1_b.contiguous(), Wgc, lng_w.contiguous(), lng_b.contiguous(), W1c,
+               ln2_w.contiguous(), ln2_b.contiguous(), W2c, b2.contiguous(),
                xr, e(T, B, H + D), zm, e(T, B), e(T, B), e(T, B, 3 * H), e(T, 3 * H // 16, 16, 2), e(T, B), e(T, B),
                e(T, B, H), e(T, B, hid), e(T, B, hid), e(T, B), e(T, B), e(T, B, S), e(T, B, S), e(T, B, S),
                torch.empty(T, B, S // disc, device=dev, dtype=torch.int32), sync]
         dims = [T, B, S, D, H, hid, disc, act1, act2]
         fl = [alpha, eps1, epsg, eps2]
         C.scanp_fwd(fwd, dims, fl)
-        ctx.save_for_backward(*fwd)
+        ctx.save_for_backward(*fwd, *trs[1:])
         ctx.dims, ctx.fl = dims, fl
         hs, mixed, samples = fwd[25], fwd[31], fwd[32]
         return hs, samples, mixed
@@ -343,7 +349,8 @@ class RSSMPersistFn(torch.autograd.Function):
         from sheeprl_prey_amd.ops import _ext
 
         C = _ext()
-        fwd = list(ctx.saved_tensors)
+        saved = list(ctx.saved_tensors)
+        fwd, (W2T, W1T, WgT) = saved[:-3], saved[-3:]
         T, B, S, D, H, hid, disc = ctx.dims[:7]
         alpha = ctx.fl[0]
         dev, f32 = fwd[0].device, torch.float32
@@ -358,8 +365,11 @@ class RSSMPersistFn(torch.autograd.Function):
         C.unimix_sample_bwd_into(logits[T - 1], dmixed[T - 1], dpost[T - 1] if d_post is not None else None, dlog[T - 1],
                                  disc, alpha)
         dv, du, dgx, dcat, dx = e(T, B, hid), e(T, B, hid), e(T, B, 3 * H), e(T, B, H + D), e(T, B, D)
-        p1g, p1b, pgg, pgb, p2g, p2b = e(T, D), e(T, D), e(T, 3 * H), e(T, 3 * H), e(T, hid), e(T, hid)
-        bwd = [W2.t().contiguous(), W1.t().contiguous(), Wg.t().contiguous(), dpost, dmixed, DH, dlog, dv, du, dgx, dcat,
+        # the six LayerNorm parameter partials as column slices of one buffer: one column sum for all of them
+        widths = (D, D, 3 * H, 3 * H, hid, hid)
+        lnp = e(T, sum(widths))
+        p1g, p1b, pgg, pgb, p2g, p2b = torch.split(lnp, widths, dim=1)
+        bwd = [W2T, W1T, WgT, dpost, dmixed, DH, dlog, dv, du, dgx, dcat,
                dx, p1g, p1b, pgg, pgb, p2g, p2b, e(T, B, 3 * H), e(T, H // 16, 16, 2)]
         _scan_health_word(dev)
         C.scanp_bwd(fwd + bwd, ctx.dims, ctx.fl)
@@ -371,8 +381,8 @@ class RSSMPersistFn(torch.autograd.Function):
         dlog2 = dlog.reshape(TB, S)
         dW2 = dlog2.t().mm(v.reshape(TB, hid))
         db2 = dlog2.sum(0)
-        return (dx, du, None, None, None, dWz, p1g.sum(0), p1b.sum(0), dWg, pgg.sum(0), pgb.sum(0), dW1, p2g.sum(0),
-                p2b.sum(0), dW2, db2, None)
+        g1w, g1b, ggw, ggb, g2w, g2b = torch.split(lnp.sum(0), widths)
+        return (dx, du, None, None, None, dWz, g1w, g1b, dWg, ggw, ggb, dW1, g2w, g2b, dW2, db2, None)
 
 
 def scanp_error(sync: Tensor) -> int:
