@@ -67,6 +67,7 @@ class _WMLoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, kl_loss, obs, rew, logits, dones, kl, kl_reg, scale):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero-filled tensor (one fill launch each)
         C = ops._ext()
         R = kl_loss.numel()
         lg = logits.detach().contiguous().view(-1) if logits is not None else None
@@ -81,6 +82,8 @@ class _WMLoss(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g, *_):
+        if g is None:
+            return (None,) * 8
         lg, dn = ctx.saved_tensors
         R, kl_reg, scale, s_kll, s_obs, s_rew, s_lg = ctx.cfg
         d_kll, d_obs, d_rew, d_lg = ops._ext().wm_loss_bwd(lg, dn, g.contiguous().view(1), R, kl_reg, scale)

@@ -282,6 +282,7 @@ def ln_gru(x: Tensor, h: Tensor, weight: Tensor, bias: Tensor, eps: float = 1e-5
 class _UnimixSample(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, uniform, classes, alpha, sample):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero-filled tensor (one fill launch each)
         l2 = logits.contiguous()
         mixed, st = _ext().unimix_sample_fwd(l2, uniform if sample else None, classes, alpha)
         ctx.save_for_backward(l2)
@@ -382,6 +383,7 @@ def twohot_mean(logits: Tensor, low: float = -20.0, high: float = 20.0) -> Tenso
 class _KLBalance(torch.autograd.Function):
     @staticmethod
     def forward(ctx, post, prior, groups, classes, dyn, rep, free):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero-filled tensor (one fill launch each)
         a = post.contiguous()
         b = prior.contiguous()
         kl, loss, ea, eb = _ext().kl_fwd(a, b, groups, classes, dyn, rep, free)
@@ -394,6 +396,8 @@ class _KLBalance(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gl, _gkl, _gea, _geb):
+        if gl is None:
+            return None, None, None, None, None, None, None
         a, b, kl = ctx.saved_tensors
         groups, classes, dyn, rep, free = ctx.cfg
         da, db = _ext().kl_bwd(a, b, kl, gl.contiguous().view(-1), groups, classes, dyn, rep, free)
@@ -509,6 +513,7 @@ __all__ = [
 class _SquashedGaussian(torch.autograd.Function):
     @staticmethod
     def forward(ctx, mean, log_std, eps, scale, bias, mode, lo, hi):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero-filled tensor (one fill launch each)
         m, r, e = mean.contiguous(), log_std.contiguous(), eps.contiguous()
         action, logp = _ext().squashed_gaussian_fwd(m, r, e, scale, bias, mode, lo, hi)
         ctx.save_for_backward(m, r, e, scale)
@@ -517,6 +522,8 @@ class _SquashedGaussian(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, ga, glp):
+        if ga is None and glp is None:
+            return (None,) * 8
         m, r, e, scale = ctx.saved_tensors
         dmean, draw = _ext().squashed_gaussian_bwd(
             m, r, e, scale, ga.contiguous() if ga is not None else None,
@@ -700,6 +707,7 @@ class _SACCriticLoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, obs, act, y, W1, b1, W2, b2, W3, b3):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero-filled tensor (one fill launch each)
         lossp, q, *saved = _ext().sac_critic_fwd(obs, act, y, W1, b1, W2, b2, W3, b3)
         ctx.save_for_backward(*saved)
         ctx.IN = W1.shape[2]
@@ -708,6 +716,8 @@ class _SACCriticLoss(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g, _gq):
+        if g is None:
+            return (None,) * 9
         grads = _ext().sac_critic_wgrad(*ctx.saved_tensors, g.reshape(1).contiguous(), ctx.IN)
         return (None, None, None, *grads)
 
@@ -780,6 +790,7 @@ def imag_discount(continue_logits: Tensor, dones: Tensor, gamma: float):
 class _LSTMSeq(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, h0, c0, W_ih, W_hh, b_ih, b_hh):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero-filled tensor (one fill launch each)
         T, B, D = x.shape
         H = W_hh.shape[1]
         C = _ext()

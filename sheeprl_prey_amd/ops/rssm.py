@@ -67,6 +67,7 @@ def _nt(A: Tensor, W: Tensor, out: Tensor, add: Tensor = None) -> None:
 class RSSMScanFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a_proj, P, is_first, uniform, z0, Wz, ln1_w, ln1_b, Wg, lng_w, lng_b, W1, ln2_w, ln2_b, W2, b2, meta):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero-filled tensor (one fill launch each)
         from sheeprl_prey_amd.ops import _ext
 
         C = _ext()
@@ -230,6 +231,7 @@ class RSSMScan4Fn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, a_proj, P, is_first, uniform, z0, Wz, ln1_w, ln1_b, Wg, lng_w, lng_b, W1, ln2_w, ln2_b, W2, b2, meta):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero-filled tensor (one fill launch each)
         from sheeprl_prey_amd.ops import _ext
 
         C = _ext()
@@ -303,6 +305,7 @@ class RSSMPersistFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, a_proj, P, is_first, uniform, z0, Wz, ln1_w, ln1_b, Wg, lng_w, lng_b, W1, ln2_w, ln2_b, W2, b2, meta):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero-filled tensor (one fill launch each)
         from sheeprl_prey_amd.ops import _ext
 
         C = _ext()
@@ -494,6 +497,7 @@ class _SplitCols(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, W: Tensor, k: int):
+        ctx.set_materialize_grads(False)  # unused outputs: None, not a zero-filled tensor (one fill launch each)
         ctx.k, ctx.n, ctx.m = k, W.shape[0], W.shape[1]
         return W[:, :k], W[:, k:]
 
