@@ -216,7 +216,9 @@ class SegmentedPPOUpdate:
             return
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
-        with torch.cuda.graph(g, pool=self.pool):
+        from sheeprl_prey_amd.parallel.graphs import capture_error_mode
+
+        with torch.cuda.graph(g, pool=self.pool, capture_error_mode=capture_error_mode()):
             fn()
         self.pool = g.pool()
         if graphs is not None:

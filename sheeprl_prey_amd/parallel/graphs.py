@@ -17,6 +17,16 @@ from torch import Tensor
 from sheeprl_prey_amd.parallel.flat_optim import gather_all_pending
 
 
+def capture_error_mode() -> str:
+    """Stream-capture mode of every hipGraph capture here: ``thread_local`` when a process group is up.
+    In the default ``global`` mode ANY thread's unsafe HIP call fails during a capture - and the RCCL
+    process group's watchdog thread polls the completion events of earlier collectives on its own schedule
+    (a query that landed inside a capture aborted a GPU-suite run with hipErrorStreamCaptureUnsupported)."""
+    import torch.distributed as dist
+
+    return "thread_local" if dist.is_available() and dist.is_initialized() else "global"
+
+
 class GraphedStep:
     def __init__(self, fn: Callable[[Dict[str, Tensor]], Dict[str, Tensor]], warmup: int = 2, enabled: bool = True,
                  name: str = "step"):
@@ -65,7 +75,7 @@ class GraphedStep:
             return out
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize()
-        with torch.cuda.graph(g, pool=self.pool):
+        with torch.cuda.graph(g, pool=self.pool, capture_error_mode=capture_error_mode()):
             self.static_out = self.fn(self.static_in)
         self.graph = g
         # capture recorded the work without executing it: run this step for real
@@ -147,7 +157,7 @@ class SegmentedGraph:
         out = None
         for i, ph in enumerate(self.phases):
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, capture_error_mode=capture_error_mode()):
                 out = ph(self.static_in)
                 # grads handed over by autograd must reach the flat slabs INSIDE this phase's graph:
                 # the collective after it runs eagerly between replays

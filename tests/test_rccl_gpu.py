@@ -105,7 +105,7 @@ def test_rccl_collectives_captured_in_hipgraph(rccl_group):
     torch.cuda.synchronize()
 
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):  # the RCCL watchdog polls from its own thread
         opt.zero_grad()
         m(static_x).square().mean().backward()
         launched = len(opt._ov["works"])
