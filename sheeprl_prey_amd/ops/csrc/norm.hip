@@ -211,7 +211,14 @@ __global__ void __launch_bounds__(256) ln_wave4_bwd_kernel(const float* __restri
                                                            const float* __restrict__ gamma, const float* __restrict__ beta,
                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
                                                            float* __restrict__ pdg, float* __restrict__ pdb, int M, int N,
-                                                           int act) {
+                                                           int act, float* __restrict__ za, float* __restrict__ zb) {
+  // za / zb (or null): the dgamma / dbeta targets the column-sum kernel after this one accumulates into
+  // atomically - zeroed here by block 0 instead of by a separate zero kernel (one launch less per call)
+  if (za != nullptr && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < N; i += 256) {
+      za[i] = 0.f;
+      zb[i] = 0.f;
+    }
   __shared__ float4 red_g[4][64 * NV4];
   __shared__ float4 red_b[4][64 * NV4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -691,6 +698,15 @@ void launch_colsum1(const float* x, int ldx, float* out, int rows, int N, hipStr
   hipLaunchKernelGGL(colsum1_kernel, dim3(cdiv(N, 64), 1, S), dim3(256), 0, st, x, ldx, out, rows, N);
 }
 
+// the reduction alone: oa / ob already zeroed (by the producing kernel)
+static void launch_colsum2_nz(const float* pa, const float* pb, float* oa, float* ob, int rows, int N, int G, hipStream_t st) {
+  const int Rg = cdiv(rows, G > 0 ? G : 1);
+  int S = cdiv(Rg, 64);
+  if (S > 32) S = 32;
+  if (S < 1) S = 1;
+  hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(N, 64), G, S), dim3(256), 0, st, pa, pb, oa, ob, rows, N, G);
+}
+
 void launch_colsum2(const float* pa, const float* pb, float* oa, float* ob, int rows, int N, int G, hipStream_t st) {
   // zero kernel + one reduction kernel (graph-capturable); ~64 partial rows per split
   launch_zero2(oa, ob, G * N, st);
@@ -715,7 +731,9 @@ bool launch_ln_act_bwd(const float* x, int ldx, const float* dy, int lddy, float
     const bool al16 = ((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)gamma | (uintptr_t)beta) % 16 == 0;
     if (G == 1 && N % 4 == 0 && ldx % 4 == 0 && lddy % 4 == 0 && lddx % 4 == 0 && al16 &&
         (gamma != nullptr) == (beta != nullptr) && maxv <= 16) {
-#define F4(NV) if (maxv == 4 * NV) { SRL_ACT_SPECIALIZE(act, hipLaunchKernelGGL((ln_wave4_bwd_kernel<NV, ACTC>), dim3(grid), dim3(256), 0, st, x, ldx, dy, lddy, dx, lddx, gamma, beta, mean, rstd, pg, pb, M, N, act)); goto reduce; }
+      float* za = (gamma && dgamma) ? dgamma : nullptr;
+      float* zb = (gamma && dgamma) ? dbeta : nullptr;
+#define F4(NV) if (maxv == 4 * NV) { SRL_ACT_SPECIALIZE(act, hipLaunchKernelGGL((ln_wave4_bwd_kernel<NV, ACTC>), dim3(grid), dim3(256), 0, st, x, ldx, dy, lddy, dx, lddx, gamma, beta, mean, rstd, pg, pb, M, N, act, za, zb)); goto reduce_zeroed; }
       F4(1) F4(2) F4(4)
 #undef F4
     }
@@ -731,6 +749,9 @@ bool launch_ln_act_bwd(const float* x, int ldx, const float* dy, int lddy, float
   }
 reduce:
   if (gamma && dgamma) launch_colsum2(pdg, pdb, dgamma, dbeta, grid * G, N, G, st);
+  return true;
+reduce_zeroed:  // the LN kernel zeroed dgamma / dbeta itself
+  if (gamma && dgamma) launch_colsum2_nz(pdg, pdb, dgamma, dbeta, grid * G, N, G, st);
   return true;
 }
 
