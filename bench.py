@@ -51,6 +51,11 @@ def parse():
     p.add_argument("--segmented", action="store_true",
                    help="use the multi-rank graph mode (one hipGraph per phase, collectives between replays) "
                         "on any N, to price it against the single-graph step at N=1")
+    p.add_argument("--graph-collectives", type=int, default=0, choices=[0, 1],
+                   help="N>1 over RCCL: 1 = capture the collectives in the one step graph (single+rccl), 0 = one graph "
+                        "per phase with the collectives issued eagerly between replays (segmented, default)")
+    p.add_argument("--pg-timeout", type=float, default=300.0,
+                   help="process-group timeout and host heartbeat (seconds): a stalled rank exits non-zero")
     p.add_argument("--check-finite", type=int, default=0,
                    help="diagnostic: run N untimed steps, report the first non-finite train output per step")
     p.add_argument("--gemm-tuning", default=None, choices=["use", "tune", "off"],
@@ -101,8 +106,6 @@ def main():
     from sheeprl_prey_amd.utils.env import make_env, make_vector_env
     from sheeprl_prey_amd.utils.utils import dotdict
 
-    if args.eager_ops:
-        ops.set_fused(False)
     if args.continuous:
         # reference configs/exp/dreamer_v3_dmc_walker_walk.yaml on the walker_walk-shaped synthetic env
         base = ["exp=dreamer_v3_dmc_walker_walk", "env=gym", "env.id=walker_walk_synthetic", "env.sync_env=True",
@@ -113,6 +116,8 @@ def main():
                 "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]"]
     overrides = base + [
         "fabric.accelerator=cuda", f"fabric.cuda_graphs={not args.no_graphs}", "metric.log_every=1000000000",
+        f"fabric.fused_ops={not args.eager_ops}", f"fabric.graph_collectives={bool(args.graph_collectives)}",
+        f"fabric.pg_timeout_s={args.pg_timeout}",
     ] + ([f"fabric.tunable_gemm={args.gemm_tuning}"] if args.gemm_tuning else []) + (XL_OVERRIDES if args.xl else []) + list(
         args.overrides)
     cfg = dotdict(compose(overrides))
@@ -122,6 +127,10 @@ def main():
     rank, world = runner.global_rank, runner.world_size
     device = runner.device
     runner.seed_everything(cfg.seed + rank)
+    from sheeprl_prey_amd.parallel.collectives import CollectiveLog, Heartbeat
+
+    heart = Heartbeat(args.pg_timeout if world > 1 else 0, "init")
+    rccl_ranks = formed_ranks(runner)
 
     envs = make_vector_env(cfg, [make_env(cfg, cfg.seed + rank * cfg.env.num_envs + i, rank * cfg.env.num_envs, None,
                                           "train", i) for i in range(cfg.env.num_envs)])
@@ -194,11 +203,16 @@ def main():
         loop.step(False, train_once)
         return loop.last_train_out
 
+    # the collectives every phase of one step issues (recorded on the second warm-up step: the first one
+    # also enables the hook-launched buckets)
+    clog = CollectiveLog()
     if args.check_finite:
         check_finite_steps(args, trainer, rb, cfg, one_step, lambda: trainer.train_step(last_batch[0]), (world_model, actor, critic),
                            (wopt, aopt, copt), moments)
-    for _ in range(args.warmup):
-        out = one_step()
+    with clog:
+        for i in range(args.warmup):
+            out = one_step()
+            heart.beat(f"warmup step {i}")
     torch.cuda.synchronize()
     if args.torch_profile and rank == 0:
         # op attribution of the small kernels: the same train step run eagerly (graphs off) under
@@ -265,8 +279,9 @@ def main():
         torch.cuda._sleep(1000)  # marker kernel: scripts/trace_window.py aggregates the dispatches after it
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         out = one_step()
+        heart.beat(f"timed step {i}")
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -331,6 +346,9 @@ def main():
                 "hipgraph": bool(trainer.uses_graphs), "graph_mode": trainer.graph_mode,
                 "fused_ops": ops.fused_enabled(),
             },
+            "backend": runner.backend if world > 1 else None,
+            "rccl_ranks": rccl_ranks,
+            "collectives_per_step": clog.per_phase(min(2, clog.step)) if world > 1 else {},
             "policy_steps_per_s": round(policy_steps / elapsed, 3),
             "grad_steps_per_s": round(args.steps * world / elapsed, 3),
             "final_wm_loss": round(loss, 4),
@@ -341,6 +359,17 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    heart.stop()
+
+
+def formed_ranks(runner) -> int:
+    """How many ranks the process group actually formed: an all-reduce of ones right after init."""
+    if runner.world_size <= 1:
+        return 1
+    dev = runner.device if runner.backend == "nccl" else torch.device("cpu")
+    t = torch.ones(1, device=dev)
+    dist.all_reduce(t)
+    return int(t.item())
 
 
 def check_finite_steps(args, trainer, rb, cfg, one_step, train_once, models, opts, moments):

@@ -277,19 +277,22 @@ class RSSM(nn.Module):
     def _uniform_mix(self, logits: Tensor) -> Tensor:
         return ops.reference.unimix_logits(logits, self.discrete, self.unimix)
 
-    def _sample(self, logits: Tensor, sample: bool = True) -> Tuple[Tensor, Tensor]:
-        mixed, st = ops.unimix_sample(logits, self.discrete, self.unimix, sample=sample)
+    def _sample(self, logits: Tensor, sample: bool = True, forced: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+        mixed, st = ops.unimix_sample(logits, self.discrete, self.unimix, sample=sample, forced=forced)
         return mixed, st.view(*st.shape[:-1], -1, self.discrete)
 
     def _representation(self, recurrent_state: Tensor, embedded_obs: Tensor) -> Tuple[Tensor, Tensor]:
         return self._sample(self.representation_model(torch.cat((recurrent_state, embedded_obs), -1)))
 
-    def _transition(self, recurrent_out: Tensor, sample_state: bool = True) -> Tuple[Tensor, Tensor]:
-        return self._sample(self.transition_model(recurrent_out), sample=sample_state)
+    def _transition(self, recurrent_out: Tensor, sample_state: bool = True,
+                    forced: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+        return self._sample(self.transition_model(recurrent_out), sample=sample_state, forced=forced)
 
-    def imagination(self, prior: Tensor, recurrent_state: Tensor, actions: Tensor) -> Tuple[Tensor, Tensor]:
+    def imagination(self, prior: Tensor, recurrent_state: Tensor, actions: Tensor,
+                    forced: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+        """``forced``: the prior sample to take (one-hot, teacher forcing of the eager oracle)."""
         recurrent_state = self.recurrent_model(torch.cat((prior, actions), -1), recurrent_state)
-        _, imagined_prior = self._transition(recurrent_state)
+        _, imagined_prior = self._transition(recurrent_state, forced=forced)
         return imagined_prior, recurrent_state
 
     # ---- MI355X imagination: buffer-resident no-grad rollout ---------------------------
@@ -439,17 +442,19 @@ class RSSM(nn.Module):
             x = m(x)
         return x
 
-    def scan_dynamic(self, embedded_obs: Tensor, actions: Tensor, is_first: Tensor, uniform: Optional[Tensor] = None):
+    def scan_dynamic(self, embedded_obs: Tensor, actions: Tensor, is_first: Tensor, uniform: Optional[Tensor] = None,
+                     forced: Optional[Tensor] = None):
         """Posterior scan over ``T`` (reference loop: ``dreamer_v3.py:122-129``).
 
-        embedded_obs [T, B, E], actions [T, B, A] (already shifted), is_first [T, B, 1].
+        embedded_obs [T, B, E], actions [T, B, A] (already shifted), is_first [T, B, 1].  ``forced`` [T, B, S]
+        (one-hot): the posterior samples to take (teacher forcing; eager path only).
         Returns recurrent_states [T,B,H], posteriors [T,B,S,D], posteriors_logits [T,B,S*D],
         priors_logits [T,B,S*D]."""
         T, B = embedded_obs.shape[:2]
         if getattr(self, "_srl_autocast", False):
             # bf16-mixed: every sub-model through its own (autocast) forward, as the reference does
             return self._scan_by_steps(embedded_obs, actions, is_first, uniform)
-        if ops._native(embedded_obs) and getattr(self, "fused_scan", True):
+        if ops._native(embedded_obs) and getattr(self, "fused_scan", True) and forced is None:
             from sheeprl_prey_amd.ops.rssm import fused_scan, fused_scan_supported
 
             if fused_scan_supported(self):
@@ -494,7 +499,7 @@ class RSSM(nn.Module):
             pl = self._uniform_mix_fused(trans(h))
             rep_pre = torch.addmm(e_proj[t], h, Wh_rep.t())
             ql, zs = ops.unimix_sample(self._mlp_head(rep, rep_pre), self.discrete, self.unimix, sample=True,
-                                       uniform=uniform[t])
+                                       uniform=uniform[t], forced=forced[t] if forced is not None else None)
             z = zs
             hs.append(h)
             posts.append(zs)
@@ -582,7 +587,9 @@ class Actor(nn.Module):
         lo, hi = mean.new_full((), -1.0), mean.new_full((), 1.0)
         return Independent(TruncatedNormal(torch.tanh(mean), std, lo, hi, validate_args=va), 1, validate_args=va)
 
-    def forward(self, state: Tensor, is_training: bool = True, mask: Optional[Dict[str, np.ndarray]] = None):
+    def forward(self, state: Tensor, is_training: bool = True, mask: Optional[Dict[str, np.ndarray]] = None,
+                forced: Optional[Sequence[Tensor]] = None):
+        """``forced``: per discrete head, the one-hot action to take (teacher forcing of the eager oracle)."""
         out = self.model(state)
         pre_dist = [head(out) for head in self.mlp_heads]
         va = self.distribution_cfg.get("validate_args", False)
@@ -596,9 +603,10 @@ class Actor(nn.Module):
                 actions = sample[log_prob.argmax(0)].view(1, 1, -1)
             return (actions,), (d,)
         actions, dists = [], []
-        for logits in pre_dist:
+        for i, logits in enumerate(pre_dist):
             C = logits.shape[-1]
-            mixed, st = ops.unimix_sample(logits, C, self._unimix, sample=is_training)
+            mixed, st = ops.unimix_sample(logits, C, self._unimix, sample=is_training,
+                                          forced=forced[i] if forced is not None else None)
             dists.append(OneHotCategoricalStraightThroughValidateArgs(logits=mixed, validate_args=va))
             actions.append(st)
         return tuple(actions), tuple(dists)

@@ -46,6 +46,7 @@ from sheeprl_prey_amd.algos.dreamer_v3.utils import Moments, compute_lambda_valu
 from sheeprl_prey_amd.data.buffers import AsyncReplayBuffer
 from sheeprl_prey_amd.data.tensordict import TensorDict
 from sheeprl_prey_amd.ops.rssm import check_scan_health
+from sheeprl_prey_amd.parallel.collectives import set_phase, step_boundary
 from sheeprl_prey_amd.parallel.flat_optim import flatten_like, build_optimizer
 from sheeprl_prey_amd.parallel.graphs import GraphedStep
 from sheeprl_prey_amd.utils.distribution import OneHotCategoricalValidateArgs
@@ -76,10 +77,10 @@ class DreamerV3Trainer:
 
     Execution:
     * one rank, graphs: ONE hipGraph for the whole step;
-    * N ranks over RCCL, graphs (``fabric.graph_collectives``, default): still ONE hipGraph per rank -
+    * N ranks over RCCL, graphs, ``fabric.graph_collectives=True`` (opt-in): still ONE hipGraph per rank -
       the collectives are captured in it; the world-model buckets launch from the backward hooks and
       overlap the rest of the world-model backward, the actor all-reduce overlaps the critic phase;
-    * N ranks otherwise (gloo, or ``graph_collectives=False``): one hipGraph per phase with the
+    * N ranks otherwise (gloo, or ``graph_collectives=False``, the default): one hipGraph per phase with the
       collectives issued eagerly between replays (for continuous actors the actor phase's backward
       then runs through the imagination graph the previous capture recorded; both captures share one
       memory pool);
@@ -107,6 +108,10 @@ class DreamerV3Trainer:
         self.cont_fast = os.environ.get("SRL_CONT_FAST", "1") != "0"
         self._st: Dict[str, Any] = {}
         self._gather_buf = None
+        # teacher forcing of the eager oracle (tests/test_dv3_step_oracle_gpu.py): {"posteriors" [T,B,S],
+        # "priors" [H+1,M,S], "actions" [H+1,M,A]} one-hot samples of a fused run, taken instead of drawing
+        # (eager discrete path only) so both runs see the same discrete latents / actions
+        self.teacher: Dict[str, Tensor] = None
         ws = runner.world_size
         graphs = bool(runner.cuda_graphs)
         capture_coll = ws > 1 and getattr(runner, "capture_collectives", False)
@@ -135,20 +140,23 @@ class DreamerV3Trainer:
         self.target_flat.lerp_(self.critic_optimizer.flat_param, float(tau))
 
     def train_step(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        step_boundary()
         if self.segmented:
             return self.seg(data)
         return self.graphed(data)
 
     def train_step_sampled(self, rb, batch_size: int, sequence_length: int):
-        """Once the single-graph step is captured: the replay sample is drawn straight into the graph's static
-        inputs by one device launch (``sample_into``) and the step replayed - None (caller samples + calls
-        ``train_step``) otherwise."""
-        g = self.graphed
-        if (self.segmented or g.graph is None or g.static_in is None or not hasattr(rb, "sample_into")
+        """Once the step is captured (single graph, or the per-phase graphs of the segmented mode): the
+        replay sample is drawn straight into the graphs' static inputs by one device launch
+        (``sample_into``) and the step replayed - None (caller samples + calls ``train_step``) otherwise."""
+        g = self.seg if self.segmented else self.graphed
+        ready = g.graphs is not None if self.segmented else g.graph is not None
+        if (not ready or g.static_in is None or not hasattr(rb, "sample_into")
                 or os.environ.get("SRL_FUSED_SAMPLE", "1") == "0"):
             return None
         if not rb.sample_into(g.static_in, batch_size, sequence_length):
             return None
+        step_boundary()
         return g.replay_static()
 
     def _full_step(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:
@@ -165,18 +173,22 @@ class DreamerV3Trainer:
     # ------------------------------------------------------------------ collectives (eager)
     # ``dry=True``: bind buffers only (called between phase captures, no communication)
     def _coll_wm(self, dry: bool = False) -> None:
+        set_phase("coll_wm")
         if not dry:
             self.runner.sync_gradients(self.world_optimizer)
 
     def _coll_actor(self, dry: bool = False) -> None:
+        set_phase("coll_actor")
         if not dry:
             self.runner.sync_gradients(self.actor_optimizer, wait=not self.defer_actor_sync)
 
     def _coll_critic(self, dry: bool = False) -> None:
+        set_phase("coll_critic")
         if not dry:
             self.runner.sync_gradients(self.critic_optimizer)
 
     def _coll_lambda(self, dry: bool = False) -> None:
+        set_phase("coll_lambda")
         lam = self._st["lambda_values"]
         ws = self.runner.world_size
         if ws <= 1:
@@ -210,6 +222,7 @@ class DreamerV3Trainer:
 
     # ------------------------------------------------------------------ phases
     def _phase_wm(self, data: Dict[str, Tensor]) -> None:
+        set_phase("wm")
         cfg = self.cfg
         wm = self.world_model
         st = self._st
@@ -225,8 +238,9 @@ class DreamerV3Trainer:
         is_first[0] = 1.0
         batch_actions = torch.cat((torch.zeros_like(data["actions"][:1]), data["actions"][:-1]), dim=0)
         embedded_obs = wm.encoder(batch_obs)
+        forced = self.teacher["posteriors"] if self.teacher is not None else None
         recurrent_states, posteriors, posteriors_logits, priors_logits = wm.rssm.scan_dynamic(
-            embedded_obs, batch_actions, is_first)
+            embedded_obs, batch_actions, is_first, forced=forced)
         latent_states = torch.cat((posteriors.view(T, B, -1), recurrent_states), -1)
         # the posteriors are exact one-hots: the heads' first layers gather those columns (ops/onehot.py)
         oh = None
@@ -269,6 +283,7 @@ class DreamerV3Trainer:
         st["recurrent_states"] = recurrent_states.detach()
 
     def _phase_imagine(self, data: Dict[str, Tensor]) -> None:
+        set_phase("imagine")
         cfg, st = self.cfg, self._st
         wm, actor, critic = self.world_model, self.actor, self.critic
         wm_cfg = cfg.algo.world_model
@@ -305,7 +320,7 @@ class DreamerV3Trainer:
         with grad_ctx:
             prior = st["posteriors"].reshape(-1, S)
             h = st["recurrent_states"].reshape(-1, H)
-            fast = (not self.is_continuous and prior.is_cuda and wm.rssm.imagine_fast_ok(actor))
+            fast = (not self.is_continuous and prior.is_cuda and wm.rssm.imagine_fast_ok(actor) and self.teacher is None)
             fast_c = (self.is_continuous and self.cont_fast and prior.is_cuda and imagine_cont.supported(wm.rssm, actor))
             if fast_c:
                 imagined_trajectories, imagined_actions_t, pre, roll = imagine_cont.imagine_continuous(
@@ -325,16 +340,23 @@ class DreamerV3Trainer:
                 if self.onehot_heads:
                     st["traj_onehot"] = (res[-1][:, :, len(self.actions_dim):], S // wm_cfg.discrete_size, A, S)
             else:
+                tf = self.teacher if not self.is_continuous else None
+
+                def act(x, t):
+                    if tf is None:
+                        return actor(x)
+                    return actor(x, forced=torch.split(tf["actions"][t], self.actions_dim, -1))
+
                 latent = torch.cat((prior, h), -1)
                 trajectories: List[Tensor] = [latent]
-                actions = torch.cat(actor(latent.detach())[0], dim=-1)
+                actions = torch.cat(act(latent.detach(), 0)[0], dim=-1)
                 imagined_actions: List[Tensor] = [actions]
-                for _ in range(cfg.algo.horizon):
-                    prior, h = wm.rssm.imagination(prior, h, actions)
+                for t in range(cfg.algo.horizon):
+                    prior, h = wm.rssm.imagination(prior, h, actions, forced=tf["priors"][t + 1] if tf is not None else None)
                     prior = prior.reshape(-1, S)
                     latent = torch.cat((prior, h), -1)
                     trajectories.append(latent)
-                    actions = torch.cat(actor(latent.detach())[0], dim=-1)
+                    actions = torch.cat(act(latent.detach(), t + 1)[0], dim=-1)
                     imagined_actions.append(actions)
                 imagined_trajectories = torch.stack(trajectories)
                 imagined_actions_t = torch.stack(imagined_actions)
@@ -361,6 +383,7 @@ class DreamerV3Trainer:
         st["lambda_values"] = lambda_values
 
     def _phase_actor(self, data: Dict[str, Tensor]) -> None:
+        set_phase("actor")
         cfg, st = self.cfg, self._st
         self.actor_optimizer.zero_grad(set_to_none=True)
         rec = st.pop("actor_rec", None)
@@ -412,6 +435,7 @@ class DreamerV3Trainer:
         st["out"]["Loss/policy_loss"] = policy_loss.detach()
 
     def _phase_critic(self, data: Dict[str, Tensor]) -> None:
+        set_phase("critic")
         cfg, st = self.cfg, self._st
         traj = st["imagined_trajectories"].detach()[:-1]
         qv_full = st.pop("critic_logits", None)
@@ -426,6 +450,7 @@ class DreamerV3Trainer:
         st["out"]["Loss/value_loss"] = value_loss.detach()
 
     def _phase_final(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:
+        set_phase("final")
         cfg, st = self.cfg, self._st
         clip = cfg.algo.actor.clip_gradients
         # joins the actor all-reduce left in flight across the critic phase
@@ -627,6 +652,9 @@ def main(runner, cfg: Dict[str, Any]):
                 e1.synchronize()
                 timer.add("Time/train_time", e0.elapsed_time(e1) / 1e3)
             train_events.clear()
+            if device.type == "cuda":
+                # optimiser updates the device skipped since the last log because a kernel recorded a fault
+                runner.log_dict({"Health/skipped_updates": float(ops.skipped_updates(reset=True))}, policy_step)
             rb.check_gather_error()
             check_scan_health()
             runner.log_dict(aggregator.compute(), policy_step)

@@ -245,11 +245,18 @@ class ReplayBuffer:
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self) -> Dict:
         buf = {} if self._buf is None else {k: v.detach().cpu().clone() for k, v in self._buf.items()}
-        return {"buffer": buf, "pos": self._pos, "full": self._full, "buffer_size": self._buffer_size, "n_envs": self._n_envs}
+        sd = {"buffer": buf, "pos": self._pos, "full": self._full, "buffer_size": self._buffer_size, "n_envs": self._n_envs}
+        if hasattr(self, "_draw_seed"):
+            # the device-side sampler's stream position: a resumed run continues the index sequence instead of
+            # replaying the original run's first draws
+            sd["draw_seed"], sd["draw_counter"] = int(self._draw_seed), int(self._draw_counter)
+        return sd
 
     def load_state_dict(self, sd: Dict) -> None:
         if sd["buffer_size"] != self._buffer_size or sd["n_envs"] != self._n_envs:
             raise RuntimeError("replay buffer size mismatch on resume")
+        if "draw_seed" in sd:
+            self._draw_seed, self._draw_counter = int(sd["draw_seed"]), int(sd["draw_counter"])
         data = TensorDict(sd["buffer"], batch_size=[self._buffer_size, self._n_envs])
         if self._buf is None or len(self._buf.keys()) == 0:
             self._ensure_storage(data)
@@ -309,6 +316,13 @@ class SequentialReplayBuffer(ReplayBuffer):
         dev = self._first_device()
         if dev.type != "cuda" or sequence_length < 1:
             return False
+        for k, o in out.items():
+            # the kernel copies rows verbatim: each destination must have the stored dtype and feature shape
+            # (the regular path casts non-uint8 keys to fp32) - otherwise the caller takes the regular path
+            b = self._buf[k]
+            if (o.dtype != b.dtype or tuple(o.shape) != (sequence_length, batch_size) + tuple(b.shape[2:])
+                    or not o.is_contiguous() or o.device != b.device):
+                return False
         if not self._full and self._pos - sequence_length + 1 < 1:
             raise ValueError(f"too long sequence length ({sequence_length})")
         if self._full:
@@ -336,7 +350,8 @@ class SequentialReplayBuffer(ReplayBuffer):
             # zero-fills its row and raises the device error word read by ``check_gather_error``
             err = getattr(self, "_gather_err", None)
             if err is None or err.device != batch_idxes.device:
-                err = self._gather_err = torch.zeros(1, dtype=torch.int32, device=batch_idxes.device)
+                # word 1 of the device's fault block: the flat optimisers skip the update of a step that set it
+                err = self._gather_err = ops.fault_block(batch_idxes.device)[1:2]
             outs = ops._ext().gather_rows([self._buf[k] for k in keys], batch_idxes.reshape(-1).contiguous(),
                                           env_idxes.reshape(-1).contiguous(), err)
             return TensorDict(dict(zip(keys, outs)), batch_size=[batch_idxes.numel()], device=self._buf.device).view(*shape)

@@ -303,11 +303,15 @@ class _UnimixSample(torch.autograd.Function):
 
 
 def unimix_sample(
-    logits: Tensor, classes: int, unimix: float = 0.01, sample: bool = True, uniform: Optional[Tensor] = None
+    logits: Tensor, classes: int, unimix: float = 0.01, sample: bool = True, uniform: Optional[Tensor] = None,
+    forced: Optional[Tensor] = None,
 ) -> Tuple[Tensor, Tensor]:
     """(mixed logits, one-hot sample with straight-through grads | mode one-hot).
 
-    ``logits[..., G*C]`` holds G categoricals of ``classes`` classes each."""
+    ``logits[..., G*C]`` holds G categoricals of ``classes`` classes each.  ``forced``: a given one-hot sample
+    (teacher forcing of the eager oracle, see ``DreamerV3Trainer.teacher``) - always the eager form."""
+    if forced is not None:
+        return ref.unimix_sample(logits, classes, unimix, sample=sample, forced=forced)
     if _native(logits) and logits.dtype == torch.float32 and classes <= 64:
         if sample and uniform is None:
             uniform = torch.rand(logits.numel() // classes, device=logits.device)
@@ -463,30 +467,74 @@ def gae_scan(rewards: Tensor, values: Tensor, dones: Tensor, next_value: Tensor,
 
 
 # =============================================================== flat optimiser
-def flat_grad_norm(grad: Tensor, scalars: Tensor, max_norm: float) -> Tensor:
+_FAULT: dict = {}
+
+
+def fault_block(device) -> Tensor:
+    """The device's fault block, int32 [4]: [0] persistent-scan health (sticky wait-timeout bits),
+    [1] replay-gather error, [2] optimiser updates skipped because [0] or [1] was set, [3] unused.
+    Kernels write [0] / [1]; the flat optimisers' norm / advance kernels read them and skip the update of
+    a faulted step on the device (no host sync); the host reads the block at log time."""
+    key = str(torch.device(device))
+    b = _FAULT.get(key)
+    if b is None:
+        b = _FAULT[key] = torch.zeros(4, dtype=torch.int32, device=device)
+    return b
+
+
+def skipped_updates(reset: bool = False) -> int:
+    """Optimiser updates skipped on the device because of a recorded kernel fault (syncs)."""
+    n = 0
+    for b in _FAULT.values():
+        n += int(b[2].item())
+        if reset:
+            b[2].zero_()
+    return n
+
+
+def _guard_tripped(guard: Optional[Tensor]) -> bool:
+    if guard is None:
+        return False
+    if int(guard[0].item()) | int(guard[1].item()):
+        guard[2] += 1
+        return True
+    return False
+
+
+def flat_grad_norm(grad: Tensor, scalars: Tensor, max_norm: float, guard: Optional[Tensor] = None) -> Tensor:
     if _native(grad):
-        return _ext().flat_grad_norm(grad, scalars, float(max_norm))
+        return _ext().flat_grad_norm(grad, scalars, float(max_norm), guard)
     norm = torch.linalg.vector_norm(grad)
     coef = torch.ones((), device=grad.device)
     if 0 < max_norm < float("inf"):
         coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+    if _guard_tripped(guard):
+        scalars[3] = 1.0
+        return norm
     scalars[0] += 1
     scalars[1] = coef
     scalars[2] = norm
+    scalars[3] = 0.0
     return norm
 
 
-def flat_advance(scalars: Tensor) -> None:
+def flat_advance(scalars: Tensor, guard: Optional[Tensor] = None) -> None:
     if _native(scalars):
-        _ext().flat_advance(scalars)
+        _ext().flat_advance(scalars, guard)
+        return
+    if _guard_tripped(guard):
+        scalars[3] = 1.0
         return
     scalars[0] += 1
     scalars[1] = 1.0
+    scalars[3] = 0.0
 
 
 def flat_adam(p, g, m, v, scalars, lr, b1, b2, eps, wd, decoupled) -> None:
     if _native(p):
         _ext().flat_adam(p, g, m, v, scalars, lr, b1, b2, eps, wd, bool(decoupled))
+        return
+    if float(scalars[3].item()) != 0.0:
         return
     t = float(scalars[0].item())
     coef = scalars[1]
@@ -505,7 +553,7 @@ def flat_adam(p, g, m, v, scalars, lr, b1, b2, eps, wd, decoupled) -> None:
 
 __all__ = [
     "ln_act", "ln_act_nchw", "ln_gru", "unimix_sample", "twohot_nll", "twohot_mean", "twohot_bins", "kl_balance",
-    "lambda_returns", "gae_scan", "flat_grad_norm", "flat_advance", "flat_adam", "native_available", "set_fused",
+    "lambda_returns", "gae_scan", "flat_grad_norm", "flat_advance", "flat_adam", "fault_block", "skipped_updates", "native_available", "set_fused",
 ]
 
 

@@ -9,8 +9,8 @@
 #include "scanp.h"
 
 // ---- launchers (defined in the .hip translation units)
-void launch_flat_grad_norm(const float*, int64_t, float*, int, float*, float*, float, hipStream_t);
-void launch_flat_advance(float*, hipStream_t);
+void launch_flat_grad_norm(const float*, int64_t, float*, int, float*, float*, float, int*, hipStream_t);
+void launch_flat_advance(float*, int*, hipStream_t);
 void launch_flat_adam(float*, const float*, float*, float*, const float*, int64_t, float, float, float, float, float, int,
                       hipStream_t);
 bool launch_ln_act_fwd(const float*, int, float*, int, const float*, const float*, float*, float*, int, int, int, float, int,
@@ -94,21 +94,30 @@ const float* opt_ptr(const c10::optional<torch::Tensor>& t) {
 }
 
 // ------------------------------------------------------------------ optimiser
-torch::Tensor flat_grad_norm(torch::Tensor g, torch::Tensor scalars, double max_norm) {
+int* guard_ptr(const c10::optional<torch::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kInt32 && t->is_contiguous() && t->numel() >= 3,
+              "optimiser guard: contiguous int32 GPU fault block [>= 3]");
+  return t->data_ptr<int>();
+}
+
+torch::Tensor flat_grad_norm(torch::Tensor g, torch::Tensor scalars, double max_norm, c10::optional<torch::Tensor> guard) {
   check_f32(g, "grad");
   check_f32(scalars, "scalars");
+  TORCH_CHECK(scalars.numel() >= 4, "scalars: [step, coef, norm, skip]");
   TORCH_CHECK(g.numel() % 4 == 0, "flat grad numel must be a multiple of 4");
   const int np = 2048;
   auto partial = torch::empty({np}, g.options());
   auto out = torch::empty({}, g.options());
   launch_flat_grad_norm(g.data_ptr<float>(), g.numel(), partial.data_ptr<float>(), np, scalars.data_ptr<float>(),
-                        out.data_ptr<float>(), (float)max_norm, cur_stream());
+                        out.data_ptr<float>(), (float)max_norm, guard_ptr(guard), cur_stream());
   return out;
 }
 
-void flat_advance(torch::Tensor scalars) {
+void flat_advance(torch::Tensor scalars, c10::optional<torch::Tensor> guard) {
   check_f32(scalars, "scalars");
-  launch_flat_advance(scalars.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(scalars.numel() >= 4, "scalars: [step, coef, norm, skip]");
+  launch_flat_advance(scalars.data_ptr<float>(), guard_ptr(guard), cur_stream());
 }
 
 void flat_adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, torch::Tensor scalars, double lr,
@@ -1094,8 +1103,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("unimix_sample_into", &unimix_sample_into, pybind11::arg("logits"), pybind11::arg("uniform"), pybind11::arg("classes"),
         pybind11::arg("alpha"), pybind11::arg("out"), pybind11::arg("idx") = pybind11::none(), pybind11::arg("idx_off") = 0);
   m.doc() = "sheeprl_prey_amd HIP kernels (gfx950)";
-  m.def("flat_grad_norm", &flat_grad_norm);
-  m.def("flat_advance", &flat_advance);
+  m.def("flat_grad_norm", &flat_grad_norm, pybind11::arg("g"), pybind11::arg("scalars"), pybind11::arg("max_norm"),
+        pybind11::arg("guard") = pybind11::none());
+  m.def("flat_advance", &flat_advance, pybind11::arg("scalars"), pybind11::arg("guard") = pybind11::none());
   m.def("flat_adam", &flat_adam);
   m.def("ln_act_fwd", &ln_act_fwd);
   m.def("ln_act_bwd", &ln_act_bwd);

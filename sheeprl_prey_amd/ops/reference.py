@@ -62,14 +62,19 @@ def unimix_logits(logits: Tensor, classes: int, unimix: float) -> Tensor:
 
 
 def unimix_sample(
-    logits: Tensor, classes: int, unimix: float, uniform: Optional[Tensor] = None, sample: bool = True
+    logits: Tensor, classes: int, unimix: float, uniform: Optional[Tensor] = None, sample: bool = True,
+    forced: Optional[Tensor] = None,
 ) -> Tuple[Tensor, Tensor]:
-    """Returns (mixed_logits, one_hot_straight_through_sample or mode)."""
+    """Returns (mixed_logits, one_hot_straight_through_sample or mode).  ``forced`` (one-hot, logits' shape):
+    the sample to take instead of drawing one (teacher forcing of an oracle run, straight-through grads
+    still through these logits' probabilities)."""
     mixed = unimix_logits(logits, classes, unimix)
     shape = mixed.shape
     m = mixed.reshape(-1, classes)
     probs = m.softmax(-1)
-    if sample:
+    if sample and forced is not None:
+        st = forced.reshape(-1, classes).to(probs) + probs - probs.detach()
+    elif sample:
         if uniform is None:
             idx = torch.multinomial(probs.detach(), 1).squeeze(-1)
         else:

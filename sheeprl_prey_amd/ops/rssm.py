@@ -412,10 +412,13 @@ _SPIN_MAX = 0  # 0 = kernel default; tests force tiny bounds to exercise the tim
 def _scan_health_word(device) -> Tensor:
     from sheeprl_prey_amd.ops import _ext
 
+    from sheeprl_prey_amd.ops import fault_block
+
     key = str(device)
     w = _HEALTH.get(key)
     if w is None:
-        w = _HEALTH[key] = torch.zeros(1, dtype=torch.int32, device=device)
+        # word 0 of the device's fault block: the flat optimisers skip the update of a step that set it
+        w = _HEALTH[key] = fault_block(device)[0:1]
     _ext().set_scanp_health(w, _SPIN_MAX)
     return w
 

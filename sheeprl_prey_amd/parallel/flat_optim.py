@@ -186,12 +186,20 @@ class FlatOptimizer:
         if grads:
             torch._foreach_copy_(views, grads)
 
+    def _guard(self) -> Optional[Tensor]:
+        """The device fault block (``ops.fault_block``) the update kernels check: a step during which a kernel
+        recorded a fault (persistent-scan hand-off timeout, out-of-range replay index) leaves the parameters and
+        the Adam moments untouched.  GPU slabs only (the CPU path has no such kernels)."""
+        from sheeprl_prey_amd import ops
+
+        return ops.fault_block(self.flat_param.device) if self.flat_param.is_cuda else None
+
     def clip_grad_norm_(self, max_norm: float) -> Tensor:
         from sheeprl_prey_amd import ops
 
         self.wait_grads()
         self._gather()
-        norm = ops.flat_grad_norm(self.flat_grad, self.scalars, float(max_norm))
+        norm = ops.flat_grad_norm(self.flat_grad, self.scalars, float(max_norm), self._guard())
         self._advanced = True
         return norm
 
@@ -364,7 +372,7 @@ class FlatOptimizer:
         self.wait_grads()
         self._gather()
         if not self._advanced:
-            ops.flat_advance(self.scalars)
+            ops.flat_advance(self.scalars, self._guard())
         self._advanced = False
         self._update()
         return None

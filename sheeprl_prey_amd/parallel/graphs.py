@@ -127,6 +127,14 @@ class SegmentedGraph:
                 self.phase_ms[i] += self._events[2 * i].elapsed_time(self._events[2 * i + 1])
             self.timed_steps += 1
 
+    def replay_static(self) -> Optional[Dict[str, Tensor]]:
+        """Replay the captured phases (and the collectives between them) on whatever the caller wrote into
+        ``static_in``; None before the capture."""
+        if self.graphs is None:
+            return None
+        self._replay_all()
+        return self.static_out
+
     def _run_eager(self, data):
         out = None
         for i, ph in enumerate(self.phases):

@@ -158,7 +158,8 @@ class Runner:
         bucket_mb: float = 32,
         tunable_gemm: str = "use",
         overlap_grad_sync: bool = True,
-        graph_collectives: bool = True,
+        graph_collectives: bool = False,
+        pg_timeout_s: float = 1800,
         process_group=None,
         **_unused,
     ) -> None:
@@ -174,19 +175,28 @@ class Runner:
         self.callbacks = list(callbacks or [])
         self._loggers = list(loggers or [])
         self.cuda_graphs = bool(cuda_graphs) and self.accelerator == "cuda"
+        # fabric.fused_ops=False routes every op through the eager fp32 oracles (ops/reference.py)
         self.fused_ops = bool(fused_ops)
+        from sheeprl_prey_amd import ops as _ops
+
+        _ops.set_fused(self.fused_ops)
         self.bucket_mb = float(bucket_mb)
         # bucketed all-reduce launched from backward hooks (FlatOptimizer.enable_overlap)
         self.overlap_grad_sync = bool(overlap_grad_sync)
         # multi-rank hipGraph steps: capture the RCCL collectives INSIDE the one step graph (N ranks replay
-        # one graph each, like N=1) instead of per-phase graphs with eager collectives in between
+        # one graph each, like N=1) instead of per-phase graphs with eager collectives in between.  Off by
+        # default: the segmented mode issues its collectives eagerly (the process group's timeout watches
+        # them); the captured mode has only run on 1-rank communicators (RCCL refuses 2 ranks on one GPU)
         self.graph_collectives = bool(graph_collectives)
+        # process-group timeout: a stalled collective ends the run with an error instead of holding the node
+        self.pg_timeout_s = float(pg_timeout_s)
         # library-GEMM solution choice (parallel/gemm_tuning.py): committed TunableOp results
         self.tunable_gemm = str(tunable_gemm)
         self._kwargs = dict(
             devices=devices, num_nodes=num_nodes, strategy=strategy, accelerator=accelerator,
             precision=precision, callbacks=callbacks, cuda_graphs=cuda_graphs, fused_ops=fused_ops, bucket_mb=bucket_mb,
             tunable_gemm=tunable_gemm, overlap_grad_sync=overlap_grad_sync, graph_collectives=graph_collectives,
+            pg_timeout_s=pg_timeout_s,
         )
         self.group = process_group  # None == WORLD
         if str(strategy).lower() in ("fsdp",):
@@ -256,7 +266,9 @@ class Runner:
 
             configure(self.tunable_gemm)
         if ws > 1 and not dist.is_initialized():
-            kwargs = dict(backend=self.backend, timeout=datetime.timedelta(minutes=30))
+            # RCCL errors / timeouts tear the process down (non-zero exit) rather than leaving it blocked
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+            kwargs = dict(backend=self.backend, timeout=datetime.timedelta(seconds=max(10.0, self.pg_timeout_s)))
             if self.accelerator == "cuda" and self.backend == "nccl":
                 kwargs["device_id"] = self.device
             dist.init_process_group(**kwargs)

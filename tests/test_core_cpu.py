@@ -293,3 +293,30 @@ def test_bf16_mixed_setup_module_hooks():
     torch.testing.assert_close(c(x), y.detach())
     with pytest.raises(ValueError):
         Runner(precision="64-true")
+
+
+def test_optimizer_fault_guard_skips_update_eager():
+    """The fault-block contract of the flat optimiser kernels (``ops/csrc/optim.hip``), on the eager oracle:
+    with word 0 (scan health) or 1 (gather error) set, norm/advance flag the step as skipped, count it in word 2
+    and Adam leaves the parameters, moments and step count untouched; a clean block updates as usual."""
+    from sheeprl_prey_amd import ops
+
+    torch.manual_seed(0)
+    p, g = torch.randn(16), torch.randn(16)
+    m, v = torch.zeros(16), torch.zeros(16)
+    scalars = torch.tensor([0.0, 1.0, 0.0, 0.0])
+    guard = torch.zeros(4, dtype=torch.int32)
+    for word in (0, 1):
+        guard[word] = 4
+        p0 = p.clone()
+        ops.flat_grad_norm(g, scalars, 1.0, guard)
+        ops.flat_adam(p, g, m, v, scalars, 1e-2, 0.9, 0.999, 1e-8, 0.0, False)
+        assert torch.equal(p, p0) and float(scalars[0]) == 0.0 and float(scalars[3]) == 1.0
+        ops.flat_advance(scalars, guard)
+        assert float(scalars[0]) == 0.0
+        guard[word] = 0
+    assert int(guard[2]) == 4
+    ops.flat_grad_norm(g, scalars, 1.0, guard)
+    ops.flat_adam(p, g, m, v, scalars, 1e-2, 0.9, 0.999, 1e-8, 0.0, False)
+    assert float(scalars[0]) == 1.0 and float(scalars[3]) == 0.0 and not torch.equal(p, p0)
+    assert int(guard[2]) == 4

@@ -186,7 +186,7 @@ def test_imagine_discrete_matches_reference_loop(monkeypatch):
     feed = iter([U[t, :M] if i == 0 else U[t, M:] for t in range(Hz + 1) for i in range(2)])
     real = ops.unimix_sample
 
-    def fed(logits, classes, unimix=0.01, sample=True, uniform=None):
+    def fed(logits, classes, unimix=0.01, sample=True, uniform=None, forced=None):
         return real(logits, classes, unimix, sample=sample, uniform=next(feed) if sample else None)
 
     monkeypatch.setattr(ops, "unimix_sample", fed)
@@ -295,15 +295,28 @@ def test_persistent_scan_timeout_is_loud():
     tr.train_step(data)
     torch.cuda.synchronize()
     assert R.check_scan_health() == 0
+    from sheeprl_prey_amd import ops
+
+    ops.skipped_updates(reset=True)
+    opts = (tr.world_optimizer, tr.actor_optimizer, tr.critic_optimizer)
     try:
         R.set_scan_spin_max(1)
+        before = [(o.flat_param.clone(), o.exp_avg.clone(), o.exp_avg_sq.clone(), float(o.scalars[0])) for o in opts]
         tr.train_step(data)
         torch.cuda.synchronize()
+        # the faulted step's updates were skipped on the device: weights, moments and step counts bit-unchanged
+        for o, (p, m, v, t) in zip(opts, before):
+            assert torch.equal(o.flat_param, p) and torch.equal(o.exp_avg, m) and torch.equal(o.exp_avg_sq, v)
+            assert float(o.scalars[0]) == t
+        assert ops.skipped_updates(reset=True) == 3
         with pytest.raises(RuntimeError, match="hand-off wait timed out"):
             R.check_scan_health()
     finally:
         R.set_scan_spin_max(0)
     assert R.check_scan_health() == 0  # the check cleared the word
+    p0 = tr.world_optimizer.flat_param.clone()
     tr.train_step(data)
     torch.cuda.synchronize()
     assert R.check_scan_health() == 0
+    assert not torch.equal(tr.world_optimizer.flat_param, p0)  # healthy again: the update is applied
+    assert ops.skipped_updates() == 0
