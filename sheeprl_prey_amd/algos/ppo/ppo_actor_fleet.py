@@ -10,6 +10,12 @@ rank 1..N-1 - actors: own ``env.num_envs`` envs each and a full agent copy (the 
          on the actor with the HIP reverse scan), collect ``rollout_steps`` x ``num_envs``
          transitions with the current weights, then wait for the next weights (on-policy).
 
+``algo.weight_lag`` (default 0 = the reference's on-policy order, ``ppo_decoupled.py:36-349``): with
+lag L >= 1 an actor does not wait for the weights of the update its rollout feeds - it posts the
+broadcast receive asynchronously into a second weight buffer and starts the next rollout at once with
+the weights it has (at most L updates old); the learner's update and the broadcast then overlap the
+actors' next rollout instead of idling them.
+
 Transport: a rollout is TWO fixed-shape slabs per actor - uint8 (pixel observations, never widened
 to fp32 on the wire) and fp32 (vector observations, actions, log-probs, values, returns,
 advantages, and three episode statistics) - gathered with ONE ``dist.gather`` each (RCCL over
@@ -158,6 +164,9 @@ def actor_fleet(runner, cfg: Dict[str, Any], log_dir: str) -> None:
     u8_dev = u8 if wire == device else torch.zeros_like(u8, device=device)
     f32_dev = f32 if wire == device else torch.zeros_like(f32, device=device)
     t_gather = t_bcast = 0.0
+    lag = int(cfg.algo.get("weight_lag", 0) or 0)
+    # lag >= 1: in-flight weight receives (oldest first), each into its own buffer
+    inflight: List[Tuple[Any, Tensor]] = []
     for update in range(1, num_updates + 1):
         t0 = time.perf_counter()
         roll = dict(roll_fn())
@@ -198,8 +207,17 @@ def actor_fleet(runner, cfg: Dict[str, Any], log_dir: str) -> None:
             dist.gather(u8, None, dst=LEARNER)
         dist.gather(f32, None, dst=LEARNER)
         t2 = time.perf_counter()
-        dist.broadcast(flat, src=LEARNER)
-        vector_to_params(flat.to(device), params)
+        if lag <= 0:
+            dist.broadcast(flat, src=LEARNER)
+            vector_to_params(flat.to(device), params)
+        else:
+            buf = torch.empty_like(flat)
+            inflight.append((dist.broadcast(buf, src=LEARNER, async_op=True), buf))
+            # keep at most ``lag`` updates in flight: the oldest weights are applied before the next rollout
+            while len(inflight) > lag or (update == num_updates and inflight):
+                work, got = inflight.pop(0)
+                work.wait()
+                vector_to_params(got.to(device), params)
         t_gather, t_bcast = t2 - t1, time.perf_counter() - t2
     if denv is None:
         envs.close()

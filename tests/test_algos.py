@@ -201,6 +201,20 @@ def test_ppo_actor_fleet(devices, env_id):
     _check_ckpt("ppo_fleet", f"{env_id}{devices}", PPO_KEYS, False)
 
 
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("lag", [1, 2])
+def test_ppo_actor_fleet_weight_lag(lag):
+    """``algo.weight_lag``: the actors post the weight receives asynchronously and keep rolling out with weights
+    up to ``lag`` updates old; over several updates the collective counts must still match (no hang) and the
+    learner finishes and checkpoints."""
+    n_updates = 4
+    _run(["env.num_envs=1", "env.sync_env=True", "env.capture_video=False", "exp=ppo_decoupled",
+          "algo.topology=actor_fleet", "env=dummy", "env.id=discrete_dummy", "algo.rollout_steps=4", "per_rank_batch_size=4",
+          "algo.update_epochs=1", f"algo.weight_lag={lag}", f"total_steps={4 * 2 * n_updates}", "metric.log_every=8",
+          "checkpoint.every=1000000", "root_dir=ppo_fleet_lag", f"run_name=l{lag}"], 3)
+    _check_ckpt("ppo_fleet_lag", f"l{lag}", PPO_KEYS, False)
+
+
 @pytest.mark.timeout(180)
 @pytest.mark.parametrize("devices", [1, 2])
 def test_ppo_recurrent(devices):
