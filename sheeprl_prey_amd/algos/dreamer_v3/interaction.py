@@ -14,7 +14,9 @@ Order of effects vs the reference (act / add / env step / add reset rows / train
 uses the trained weights, as there; the gradient steps are launched BEFORE the env step so the CPU
 env step overlaps them.  Divergence: the reset rows (final obs, ``done=1``) of episodes that end at
 this env step are added after this step's gradient launch, so they reach training one step later
-than in the reference.  CPU runs keep the same order in serial form.
+than in the reference (a sequence sample covers the newest row with probability ~ B*L / buffer
+length).  ``algo.interaction_serial_order=True`` restores the reference's order exactly: the
+gradient steps run after the env step and the reset rows (no CPU/GPU overlap).
 
 ``last_train_host_s`` is the host time spent inside ``train_fn`` during the last ``step``; callers
 timing the env interaction subtract it (the reference times interaction and training separately,
@@ -45,6 +47,8 @@ class InteractionLoop:
         self.obs_keys = self.cnn_keys + self.mlp_keys
         self.row_keys = self.obs_keys + ["rewards", "dones", "is_first"]
         self.pipelined = self.device.type == "cuda"
+        # reference effect order (act, add, env step, add reset rows, train) instead of training before the env step
+        self.serial_order = bool(cfg.algo.get("interaction_serial_order", False))
         self.step_data = TensorDict({}, batch_size=[self.ne], device="cpu")
         self._slot = 0
         self._ring: List[Dict[str, torch.Tensor]] = []
@@ -149,6 +153,9 @@ class InteractionLoop:
         cfg, ne = self.cfg, self.ne
         train_fn = self._timed(train_fn)
         self.last_train_host_s = 0.0
+        deferred = None
+        if self.serial_order:
+            deferred, train_fn = train_fn, None
         if random_actions:
             real, acts = self._random_actions()
             self.step_data["actions"] = torch.from_numpy(np.asarray(acts, dtype=np.float32)).view(ne, -1)
@@ -209,4 +216,6 @@ class InteractionLoop:
             sd["dones"][idxes] = 0.0
             sd["is_first"][idxes] = 1.0
             self.player.init_states(idxes)
+        if deferred is not None:
+            self.last_train_out = deferred()
         return infos

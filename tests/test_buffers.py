@@ -235,3 +235,42 @@ def test_replay_buffer_whole_buffer_adds_after_full():
     rb.add(TensorDict({"a": torch.full((1, 2, 1), 9.0)}, batch_size=[1, 2]))
     rb.add(TensorDict({"a": torch.arange(4.0).view(4, 1, 1).expand(4, 2, 1)}, batch_size=[4, 2]))
     assert rb["a"][:, 0, 0].tolist() == [3.0, 0.0, 1.0, 2.0] and rb._pos == 1
+
+
+@pytest.mark.parametrize("serial", [False, True])
+def test_dv3_interaction_order_of_reset_rows(serial):
+    """``InteractionLoop`` effect order (reference ``dreamer_v3.py:609-709``: act, add the row, env step, add the
+    reset rows of finished episodes, then train).  The default launches the gradient steps before the env step
+    (so they overlap it): the reset row of an episode ending at this step reaches the replay buffer after that
+    step's training.  ``algo.interaction_serial_order=True`` gives the reference order: training sees it."""
+    from sheeprl_prey_amd.algos.dreamer_v3.interaction import InteractionLoop
+    from sheeprl_prey_amd.config.compose import compose
+    from sheeprl_prey_amd.data.buffers import AsyncReplayBuffer
+    from sheeprl_prey_amd.parallel.runner import Runner
+    from sheeprl_prey_amd.utils.env import make_env, make_vector_env
+    from sheeprl_prey_amd.utils.utils import dotdict
+
+    cfg = dotdict(compose(["exp=dreamer_v3", "env=dummy", "env.id=discrete_dummy", "env.num_envs=1", "env.sync_env=True",
+                           "env.capture_video=False", "cnn_keys.encoder=[rgb]", f"algo.interaction_serial_order={serial}"]))
+    runner = Runner(accelerator="cpu")
+    envs = make_vector_env(cfg, [make_env(cfg, 0, 0, None, "train", 0)])
+
+    class _Player:
+        def init_states(self, *a):
+            pass
+
+    rb = AsyncReplayBuffer(64, 1, device="cpu", sequential=True)
+    loop = InteractionLoop(runner, cfg, envs, _Player(), rb, [2], False)
+    loop.reset(0)
+    seen = []
+
+    def train():
+        b = rb.buffer[0]
+        seen.append(float(b["dones"][: b._pos].sum()))
+        return None
+
+    for _ in range(5):  # the dummy episode ends at the 5th env step (4 steps + the terminal one)
+        loop.step(True, train)
+    envs.close()
+    # dones rows in the buffer when the 5th step's training ran: the reset row only in the serial order
+    assert seen[-1] == (1.0 if serial else 0.0), seen
