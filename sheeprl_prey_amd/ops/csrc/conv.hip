@@ -23,6 +23,7 @@
 // side: a power of two below 32); all host-checked.
 #include "common.h"
 #include "conv.h"
+#include <string>
 
 #ifndef NARROW_DEFAULT
 #define NARROW_DEFAULT 1  // measured: 128x64 tiles for 64 channels -1.4% on the stack, 128x32 no gain
@@ -1223,9 +1224,133 @@ __global__ __launch_bounds__(256) void up_small2_kernel(const float* __restrict_
   }
 }
 
+// The final ConvTranspose2d (Ca -> CO <= 4 image channels, k4 s2 p1) on MFMA, input-centric: for every small-grid
+// pixel (p, q) the 16 taps x CO outputs it feeds are ONE row of a dense GEMM
+//     C[(p,q)][tap * CO + co] = sum_a P[p,q,a] W[a][co][tap]        (M = pixels, N = 16 CO, K = Ca)
+// so N = 48 for RGB fills three 16-wide MFMA tiles exactly (the output-centric form would pad N = CO to 16),
+// and no K entry is a structural zero.  A workgroup owns a 16 x 16 small-pixel tile of one image: it stages the
+// 18 x 18 halo window (32 channels per pass) in LDS, runs the window's 21 x CO 16x16 tiles on
+// v_mfma_f32_16x16x4_f32 (B fragments - the packed weights - held in registers for the whole pass), parks C in
+// LDS over the dead window, and each thread then sums the 4 (tap, neighbour) contributions of each of its 2 x 2
+// x CO output pixels (col2im) and writes the NCHW image rows as float2.
+template <int CO>
+__global__ __launch_bounds__(256) void up_last_mfma_kernel(const float* __restrict__ P, const float* __restrict__ W,
+                                                           const float* __restrict__ bias, float c0, float* __restrict__ out,
+                                                           int SH, int SW, int CA) {
+  static_assert(CO >= 1 && CO <= 4, "up_last_mfma: CO <= 4");
+  constexpr int T = 16, TH = T + 2, NPIX = TH * TH;  // 324 window pixels
+  constexpr int MT = (NPIX + 15) / 16;               // 21 M tiles
+  constexpr int MPW = (MT + 3) / 4;                  // M tiles per wave
+  constexpr int LDA = 36, LDC = 16 * CO + 1;
+  constexpr int LDS_A = MT * 16 * LDA, LDS_C = MT * 16 * LDC;
+  __shared__ float sm[LDS_A > LDS_C ? LDS_A : LDS_C];
+  const int tiles_x = SW / T;
+  const int n = blockIdx.y, ty0 = (blockIdx.x / tiles_x) * T, tx0 = (blockIdx.x % tiles_x) * T;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+  f4 acc[MPW][CO];
+#pragma unroll
+  for (int m = 0; m < MPW; ++m)
+#pragma unroll
+    for (int t = 0; t < CO; ++t) acc[m][t] = zero4();
+  for (int a0 = 0; a0 < CA; a0 += 32) {
+    __syncthreads();  // the previous pass's A reads are done
+    for (int e = threadIdx.x; e < MT * 16 * 8; e += 256) {
+      const int r = e >> 3, q4 = (e & 7) * 4;
+      f4 v = zero4();
+      if (r < NPIX) {
+        const int p = ty0 - 1 + r / TH, q = tx0 - 1 + r % TH;
+        if (p >= 0 && p < SH && q >= 0 && q < SW) v = *(const f4*)(P + (((size_t)n * SH + p) * SW + q) * CA + a0 + q4);
+      }
+      *(f4*)(sm + r * LDA + q4) = v;
+    }
+    // B fragments: lane (i, g) of MFMA j in K chunk c holds B[k = a0 + 16c + 4g + j][col = 16t + i], col = tap * CO + co
+    float b[2][CO][4];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int t = 0; t < CO; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int col = 16 * t + i, tap = col / CO, co = col - tap * CO;
+          b[c][t][j] = W[((size_t)(a0 + 16 * c + 4 * g + j) * CO + co) * 16 + tap];
+        }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MPW; ++m) {
+      const int mt = w + 4 * m;
+      if (mt < MT) {  // wave-uniform
+        const float* arow = sm + (mt * 16 + i) * LDA + 4 * g;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const f4 a = *(const f4*)(arow + 16 * c);
+#pragma unroll
+          for (int t = 0; t < CO; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[c][t][j], acc[m][t], 0, 0, 0);
+        }
+      }
+    }
+  }
+  __syncthreads();  // every wave's A reads are done: C overwrites the window
+#pragma unroll
+  for (int m = 0; m < MPW; ++m) {
+    const int mt = w + 4 * m;
+    if (mt < MT) {
+#pragma unroll
+      for (int t = 0; t < CO; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sm[(mt * 16 + 4 * g + e) * LDC + 16 * t + i] = acc[m][t][e];
+    }
+  }
+  __syncthreads();
+  // col2im: thread = small pixel (u, v); output (2u + cy, 2v + cx) sums taps (1 - cy + 2th, 1 - cx + 2tw) of the
+  // small pixels (u + cy - th, v + cx - tw), th, tw in {0, 1}
+  const int u = threadIdx.x >> 4, v = threadIdx.x & 15;
+  const int LH = 2 * SH, LW = 2 * SW;
+#pragma unroll
+  for (int co = 0; co < CO; ++co) {
+    const float bb = (bias ? bias[co] : 0.f) + c0;
+#pragma unroll
+    for (int cy = 0; cy < 2; ++cy) {
+      float o[2];
+#pragma unroll
+      for (int cx = 0; cx < 2; ++cx) {
+        float s = bb;
+#pragma unroll
+        for (int th = 0; th < 2; ++th)
+#pragma unroll
+          for (int tw = 0; tw < 2; ++tw) {
+            const int r = (u + cy - th + 1) * TH + (v + cx - tw + 1);
+            const int tap = (1 - cy + 2 * th) * 4 + (1 - cx + 2 * tw);
+            s += sm[r * LDC + tap * CO + co];
+          }
+        o[cx] = s;
+      }
+      *(float2*)(out + (((size_t)n * CO + co) * LH + 2 * (ty0 + u) + cy) * LW + 2 * (tx0 + v)) = make_float2(o[0], o[1]);
+    }
+  }
+}
+
+// final-layer form: 0 = MFMA, 1 = the VALU kernels below (default until measured on the box; SRL_UP_LAST=mfma|valu)
+static int g_up_last_form = [] {
+  const char* e = getenv("SRL_UP_LAST");
+  return (e && std::string(e) == "mfma") ? 0 : 1;
+}();
+void set_up_last_form(int f) { g_up_last_form = f; }
+
 bool launch_up_small(const float* P, const float* W, const float* bias, float c0, float* out, int N, int SH, int SW, int Ca,
                      int CO, hipStream_t st) {
   if (SH % 16 || SW % 16 || CO < 1 || CO > 4 || Ca % 32 != 0) return false;
+  if (g_up_last_form == 0) {
+    dim3 g1((SH / 16) * (SW / 16), N);
+    switch (CO) {
+      case 1: hipLaunchKernelGGL((up_last_mfma_kernel<1>), g1, dim3(256), 0, st, P, W, bias, c0, out, SH, SW, Ca); break;
+      case 2: hipLaunchKernelGGL((up_last_mfma_kernel<2>), g1, dim3(256), 0, st, P, W, bias, c0, out, SH, SW, Ca); break;
+      case 3: hipLaunchKernelGGL((up_last_mfma_kernel<3>), g1, dim3(256), 0, st, P, W, bias, c0, out, SH, SW, Ca); break;
+      default: hipLaunchKernelGGL((up_last_mfma_kernel<4>), g1, dim3(256), 0, st, P, W, bias, c0, out, SH, SW, Ca); break;
+    }
+    return true;
+  }
   if (SH % 32 == 0 && SW % 32 == 0 && Ca <= 512) {  // 122.5 vs 134 us at 1024 x 32x32x32 -> 3 channels
     dim3 g2((SH / 32) * (SW / 32), N);
     const size_t lds = (size_t)Ca * 16 * sizeof(f4);

@@ -20,6 +20,7 @@ void launch_to_nhwc4(const void*, bool, float*, int, int, int, float, hipStream_
 bool launch_ln_bwd_flat(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
                         float*, int, int, int, int, hipStream_t);
 bool launch_up_small(const float*, const float*, const float*, float, float*, int, int, int, int, int, hipStream_t);
+void set_up_last_form(int);
 bool conv_channels_supported(int);
 
 namespace {
@@ -300,5 +301,6 @@ void register_conv(pybind11::module& m) {
   m.def("conv_to_nhwc4", &conv_to_nhwc4);
   m.def("conv_ln_bwd_flat", &conv_ln_bwd_flat);
   m.def("conv_up_small", &conv_up_small);
+  m.def("set_up_last_form", &set_up_last_form);  // 0 = MFMA final ConvT (default), 1 = VALU (A/B, tests)
   m.def("conv_small_encoder", &conv_small_encoder);
 }

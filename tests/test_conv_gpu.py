@@ -68,15 +68,21 @@ def test_wgrad_matches_autograd(cin, cout, hw, n):
     _close(dw, w.grad, rtol=5e-4, atol=5e-4)
 
 
-@pytest.mark.parametrize("ca,co,hw", [(32, 3, 32), (96, 3, 32), (64, 1, 64), (128, 4, 16), (64, 2, 32)])
-def test_up_small_matches_conv_transpose(ca, co, hw):
+@pytest.mark.parametrize("form", [0, 1])
+@pytest.mark.parametrize("ca,co,hw", [(32, 3, 32), (96, 3, 32), (64, 1, 64), (128, 4, 16), (64, 2, 32), (32, 3, 48)])
+def test_up_small_matches_conv_transpose(ca, co, hw, form):
+    """The decoder's final ConvTranspose2d: form 0 = input-centric MFMA kernel (default), 1 = VALU form."""
     C = ops._ext()
     torch.manual_seed(0)
-    x = torch.randn(2, ca, hw, hw, device=DEV)
+    x = torch.randn(3, ca, hw, hw, device=DEV)
     w = torch.randn(ca, co, 4, 4, device=DEV) * 0.1
     b = torch.randn(co, device=DEV)
     ref = F.conv_transpose2d(x, w, b, stride=2, padding=1) + 0.5
-    out = C.conv_up_small(_nhwc(x), w, b, 0.5)
+    C.set_up_last_form(form)
+    try:
+        out = C.conv_up_small(_nhwc(x), w, b, 0.5)
+    finally:
+        C.set_up_last_form(1)
     _close(out, ref)
 
 
