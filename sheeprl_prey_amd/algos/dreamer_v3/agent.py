@@ -297,6 +297,7 @@ class RSSM(nn.Module):
 
     # ---- MI355X imagination: buffer-resident no-grad rollout ---------------------------
     _actor_tail_ok = os.environ.get("SRL_ACTOR_TAIL", "1") != "0"  # A/B switch of the fused rollout actor tail
+    _merge_h_ok = os.environ.get("SRL_IMAG_MERGE", "1") != "0"  # A/B switch of the merged h_{t+1} GEMM (imagine_discrete)
 
     def imagine_fast_ok(self, actor) -> bool:
         gru = self.recurrent_model.rnn
@@ -385,18 +386,33 @@ class RSSM(nn.Module):
         if trunk_rec is not None and a_table is not None:
             trunk_rec.onehot = (IDX[:, :, nh:], G, A, S)  # the trunk backward scatters the prior columns' dW
         one_head = nh == 1 and self._actor_tail_ok
+        # every GEMM reading h_{t+1} as ONE: the transition's first layer, the actor trunk's dense first-layer part
+        # (used at step t+1) and the h half of step t+1's GRU input projection - [M, Hd] x [Hd, Ntr + Na + 3H]; the
+        # GRU then multiplies only x_{t+1} (K = D) and the LN-GRU kernel adds the two parts
+        tr_sp = oh.mlp_split(self.transition_model)
+        merge = (self._merge_h_ok and use_gather and a_table is not None and layers is not None and gru.linear.bias is None
+                 and tr_sp is not None and tr_sp[1] is not None and tr_sp[0].bias is None and len(tr_sp[2]) > 0)
+        if merge:
+            tr_lin, tr_ln, tr_rest = tr_sp
+            Ntr, Na = tr_lin.out_features, a0.out_features
+            Wm = torch.cat((tr_lin.weight, a0.weight[:, S:], Wg[:, :Hd]), 0)
+            Wgx_t = Wg[:, Hd:].t()
+            hm = torch.mm(h, Wm.t())
+            ytr, mtr, rtr = post.new_empty(M, Ntr), post.new_empty(M), post.new_empty(M)
+            tr_act = ops._act_code(tr_ln.act)
         for t in range(horizon + 1):
             traj_t = buf[t, :, Ap:Ap + S + Hd]
             # single-head actors: last LayerNorm + head + unimix sample in one kernel (TrunkRecord.step tail)
             tail = ((actor.mlp_heads[0], U[t, :M], float(actor._unimix), buf[t, :, :A], IDX[t, :, :1], 0)
                     if one_head else None)
+            ga = ((IDX[t, :, nh:], G, A, S, a_table) + ((hm[:, Ntr:Ntr + Na],) if merge else ())
+                  if a_table is not None else None)
             if trunk_rec is not None:
-                out = trunk_rec.step(t, traj_t, gather=(IDX[t, :, nh:], G, A, S, a_table) if a_table is not None else None,
-                                     tail=tail)
+                out = trunk_rec.step(t, traj_t, gather=ga, tail=tail)
             elif layers is not None and a_table is not None:
                 if act_scratch is None:
                     act_scratch = TrunkRecord(layers, 1, M, dev)
-                out = act_scratch.step(0, traj_t, gather=(IDX[t, :, nh:], G, A, S, a_table), tail=tail)
+                out = act_scratch.step(0, traj_t, gather=ga, tail=tail)
             else:
                 out = actor.model(traj_t)
             c0 = 0
@@ -419,11 +435,24 @@ class RSSM(nn.Module):
                 for m in list(self.recurrent_model.mlp.model)[1:]:
                     x = m(x)
                 xs.copy_(x)
-            gx = torch.mm(buf[t, :, Ap + S:Ap + S + Hd + D], Wg.t())  # (h | x) in one GEMM
-            if gru.linear.bias is not None:
-                gx = gx + gru.linear.bias
-            C.ln_gru_into(gx, buf[t, :, Ap + S:Ap + S + Hd], ln.weight, ln.bias, float(ln.eps), buf[t + 1, :, Ap + S:Ap + S + Hd])
-            logits = self.transition_model(buf[t + 1, :, Ap + S:Ap + S + Hd])
+            if merge:
+                # x half of the GRU input projection; the h half is the last block of hm (h_t)
+                gx = torch.mm(xs, Wgx_t)
+                C.ln_gru_into(gx, buf[t, :, Ap + S:Ap + S + Hd], ln.weight, ln.bias, float(ln.eps),
+                              buf[t + 1, :, Ap + S:Ap + S + Hd], x2=hm[:, Ntr + Na:])
+                torch.mm(buf[t + 1, :, Ap + S:Ap + S + Hd], Wm.t(), out=hm)
+                C.ln_act_fwd_into(hm, hm.stride(0), ytr, Ntr, tr_ln.weight, tr_ln.bias, mtr, rtr, M, Ntr, 1,
+                                  float(tr_ln.eps), tr_act)
+                logits = ytr
+                for m in tr_rest:
+                    logits = m(logits)
+            else:
+                gx = torch.mm(buf[t, :, Ap + S:Ap + S + Hd + D], Wg.t())  # (h | x) in one GEMM
+                if gru.linear.bias is not None:
+                    gx = gx + gru.linear.bias
+                C.ln_gru_into(gx, buf[t, :, Ap + S:Ap + S + Hd], ln.weight, ln.bias, float(ln.eps),
+                              buf[t + 1, :, Ap + S:Ap + S + Hd])
+                logits = self.transition_model(buf[t + 1, :, Ap + S:Ap + S + Hd])
             C.unimix_sample_into(logits.contiguous(), U[t, nh * M:], disc, float(self.unimix), buf[t + 1, :, Ap:Ap + S],
                                  IDX[t + 1, :, nh:], A)
         out = (buf[:, :, Ap:Ap + S + Hd], buf[:, :, :A])

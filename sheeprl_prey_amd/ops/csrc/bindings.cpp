@@ -32,7 +32,7 @@ int ln_nchw_splits(int, int);
 void launch_ln_nchw_bwd(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
                         float*, float*, float*, int, int, int, int, hipStream_t);
 bool launch_ln_gru_fwd(const float*, const float*, int, const float*, const float*, float*, float*, float*, int, int, float,
-                       hipStream_t, int ldo = 0);
+                       hipStream_t, int ldo = 0, const float* x2 = nullptr, int ldx2 = 0);
 int ln_gru_bwd_grid(int);
 bool launch_ln_gru_bwd(const float*, const float*, int, const float*, const float*, const float*, const float*, const float*,
                        float*, float*, float*, float*, float*, float*, int, int, hipStream_t);
@@ -777,7 +777,7 @@ std::vector<int64_t> scanp_info(int64_t B, int64_t S, int64_t D, int64_t H, int6
 // out must have unit stride in its last dim; rows may be strided.
 // ``mean`` / ``rstd`` (optional [M]): keep the LayerNorm row statistics (for a later ln_gru_bwd_into).
 void ln_gru_into(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::Tensor beta, double eps, torch::Tensor out,
-                 c10::optional<torch::Tensor> mean_out, c10::optional<torch::Tensor> rstd_out) {
+                 c10::optional<torch::Tensor> mean_out, c10::optional<torch::Tensor> rstd_out, c10::optional<torch::Tensor> x2) {
   check_f32(x, "x");
   check_f32(gamma, "gamma");
   check_f32(beta, "beta");
@@ -785,13 +785,22 @@ void ln_gru_into(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::T
               "ln_gru_into: h/out must be row-strided 2-D views");
   const int H = h.size(1), M = h.size(0);
   TORCH_CHECK(x.numel() == (int64_t)M * 3 * H && out.size(0) == M && out.size(1) == H, "ln_gru_into: shapes");
+  const float* x2p = nullptr;
+  int64_t ldx2 = 0;
+  if (x2.has_value() && x2->defined()) {  // gx = x + x2: the two parts of a split GRU input GEMM
+    TORCH_CHECK(x2->is_cuda() && x2->scalar_type() == torch::kFloat32 && x2->dim() == 2 && x2->size(0) == M &&
+                    x2->size(1) == 3 * H && x2->stride(1) == 1,
+                "ln_gru_into: x2 must be a row-strided float32 [M, 3H] view");
+    x2p = x2->data_ptr<float>();
+    ldx2 = x2->stride(0);
+  }
   const bool keep = mean_out.has_value() && mean_out->defined() && rstd_out.has_value() && rstd_out->defined();
   if (keep) TORCH_CHECK(mean_out->numel() == M && rstd_out->numel() == M, "ln_gru_into: mean/rstd must hold M rows");
   auto mean = keep ? *mean_out : torch::empty({M}, x.options());
   auto rstd = keep ? *rstd_out : torch::empty({M}, x.options());
   bool ok = launch_ln_gru_fwd(x.data_ptr<float>(), h.data_ptr<float>(), h.stride(0), gamma.data_ptr<float>(),
                               beta.data_ptr<float>(), out.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                              M, H, (float)eps, cur_stream(), out.stride(0));
+                              M, H, (float)eps, cur_stream(), out.stride(0), x2p, (int)ldx2);
   TORCH_CHECK(ok, "ln_gru_into: unsupported hidden size ", H);
 }
 
@@ -1094,7 +1103,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_ext(m);
   m.def("ln_gru_into", &ln_gru_into, pybind11::arg("x"), pybind11::arg("h"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("eps"), pybind11::arg("out"), pybind11::arg("mean") = pybind11::none(),
-        pybind11::arg("rstd") = pybind11::none());
+        pybind11::arg("rstd") = pybind11::none(), pybind11::arg("x2") = pybind11::none());
   m.def("colsum", &colsum);
   m.def("cartpole_step", &cartpole_step);
   m.def("ppo_cartpole_rollout", &ppo_cartpole_rollout);

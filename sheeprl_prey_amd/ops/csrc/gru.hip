@@ -13,11 +13,12 @@ __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict
                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
                                                          float* __restrict__ hn, float* __restrict__ mean_out,
                                                          float* __restrict__ rstd_out, int M, int H, float eps,
-                                                         int ldo) {
+                                                         int ldo, const float* __restrict__ x2, int ldx2) {
   __shared__ float red[4];
   const int T = 256, N = 3 * H;
   for (int row = blockIdx.x; row < M; row += gridDim.x) {
     const float* xr = x + (int64_t)row * N;
+    const float* x2r = x2 ? x2 + (int64_t)row * ldx2 : nullptr;  // optional second GEMM part (row-strided)
     float v[3][MAXH];
     float s = 0.f;
 #pragma unroll
@@ -25,7 +26,7 @@ __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict
       int j = threadIdx.x + k * T;
 #pragma unroll
       for (int g = 0; g < 3; ++g) {
-        v[g][k] = j < H ? xr[g * H + j] : 0.f;
+        v[g][k] = j < H ? xr[g * H + j] + (x2r ? x2r[g * H + j] : 0.f) : 0.f;
         s += v[g][k];
       }
     }
@@ -152,15 +153,15 @@ static int gru_maxh(int H) {
 }
 
 bool launch_ln_gru_fwd(const float* x, const float* h, int ldh, const float* gamma, const float* beta, float* hn,
-                       float* mean, float* rstd, int M, int H, float eps, hipStream_t st, int ldo) {
+                       float* mean, float* rstd, int M, int H, float eps, hipStream_t st, int ldo, const float* x2, int ldx2) {
   if (ldo <= 0) ldo = H;
   int mh = gru_maxh(H);
   dim3 g(M < 8192 ? M : 8192), b(256);
   switch (mh) {
-    case 2: hipLaunchKernelGGL(ln_gru_fwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo); return true;
-    case 4: hipLaunchKernelGGL(ln_gru_fwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo); return true;
-    case 8: hipLaunchKernelGGL(ln_gru_fwd_kernel<8>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo); return true;
-    case 16: hipLaunchKernelGGL(ln_gru_fwd_kernel<16>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo); return true;
+    case 2: hipLaunchKernelGGL(ln_gru_fwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
+    case 4: hipLaunchKernelGGL(ln_gru_fwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
+    case 8: hipLaunchKernelGGL(ln_gru_fwd_kernel<8>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
+    case 16: hipLaunchKernelGGL(ln_gru_fwd_kernel<16>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
     default: return false;
   }
 }

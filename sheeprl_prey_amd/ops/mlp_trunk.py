@@ -60,9 +60,10 @@ class TrunkRecord:
     @torch.no_grad()
     def step(self, t: int, x: Tensor, gather=None, tail=None) -> Optional[Tensor]:
         """Forward of step ``t`` on ``x`` [M, K0] (row stride allowed); returns the trunk output [M, N].
-        ``gather`` = (idx, G, off, n_onehot, table): the first ``n_onehot`` input columns are one-hot with hot
-        columns ``idx - off`` - the first layer is then a GEMM over the dense columns plus a row gather of
-        ``table`` (its transposed one-hot weight columns) with the LayerNorm fused (``ops/onehot.py``).
+        ``gather`` = (idx, G, off, n_onehot, table[, Y]): the first ``n_onehot`` input columns are one-hot with hot
+        columns ``idx - off`` - the first layer is then a GEMM over the dense columns (or ``Y``, that product
+        precomputed by the caller) plus a row gather of ``table`` (its transposed one-hot weight columns) with the
+        LayerNorm fused (``ops/onehot.py``).
         ``tail`` = (head Linear, uniforms [M], unimix, sample_out, idx_out, idx_off): the last LayerNorm, the head
         and the unimix one-hot sample run as one kernel (``csrc/actor_tail.hip``); returns None when it did (the
         sample is in ``sample_out``), else the trunk output as without ``tail``."""
@@ -73,9 +74,9 @@ class TrunkRecord:
             if i == 0 and gather is not None:
                 from sheeprl_prey_amd.ops.onehot import gather_first_layer
 
-                idx, G, off, n1, table = gather
+                idx, G, off, n1, table = gather[:5]
                 gather_first_layer(x, idx, G, off, lin, ln, n1, table=table, y_out=self.y[0][t], z_out=pre,
-                                   mean=self.mean[0][t], rstd=self.rstd[0][t])
+                                   mean=self.mean[0][t], rstd=self.rstd[0][t], Y=gather[5] if len(gather) > 5 else None)
                 x = self.y[0][t]
                 continue
             if lin.bias is not None:

@@ -58,18 +58,18 @@ def _ln_parts(ln: Optional[nn.Module]):
 
 def gather_first_layer(x: Tensor, idx: Tensor, G: int, off: int, lin: nn.Linear, ln: Optional[nn.Module], n_onehot: int,
                        table: Optional[Tensor] = None, y_out: Optional[Tensor] = None, z_out: Optional[Tensor] = None,
-                       mean: Optional[Tensor] = None, rstd: Optional[Tensor] = None) -> Tensor:
+                       mean: Optional[Tensor] = None, rstd: Optional[Tensor] = None, Y: Optional[Tensor] = None) -> Tensor:
     """No-grad forward of ``act(LN(lin(x)))`` where ``x[:, :n_onehot]`` is one-hot with hot columns
     ``idx[:, :G] - off`` (x may be a row-strided 2-D view; the dense tail ``x[:, n_onehot:]`` goes through
-    a K = in - n_onehot GEMM).  ``table`` = ``lin.weight[:, :n_onehot].T`` (contiguous) when cached by the
-    caller.  Outputs may be preallocated row-strided views."""
+    a K = in - n_onehot GEMM - or ``Y``, that product computed by the caller, e.g. as one column block of a
+    wider GEMM over the same rows).  ``table`` = ``lin.weight[:, :n_onehot].T`` (contiguous) when cached by
+    the caller.  Outputs may be preallocated row-strided views."""
     C = ops._ext()
     W = lin.weight
     M, N = x.shape[0], W.shape[0]
     if table is None:
         table = ops.transpose_many([W[:, :n_onehot]])[0]
-    Y = None
-    if x.shape[1] > n_onehot:
+    if Y is None and x.shape[1] > n_onehot:
         Y = torch.mm(x[:, n_onehot:], W[:, n_onehot:].t())
     if y_out is None:
         y_out = torch.empty(M, N, device=x.device, dtype=x.dtype)
