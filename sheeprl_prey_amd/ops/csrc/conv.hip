@@ -568,11 +568,13 @@ struct EpiPlain : EpiPlainP {  // out = acc + bias[c] + c0 for c < Nreal; NHWC (
 // --------------------------------------------------------------------------- GEMM main loops
 // Tile BM x BN, WM x WN waves of (TM*32) x (TN*32); 64*WM*WN threads; one LDS stage + register
 // prefetch of the next stage.
-template <int BM, int BN, int WM, int WN, class LA, class LB, class EP, class RM>
+// DB: two LDS stages - the next stage's registers are stored into the other buffer right after this
+// stage's MFMAs, so each K stage needs ONE workgroup barrier instead of two (A/B: SRL_CONV_DB).
+template <int BM, int BN, int WM, int WN, class LA, class LB, class EP, class RM, bool DB = false>
 __global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep, RM rm, int K, int ncls, int remap) {
   constexpr int NTH = 64 * WM * WN, TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(TM >= 1 && TN >= 1 && TM * WM * 32 == BM && TN * WN * 32 == BN, "bad tile");
-  constexpr int LDS_MAIN = (BM + BN) * LDK;
+  constexpr int LDS_MAIN = (DB ? 2 : 1) * (BM + BN) * LDK;
   constexpr int LDS_EPI = WM * 32 * (BN + 4) > 2 * WM * WN * BN ? WM * 32 * (BN + 4) : 2 * WM * WN * BN;
   __shared__ float lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
   float* As = lds;
@@ -608,22 +610,14 @@ __global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep,
   la.load(0, ra);
   lb.load(0, rb);
   const int arow = f.wm * TM * 32 + (f.lane & 31), brow = f.wn * TN * 32 + (f.lane & 31), kof = 4 * (f.lane >> 5);
-  for (int k0 = 0; k0 < K; k0 += BK) {
-    __syncthreads();
-    la.store(ra, As);
-    lb.store(rb, Bs);
-    __syncthreads();
-    if (k0 + BK < K) {
-      la.load(k0 + BK, ra);
-      lb.load(k0 + BK, rb);
-    }
+  auto stage_mfma = [&](const float* A_, const float* B_) {
 #pragma unroll
     for (int s = 0; s < BK / 8; ++s) {
       f4 a[TM], b[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = *(const f4*)(As + (arow + 32 * i) * LDK + 8 * s + kof);
+      for (int i = 0; i < TM; ++i) a[i] = *(const f4*)(A_ + (arow + 32 * i) * LDK + 8 * s + kof);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) b[j] = *(const f4*)(Bs + (brow + 32 * j) * LDK + 8 * s + kof);
+      for (int j = 0; j < TN; ++j) b[j] = *(const f4*)(B_ + (brow + 32 * j) * LDK + 8 * s + kof);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -631,8 +625,42 @@ __global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep,
 #pragma unroll
           for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
     }
+  };
+  if constexpr (DB) {
+    la.store(ra, As);
+    lb.store(rb, Bs);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = 0; k0 < K; k0 += BK) {
+      const bool more = k0 + BK < K;
+      if (more) {
+        la.load(k0 + BK, ra);
+        lb.load(k0 + BK, rb);
+      }
+      const float* Ac = lds + buf * (BM + BN) * LDK;
+      stage_mfma(Ac, Ac + BM * LDK);
+      if (more) {  // the other buffer was last read in the previous stage, which every wave has left (barrier)
+        float* An = lds + (buf ^ 1) * (BM + BN) * LDK;
+        la.store(ra, An);
+        lb.store(rb, An + BM * LDK);
+      }
+      __syncthreads();
+      buf ^= 1;
+    }
+  } else {
+    for (int k0 = 0; k0 < K; k0 += BK) {
+      __syncthreads();
+      la.store(ra, As);
+      lb.store(rb, Bs);
+      __syncthreads();
+      if (k0 + BK < K) {
+        la.load(k0 + BK, ra);
+        lb.load(k0 + BK, rb);
+      }
+      stage_mfma(As, Bs);
+    }
+    __syncthreads();
   }
-  __syncthreads();
   ep.template run<BM, BN, TM, TN, WM, WN>(acc, f, m0, lds, rm);
 }
 
@@ -906,7 +934,7 @@ void launch(K kernel, dim3 grid, dim3 block, hipStream_t st, Args... args) {
 }
 }  // namespace
 
-template <int BM, int BN, int WM, int WN, class LA, class RM>
+template <int BM, int BN, int WM, int WN, bool DB, class LA, class RM>
 static void dispatch_epi(const LA& la, const Dense<BN, 64 * WM * WN>& lb, const ConvEpi& e, const RM& rm, int K, int mtiles,
                          int ncls, hipStream_t st) {
   dim3 block(64 * WM * WN);
@@ -915,15 +943,15 @@ static void dispatch_epi(const LA& la, const Dense<BN, 64 * WM * WN>& lb, const 
   if (e.mode == 0) {
     EpiLNAct ep;
     static_cast<EpiLNActP&>(ep) = e.ln;
-    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNAct, RM>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNAct, RM, DB>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
   } else if (e.mode == 1) {
     EpiLNBwd ep;
     static_cast<EpiLNBwdP&>(ep) = e.lb;
-    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNBwd, RM>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNBwd, RM, DB>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
   } else {
     EpiPlain ep;
     static_cast<EpiPlainP&>(ep) = e.pl;
-    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiPlain, RM>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiPlain, RM, DB>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
   }
 }
 
@@ -933,6 +961,16 @@ static int narrow_tiles() {
   static const int v = [] {
     const char* e = getenv("SRL_CONV_NARROW");
     return e ? atoi(e) : NARROW_DEFAULT;
+  }();
+  return v;
+}
+
+// Double-buffered main loop for the narrow layers; SRL_CONV_DB bit 0: 128x32 tiles (32 channels), bit 1: 128x64
+// (64 channels) (A/B knob, read once; default off until measured)
+static int conv_db() {
+  static const int v = [] {
+    const char* e = getenv("SRL_CONV_DB");
+    return e ? atoi(e) : 0;
   }();
   return v;
 }
@@ -949,11 +987,13 @@ static int narrow_tiles() {
 #define SRL_CONV_TILES(X, ...)                                                                     \
   switch (Nc) {                                                                                     \
     case 32:                                                                                        \
-      if (narrow_tiles() & 2) X<128, 32, 4, 1>(__VA_ARGS__);                                        \
+      if (conv_db() & 1) X<128, 32, 4, 1, true>(__VA_ARGS__);                                       \
+      else if (narrow_tiles() & 2) X<128, 32, 4, 1>(__VA_ARGS__);                                   \
       else X<256, 32, 4, 1>(__VA_ARGS__);                                                           \
       return true;                                                                                  \
     case 64:                                                                                        \
-      if (narrow_tiles() & 1) X<128, 64, 2, 2>(__VA_ARGS__);                                        \
+      if (conv_db() & 2) X<128, 64, 2, 2, true>(__VA_ARGS__);                                       \
+      else if (narrow_tiles() & 1) X<128, 64, 2, 2>(__VA_ARGS__);                                   \
       else X<256, 64, 4, 1>(__VA_ARGS__);                                                           \
       return true;                                                                                  \
     case 96: X<128, 96, 4, 1>(__VA_ARGS__); return true;                                            \
@@ -976,7 +1016,7 @@ bool conv_channels_supported(int Nc) {
 
 // DOWN: out grid (N, SH, SW) with Nc output channels, input Q NHWC (N, 2SH, 2SW, Cb); Cb is a
 // multiple of 32 or a power of two below 32
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool DB = false>
 static void down_cfg(const float* Q, const float* Wp, int N, int SH, int SW, int Cb, const ConvEpi& e, hipStream_t st) {
   constexpr int NTH = 64 * WM * WN;
   const int M = N * SH * SW;
@@ -991,7 +1031,7 @@ static void down_cfg(const float* Q, const float* Wp, int N, int SH, int SW, int
   lb.W = Wp;
   lb.K = 16 * Cb;
   lb.cls_stride = 0;
-  dispatch_epi<BM, BN, WM, WN>(la, lb, e, RowDown{0}, 16 * Cb, (M + BM - 1) / BM, 1, st);
+  dispatch_epi<BM, BN, WM, WN, DB>(la, lb, e, RowDown{0}, 16 * Cb, (M + BM - 1) / BM, 1, st);
 }
 
 bool launch_conv_down(const float* Q, const float* Wp, int N, int SH, int SW, int Cb, int Nc, const ConvEpi& e,
@@ -1000,7 +1040,7 @@ bool launch_conv_down(const float* Q, const float* Wp, int N, int SH, int SW, in
   SRL_CONV_TILES(down_cfg, Q, Wp, N, SH, SW, Cb, e, st)
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool DB = false>
 static void up_cfg(const float* P, const float* Wp, int N, int SH, int SW, int Ca, int Bp, const ConvEpi& e, hipStream_t st) {
   constexpr int NTH = 64 * WM * WN;
   const int M = N * SH * SW;
@@ -1015,7 +1055,7 @@ static void up_cfg(const float* P, const float* Wp, int N, int SH, int SW, int C
   lb.K = 4 * Ca;
   lb.cls_stride = (size_t)Bp * 4 * Ca;
   RowUp rm{ilog2(SH), ilog2(SW), 0};
-  dispatch_epi<BM, BN, WM, WN>(la, lb, e, rm, 4 * Ca, (M + BM - 1) / BM, 4, st);
+  dispatch_epi<BM, BN, WM, WN, DB>(la, lb, e, rm, 4 * Ca, (M + BM - 1) / BM, 4, st);
 }
 
 // UP: P NHWC (N, SH, SW, Ca) -> out grid (N, 2SH, 2SW) with Bp output channels (pack padding)
