@@ -274,3 +274,17 @@ def test_dv3_interaction_order_of_reset_rows(serial):
     envs.close()
     # dones rows in the buffer when the 5th step's training ran: the reset row only in the serial order
     assert seen[-1] == (1.0 if serial else 0.0), seen
+
+
+def test_sequential_buffer_sampler_stream_survives_checkpoint():
+    """The device-side sampler's (seed, counter) travel with the buffer's state_dict, so a resumed run continues
+    the index stream instead of replaying the first draws of the original run."""
+    from sheeprl_prey_amd.data.buffers import SequentialReplayBuffer
+    from sheeprl_prey_amd.data.tensordict import TensorDict
+
+    rb = SequentialReplayBuffer(8, 1)
+    rb.add(TensorDict({"a": torch.arange(4.0).view(4, 1, 1)}, batch_size=[4, 1]))
+    rb._draw_seed, rb._draw_counter = 1234567, 42
+    rb2 = SequentialReplayBuffer(8, 1)
+    rb2.load_state_dict(rb.state_dict())
+    assert (rb2._draw_seed, rb2._draw_counter) == (1234567, 42)
