@@ -4,9 +4,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 mkdir -p gpurun_out/pmc
-CONV_LAYOUTS=fused timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES --output-format csv -d gpurun_out/pmc -o conv -- python3 scripts/conv_bench.py > gpurun_out/pmc/conv.log 2>&1 || exit $?
+CONV_LAYOUTS=fused timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES --output-format csv -d gpurun_out/pmc -o ${TAG:-conv} -- python3 scripts/conv_bench.py > gpurun_out/pmc/${TAG:-conv}.log 2>&1 || exit $?
 f=$(find gpurun_out/pmc -name '*counter_collection.csv' | head -1)
-python3 - "$f" <<'PY' > gpurun_out/pmc/summary.md
+python3 - "$f" <<'PY' > gpurun_out/pmc/${TAG:-conv}_summary.md
 import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -23,4 +23,4 @@ for k, d in sorted(agg.items(), key=lambda x: -x[1]["SQ_WAVE_CYCLES"])[:25]:
           + f" | {100*d['SQ_WAIT_ANY']/wc:.0f} | {100*d['SQ_WAIT_INST_ANY']/wc:.0f} | {d['SQ_VALU_MFMA_BUSY_CYCLES']/max(d['SQ_BUSY_CYCLES'],1):.3g} |")
 PY
 rm -f "$f"
-cat gpurun_out/pmc/summary.md | cut -c1-400
+cat gpurun_out/pmc/${TAG:-conv}_summary.md | cut -c1-400

@@ -13,3 +13,6 @@ for v in "0 valu" "1 mfma" "2 mfma" "3 mfma" "0 mfma"; do
   SRL_CONV_DB=$1 SRL_UP_LAST=$2 timeout -k 10 300 python bench.py > gpurun_out/r4c_bench_$1_$2.log 2>&1 \
     && echo "db=$1 up=$2 $(tail -1 gpurun_out/r4c_bench_$1_$2.log | cut -c1-120)" || { tail -20 gpurun_out/r4c_bench_$1_$2.log; exit 1; }
 done
+TAG=base bash scripts/conv_pmc.sh > /dev/null 2>&1 || { echo pmc base failed; exit 1; }
+SRL_CONV_DB=3 SRL_UP_LAST=mfma TAG=db3 bash scripts/conv_pmc.sh > /dev/null 2>&1 || { echo pmc db3 failed; exit 1; }
+head -14 gpurun_out/pmc/base_summary.md | cut -c1-250; head -14 gpurun_out/pmc/db3_summary.md | cut -c1-250

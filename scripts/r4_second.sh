@@ -13,3 +13,4 @@ for i in 1 2; do
   timeout -k 10 300 python bench.py --algo sac --steps 400 --warmup 50 > gpurun_out/r4_sac_fused_$i.log 2>&1 && tail -1 gpurun_out/r4_sac_fused_$i.log | cut -c1-300 || exit 1
   SRL_SAC_FUSED=0 timeout -k 10 300 python bench.py --algo sac --steps 400 --warmup 50 > gpurun_out/r4_sac_eager_$i.log 2>&1 && tail -1 gpurun_out/r4_sac_eager_$i.log | cut -c1-300 || exit 1
 done
+bash scripts/rehearse_2rank.sh > gpurun_out/r4_rehearse2.log 2>&1 && tail -1 gpurun_out/r4_rehearse2.log | cut -c1-1500 || { tail -30 gpurun_out/r4_rehearse2.log; exit 1; }
