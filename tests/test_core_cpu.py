@@ -320,3 +320,63 @@ def test_optimizer_fault_guard_skips_update_eager():
     ops.flat_adam(p, g, m, v, scalars, 1e-2, 0.9, 0.999, 1e-8, 0.0, False)
     assert float(scalars[0]) == 1.0 and float(scalars[3]) == 0.0 and not torch.equal(p, p0)
     assert int(guard[2]) == 4
+
+
+def test_runner_fused_ops_knob_routes_ops():
+    """``fabric.fused_ops`` is wired: a Runner built with it off routes the ops through the eager oracles."""
+    from sheeprl_prey_amd import ops
+    from sheeprl_prey_amd.parallel.runner import Runner
+
+    try:
+        Runner(accelerator="cpu", fused_ops=False)
+        assert not ops.fused_enabled()
+        Runner(accelerator="cpu", fused_ops=True)
+        assert ops.fused_enabled()
+    finally:
+        ops.set_fused(True)
+
+
+def test_collective_log_records_and_counts_per_phase():
+    """``CollectiveLog`` wraps the torch.distributed entry points: (step, phase, op, numel, dtype) per call."""
+    import torch.distributed as dist
+
+    from sheeprl_prey_amd.parallel.collectives import CollectiveLog, set_phase, step_boundary
+
+    calls = []
+    orig = dist.all_reduce
+    with CollectiveLog() as log:
+        assert dist.all_reduce is not orig and dist.all_reduce.__wrapped__ is orig
+        step_boundary()
+        set_phase("wm")
+        # wrappers around stand-ins: no process group needed
+        wrapped = log._wrap("all_reduce", lambda t, **kw: calls.append(t.numel()))
+        wrapped(torch.zeros(7))
+        wrapped(torch.zeros(3))
+        set_phase("coll_lambda")
+        log._wrap("all_gather_into_tensor", lambda o, t, **kw: None)(torch.zeros(4), torch.zeros(2))
+    assert dist.all_reduce is orig
+    assert calls == [7, 3]
+    assert log.sequence(1) == [("wm", "all_reduce", 7, "float32"), ("wm", "all_reduce", 3, "float32"),
+                               ("coll_lambda", "all_gather_into_tensor", 4, "float32")]
+    assert log.per_phase(1) == {"wm": {"all_reduce": 2}, "coll_lambda": {"all_gather_into_tensor": 1}}
+    set_phase("-")
+
+
+def test_heartbeat_ends_a_stalled_process():
+    """``Heartbeat``: a process whose main loop stops beating exits with status 3 (a rank stuck in a device wait
+    never returns to Python, so the daemon thread ends it); one that keeps beating is left alone."""
+    import subprocess
+    import sys
+
+    code = ("import time, sys; sys.path.insert(0, {root!r});"
+            "from sheeprl_prey_amd.parallel.collectives import Heartbeat;"
+            "h = Heartbeat(1.0, 'probe');"
+            "[(h.beat('ok'), time.sleep(0.2)) for _ in range({n})];"
+            "time.sleep({idle}); print('survived')")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    stalled = subprocess.run([sys.executable, "-c", code.format(root=root, n=2, idle=10)], capture_output=True, text=True,
+                             timeout=60)
+    assert stalled.returncode == 3 and "heartbeat: no progress" in stalled.stderr and "survived" not in stalled.stdout
+    alive = subprocess.run([sys.executable, "-c", code.format(root=root, n=10, idle=0)], capture_output=True, text=True,
+                           timeout=60)
+    assert alive.returncode == 0 and "survived" in alive.stdout
