@@ -370,11 +370,15 @@ class DreamerV3Trainer:
                 predicted_values = ops.twohot_mean(st["critic_logits"].detach())
             else:
                 predicted_values = ops.twohot_mean(self._head(critic, imagined_trajectories, oh))
-            predicted_rewards = ops.twohot_mean(self._head(wm.reward_model, imagined_trajectories, oh))
+            # the reward and continue heads only on the imagined steps 1..H: the losses never read row 0 (reference
+            # dreamer_v3.py:261-276 uses rewards[1:] and replaces continues[0] by 1 - done)
+            traj1 = imagined_trajectories[1:]
+            oh1 = (oh[0][1:],) + tuple(oh[1:]) if oh is not None else None
+            predicted_rewards = ops.twohot_mean(self._head(wm.reward_model, traj1, oh1))
             # continuation flags, their gamma-discounts and the cumulative discount: one kernel (K11)
-            cont_g, discount = ops.imag_discount(self._head(wm.continue_model, imagined_trajectories, oh), data["dones"],
-                                                 cfg.algo.gamma)
-            lambda_values = compute_lambda_values(predicted_rewards[1:], predicted_values[1:], cont_g,
+            cont_g, discount = ops.imag_discount(self._head(wm.continue_model, traj1, oh1), data["dones"],
+                                                 cfg.algo.gamma, skip_first=True)
+            lambda_values = compute_lambda_values(predicted_rewards, predicted_values[1:], cont_g,
                                                   lmbda=cfg.algo.lmbda)
         st["discount"] = discount.detach()
         st["imagined_trajectories"] = imagined_trajectories

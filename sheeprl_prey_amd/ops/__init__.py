@@ -823,14 +823,16 @@ def obs_mse(rec: Tensor, target: Tensor, scale: float = 1.0, symlog: bool = Fals
     return ((rec - tgt) ** 2).sum(dim=dims)
 
 
-def imag_discount(continue_logits: Tensor, dones: Tensor, gamma: float):
+def imag_discount(continue_logits: Tensor, dones: Tensor, gamma: float, skip_first: bool = False):
     """``(c[1:] * gamma, cumprod(c * gamma) / gamma)`` with ``c_0 = 1 - done`` and ``c_t = [logit_t > 0]``
-    (reference ``dreamer_v3.py:680-700``), one kernel on GPU; shapes [T, M, 1] / [T+1, M, 1]."""
+    (reference ``dreamer_v3.py:262-279``), one kernel on GPU; shapes [T, M, 1] / [T+1, M, 1].  ``skip_first``:
+    ``continue_logits`` holds only the rows 1.. (row 0 is replaced by ``1 - done``, so it need not be computed)."""
     if _native(continue_logits) and continue_logits.dtype == torch.float32 and dones.dtype == torch.float32:
-        cg, disc = _ext().imag_discount(continue_logits.detach().contiguous(), dones.reshape(-1).contiguous(), float(gamma))
+        cg, disc = _ext().imag_discount(continue_logits.detach().contiguous(), dones.reshape(-1).contiguous(), float(gamma),
+                                        bool(skip_first))
         return cg, disc
     c = (continue_logits > 0).to(continue_logits.dtype)
-    c = torch.cat(((1 - dones).reshape(1, -1, 1).to(c.dtype), c[1:]))
+    c = torch.cat(((1 - dones).reshape(1, -1, 1).to(c.dtype), c if skip_first else c[1:]))
     return c[1:] * gamma, torch.cumprod(c * gamma, dim=0) / gamma
 
 

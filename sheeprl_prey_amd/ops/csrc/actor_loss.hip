@@ -87,16 +87,17 @@ __global__ void actor_loss_final(const float* __restrict__ partial, int n, float
 // c_t = [continue_logit_t > 0]; cont_g[t-1] = c_t * gamma (the lambda-return discount) and
 // discount[t] = cumprod(c * gamma)[t] / gamma, one thread per imagined row, same fp32 operation
 // order as the torch form (bitwise equal).
+// clog holds rows t0 .. T1-1 of the continue logits (t0 = 1: row 0 - replaced by 1 - done - was never computed)
 __global__ __launch_bounds__(256) void imag_discount_kernel(const float* __restrict__ clog, const float* __restrict__ dones,
                                                             int T1, int M, float gamma, float* __restrict__ cont_g,
-                                                            float* __restrict__ discount) {
+                                                            float* __restrict__ discount, int t0) {
   const int m = blockIdx.x * 256 + threadIdx.x;
   if (m >= M) return;
   const float inv = 1.f / gamma;  // torch divides by a scalar as a multiply by its fp32 reciprocal
   float acc = (1.f - dones[m]) * gamma;
   discount[m] = acc * inv;
   for (int t = 1; t < T1; ++t) {
-    const float cg = (clog[(size_t)t * M + m] > 0.f ? 1.f : 0.f) * gamma;
+    const float cg = (clog[(size_t)(t - t0) * M + m] > 0.f ? 1.f : 0.f) * gamma;
     cont_g[(size_t)(t - 1) * M + m] = cg;
     acc = acc * cg;
     discount[(size_t)t * M + m] = acc * inv;
@@ -107,9 +108,9 @@ __global__ __launch_bounds__(256) void imag_discount_kernel(const float* __restr
 }  // namespace srl
 
 void launch_imag_discount(const float* clog, const float* dones, int T1, int M, float gamma, float* cont_g, float* discount,
-                          hipStream_t st) {
+                          hipStream_t st, int t0) {
   hipLaunchKernelGGL(srl::aloss::imag_discount_kernel, dim3((M + 255) / 256), dim3(256), 0, st, clog, dones, T1, M, gamma,
-                     cont_g, discount);
+                     cont_g, discount, t0);
 }
 
 int actor_loss_blocks(int rows) { return std::min(256, std::max(1, (rows + srl::aloss::NTH - 1) / srl::aloss::NTH)); }

@@ -42,7 +42,7 @@ void launch_obs_mse_fwd(const float* rec, const void* tgt, bool u8, int rows, in
 void launch_obs_mse_bwd(const float* rec, const void* tgt, bool u8, int rows, int n, float scale, int symlog, const float* g,
                         float* drec, hipStream_t st);
 void launch_imag_discount(const float* clog, const float* dones, int T1, int M, float gamma, float* cont_g, float* discount,
-                          hipStream_t st);
+                          hipStream_t st, int t0);
 void launch_lstm_fwd(const float* xg, const float* Whh, const float* h0, const float* c0, float* out, float* gates, float* cs,
                      float* hT, float* cT, int T, int B, int H, hipStream_t st);
 void launch_lstm_bwd(const float* Whh, const float* c0, const float* gates, const float* cs, const float* dout, const float* dhT,
@@ -483,16 +483,18 @@ torch::Tensor obs_mse_bwd(torch::Tensor rec, torch::Tensor tgt, int64_t rows, do
   return drec;
 }
 
-// continue logits [T1, M(, 1)], dones [M] -> {cont_g [T1-1, M, 1], discount [T1, M, 1]}
-std::vector<torch::Tensor> imag_discount(torch::Tensor clog, torch::Tensor dones, double gamma) {
+// continue logits [T1, M(, 1)] (skip_first: [T1-1, M(, 1)], the rows 1.. - row 0 is replaced by 1 - done), dones [M]
+// -> {cont_g [T1-1, M, 1], discount [T1, M, 1]}
+std::vector<torch::Tensor> imag_discount(torch::Tensor clog, torch::Tensor dones, double gamma, bool skip_first) {
   nc_check(clog, "imag_discount logits");
   nc_check(dones, "imag_discount dones");
-  const int64_t T1 = clog.size(0), M = clog.numel() / T1;
+  const int64_t t0 = skip_first ? 1 : 0;
+  const int64_t T1 = clog.size(0) + t0, M = clog.numel() / clog.size(0);
   TORCH_CHECK(T1 >= 2 && dones.numel() == M, "imag_discount: logits [T1, M], dones [M]");
   auto cg = torch::empty({T1 - 1, M, 1}, clog.options());
   auto disc = torch::empty({T1, M, 1}, clog.options());
   launch_imag_discount(clog.data_ptr<float>(), dones.data_ptr<float>(), (int)T1, (int)M, (float)gamma, cg.data_ptr<float>(),
-                       disc.data_ptr<float>(), stream());
+                       disc.data_ptr<float>(), stream(), (int)t0);
   return {cg, disc};
 }
 
@@ -764,7 +766,8 @@ void register_ext(pybind11::module& m) {
   m.def("lstm_fwd", &lstm_fwd);
   m.def("lstm_bwd", &lstm_bwd, pybind11::arg("Whh"), pybind11::arg("c0"), pybind11::arg("gates"), pybind11::arg("cs"),
         pybind11::arg("dout"), pybind11::arg("dhT") = pybind11::none(), pybind11::arg("dcT") = pybind11::none());
-  m.def("imag_discount", &imag_discount);
+  m.def("imag_discount", &imag_discount, pybind11::arg("clog"), pybind11::arg("dones"), pybind11::arg("gamma"),
+        pybind11::arg("skip_first") = false);
   m.def("ens_disagreement", &ens_disagreement);
   m.def("wm_loss_fwd", &wm_loss_fwd);
   m.def("wm_loss_bwd", &wm_loss_bwd);

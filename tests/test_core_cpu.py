@@ -380,3 +380,16 @@ def test_heartbeat_ends_a_stalled_process():
     alive = subprocess.run([sys.executable, "-c", code.format(root=root, n=10, idle=0)], capture_output=True, text=True,
                            timeout=60)
     assert alive.returncode == 0 and "survived" in alive.stdout
+
+
+def test_imag_discount_skip_first_matches_full_rows():
+    """``ops.imag_discount(..., skip_first=True)`` on the continue logits of rows 1.. equals the full-row form
+    (row 0 of the continue head is replaced by ``1 - done``, reference ``dreamer_v3.py:267-268``)."""
+    from sheeprl_prey_amd import ops
+
+    torch.manual_seed(0)
+    logits = torch.randn(6, 10, 1)
+    dones = (torch.rand(10) < 0.3).float()
+    cg, disc = ops.imag_discount(logits, dones, 0.99)
+    cg1, disc1 = ops.imag_discount(logits[1:], dones, 0.99, skip_first=True)
+    assert torch.equal(cg, cg1) and torch.equal(disc, disc1)

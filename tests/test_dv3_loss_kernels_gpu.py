@@ -155,6 +155,9 @@ def test_imag_discount_kernel_matches_torch():
     c = torch.cat(((1 - dones).reshape(1, -1, 1), c[1:]))
     assert torch.equal(cg, c[1:] * gamma)
     assert torch.equal(disc, torch.cumprod(c * gamma, dim=0) / gamma)
+    # skip_first: only the rows 1.. of the logits are given (the trainer never computes row 0)
+    cg1, disc1 = ops.imag_discount(logits[1:].contiguous(), dones, gamma, skip_first=True)
+    assert torch.equal(cg1, cg) and torch.equal(disc1, disc)
 
 
 def test_wm_loss_assembly_matches_eager():
