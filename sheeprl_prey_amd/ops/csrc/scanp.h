@@ -13,6 +13,8 @@ struct PP {
   int grid;  // workgroups of the launch (every one resident: 1 per CU)
   int offC;  // first workgroup of the forward C phase (categorical tiles)
   int off2;  // first workgroup of the backward G2 / G4 phases
+  int ag;    // forward form: 0 = A (gx tiles of 16 columns) -> B (LN-GRU of whole rows + u); 1 = A owns the 16 h
+             // columns of all three gates and finishes the LN-GRU of its tile itself (rssm_persist.hip fwd_AG)
   // forward inputs (never written in the launch: plain loads)
   const float *P, *first, *uni, *z0, *Wz, *WzT, *ln1w, *ln1b, *Wg, *lngw, *lngb, *W1, *ln2w, *ln2b, *W2, *b2;
   // forward state: xr holds a_proj + first * (z0 Wz^T) on entry and receives the posterior row gathers
