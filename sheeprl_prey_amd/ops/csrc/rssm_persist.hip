@@ -93,11 +93,11 @@ __device__ __forceinline__ void st_wt2(float* p, float a, float b) {
 
 // 16 x cols tile (cols % 4 == 0) from global (row stride ls) into LDS (row stride ld); rows >= nvalid
 // are zero; rows are optionally scaled by (1 - first[row]).  Every load is a 16-B sc1 buffer load.
+template <int U = 4>
 __device__ __forceinline__ void stage_wt(float* dst, int ld, const float* src, int ls, int nvalid, int cols,
                                          const float* first = nullptr) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, nvalid * ls * 4, 0x00020000);
   const int c4 = cols >> 2, n = 16 * c4;
-  constexpr int U = 4;
   for (int base = 0; base < n; base += NTH * U) {
     f4 r[U];
 #pragma unroll
@@ -236,7 +236,7 @@ __device__ __forceinline__ void gemm_reg(const WTile<NT, U>& wt, const float* As
 // One role per workgroup; each role carves the dynamic LDS its own way (floats).
 __host__ __device__ inline int lds_A(int D, int H) { return 16 * (H + D + 4) + 2 * D + 4096 + 256 + 32 + 16; }
 __host__ __device__ inline int lds_B(int H) { return 16 * (H + 4) + 6 * H + 4096 + 256 + 32 + 16; }
-__host__ __device__ inline int lds_AG(int D, int H) { return 16 * (H + D + 4) + 2 * D + 96 + 16 * 16 * 48 + 768 + 64 + 16; }
+__host__ __device__ inline int lds_AG(int D, int H) { return 16 * (H + D + 4) + 2 * D + 96 + 8 * 16 * 48 + 768 + 64 + 16 + 48 * 260; }
 __host__ __device__ inline int lds_BU(int H) { return 16 * (H + 4) + 4096 + 256 + 16; }
 __host__ __device__ inline int lds_C_base(int hid, int S, int C) { return 16 * (hid + 4) + 2 * hid + 8192 + 512 + 16 + 16 * (S / C) + 32 + 1024 + 512; }
 // C also keeps its Wz^T column tiles (S rows x 16 columns each, ceil(D/16 / nC) of them) in LDS when they fit:
@@ -617,23 +617,26 @@ __device__ __forceinline__ void fwd_AG(const PP& p, int a, float* sm) {
   float* l1w = As + 16 * lda;
   float* l1b = l1w + D;
   float* lgp = l1b + D;            // [2][48]: LN-GRU gamma / beta of this workgroup's gx columns (gate-major)
-  float* red = lgp + 96;           // [16 waves][16][48]
-  float* ct = red + 16 * 16 * 48;  // [16][48] gx tile
+  float* red = lgp + 96;           // [8 waves][16][48]: two-stage cross-wave reduction (waves 8..15 store, 0..7 add)
+  float* ct = red + 8 * 16 * 48;   // [16][48] gx tile
   float* rowst = ct + 768;         // [16][2] LN-GRU row mean / rstd; [32..64): LN1 row statistics (workgroup 0)
   int* flag = (int*)(rowst + 64);
-  // weight fragments: rows g*H + 16a + (lane & 15) of Wg, g = 0..2, over the whole K = H + D
-  WTile<3, UA> wt;
+  float* wl = (float*)(flag + 16);  // [48 rows][260]: the second x-half weight chunk of every wave (K columns H + 256 ..)
+  // weight fragments (rows g*H + 16a + (lane & 15) of Wg, g = 0..2) for the x half (K = D, after the wait for C): the
+  // first chunk of each wave in registers, the second (K columns H + 256 ..) in LDS, both resident for the whole scan;
+  // the h half (K = H, before the wait) is streamed from L2 each step - its latency is off the critical path, and three
+  // register tiles of the whole K would not fit the 128-VGPR budget.  D <= 512 (host gate).
+  WTile<3, 1> wt;
   const int nch = HD >> 4, nH = H >> 4;
-  {
-    const float* wrow = p.Wg + (size_t)(16 * a + li) * HD + 4 * lg4;
+  const float* wrow = p.Wg + (size_t)(16 * a + li) * HD + 4 * lg4;
+  if (nH + w < nch) {
 #pragma unroll
-    for (int q = 0; q < UA; ++q) {
-      const int c = w + NWV * q;
-      if (c < nch) {
-#pragma unroll
-        for (int g = 0; g < 3; ++g) wt.b[q][g] = *(const f4*)(wrow + (size_t)g * H * HD + (c << 4));
-      }
-    }
+    for (int g = 0; g < 3; ++g) wt.b[0][g] = *(const f4*)(wrow + (size_t)g * H * HD + ((nH + w) << 4));
+  }
+  for (int e = threadIdx.x; e < 48 * 64; e += NTH) {  // 48 rows x 256 columns as float4
+    const int r = e >> 6, k4 = (e & 63) << 2, g = r >> 4, i = r & 15;
+    const int col = H + 256 + k4;
+    *(f4*)(wl + r * 260 + k4) = col < HD ? *(const f4*)(p.Wg + (size_t)(g * H + 16 * a + i) * HD + col) : f4{0.f, 0.f, 0.f, 0.f};
   }
   stage_vec(l1w, p.ln1w, D);
   stage_vec(l1b, p.ln1b, D);
@@ -654,33 +657,41 @@ __device__ __forceinline__ void fwd_AG(const PP& p, int a, float* sm) {
     if (t > 0) {
       // every A' workgroup's h_{t-1} tile
       if (!wait_ctr(p, 5, eA, t, 1, flag)) return;
-      stage_wt(As, lda, p.hs + (size_t)(t - 1) * B * H, H, B, H, p.first + (size_t)t * B);
+      stage_wt<2>(As, lda, p.hs + (size_t)(t - 1) * B * H, H, B, H, p.first + (size_t)t * B);
       __syncthreads();
     }
-    // h half of the GEMM (chunks c < nH) while C finishes the previous step
+    // h half of the GEMM (chunks c < nH, weights streamed) while C finishes the previous step
+    for (int c = w; c < nH; c += NWV) {
+      f4 bw[3];
 #pragma unroll
-    for (int q = 0; q < UA; ++q) {
-      const int c = w + NWV * q;
-      if (c < nH) {
-        const f4 av = *(const f4*)(arow + (c << 4));
+      for (int g = 0; g < 3; ++g) bw[g] = *(const f4*)(wrow + (size_t)g * H * HD + (c << 4));
+      const f4 av = *(const f4*)(arow + (c << 4));
 #pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], wt.b[q][g][0], acc[g], 0, 0, 0);
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], wt.b[q][g][1], acc[g], 0, 0, 0);
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], wt.b[q][g][2], acc[g], 0, 0, 0);
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], wt.b[q][g][3], acc[g], 0, 0, 0);
-        }
+      for (int g = 0; g < 3; ++g) {
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bw[g][0], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bw[g][1], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bw[g][2], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bw[g][3], acc[g], 0, 0, 0);
       }
     }
-    // park the h-half partial sums in this wave's slice of the reduction buffer: no accumulator registers live
-    // across the wait and the LN1 prologue (the kernel is at the 128-VGPR cap with the 48-column weight tile)
+    // park the h-half partial sums in the reduction buffer (slot w & 7: waves 0..7 store, then waves 8..15 add): no
+    // accumulator registers live across the wait and the LN1 prologue
+    if (w < 8) {
 #pragma unroll
-    for (int g = 0; g < 3; ++g)
+      for (int g = 0; g < 3; ++g)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[(w * 16 + 4 * lg4 + r) * 48 + 16 * g + li] = acc[g][r];
+        for (int r = 0; r < 4; ++r) red[(w * 16 + 4 * lg4 + r) * 48 + 16 * g + li] = acc[g][r];
+    }
+    __syncthreads();
+    if (w >= 8) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[((w - 8) * 16 + 4 * lg4 + r) * 48 + 16 * g + li] += acc[g][r];
+    }
     if (t > 0 && !wait_ctr(p, 2, eC, t, 2, flag)) return;
     PROF(0, 1);
-    stage_wt(As + H, lda, p.xr + (size_t)t * B * D, D, B, D);
+    stage_wt<2>(As + H, lda, p.xr + (size_t)t * B * D, D, B, D);
     __syncthreads();
     PROF(0, 5);
     if (w < B) {
@@ -693,43 +704,58 @@ __device__ __forceinline__ void fwd_AG(const PP& p, int a, float* sm) {
     }
     __syncthreads();
     PROF(0, 2);
-    // x half (chunks nH <= c < nch), then the cross-wave reduction of the 16 x 48 tile
+    // x half (chunks nH <= c < nch, resident weights), then the cross-wave reduction of the 16 x 48 tile
 #pragma unroll
     for (int g = 0; g < 3; ++g) acc[g] = f4{0.f, 0.f, 0.f, 0.f};
+    if (nH + w < nch) {  // first chunk: register weights
+      const f4 av = *(const f4*)(arow + ((nH + w) << 4));
 #pragma unroll
-    for (int q = 0; q < UA; ++q) {
-      const int c = w + NWV * q;
-      if (c >= nH && c < nch) {
-        const f4 av = *(const f4*)(arow + (c << 4));
-#pragma unroll
-        for (int g = 0; g < 3; ++g) {
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], wt.b[q][g][0], acc[g], 0, 0, 0);
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], wt.b[q][g][1], acc[g], 0, 0, 0);
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], wt.b[q][g][2], acc[g], 0, 0, 0);
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], wt.b[q][g][3], acc[g], 0, 0, 0);
-        }
+      for (int g = 0; g < 3; ++g) {
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], wt.b[0][g][0], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], wt.b[0][g][1], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], wt.b[0][g][2], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], wt.b[0][g][3], acc[g], 0, 0, 0);
       }
     }
+    if (nH + w + NWV < nch) {  // second chunk: LDS weights
+      const f4 av = *(const f4*)(arow + ((nH + w + NWV) << 4));
 #pragma unroll
-    for (int g = 0; g < 3; ++g)
+      for (int g = 0; g < 3; ++g) {
+        const f4 bw = *(const f4*)(wl + (16 * g + li) * 260 + (w << 4) + 4 * lg4);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bw[0], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bw[1], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bw[2], acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bw[3], acc[g], 0, 0, 0);
+      }
+    }
+    // x-half partials onto the parked h-half sums: waves 8..15 add into slot w - 8, then waves 0..7 into slot w
+    __syncthreads();
+    if (w >= 8) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) red[(w * 16 + 4 * lg4 + r) * 48 + 16 * g + li] += acc[g][r];
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[((w - 8) * 16 + 4 * lg4 + r) * 48 + 16 * g + li] += acc[g][r];
+    }
+    __syncthreads();
+    if (w < 8) {
+#pragma unroll
+      for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(w * 16 + 4 * lg4 + r) * 48 + 16 * g + li] += acc[g][r];
+    }
     __syncthreads();
     if (threadIdx.x < 768) {
       float v = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < NWV; ++ww) v += red[ww * 768 + threadIdx.x];
+      for (int ww = 0; ww < 8; ++ww) v += red[ww * 768 + threadIdx.x];
       ct[threadIdx.x] = v;
     }
     __syncthreads();
     PROF(0, 3);
     // per-row (mean, M2) of the tile's 48 columns -> the other A' workgroups
     const int eb = threadIdx.x >> 4, ec = threadIdx.x & 15;
-    float x0 = 0.f, x1 = 0.f, x2 = 0.f;
     if (threadIdx.x < 256) {
-      x0 = ct[eb * 48 + ec];
-      x1 = ct[eb * 48 + 16 + ec];
-      x2 = ct[eb * 48 + 32 + ec];
+      const float x0 = ct[eb * 48 + ec], x1 = ct[eb * 48 + 16 + ec], x2 = ct[eb * 48 + 32 + ec];
       const float m = row16_sum(x0 + x1 + x2) * (1.f / 48.f);
       const float q = row16_sum((x0 - m) * (x0 - m) + (x1 - m) * (x1 - m) + (x2 - m) * (x2 - m));
       if (eb < B && ec == 0) st_wt2(p.gst + (((size_t)t * nA + a) * 16 + eb) * 2, m, q);
@@ -766,6 +792,7 @@ __device__ __forceinline__ void fwd_AG(const PP& p, int a, float* sm) {
     __syncthreads();
     if (threadIdx.x < 256 && eb < B) {  // the LN-GRU of the tile: h column 16a + ec of row eb
       const float mu = rowst[2 * eb], rs = rowst[2 * eb + 1];
+      const float x0 = ct[eb * 48 + ec], x1 = ct[eb * 48 + 16 + ec], x2 = ct[eb * 48 + 32 + ec];  // re-read: not live across the wait
       const float zr = (x0 - mu) * rs * lgp[ec] + lgp[48 + ec];
       const float zc = (x1 - mu) * rs * lgp[16 + ec] + lgp[64 + ec];
       const float zu = (x2 - mu) * rs * lgp[32 + ec] + lgp[80 + ec];
@@ -1255,6 +1282,7 @@ bool scanp_supported(int B, int S, int D, int H, int hid, int C, int ag) {
   if (D > 64 * LN_M || hid > 64 * LN_M) return false;
   if (3 * H / 16 > 128) return false;  // Chan combine: two partials per lane
   const int mx = 160 * 1024;
+  if (ag && D > 16 * 16 * 2) return false;  // fwd_AG: x-half weight tiles UX = 2
   if (scanp_fwd_lds(S, D, H, hid, C, ag) > mx || scanp_bwd_lds(S, D, H, hid) > mx) return false;
   int dev = 0, cus = 0;
   (void)hipGetDevice(&dev);

@@ -401,8 +401,9 @@ def scanp_error(sync: Tensor) -> int:
 # which every launch shares.  The host reads it off the hot path (log / checkpoint time, end of a bench)
 # and raises, so a starved scan can never silently produce garbage gradients.
 SCAN_WAIT_CODES = {
-    1: "fwd A waits h_{t-1} (B)", 2: "fwd A waits x_{t} (C gathers)", 3: "fwd B waits gx (A)", 4: "fwd C waits u (B)",
-    5: "fwd C waits every C sample", 11: "bwd G1 waits dlog (G4)", 12: "bwd G2 waits dv (G1)", 13: "bwd G3 waits dZ (G2)",
+    1: "fwd A waits h_{t-1} (B; ag form: every A' h tile)", 2: "fwd A waits x_{t} (C gathers)",
+    3: "fwd B waits gx (A; ag form: every A' h tile)", 4: "fwd C waits u (B)", 5: "fwd C waits every C sample",
+    6: "fwd A' waits every A' row-statistics partial (ag form)", 11: "bwd G1 waits dlog (G4)", 12: "bwd G2 waits dv (G1)", 13: "bwd G3 waits dZ (G2)",
     14: "bwd G4 waits dcat (G3)",
 }
 _HEALTH: dict = {}
