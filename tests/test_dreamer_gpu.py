@@ -5,7 +5,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _build(graphs: bool, seed: int = 0, continuous: bool = False, cnn_mult: int = 8):
+def _build(graphs: bool, seed: int = 0, continuous: bool = False, cnn_mult: int = 8, extra=()):
     from sheeprl_prey_amd.algos.dreamer_v3.agent import build_models
     from sheeprl_prey_amd.algos.dreamer_v3.dreamer_v3 import DreamerV3Trainer
     from sheeprl_prey_amd.algos.dreamer_v3.utils import Moments
@@ -20,7 +20,7 @@ def _build(graphs: bool, seed: int = 0, continuous: bool = False, cnn_mult: int 
         "algo.mlp_layers=2", f"algo.world_model.encoder.cnn_channels_multiplier={cnn_mult}",
         "algo.world_model.recurrent_model.recurrent_state_size=64", "algo.world_model.representation_model.hidden_size=64",
         "algo.world_model.transition_model.hidden_size=64", "algo.horizon=5", "fabric.accelerator=cuda",
-        f"fabric.cuda_graphs={graphs}",
+        f"fabric.cuda_graphs={graphs}", *extra,
     ]))
     torch.manual_seed(seed)
     runner = Runner(**dict(cfg.fabric))

@@ -142,7 +142,7 @@ def test_dv3_step_graph_with_captured_collectives(rccl_group, monkeypatch):
         out[1:].copy_(out[:1].expand_as(out[1:]))
 
     monkeypatch.setattr(dist, "all_gather_into_tensor", gather_2)
-    tr = _build(graphs=True, seed=5)
+    tr = _build(graphs=True, seed=5, extra=("fabric.graph_collectives=True",))  # opt-in mode (default: segmented)
     assert tr.graph_mode == "single+rccl", tr.graph_mode
     data = _data(seed=9)
     la, lb = [], []
