@@ -108,7 +108,19 @@ class ContinuousRollout:
         self.gx = post.new_empty(horizon, M, 3 * Hd)
         self.g_mean = post.new_empty(horizon, M)
         self.g_rstd = post.new_empty(horizon, M)
-        self.tr_pre = post.new_empty(horizon, M, hid)
+        # every GEMM reading h_{t+1} as ONE per step (as imagine_discrete): [M, Hd] x [Hd, hid + Na + 3Hd] gives the
+        # transition's first-layer pre-activations (kept: the backward reads them with this row stride), the actor
+        # trunk's dense first-layer part for step t+1 and the h half of step t+1's GRU input projection
+        a0 = self.layers[0][0]
+        self.merge = (self.tr1.bias is None and self.gru.linear.bias is None
+                      and getattr(rssm, "_merge_h_ok", True))
+        if self.merge:
+            self.Na = a0.out_features
+            self.Wm = torch.cat((self.tr1.weight, a0.weight[:, S:], self.gru.linear.weight[:, :Hd]), 0)
+            self.hm = post.new_empty(horizon + 1, M, self.Wm.shape[0])  # row t: products of h_t
+            self.tr_pre = self.hm[1:, :, :hid]  # transition pre-activations of h_{t+1}, row stride hid + Na + 3Hd
+        else:
+            self.tr_pre = post.new_empty(horizon, M, hid)
         self.tr_y = post.new_empty(horizon, M, hid)
         self.tr_mean = post.new_empty(horizon, M)
         self.tr_rstd = post.new_empty(horizon, M)
@@ -134,8 +146,14 @@ class ContinuousRollout:
         gln = self.gru.layer_norm
         rln, tln = self.rec_ln, self.tr_ln
         err = _err_word(buf.device)
+        merge = self.merge
+        if merge:
+            hidm, Na = self.tr1.out_features, self.Na
+            torch.mm(buf[0, :, S:S + Hd], self.Wm.t(), out=self.hm[0])
+            Wgx_t = Wg[:, Hd:].t()
         for t in range(self.H + 1):
-            out = self.trunk.step(t, buf[t, :, :S + Hd], gather=(self.IDX[t], G, 0, S, self.a_table))
+            ga = (self.IDX[t], G, 0, S, self.a_table) + ((self.hm[t][:, hidm:hidm + Na],) if merge else ())
+            out = self.trunk.step(t, buf[t, :, :S + Hd], gather=ga)
             torch.addmm(self.head.bias, out, self.head.weight.t(), out=self.pre[t])
             C.tn_head_sample_fwd(self.pre[t], self.u_act[t], init_std, min_std, -1.0, 1.0, self.loc[t], self.scale[t],
                                  self.acts[t])
@@ -149,18 +167,27 @@ class ContinuousRollout:
             if not ok:
                 raise RuntimeError("onehot_gather_ln: unsupported recurrent layer width")
             gx = self.gx[t]
-            torch.mm(buf[t, :, S:], Wg.t(), out=gx)  # (h | x) in one GEMM
-            if self.gru.linear.bias is not None:
-                gx += self.gru.linear.bias
-            C.ln_gru_into(gx, buf[t, :, S:S + Hd], gln.weight, gln.bias, float(gln.eps), buf[t + 1, :, S:S + Hd],
-                          self.g_mean[t], self.g_rstd[t])
-            hid = self.tr_pre.shape[-1]
-            if self.tr1.bias is not None:
-                torch.addmm(self.tr1.bias, buf[t + 1, :, S:S + Hd], self.tr1.weight.t(), out=self.tr_pre[t])
+            hid = self.tr_y.shape[-1]
+            if merge:
+                # gx = x Wg_x^T + (h_t Wg_h^T from the merged GEMM): materialised - the backward reads the whole gx
+                torch.addmm(self.hm[t][:, hidm + Na:], buf[t, :, S + Hd:], Wgx_t, out=gx)
+                C.ln_gru_into(gx, buf[t, :, S:S + Hd], gln.weight, gln.bias, float(gln.eps), buf[t + 1, :, S:S + Hd],
+                              self.g_mean[t], self.g_rstd[t])
+                torch.mm(buf[t + 1, :, S:S + Hd], self.Wm.t(), out=self.hm[t + 1])
+                C.ln_act_fwd_into(self.hm[t + 1], self.hm.shape[-1], self.tr_y[t], hid, tln.weight, tln.bias,
+                                  self.tr_mean[t], self.tr_rstd[t], M, hid, 1, float(tln.eps), ops._act_code(tln.act))
             else:
-                torch.mm(buf[t + 1, :, S:S + Hd], self.tr1.weight.t(), out=self.tr_pre[t])
-            C.ln_act_fwd_into(self.tr_pre[t], hid, self.tr_y[t], hid, tln.weight, tln.bias, self.tr_mean[t],
-                              self.tr_rstd[t], M, hid, 1, float(tln.eps), ops._act_code(tln.act))
+                torch.mm(buf[t, :, S:], Wg.t(), out=gx)  # (h | x) in one GEMM
+                if self.gru.linear.bias is not None:
+                    gx += self.gru.linear.bias
+                C.ln_gru_into(gx, buf[t, :, S:S + Hd], gln.weight, gln.bias, float(gln.eps), buf[t + 1, :, S:S + Hd],
+                              self.g_mean[t], self.g_rstd[t])
+                if self.tr1.bias is not None:
+                    torch.addmm(self.tr1.bias, buf[t + 1, :, S:S + Hd], self.tr1.weight.t(), out=self.tr_pre[t])
+                else:
+                    torch.mm(buf[t + 1, :, S:S + Hd], self.tr1.weight.t(), out=self.tr_pre[t])
+                C.ln_act_fwd_into(self.tr_pre[t], hid, self.tr_y[t], hid, tln.weight, tln.bias, self.tr_mean[t],
+                                  self.tr_rstd[t], M, hid, 1, float(tln.eps), ops._act_code(tln.act))
             if self.tr2.bias is not None:
                 torch.addmm(self.tr2.bias, self.tr_y[t], self.tr2.weight.t(), out=self.logits[t])
             else:
@@ -192,7 +219,8 @@ class ContinuousRollout:
         pdb = torch.empty(grid, gcols, device=dev)
         dgx = torch.empty(M, gcols, device=dev)
         dh_prev = torch.empty(M, Hd, device=dev)
-        hid = self.tr_pre.shape[-1]
+        hid = self.tr_y.shape[-1]
+        ldtr = self.tr_pre.stride(1)  # merged form: a column block of the per-step h products
         dtr = torch.empty(M, hid, device=dev)
         D = self.D
         dz = torch.empty(M, D, device=dev)
@@ -202,7 +230,7 @@ class ContinuousRollout:
             # prior_t = straight-through unimix sample of logits[s]
             dlog = C.unimix_sample_bwd(self.logits[s], None, dp, self.disc, float(self.rssm.unimix))
             du = torch.mm(dlog, self.tr2.weight)
-            C.ln_act_bwd_into(self.tr_pre[s], hid, du, hid, dtr, hid, tln.weight, tln.bias, self.tr_mean[s], self.tr_rstd[s],
+            C.ln_act_bwd_into(self.tr_pre[s], ldtr, du, hid, dtr, hid, tln.weight, tln.bias, self.tr_mean[s], self.tr_rstd[s],
                               None, None, None, None, M, hid, 1, t_act)
             dh.addmm_(dtr, self.tr1.weight)
             # h_t = LN-GRU(gx[s], h_s)
