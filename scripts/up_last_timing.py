@@ -35,7 +35,7 @@ def main(N=1024, Ca=32, CO=3, SH=32, iters=50):
         ev[1].record()
         torch.cuda.synchronize()
         res[name] = {"us": round(ev[0].elapsed_time(ev[1]) * 1e3 / iters, 1), "max_abs_err": err}
-    C.set_up_last_form(1)
+    C.set_up_last_form(0)
     print(json.dumps(res))
 
 

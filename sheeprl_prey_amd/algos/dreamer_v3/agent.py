@@ -298,6 +298,7 @@ class RSSM(nn.Module):
     # ---- MI355X imagination: buffer-resident no-grad rollout ---------------------------
     _actor_tail_ok = os.environ.get("SRL_ACTOR_TAIL", "1") != "0"  # A/B switch of the fused rollout actor tail
     _merge_h_ok = os.environ.get("SRL_IMAG_MERGE", "1") != "0"  # A/B switch of the merged h_{t+1} GEMM (imagine_discrete)
+    _prior_head_ok = os.environ.get("SRL_PRIOR_HEAD", "1") != "0"  # A/B switch of the one-launch prior head (prior_head.hip)
 
     def imagine_fast_ok(self, actor) -> bool:
         gru = self.recurrent_model.rnn
@@ -400,6 +401,9 @@ class RSSM(nn.Module):
             hm = torch.mm(h, Wm.t())
             ytr, mtr, rtr = post.new_empty(M, Ntr), post.new_empty(M), post.new_empty(M)
             tr_act = ops._act_code(tr_ln.act)
+            # LayerNorm + act + output Linear + unimix sample of the prior in one launch (prior_head.hip)
+            phead = (self._prior_head_ok and disc == 32 and len(tr_rest) == 1 and isinstance(tr_rest[0], nn.Linear)
+                     and S % 256 == 0 and Ntr % 16 == 0 and Ntr <= 1024)
         for t in range(horizon + 1):
             traj_t = buf[t, :, Ap:Ap + S + Hd]
             # single-head actors: last LayerNorm + head + unimix sample in one kernel (TrunkRecord.step tail)
@@ -441,6 +445,10 @@ class RSSM(nn.Module):
                 C.ln_gru_into(gx, buf[t, :, Ap + S:Ap + S + Hd], ln.weight, ln.bias, float(ln.eps),
                               buf[t + 1, :, Ap + S:Ap + S + Hd], x2=hm[:, Ntr + Na:])
                 torch.mm(buf[t + 1, :, Ap + S:Ap + S + Hd], Wm.t(), out=hm)
+                if phead and C.prior_head(hm[:, :Ntr], tr_ln.weight, tr_ln.bias, float(tr_ln.eps), tr_act, tr_rest[0].weight,
+                                          tr_rest[0].bias, U[t, nh * M:], float(self.unimix), buf[t + 1, :, Ap:Ap + S],
+                                          IDX[t + 1, :, nh:], A):
+                    continue
                 C.ln_act_fwd_into(hm, hm.stride(0), ytr, Ntr, tr_ln.weight, tr_ln.bias, mtr, rtr, M, Ntr, 1,
                                   float(tr_ln.eps), tr_act)
                 logits = ytr

@@ -28,6 +28,7 @@ import torch.nn.functional as F
 from torch import Tensor
 
 from sheeprl_prey_amd import ops
+from sheeprl_prey_amd.ops import sidestream
 from sheeprl_prey_amd.algos.common import (
     action_info,
     build_envs,
@@ -268,7 +269,8 @@ class DreamerV3Trainer:
             continue_logits, None, wm_cfg.continue_scale_factor, entropies=ents, dones=data["dones"],
         )
         self.world_optimizer.zero_grad(set_to_none=True)
-        rec_loss.backward()
+        with sidestream.scope():  # decoder weight gradients beside the scan backward (ops/sidestream.py)
+            rec_loss.backward()
         out["Loss/world_model_loss"] = rec_loss.detach()
         out["Loss/observation_loss"] = observation_loss.detach()
         out["Loss/reward_loss"] = reward_loss.detach()

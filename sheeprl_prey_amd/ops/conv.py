@@ -21,6 +21,8 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 from torch import Tensor, nn
 
+from sheeprl_prey_amd.ops import sidestream as ss
+
 _OK_CH = (32, 64, 96, 128, 192, 256, 384, 512, 768, 1024)  # conv.hip tile table
 ENABLED = True  # A/B switch: False routes the stacks through the per-layer modules (MIOpen + LN kernels)
 # Below this many frames (e.g. the env-interaction player, one frame per env) the deepest stage has
@@ -252,7 +254,11 @@ class DecoderConvFn(torch.autograd.Function):
         dbias = dout.sum(dim=(0, 2, 3))
         dws: List[Optional[Tensor]] = [None] * (L + 1)
         cout_last = ws[L].shape[1]
-        dws[L] = _wgrad(C, p_last, q, cout_last, ws[L])
+        # the weight gradients leave the critical path (data gradients -> scan backward -> encoder): each runs
+        # on the side stream as soon as its output gradient exists (ops/sidestream.py; joined by the optimiser)
+        dev = dout.device
+        with ss.on_side(dev, p_last, q):
+            dws[L] = _wgrad(C, p_last, q, cout_last, ws[L])
         wp = C.conv_pack_down(ws[L], q.shape[3])
         _, zp, mp, rp = acts[4 * (L - 1):4 * L]
         dz = C.conv_gemm(0, q, wp, ws[L].shape[0], 1, gs[L - 1], bs[L - 1], 0.0, act[L - 1], False, zp, mp, rp,
@@ -261,7 +267,8 @@ class DecoderConvFn(torch.autograd.Function):
         for i in range(L - 1, -1, -1):
             p = acts[4 * i]
             cout = ws[i].shape[1]
-            dws[i] = _wgrad(C, p, dz, cout, ws[i])
+            with ss.on_side(dev, p, dz):
+                dws[i] = _wgrad(C, p, dz, cout, ws[i])
             wp = C.conv_pack_down(ws[i], cout)
             cin = ws[i].shape[0]
             if i > 0:
@@ -272,6 +279,8 @@ class DecoderConvFn(torch.autograd.Function):
                 dh = C.conv_gemm(0, dz, wp, cin, 2, None, None, 0.0, 0, True, None, None, None, None, None, None,
                                  0.0, cin)[0]
         dh = dh.reshape(dh.shape[0], -1)
+        for d in dws:
+            ss.mark_main(d)
         return (dh, None, *dws, *[d.view_as(g) for d, g in zip(dgs, gs)], *[d.view_as(b) for d, b in zip(dbs, bs)],
                 dbias)
 

@@ -1371,10 +1371,11 @@ __global__ __launch_bounds__(256) void up_last_mfma_kernel(const float* __restri
   }
 }
 
-// final-layer form: 0 = MFMA, 1 = the VALU kernels below (default until measured on the box; SRL_UP_LAST=mfma|valu)
+// final-layer form: 0 = MFMA (default: 96.6 vs 120.2 us at the Atari-100k shape, profiles/r4_up_last.json),
+// 1 = the VALU kernels below (SRL_UP_LAST=valu)
 static int g_up_last_form = [] {
   const char* e = getenv("SRL_UP_LAST");
-  return (e && std::string(e) == "mfma") ? 0 : 1;
+  return (e && std::string(e) == "valu") ? 1 : 0;
 }();
 void set_up_last_form(int f) { g_up_last_form = f; }
 

@@ -71,6 +71,10 @@ bool launch_actor_tail(const float* pre, long ldp, float* y, long ldy, const flo
                        float alpha, float* sample, long lds, int* idx, long ldi, int ioff, float* logits, int M, int N,
                        hipStream_t st);
 
+bool launch_prior_head(const float* x, long ldx, const float* gamma, const float* beta, float eps, int act, const float* W,
+                       const float* b, const float* uni, float alpha, float* sample, long lds, int* idx, long ldi, int ioff,
+                       int M, int K, int N, hipStream_t st);
+
 bool launch_seq_sample(const void* const* src, void* const* dst, const long* row_bytes, int nk, int n_envs, long cap, int B,
                        int L, long n1, long start2, long n2, unsigned long long seed, unsigned long long counter,
                        hipStream_t st);
@@ -681,6 +685,35 @@ bool actor_tail(torch::Tensor pre, torch::Tensor y, c10::optional<torch::Tensor>
                            (int)M, (int)N, stream());
 }
 
+// ------------------------------------------------------------------ imagination prior head (prior_head.hip)
+// sample = onehot(Categorical(unimix(act(LN(x)) W^T + b))) per 32-class categorical of each row: one-hot rows into
+// `sample` [M, >= N] and hot columns (ioff + g * 32 + pick) into idx [M, >= N / 32]; x / sample / idx row-strided;
+// uniform [M * N / 32].  false: shape not covered.
+bool prior_head(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, double eps, int64_t act, torch::Tensor W,
+                c10::optional<torch::Tensor> b, torch::Tensor uniform, double alpha, torch::Tensor sample,
+                c10::optional<torch::Tensor> idx, int64_t ioff) {
+  const int64_t M = x.size(0), K = x.size(1), N = W.size(0);
+  rowview(x, "x", M, K, torch::kFloat32);
+  rowview(sample, "sample", M, N, torch::kFloat32);
+  TORCH_CHECK(W.is_cuda() && W.scalar_type() == torch::kFloat32 && W.is_contiguous() && W.dim() == 2 && W.size(1) == K,
+              "prior_head: W [N, K] contiguous float32");
+  TORCH_CHECK(N % 32 == 0, "prior_head: N must be a multiple of 32 classes");
+  const float* gp = optf(gamma, "gamma", K);
+  const float* bp = optf(beta, "beta", K);
+  const float* hp = optf(b, "b", N);
+  const float* up = optf(uniform, "uniform", M * (N / 32));
+  int* ip = nullptr;
+  int64_t ldi = 0;
+  if (idx.has_value() && idx->defined()) {
+    rowview(*idx, "idx", M, N / 32, torch::kInt);
+    ip = idx->data_ptr<int>();
+    ldi = idx->stride(0);
+  }
+  return launch_prior_head(x.data_ptr<float>(), x.stride(0), gp, bp, (float)eps, (int)act, W.data_ptr<float>(), hp, up,
+                           (float)alpha, sample.data_ptr<float>(), sample.stride(0), ip, ldi, (int)ioff, (int)M, (int)K,
+                           (int)N, stream());
+}
+
 // Fused replay sequence sample into preallocated [L, B, ...] outputs (gather.hip seq_sample_kernel): srcs are
 // the store's keys [cap, n_envs, ...]; starts uniform over [0, n1) U [start2, start2 + n2), envs uniform.
 bool seq_sample_into(std::vector<torch::Tensor> srcs, std::vector<torch::Tensor> dsts, int64_t B, int64_t L, int64_t n1,
@@ -755,6 +788,9 @@ void register_ext(pybind11::module& m) {
         pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("eps"), pybind11::arg("act"), pybind11::arg("Wh"),
         pybind11::arg("bh"), pybind11::arg("uniform"), pybind11::arg("alpha"), pybind11::arg("sample"), pybind11::arg("idx"),
         pybind11::arg("ioff"), pybind11::arg("logits") = pybind11::none());
+  m.def("prior_head", &prior_head, pybind11::arg("x"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("eps"),
+        pybind11::arg("act"), pybind11::arg("W"), pybind11::arg("b"), pybind11::arg("uniform"), pybind11::arg("alpha"),
+        pybind11::arg("sample"), pybind11::arg("idx"), pybind11::arg("ioff"));
   m.def("wgrad", &wgrad, pybind11::arg("dz"), pybind11::arg("x"), pybind11::arg("idx"), pybind11::arg("G"), pybind11::arg("C"),
         pybind11::arg("off"), pybind11::arg("dW"), pybind11::arg("db"), pybind11::arg("accumulate") = false);
   m.def("onehot_gather_ln", &onehot_gather_ln, pybind11::arg("Y"), pybind11::arg("idx"), pybind11::arg("G"), pybind11::arg("off"),

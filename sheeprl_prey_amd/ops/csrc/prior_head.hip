@@ -1,0 +1,206 @@
+// Prior (transition) head of the DreamerV3 imagination step in ONE launch (reference: RSSM._transition ->
+// transition_model MLP -> _uniform_mix -> OneHotCategoricalStraightThrough sample, dreamer_v3/agent.py:439-455
+// and utils/distribution.py:380-393, once per imagined step at dreamer_v3.py:235-257):
+//
+//   y = act(LN(x))                      x: the transition's first-layer pre-activations [M, K] (row-strided: a
+//                                       column block of the rollout's merged h_{t+1} GEMM output)
+//   l = y W^T + b                       W [N, K], N = G categoricals x 32 classes
+//   sample ~ Categorical(unimix(l))     one-hot rows into the rollout buffer + each categorical's hot column
+//
+// was three launches per step (LayerNorm, hipBLASLt GEMM + bias, sampler) on the rollout's critical path.  The
+// imagination is no-grad (the discrete objective never back-propagates through the dynamics), so neither y nor
+// the logits are stored.
+//
+// Tiling: one workgroup = 16 rows x 256 logit columns (8 waves; wave w = ONE categorical group of 32 classes = two
+// 16-column MFMA tiles), grid (M / 16, N / 256) = 256 workgroups at M = 1024 (one per CU).  The 16 x K row tile
+// is staged in LDS once and LayerNorm-ed in place (each of the N / 256 column workgroups of a row tile repeats
+// the row statistics: 16 rows, trivial).  B fragments (W rows) stream from L2 (W = 2 MB stays resident in each
+// XCD's L2) through a double-buffered register batch of UK chunks; v_mfma_f32_16x16x4_f32 with the
+// float4-permuted K order of scan_dev.h (a[j] / b[j] = K index 16c + 4g + j on both operands).  The accumulator
+// map (col = lane & 15, row = 4 (lane >> 4) + r) puts a row's 32 classes on the 16 lanes of one DPP row x two
+// registers, so the unimix / softmax / CDF of the sampler are 16-lane shuffles with no LDS round trip.
+#include "common.h"
+#include "scan_dev.h"
+
+namespace srl {
+namespace phead {
+
+using scandev::f4;
+
+constexpr int NT = 512;  // 8 waves
+constexpr int CL = 32;   // classes per categorical
+constexpr int UK = 8;    // 16-wide K chunks of B fragments per register batch
+
+struct HP {
+  const float* x;
+  long ldx;
+  const float* gamma;
+  const float* beta;
+  const float* W;  // [N, K]
+  const float* b;  // [N] or null
+  const float* uni;  // [M * G]: uniform of (row m, categorical g) at m * G + g
+  float* sample;     // [M, >= N] row-strided
+  long lds;
+  int* idx;          // [M, >= G] row-strided or null: ioff + g * 32 + pick
+  long ldi;
+  int ioff, M, K, N, act;
+  float eps, alpha;
+};
+
+__device__ __forceinline__ float max16(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 16));
+  return v;
+}
+__device__ __forceinline__ float sum16(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 16);
+  return v;
+}
+__device__ __forceinline__ float incl16(float v, int j) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    const float t = __shfl_up(v, o, 16);
+    if (j >= o) v += t;
+  }
+  return v;
+}
+
+template <int KV>
+__global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
+  extern __shared__ float sm[];
+  const int lda = p.K + 4;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i = lane & 15, g = lane >> 4;
+  const int r0 = blockIdx.x * 16;
+  const int nrow = min(16, p.M - r0);
+  const int G = p.N / CL;
+  const int gg = blockIdx.y * 8 + w;  // this wave's categorical
+  const int n0 = gg * CL;
+  const int nch = p.K >> 4;
+  // first B batch requested before anything else: its latency hides behind the staging and the LayerNorm
+  const float* wr0 = p.W + (long)(n0 + i) * p.K + 4 * g;
+  const float* wr1 = wr0 + 16L * p.K;
+  f4 cb0[UK], cb1[UK];
+#pragma unroll
+  for (int q = 0; q < UK; ++q) {
+    const int c = min(q, nch - 1);
+    cb0[q] = *(const f4*)(wr0 + 16 * c);
+    cb1[q] = *(const f4*)(wr1 + 16 * c);
+  }
+  const float bb0 = p.b ? p.b[n0 + i] : 0.f, bb1 = p.b ? p.b[n0 + 16 + i] : 0.f;
+  // 16 x K row tile -> LDS (rows past M zero), then LayerNorm + act in place (two rows per wave)
+  const int c4 = p.K >> 2;
+  for (int e = threadIdx.x; e < 16 * c4; e += NT) {
+    const int r = e / c4, k = (e - r * c4) << 2;
+    *(f4*)(sm + r * lda + k) = r < nrow ? *(const f4*)(p.x + (long)(r0 + r) * p.ldx + k) : f4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+  for (int r = w; r < 16; r += NT / 64) {
+    float mu, rs;
+    scandev::wave_ln_act_row<KV>(sm + r * lda, p.K, p.eps, p.gamma, p.beta, p.act, mu, rs);
+  }
+  __syncthreads();
+  // logits tile [16 rows x 32 classes] of this wave's categorical
+  const float* arow = sm + i * lda + 4 * g;
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c0 = 0; c0 < 4 * KV; c0 += UK) {
+    if (c0 >= nch) break;
+    f4 nb0[UK], nb1[UK];
+    const bool more = c0 + UK < nch;
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < UK; ++q) {
+        const int c = min(c0 + UK + q, nch - 1);
+        nb0[q] = *(const f4*)(wr0 + 16 * c);
+        nb1[q] = *(const f4*)(wr1 + 16 * c);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < UK; ++q) {
+      if (c0 + q < nch) {
+        const f4 a = *(const f4*)(arow + 16 * (c0 + q));
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], cb0[q][0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], cb1[q][0], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], cb0[q][1], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], cb1[q][1], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], cb0[q][2], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], cb1[q][2], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], cb0[q][3], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], cb1[q][3], acc1, 0, 0, 0);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < UK; ++q) {
+        cb0[q] = nb0[q];
+        cb1[q] = nb1[q];
+      }
+    }
+  }
+  // unimix + categorical sample per (row, categorical): class j on lane i of register 0, class 16 + j on register 1
+  const float inv = 1.f / CL;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 4 * g + r;
+    const float l0 = acc0[r] + bb0, l1 = acc1[r] + bb1;
+    float m0 = l0, m1 = l1;
+    if (p.alpha > 0.f) {
+      const float mx = max16(fmaxf(l0, l1));
+      const float e0 = __expf(l0 - mx), e1 = __expf(l1 - mx);
+      const float s = sum16(e0 + e1);
+      float q0 = (1.f - p.alpha) * (e0 / s) + p.alpha * inv;
+      float q1 = (1.f - p.alpha) * (e1 / s) + p.alpha * inv;
+      q0 = fminf(fmaxf(q0, FEPS), 1.f - FEPS);
+      q1 = fminf(fmaxf(q1, FEPS), 1.f - FEPS);
+      m0 = logf(q0);
+      m1 = logf(q1);
+    }
+    const float mx2 = max16(fmaxf(m0, m1));
+    const float e0 = __expf(m0 - mx2), e1 = __expf(m1 - mx2);
+    const float s2 = sum16(e0 + e1);
+    const float cdf0 = incl16(e0 / s2, i);
+    const float cdf1 = __shfl(cdf0, 15, 16) + incl16(e1 / s2, i);
+    const float cmax = __shfl(cdf1, 15, 16);
+    const float u = row < nrow ? p.uni[(long)(r0 + row) * G + gg] : 0.f;
+    const float thr = u * cmax;
+    int pick = (int)sum16((cdf0 < thr ? 1.f : 0.f) + (cdf1 < thr ? 1.f : 0.f));
+    if (pick > CL - 1) pick = CL - 1;
+    if (row < nrow) {
+      float* srow = p.sample + (long)(r0 + row) * p.lds + n0;
+      srow[i] = i == pick ? 1.f : 0.f;
+      srow[16 + i] = 16 + i == pick ? 1.f : 0.f;
+      if (p.idx != nullptr && i == 0) p.idx[(long)(r0 + row) * p.ldi + gg] = p.ioff + n0 + pick;
+    }
+  }
+}
+
+}  // namespace phead
+
+// false: shape not covered (caller runs the three-launch path)
+bool launch_prior_head(const float* x, long ldx, const float* gamma, const float* beta, float eps, int act, const float* W,
+                       const float* b, const float* uni, float alpha, float* sample, long lds, int* idx, long ldi, int ioff,
+                       int M, int K, int N, hipStream_t st) {
+  using namespace phead;
+  if (M <= 0 || K <= 0 || K % 16 != 0 || K > 1024 || N % 256 != 0 || ldx % 4 != 0 || !gamma || !beta) return false;
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W)) & 15) return false;
+  HP p{x, ldx, gamma, beta, W, b, uni, sample, lds, idx, ldi, ioff, M, K, N, act, eps, alpha};
+  const dim3 grid((M + 15) / 16, N / 256);
+  const size_t shm = (size_t)16 * (K + 4) * sizeof(float);
+  static const bool lds_set = [] {  // K = 1024 needs 65.8 KB of the 160 KB
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prior_head_kernel<8>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              16 * 516 * 4);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prior_head_kernel<16>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              16 * 1028 * 4);
+    return true;
+  }();
+  (void)lds_set;
+  if (K <= 512)
+    hipLaunchKernelGGL(prior_head_kernel<8>, grid, dim3(NT), shm, st, p);
+  else
+    hipLaunchKernelGGL(prior_head_kernel<16>, grid, dim3(NT), shm, st, p);
+  return true;
+}
+
+}  // namespace srl

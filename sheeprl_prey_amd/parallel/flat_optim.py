@@ -43,6 +43,12 @@ def _aligned(n: int) -> int:
     return (n + _ALIGN - 1) // _ALIGN * _ALIGN
 
 
+def _side_join() -> None:
+    from sheeprl_prey_amd.ops import sidestream
+
+    sidestream.join()
+
+
 class FlatOptimizer:
     kind = "base"
 
@@ -163,6 +169,7 @@ class FlatOptimizer:
         self._detached = False
 
     def _gather(self) -> None:
+        _side_join()
         if not self._detached:
             return
         self._detached = False
@@ -290,6 +297,7 @@ class FlatOptimizer:
         ov = self._ov
         if ov["seen"][i]:
             return
+        _side_join()  # the gradient may still be in flight on the side stream
         v = self._ov_view(i)
         g = p.grad
         if g is not None and g.data_ptr() != v.data_ptr():
@@ -354,7 +362,9 @@ class FlatOptimizer:
             self.wait_grads()
 
     def wait_grads(self) -> None:
-        """Join the gradient collectives ``all_reduce_grads(wait=False)`` left in flight."""
+        """Join the gradient collectives ``all_reduce_grads(wait=False)`` left in flight (and any side-stream
+        gradient work, ``ops/sidestream.py``)."""
+        _side_join()
         pending = getattr(self, "_pending", None)
         if pending is None:
             return
