@@ -12,3 +12,4 @@ for v in "1 1 a" "0 1 b" "1 0 c" "1 1 d"; do
     && echo "side=$1 phead=$2 $(tail -1 gpurun_out/r4t_bench_$1$2$3.log | cut -c1-140)" || { tail -20 gpurun_out/r4t_bench_$1$2$3.log; exit 1; }
 done
 bash scripts/prof.sh r4t_dv3 10 || exit 1
+STEPS=6000 bash scripts/dv3_cli.sh > gpurun_out/r4t_cli.log 2>&1 && tail -1 gpurun_out/r4t_cli.log | cut -c1-1500 || { tail -30 gpurun_out/r4t_cli.log; exit 1; }

@@ -72,6 +72,7 @@ def _act_code(act: str) -> int:
 
 # =============================================================== Linear (library GEMMs, column-sum bias grad)
 _LIN2D = os.environ.get("SRL_LIN2D", "1") != "0"  # A/B switch
+_SIDE_LIN = os.environ.get("SRL_SIDE_LIN", "1") != "0"  # A/B switch: Linear parameter gradients on the side stream
 
 
 def _lin2d(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
@@ -181,19 +182,32 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy):
+        from sheeprl_prey_amd.ops import sidestream as ss
+
         x, w = ctx.saved_tensors
         g2 = gy.reshape(-1, gy.shape[-1])
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = (g2 @ w).view(*gy.shape[:-1], w.shape[1])
+        if ss.active(gy.device) and ctx.needs_input_grad[1] and _SIDE_LIN:
+            # inside a side-stream scope (the world-model backward): the parameter gradients leave the data-gradient
+            # chain and run beside it (ops/sidestream.py)
+            with ss.on_side(gy.device, g2, x):
+                dw, db = _Linear._param_grads(ctx, g2, x)
+            return dx, ss.mark_main(dw), (ss.mark_main(db) if db is not None else None)
+        dw, db = _Linear._param_grads(ctx, g2, x)
+        return dx, dw, db
+
+    @staticmethod
+    def _param_grads(ctx, g2, x):
+        dw = db = None
         if ctx.needs_input_grad[1] and wgrad_ok(g2):
-            dw, db = wgrad(g2, x, bias=ctx.has_bias and ctx.needs_input_grad[2])
-            return dx, dw, db
+            return wgrad(g2, x, bias=ctx.has_bias and ctx.needs_input_grad[2])
         if ctx.needs_input_grad[1]:
             dw = g2.t() @ x.reshape(-1, x.shape[-1])
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = _ext().colsum(g2 if g2.stride(-1) == 1 else g2.contiguous())
-        return dx, dw, db
+        return dw, db
 
 
 def linear(x: Tensor, weight: Tensor, bias: Optional[Tensor] = None) -> Tensor:

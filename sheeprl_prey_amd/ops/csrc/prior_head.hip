@@ -177,12 +177,13 @@ __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
 }
 
 }  // namespace phead
+}  // namespace srl
 
 // false: shape not covered (caller runs the three-launch path)
 bool launch_prior_head(const float* x, long ldx, const float* gamma, const float* beta, float eps, int act, const float* W,
                        const float* b, const float* uni, float alpha, float* sample, long lds, int* idx, long ldi, int ioff,
                        int M, int K, int N, hipStream_t st) {
-  using namespace phead;
+  using namespace srl::phead;
   if (M <= 0 || K <= 0 || K % 16 != 0 || K > 1024 || N % 256 != 0 || ldx % 4 != 0 || !gamma || !beta) return false;
   if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W)) & 15) return false;
   HP p{x, ldx, gamma, beta, W, b, uni, sample, lds, idx, ldi, ioff, M, K, N, act, eps, alpha};
@@ -202,5 +203,3 @@ bool launch_prior_head(const float* x, long ldx, const float* gamma, const float
     hipLaunchKernelGGL(prior_head_kernel<16>, grid, dim3(NT), shm, st, p);
   return true;
 }
-
-}  // namespace srl

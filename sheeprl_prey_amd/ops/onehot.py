@@ -121,9 +121,27 @@ class _GatherFirstLayer(torch.autograd.Function):
             dz = torch.autograd.grad(yy, zz, dy2)[0]
         else:
             dz = dy2
-        dx = dW = dbias = None
+        dx = None
         if ctx.needs_input_grad[0]:
             dx = dz.mm(W).view(xshape)
+        from sheeprl_prey_amd.ops import sidestream as ss
+
+        if ss.active(dz.device) and ops._SIDE_LIN and ctx.needs_input_grad[2]:
+            # inside a side-stream scope (the world-model backward): parameter gradients beside the data chain
+            with ss.on_side(dz.device, dz, x2, idx2):
+                dW, dbias = _GatherFirstLayer._param_grads(ctx, dz, x2, idx2)
+            ss.mark_main(dW)
+            if dbias is not None:
+                ss.mark_main(dbias)
+        else:
+            dW, dbias = _GatherFirstLayer._param_grads(ctx, dz, x2, idx2)
+        return (dx, None, dW, dbias, dg if ctx.needs_input_grad[4] else None, db if ctx.needs_input_grad[5] else None,
+                None, None, None, None, None, None)
+
+    @staticmethod
+    def _param_grads(ctx, dz, x2, idx2):
+        act, use_ln, has_bias, xshape, G, off, n_onehot = ctx.meta
+        dW = dbias = None
         if ctx.needs_input_grad[2] and ops.wgrad_ok(dz):
             # one-hot columns scattered, the dense tail by the split-K kernel, the bias sum on the side (wgrad.hip)
             want_b = has_bias and ctx.needs_input_grad[3]
@@ -134,9 +152,8 @@ class _GatherFirstLayer(torch.autograd.Function):
         elif ctx.needs_input_grad[2]:
             dW = dz.t().mm(x2)  # x2 may be row-strided (a view into the trajectory buffer): mm takes the stride
         if has_bias and ctx.needs_input_grad[3] and dbias is None:
-            dbias = C.colsum(dz)
-        return (dx, None, dW, dbias, dg if ctx.needs_input_grad[4] else None, db if ctx.needs_input_grad[5] else None,
-                None, None, None, None, None, None)
+            dbias = ops._ext().colsum(dz)
+        return dW, dbias
 
 
 def first_layer(x: Tensor, idx: Tensor, G: int, off: int, lin: nn.Linear, ln: Optional[nn.Module], n_onehot: int) -> Tensor:

@@ -393,3 +393,20 @@ def test_imag_discount_skip_first_matches_full_rows():
     cg, disc = ops.imag_discount(logits, dones, 0.99)
     cg1, disc1 = ops.imag_discount(logits[1:], dones, 0.99, skip_first=True)
     assert torch.equal(cg, cg1) and torch.equal(disc, disc1)
+
+
+def test_built_extension_links():
+    """The in-tree HIP extension, when built, imports on the CPU host too (every launcher the bindings declare is
+    defined: an undefined symbol otherwise surfaces only on the GPU box)."""
+    import glob
+    import importlib
+    import os
+
+    import sheeprl_prey_amd
+
+    root = os.path.dirname(sheeprl_prey_amd.__file__)
+    if not glob.glob(os.path.join(root, "ops", "_C*.so")):
+        pytest.skip("extension not built")
+    m = importlib.import_module("sheeprl_prey_amd.ops._C")
+    for name in ("prior_head", "actor_tail", "conv_up_small", "set_up_last_form", "flat_grad_norm"):
+        assert hasattr(m, name), name
