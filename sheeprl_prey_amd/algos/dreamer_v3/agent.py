@@ -392,13 +392,19 @@ class RSSM(nn.Module):
         # GRU then multiplies only x_{t+1} (K = D) and the LN-GRU kernel adds the two parts
         tr_sp = oh.mlp_split(self.transition_model)
         merge = (self._merge_h_ok and use_gather and a_table is not None and layers is not None and gru.linear.bias is None
-                 and tr_sp is not None and tr_sp[1] is not None and tr_sp[0].bias is None and len(tr_sp[2]) > 0)
+                 and tr_sp is not None and tr_sp[1] is not None and len(tr_sp[2]) > 0)
         if merge:
             tr_lin, tr_ln, tr_rest = tr_sp
             Ntr, Na = tr_lin.out_features, a0.out_features
             Wm = torch.cat((tr_lin.weight, a0.weight[:, S:], Wg[:, :Hd]), 0)
             Wgx_t = Wg[:, Hd:].t()
-            hm = torch.mm(h, Wm.t())
+            # the transition layer's bias rides in the GEMM epilogue (zero on the actor / GRU columns: the actor's bias
+            # is added by the gather kernel, the GRU projection has none)
+            bm = None
+            if tr_lin.bias is not None:
+                bm = torch.zeros(Wm.shape[0], device=dev, dtype=Wm.dtype)
+                bm[:Ntr] = tr_lin.bias
+            hm = torch.addmm(bm, h, Wm.t()) if bm is not None else torch.mm(h, Wm.t())
             ytr, mtr, rtr = post.new_empty(M, Ntr), post.new_empty(M), post.new_empty(M)
             tr_act = ops._act_code(tr_ln.act)
             # LayerNorm + act + output Linear + unimix sample of the prior in one launch (prior_head.hip)
@@ -444,7 +450,10 @@ class RSSM(nn.Module):
                 gx = torch.mm(xs, Wgx_t)
                 C.ln_gru_into(gx, buf[t, :, Ap + S:Ap + S + Hd], ln.weight, ln.bias, float(ln.eps),
                               buf[t + 1, :, Ap + S:Ap + S + Hd], x2=hm[:, Ntr + Na:])
-                torch.mm(buf[t + 1, :, Ap + S:Ap + S + Hd], Wm.t(), out=hm)
+                if bm is not None:
+                    torch.addmm(bm, buf[t + 1, :, Ap + S:Ap + S + Hd], Wm.t(), out=hm)
+                else:
+                    torch.mm(buf[t + 1, :, Ap + S:Ap + S + Hd], Wm.t(), out=hm)
                 if phead and C.prior_head(hm[:, :Ntr], tr_ln.weight, tr_ln.bias, float(tr_ln.eps), tr_act, tr_rest[0].weight,
                                           tr_rest[0].bias, U[t, nh * M:], float(self.unimix), buf[t + 1, :, Ap:Ap + S],
                                           IDX[t + 1, :, nh:], A):

@@ -112,11 +112,15 @@ class ContinuousRollout:
         # transition's first-layer pre-activations (kept: the backward reads them with this row stride), the actor
         # trunk's dense first-layer part for step t+1 and the h half of step t+1's GRU input projection
         a0 = self.layers[0][0]
-        self.merge = (self.tr1.bias is None and self.gru.linear.bias is None
-                      and getattr(rssm, "_merge_h_ok", True))
+        self.merge = self.gru.linear.bias is None and getattr(rssm, "_merge_h_ok", True)
         if self.merge:
             self.Na = a0.out_features
             self.Wm = torch.cat((self.tr1.weight, a0.weight[:, S:], self.gru.linear.weight[:, :Hd]), 0)
+            # the transition layer's bias in the GEMM epilogue (zero elsewhere: the gather kernel adds the actor's)
+            self.bm = None
+            if self.tr1.bias is not None:
+                self.bm = torch.zeros(self.Wm.shape[0], device=dev, dtype=self.Wm.dtype)
+                self.bm[:hid] = self.tr1.bias.detach()
             self.hm = post.new_empty(horizon + 1, M, self.Wm.shape[0])  # row t: products of h_t
             self.tr_pre = self.hm[1:, :, :hid]  # transition pre-activations of h_{t+1}, row stride hid + Na + 3Hd
         else:
@@ -131,6 +135,12 @@ class ContinuousRollout:
         self.buf[0, :, :S].copy_(post)
         self.buf[0, :, S:S + Hd].copy_(h)
         oh.onehot_index(post, self.disc, self.IDX[0], 0)
+
+    def _hmm(self, h: Tensor, out: Tensor) -> None:
+        if self.bm is not None:
+            torch.addmm(self.bm, h, self.Wm.t(), out=out)
+        else:
+            torch.mm(h, self.Wm.t(), out=out)
 
     @torch.no_grad()
     def forward(self) -> None:
@@ -149,7 +159,7 @@ class ContinuousRollout:
         merge = self.merge
         if merge:
             hidm, Na = self.tr1.out_features, self.Na
-            torch.mm(buf[0, :, S:S + Hd], self.Wm.t(), out=self.hm[0])
+            self._hmm(buf[0, :, S:S + Hd], self.hm[0])
             Wgx_t = Wg[:, Hd:].t()
         for t in range(self.H + 1):
             ga = (self.IDX[t], G, 0, S, self.a_table) + ((self.hm[t][:, hidm:hidm + Na],) if merge else ())
@@ -173,7 +183,7 @@ class ContinuousRollout:
                 torch.addmm(self.hm[t][:, hidm + Na:], buf[t, :, S + Hd:], Wgx_t, out=gx)
                 C.ln_gru_into(gx, buf[t, :, S:S + Hd], gln.weight, gln.bias, float(gln.eps), buf[t + 1, :, S:S + Hd],
                               self.g_mean[t], self.g_rstd[t])
-                torch.mm(buf[t + 1, :, S:S + Hd], self.Wm.t(), out=self.hm[t + 1])
+                self._hmm(buf[t + 1, :, S:S + Hd], self.hm[t + 1])
                 C.ln_act_fwd_into(self.hm[t + 1], self.hm.shape[-1], self.tr_y[t], hid, tln.weight, tln.bias,
                                   self.tr_mean[t], self.tr_rstd[t], M, hid, 1, float(tln.eps), ops._act_code(tln.act))
             else:

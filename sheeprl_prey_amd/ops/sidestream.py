@@ -22,7 +22,11 @@ branch before its capture ends.  ``join()`` makes the current stream wait for al
 also calls it before it reads a gradient (``parallel/flat_optim.py``: ``wait_grads`` / ``_gather`` / the overlap
 hooks).
 
-``SRL_SIDE_WGRAD=0`` runs the work in line (A/B switch)."""
+Measured SLOWER, so opt-in: ``SRL_SIDE_WGRAD=1`` (default 0).  On the Atari-100k bench the branch took the
+step from 323.4 to 307.4-307.8 env-steps/s (``profiles/r4_side_stream.md``): the side kernels slow the conv
+stack (3.74 -> 4.28 ms/step of kernel time) and the scan while they share the chip, and the busy time barely
+overlaps (13.63 ms kernel time in a 13.48 ms wall window) - the same verdict as round 2's side-stream weight
+gradients in the imagination phase."""
 from __future__ import annotations
 
 import os
@@ -32,7 +36,7 @@ from typing import Dict, Iterator
 import torch
 from torch import Tensor
 
-ENABLED = os.environ.get("SRL_SIDE_WGRAD", "1") != "0"
+ENABLED = os.environ.get("SRL_SIDE_WGRAD", "0") == "1"
 _streams: Dict[int, "torch.cuda.Stream"] = {}
 _pending: Dict[int, bool] = {}
 _depth = 0  # open scopes (module-level: autograd runs GPU backward functions on its own device threads)
