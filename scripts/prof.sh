@@ -12,7 +12,7 @@ timeout -k 10 ${TLIM:-600} rocprofv3 --kernel-trace --output-format csv -d gpuru
 rc=$?
 tail -1 gpurun_out/$NAME.log | cut -c1-400
 f=$(find gpurun_out/tr_$NAME -name "*kernel_trace.csv" | head -1)
-[ -n "$f" ] && python3 scripts/trace_window.py "$f" $STEPS ${TOP:-40} > gpurun_out/${NAME}_summary.md
+[ -n "$f" ] && python3 scripts/trace_window.py "$f" $STEPS ${TOP:-120} > gpurun_out/${NAME}_summary.md
 rm -rf gpurun_out/tr_$NAME
 [ -f gpurun_out/${NAME}_summary.md ] && head -12 gpurun_out/${NAME}_summary.md
 exit $rc

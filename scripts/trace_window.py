@@ -45,7 +45,20 @@ def main(path, steps, top=40):
     print()
     print("| ms/step | calls/step | avg us | % busy | kernel |\n|---:|---:|---:|---:|---|")
     for name, (d, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:top]:
-        print(f"| {d / 1e6 / steps:.3f} | {c / steps:.1f} | {d / c / 1e3:.1f} | {100 * d / busy:.1f} | `{name[:95]}` |")
+        print(f"| {d / 1e6 / steps:.3f} | {c / steps:.1f} | {d / c / 1e3:.1f} | {100 * d / busy:.1f} | `{_short(name)}` |")
+
+
+def _short(name: str) -> str:
+    """First 95 characters; ATen kernels also name their functor / op (templated names share the prefix)."""
+    if "at::native" not in name or len(name) <= 95:
+        return name[:95]
+    import re
+
+    ops = []
+    for m in re.findall(r"(\w*(?:Functor|functor|_kernel_cuda|_kernel_impl|copy_kernel|Op)\w*)", name):
+        if m not in ops and not m.startswith("gpu_kernel"):
+            ops.append(m)
+    return name[:60] + " .. " + ",".join(ops[:3])
 
 
 if __name__ == "__main__":

@@ -297,8 +297,13 @@ class RSSM(nn.Module):
 
     # ---- MI355X imagination: buffer-resident no-grad rollout ---------------------------
     _actor_tail_ok = os.environ.get("SRL_ACTOR_TAIL", "1") != "0"  # A/B switch of the fused rollout actor tail
-    _merge_h_ok = os.environ.get("SRL_IMAG_MERGE", "1") != "0"  # A/B switch of the merged h_{t+1} GEMM (imagine_discrete)
-    _prior_head_ok = os.environ.get("SRL_PRIOR_HEAD", "1") != "0"  # A/B switch of the one-launch prior head (prior_head.hip)
+    # merged h_{t+1} GEMM of the imagination step (imagine_discrete / imagine_cont), opt-in: measured slower on the
+    # Atari-100k bench (313.0 / 313.5 vs 323.3 env-steps/s, continuous 115.6 vs 118.0; profiles/r4_imag_merge.md) -
+    # hipBLASLt runs the merged [1024, 512] x [512, 2560] + bias GEMM at ~78 TF/s (34.5 us) and the remaining
+    # K = 512 GRU half at ~70 TF/s (23.1 us) where the (h | x) K = 1024 GEMM ran at ~116 TF/s
+    _merge_h_ok = os.environ.get("SRL_IMAG_MERGE", "0") == "1"
+    # one-launch prior head (prior_head.hip; used on the merged path): 30.6 us vs ~28 us for LayerNorm + GEMM + sampler
+    _prior_head_ok = os.environ.get("SRL_PRIOR_HEAD", "1") != "0"
 
     def imagine_fast_ok(self, actor) -> bool:
         gru = self.recurrent_model.rnn
