@@ -18,7 +18,7 @@
 // XCD's L2) through a double-buffered register batch of UK chunks; v_mfma_f32_16x16x4_f32 with the
 // float4-permuted K order of scan_dev.h (a[j] / b[j] = K index 16c + 4g + j on both operands).  The accumulator
 // map (col = lane & 15, row = 4 (lane >> 4) + r) puts a row's 32 classes on the 16 lanes of one DPP row x two
-// registers, so the unimix / softmax / CDF of the sampler are 16-lane shuffles with no LDS round trip.
+// registers, so the unimix / softmax / CDF of the sampler are DPP row reductions with no LDS round trip.
 #include "common.h"
 #include "scan_dev.h"
 
@@ -47,23 +47,11 @@ struct HP {
   float eps, alpha;
 };
 
-__device__ __forceinline__ float max16(float v) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 16));
-  return v;
-}
-__device__ __forceinline__ float sum16(float v) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 16);
-  return v;
-}
-__device__ __forceinline__ float incl16(float v, int j) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) {
-    const float t = __shfl_up(v, o, 16);
-    if (j >= o) v += t;
-  }
-  return v;
+// 16-lane (DPP row) reductions / scan: no LDS-crossbar shuffles (common.h row16_*); the row's last lane by readlanes
+__device__ __forceinline__ float row16_last(float v) {
+  const float a = lane_f(v, 15), b = lane_f(v, 31), c = lane_f(v, 47), d = lane_f(v, 63);
+  const int r = (threadIdx.x >> 4) & 3;
+  return r == 0 ? a : (r == 1 ? b : (r == 2 ? c : d));
 }
 
 template <int KV>
@@ -147,9 +135,9 @@ __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
     const float l0 = acc0[r] + bb0, l1 = acc1[r] + bb1;
     float m0 = l0, m1 = l1;
     if (p.alpha > 0.f) {
-      const float mx = max16(fmaxf(l0, l1));
+      const float mx = row16_max(fmaxf(l0, l1));
       const float e0 = __expf(l0 - mx), e1 = __expf(l1 - mx);
-      const float s = sum16(e0 + e1);
+      const float s = row16_sum(e0 + e1);
       float q0 = (1.f - p.alpha) * (e0 / s) + p.alpha * inv;
       float q1 = (1.f - p.alpha) * (e1 / s) + p.alpha * inv;
       q0 = fminf(fmaxf(q0, FEPS), 1.f - FEPS);
@@ -157,15 +145,15 @@ __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
       m0 = logf(q0);
       m1 = logf(q1);
     }
-    const float mx2 = max16(fmaxf(m0, m1));
+    const float mx2 = row16_max(fmaxf(m0, m1));
     const float e0 = __expf(m0 - mx2), e1 = __expf(m1 - mx2);
-    const float s2 = sum16(e0 + e1);
-    const float cdf0 = incl16(e0 / s2, i);
-    const float cdf1 = __shfl(cdf0, 15, 16) + incl16(e1 / s2, i);
-    const float cmax = __shfl(cdf1, 15, 16);
+    const float s2 = row16_sum(e0 + e1);
+    const float cdf0 = row16_scan(e0 / s2);
+    const float cdf1 = row16_last(cdf0) + row16_scan(e1 / s2);
+    const float cmax = row16_last(cdf1);
     const float u = row < nrow ? p.uni[(long)(r0 + row) * G + gg] : 0.f;
     const float thr = u * cmax;
-    int pick = (int)sum16((cdf0 < thr ? 1.f : 0.f) + (cdf1 < thr ? 1.f : 0.f));
+    int pick = (int)row16_sum((cdf0 < thr ? 1.f : 0.f) + (cdf1 < thr ? 1.f : 0.f));
     if (pick > CL - 1) pick = CL - 1;
     if (row < nrow) {
       float* srow = p.sample + (long)(r0 + row) * p.lds + n0;
