@@ -21,7 +21,7 @@ BASE = ["exp=dreamer_v3", "env=gym", "env.id=CartPole-v1", "mlp_keys.encoder=[st
         "env.sync_env=True", "env.capture_video=False", "algo.train_every=4", "algo.learning_starts=1024",
         "algo.dense_units=512", "algo.mlp_layers=2", "algo.world_model.recurrent_model.recurrent_state_size=512",
         "algo.world_model.transition_model.hidden_size=512", "algo.world_model.representation_model.hidden_size=512",
-        "buffer.size=100000", "checkpoint.every=100000000", "metric.log_every=2000", "seed=5"]
+        "buffer.size=100000", "checkpoint.every=100000000", "metric.log_every=500", "seed=5"]
 
 
 def run(name, over):

@@ -4,7 +4,7 @@
 set -u
 export TMPDIR=/tmp PYTHONPATH=.
 mkdir -p gpurun_out
-timeout -k 10 700 python -u scripts/dv3_return_curve.py gpurun_out/r4_dv3_cartpole_curve.md 30000 3000 > gpurun_out/r4_curve.log 2>&1 \
+timeout -k 10 700 python -u scripts/dv3_return_curve.py gpurun_out/r4_dv3_cartpole_curve.md 40000 3000 > gpurun_out/r4_curve.log 2>&1 \
   && tail -1 gpurun_out/r4_curve.log || { tail -30 gpurun_out/r4_curve.log; exit 1; }
 LAG=0 STEPS=20480 bash scripts/rehearse_fleet.sh > gpurun_out/r4_fleet_lag0.log 2>&1 && tail -1 gpurun_out/r4_fleet_lag0.log | cut -c1-1500 || { tail -30 gpurun_out/r4_fleet_lag0.log; exit 1; }
 LAG=1 STEPS=20480 bash scripts/rehearse_fleet.sh > gpurun_out/r4_fleet_lag1.log 2>&1 && tail -1 gpurun_out/r4_fleet_lag1.log | cut -c1-1500 || { tail -30 gpurun_out/r4_fleet_lag1.log; exit 1; }
