@@ -65,16 +65,14 @@ __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
   const int G = p.N / CL;
   const int gg = blockIdx.y * 8 + w;  // this wave's categorical
   const int n0 = gg * CL;
-  const int nch = p.K >> 4;
   // first B batch requested before anything else: its latency hides behind the staging and the LayerNorm
   const float* wr0 = p.W + (long)(n0 + i) * p.K + 4 * g;
   const float* wr1 = wr0 + 16L * p.K;
   f4 cb0[UK], cb1[UK];
 #pragma unroll
   for (int q = 0; q < UK; ++q) {
-    const int c = min(q, nch - 1);
-    cb0[q] = *(const f4*)(wr0 + 16 * c);
-    cb1[q] = *(const f4*)(wr1 + 16 * c);
+    cb0[q] = *(const f4*)(wr0 + 16 * q);
+    cb1[q] = *(const f4*)(wr1 + 16 * q);
   }
   const float bb0 = p.b ? p.b[n0 + i] : 0.f, bb1 = p.b ? p.b[n0 + 16 + i] : 0.f;
   // 16 x K row tile -> LDS (rows past M zero), then LayerNorm + act in place (two rows per wave)
@@ -89,42 +87,39 @@ __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
     scandev::wave_ln_act_row<KV>(sm + r * lda, p.K, p.eps, p.gamma, p.beta, p.act, mu, rs);
   }
   __syncthreads();
-  // logits tile [16 rows x 32 classes] of this wave's categorical
+  // logits tile [16 rows x 32 classes] of this wave's categorical.  K = 64 * KV exactly (compile-time trip count,
+  // fully unrolled) and every B load unconditional (the last batch re-reads itself): an exec-masked or branched
+  // load makes the wait-count pass drain vmcnt before the next batch, serialising load latency with the MFMAs
+  // (the conv.hip main-loop lesson)
   const float* arow = sm + i * lda + 4 * g;
   f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  constexpr int NCH = 4 * KV;
+  static_assert(NCH % UK == 0, "K chunks per batch");
 #pragma unroll
-  for (int c0 = 0; c0 < 4 * KV; c0 += UK) {
-    if (c0 >= nch) break;
+  for (int c0 = 0; c0 < NCH; c0 += UK) {
     f4 nb0[UK], nb1[UK];
-    const bool more = c0 + UK < nch;
-    if (more) {
+    const int cn = c0 + UK < NCH ? c0 + UK : c0;
 #pragma unroll
-      for (int q = 0; q < UK; ++q) {
-        const int c = min(c0 + UK + q, nch - 1);
-        nb0[q] = *(const f4*)(wr0 + 16 * c);
-        nb1[q] = *(const f4*)(wr1 + 16 * c);
-      }
+    for (int q = 0; q < UK; ++q) {
+      nb0[q] = *(const f4*)(wr0 + 16 * (cn + q));
+      nb1[q] = *(const f4*)(wr1 + 16 * (cn + q));
     }
 #pragma unroll
     for (int q = 0; q < UK; ++q) {
-      if (c0 + q < nch) {
-        const f4 a = *(const f4*)(arow + 16 * (c0 + q));
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], cb0[q][0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], cb1[q][0], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], cb0[q][1], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], cb1[q][1], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], cb0[q][2], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], cb1[q][2], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], cb0[q][3], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], cb1[q][3], acc1, 0, 0, 0);
-      }
+      const f4 a = *(const f4*)(arow + 16 * (c0 + q));
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], cb0[q][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], cb1[q][0], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], cb0[q][1], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], cb1[q][1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], cb0[q][2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], cb1[q][2], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], cb0[q][3], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], cb1[q][3], acc1, 0, 0, 0);
     }
-    if (more) {
 #pragma unroll
-      for (int q = 0; q < UK; ++q) {
-        cb0[q] = nb0[q];
-        cb1[q] = nb1[q];
-      }
+    for (int q = 0; q < UK; ++q) {
+      cb0[q] = nb0[q];
+      cb1[q] = nb1[q];
     }
   }
   // unimix + categorical sample per (row, categorical): class j on lane i of register 0, class 16 + j on register 1
@@ -172,12 +167,14 @@ bool launch_prior_head(const float* x, long ldx, const float* gamma, const float
                        const float* b, const float* uni, float alpha, float* sample, long lds, int* idx, long ldi, int ioff,
                        int M, int K, int N, hipStream_t st) {
   using namespace srl::phead;
-  if (M <= 0 || K <= 0 || K % 16 != 0 || K > 1024 || N % 256 != 0 || ldx % 4 != 0 || !gamma || !beta) return false;
+  if (M <= 0 || (K != 256 && K != 512 && K != 1024) || N % 256 != 0 || ldx % 4 != 0 || !gamma || !beta) return false;
   if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W)) & 15) return false;
   HP p{x, ldx, gamma, beta, W, b, uni, sample, lds, idx, ldi, ioff, M, K, N, act, eps, alpha};
   const dim3 grid((M + 15) / 16, N / 256);
   const size_t shm = (size_t)16 * (K + 4) * sizeof(float);
   static const bool lds_set = [] {  // K = 1024 needs 65.8 KB of the 160 KB
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prior_head_kernel<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              16 * 260 * 4);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prior_head_kernel<8>), hipFuncAttributeMaxDynamicSharedMemorySize,
                               16 * 516 * 4);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prior_head_kernel<16>), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -185,7 +182,9 @@ bool launch_prior_head(const float* x, long ldx, const float* gamma, const float
     return true;
   }();
   (void)lds_set;
-  if (K <= 512)
+  if (K == 256)
+    hipLaunchKernelGGL(prior_head_kernel<4>, grid, dim3(NT), shm, st, p);
+  else if (K == 512)
     hipLaunchKernelGGL(prior_head_kernel<8>, grid, dim3(NT), shm, st, p);
   else
     hipLaunchKernelGGL(prior_head_kernel<16>, grid, dim3(NT), shm, st, p);
