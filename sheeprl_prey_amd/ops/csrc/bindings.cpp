@@ -784,6 +784,8 @@ std::vector<int64_t> scanp_info(int64_t B, int64_t S, int64_t D, int64_t H, int6
 // Write into a caller-owned row-strided view (e.g. a slice of an imagination trajectory buffer):
 // out must have unit stride in its last dim; rows may be strided.
 // ``mean`` / ``rstd`` (optional [M]): keep the LayerNorm row statistics (for a later ln_gru_bwd_into).
+void set_gru_vec(bool on);
+
 void ln_gru_into(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::Tensor beta, double eps, torch::Tensor out,
                  c10::optional<torch::Tensor> mean_out, c10::optional<torch::Tensor> rstd_out, c10::optional<torch::Tensor> x2) {
   check_f32(x, "x");
@@ -1109,6 +1111,7 @@ void register_ext(pybind11::module& m);
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_conv(m);
   register_ext(m);
+  m.def("set_gru_vec", &set_gru_vec);  // float4 wide-row LN-GRU forward on (default) / off (A/B, tests)
   m.def("ln_gru_into", &ln_gru_into, pybind11::arg("x"), pybind11::arg("h"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("eps"), pybind11::arg("out"), pybind11::arg("mean") = pybind11::none(),
         pybind11::arg("rstd") = pybind11::none(), pybind11::arg("x2") = pybind11::none());

@@ -6,6 +6,9 @@
 // so every load is coalesced.  Backward recomputes z from (x, mean, rstd).
 #include "common.h"
 
+#include <cstdint>
+#include <cstdlib>
+
 namespace srl {
 
 template <int MAXH>
@@ -55,6 +58,75 @@ __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict
         float hp = h[(int64_t)row * ldh + j];
         hn[(int64_t)row * ldo + j] = u * c + (1.f - u) * hp;
       }
+    }
+    if (threadIdx.x == 0) {
+      mean_out[row] = mu;
+      rstd_out[row] = rs;
+    }
+  }
+}
+
+// Wide-row form (H a multiple of 1024: the L / XL deter sizes): float4 loads and stores, Q float4 per gate per
+// thread, gamma / beta / h requested while the row statistics reduce.  The scalar form above issues 3 * MAXH
+// four-byte loads per thread per row.
+template <int Q>
+__global__ void __launch_bounds__(256) ln_gru_fwd4_kernel(const float* __restrict__ x, const float* __restrict__ h, int ldh,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          float* __restrict__ hn, float* __restrict__ mean_out,
+                                                          float* __restrict__ rstd_out, int M, int H, float eps,
+                                                          int ldo, const float* __restrict__ x2, int ldx2) {
+  __shared__ float red[4];
+  const int N = 3 * H, H4 = H >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(gamma);
+  const float4* b4 = reinterpret_cast<const float4*>(beta);
+  for (int row = blockIdx.x; row < M; row += gridDim.x) {
+    const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)row * N);
+    const float4* x2r = x2 ? reinterpret_cast<const float4*>(x2 + (int64_t)row * ldx2) : nullptr;
+    float4 v[3][Q];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+      const int j4 = threadIdx.x + k * 256;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        float4 a = xr[g * H4 + j4];
+        if (x2r) {
+          const float4 b = x2r[g * H4 + j4];
+          a.x += b.x, a.y += b.y, a.z += b.z, a.w += b.w;
+        }
+        v[g][k] = a;
+        s += (a.x + a.y) + (a.z + a.w);
+      }
+    }
+    const float mu = block_sum<4>(s, red) / N;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < Q; ++k)
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        const float a = v[g][k].x - mu, b = v[g][k].y - mu, c = v[g][k].z - mu, d = v[g][k].w - mu;
+        q += (a * a + b * b) + (c * c + d * d);
+      }
+    const float rs = rsqrtf(block_sum<4>(q, red) / N + eps);
+    const float4* hr = reinterpret_cast<const float4*>(h + (int64_t)row * ldh);
+    float4* outr = reinterpret_cast<float4*>(hn + (int64_t)row * ldo);
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {
+      const int j4 = threadIdx.x + k * 256;
+      const float4 gr = g4[j4], gc = g4[H4 + j4], gu = g4[2 * H4 + j4];
+      const float4 br = b4[j4], bc = b4[H4 + j4], bu = b4[2 * H4 + j4];
+      const float4 hp = hr[j4];
+      float4 o;
+#define SRL_GRU_LANE(C)                                                        \
+  {                                                                            \
+    const float r = sigmoidf_((v[0][k].C - mu) * rs * gr.C + br.C);            \
+    const float c = tanhf(r * ((v[1][k].C - mu) * rs * gc.C + bc.C));          \
+    const float u = sigmoidf_((v[2][k].C - mu) * rs * gu.C + bu.C - 1.f);      \
+    o.C = u * c + (1.f - u) * hp.C;                                            \
+  }
+      SRL_GRU_LANE(x) SRL_GRU_LANE(y) SRL_GRU_LANE(z) SRL_GRU_LANE(w)
+#undef SRL_GRU_LANE
+      outr[j4] = o;
     }
     if (threadIdx.x == 0) {
       mean_out[row] = mu;
@@ -144,6 +216,13 @@ __global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict
 
 using namespace srl;
 
+// A/B switch of the float4 wide-row forward (SRL_GRU_VEC=0: the scalar kernel for every H)
+static bool g_gru_vec = [] {
+  const char* e = getenv("SRL_GRU_VEC");
+  return !(e && e[0] == '0');
+}();
+void set_gru_vec(bool on) { g_gru_vec = on; }
+
 static int gru_maxh(int H) {
   if (H <= 512) return 2;
   if (H <= 1024) return 4;
@@ -157,6 +236,17 @@ bool launch_ln_gru_fwd(const float* x, const float* h, int ldh, const float* gam
   if (ldo <= 0) ldo = H;
   int mh = gru_maxh(H);
   dim3 g(M < 8192 ? M : 8192), b(256);
+  const bool al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(h) | reinterpret_cast<uintptr_t>(hn) |
+                    reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
+                    reinterpret_cast<uintptr_t>(x2)) & 15) == 0 && ldh % 4 == 0 && ldo % 4 == 0 && (!x2 || ldx2 % 4 == 0);
+  if (g_gru_vec && al && H % 1024 == 0 && H <= 4096) {
+    switch (H / 1024) {
+      case 1: hipLaunchKernelGGL(ln_gru_fwd4_kernel<1>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
+      case 2: hipLaunchKernelGGL(ln_gru_fwd4_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
+      case 4: hipLaunchKernelGGL(ln_gru_fwd4_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
+      default: break;
+    }
+  }
   switch (mh) {
     case 2: hipLaunchKernelGGL(ln_gru_fwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
     case 4: hipLaunchKernelGGL(ln_gru_fwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;

@@ -243,3 +243,37 @@ def test_colsum_graph_replay_zeroes_accumulator():
         _close(out, x.sum(0), rtol=1e-4, atol=1e-3)
         _close(oa, ref_a, rtol=1e-4, atol=1e-4)
         _close(ob, ref_b, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("H", [1024, 2048, 4096])
+@pytest.mark.parametrize("split", [False, True])
+def test_ln_gru_wide_rows_vec_vs_scalar(H, split):
+    """Wide-row float4 LN-GRU forward (H % 1024 == 0) vs the scalar kernel and the fp32 reference; optional second
+    GEMM part (x2, row-strided) and a row-strided output view."""
+    C = ops._ext()
+    torch.manual_seed(0)
+    M = 37
+    x = torch.randn(M, 3 * H, device=DEV)
+    h = torch.randn(M, H, device=DEV)
+    w = 1 + 0.1 * torch.randn(3 * H, device=DEV)
+    b = 0.1 * torch.randn(3 * H, device=DEV)
+    ref_y = ref.ln_gru(x, h, w, b, 1e-3)
+    outs = []
+    for vec in (True, False):
+        C.set_gru_vec(vec)
+        try:
+            buf = torch.full((M, H + 8), 7.0, device=DEV)
+            mean, rstd = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+            if split:
+                x2s = torch.randn(M, 3 * H + 4, device=DEV)
+                x2 = x2s[:, :3 * H]
+                C.ln_gru_into(x - x2, h, w, b, 1e-3, buf[:, 4:4 + H], mean, rstd, x2=x2)
+            else:
+                C.ln_gru_into(x, h, w, b, 1e-3, buf[:, 4:4 + H], mean, rstd)
+        finally:
+            C.set_gru_vec(True)
+        assert torch.all(buf[:, :4] == 7.0) and torch.all(buf[:, 4 + H:] == 7.0)
+        outs.append(buf[:, 4:4 + H].clone())
+        _close(buf[:, 4:4 + H], ref_y, rtol=1e-4, atol=1e-5)
+        _close(mean, x.mean(-1), rtol=1e-4, atol=1e-5)
+    _close(outs[0], outs[1], rtol=1e-5, atol=1e-6)
