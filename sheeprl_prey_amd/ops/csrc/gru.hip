@@ -66,73 +66,128 @@ __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict
   }
 }
 
-// Wide-row form (H a multiple of 1024: the L / XL deter sizes): float4 loads and stores, Q float4 per gate per
-// thread, gamma / beta / h requested while the row statistics reduce.  The scalar form above issues 3 * MAXH
-// four-byte loads per thread per row.
-template <int Q>
-__global__ void __launch_bounds__(256) ln_gru_fwd4_kernel(const float* __restrict__ x, const float* __restrict__ h, int ldh,
-                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                          float* __restrict__ hn, float* __restrict__ mean_out,
-                                                          float* __restrict__ rstd_out, int M, int H, float eps,
-                                                          int ldo, const float* __restrict__ x2, int ldx2) {
-  __shared__ float red[4];
-  const int N = 3 * H, H4 = H >> 2;
+// Wide-row forms (H a multiple of 1024: the L / XL deter sizes): one float4 per gate per thread, H / 4 threads
+// (NW = H / 256 waves) per row, so a 16-row scan step still runs 16 x NW waves, and every load is a 16-byte
+// vector load issued before the row statistics reduce.  The scalar forms issue 3 * MAXH four-byte loads per
+// thread per row from 256 threads.
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) ln_gru_fwd4_kernel(const float* __restrict__ x, const float* __restrict__ h, int ldh,
+                                                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                              float* __restrict__ hn, float* __restrict__ mean_out,
+                                                              float* __restrict__ rstd_out, int M, int H, float eps,
+                                                              int ldo, const float* __restrict__ x2, int ldx2) {
+  __shared__ float red[NW];
+  const int N = 3 * H, H4 = H >> 2, j4 = threadIdx.x;
   const float4* g4 = reinterpret_cast<const float4*>(gamma);
   const float4* b4 = reinterpret_cast<const float4*>(beta);
+  const float4 gr = g4[j4], gc = g4[H4 + j4], gu = g4[2 * H4 + j4];
+  const float4 br = b4[j4], bc = b4[H4 + j4], bu = b4[2 * H4 + j4];
   for (int row = blockIdx.x; row < M; row += gridDim.x) {
     const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)row * N);
     const float4* x2r = x2 ? reinterpret_cast<const float4*>(x2 + (int64_t)row * ldx2) : nullptr;
-    float4 v[3][Q];
+    float4 v[3];
     float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < Q; ++k) {
-      const int j4 = threadIdx.x + k * 256;
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        float4 a = xr[g * H4 + j4];
-        if (x2r) {
-          const float4 b = x2r[g * H4 + j4];
-          a.x += b.x, a.y += b.y, a.z += b.z, a.w += b.w;
-        }
-        v[g][k] = a;
-        s += (a.x + a.y) + (a.z + a.w);
+    for (int g = 0; g < 3; ++g) {
+      float4 a = xr[g * H4 + j4];
+      if (x2r) {
+        const float4 b = x2r[g * H4 + j4];
+        a.x += b.x, a.y += b.y, a.z += b.z, a.w += b.w;
       }
+      v[g] = a;
+      s += (a.x + a.y) + (a.z + a.w);
     }
-    const float mu = block_sum<4>(s, red) / N;
+    const float4 hp = reinterpret_cast<const float4*>(h + (int64_t)row * ldh)[j4];
+    const float mu = block_sum<NW>(s, red) / N;
     float q = 0.f;
 #pragma unroll
-    for (int k = 0; k < Q; ++k)
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        const float a = v[g][k].x - mu, b = v[g][k].y - mu, c = v[g][k].z - mu, d = v[g][k].w - mu;
-        q += (a * a + b * b) + (c * c + d * d);
-      }
-    const float rs = rsqrtf(block_sum<4>(q, red) / N + eps);
-    const float4* hr = reinterpret_cast<const float4*>(h + (int64_t)row * ldh);
-    float4* outr = reinterpret_cast<float4*>(hn + (int64_t)row * ldo);
-#pragma unroll
-    for (int k = 0; k < Q; ++k) {
-      const int j4 = threadIdx.x + k * 256;
-      const float4 gr = g4[j4], gc = g4[H4 + j4], gu = g4[2 * H4 + j4];
-      const float4 br = b4[j4], bc = b4[H4 + j4], bu = b4[2 * H4 + j4];
-      const float4 hp = hr[j4];
-      float4 o;
-#define SRL_GRU_LANE(C)                                                        \
-  {                                                                            \
-    const float r = sigmoidf_((v[0][k].C - mu) * rs * gr.C + br.C);            \
-    const float c = tanhf(r * ((v[1][k].C - mu) * rs * gc.C + bc.C));          \
-    const float u = sigmoidf_((v[2][k].C - mu) * rs * gu.C + bu.C - 1.f);      \
-    o.C = u * c + (1.f - u) * hp.C;                                            \
-  }
-      SRL_GRU_LANE(x) SRL_GRU_LANE(y) SRL_GRU_LANE(z) SRL_GRU_LANE(w)
-#undef SRL_GRU_LANE
-      outr[j4] = o;
+    for (int g = 0; g < 3; ++g) {
+      const float a = v[g].x - mu, b = v[g].y - mu, c = v[g].z - mu, d = v[g].w - mu;
+      q += (a * a + b * b) + (c * c + d * d);
     }
+    const float rs = rsqrtf(block_sum<NW>(q, red) / N + eps);
+    float4 o;
+#define SRL_GRU_LANE(C)                                                   \
+  {                                                                       \
+    const float r = sigmoidf_((v[0].C - mu) * rs * gr.C + br.C);          \
+    const float c = tanhf(r * ((v[1].C - mu) * rs * gc.C + bc.C));        \
+    const float u = sigmoidf_((v[2].C - mu) * rs * gu.C + bu.C - 1.f);    \
+    o.C = u * c + (1.f - u) * hp.C;                                       \
+  }
+    SRL_GRU_LANE(x) SRL_GRU_LANE(y) SRL_GRU_LANE(z) SRL_GRU_LANE(w)
+#undef SRL_GRU_LANE
+    reinterpret_cast<float4*>(hn + (int64_t)row * ldo)[j4] = o;
     if (threadIdx.x == 0) {
       mean_out[row] = mu;
       rstd_out[row] = rs;
     }
   }
+}
+
+// Backward of the wide-row form: same thread map; per-block LN-GRU parameter partials kept in registers across
+// the block's rows ([grid, 3H] partial rows, reduced by colsum2 as for the scalar form).
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) ln_gru_bwd4_kernel(const float* __restrict__ x, const float* __restrict__ h, int ldh,
+                                                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                              const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                              const float* __restrict__ dhn, float* __restrict__ dx,
+                                                              float* __restrict__ dh, float* __restrict__ pdg,
+                                                              float* __restrict__ pdb, int M, int H) {
+  __shared__ float red[NW];
+  const int N = 3 * H, H4 = H >> 2, j4 = threadIdx.x;
+  const float4* g4 = reinterpret_cast<const float4*>(gamma);
+  const float4* b4 = reinterpret_cast<const float4*>(beta);
+  const float4 G0 = g4[j4], G1 = g4[H4 + j4], G2 = g4[2 * H4 + j4];
+  const float4 B0 = b4[j4], B1 = b4[H4 + j4], B2 = b4[2 * H4 + j4];
+  float4 ag0 = {0.f, 0.f, 0.f, 0.f}, ag1 = ag0, ag2 = ag0, ab0 = ag0, ab1 = ag0, ab2 = ag0;
+  for (int row = blockIdx.x; row < M; row += gridDim.x) {
+    const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)row * N);
+    const float4 X0 = xr[j4], X1 = xr[H4 + j4], X2 = xr[2 * H4 + j4];
+    const float4 hp = reinterpret_cast<const float4*>(h + (int64_t)row * ldh)[j4];
+    const float4 go = reinterpret_cast<const float4*>(dhn + (int64_t)row * H)[j4];
+    const float mu = mean[row], rs = rstd[row];
+    float4 xh0, xh1, xh2, d0, d1, d2, dho;
+    float s1 = 0.f, s2 = 0.f;
+#define SRL_GRU_BWD_LANE(C)                                                       \
+  {                                                                               \
+    const float hr = (X0.C - mu) * rs, hc = (X1.C - mu) * rs, hu = (X2.C - mu) * rs; \
+    const float zc = hc * G1.C + B1.C;                                            \
+    const float r = sigmoidf_(hr * G0.C + B0.C);                                  \
+    const float c = tanhf(r * zc);                                                \
+    const float u = sigmoidf_(hu * G2.C + B2.C - 1.f);                            \
+    const float g = go.C;                                                         \
+    dho.C = g * (1.f - u);                                                        \
+    const float dzu = g * (c - hp.C) * u * (1.f - u);                             \
+    const float da = g * u * (1.f - c * c);                                       \
+    const float dzc = da * r;                                                     \
+    const float dzr = da * zc * r * (1.f - r);                                    \
+    ag0.C += dzr * hr, ag1.C += dzc * hc, ag2.C += dzu * hu;                      \
+    ab0.C += dzr, ab1.C += dzc, ab2.C += dzu;                                     \
+    xh0.C = hr, xh1.C = hc, xh2.C = hu;                                           \
+    d0.C = dzr * G0.C, d1.C = dzc * G1.C, d2.C = dzu * G2.C;                      \
+    s1 += d0.C + d1.C + d2.C;                                                     \
+    s2 += d0.C * hr + d1.C * hc + d2.C * hu;                                      \
+  }
+    SRL_GRU_BWD_LANE(x) SRL_GRU_BWD_LANE(y) SRL_GRU_BWD_LANE(z) SRL_GRU_BWD_LANE(w)
+#undef SRL_GRU_BWD_LANE
+    reinterpret_cast<float4*>(dh + (int64_t)row * H)[j4] = dho;
+    const float m1 = block_sum<NW>(s1, red) / N;
+    const float m2 = block_sum<NW>(s2, red) / N;
+    float4* dxr = reinterpret_cast<float4*>(dx + (int64_t)row * N);
+    float4 o;
+#define SRL_DX(D, XH, OUTI)                                       \
+  o.x = rs * (D.x - m1 - XH.x * m2), o.y = rs * (D.y - m1 - XH.y * m2); \
+  o.z = rs * (D.z - m1 - XH.z * m2), o.w = rs * (D.w - m1 - XH.w * m2); \
+  dxr[OUTI] = o;
+    SRL_DX(d0, xh0, j4)
+    SRL_DX(d1, xh1, H4 + j4)
+    SRL_DX(d2, xh2, 2 * H4 + j4)
+#undef SRL_DX
+  }
+  float4* pg = reinterpret_cast<float4*>(pdg + (int64_t)blockIdx.x * N);
+  float4* pb = reinterpret_cast<float4*>(pdb + (int64_t)blockIdx.x * N);
+  pg[j4] = ag0, pg[H4 + j4] = ag1, pg[2 * H4 + j4] = ag2;
+  pb[j4] = ab0, pb[H4 + j4] = ab1, pb[2 * H4 + j4] = ab2;
 }
 
 template <int MAXH>
@@ -216,7 +271,7 @@ __global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict
 
 using namespace srl;
 
-// A/B switch of the float4 wide-row forward (SRL_GRU_VEC=0: the scalar kernel for every H)
+// A/B switch of the float4 wide-row forward / backward (SRL_GRU_VEC=0: the scalar kernels for every H)
 static bool g_gru_vec = [] {
   const char* e = getenv("SRL_GRU_VEC");
   return !(e && e[0] == '0');
@@ -240,10 +295,11 @@ bool launch_ln_gru_fwd(const float* x, const float* h, int ldh, const float* gam
                     reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
                     reinterpret_cast<uintptr_t>(x2)) & 15) == 0 && ldh % 4 == 0 && ldo % 4 == 0 && (!x2 || ldx2 % 4 == 0);
   if (g_gru_vec && al && H % 1024 == 0 && H <= 4096) {
+    const dim3 bw(H / 4);
     switch (H / 1024) {
-      case 1: hipLaunchKernelGGL(ln_gru_fwd4_kernel<1>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
-      case 2: hipLaunchKernelGGL(ln_gru_fwd4_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
-      case 4: hipLaunchKernelGGL(ln_gru_fwd4_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
+      case 1: hipLaunchKernelGGL(ln_gru_fwd4_kernel<4>, g, bw, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
+      case 2: hipLaunchKernelGGL(ln_gru_fwd4_kernel<8>, g, bw, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
+      case 4: hipLaunchKernelGGL(ln_gru_fwd4_kernel<16>, g, bw, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
       default: break;
     }
   }
@@ -267,6 +323,18 @@ bool launch_ln_gru_bwd(const float* x, const float* h, int ldh, const float* gam
   int mh = gru_maxh(H);
   int grid = ln_gru_bwd_grid(M);
   dim3 g(grid), b(256);
+  const bool al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(h) | reinterpret_cast<uintptr_t>(dhn) |
+                    reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(dh) | reinterpret_cast<uintptr_t>(pdg) |
+                    reinterpret_cast<uintptr_t>(pdb) | reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta)) &
+                   15) == 0 && ldh % 4 == 0;
+  if (g_gru_vec && al && H % 1024 == 0 && H <= 4096 && (H / 1024 == 1 || H / 1024 == 2 || H / 1024 == 4)) {
+    const dim3 bw(H / 4);
+    if (H == 1024) hipLaunchKernelGGL(ln_gru_bwd4_kernel<4>, g, bw, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H);
+    else if (H == 2048) hipLaunchKernelGGL(ln_gru_bwd4_kernel<8>, g, bw, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H);
+    else hipLaunchKernelGGL(ln_gru_bwd4_kernel<16>, g, bw, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H);
+    if (dgamma) launch_colsum2(pdg, pdb, dgamma, dbeta, grid, 3 * H, 1, st);
+    return true;
+  }
   switch (mh) {
     case 2: hipLaunchKernelGGL(ln_gru_bwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
     case 4: hipLaunchKernelGGL(ln_gru_bwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
