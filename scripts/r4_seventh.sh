@@ -10,3 +10,4 @@ for v in 1 0; do
   SRL_GRU_VEC=$v timeout -k 10 500 python bench.py --xl --steps 12 --warmup 4 --prefill 100 > gpurun_out/r47_xl_$v.log 2>&1 \
     && echo "xl vec=$v $(grep '"metric"' gpurun_out/r47_xl_$v.log | tail -1 | cut -c1-160)" || { tail -20 gpurun_out/r47_xl_$v.log; exit 1; }
 done
+TRACE_BY_GRID="ln_,skinny,gru" TLIM=600 bash scripts/prof.sh r47_xl 6 --xl --prefill 100 || exit 1

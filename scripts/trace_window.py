@@ -46,6 +46,28 @@ def main(path, steps, top=40):
     print("| ms/step | calls/step | avg us | % busy | kernel |\n|---:|---:|---:|---:|---|")
     for name, (d, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:top]:
         print(f"| {d / 1e6 / steps:.3f} | {c / steps:.1f} | {d / c / 1e3:.1f} | {100 * d / busy:.1f} | `{_short(name)}` |")
+    import os
+
+    for pat in filter(None, os.environ.get("TRACE_BY_GRID", "").split(",")):
+        by_grid(win, steps, pat)
+
+
+def by_grid(win, steps, pat):
+    """Per (kernel, grid size) breakdown of the kernels whose name contains ``pat`` (TRACE_BY_GRID=pat)."""
+    import collections
+
+    gkey = next((k for k in ("Grid_Size", "Grid_Size_X", "grid_size") if k in win[0]), None)
+    if gkey is None:
+        return
+    agg = collections.defaultdict(lambda: [0, 0])
+    for r in win:
+        if pat in r["Kernel_Name"]:
+            a = agg[(r["Kernel_Name"], r[gkey], r.get("Workgroup_Size", r.get("Workgroup_Size_X", "")))]
+            a[0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            a[1] += 1
+    print(f"\n| ms/step | calls/step | avg us | grid | wg | kernel (by grid: {pat}) |\n|---:|---:|---:|---:|---:|---|")
+    for (name, g, w), (d, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:40]:
+        print(f"| {d / 1e6 / steps:.3f} | {c / steps:.1f} | {d / c / 1e3:.1f} | {g} | {w} | `{_short(name)}` |")
 
 
 def _short(name: str) -> str:
