@@ -410,3 +410,29 @@ def test_built_extension_links():
     m = importlib.import_module("sheeprl_prey_amd.ops._C")
     for name in ("prior_head", "actor_tail", "conv_up_small", "set_up_last_form", "flat_grad_norm"):
         assert hasattr(m, name), name
+
+
+def test_sidestream_scope_is_inert_on_cpu_and_outside_scopes():
+    """ops/sidestream.py: on CPU tensors and outside a scope ``on_side`` runs the block in line and nothing is left to
+    join; the scope counter nests and unwinds on exceptions."""
+    import torch
+
+    from sheeprl_prey_amd.ops import sidestream as ss
+
+    x = torch.ones(3)
+    with ss.on_side(x.device, x):
+        y = x * 2
+    assert torch.equal(y, torch.full((3,), 2.0)) and not ss._pending
+    ss.join()
+    assert not ss.active(torch.device("cpu"))
+    with ss.scope():
+        with ss.scope():
+            assert ss._depth == 2
+            assert not ss.active(torch.device("cpu"))  # CPU: never a side stream
+        try:
+            with ss.scope():
+                raise RuntimeError("boom")
+        except RuntimeError:
+            pass
+        assert ss._depth == 1
+    assert ss._depth == 0
