@@ -244,8 +244,10 @@ class ContinuousRollout:
                               None, None, None, None, M, hid, 1, t_act)
             dh.addmm_(dtr, self.tr1.weight)
             # h_t = LN-GRU(gx[s], h_s)
+            # the direct path into h_s (+ the trajectory gradient of h_s, added by the kernel)
             C.ln_gru_bwd_into(self.gx[s], buf[s, :, S:S + Hd], buf.stride(1), gln.weight, gln.bias, self.g_mean[s],
-                              self.g_rstd[s], dh, dgx, dh_prev, pdg, pdb, None, None, M, Hd)
+                              self.g_rstd[s], dh, dgx, dh_prev, pdg, pdb, None, None, M, Hd,
+                              dadd=d_traj[s, :, S:] if (d_traj is not None and s > 0) else None)
             dcat = torch.mm(dgx, Wg)  # [M, Hd + D]: (h | x)
             # x_s = act(LN([prior_s | a_s] Wr^T)) (no bias)
             C.ln_act_bwd_into(self.rec_z[s], D, dcat[:, Hd:], Hd + D, dz, D, rln.weight, rln.bias, self.rec_mean[s],
@@ -254,10 +256,10 @@ class ContinuousRollout:
             if s == 0:
                 break  # (prior_0, h_0) are the detached posteriors
             dp = torch.mm(dz, Wr[:, :S])
-            dh = dh_prev + dcat[:, :Hd]
             if d_traj is not None:
                 dp += d_traj[s, :, :S]
-                dh += d_traj[s, :, S:]
+            # dh_s = (direct + d_traj) + the h half of d(h | x); the consumed dh buffer becomes the next dh_prev
+            dh, dh_prev = dh_prev.add_(dcat[:, :Hd]), dh
         # one batched actor backward over all (H+1) M rows
         R = (H + 1) * M
         dpre = C.tn_head_sample_bwd(self.loc.view(R, A), self.scale.view(R, A), self.u_act.view(R, A), d_a.view(R, A),

@@ -35,7 +35,8 @@ bool launch_ln_gru_fwd(const float*, const float*, int, const float*, const floa
                        hipStream_t, int ldo = 0, const float* x2 = nullptr, int ldx2 = 0);
 int ln_gru_bwd_grid(int);
 bool launch_ln_gru_bwd(const float*, const float*, int, const float*, const float*, const float*, const float*, const float*,
-                       float*, float*, float*, float*, float*, float*, int, int, hipStream_t);
+                       float*, float*, float*, float*, float*, float*, int, int, hipStream_t, const float* dadd = nullptr,
+                       int ldadd = 0);
 bool launch_unimix_sample_fwd(const float*, const float*, float*, float*, int, int, float, hipStream_t, int G = 0,
                               int lds = 0, int* idx = nullptr, int ldi = 0, int ioff = 0);
 bool launch_unimix_sample_bwd(const float*, const float*, const float*, float*, int, int, float, hipStream_t);
@@ -469,9 +470,19 @@ void ln_gru_fwd_into(torch::Tensor x, torch::Tensor h, int64_t ldh, torch::Tenso
 void ln_gru_bwd_into(torch::Tensor x, torch::Tensor h, int64_t ldh, torch::Tensor gamma, torch::Tensor beta,
                      torch::Tensor mean, torch::Tensor rstd, torch::Tensor dhn, torch::Tensor dx, torch::Tensor dh,
                      torch::Tensor pdg, torch::Tensor pdb, c10::optional<torch::Tensor> dgamma,
-                     c10::optional<torch::Tensor> dbeta, int64_t M, int64_t H) {
+                     c10::optional<torch::Tensor> dbeta, int64_t M, int64_t H, c10::optional<torch::Tensor> dadd) {
+  // dadd (optional, [M, H] row-strided): added to the dh output (a second gradient into h_{t-1})
+  const float* ap = nullptr;
+  int ldadd = 0;
+  if (dadd.has_value() && dadd->defined()) {
+    TORCH_CHECK(dadd->is_cuda() && dadd->scalar_type() == torch::kFloat32 && dadd->dim() == 2 && dadd->size(0) == M &&
+                    dadd->size(1) == H && dadd->stride(1) == 1,
+                "ln_gru_bwd_into: dadd must be a row-strided [M, H] float32 view");
+    ap = dadd->data_ptr<float>();
+    ldadd = (int)dadd->stride(0);
+  }
   bool ok = launch_ln_gru_bwd(fp(x), fp(h), ldh, fp(gamma), fp(beta), fp(mean), fp(rstd), fp(dhn), mp(dx), mp(dh), mp(pdg),
-                              mp(pdb), omp(dgamma), omp(dbeta), M, H, cur_stream());
+                              mp(pdb), omp(dgamma), omp(dbeta), M, H, cur_stream(), ap, ldadd);
   TORCH_CHECK(ok, "ln_gru_bwd_into: unsupported H ", H);
 }
 
@@ -1151,7 +1162,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd_grid", &ln_bwd_grid_py);
   m.def("ln_gru_bwd_grid", &ln_gru_bwd_grid_py);
   m.def("ln_gru_fwd_into", &ln_gru_fwd_into);
-  m.def("ln_gru_bwd_into", &ln_gru_bwd_into);
+  m.def("ln_gru_bwd_into", &ln_gru_bwd_into, pybind11::arg("x"), pybind11::arg("h"), pybind11::arg("ldh"), pybind11::arg("gamma"),
+        pybind11::arg("beta"), pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("dhn"), pybind11::arg("dx"),
+        pybind11::arg("dh"), pybind11::arg("pdg"), pybind11::arg("pdb"), pybind11::arg("dgamma"), pybind11::arg("dbeta"),
+        pybind11::arg("M"), pybind11::arg("H"), pybind11::arg("dadd") = pybind11::none());
   m.def("colsum2", &colsum2);
   m.def("rssm_mask_fwd", &rssm_mask_fwd);
   m.def("rssm_mask_bwd", &rssm_mask_bwd);

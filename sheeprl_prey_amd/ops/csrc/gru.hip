@@ -132,7 +132,8 @@ __global__ void __launch_bounds__(64 * NW) ln_gru_bwd4_kernel(const float* __res
                                                               const float* __restrict__ mean, const float* __restrict__ rstd,
                                                               const float* __restrict__ dhn, float* __restrict__ dx,
                                                               float* __restrict__ dh, float* __restrict__ pdg,
-                                                              float* __restrict__ pdb, int M, int H) {
+                                                              float* __restrict__ pdb, int M, int H,
+                                                              const float* __restrict__ dadd, int ldadd) {
   __shared__ float red[NW];
   const int N = 3 * H, H4 = H >> 2, j4 = threadIdx.x;
   const float4* g4 = reinterpret_cast<const float4*>(gamma);
@@ -170,6 +171,10 @@ __global__ void __launch_bounds__(64 * NW) ln_gru_bwd4_kernel(const float* __res
   }
     SRL_GRU_BWD_LANE(x) SRL_GRU_BWD_LANE(y) SRL_GRU_BWD_LANE(z) SRL_GRU_BWD_LANE(w)
 #undef SRL_GRU_BWD_LANE
+    if (dadd) {  // an extra gradient into h_{t-1} (row-strided), added here instead of by a separate kernel
+      const float4 e = reinterpret_cast<const float4*>(dadd + (int64_t)row * ldadd)[j4];
+      dho.x += e.x, dho.y += e.y, dho.z += e.z, dho.w += e.w;
+    }
     reinterpret_cast<float4*>(dh + (int64_t)row * H)[j4] = dho;
     const float m1 = block_sum<NW>(s1, red) / N;
     const float m2 = block_sum<NW>(s2, red) / N;
@@ -196,7 +201,8 @@ __global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict
                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
                                                          const float* __restrict__ dhn, float* __restrict__ dx,
                                                          float* __restrict__ dh, float* __restrict__ pdg,
-                                                         float* __restrict__ pdb, int M, int H) {
+                                                         float* __restrict__ pdb, int M, int H,
+                                                         const float* __restrict__ dadd, int ldadd) {
   __shared__ float red[4];
   const int T = 256, N = 3 * H;
   float ag[3][MAXH], ab[3][MAXH];
@@ -223,7 +229,7 @@ __global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict
         float u = sigmoidf_(zu - 1.f);
         float hp = h[(int64_t)row * ldh + j];
         float g_out = dhn[(int64_t)row * H + j];
-        dh[(int64_t)row * H + j] = g_out * (1.f - u);
+        dh[(int64_t)row * H + j] = g_out * (1.f - u) + (dadd ? dadd[(int64_t)row * ldadd + j] : 0.f);
         float du = g_out * (c - hp);
         float dc = g_out * u;
         float dzu = du * u * (1.f - u);
@@ -319,27 +325,27 @@ void launch_colsum2(const float* pa, const float* pb, float* oa, float* ob, int 
 // pdg/pdb: [grid, 3H] partial rows; reduced into dgamma/dbeta when those are non-null.
 bool launch_ln_gru_bwd(const float* x, const float* h, int ldh, const float* gamma, const float* beta, const float* mean,
                        const float* rstd, const float* dhn, float* dx, float* dh, float* pdg, float* pdb, float* dgamma,
-                       float* dbeta, int M, int H, hipStream_t st) {
+                       float* dbeta, int M, int H, hipStream_t st, const float* dadd, int ldadd) {
   int mh = gru_maxh(H);
   int grid = ln_gru_bwd_grid(M);
   dim3 g(grid), b(256);
   const bool al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(h) | reinterpret_cast<uintptr_t>(dhn) |
                     reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(dh) | reinterpret_cast<uintptr_t>(pdg) |
                     reinterpret_cast<uintptr_t>(pdb) | reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta)) &
-                   15) == 0 && ldh % 4 == 0;
+                   15) == 0 && ldh % 4 == 0 && (!dadd || ((reinterpret_cast<uintptr_t>(dadd) & 15) == 0 && ldadd % 4 == 0));
   if (g_gru_vec && al && H % 1024 == 0 && H <= 4096 && (H / 1024 == 1 || H / 1024 == 2 || H / 1024 == 4)) {
     const dim3 bw(H / 4);
-    if (H == 1024) hipLaunchKernelGGL(ln_gru_bwd4_kernel<4>, g, bw, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H);
-    else if (H == 2048) hipLaunchKernelGGL(ln_gru_bwd4_kernel<8>, g, bw, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H);
-    else hipLaunchKernelGGL(ln_gru_bwd4_kernel<16>, g, bw, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H);
+    if (H == 1024) hipLaunchKernelGGL(ln_gru_bwd4_kernel<4>, g, bw, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H, dadd, ldadd);
+    else if (H == 2048) hipLaunchKernelGGL(ln_gru_bwd4_kernel<8>, g, bw, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H, dadd, ldadd);
+    else hipLaunchKernelGGL(ln_gru_bwd4_kernel<16>, g, bw, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H, dadd, ldadd);
     if (dgamma) launch_colsum2(pdg, pdb, dgamma, dbeta, grid, 3 * H, 1, st);
     return true;
   }
   switch (mh) {
-    case 2: hipLaunchKernelGGL(ln_gru_bwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
-    case 4: hipLaunchKernelGGL(ln_gru_bwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
-    case 8: hipLaunchKernelGGL(ln_gru_bwd_kernel<8>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
-    case 16: hipLaunchKernelGGL(ln_gru_bwd_kernel<16>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H); break;
+    case 2: hipLaunchKernelGGL(ln_gru_bwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H, dadd, ldadd); break;
+    case 4: hipLaunchKernelGGL(ln_gru_bwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H, dadd, ldadd); break;
+    case 8: hipLaunchKernelGGL(ln_gru_bwd_kernel<8>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H, dadd, ldadd); break;
+    case 16: hipLaunchKernelGGL(ln_gru_bwd_kernel<16>, g, b, 0, st, x, h, ldh, gamma, beta, mean, rstd, dhn, dx, dh, pdg, pdb, M, H, dadd, ldadd); break;
     default: return false;
   }
   if (dgamma) launch_colsum2(pdg, pdb, dgamma, dbeta, grid, 3 * H, 1, st);
