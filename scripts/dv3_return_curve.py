@@ -28,8 +28,13 @@ def run(name, over):
     root = os.path.abspath(f"gpurun_out/dv3curve_{name}")
     t0 = time.perf_counter()
     log = open(f"gpurun_out/dv3curve_{name}.log", "w")
-    subprocess.run([sys.executable, "-u", "sheeprl.py"] + BASE + over + [f"root_dir={root}", f"run_name={name}"],
-                   check=True, stdout=log, stderr=subprocess.STDOUT)
+    rc = subprocess.run([sys.executable, "-u", "sheeprl.py"] + BASE + over + [f"root_dir={root}", f"run_name={name}"],
+                        stdout=log, stderr=subprocess.STDOUT).returncode
+    if rc != 0:
+        subprocess.run(["rm", "-rf", root])  # the replay memmaps: too large to copy back
+        log.close()
+        print("".join(open(f"gpurun_out/dv3curve_{name}.log").readlines()[-40:]))
+        raise SystemExit(f"{name} run failed with exit code {rc}")
     wall = time.perf_counter() - t0
     f = sorted(glob.glob(f"{root}/{name}/version_*/metrics.jsonl"))[-1]
     rows = [json.loads(line) for line in open(f)]
