@@ -338,3 +338,46 @@ def test_persistent_scan_timeout_is_loud():
     assert R.check_scan_health() == 0
     assert not torch.equal(tr.world_optimizer.flat_param, p0)  # healthy again: the update is applied
     assert ops.skipped_updates() == 0
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_dv3_vector_obs_train_step(graphs):
+    """Vector observations only (no CNN encoder / decoder: the CartPole-style config), fused ops, with and without
+    the captured step: finite losses that decrease on a fixed batch."""
+    from sheeprl_prey_amd.algos.dreamer_v3.agent import build_models
+    from sheeprl_prey_amd.algos.dreamer_v3.dreamer_v3 import DreamerV3Trainer
+    from sheeprl_prey_amd.algos.dreamer_v3.utils import Moments
+    from sheeprl_prey_amd.config.compose import compose
+    from sheeprl_prey_amd.envs import spaces
+    from sheeprl_prey_amd.parallel.flat_optim import build_optimizer
+    from sheeprl_prey_amd.parallel.runner import Runner
+    from sheeprl_prey_amd.utils.utils import dotdict
+
+    cfg = dotdict(compose([
+        "exp=dreamer_v3", "env=dummy", "cnn_keys.encoder=[]", "cnn_keys.decoder=[]", "mlp_keys.encoder=[state]",
+        "mlp_keys.decoder=[state]", "algo.dense_units=64", "algo.mlp_layers=2",
+        "algo.world_model.recurrent_model.recurrent_state_size=64", "algo.world_model.representation_model.hidden_size=64",
+        "algo.world_model.transition_model.hidden_size=64", "algo.horizon=5", "fabric.accelerator=cuda",
+        f"fabric.cuda_graphs={graphs}",
+    ]))
+    torch.manual_seed(0)
+    runner = Runner(**dict(cfg.fabric))
+    obs_space = spaces.Dict({"state": spaces.Box(-10, 10, (4,), "float32")})
+    wm, actor, critic, target = build_models(runner, [2], False, cfg, obs_space)
+    opts = [build_optimizer(c, m.parameters()) for c, m in
+            ((cfg.algo.world_model.optimizer, wm), (cfg.algo.actor.optimizer, actor), (cfg.algo.critic.optimizer, critic))]
+    tr = DreamerV3Trainer(runner, cfg, wm, actor, critic, target, *opts, Moments(None).cuda(), False, [2])
+    g = torch.Generator(device="cuda").manual_seed(1)
+    T, B = 16, 4
+    data = {
+        "state": torch.randn(T, B, 4, device="cuda", generator=g),
+        "actions": torch.nn.functional.one_hot(torch.randint(0, 2, (T, B), device="cuda", generator=g), 2).float(),
+        "rewards": torch.randn(T, B, 1, device="cuda", generator=g),
+        "dones": (torch.rand(T, B, 1, device="cuda", generator=g) < 0.1).float(),
+        "is_first": (torch.rand(T, B, 1, device="cuda", generator=g) < 0.1).float(),
+    }
+    losses = [float(tr.train_step(data)["Loss/world_model_loss"]) for _ in range(8)]
+    assert all(l == l and abs(l) < 1e6 for l in losses), losses
+    assert losses[-1] < losses[0], losses
+    if graphs:
+        assert tr.graphed.graph is not None
