@@ -14,7 +14,7 @@ rc=$?
 echo "curve dbg rc=$rc"; tail -40 gpurun_out/r4_curve_dbg.log | cut -c1-400
 rm -rf /tmp/dv3dbg
 case $rc in 124|134|137|139) exit 1 ;; esac  # a hang / abort / crash: nothing more on the GPU in this call
-timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py tests/test_imagine_cont_gpu.py tests/test_dreamer_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "ln_gru or cont or imagine" > gpurun_out/r47_tests.log 2>&1 \
+timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py tests/test_imagine_cont_gpu.py tests/test_dreamer_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "ln_gru or cont or imagine or vector" > gpurun_out/r47_tests.log 2>&1 \
   && tail -1 gpurun_out/r47_tests.log || { tail -20 gpurun_out/r47_tests.log; exit 1; }
 timeout -k 10 120 python scripts/gru_timing.py > gpurun_out/r47_gru_timing.log 2>&1 && tail -1 gpurun_out/r47_gru_timing.log || exit 1
 for v in 1 0; do

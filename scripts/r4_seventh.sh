@@ -3,7 +3,7 @@
 set -u
 export TMPDIR=/tmp PYTHONPATH=.
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py tests/test_imagine_cont_gpu.py tests/test_dreamer_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "ln_gru or cont or imagine" > gpurun_out/r47_tests.log 2>&1 \
+timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py tests/test_imagine_cont_gpu.py tests/test_dreamer_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "ln_gru or cont or imagine or vector" > gpurun_out/r47_tests.log 2>&1 \
   && tail -1 gpurun_out/r47_tests.log || { tail -20 gpurun_out/r47_tests.log; exit 1; }
 timeout -k 10 120 python scripts/gru_timing.py > gpurun_out/r47_gru_timing.log 2>&1 && tail -1 gpurun_out/r47_gru_timing.log || exit 1
 for v in 1 0; do
