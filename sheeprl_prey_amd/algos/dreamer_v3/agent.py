@@ -735,6 +735,10 @@ class PlayerDV3(nn.Module):
             actions = torch.zeros(1, self.num_envs, int(np.sum(self.actions_dim)), device=self.device)
             h = torch.tanh(torch.zeros(1, self.num_envs, self.recurrent_state_size, device=self.device))
             z = self.rssm._transition(h, sample_state=False)[1].reshape(1, self.num_envs, -1)
+            if self._graphed is not None and self.actions.shape[1] != self.num_envs:
+                # a new env count (e.g. the single-env test episode after training on N envs): the captured
+                # graphs were recorded for the old buffer shapes - drop them, the next call re-captures
+                self._graphed = None
             if self._graphed is not None:  # keep the captured buffers' addresses
                 self.actions.copy_(actions)
                 self.recurrent_state.copy_(h)
