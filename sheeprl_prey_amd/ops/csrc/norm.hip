@@ -28,23 +28,32 @@ __global__ void __launch_bounds__(256) ln_wave_fwd_kernel(const float* __restric
   const int g = gw % G;
   const float* gam = gamma ? gamma + (int64_t)g * N : nullptr;
   const float* bet = beta ? beta + (int64_t)g * N : nullptr;
+  // every load is unconditional (indices clamped into the row, out-of-row lanes masked after the load): a load
+  // under a lane branch made the wait-count pass drain vmcnt per element, one memory round trip each
+  float gv[MAXV], bv[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int idx = min(lane + 64 * k, N - 1);
+    gv[k] = gam ? gam[idx] : 1.f;
+    bv[k] = gam ? bet[idx] : 0.f;
+  }
   for (int b = gw / G; b < Bn; b += nwaves / G) {
     const int r = b * G + g;
     const float* xr = x + (int64_t)r * ldx;
     float v[MAXV];
     float s = 0.f;
 #pragma unroll
+    for (int k = 0; k < MAXV; ++k) v[k] = xr[min(lane + 64 * k, N - 1)];
+#pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      int idx = lane + 64 * k;
-      v[k] = idx < N ? xr[idx] : 0.f;
+      if (lane + 64 * k >= N) v[k] = 0.f;
       s += v[k];
     }
     const float mu = wave_sum_dpp(s) / N;
     float q = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      int idx = lane + 64 * k;
-      float d = idx < N ? v[k] - mu : 0.f;
+      const float d = lane + 64 * k < N ? v[k] - mu : 0.f;
       q += d * d;
     }
     const float rs = rsqrtf(wave_sum_dpp(q) / N + eps);
@@ -53,11 +62,7 @@ __global__ void __launch_bounds__(256) ln_wave_fwd_kernel(const float* __restric
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
       int idx = lane + 64 * k;
-      if (idx < N) {
-        float z = (v[k] - mu) * rs;
-        if (gam) z = z * gam[idx] + bet[idx];
-        yr[idx] = act_fwd(z, act);
-      }
+      if (idx < N) yr[idx] = act_fwd((v[k] - mu) * rs * gv[k] + bv[k], act);
     }
     if (lane == 0) {
       mean_out[r] = mu;
@@ -144,30 +149,40 @@ __global__ void __launch_bounds__(256) ln_wave_bwd_kernel(const float* __restric
   float ag[MAXV], ab[MAXV];
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) ag[k] = ab[k] = 0.f;
+  float gv[MAXV], bv[MAXV];  // this wave's group parameters, loaded once (clamped, unconditional)
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int idx = min(lane + 64 * k, N - 1);
+    gv[k] = gam ? gam[idx] : 1.f;
+    bv[k] = gam ? bet[idx] : 0.f;
+  }
   for (int b = gw / G; b < Bn; b += nwaves / G) {
     const int r = b * G + g;
     const int ro = (G == 1) ? r : g * Bn + b;
     const float* xr = x + (int64_t)r * ldx;
     const float* dyr = dy + (int64_t)ro * lddy;
     const float mu = mean[r], rs = rstd[r];
+    // all of the row's loads first, unconditionally (see the forward)
     float xh[MAXV], dxh[MAXV];
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+      const int idx = min(lane + 64 * k, N - 1);
+      xh[k] = xr[idx];
+      dxh[k] = dyr[idx];
+    }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
-      int idx = lane + 64 * k;
-      xh[k] = dxh[k] = 0.f;
-      if (idx < N) {
-        float h = (xr[idx] - mu) * rs;
-        float gg = gam ? gam[idx] : 1.f;
-        float z = gam ? h * gg + bet[idx] : h;
-        float dz = dyr[idx] * act_grad(z, act);
-        ag[k] += dz * h;
-        ab[k] += dz;
-        xh[k] = h;
-        dxh[k] = dz * gg;
-        s1 += dxh[k];
-        s2 += dxh[k] * h;
-      }
+      const bool ok = lane + 64 * k < N;
+      const float h = (xh[k] - mu) * rs;
+      const float z = gam ? h * gv[k] + bv[k] : h;
+      const float dz = ok ? dxh[k] * act_grad(z, act) : 0.f;
+      ag[k] += dz * h;
+      ab[k] += dz;
+      xh[k] = ok ? h : 0.f;
+      dxh[k] = dz * gv[k];
+      s1 += dxh[k];
+      s2 += dxh[k] * xh[k];
     }
     const float m1 = wave_sum_dpp(s1) / N;
     const float m2 = wave_sum_dpp(s2) / N;

@@ -260,16 +260,16 @@ def test_player_graphed_steps_and_resets():
     player.init_states([1])
     torch.testing.assert_close(player.recurrent_state[:, 1], h0[:, 1])
     torch.testing.assert_close(player.stochastic_state[:, 1], z0[:, 1])
+    assert torch.all(player.actions[:, 1] == 0)
+    player.init_states()
+    assert player.recurrent_state.data_ptr() == buf_ptr
+    torch.testing.assert_close(player.recurrent_state, h0)
     # the single-env test episode after training on 3 envs (utils.test): new state shapes, captures dropped
     player.num_envs = 1
     player.init_states()
     assert player._graphed is None and player.recurrent_state.shape[1] == 1
     a = player.get_greedy_action({"rgb": torch.rand(1, 1, 3, 64, 64, device="cuda")}, False)[0]
     assert a.shape == (1, 1, 5) and torch.all(a.sum(-1) == 1)
-    assert torch.all(player.actions[:, 1] == 0)
-    player.init_states()
-    assert player.recurrent_state.data_ptr() == buf_ptr
-    torch.testing.assert_close(player.recurrent_state, h0)
 
 
 @pytest.mark.parametrize("graphs", [False, True])
