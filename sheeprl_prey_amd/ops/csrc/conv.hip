@@ -1092,17 +1092,91 @@ static void wgrad_tile(int Ca, int Cbp, int* BM, int* BN) {
   *BN = (16 * Cbp) % 128 == 0 ? 128 : 64;
 }
 
-// number of K splits (and pixels per split) for a WGRAD problem; slab = S * Ca * 16 * Cbp floats
+// resident workgroups per CU of a WGRAD tile config (occupancy query, cached) and the CU count
+static int wgrad_occ(int BM, int BN) {
+  static int cache[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+  const int i = BM == 128 ? 0 : (BM == 64 ? 1 : 2), j = BN == 128 ? 0 : 1;
+  if (cache[i][j] == 0) {
+    const void* fn = nullptr;
+    int nth = 256;
+    if (BN == 128) {
+      if (BM == 128) fn = reinterpret_cast<const void*>(wgrad_kernel<128, 128, 2, 2>);
+      else if (BM == 64) fn = reinterpret_cast<const void*>(wgrad_kernel<64, 128, 1, 4>);
+      else fn = reinterpret_cast<const void*>(wgrad_kernel<32, 128, 1, 4>);
+    } else {
+      nth = BM == 128 ? 256 : 128;
+      if (BM == 128) fn = reinterpret_cast<const void*>(wgrad_kernel<128, 64, 2, 2>);
+      else if (BM == 64) fn = reinterpret_cast<const void*>(wgrad_kernel<64, 64, 1, 2>);
+      else fn = reinterpret_cast<const void*>(wgrad_kernel<32, 64, 1, 2>);
+    }
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, nth, 0) != hipSuccess || n < 1) n = 2;
+    cache[i][j] = n;
+  }
+  return cache[i][j];
+}
+
+static int num_cus() {
+  static int n = [] {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v < 1) v = 256;
+    return v;
+  }();
+  return n;
+}
+
+// SRL_WGRAD_PLAN=0: the previous split rule (~512 workgroups whatever the residency)
+static const bool g_wgrad_rounds = [] {
+  const char* e = getenv("SRL_WGRAD_PLAN");
+  return !(e && e[0] == '0');
+}();
+
+// number of K splits (and pixels per split) for a WGRAD problem; slab = S * Ca * 16 * Cbp floats.
+// Rounds-aware: with T output tiles and R resident slots (occupancy x CUs) a launch of T * S workgroups runs
+// ceil(T * S / R) rounds of M / S pixels each, so its time goes as ceil(T S / R) / S: a grid just over a
+// multiple of R (the XL layers: 540 / 576 workgroups on 512 slots) pays a nearly empty extra round.  S is
+// picked by a small time model (rounds x tile time + partial-slab traffic), with at least 1024 pixels per split.
 void conv_wgrad_plan(int N, int SH, int SW, int Ca, int Cbp, int* S, int* kper) {
   const int M = N * SH * SW;
   int BM, BN;
   wgrad_tile(Ca, Cbp, &BM, &BN);
   const int tiles = (Ca / BM) * (16 * Cbp / BN);
-  // ~512 workgroups (2 per CU); 1024 for a single-tile problem (E1 / D4: 2K outputs, 1M pixels)
-  int want = tiles == 1 ? 1024 : (512 + tiles - 1) / tiles;
+  // previous rule: ~512 workgroups (2 per CU); 1024 for a single-tile problem (E1 / D4: 2K outputs, 1M pixels)
+  const int want = tiles == 1 ? 1024 : (512 + tiles - 1) / tiles;
   int kp = (M + want - 1) / want;
   kp = ((kp + 31) / 32) * 32;
   if (kp < 1024) kp = 1024;
+  if (g_wgrad_rounds) {
+    const int occ = wgrad_occ(BM, BN);
+    const int R = occ * num_cus();
+    const int smax = std::max(1, M / 1024);
+    // estimated microseconds: rounds x one workgroup's tile at 1/occ of a CU's fp32 MFMA rate (~0.61 TF/s)
+    // + the partial slab written and re-read at ~5 TB/s
+    const double wg_rate = 0.61e6 / occ;                    // FLOP per microsecond per resident workgroup
+    const double slab_us = 2.0 * Ca * 16.0 * Cbp * 4 / 5e6;  // per split
+    double best = 1e30;
+    int bs = 1;
+    for (int s = 1; s <= smax; ++s) {
+      int k = (M + s - 1) / s;
+      k = ((k + 31) / 32) * 32;
+      const int se = (M + k - 1) / k;  // effective splits after rounding
+      const long total = (long)tiles * se;
+      const double rounds = (double)((total + R - 1) / R);
+      const double cost = rounds * (2.0 * k * BM * BN / wg_rate) + se * slab_us;
+      if (cost < best - 1e-9) {
+        best = cost;
+        bs = se;
+      }
+    }
+    // keep the previous split unless the model predicts a clear (> 10 %) gain
+    const int so = (M + kp - 1) / kp;
+    const double old_cost = (double)(((long)tiles * so + R - 1) / R) * (2.0 * kp * BM * BN / wg_rate) + so * slab_us;
+    if (best < 0.9 * old_cost) {
+      kp = (M + bs - 1) / bs;
+      kp = ((kp + 31) / 32) * 32;
+    }
+  }
   *kper = kp;
   *S = (M + kp - 1) / kp;
 }
