@@ -5,7 +5,7 @@ set -u
 export TMPDIR=/tmp PYTHONPATH=.
 mkdir -p gpurun_out
 bash scripts/r4_sites.sh || exit 1
-for i in 1 2; do
+for i in 1; do
   timeout -k 10 300 python bench.py --algo sac --steps 400 --warmup 50 > gpurun_out/r4_sac_fused_$i.log 2>&1 && echo "sac fused $(tail -1 gpurun_out/r4_sac_fused_$i.log | cut -c1-200)" || exit 1
   SRL_SAC_FUSED=0 timeout -k 10 300 python bench.py --algo sac --steps 400 --warmup 50 > gpurun_out/r4_sac_eager_$i.log 2>&1 && echo "sac eager $(tail -1 gpurun_out/r4_sac_eager_$i.log | cut -c1-200)" || exit 1
 done
