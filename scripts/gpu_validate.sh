@@ -1,5 +1,5 @@
 #!/bin/bash
-# End-of-session validation: the whole GPU suite (as the driver runs it), smoke(), the default bench twice.
+# End-of-session GPU validation (the driver's round-end checks): the whole GPU suite (as the driver runs it), smoke(), the default bench twice.
 set -u
 export TMPDIR=/tmp PYTHONPATH=.
 mkdir -p gpurun_out
