@@ -55,7 +55,8 @@ def test_up_plain_matches_conv_transpose(cin, cout, hw, n):
 
 @pytest.mark.parametrize("cin,cout,hw,n", [(4, 32, 64, 3), (32, 64, 32, 2), (64, 128, 16, 3), (128, 256, 8, 4),
                                             (4, 96, 64, 2), (96, 192, 32, 2), (192, 384, 16, 2), (384, 768, 8, 2),
-                                            (512, 1024, 8, 2), (4, 64, 128, 1), (768, 96, 8, 2), (1024, 64, 8, 2)])
+                                            (512, 1024, 8, 2), (4, 64, 128, 1), (768, 96, 8, 2), (1024, 64, 8, 2),
+                                            (96, 192, 32, 24), (192, 384, 16, 40), (384, 768, 8, 96)])
 def test_wgrad_matches_autograd(cin, cout, hw, n):
     C = ops._ext()
     torch.manual_seed(0)
