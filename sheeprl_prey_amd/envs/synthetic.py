@@ -57,42 +57,66 @@ class SyntheticAtari(Env):
         self._moves = np.array([(dx, dy) for dy in (-1, 0, 1) for dx in (-1, 0, 1)], dtype=np.int64)
 
     def _render_frame(self) -> np.ndarray:
+        # the background (RGB or its grayscale) is cached; sprites are drawn straight into the output format with
+        # their precomputed values (grayscale = the luma formula applied to the RGB sprite, as a per-pixel
+        # conversion of the RGB frame would give)
         s = self.size
-        img = np.repeat(self._bg[..., None], 3, axis=-1)
-        for i, (p, col) in enumerate(zip(self._pos, self._colors)):
-            x, y = int(p[0]), int(p[1])
+        img = self._bg_out.copy()
+        for i, ((x, y), col) in enumerate(zip(self._pos, self._col_out)):
+            x, y = int(x), int(y)
             r = 3 if i == 0 else 2
             img[max(y - r, 0) : min(y + r, s), max(x - r, 0) : min(x + r, s)] = col
-        if self.grayscale:
-            g = (img[..., 0] * 0.299 + img[..., 1] * 0.587 + img[..., 2] * 0.114).astype(np.uint8)
-            return g[..., None]
         return img
 
     def reset(self, *, seed: Optional[int] = None, options=None):
         if seed is not None:
             self._rng = np.random.default_rng(seed)
         self._t = 0
-        self._pos = self._rng.uniform(4, self.size - 4, size=(self.n_sprites, 2))
-        self._vel = self._rng.uniform(-1.5, 1.5, size=(self.n_sprites, 2))
-        self._colors = self._rng.integers(60, 255, size=(self.n_sprites, 3)).astype(np.uint8)
+        # sprite state as Python floats: a handful of scalars per step, where numpy's per-call overhead dominated
+        self._pos = self._rng.uniform(4, self.size - 4, size=(self.n_sprites, 2)).tolist()
+        self._vel = self._rng.uniform(-1.5, 1.5, size=(self.n_sprites, 2)).tolist()
+        colors = self._rng.integers(60, 255, size=(self.n_sprites, 3)).astype(np.uint8)
+        if self.grayscale:
+            bg = self._bg.astype(np.float64)
+            self._bg_out = (bg * 0.299 + bg * 0.587 + bg * 0.114).astype(np.uint8)[..., None]
+            self._col_out = [np.uint8(int(float(c[0]) * 0.299 + float(c[1]) * 0.587 + float(c[2]) * 0.114)) for c in colors]
+        else:
+            self._bg_out = np.repeat(self._bg[..., None], 3, axis=-1)
+            self._col_out = [c for c in colors]
         self._frame = self._render_frame()
         return self._frame.copy(), {}
 
     def step(self, action):
         a = int(np.asarray(action).reshape(-1)[0]) % self.n_actions
         reward = 0.0
+        lo, hi = 3.0, float(self.size - 4)
+        pos, vel = self._pos, self._vel
+        dx, dy = (int(v) for v in self._moves[a % len(self._moves)])
         for _ in range(self.frame_skip):
-            mv = self._moves[a % len(self._moves)]
-            self._pos[0] = np.clip(self._pos[0] + 2 * mv, 3, self.size - 4)
-            self._pos[1:] += self._vel[1:]
-            bounce = (self._pos[1:] < 3) | (self._pos[1:] > self.size - 4)
-            self._vel[1:][bounce] *= -1
-            self._pos[1:] = np.clip(self._pos[1:], 3, self.size - 4)
-            d = np.abs(self._pos[1:] - self._pos[0]).max(axis=1)
-            hit = d < 4
-            if hit.any():
-                reward += float(hit.sum())
-                self._pos[1:][hit] = self._rng.uniform(4, self.size - 4, size=(int(hit.sum()), 2))
+            p0 = pos[0]
+            x0, y0 = p0[0] + 2 * dx, p0[1] + 2 * dy
+            x0 = lo if x0 < lo else (hi if x0 > hi else x0)
+            y0 = lo if y0 < lo else (hi if y0 > hi else y0)
+            p0[0], p0[1] = x0, y0
+            hits = []
+            for i in range(1, self.n_sprites):
+                p, v = pos[i], vel[i]
+                x, y = p[0] + v[0], p[1] + v[1]
+                if x < lo or x > hi:  # bounce, then clip into the field
+                    v[0] = -v[0]
+                    x = lo if x < lo else hi
+                if y < lo or y > hi:
+                    v[1] = -v[1]
+                    y = lo if y < lo else hi
+                p[0], p[1] = x, y
+                ax, ay = x - x0, y - y0
+                if (ax if ax >= 0 else -ax) < 4 and (ay if ay >= 0 else -ay) < 4:
+                    hits.append(i)
+            if hits:
+                reward += float(len(hits))
+                new = self._rng.uniform(4, self.size - 4, size=(len(hits), 2)).tolist()
+                for i, q in zip(hits, new):
+                    pos[i] = q
         self._t += 1
         self._frame = self._render_frame()
         terminated = False
