@@ -182,8 +182,10 @@ class SyntheticControl(Env):
         """A 'stick figure' of the state: 8 segments whose endpoints follow pairs of state coordinates,
         drawn over a tiled floor (64x64x3 uint8 by default)."""
         s = self.size
-        yy, xx = np.mgrid[0:s, 0:s]
-        img = np.repeat((((xx // 8 + yy // 8) % 2) * 30 + 40).astype(np.uint8)[..., None], 3, axis=-1)
+        if getattr(self, "_floor", None) is None:  # the tiled floor is the same every frame
+            yy, xx = np.mgrid[0:s, 0:s]
+            self._floor = np.repeat((((xx // 8 + yy // 8) % 2) * 30 + 40).astype(np.uint8)[..., None], 3, axis=-1)
+        img = self._floor.copy()
         pts = np.clip((np.tanh(self._x[:16].reshape(8, 2)) * 0.45 + 0.5) * (s - 1), 0, s - 1).astype(np.int64)
         for i, (x, y) in enumerate(pts):
             img[max(y - 2, 0):y + 2, max(x - 2, 0):x + 2] = (200, 60 + 20 * i, 255 - 25 * i)
