@@ -667,15 +667,28 @@ __global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep,
 // WGRAD: rows a (Ca), cols (tap,b) (16 Cb), K = pixel range of split blockIdx.z; writes the partial slab.
 template <int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(64 * WM* WN) void wgrad_kernel(WgP<BM, 64 * WM * WN> la, WgQ<BN, 64 * WM * WN> lb,
-                                                              float* slab, int ldn, int Mrows, int kper) {
+                                                              float* slab, int ldn, int Mrows, int kper, int remap) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   __shared__ float lds[(BM + BN) * LDK];
   float* As = lds;
   float* Bs = lds + BM * LDK;
-  const int r0 = blockIdx.x * BM, c0 = blockIdx.y * BN;
+  // XCD-aware order (remap, grid size a multiple of 8): workgroups are dealt round-robin over the 8 XCDs, so
+  // XCD x runs linear ids x, x + 8, ...; give it a contiguous run of (split, tile) pairs instead, i.e. whole
+  // K splits, so every output tile of a split reads that split's P / Q pixels from the same L2
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (remap) {
+    const int gxy = gridDim.x * gridDim.y;
+    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int L = (b & 7) * ((gxy * (int)gridDim.z) >> 3) + (b >> 3);
+    bz = L / gxy;
+    const int t = L - bz * gxy;
+    by = t / gridDim.x;
+    bx = t - by * gridDim.x;
+  }
+  const int r0 = bx * BM, c0 = by * BN;
   la.init(r0);
   lb.init(c0);
-  const int kb = blockIdx.z * kper, ke = kb + kper;
+  const int kb = bz * kper, ke = kb + kper;
   Frag<TM, TN, WN> f;
   f.lane = threadIdx.x & 63;
   f.wm = (threadIdx.x >> 6) / WN;
@@ -715,7 +728,7 @@ __global__ __launch_bounds__(64 * WM* WN) void wgrad_kernel(WgP<BM, 64 * WM * WN
           for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
     }
   }
-  float* out = slab + (size_t)blockIdx.z * Mrows * ldn;
+  float* out = slab + (size_t)bz * Mrows * ldn;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1066,6 +1079,12 @@ bool launch_conv_up(const float* P, const float* Wp, int N, int SH, int SW, int 
   SRL_CONV_TILES(up_cfg, P, Wp, N, SH, SW, Ca, Bp, e, st)
 }
 
+// SRL_WGRAD_REMAP=0: hardware workgroup order (A/B)
+static const bool g_wgrad_remap = [] {
+  const char* e = getenv("SRL_WGRAD_REMAP");
+  return !(e && e[0] == '0');
+}();
+
 template <int BM, int BN, int WM, int WN>
 static void wgrad_cfg(const float* P, const float* Q, float* slab, int S, int kper, int N, int SH, int SW, int Ca, int Cbp,
                       hipStream_t st) {
@@ -1082,7 +1101,8 @@ static void wgrad_cfg(const float* P, const float* Q, float* slab, int S, int kp
   lb.lSW = ilog2(SW);
   lb.M = M;
   dim3 grid(Ca / BM, 16 * Cbp / BN, S);
-  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN>), grid, dim3(NTH), 0, st, la, lb, slab, 16 * Cbp, Ca, kper);
+  const int remap = g_wgrad_remap && (grid.x * grid.y * grid.z) % 8 == 0;
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN>), grid, dim3(NTH), 0, st, la, lb, slab, 16 * Cbp, Ca, kper, remap);
 }
 
 // WGRAD tile: rows = Ca (the largest of 128 / 64 / 32 dividing it), columns = 16 * Cbp (128, or 64 for
