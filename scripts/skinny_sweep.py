@@ -6,7 +6,8 @@ import torch
 
 from sheeprl_prey_amd import ops
 
-shapes = [(16, 12288, 5120, "Wg fwd"), (16, 5120, 12288, "Wg bwd"), (16, 2048, 4096, "W1 fwd"), (16, 4096, 2048, "W1 bwd")]
+shapes = [(16, 12288, 5120, "Wg fwd"), (16, 5120, 12288, "Wg bwd"), (16, 2048, 4096, "W1 fwd"), (16, 4096, 2048, "W1 bwd"),
+          (16, 1024, 1024, "Wz")]
 res = []
 for M, N, K, name in shapes:
     A = torch.randn(M, K, device="cuda")
@@ -26,4 +27,5 @@ for M, N, K, name in shapes:
         us = e0.elapsed_time(e1) / 50 * 1e3
         row.append(f"{impl} {us:6.1f} us ({N * K * 4 / us / 1e6:5.2f} TB/s)")
     res.append("  ".join(row))
-print(f"WGS={os.environ.get('SRL_SKINNY_WGS', 'default')} NT={os.environ.get('SRL_SKINNY_NT', '0')}: " + " | ".join(res), flush=True)
+print(f"WGS={os.environ.get('SRL_SKINNY_WGS', 'default')} FUSED={os.environ.get('SRL_SKINNY_FUSED', '1')}:\n  " +
+      "\n  ".join(res), flush=True)

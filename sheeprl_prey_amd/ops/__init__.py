@@ -719,8 +719,29 @@ def skinny_nt(A: Tensor, W: Tensor, out: Tensor, add: Optional[Tensor] = None) -
     Z = A.shape[0] if A.dim() == 3 else 1
     need = C.skinny_workspace(W.shape[-2], A.shape[-1], Z)
     part = torch.empty(need, device=A.device, dtype=torch.float32) if need else None
-    C.skinny_nt(A, W, out, add, part)
+    C.skinny_nt(A, W, out, add, part, _skinny_tickets(A.device, Z * (W.shape[-2] // 128)) if need else None)
     return True
+
+
+# Ticket counters of skinny_nt's in-launch split combine: one zeroed int32 pool per device, created on first use
+# (the first calls run eagerly, before any step is captured), handed out in rotating slices so that launches close
+# together never share a counter; each launch's last-arriving workgroup returns its counters to zero.
+_SKINNY_POOL = 1 << 16
+_skinny_pool: dict = {}
+
+
+def _skinny_tickets(device, n: int) -> Optional[Tensor]:
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    pool = _skinny_pool.get(key)
+    if pool is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None  # never allocate the pool inside a capture (graph-private memory): separate reduce launch
+        pool = _skinny_pool[key] = [torch.zeros(_SKINNY_POOL, device=device, dtype=torch.int32), 0]
+    if pool[1] + n > _SKINNY_POOL:
+        pool[1] = 0
+    sl = pool[0][pool[1]:pool[1] + n]
+    pool[1] += (n + 63) // 64 * 64  # slices start on separate 256-byte lines
+    return sl
 
 
 # =============================================================== P2E disagreement (K20)

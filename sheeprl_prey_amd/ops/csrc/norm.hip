@@ -71,26 +71,35 @@ __global__ void __launch_bounds__(256) ln_wave_fwd_kernel(const float* __restric
   }
 }
 
-// Same op, 16-byte form for aligned rows (N % 4 == 0, row strides % 4, 16-B aligned pointers, one
-// group): each lane holds NV4 float4 of the row, and gamma/beta are loaded together with x - before
-// the two reductions - so the row costs one memory round trip instead of two.  (The imagination
-// rollout runs ~60 of these per step at M = 1024, N = 512, where the kernel is latency-bound.)
+// Same op, 16-byte form for aligned rows (N % 4 == 0, row strides % 4, 16-B aligned pointers, G dividing
+// 4): each lane holds NV4 float4 of the row, and gamma/beta are loaded together with x - before the two
+// reductions - so the row costs one memory round trip instead of two.  (The imagination rollout runs ~60 of
+// these per step at M = 1024, N = 512, where the kernel is latency-bound; the XL scan's two-group prior /
+// posterior LayerNorm, 32 x 1024, ran 9.1 us per step on the scalar form.)  Groups as in ln_wave_fwd_kernel:
+// wave gw serves group gw % G, input row b G + g, output row g (M / G) + b when G > 1.
 template <int NV4>
 __global__ void __launch_bounds__(256) ln_wave4_fwd_kernel(const float* __restrict__ x, int ldx, float* __restrict__ y,
                                                            int ldy, const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float* __restrict__ mean_out,
-                                                           float* __restrict__ rstd_out, int M, int N, float eps, int act) {
+                                                           float* __restrict__ rstd_out, int M, int N, float eps, int act,
+                                                           int G) {
   const int lane = threadIdx.x & 63;
   const int nwaves = gridDim.x * 4;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int g = gw % G, Bn = M / G;
   const int N4 = N >> 2;
+  const float4* gam4 = gamma ? reinterpret_cast<const float4*>(gamma + (int64_t)g * N) : nullptr;
+  const float4* bet4 = beta ? reinterpret_cast<const float4*>(beta + (int64_t)g * N) : nullptr;
   float4 gv[NV4], bv[NV4];
 #pragma unroll
   for (int k = 0; k < NV4; ++k) {
     const int i4 = lane + 64 * k;
-    gv[k] = (gamma && i4 < N4) ? reinterpret_cast<const float4*>(gamma)[i4] : make_float4(1.f, 1.f, 1.f, 1.f);
-    bv[k] = (beta && i4 < N4) ? reinterpret_cast<const float4*>(beta)[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[k] = (gam4 && i4 < N4) ? gam4[i4] : make_float4(1.f, 1.f, 1.f, 1.f);
+    bv[k] = (bet4 && i4 < N4) ? bet4[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < M; r += nwaves) {
+  for (int b = gw / G; b < Bn; b += nwaves / G) {
+    const int r = b * G + g;
+    const int ro = G == 1 ? r : g * Bn + b;
     const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)r * ldx);
     float4 v[NV4];
     float s = 0.f;
@@ -110,7 +119,7 @@ __global__ void __launch_bounds__(256) ln_wave4_fwd_kernel(const float* __restri
       }
     }
     const float rs = rsqrtf(wave_sum_dpp(q) / N + eps);
-    float4* yr = reinterpret_cast<float4*>(y + (int64_t)r * ldy);
+    float4* yr = reinterpret_cast<float4*>(y + (int64_t)ro * ldy);
 #pragma unroll
     for (int k = 0; k < NV4; ++k) {
       const int i4 = lane + 64 * k;
@@ -226,11 +235,11 @@ __global__ void __launch_bounds__(256) ln_wave4_bwd_kernel(const float* __restri
                                                            const float* __restrict__ gamma, const float* __restrict__ beta,
                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
                                                            float* __restrict__ pdg, float* __restrict__ pdb, int M, int N,
-                                                           int act, float* __restrict__ za, float* __restrict__ zb) {
-  // za / zb (or null): the dgamma / dbeta targets the column-sum kernel after this one accumulates into
-  // atomically - zeroed here by block 0 instead of by a separate zero kernel (one launch less per call)
+                                                           int act, float* __restrict__ za, float* __restrict__ zb, int G) {
+  // za / zb (or null): the dgamma / dbeta targets ([G, N]) the column-sum kernel after this one accumulates
+  // into atomically - zeroed here by block 0 instead of by a separate zero kernel (one launch less per call)
   if (za != nullptr && blockIdx.x == 0)
-    for (int i = threadIdx.x; i < N; i += 256) {
+    for (int i = threadIdx.x; i < G * N; i += 256) {
       za[i] = 0.f;
       zb[i] = 0.f;
     }
@@ -238,22 +247,29 @@ __global__ void __launch_bounds__(256) ln_wave4_bwd_kernel(const float* __restri
   __shared__ float4 red_b[4][64 * NV4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nwaves = gridDim.x * 4;
+  // groups as in the forward: wave gw serves group gw % G (= w % G: G divides 4), x / dx row b G + g, dy row
+  // g (M / G) + b when G > 1; the block's partial row of group g' sums its waves w with w % G == g'
+  const int gw = blockIdx.x * 4 + w;
+  const int g = gw % G, Bn = M / G, bstep = nwaves / G;
   const int N4 = N >> 2;
   const float inv_n = 1.f / (float)N;
+  const float4* gam4 = gamma ? reinterpret_cast<const float4*>(gamma + (int64_t)g * N) : nullptr;
+  const float4* bet4 = beta ? reinterpret_cast<const float4*>(beta + (int64_t)g * N) : nullptr;
   float4 gv[NV4], bv[NV4], ag[NV4], ab[NV4];
 #pragma unroll
   for (int k = 0; k < NV4; ++k) {
     const int i4 = lane + 64 * k;
-    gv[k] = (gamma && i4 < N4) ? reinterpret_cast<const float4*>(gamma)[i4] : make_float4(1.f, 1.f, 1.f, 1.f);
-    bv[k] = (beta && i4 < N4) ? reinterpret_cast<const float4*>(beta)[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[k] = (gam4 && i4 < N4) ? gam4[i4] : make_float4(1.f, 1.f, 1.f, 1.f);
+    bv[k] = (bet4 && i4 < N4) ? bet4[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
     ag[k] = ab[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  int r = blockIdx.x * 4 + w;
+  int b = gw / G;
   float4 xv[NV4], dv[NV4];
   float mu = 0.f, rs = 0.f;
-  auto load = [&](int row, float4 (&xa)[NV4], float4 (&da)[NV4], float& m_, float& r_) {
+  auto load = [&](int bb, float4 (&xa)[NV4], float4 (&da)[NV4], float& m_, float& r_) {
+    const int row = bb * G + g;
     const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)row * ldx);
-    const float4* dr = reinterpret_cast<const float4*>(dy + (int64_t)row * lddy);
+    const float4* dr = reinterpret_cast<const float4*>(dy + (int64_t)(G == 1 ? row : g * Bn + bb) * lddy);
 #pragma unroll
     for (int k = 0; k < NV4; ++k) {
       const int i4 = lane + 64 * k;
@@ -263,12 +279,13 @@ __global__ void __launch_bounds__(256) ln_wave4_bwd_kernel(const float* __restri
     m_ = mean[row];
     r_ = rstd[row];
   };
-  if (r < M) load(r, xv, dv, mu, rs);
-  while (r < M) {
-    const int rn = r + nwaves;
+  if (b < Bn) load(b, xv, dv, mu, rs);
+  while (b < Bn) {
+    const int r = b * G + g;
+    const int bn = b + bstep;
     float4 xn[NV4], dn[NV4];
     float mun = 0.f, rsn = 0.f;
-    if (rn < M) load(rn, xn, dn, mun, rsn);
+    if (bn < Bn) load(bn, xn, dn, mun, rsn);
     float4 h[NV4], g[NV4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -308,7 +325,7 @@ __global__ void __launch_bounds__(256) ln_wave4_bwd_kernel(const float* __restri
         dxr[i4] = o;
       }
     }
-    r = rn;
+    b = bn;
 #pragma unroll
     for (int k = 0; k < NV4; ++k) {
       xv[k] = xn[k];
@@ -324,17 +341,17 @@ __global__ void __launch_bounds__(256) ln_wave4_bwd_kernel(const float* __restri
       red_b[w][lane + 64 * k] = ab[k];
     }
     __syncthreads();
-    for (int i4 = threadIdx.x; i4 < N4; i4 += 256) {
-      float4 a = red_g[0][i4], b = red_b[0][i4];
-#pragma unroll
-      for (int ww = 1; ww < 4; ++ww) {
-        const float4 c = red_g[ww][i4], d = red_b[ww][i4];
-        a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
-        b.x += d.x; b.y += d.y; b.z += d.z; b.w += d.w;
+    for (int gg = 0; gg < G; ++gg)
+      for (int i4 = threadIdx.x; i4 < N4; i4 += 256) {
+        float4 a = red_g[gg][i4], c2 = red_b[gg][i4];
+        for (int ww = gg + G; ww < 4; ww += G) {
+          const float4 c = red_g[ww][i4], d = red_b[ww][i4];
+          a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
+          c2.x += d.x; c2.y += d.y; c2.z += d.z; c2.w += d.w;
+        }
+        reinterpret_cast<float4*>(pdg + ((int64_t)blockIdx.x * G + gg) * N)[i4] = a;
+        reinterpret_cast<float4*>(pdb + ((int64_t)blockIdx.x * G + gg) * N)[i4] = c2;
       }
-      reinterpret_cast<float4*>(pdg + (int64_t)blockIdx.x * N)[i4] = a;
-      reinterpret_cast<float4*>(pdb + (int64_t)blockIdx.x * N)[i4] = b;
-    }
   }
 }
 
@@ -664,6 +681,12 @@ int ln_bwd_grid(int M, int N, int G) {
   return M < 512 ? M : 512;
 }
 
+// SRL_LN_VEC_GROUPS=0: grouped (G > 1) rows on the scalar wave kernels (A/B)
+static const bool g_ln_vec_groups = [] {
+  const char* e = getenv("SRL_LN_VEC_GROUPS");
+  return !(e && e[0] == '0');
+}();
+
 bool launch_ln_act_fwd(const float* x, int ldx, float* y, int ldy, const float* gamma, const float* beta, float* mean,
                        float* rstd, int M, int N, int G, float eps, int act, hipStream_t st) {
   int mode, maxv;
@@ -672,8 +695,9 @@ bool launch_ln_act_fwd(const float* x, int ldx, float* y, int ldy, const float* 
     int grid = cdiv(M, 4);
     if (grid > 4096) grid = 4096;
     const bool al16 = ((uintptr_t)x | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) % 16 == 0;
-    if (G == 1 && N % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && al16 && (gamma != nullptr) == (beta != nullptr)) {
-#define F4(NV) if (maxv == 4 * NV) { hipLaunchKernelGGL(ln_wave4_fwd_kernel<NV>, dim3(grid), dim3(256), 0, st, x, ldx, y, ldy, gamma, beta, mean, rstd, M, N, eps, act); return true; }
+    if ((G == 1 || (g_ln_vec_groups && (G == 2 || G == 4) && M % G == 0)) && N % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 &&
+        al16 && (gamma != nullptr) == (beta != nullptr)) {
+#define F4(NV) if (maxv == 4 * NV) { hipLaunchKernelGGL(ln_wave4_fwd_kernel<NV>, dim3(grid), dim3(256), 0, st, x, ldx, y, ldy, gamma, beta, mean, rstd, M, N, eps, act, G); return true; }
       F4(1) F4(2) F4(4) F4(8)
 #undef F4
     }
@@ -744,11 +768,11 @@ bool launch_ln_act_bwd(const float* x, int ldx, const float* dy, int lddy, float
   float* pb = gamma ? pdb : nullptr;
   if (mode == 0) {
     const bool al16 = ((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)gamma | (uintptr_t)beta) % 16 == 0;
-    if (G == 1 && N % 4 == 0 && ldx % 4 == 0 && lddy % 4 == 0 && lddx % 4 == 0 && al16 &&
-        (gamma != nullptr) == (beta != nullptr) && maxv <= 16) {
+    if ((G == 1 || (g_ln_vec_groups && (G == 2 || G == 4) && M % G == 0)) && N % 4 == 0 && ldx % 4 == 0 &&
+        lddy % 4 == 0 && lddx % 4 == 0 && al16 && (gamma != nullptr) == (beta != nullptr) && maxv <= 16) {
       float* za = (gamma && dgamma) ? dgamma : nullptr;
       float* zb = (gamma && dgamma) ? dbeta : nullptr;
-#define F4(NV) if (maxv == 4 * NV) { SRL_ACT_SPECIALIZE(act, hipLaunchKernelGGL((ln_wave4_bwd_kernel<NV, ACTC>), dim3(grid), dim3(256), 0, st, x, ldx, dy, lddy, dx, lddx, gamma, beta, mean, rstd, pg, pb, M, N, act, za, zb)); goto reduce_zeroed; }
+#define F4(NV) if (maxv == 4 * NV) { SRL_ACT_SPECIALIZE(act, hipLaunchKernelGGL((ln_wave4_bwd_kernel<NV, ACTC>), dim3(grid), dim3(256), 0, st, x, ldx, dy, lddy, dx, lddx, gamma, beta, mean, rstd, pg, pb, M, N, act, za, zb, G)); goto reduce_zeroed; }
       F4(1) F4(2) F4(4)
 #undef F4
     }

@@ -277,3 +277,37 @@ def test_ln_gru_wide_rows_vec_vs_scalar(H, split):
         _close(buf[:, 4:4 + H], ref_y, rtol=1e-4, atol=1e-5)
         _close(mean, x.mean(-1), rtol=1e-4, atol=1e-5)
     _close(outs[0], outs[1], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("G,N,Bn", [(2, 1024, 16), (2, 512, 37), (4, 256, 9), (2, 1000, 16)])
+def test_ln_grouped_rows(G, N, Bn):
+    """Grouped LayerNorm + SiLU of the XL scan's prior / posterior hidden layers (``ln_act_*_into`` with G parameter
+    sets): input row b G + g, output / dy row g Bn + b.  N % 4 == 0 runs the 16-byte wave kernels, N = 1000 the
+    scalar ones; both against the fp64 torch reference, including the partial-row dgamma / dbeta reduction."""
+    C = ops._ext()
+    act = ops._act_code("silu")
+    torch.manual_seed(0)
+    M = G * Bn
+    x = torch.randn(Bn, G * N, device=DEV) * 2 + 0.5
+    w = torch.randn(G, N, device=DEV)
+    b = torch.randn(G, N, device=DEV)
+    y = torch.empty(G, Bn, N, device=DEV)
+    mean = torch.empty(M, device=DEV)
+    rstd = torch.empty(M, device=DEV)
+    C.ln_act_fwd_into(x, N, y, N, w, b, mean, rstd, M, N, G, 1e-3, act)
+    xd = x.double().view(Bn, G, N).transpose(0, 1).requires_grad_(True)  # [G, Bn, N]
+    wd, bd = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    yr = torch.nn.functional.silu(torch.nn.functional.layer_norm(xd, (N,), eps=1e-3) * wd[:, None] + bd[:, None])
+    torch.testing.assert_close(y.double(), yr.detach(), rtol=1e-4, atol=1e-4)
+    dy = torch.randn(G, Bn, N, device=DEV)
+    (yr * dy.double()).sum().backward()
+    dx = torch.empty(Bn, G * N, device=DEV)
+    grid = C.ln_bwd_grid(M, N, G)
+    pdg = torch.empty(grid * G, N, device=DEV)
+    pdb = torch.empty_like(pdg)
+    dw = torch.full((G, N), float("nan"), device=DEV)  # the kernels must zero / overwrite these
+    db = torch.full((G, N), float("nan"), device=DEV)
+    C.ln_act_bwd_into(x, N, dy, N, dx, N, w, b, mean, rstd, pdg, pdb, dw, db, M, N, G, act)
+    torch.testing.assert_close(dx.double().view(Bn, G, N).transpose(0, 1), xd.grad, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(dw.double(), wd.grad, rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(db.double(), bd.grad, rtol=1e-3, atol=1e-3)
