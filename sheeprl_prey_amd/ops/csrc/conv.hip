@@ -978,8 +978,9 @@ static int narrow_tiles() {
   return v;
 }
 
-// Double-buffered main loop for the narrow layers; SRL_CONV_DB bit 0: 128x32 tiles (32 channels), bit 1: 128x64
-// (64 channels) (A/B knob, read once; default off until measured)
+// Double-buffered main loop (one barrier per K stage); SRL_CONV_DB bit 0: 128x32 tiles (32 channels), bit 1: 128x64
+// (64), bit 2: 128x96, bit 3: 128x128, bit 4: 128x192, bit 5: 64x256, bit 6: 64x384 (A/B knob, read once; default
+// off: profiles/r4_conv_ab.md for the narrow tiles)
 static int conv_db() {
   static const int v = [] {
     const char* e = getenv("SRL_CONV_DB");
@@ -1009,11 +1010,26 @@ static int conv_db() {
       else if (narrow_tiles() & 1) X<128, 64, 2, 2>(__VA_ARGS__);                                   \
       else X<256, 64, 4, 1>(__VA_ARGS__);                                                           \
       return true;                                                                                  \
-    case 96: X<128, 96, 4, 1>(__VA_ARGS__); return true;                                            \
-    case 128: X<128, 128, 2, 2>(__VA_ARGS__); return true;                                          \
-    case 192: X<128, 192, 2, 2>(__VA_ARGS__); return true;                                          \
-    case 256: X<64, 256, 1, 4>(__VA_ARGS__); return true;                                           \
-    case 384: X<64, 384, 1, 4>(__VA_ARGS__); return true;                                           \
+    case 96:                                                                                        \
+      if (conv_db() & 4) X<128, 96, 4, 1, true>(__VA_ARGS__);                                       \
+      else X<128, 96, 4, 1>(__VA_ARGS__);                                                           \
+      return true;                                                                                  \
+    case 128:                                                                                       \
+      if (conv_db() & 8) X<128, 128, 2, 2, true>(__VA_ARGS__);                                      \
+      else X<128, 128, 2, 2>(__VA_ARGS__);                                                          \
+      return true;                                                                                  \
+    case 192:                                                                                       \
+      if (conv_db() & 16) X<128, 192, 2, 2, true>(__VA_ARGS__);                                     \
+      else X<128, 192, 2, 2>(__VA_ARGS__);                                                          \
+      return true;                                                                                  \
+    case 256:                                                                                       \
+      if (conv_db() & 32) X<64, 256, 1, 4, true>(__VA_ARGS__);                                      \
+      else X<64, 256, 1, 4>(__VA_ARGS__);                                                           \
+      return true;                                                                                  \
+    case 384:                                                                                       \
+      if (conv_db() & 64) X<64, 384, 1, 4, true>(__VA_ARGS__);                                      \
+      else X<64, 384, 1, 4>(__VA_ARGS__);                                                           \
+      return true;                                                                                  \
     case 512: X<64, 512, 1, 8>(__VA_ARGS__); return true;                                           \
     case 768: X<64, 768, 1, 8>(__VA_ARGS__); return true;                                           \
     case 1024: X<32, 1024, 1, 8>(__VA_ARGS__); return true;                                         \
