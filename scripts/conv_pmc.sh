@@ -1,10 +1,11 @@
 #!/bin/bash
-# PMC pass over the fused conv stack (scripts/conv_bench.py, fused layout only).
+# PMC pass over the fused conv stack (scripts/conv_bench.py, fused layout only), or over any python command:
+#   TAG=natcnn PMC_CMD="bench.py --algo ppo --pixel --steps 2 --warmup 1" bash scripts/conv_pmc.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 mkdir -p gpurun_out/pmc
-CONV_LAYOUTS=fused timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES --output-format csv -d gpurun_out/pmc -o ${TAG:-conv} -- python3 scripts/conv_bench.py > gpurun_out/pmc/${TAG:-conv}.log 2>&1 || exit $?
+CONV_LAYOUTS=fused timeout -s KILL ${PMC_TLIM:-120} rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES --output-format csv -d gpurun_out/pmc -o ${TAG:-conv} -- python3 ${PMC_CMD:-scripts/conv_bench.py} > gpurun_out/pmc/${TAG:-conv}.log 2>&1 || exit $?
 f=$(find gpurun_out/pmc -name '*counter_collection.csv' | head -1)
 python3 - "$f" <<'PY' > gpurun_out/pmc/${TAG:-conv}_summary.md
 import csv, sys, collections
