@@ -4,7 +4,12 @@ Atari env (``envs/synthetic.py``: the action moves sprite 0 on a 3x3 stencil, ev
 reward of 1 and respawns), 250-step episodes.  On this env a random policy scores 13.8 +- 4.4 per episode and a
 hand-written "chase the nearest sprite" policy 89.1 +- 9.8 (20 episodes each, computed by this script on the host).
 
-usage: python scripts/dv3_atari_curve.py <out.md> [total_policy_steps]"""
+With ``--walker``: the continuous path instead (``exp=dreamer_v3_dmc_walker_walk`` on the walker_walk-shaped
+synthetic control env: 64x64 renders + 24-dim state, 6-dim TruncatedNormal actions, 1000-step episodes, the
+imagination back-propagating through the dynamics in ``imagine_cont.py``); host baselines: uniform random actions,
+zero actions, and the one-step greedy action sign(B^T w) of the env's own linear system.
+
+usage: python scripts/dv3_atari_curve.py <out.md> [total_policy_steps] [--walker]"""
 import glob
 import json
 import os
@@ -16,8 +21,10 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-OUT = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/dv3_atari_curve.md"
-TOTAL = int(sys.argv[2]) if len(sys.argv) > 2 else 30000
+WALKER = "--walker" in sys.argv
+_pos = [a for a in sys.argv[1:] if not a.startswith("--")]
+OUT = _pos[0] if len(_pos) > 0 else "gpurun_out/dv3_atari_curve.md"
+TOTAL = int(_pos[1]) if len(_pos) > 1 else 30000
 EP_LEN = 250
 
 
@@ -48,14 +55,52 @@ def baselines(eps: int = 20):
     return run(lambda env, rng: int(rng.integers(9))), run(chase)
 
 
+def walker_baselines(eps: int = 5):
+    from sheeprl_prey_amd.envs.synthetic import SyntheticControl
+
+    def run(policy):
+        tot = []
+        for s in range(eps):
+            env = SyntheticControl(seed=s)
+            env.reset(seed=s)
+            rng = np.random.default_rng(s)
+            r_ep, done = 0.0, False
+            while not done:
+                _, r, term, trunc, _ = env.step(policy(env, rng))
+                r_ep += r
+                done = term or trunc
+            tot.append(r_ep)
+        return float(np.mean(tot)), float(np.std(tot))
+
+    return (run(lambda env, rng: rng.uniform(-1, 1, env.act_dim)), run(lambda env, rng: np.zeros(env.act_dim)),
+            run(lambda env, rng: np.sign(env._B.T @ env._w)))
+
+
 def main():
     os.makedirs("gpurun_out", exist_ok=True)
-    (rm, rs), (cm, cs) = baselines()
-    root = os.path.abspath("gpurun_out/dv3atari_run")
-    args = ["exp=dreamer_v3_100k_ms_pacman", "env=synthetic_atari", "fabric=mi355x", "fabric.devices=1",
-            f"total_steps={TOTAL}", "algo.learning_starts=1024", "metric.log_every=1000", "checkpoint.every=100000000",
-            "env.sync_env=True", "env.capture_video=False", "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]",
-            f"env.wrapper.episode_length={EP_LEN}", "seed=7", f"root_dir={root}", "run_name=atari"]
+    if WALKER:
+        (rm, rs), (zm, zs), (cm, cs) = walker_baselines()
+        root = os.path.abspath("gpurun_out/dv3walker_run")
+        args = ["exp=dreamer_v3_dmc_walker_walk", "env=gym", "env.id=walker_walk_synthetic", "fabric=mi355x",
+                "fabric.devices=1", f"total_steps={TOTAL}", "algo.learning_starts=1024", "metric.log_every=2000",
+                "checkpoint.every=100000000", "env.sync_env=True", "env.capture_video=False", "cnn_keys.encoder=[rgb]",
+                "cnn_keys.decoder=[rgb]", "mlp_keys.encoder=[state]", "mlp_keys.decoder=[state]", "buffer.memmap=False",
+                "seed=7", f"root_dir={root}", "run_name=atari"]
+        title = (f"# DreamerV3 continuous (pixels + state): walker_walk-shaped synthetic env, 1000-step episodes "
+                 f"(GPU fast path, CLI; {TOTAL} policy steps)\n")
+        base = (f"Episode return baselines on this env (5 episodes, host): uniform random actions {rm:.1f} +- {rs:.1f}; zero "
+                f"actions {zm:.1f} +- {zs:.1f}; one-step greedy sign(B^T w) {cm:.1f} +- {cs:.1f}.\n")
+    else:
+        (rm, rs), (cm, cs) = baselines()
+        root = os.path.abspath("gpurun_out/dv3atari_run")
+        args = ["exp=dreamer_v3_100k_ms_pacman", "env=synthetic_atari", "fabric=mi355x", "fabric.devices=1",
+                f"total_steps={TOTAL}", "algo.learning_starts=1024", "metric.log_every=1000", "checkpoint.every=100000000",
+                "env.sync_env=True", "env.capture_video=False", "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]",
+                f"env.wrapper.episode_length={EP_LEN}", "seed=7", f"root_dir={root}", "run_name=atari"]
+        title = (f"# DreamerV3 from pixels: synthetic Atari, {EP_LEN}-step episodes (GPU fast path, CLI; {TOTAL} policy "
+                 f"steps)\n")
+        base = (f"Episode return baselines on this env (20 episodes, host): random policy {rm:.1f} +- {rs:.1f}; "
+                f"chase-the-nearest-sprite heuristic {cm:.1f} +- {cs:.1f}.\n")
     t0 = time.perf_counter()
     with open("gpurun_out/dv3atari.log", "w") as log:
         rc = subprocess.run([sys.executable, "-u", "sheeprl.py"] + args, stdout=log, stderr=subprocess.STDOUT).returncode
@@ -70,9 +115,7 @@ def main():
     loss = [(r["step"], r.get("Loss/world_model_loss"), r.get("Loss/policy_loss"), r.get("Loss/observation_loss"))
             for r in rows if "Loss/world_model_loss" in r]
     sps = [(r["step"], r.get("Time/sps_train")) for r in rows if "Time/sps_train" in r]
-    lines = [f"# DreamerV3 from pixels: synthetic Atari, {EP_LEN}-step episodes (GPU fast path, CLI; {TOTAL} policy steps)\n",
-             f"Episode return baselines on this env (20 episodes, host): random policy {rm:.1f} +- {rs:.1f}; "
-             f"chase-the-nearest-sprite heuristic {cm:.1f} +- {cs:.1f}.\n",
+    lines = [title, base,
              f"Run: `python sheeprl.py {' '.join(a for a in args if not a.startswith('root_dir'))}`; "
              f"{wall:.1f} s wall-clock incl. start-up and capture.\n",
              "| policy step | Rewards/rew_avg |", "|---:|---:|"]
@@ -83,7 +126,7 @@ def main():
     lines += [f"| {s} | {v} |" for s, v in sps]
     open(OUT, "w").write("\n".join(lines) + "\n")
     print("\n".join(lines[:6 + len(curve)]))
-    print(json.dumps({"random": rm, "chase": cm, "best_rew_avg": max((r for _, r in curve), default=None),
+    print(json.dumps({"random": rm, "heuristic": cm, "best_rew_avg": max((r for _, r in curve), default=None),
                       "final_rew_avg": curve[-1][1] if curve else None, "wall_s": round(wall, 1)}))
 
 
