@@ -9,7 +9,11 @@ synthetic control env: 64x64 renders + 24-dim state, 6-dim TruncatedNormal actio
 imagination back-propagating through the dynamics in ``imagine_cont.py``); host baselines: uniform random actions,
 zero actions, and the one-step greedy action sign(B^T w) of the env's own linear system.
 
-usage: python scripts/dv3_atari_curve.py <out.md> [total_policy_steps] [--walker]"""
+With ``--prey``: the fork's own preset (``exp=dreamer_v3_prey``) on the predator-prey cellworld ``prey_d_1``
+(``envs/prey``: vector observation, Discrete(100) speed x turning actions, -distance per step, +100 at the goal,
+-50 on capture); host baseline: a uniform random policy (100 episodes).
+
+usage: python scripts/dv3_atari_curve.py <out.md> [total_policy_steps] [--walker | --prey]"""
 import glob
 import json
 import os
@@ -22,6 +26,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 WALKER = "--walker" in sys.argv
+PREY = "--prey" in sys.argv
 _pos = [a for a in sys.argv[1:] if not a.startswith("--")]
 OUT = _pos[0] if len(_pos) > 0 else "gpurun_out/dv3_atari_curve.md"
 TOTAL = int(_pos[1]) if len(_pos) > 1 else 30000
@@ -76,9 +81,39 @@ def walker_baselines(eps: int = 5):
             run(lambda env, rng: np.sign(env._B.T @ env._w)))
 
 
+def prey_baseline(eps: int = 100):
+    from sheeprl_prey_amd.envs.registry import make
+
+    env = make("prey_d_1")
+    rng = np.random.default_rng(0)
+    tot, goals = [], 0
+    for ep in range(eps):
+        env.reset(seed=ep)
+        r_ep, n = 0.0, 0
+        while True:
+            _, r, term, trunc, _ = env.step(int(rng.integers(env.action_space.n)))
+            r_ep += r
+            n += 1
+            if term or trunc or n >= 300:
+                goals += int(term)
+                break
+        tot.append(r_ep)
+    return float(np.mean(tot)), float(np.std(tot)), goals / eps
+
+
 def main():
     os.makedirs("gpurun_out", exist_ok=True)
-    if WALKER:
+    if PREY:
+        rm, rs, gr = prey_baseline()
+        cm = None
+        root = os.path.abspath("gpurun_out/dv3prey_run")
+        args = ["exp=dreamer_v3_prey", "fabric=mi355x", "fabric.devices=1", f"total_steps={TOTAL}", "metric.log_every=5000",
+                "checkpoint.every=100000000", "env.sync_env=True", "env.capture_video=False", "seed=7",
+                f"root_dir={root}", "run_name=atari"]
+        title = f"# DreamerV3 on the predator-prey cellworld prey_d_1 (exp=dreamer_v3_prey, GPU, CLI; {TOTAL} policy steps)\n"
+        base = (f"Baseline (100 episodes, host): uniform random policy {rm:.1f} +- {rs:.1f} per episode, goal reached in "
+                f"{100 * gr:.0f} % of episodes (captured or timed out otherwise).\n")
+    elif WALKER:
         (rm, rs), (zm, zs), (cm, cs) = walker_baselines()
         root = os.path.abspath("gpurun_out/dv3walker_run")
         args = ["exp=dreamer_v3_dmc_walker_walk", "env=gym", "env.id=walker_walk_synthetic", "fabric=mi355x",

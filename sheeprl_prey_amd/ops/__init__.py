@@ -326,7 +326,7 @@ def unimix_sample(
     (teacher forcing of the eager oracle, see ``DreamerV3Trainer.teacher``) - always the eager form."""
     if forced is not None:
         return ref.unimix_sample(logits, classes, unimix, sample=sample, forced=forced)
-    if _native(logits) and logits.dtype == torch.float32 and classes <= 64:
+    if _native(logits) and logits.dtype == torch.float32 and classes <= 1024:
         if sample and uniform is None:
             uniform = torch.rand(logits.numel() // classes, device=logits.device)
         return _UnimixSample.apply(logits, uniform, int(classes), float(unimix), bool(sample))

@@ -845,7 +845,7 @@ void unimix_sample_into(torch::Tensor logits, c10::optional<torch::Tensor> unifo
   }
   bool ok = launch_unimix_sample_fwd(logits.data_ptr<float>(), opt_ptr(uniform), nullptr, out.data_ptr<float>(), R, C,
                                      (float)alpha, cur_stream(), N / C, out.stride(0), ip, ldi, (int)idx_off);
-  TORCH_CHECK(ok, "unimix_sample_into: classes must be <= 64");
+  TORCH_CHECK(ok, "unimix_sample_into: classes must be <= 1024");
 }
 
 // column sums of a row-strided 2-D view [rows, N] (stride(1) == 1) -> [N]

@@ -134,6 +134,190 @@ __global__ void __launch_bounds__(256) unimix_sample_bwd_kernel(const float* __r
   if (valid) dlogits[off] = dl;
 }
 
+// ---------------------------------------------------------------- wide categoricals (64 < C <= 64 V)
+// One wave per categorical (the fork's prey_d_1 actor has Discrete(100)): lane l holds classes l + 64 v.  Same
+// arithmetic as the segment form above; the sampler's CDF is each 64-class chunk's wave scan plus the running total
+// of the chunks before it.
+template <int V>
+__global__ void __launch_bounds__(256) unimix_sample_wide_fwd_kernel(const float* __restrict__ logits,
+                                                                     const float* __restrict__ uniform,
+                                                                     float* __restrict__ mixed, float* __restrict__ sample,
+                                                                     int R, int C, float alpha, int G, int lds,
+                                                                     int* __restrict__ idx, int ldi, int ioff) {
+  const int lane = threadIdx.x & 63;
+  const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;  // wave-uniform
+  const float* lr = logits + (int64_t)r * C;
+  float l[V], m[V];
+  bool ok[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int k = lane + 64 * v;
+    ok[v] = k < C;
+    const float x = lr[k < C ? k : C - 1];  // unconditional (clamped) load
+    l[v] = ok[v] ? x : -INFINITY;
+    m[v] = l[v];
+  }
+  if (alpha > 0.f) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < V; ++v) mx = fmaxf(mx, l[v]);
+    mx = seg_max_f(mx, 64);
+    float e[V], s = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      e[v] = ok[v] ? __expf(l[v] - mx) : 0.f;
+      s += e[v];
+    }
+    s = seg_sum_f(s, 64);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float pm = (1.f - alpha) * (e[v] / s) + alpha / C;
+      pm = fminf(fmaxf(pm, FEPS), 1.f - FEPS);
+      m[v] = ok[v] ? logf(pm) : -INFINITY;
+    }
+  }
+  float mx2 = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < V; ++v) mx2 = fmaxf(mx2, m[v]);
+  mx2 = seg_max_f(mx2, 64);
+  float p[V], s2 = 0.f;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    p[v] = ok[v] ? __expf(m[v] - mx2) : 0.f;
+    s2 += p[v];
+  }
+  s2 = seg_sum_f(s2, 64);
+#pragma unroll
+  for (int v = 0; v < V; ++v) p[v] /= s2;
+  int pick;
+  if (uniform != nullptr) {
+    float cdf[V], run = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      cdf[v] = seg_prefix_sum(p[v], 64, lane) + run;
+      run = __shfl(cdf[v], 63, 64);
+    }
+    const float thr = uniform[r] * run;  // run = the last class's CDF (the segment form's max of the CDF)
+    float below = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) below += (ok[v] && cdf[v] < thr) ? 1.f : 0.f;
+    pick = (int)seg_sum_f(below, 64);
+    if (pick > C - 1) pick = C - 1;
+  } else {
+    float bv = -1.f;
+    int bi = 0;
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+      if (ok[v] && p[v] > bv) {  // ascending k within a lane: first index on ties
+        bv = p[v];
+        bi = lane + 64 * v;
+      }
+    pick = seg_argmax(bv, bi, 64);
+  }
+  const int64_t srow = (int64_t)(r / G) * lds + (int64_t)(r % G) * C;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int k = lane + 64 * v;
+    if (ok[v]) {
+      if (mixed) mixed[(int64_t)r * C + k] = m[v];
+      sample[srow + k] = k == pick ? 1.f : 0.f;
+    }
+  }
+  if (idx != nullptr && lane == 0) idx[(int64_t)(r / G) * ldi + (r % G)] = ioff + (r % G) * C + pick;
+}
+
+template <int V>
+__global__ void __launch_bounds__(256) unimix_sample_wide_bwd_kernel(const float* __restrict__ logits,
+                                                                     const float* __restrict__ g_mixed,
+                                                                     const float* __restrict__ g_sample,
+                                                                     float* __restrict__ dlogits, int R, int C, float alpha) {
+  const int lane = threadIdx.x & 63;
+  const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (r >= R) return;  // wave-uniform
+  const int64_t base = (int64_t)r * C;
+  float l[V], q[V], pm[V], m[V], gm[V];
+  bool ok[V], clamped[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int k = lane + 64 * v;
+    ok[v] = k < C;
+    const int kc = k < C ? k : C - 1;
+    const float x = logits[base + kc];
+    l[v] = ok[v] ? x : -INFINITY;
+    m[v] = l[v];
+    q[v] = pm[v] = 0.f;
+    clamped[v] = false;
+    const float g = g_mixed ? g_mixed[base + kc] : 0.f;
+    gm[v] = ok[v] ? g : 0.f;
+  }
+  if (alpha > 0.f) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < V; ++v) mx = fmaxf(mx, l[v]);
+    mx = seg_max_f(mx, 64);
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      q[v] = ok[v] ? __expf(l[v] - mx) : 0.f;
+      s += q[v];
+    }
+    s = seg_sum_f(s, 64);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      q[v] /= s;
+      pm[v] = (1.f - alpha) * q[v] + alpha / C;
+      clamped[v] = pm[v] <= FEPS || pm[v] >= 1.f - FEPS;
+      m[v] = ok[v] ? logf(fminf(fmaxf(pm[v], FEPS), 1.f - FEPS)) : -INFINITY;
+    }
+  }
+  if (g_sample) {
+    float mx2 = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < V; ++v) mx2 = fmaxf(mx2, m[v]);
+    mx2 = seg_max_f(mx2, 64);
+    float p[V], gs[V], s2 = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      p[v] = ok[v] ? __expf(m[v] - mx2) : 0.f;
+      s2 += p[v];
+      const int k = lane + 64 * v;
+      const float g = g_sample[base + (k < C ? k : C - 1)];
+      gs[v] = ok[v] ? g : 0.f;
+    }
+    s2 = seg_sum_f(s2, 64);
+    float dot = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      p[v] /= s2;
+      dot += p[v] * gs[v];
+    }
+    dot = seg_sum_f(dot, 64);
+#pragma unroll
+    for (int v = 0; v < V; ++v) gm[v] += p[v] * (gs[v] - dot);
+  }
+  float dl[V];
+  if (alpha > 0.f) {
+    float w[V], dot = 0.f;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      w[v] = (ok[v] && !clamped[v]) ? (1.f - alpha) * gm[v] / pm[v] : 0.f;
+      dot += q[v] * w[v];
+    }
+    dot = seg_sum_f(dot, 64);
+#pragma unroll
+    for (int v = 0; v < V; ++v) dl[v] = q[v] * (w[v] - dot);
+  } else {
+#pragma unroll
+    for (int v = 0; v < V; ++v) dl[v] = gm[v];
+  }
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const int k = lane + 64 * v;
+    if (ok[v]) dlogits[base + k] = dl[v];
+  }
+}
+
 // ---------------------------------------------------------------- two-hot (one wave per row)
 template <int MAXK>
 __global__ void __launch_bounds__(256) twohot_nll_fwd_kernel(const float* __restrict__ logits, const float* __restrict__ y,
@@ -381,10 +565,20 @@ static int next_pow2(int c) {
 
 bool launch_unimix_sample_fwd(const float* logits, const float* uniform, float* mixed, float* sample, int R, int C,
                               float alpha, hipStream_t st, int G, int lds, int* idx, int ldi, int ioff) {
-  if (C > 64) return false;
+  if (C < 1 || C > 1024) return false;
   if (G <= 0) {
     G = 1;
     lds = C;
+  }
+  if (C > 64) {  // one wave per categorical, 4 per block
+    const dim3 g(cdiv(R, 4)), b(256);
+#define SRL_UW(V) hipLaunchKernelGGL(unimix_sample_wide_fwd_kernel<V>, g, b, 0, st, logits, uniform, mixed, sample, R, C, alpha, G, lds, idx, ldi, ioff)
+    if (C <= 128) SRL_UW(2);
+    else if (C <= 256) SRL_UW(4);
+    else if (C <= 512) SRL_UW(8);
+    else SRL_UW(16);
+#undef SRL_UW
+    return true;
   }
   int W = next_pow2(C);
   int segs_per_block = 4 * (64 / W);
@@ -395,7 +589,17 @@ bool launch_unimix_sample_fwd(const float* logits, const float* uniform, float* 
 
 bool launch_unimix_sample_bwd(const float* logits, const float* g_mixed, const float* g_sample, float* dlogits, int R,
                               int C, float alpha, hipStream_t st) {
-  if (C > 64) return false;
+  if (C < 1 || C > 1024) return false;
+  if (C > 64) {
+    const dim3 g(cdiv(R, 4)), b(256);
+#define SRL_UW(V) hipLaunchKernelGGL(unimix_sample_wide_bwd_kernel<V>, g, b, 0, st, logits, g_mixed, g_sample, dlogits, R, C, alpha)
+    if (C <= 128) SRL_UW(2);
+    else if (C <= 256) SRL_UW(4);
+    else if (C <= 512) SRL_UW(8);
+    else SRL_UW(16);
+#undef SRL_UW
+    return true;
+  }
   int W = next_pow2(C);
   int segs_per_block = 4 * (64 / W);
   hipLaunchKernelGGL(unimix_sample_bwd_kernel, dim3(cdiv(R, segs_per_block)), dim3(256), 0, st, logits, g_mixed, g_sample,

@@ -346,10 +346,11 @@ def test_persistent_scan_timeout_is_loud():
     assert ops.skipped_updates() == 0
 
 
-@pytest.mark.parametrize("graphs", [False, True])
-def test_dv3_vector_obs_train_step(graphs):
+@pytest.mark.parametrize("graphs,n_act", [(False, 2), (True, 2), (True, 100)])
+def test_dv3_vector_obs_train_step(graphs, n_act):
     """Vector observations only (no CNN encoder / decoder: the CartPole-style config), fused ops, with and without
-    the captured step: finite losses that decrease on a fixed batch."""
+    the captured step: finite losses that decrease on a fixed batch.  n_act = 100: the fork's prey_d_1 action space
+    (Discrete(100)), whose actor categorical runs on the wide (one wave per categorical) unimix kernels."""
     from sheeprl_prey_amd.algos.dreamer_v3.agent import build_models
     from sheeprl_prey_amd.algos.dreamer_v3.dreamer_v3 import DreamerV3Trainer
     from sheeprl_prey_amd.algos.dreamer_v3.utils import Moments
@@ -369,15 +370,15 @@ def test_dv3_vector_obs_train_step(graphs):
     torch.manual_seed(0)
     runner = Runner(**dict(cfg.fabric))
     obs_space = spaces.Dict({"state": spaces.Box(-10, 10, (4,), "float32")})
-    wm, actor, critic, target = build_models(runner, [2], False, cfg, obs_space)
+    wm, actor, critic, target = build_models(runner, [n_act], False, cfg, obs_space)
     opts = [build_optimizer(c, m.parameters()) for c, m in
             ((cfg.algo.world_model.optimizer, wm), (cfg.algo.actor.optimizer, actor), (cfg.algo.critic.optimizer, critic))]
-    tr = DreamerV3Trainer(runner, cfg, wm, actor, critic, target, *opts, Moments(None).cuda(), False, [2])
+    tr = DreamerV3Trainer(runner, cfg, wm, actor, critic, target, *opts, Moments(None).cuda(), False, [n_act])
     g = torch.Generator(device="cuda").manual_seed(1)
     T, B = 16, 4
     data = {
         "state": torch.randn(T, B, 4, device="cuda", generator=g),
-        "actions": torch.nn.functional.one_hot(torch.randint(0, 2, (T, B), device="cuda", generator=g), 2).float(),
+        "actions": torch.nn.functional.one_hot(torch.randint(0, n_act, (T, B), device="cuda", generator=g), n_act).float(),
         "rewards": torch.randn(T, B, 1, device="cuda", generator=g),
         "dones": (torch.rand(T, B, 1, device="cuda", generator=g) < 0.1).float(),
         "is_first": (torch.rand(T, B, 1, device="cuda", generator=g) < 0.1).float(),

@@ -77,7 +77,7 @@ def test_ln_gru(H):
         _close(a, c, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("C,G", [(32, 32), (9, 1), (18, 1), (2, 3), (64, 2)])
+@pytest.mark.parametrize("C,G", [(32, 32), (9, 1), (18, 1), (2, 3), (64, 2), (100, 1), (300, 2), (1024, 1)])
 @pytest.mark.parametrize("alpha", [0.0, 0.01])
 def test_unimix_sample(C, G, alpha):
     torch.manual_seed(0)
