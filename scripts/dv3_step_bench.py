@@ -2,6 +2,7 @@
 synthetic data - e.g. the XL Crafter model the 100k bench does not cover.
 
     python scripts/dv3_step_bench.py exp=dreamer_v3_XL_crafter [overrides] --actions 17 --steps 10
+    python scripts/dv3_step_bench.py exp=dreamer_v3_prey --vector 14 --actions 100     (vector observations)
 """
 import argparse
 import os
@@ -18,6 +19,7 @@ def main():
     ap.add_argument("--actions", type=int, default=17)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--vector", type=int, default=0, help="vector observation size (0: 64x64 rgb frames)")
     ap.add_argument("overrides", nargs="*")
     a = ap.parse_args()
     from sheeprl_prey_amd.algos.dreamer_v3.agent import build_models
@@ -29,11 +31,13 @@ def main():
     from sheeprl_prey_amd.parallel.runner import Runner
     from sheeprl_prey_amd.utils.utils import dotdict
 
-    cfg = dotdict(compose(list(a.overrides) + ["cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]", "mlp_keys.encoder=[]",
-                                               "mlp_keys.decoder=[]", "fabric.accelerator=cuda", "fabric.cuda_graphs=True"]))
+    keys = (["cnn_keys.encoder=[]", "cnn_keys.decoder=[]", "mlp_keys.encoder=[state]", "mlp_keys.decoder=[state]"] if a.vector
+            else ["cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]", "mlp_keys.encoder=[]", "mlp_keys.decoder=[]"])
+    cfg = dotdict(compose(list(a.overrides) + keys + ["fabric.accelerator=cuda", "fabric.cuda_graphs=True"]))
     runner = Runner(**dict(cfg.fabric))
     torch.manual_seed(0)
-    obs_space = spaces.Dict({"rgb": spaces.Box(0, 255, (3, 64, 64), "uint8")})
+    obs_space = spaces.Dict({"state": spaces.Box(-10, 10, (a.vector,), "float32")} if a.vector else
+                            {"rgb": spaces.Box(0, 255, (3, 64, 64), "uint8")})
     A = a.actions
     wm, actor, critic, target = build_models(runner, [A], False, cfg, obs_space)
     opts = [build_optimizer(c, m.parameters()) for c, m in
@@ -42,7 +46,8 @@ def main():
     T, B = cfg.per_rank_sequence_length, cfg.per_rank_batch_size
     g = torch.Generator(device="cuda").manual_seed(1)
     data = {
-        "rgb": torch.randint(0, 255, (T, B, 3, 64, 64), dtype=torch.uint8, device="cuda", generator=g),
+        **({"state": torch.randn(T, B, a.vector, device="cuda", generator=g)} if a.vector else
+           {"rgb": torch.randint(0, 255, (T, B, 3, 64, 64), dtype=torch.uint8, device="cuda", generator=g)}),
         "actions": torch.nn.functional.one_hot(torch.randint(0, A, (T, B), device="cuda", generator=g), A).float(),
         "rewards": torch.randn(T, B, 1, device="cuda", generator=g),
         "dones": torch.zeros(T, B, 1, device="cuda"),

@@ -554,6 +554,8 @@ __global__ void __launch_bounds__(NTH) g3_kernel(SP p, int t) {
 }
 
 // ------------------------------------------------------------------------------------------ G4
+constexpr int G4_RED = 8192 + 512;  // red + ct of gemm16<2, .>
+
 __global__ void __launch_bounds__(NTH) g4_kernel(SP p, int t) {
   STAMP(7, 0);
   extern __shared__ float sm[];
@@ -566,7 +568,9 @@ __global__ void __launch_bounds__(NTH) g4_kernel(SP p, int t) {
   float* st = R + 16 * lda;   // s1[16], s2[16], rs[16]
   float* lw = st + 48;        // ln1 gamma, beta
   float* lb = lw + D;
-  float* red = lb + D;
+  // the GEMM's cross-wave reduction scratch (8192 + 512 floats) reuses R once R is dead (after the LN backward)
+  // when R is large enough (D >= 540: the prey preset's dense 1024 then fits the 160 KB of LDS)
+  float* red = 16 * lda >= G4_RED ? R : lb + D;
   float* ct = red + 8192;
   stage_vec(lw, p.ln1w, D);
   stage_vec(lb, p.ln1b, D);
@@ -679,7 +683,7 @@ static Lds scan4_lds_sizes(int S, int D, int H, int hid) {
   l.g1 = 16 * (S + 4) + r1;
   l.g2 = 2 * 16 * (2 * hid + 4) + 96 + 4 * hid + r1;
   l.g3 = 16 * (N3 + 4) + 2 * N3 + r1 + 2 * 16 * g3_nch;
-  l.g4 = 2 * 16 * (D + 4) + 48 + 2 * D + r2;
+  l.g4 = 2 * 16 * (D + 4) + 48 + 2 * D + (16 * (D + 4) >= G4_RED ? 0 : r2);  // red aliases the dead dz tile
   int* v = &l.f1;
   for (int k = 0; k < 8; ++k) v[k] *= 4;
   return l;

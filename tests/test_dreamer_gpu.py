@@ -71,11 +71,13 @@ def test_dv3_graph_matches_eager_losses():
 
 
 @pytest.mark.parametrize("impl", ["persist", "scan4", "scan9"])
-@pytest.mark.parametrize("H,D,hid,B,T", [(64, 64, 64, 4, 16), (512, 512, 512, 16, 8), (96, 80, 48, 3, 5)])
+@pytest.mark.parametrize("H,D,hid,B,T", [(64, 64, 64, 4, 16), (512, 512, 512, 16, 8), (96, 80, 48, 3, 5),
+                                         (256, 1024, 256, 16, 8)])  # the prey preset: deter 256, dense 1024
 def test_fused_rssm_scan_matches_python_scan(H, D, hid, B, T, impl):
     """The fused scans (persist: one persistent launch per direction; scan4: 4+4 MFMA launches/step;
-    scan9: 9+9 launches/step; batched weight grads) vs the python step loop, same noise."""
-    _check_scan_vs_python(H, D, hid, B, T, impl)
+    scan9: 9+9 launches/step; batched weight grads) vs the python step loop, same noise.  D = 1024 is beyond the
+    persistent scan's register tiles: "persist" falls back to scan4 there."""
+    _check_scan_vs_python(H, D, hid, B, T, impl, expect="scan4" if (impl == "persist" and D > 512) else None)
 
 
 @pytest.mark.parametrize("H,D,hid,B,T", [(64, 64, 64, 4, 16), (512, 512, 512, 16, 8), (96, 80, 48, 3, 5),
