@@ -35,6 +35,7 @@ def main():
             else ["cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]", "mlp_keys.encoder=[]", "mlp_keys.decoder=[]"])
     cfg = dotdict(compose(list(a.overrides) + keys + ["fabric.accelerator=cuda", "fabric.cuda_graphs=True"]))
     runner = Runner(**dict(cfg.fabric))
+    runner._init_distributed()  # device + TunableOp mode (fabric.tunable_gemm), as the CLI's launch does
     torch.manual_seed(0)
     obs_space = spaces.Dict({"state": spaces.Box(-10, 10, (a.vector,), "float32")} if a.vector else
                             {"rgb": spaces.Box(0, 255, (3, 64, 64), "uint8")})
