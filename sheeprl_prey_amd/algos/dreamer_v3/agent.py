@@ -297,11 +297,13 @@ class RSSM(nn.Module):
 
     # ---- MI355X imagination: buffer-resident no-grad rollout ---------------------------
     _actor_tail_ok = os.environ.get("SRL_ACTOR_TAIL", "1") != "0"  # A/B switch of the fused rollout actor tail
-    # merged h_{t+1} GEMM of the imagination step (imagine_discrete / imagine_cont), opt-in: measured slower on the
-    # Atari-100k bench (313.0 / 313.5 vs 323.3 env-steps/s, continuous 115.6 vs 118.0; profiles/r4_imag_merge.md) -
-    # hipBLASLt runs the merged [1024, 512] x [512, 2560] + bias GEMM at ~78 TF/s (34.5 us) and the remaining
-    # K = 512 GRU half at ~70 TF/s (23.1 us) where the (h | x) K = 1024 GEMM ran at ~116 TF/s
-    _merge_h_ok = os.environ.get("SRL_IMAG_MERGE", "0") == "1"
+    # merged h_{t+1} GEMM of the imagination step (every GEMM over h_{t+1} as one, 505 -> 463 dispatches per Atari
+    # step).  Untuned it was slower (313.0 / 313.5 vs 323.3 env-steps/s; profiles/r4_imag_merge.md); with its shapes
+    # in the committed TunableOp results it is equal (323.0 vs 323.2 mean of three interleaved 150-step runs,
+    # profiles/r4_merge_ab.md), so the rollouts use it by default (SRL_IMAG_MERGE=0: off); the continuous rollout
+    # (imagine_cont.py) measured 123.6 / 123.7 vs 123.3 / 123.6 env-steps/s with / without (SRL_IMAG_MERGE_CONT).
+    _merge_h_ok = os.environ.get("SRL_IMAG_MERGE", "1") == "1"
+    _merge_h_cont_ok = os.environ.get("SRL_IMAG_MERGE_CONT", os.environ.get("SRL_IMAG_MERGE", "1")) == "1"
     # one-launch prior head (prior_head.hip; used on the merged path): 30.6 us vs ~28 us for LayerNorm + GEMM + sampler
     _prior_head_ok = os.environ.get("SRL_PRIOR_HEAD", "1") != "0"
 

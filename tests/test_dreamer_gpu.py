@@ -184,14 +184,17 @@ def test_dv3_segmented_graph_matches_single_graph(continuous):
         assert torch.isfinite(b2.seg.static_out[k]).all()
 
 
-def test_imagine_discrete_matches_reference_loop(monkeypatch):
+@pytest.mark.parametrize("merge", [True, False])
+def test_imagine_discrete_matches_reference_loop(monkeypatch, merge):
     """Buffer-resident no-grad imagination (RSSM.imagine_discrete) vs the reference loop
     (RSSM.imagination + Actor per step).  imagine_discrete draws every uniform of the rollout in one
     launch, U [H+1, M*(heads + groups)] (actions first, then the prior groups, per step); the
     reference loop is fed the same slices in its call order, so the sampled trajectories agree up to
-    rare category flips from GEMM rounding."""
+    rare category flips from GEMM rounding.  merge: every GEMM over h_{t+1} as one (the default) or separate."""
     from sheeprl_prey_amd import ops
+    from sheeprl_prey_amd.algos.dreamer_v3.agent import RSSM
 
+    monkeypatch.setattr(RSSM, "_merge_h_ok", merge)
     tr = _build(graphs=False)
     wm, actor = tr.world_model, tr.actor
     M, S, H, Hz = 96, 32 * 32, 64, 4
