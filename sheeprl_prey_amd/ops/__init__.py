@@ -723,6 +723,29 @@ def skinny_nt(A: Tensor, W: Tensor, out: Tensor, add: Optional[Tensor] = None) -
     return True
 
 
+# Workspace of the one-launch column sums (LayerNorm parameter / bias gradients, csrc/norm.hip colsum_t_kernel):
+# without it they run as a zero kernel + an atomic reduction (two launches, order-dependent float sums).  One per
+# process, on the device it trains on (Runner sets it up before any step is captured).
+_reduce_ws: dict = {}
+
+
+def init_reduce_workspace(device, floats: int = 1 << 22, counters: int = 1 << 16) -> bool:
+    if not (torch.cuda.is_available() and native_available()) or torch.cuda.is_current_stream_capturing():
+        return False
+    device = torch.device(device)
+    if device.type != "cuda":
+        return False
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    with torch.cuda.device(device):
+        ws = torch.empty(floats, device=device, dtype=torch.float32)
+        cnt = torch.zeros(counters, device=device, dtype=torch.int32)
+        _ext().set_colsum_workspace(ws, cnt)
+    _reduce_ws.clear()
+    _reduce_ws[device.index] = (ws, cnt)  # keep the storage alive for the process
+    return True
+
+
 # Ticket counters of skinny_nt's in-launch split combine: one zeroed int32 pool per device, created on first use
 # (the first calls run eagerly, before any step is captured), handed out in rotating slices so that launches close
 # together never share a counter; each launch's last-arriving workgroup returns its counters to zero.

@@ -20,6 +20,7 @@ bool launch_ln_act_bwd(const float*, int, const float*, int, float*, int, const 
                        const float*, float*, float*, float*, float*, int, int, int, int, hipStream_t);
 void launch_colsum2(const float*, const float*, float*, float*, int, int, int, hipStream_t);
 void launch_colsum1(const float*, int, float*, int, int, hipStream_t);
+void set_colsum_workspace(float*, int64_t, int*, int64_t);
 void launch_cartpole_step(float*, int*, float*, const int64_t*, const float*, float*, float*, float*, float*, float*, float*,
                           float*, int, int, hipStream_t);
 void launch_rssm_mask_fwd(const float*, int, const float*, const float*, const float*, float*, int, float*, int, int, int,
@@ -455,6 +456,18 @@ void ln_act_bwd_into(torch::Tensor x, int64_t ldx, torch::Tensor dy, int64_t ldd
   bool ok = launch_ln_act_bwd(fp(x), ldx, fp(dy), lddy, mp(dx), lddx, ofp(gamma), ofp(beta), fp(mean), fp(rstd), omp(pdg),
                               omp(pdb), omp(dgamma), omp(dbeta), M, N, G, (int)act, cur_stream());
   TORCH_CHECK(ok, "ln_act_bwd_into: unsupported N/G ", N, "/", G);
+}
+
+// column-sum workspace (float32) + ticket counters (int32 zeros) on the current device; None, None: detach
+void set_colsum_workspace_py(c10::optional<torch::Tensor> ws, c10::optional<torch::Tensor> cnt) {
+  if (!ws.has_value() || !ws->defined()) {
+    set_colsum_workspace(nullptr, 0, nullptr, 0);
+    return;
+  }
+  TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == torch::kFloat32 && ws->is_contiguous(), "colsum workspace: float32 GPU");
+  TORCH_CHECK(cnt.has_value() && cnt->is_cuda() && cnt->scalar_type() == torch::kInt32 && cnt->is_contiguous() &&
+                  cnt->device() == ws->device(), "colsum counters: int32 zeros on the workspace's device");
+  set_colsum_workspace(ws->data_ptr<float>(), ws->numel(), cnt->data_ptr<int>(), cnt->numel());
 }
 
 int64_t ln_bwd_grid_py(int64_t M, int64_t N, int64_t G) { return ln_bwd_grid(M, N, G); }
@@ -1160,6 +1173,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_act_fwd_into", &ln_act_fwd_into);
   m.def("ln_act_bwd_into", &ln_act_bwd_into);
   m.def("ln_bwd_grid", &ln_bwd_grid_py);
+  m.def("set_colsum_workspace", &set_colsum_workspace_py);
   m.def("ln_gru_bwd_grid", &ln_gru_bwd_grid_py);
   m.def("ln_gru_fwd_into", &ln_gru_fwd_into);
   m.def("ln_gru_bwd_into", &ln_gru_bwd_into, pybind11::arg("x"), pybind11::arg("h"), pybind11::arg("ldh"), pybind11::arg("gamma"),

@@ -507,6 +507,73 @@ __global__ void __launch_bounds__(256) colsum1_kernel(const float* __restrict__ 
   }
 }
 
+// Ticket-combined form of both column sums (no zero kernel, no float atomics, deterministic): each split block
+// stores its 64-column partial write-through (agent-scope relaxed stores = sc1), drains, joins and draws a ticket
+// from its column tile's counter; the block drawing S - 1 sums the S partials in split order (each wave a fixed
+// quarter of the splits, combined in LDS in wave order) and writes the result, then returns the counter to zero
+// (cdna_hip_programming.md section 6 Guideline 16, split-K counter form).  Rows: r(j) = g + G j, row stride ld.
+__global__ void __launch_bounds__(256) colsum_t_kernel(const float* __restrict__ pa, const float* __restrict__ pb, int ld,
+                                                       float* __restrict__ oa, float* __restrict__ ob, int rows, int N,
+                                                       int G, float* __restrict__ ws, int* __restrict__ cnt) {
+  __shared__ float sa[4][64], sb[4][64];
+  __shared__ int last;
+  const int c = threadIdx.x & 63, n = blockIdx.x * 64 + c;
+  const int slice = threadIdx.x >> 6;
+  const int g = blockIdx.y, S = gridDim.z, s = blockIdx.z;
+  const int Rg = rows > g ? (rows - g + G - 1) / G : 0;
+  const int j0 = (int)((int64_t)Rg * s / S), j1 = (int)((int64_t)Rg * (s + 1) / S);
+  float a = 0.f, b = 0.f;
+  if (n < N) {
+#pragma unroll 4
+    for (int j = j0 + slice; j < j1; j += 4) {
+      const int64_t p = (int64_t)g + (int64_t)G * j;
+      a += pa[p * ld + n];
+      if (pb) b += pb[p * ld + n];
+    }
+  }
+  sa[slice][c] = a;
+  sb[slice][c] = b;
+  __syncthreads();
+  const float ta = (sa[0][c] + sa[1][c]) + (sa[2][c] + sa[3][c]);
+  const float tb = (sb[0][c] + sb[1][c]) + (sb[2][c] + sb[3][c]);
+  if (S == 1) {
+    if (slice == 0 && n < N) {
+      oa[(int64_t)g * N + n] = ta;
+      if (ob) ob[(int64_t)g * N + n] = tb;
+    }
+    return;
+  }
+  const int64_t plane = (int64_t)S * G * N;  // ws: [2][S][G][N]
+  if (slice == 0 && n < N) {
+    __hip_atomic_store(ws + ((int64_t)s * G + g) * N + n, ta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (pb) __hip_atomic_store(ws + plane + ((int64_t)s * G + g) * N + n, tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains its write-through stores
+  __syncthreads();
+  int* ctr = cnt + (int64_t)g * gridDim.x + blockIdx.x;
+  if (threadIdx.x == 0) last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: every read below is sc1
+  a = 0.f;
+  b = 0.f;
+  if (n < N) {
+    for (int q = slice; q < S; q += 4) {
+      a += __hip_atomic_load(ws + ((int64_t)q * G + g) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (pb) b += __hip_atomic_load(ws + plane + ((int64_t)q * G + g) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();  // every wave has read its ta / tb out of sa / sb
+  sa[slice][c] = a;
+  sb[slice][c] = b;
+  __syncthreads();
+  if (slice == 0 && n < N) {
+    oa[(int64_t)g * N + n] = (sa[0][c] + sa[1][c]) + (sa[2][c] + sa[3][c]);
+    if (ob) ob[(int64_t)g * N + n] = (sb[0][c] + sb[1][c]) + (sb[2][c] + sb[3][c]);
+  }
+}
+
 // ---------------------------------------------------------------- NCHW (normalise over C)
 // One thread per pixel.  C <= MAXC: the pixel's C values stay in registers (1 read + 1 write of the
 // tensor); otherwise 3 passes over global memory.
@@ -729,11 +796,49 @@ static void launch_zero2(float* a, float* b, int n, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(zero2_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, a, b, n);
 }
 
+// Workspace + ticket counters of colsum_t_kernel (set once per process by ops.init_reduce_workspace on the device
+// it trains on; until then - or on another device - the zero kernel + atomic form runs).  Launches take rotating
+// slices so launches close together (e.g. on a side stream) never share one.
+static float* g_cs_ws = nullptr;
+static int* g_cs_cnt = nullptr;
+static int64_t g_cs_ws_n = 0, g_cs_cnt_n = 0, g_cs_ws_cur = 0, g_cs_cnt_cur = 0;
+static int g_cs_dev = -1;
+
+void set_colsum_workspace(float* ws, int64_t ws_n, int* cnt, int64_t cnt_n) {
+  g_cs_ws = ws;
+  g_cs_ws_n = ws_n;
+  g_cs_cnt = cnt;
+  g_cs_cnt_n = cnt_n;
+  g_cs_ws_cur = g_cs_cnt_cur = 0;
+  g_cs_dev = -1;
+  if (ws != nullptr) (void)hipGetDevice(&g_cs_dev);
+}
+
+// true: launched the ticket form (out written directly, no zeroing needed)
+static bool colsum_ticket(const float* pa, const float* pb, int ld, float* oa, float* ob, int rows, int N, int G, int S,
+                          hipStream_t st) {
+  if (g_cs_ws == nullptr) return false;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != g_cs_dev) return false;
+  const int nx = cdiv(N, 64);
+  const int64_t need = S > 1 ? 2LL * S * G * N : 0, nc = S > 1 ? (int64_t)G * nx : 0;
+  if (need > g_cs_ws_n || nc > g_cs_cnt_n) return false;
+  if (g_cs_ws_cur + need > g_cs_ws_n) g_cs_ws_cur = 0;
+  if (g_cs_cnt_cur + nc > g_cs_cnt_n) g_cs_cnt_cur = 0;
+  float* ws = g_cs_ws + g_cs_ws_cur;
+  int* cnt = g_cs_cnt + g_cs_cnt_cur;
+  g_cs_ws_cur += (need + 63) / 64 * 64;
+  g_cs_cnt_cur += (nc + 63) / 64 * 64;
+  hipLaunchKernelGGL(colsum_t_kernel, dim3(nx, G, S), dim3(256), 0, st, pa, pb, ld, oa, ob, rows, N, G, ws, cnt);
+  return true;
+}
+
 void launch_colsum1(const float* x, int ldx, float* out, int rows, int N, hipStream_t st) {
-  launch_zero2(out, nullptr, N, st);
   int S = cdiv(rows, 128);
   if (S > 64) S = 64;
   if (S < 1) S = 1;
+  if (colsum_ticket(x, nullptr, ldx, out, nullptr, rows, N, 1, S, st)) return;
+  launch_zero2(out, nullptr, N, st);
   hipLaunchKernelGGL(colsum1_kernel, dim3(cdiv(N, 64), 1, S), dim3(256), 0, st, x, ldx, out, rows, N);
 }
 
@@ -747,12 +852,14 @@ static void launch_colsum2_nz(const float* pa, const float* pb, float* oa, float
 }
 
 void launch_colsum2(const float* pa, const float* pb, float* oa, float* ob, int rows, int N, int G, hipStream_t st) {
-  // zero kernel + one reduction kernel (graph-capturable); ~64 partial rows per split
-  launch_zero2(oa, ob, G * N, st);
+  // ticket form (one launch), else zero kernel + one atomic reduction kernel (graph-capturable); ~64 partial rows
+  // per split
   const int Rg = cdiv(rows, G > 0 ? G : 1);
   int S = cdiv(Rg, 64);
   if (S > 32) S = 32;
   if (S < 1) S = 1;
+  if (colsum_ticket(pa, pb, N, oa, ob, rows, N, G, S, st)) return;
+  launch_zero2(oa, ob, G * N, st);
   hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(N, 64), G, S), dim3(256), 0, st, pa, pb, oa, ob, rows, N, G);
 }
 

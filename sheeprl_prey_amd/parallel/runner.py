@@ -258,13 +258,21 @@ class Runner:
         return self._loggers
 
     # ------------------------------------------------------------------ launch
+    def _device_setup(self) -> None:
+        """Per-process GPU setup after set_device: TunableOp mode, the one-launch column-sum workspace."""
+        from sheeprl_prey_amd.parallel.gemm_tuning import configure
+
+        configure(self.tunable_gemm)
+        if self.fused_ops:
+            from sheeprl_prey_amd import ops
+
+            ops.init_reduce_workspace(self.device)
+
     def _init_distributed(self) -> None:
         ws = int(os.environ.get("WORLD_SIZE", "1"))
         if self.accelerator == "cuda":
             torch.cuda.set_device(self.device)
-            from sheeprl_prey_amd.parallel.gemm_tuning import configure
-
-            configure(self.tunable_gemm)
+            self._device_setup()
         if ws > 1 and not dist.is_initialized():
             # RCCL errors / timeouts tear the process down (non-zero exit) rather than leaving it blocked
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
@@ -281,9 +289,7 @@ class Runner:
                 self._init_distributed()
             elif self.accelerator == "cuda":
                 torch.cuda.set_device(self.device)
-                from sheeprl_prey_amd.parallel.gemm_tuning import configure
-
-                configure(self.tunable_gemm)
+                self._device_setup()
             return fn(self, cfg)
         import torch.multiprocessing as mp
 

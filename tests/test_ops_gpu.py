@@ -311,3 +311,49 @@ def test_ln_grouped_rows(G, N, Bn):
     torch.testing.assert_close(dx.double().view(Bn, G, N).transpose(0, 1), xd.grad, rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(dw.double(), wd.grad, rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(db.double(), bd.grad, rtol=1e-3, atol=1e-3)
+
+
+def test_colsum_ticket_form_deterministic_and_graphed():
+    """One-launch column sums (colsum_t_kernel: split partials combined by the last-arriving block through ticket
+    counters, no zero kernel, no float atomics) vs the fp64 torch sum: bias-gradient form (colsum) and the grouped
+    LayerNorm partial-row form (colsum2), bitwise repeatable, and under hipGraph replay."""
+    C = ops._ext()
+    assert ops.init_reduce_workspace("cuda")
+    try:
+        torch.manual_seed(0)
+        for rows, N in [(16384, 512), (1000, 100), (37, 1536), (130, 64), (9000, 255)]:
+            x = torch.randn(rows, N + 3, device=DEV)[:, :N]
+            out = C.colsum(x)
+            torch.testing.assert_close(out.double(), x.double().sum(0), rtol=1e-5, atol=1e-3)
+            for _ in range(3):
+                assert torch.equal(C.colsum(x), out)
+        for rows, N, G in [(2048, 512, 1), (4096, 1024, 2), (50, 96, 2)]:
+            pa = torch.randn(rows, N, device=DEV)
+            pb = torch.randn(rows, N, device=DEV)
+            oa = torch.full((G, N), float("nan"), device=DEV)
+            ob = torch.full((G, N), float("nan"), device=DEV)
+            C.colsum2(pa, pb, oa, ob, rows, N, G)
+            ra = pa.double().view(-1, G, N).sum(0) if rows % G == 0 else None
+            if ra is not None:
+                torch.testing.assert_close(oa.double(), ra, rtol=1e-5, atol=1e-3)
+                torch.testing.assert_close(ob.double(), pb.double().view(-1, G, N).sum(0), rtol=1e-5, atol=1e-3)
+        # graph replay: the counters return to zero every launch
+        x = torch.randn(4096, 300, device=DEV)
+        ref_out = C.colsum(x)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g):
+                y = C.colsum(x)
+        torch.cuda.current_stream().wait_stream(s)
+        for _ in range(4):
+            y.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(y, ref_out)
+        cnt = ops._reduce_ws[torch.cuda.current_device()][1]
+        assert int(cnt.abs().sum()) == 0
+    finally:
+        C.set_colsum_workspace(None, None)
+        ops._reduce_ws.clear()
