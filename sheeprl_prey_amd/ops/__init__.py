@@ -738,11 +738,13 @@ def init_reduce_workspace(device, floats: int = 1 << 22, counters: int = 1 << 16
     if device.index is None:
         device = torch.device("cuda", torch.cuda.current_device())
     with torch.cuda.device(device):
-        ws = torch.empty(floats, device=device, dtype=torch.float32)
-        cnt = torch.zeros(counters, device=device, dtype=torch.int32)
+        if device.index in _reduce_ws:  # one per device for the process: captured graphs keep its addresses
+            ws, cnt = _reduce_ws[device.index]
+        else:
+            ws = torch.empty(floats, device=device, dtype=torch.float32)
+            cnt = torch.zeros(counters, device=device, dtype=torch.int32)
+            _reduce_ws[device.index] = (ws, cnt)  # never freed: a graph captured with it may replay at any time
         _ext().set_colsum_workspace(ws, cnt)
-    _reduce_ws.clear()
-    _reduce_ws[device.index] = (ws, cnt)  # keep the storage alive for the process
     return True
 
 

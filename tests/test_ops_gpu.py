@@ -355,5 +355,4 @@ def test_colsum_ticket_form_deterministic_and_graphed():
         cnt = ops._reduce_ws[torch.cuda.current_device()][1]
         assert int(cnt.abs().sum()) == 0
     finally:
-        C.set_colsum_workspace(None, None)
-        ops._reduce_ws.clear()
+        C.set_colsum_workspace(None, None)  # later tests: the two-launch form (the workspace stays allocated)
