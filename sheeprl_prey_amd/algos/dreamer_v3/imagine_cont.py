@@ -112,7 +112,7 @@ class ContinuousRollout:
         # transition's first-layer pre-activations (kept: the backward reads them with this row stride), the actor
         # trunk's dense first-layer part for step t+1 and the h half of step t+1's GRU input projection
         a0 = self.layers[0][0]
-        self.merge = self.gru.linear.bias is None and getattr(rssm, "_merge_h_cont_ok", True)
+        self.merge = self.gru.linear.bias is None and rssm.merge_enabled(getattr(rssm, "_merge_h_cont_ok", "auto"), Hd)
         if self.merge:
             self.Na = a0.out_features
             self.Wm = torch.cat((self.tr1.weight, a0.weight[:, S:], self.gru.linear.weight[:, :Hd]), 0)

@@ -194,7 +194,7 @@ def test_imagine_discrete_matches_reference_loop(monkeypatch, merge):
     from sheeprl_prey_amd import ops
     from sheeprl_prey_amd.algos.dreamer_v3.agent import RSSM
 
-    monkeypatch.setattr(RSSM, "_merge_h_ok", merge)
+    monkeypatch.setattr(RSSM, "_merge_h_ok", "1" if merge else "0")
     tr = _build(graphs=False)
     wm, actor = tr.world_model, tr.actor
     M, S, H, Hz = 96, 32 * 32, 64, 4
