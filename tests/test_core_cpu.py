@@ -436,3 +436,21 @@ def test_sidestream_scope_is_inert_on_cpu_and_outside_scopes():
             pass
         assert ss._depth == 1
     assert ss._depth == 0
+
+
+def test_imagination_merge_policy():
+    """SRL_IMAG_MERGE policy: "auto" merges the h_{t+1} GEMMs for recurrent states <= 1024 only (XL measured slower
+    merged), "1" / "0" force it."""
+    from sheeprl_prey_amd.algos.dreamer_v3.agent import RSSM
+
+    assert RSSM.merge_enabled("auto", 512) and RSSM.merge_enabled("auto", 1024)
+    assert not RSSM.merge_enabled("auto", 4096)
+    assert RSSM.merge_enabled("1", 4096) and not RSSM.merge_enabled("0", 256)
+    assert RSSM.merge_enabled(True, 4096) and not RSSM.merge_enabled(False, 256)
+
+
+def test_reduce_workspace_is_gpu_only():
+    """The one-launch column-sum workspace is a GPU-process setup: a no-op (False) for CPU devices."""
+    from sheeprl_prey_amd import ops
+
+    assert ops.init_reduce_workspace("cpu") is False
