@@ -573,7 +573,7 @@ void set_scan4_prof(c10::optional<torch::Tensor> buf) {
 }
 
 void scan4_fwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints, const std::vector<double>& fl,
-               torch::Tensor WzT, torch::Tensor c0) {
+               torch::Tensor WzT, torch::Tensor c0, torch::Tensor sel) {
   TORCH_CHECK(ts.size() == 32, "scan4_fwd: expects 32 tensors");
   auto p = scan4_params(ts, ints, fl);
   p.prof = g_scan4_prof;
@@ -583,6 +583,10 @@ void scan4_fwd(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>&
   TORCH_CHECK(WzT.size(0) == p.S && WzT.size(1) == p.D && c0.numel() == p.D, "scan4_fwd: WzT [S, D] / c0 [D]");
   p.WzT = WzT.data_ptr<float>();
   p.c0 = c0.data_ptr<float>();
+  TORCH_CHECK(sel.is_cuda() && sel.scalar_type() == torch::kInt32 && sel.is_contiguous() &&
+                  sel.numel() >= (int64_t)p.T * 16 * (p.S / p.C) && p.D % 4 == 0,
+              "scan4_fwd: sel must be int32 [T, 16, S / C]");
+  p.sel = sel.data_ptr<int>();
   launch_scan4_fwd(p, cur_stream());
 }
 

@@ -204,21 +204,13 @@ __global__ void __launch_bounds__(NTH) f3_kernel(SP p, int t) {
   float* hs = p.hs + (size_t)t * B * H;
   for (int e = lo + threadIdx.x; e < hi; e += NTH) hs[e] = As[(e / H) * lda + e % H];
   if (t + 1 < p.T) {
-    // step t+1's F1 work that does not need the posterior sample: the masked h half of its GRU input
-    // and the recurrent input xr[t+1] = a_proj[t+1] (+ z0 Wz^T for reset rows); F4 adds z_t Wz^T
+    // step t+1's F1 work that does not need the posterior sample: the masked h half of its GRU input (its
+    // recurrent input xr[t+1] is formed by FX of step t+1 from F4's selected rows)
     const float* first1 = p.first + (size_t)(t + 1) * B;
     float* cat1 = p.cat + (size_t)(t + 1) * B * HD;
     for (int e = lo + threadIdx.x; e < hi; e += NTH) {
       const int b = e / H, j = e - b * H;
       cat1[(size_t)b * HD + j] = (1.f - first1[b]) * As[b * lda + j];
-    }
-    int lo2, hi2;
-    chunk(B * p.D, lo2, hi2);
-    const float* ap = p.a_proj + (size_t)(t + 1) * B * p.D;
-    float* xr1 = p.xr + (size_t)(t + 1) * B * p.D;
-    for (int e = lo2 + threadIdx.x; e < hi2; e += NTH) {
-      const int b = e / p.D, j = e - b * p.D;
-      xr1[e] = ap[e] + first1[b] * p.c0[j];
     }
   }
   STAMP(2, 3);
@@ -318,25 +310,54 @@ __global__ void __launch_bounds__(NTH) f4_kernel(SP p, int t) {
         const size_t o = ((size_t)(t + 1) * B + b) * S + n0 + c;
         p.zm[o] = (1.f - f1) * (k == pick ? 1.f : 0.f) + f1 * p.z0[n0 + c];
       }
-      // [16 rows][32 / C groups]: selected WzT row, -1 = reset row (is_first is binary) / padding row
-      int* sel = (int*)red;
-      if (k == 0) sel[b * (32 / C) + c / C] = (valid && f1 == 0.f) ? n0 + (c - k) + pick : -1;
-    }
-  }
-  if (g == 1 && t + 1 < T) {
-    // xr[t+1][b][:] += WzT[sel][:] for every (row, group) of this workgroup: one coalesced row gather
-    // + no-return atomics per pair (the 32 / C group workgroups of a row add into the same row)
-    __syncthreads();
-    const int* sel = (const int*)red;
-    const int npair = 16 * (32 / C), D = p.D;
-    float* xr1 = p.xr + (size_t)(t + 1) * B * D;
-    for (int e = threadIdx.x; e < npair * D; e += NTH) {
-      const int pr = e / D, j = e - pr * D;
-      const int row = sel[pr];
-      if (row >= 0) atomicAdd(xr1 + (size_t)(pr / (32 / C)) * D + j, p.WzT[(size_t)row * D + j]);
+      // [t+1][16 rows][S / C categoricals]: selected WzT row, -1 = reset row (is_first is binary) / padding row;
+      // FX of step t+1 sums the rows (no atomics: one thread per output element)
+      if (k == 0) p.sel[((size_t)(t + 1) * 16 + b) * (S / C) + (n0 + c) / C] = (valid && f1 == 0.f) ? n0 + (c - k) + pick : -1;
     }
   }
   STAMP(3, 5);
+}
+
+// ------------------------------------------------------------------------------------------ FX
+// xr[t][b][:] = a_proj[t][b][:] + first[t][b] z0 Wz^T + sum over categoricals of WzT[sel[t][b][g]][:] (t >= 1): the
+// posterior one-hot of step t-1 as row gathers.  Grid D / 64 workgroups; thread (b, quad) owns 4 columns of row b,
+// every gathered row load unconditional (a clamped row 0, weighted 0 for -1).
+__global__ void __launch_bounds__(NTH) fx_kernel(SP p, int t) {
+  const int B = p.B, D = p.D, nseg = p.S / p.C;
+  const int b = threadIdx.x >> 4, j = blockIdx.x * 64 + 4 * (threadIdx.x & 15);
+  if (b >= B || j >= D) return;
+  const int* sl = p.sel + ((size_t)t * 16 + b) * nseg;
+  const size_t o = ((size_t)t * B + b) * D + j;
+  const float f = p.first[(size_t)t * B + b];
+  float4 x = *reinterpret_cast<const float4*>(p.a_proj + o);
+  const float4 c = *reinterpret_cast<const float4*>(p.c0 + j);
+  x.x += f * c.x;
+  x.y += f * c.y;
+  x.z += f * c.z;
+  x.w += f * c.w;
+  // batches of 8 categoricals: the 8 indices, then the 8 row loads in flight together (4 round trips at 32
+  // categoricals instead of 32)
+  for (int g0 = 0; g0 < nseg; g0 += 8) {
+    int row[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int gi = g0 + u < nseg ? g0 + u : nseg - 1;
+      const int r = sl[gi];
+      row[u] = g0 + u < nseg ? r : -1;
+    }
+    float4 rv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) rv[u] = *reinterpret_cast<const float4*>(p.WzT + (size_t)(row[u] >= 0 ? row[u] : 0) * D + j);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float w = row[u] >= 0 ? 1.f : 0.f;
+      x.x += w * rv[u].x;
+      x.y += w * rv[u].y;
+      x.z += w * rv[u].z;
+      x.w += w * rv[u].w;
+    }
+  }
+  *reinterpret_cast<float4*>(p.xr + o) = x;
 }
 
 // ------------------------------------------------------------------------------------------ G1
@@ -714,8 +735,11 @@ void launch_scan4_fwd(const SP& p, hipStream_t st) {
   }
   const Lds l = scan4_lds_sizes(p.S, p.D, p.H, p.hid);
   for (int t = 0; t < p.T; ++t) {
-    // F1 only starts the scan: later steps get xr / masked z / masked h from F3 and F4 of step t-1
-    if (t == 0) hipLaunchKernelGGL(f1_kernel, dim3(p.D / 16), dim3(NTH), l.f1, st, p, t);
+    // F1 only starts the scan: later steps get masked z / masked h from F3 and F4 of step t-1, xr from FX
+    if (t == 0)
+      hipLaunchKernelGGL(f1_kernel, dim3(p.D / 16), dim3(NTH), l.f1, st, p, t);
+    else
+      hipLaunchKernelGGL(fx_kernel, dim3((p.D + 63) / 64), dim3(NTH), 0, st, p, t);
     hipLaunchKernelGGL(f2_kernel, dim3(3 * p.H / 16), dim3(NTH), l.f2, st, p, t);
     hipLaunchKernelGGL(f3_kernel, dim3(2 * p.hid / 16), dim3(NTH), l.f3, st, p, t);
     hipLaunchKernelGGL(f4_kernel, dim3(2 * p.S / 32), dim3(NTH), l.f4, st, p, t);

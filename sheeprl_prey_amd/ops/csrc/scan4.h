@@ -18,6 +18,9 @@ struct SP {
   // forward: z0 Wz^T (the recurrent input of a reset row), so F4 can fold the one-hot posterior
   // into the next step's recurrent input by row gathers of WzT instead of an F1 GEMM launch
   const float* c0;
+  // forward: the posterior's selected WzT row per (step, row, categorical) [T][16][S / C], -1 = none (reset /
+  // padding row); F4 of step t writes step t + 1's, FX of step t + 1 gathers them
+  int* sel;
   // optional phase timestamps (block 0, thread 0): prof[kernel * 16 + phase] = s_memtime
   long long* prof;
 };

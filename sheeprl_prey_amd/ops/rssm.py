@@ -253,7 +253,8 @@ class RSSMScan4Fn(torch.autograd.Function):
         fl = [alpha, eps1, epsg, eps2]
         WzT = Wz_c.t().contiguous()
         c0 = torch.mv(Wz_c, z0.reshape(-1))  # recurrent input of a reset row
-        C.scan4_fwd(fwd, dims, fl, WzT, c0)
+        sel = torch.empty(T, 16, S // disc, device=dev, dtype=torch.int32)  # F4 -> FX selected WzT rows
+        C.scan4_fwd(fwd, dims, fl, WzT, c0, sel)
         ctx.save_for_backward(*fwd[:32], WzT)
         ctx.dims, ctx.fl = dims, fl
         hs, mixed, samples = fwd[24], fwd[30], fwd[31]
