@@ -1,7 +1,10 @@
 """Per-phase cycle counts of the 4-launch RSSM scan kernels (block 0, last recorded step).
 
     python scripts/scan4_phases.py            # DreamerV3 Atari-100k shapes: B16 T64 H512 D512 hid512 S1024
+    python scripts/scan4_phases.py 256 1024 256 100   # the prey preset: deter 256, dense 1024, hidden 256, 100 actions
 """
+import sys
+
 import torch
 
 from sheeprl_prey_amd import ops
@@ -39,4 +42,5 @@ def main(H=512, D=512, hid=512, B=16, T=64, E=4096, A=9):
 
 
 if __name__ == "__main__":
-    main()
+    a = [int(x) for x in sys.argv[1:]]
+    main(*a[:3], A=a[3]) if len(a) >= 4 else main(*a)
