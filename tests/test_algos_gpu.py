@@ -142,3 +142,21 @@ def test_bf16_mixed_gpu(algo):
     # every sub-model the step calls ran its forward under autocast (the world model has no forward of its own)
     want = {"PPOAgent"} if algo == "ppo" else {"MultiEncoder", "RecurrentModel", "MLP", "MultiDecoder", "Actor"}
     assert want <= set(seen), f"forwards run under autocast: {dict(seen)}"
+
+
+def test_dreamer_v3_prey_preset_gpu():
+    """The fork's own preset (exp=dreamer_v3_prey) on the native prey_d_1 cellworld through the CLI on the GPU:
+    vector observations, the Discrete(100) actor on the wide-categorical unimix kernels, the 4-launch RSSM scan at
+    dense 1024 (scaled down here: dense 256, 64-step sequences kept short), captured train steps."""
+    _run(["exp=dreamer_v3_prey", "env.sync_env=True", "env.capture_video=False", "total_steps=260",
+          "algo.learning_starts=200", "per_rank_sequence_length=16", "per_rank_batch_size=4", "algo.dense_units=256",
+          "metric.log_every=100", "checkpoint.every=0", "root_dir=dv3prey", "run_name=g"])
+    _check_ckpt("dv3prey", "g", DV3_KEYS, False)
+
+
+def test_ppo_prey_gpu():
+    """PPO on prey_d_1 (Discrete(100)) through the CLI on the GPU path."""
+    _run(["exp=ppo", "env=prey", "mlp_keys.encoder=[state]", "env.num_envs=2", "env.sync_env=True",
+          "env.capture_video=False", "total_steps=512", "algo.rollout_steps=128", "per_rank_batch_size=64",
+          "metric.log_every=256", "checkpoint.every=0", "root_dir=ppoprey", "run_name=g"])
+    _check_ckpt("ppoprey", "g", PPO_KEYS, False)
