@@ -146,8 +146,9 @@ def test_bf16_mixed_gpu(algo):
 
 def test_dreamer_v3_prey_preset_gpu():
     """The fork's own preset (exp=dreamer_v3_prey) on the native prey_d_1 cellworld through the CLI on the GPU:
-    vector observations, the Discrete(100) actor on the wide-categorical unimix kernels, the 4-launch RSSM scan at
-    dense 1024 (scaled down here: dense 256, 64-step sequences kept short), captured train steps."""
+    vector observations, the Discrete(100) actor on the wide-categorical unimix kernels, captured train steps.
+    Scaled down (dense 256, 16-step sequences: the persistent scan); the preset's dense 1024 runs the 4-launch scan,
+    whose shape tests/test_dreamer_gpu.py covers."""
     _run(["exp=dreamer_v3_prey", "env.sync_env=True", "env.capture_video=False", "total_steps=260",
           "algo.learning_starts=200", "per_rank_sequence_length=16", "per_rank_batch_size=4", "algo.dense_units=256",
           "metric.log_every=100", "checkpoint.every=0", "root_dir=dv3prey", "run_name=g"])
