@@ -169,14 +169,26 @@ class ReplayBuffer:
         self._ensure_storage(data_to_store)
         dev = self._first_device()
         if dev.type != "cpu" and len(idxes) == next_pos - self._pos > 0:
-            # contiguous rows: a slice copy, no index upload
+            # contiguous rows: a slice copy, no index upload.  Device-resident sources of the buffer's dtype
+            # (e.g. SAC's one staged row, sliced per key) go as ONE multi-tensor copy launch instead of one
+            # copy per key
+            dsts, srcs = [], []
             for k, v in data_to_store.items():
+                dst = self._buf._data[k][self._pos : next_pos]
+                if v.device == dst.device and v.dtype == dst.dtype and v.shape == dst.shape:
+                    dsts.append(dst)
+                    srcs.append(v)
+                    continue
                 # pinned / device sources copy without blocking the host (stream-ordered).  A pageable
                 # host source must copy synchronously: an async DMA from pageable memory may read it
                 # after the caller has freed or overwritten it (seen as NaN gradients once the
                 # stream runs a captured train step ahead of the host)
                 nb = v.device.type != "cpu" or v.is_pinned()
-                self._buf._data[k][self._pos : next_pos].copy_(v, non_blocking=nb)
+                dst.copy_(v, non_blocking=nb)
+            if len(dsts) > 1:
+                torch._foreach_copy_(dsts, srcs)
+            elif dsts:
+                dsts[0].copy_(srcs[0])
         else:
             idxes = idxes.to(dev)
             for k, v in data_to_store.items():
