@@ -33,3 +33,25 @@ def test_synthetic_atari_truncates_and_resets():
     f1, _ = e.reset(seed=1)
     f2, _ = SyntheticAtari("MsPacmanNoFrameskip-v4", screen_size=64).reset(seed=1)
     assert np.array_equal(f1, f2)
+
+
+def test_synthetic_control_states_renders_and_rewards_pinned():
+    """The walker_walk-shaped control env (SyntheticControl): states, renders and rewards of 100 seeded steps pinned
+    by checksum (its render caches the tiled floor, which equals the per-call formula it replaced)."""
+    from sheeprl_prey_amd.envs.synthetic import SyntheticControl
+
+    e = SyntheticControl(seed=3)
+    e.reset(seed=3)
+    h = hashlib.sha256(e.render().tobytes())
+    tot = 0.0
+    rng = np.random.default_rng(0)
+    for _ in range(100):
+        o, r, term, trunc, _ = e.step(rng.uniform(-1, 1, 6))
+        tot += r
+        h.update(o.tobytes())
+        h.update(e.render().tobytes())
+    assert h.hexdigest()[:16] == "11bd4e172c8f129d"
+    assert abs(tot - 47.48275099571548) < 1e-9
+    s = e.size
+    yy, xx = np.mgrid[0:s, 0:s]
+    assert np.array_equal(e._floor, np.repeat((((xx // 8 + yy // 8) % 2) * 30 + 40).astype(np.uint8)[..., None], 3, -1))
