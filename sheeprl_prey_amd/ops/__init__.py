@@ -730,6 +730,8 @@ _reduce_ws: dict = {}
 
 
 def init_reduce_workspace(device, floats: int = 1 << 22, counters: int = 1 << 16) -> bool:
+    if os.environ.get("SRL_COLSUM_TICKET", "1") == "0":  # A/B: the two-launch (zero + atomic) column sums
+        return False
     if not (torch.cuda.is_available() and native_available()) or torch.cuda.is_current_stream_capturing():
         return False
     device = torch.device(device)
