@@ -214,6 +214,9 @@ def main():
             out = one_step()
             heart.beat(f"warmup step {i}")
     torch.cuda.synchronize()
+    heart.beat("warmup done")
+    if args.torch_profile:
+        heart.grace("rank-0 torch profile")
     if args.torch_profile and rank == 0:
         # op attribution of the small kernels: the same train step run eagerly (graphs off) under
         # torch.profiler; a graph replay dispatches the very same kernels
@@ -273,6 +276,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    heart.beat("pre-timed barrier")
     if args.phase_times:
         trainer.seg.enable_timing()
     if args.profile_steps:

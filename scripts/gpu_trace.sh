@@ -10,6 +10,7 @@ rc=$?
 tail -1 gpurun_out/trace.log
 f=$(find gpurun_out/trace -name "*kernel_trace.csv" | head -1)
 [ -n "$f" ] && python scripts/trace_window.py "$f" $STEPS ${TOP:-45} > gpurun_out/trace_summary.md
+[ -n "$f" ] && [ -n "${STEPDUMP:-}" ] && python scripts/trace_step.py "$f" $STEPS > "$STEPDUMP"
 rm -f gpurun_out/trace/*kernel_trace.csv
 head -3 gpurun_out/trace_summary.md
 exit $rc

@@ -89,7 +89,11 @@ def one_hot_actions(actions: np.ndarray, actions_dim: Sequence[int]) -> np.ndarr
 
 def log_throughput(runner, timer_metrics: Dict[str, float], policy_step: int, last_log: int, train_step: int,
                    last_train: int, action_repeat: int) -> None:
-    """``Time/sps_train`` and ``Time/sps_env_interaction`` (reference ``dreamer_v3.py:754-767``)."""
+    """``Time/sps_train`` and ``Time/sps_env_interaction`` (reference ``dreamer_v3.py:754-767``).  Also the
+    shared device health check (``ops.check_faults``): a recorded kernel fault raises here at the latest."""
+    from sheeprl_prey_amd import ops
+
+    ops.check_faults()
     ws = runner.world_size
     if "Time/train_time" in timer_metrics and timer_metrics["Time/train_time"] > 0:
         runner.log("Time/sps_train", (train_step - last_train) / timer_metrics["Time/train_time"], policy_step)

@@ -47,13 +47,13 @@ class DreamerV1Trainer:
         self._st: Dict[str, Any] = {}
         self.detach_heads = False  # Plan2Explore trains the reward/continue heads on detached latents
         self.step = PhasedStep(runner, [self._phase_wm, self._phase_behaviour, self._phase_critic, self._phase_final],
-                               [self._coll(world_optimizer), self._coll(actor_optimizer), self._coll(critic_optimizer)],
+                               [self._coll(world_optimizer, True), self._coll(actor_optimizer), self._coll(critic_optimizer)],
                                graphs=bool(cfg.fabric.get("cuda_graphs", False)), name="dreamer_v1_train")
 
-    def _coll(self, opt):
+    def _coll(self, opt, faults: bool = False):
         def f(dry: bool = False):
             if not dry:
-                self.runner.sync_gradients(opt)
+                self.runner.sync_gradients(opt, faults=faults)
         return f
 
     def train_step(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:

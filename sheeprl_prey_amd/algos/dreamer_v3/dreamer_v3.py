@@ -176,7 +176,7 @@ class DreamerV3Trainer:
     def _coll_wm(self, dry: bool = False) -> None:
         set_phase("coll_wm")
         if not dry:
-            self.runner.sync_gradients(self.world_optimizer)
+            self.runner.sync_gradients(self.world_optimizer, faults=True)
 
     def _coll_actor(self, dry: bool = False) -> None:
         set_phase("coll_actor")

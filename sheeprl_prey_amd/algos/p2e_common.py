@@ -79,11 +79,11 @@ class P2EMixin:
             self.runner,
             [self._phase_wm, self._phase_ensemble, self._phase_expl_actor, self._phase_expl_critic,
              self._phase_task_actor, self._phase_critic_task, self._phase_final_task],
-            [c(self.world_optimizer), c(ensemble_optimizer), c(actor_expl_optimizer), c(critic_expl_optimizer),
+            [c(self.world_optimizer, True), c(ensemble_optimizer), c(actor_expl_optimizer), c(critic_expl_optimizer),
              c(self.actor_optimizer), c(self.critic_optimizer)], graphs=g, name="p2e_explore")
         self.task_step = PhasedStep(
             self.runner, [self._phase_wm, self._phase_task_actor_wm, self._phase_critic_task, self._phase_final_task],
-            [c(self.world_optimizer), c(self.actor_optimizer), c(self.critic_optimizer)], graphs=g, name="p2e_task")
+            [c(self.world_optimizer, True), c(self.actor_optimizer), c(self.critic_optimizer)], graphs=g, name="p2e_task")
         self.is_exploring = True
 
     def train_step(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:

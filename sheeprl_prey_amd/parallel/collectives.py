@@ -117,10 +117,14 @@ def step_boundary() -> None:
 class Heartbeat:
     """Daemon watchdog: if ``beat()`` is not called for ``timeout_s`` seconds the process prints the
     last beat's label and exits with status 3 (``os._exit``: a rank stuck in a device wait never
-    returns to Python).  ``timeout_s <= 0`` disables it."""
+    returns to Python).  ``timeout_s <= 0`` disables it.  Until the first ``beat()`` the limit is
+    ``max(timeout_s, startup_grace_s)``: model / env construction, the first graph captures, TunableOp
+    tuning and diagnostic passes run before any step completes and must not trip a short step timeout."""
 
-    def __init__(self, timeout_s: float, label: str = "start"):
+    def __init__(self, timeout_s: float, label: str = "start", startup_grace_s: float = 1800.0):
         self.timeout_s = float(timeout_s)
+        self.startup_grace_s = float(startup_grace_s)
+        self._beaten = False
         self.label = label
         self._last = time.monotonic()
         self._stop = threading.Event()
@@ -131,6 +135,15 @@ class Heartbeat:
 
     def beat(self, label: str = "") -> None:
         self._last = time.monotonic()
+        self._beaten = True
+        if label:
+            self.label = label
+
+    def grace(self, label: str = "") -> None:
+        """Re-arm the start-up grace until the next ``beat()`` (long diagnostic passes, e.g. a rank-0 profile
+        that the other ranks wait for at a barrier)."""
+        self._last = time.monotonic()
+        self._beaten = False
         if label:
             self.label = label
 
@@ -140,7 +153,8 @@ class Heartbeat:
     def _run(self) -> None:
         while not self._stop.wait(min(5.0, self.timeout_s / 4)):
             idle = time.monotonic() - self._last
-            if idle > self.timeout_s:
+            limit = self.timeout_s if self._beaten else max(self.timeout_s, self.startup_grace_s)
+            if idle > limit:
                 rank = os.environ.get("RANK", "0")
                 print(f"[rank {rank}] heartbeat: no progress for {idle:.0f} s after '{self.label}' "
                       f"(a collective or kernel never completed); exiting", file=sys.stderr, flush=True)

@@ -379,13 +379,32 @@ class Runner:
         if optimizer is not None:
             self.sync_gradients(optimizer)
 
-    def sync_gradients(self, optimizer, wait: bool = True) -> None:
+    def agree_faults(self, device) -> None:
+        """Make the device-side skip decision collective: all-reduce (max) words 0/1 of the device fault block
+        (persistent-scan hand-off timeout, replay-gather error; ``ops.fault_block``) so that when ONE rank's
+        kernels recorded a fault every rank skips the same optimiser update (the flat optimisers' norm /
+        advance kernels read those words) and every rank raises at its next host health check, instead of the
+        faulted rank keeping its parameters while the others step and the replicas silently diverging."""
+        if self.world_size <= 1 or torch.device(device).type != "cuda":
+            return
+        from sheeprl_prey_amd import ops
+
+        dist.all_reduce(ops.fault_block(device)[:2], op=dist.ReduceOp.MAX, group=self.group)
+
+    def sync_gradients(self, optimizer, wait: bool = True, faults: bool = False) -> None:
         """Average ``optimizer``'s gradients over the ranks.  ``wait=False`` (flat optimisers): the
-        collectives stay in flight until the optimiser's next ``clip_grad_norm_`` / ``step`` joins them."""
+        collectives stay in flight until the optimiser's next ``clip_grad_norm_`` / ``step`` joins them.
+        ``faults=True``: first agree on the device fault words (``agree_faults``) - pass it on the step's first
+        sync, after the kernels that can record a fault (replay gather, scan) and before any optimiser reads
+        them."""
         if self.world_size <= 1:
             return
         from sheeprl_prey_amd.parallel.flat_optim import FlatOptimizer
 
+        if faults:
+            dev = optimizer.flat_param.device if isinstance(optimizer, FlatOptimizer) else next(
+                (p.device for g in optimizer.param_groups for p in g["params"]), torch.device("cpu"))
+            self.agree_faults(dev)
         if isinstance(optimizer, FlatOptimizer):
             optimizer.all_reduce_grads(self.group, self.world_size, bucket_mb=self.bucket_mb, wait=wait)
             if self.overlap_grad_sync:

@@ -69,7 +69,7 @@ def test_ppo_device_env_gpu(fused):
     _check_ckpt("ppo_dev", f"f{int(fused)}", PPO_KEYS, False)
 
 
-@pytest.mark.parametrize("env_id", ["discrete_dummy", "continuous_dummy"])
+@pytest.mark.parametrize("env_id", ["discrete_dummy", "multidiscrete_dummy", "continuous_dummy"])
 def test_dreamer_v3_gpu(env_id):
     _run(STD + ["exp=dreamer_v3", "env=dummy", f"env.id={env_id}", "buffer.size=4", "root_dir=dv3",
                 f"run_name={env_id}", "buffer.checkpoint=True"] + TINY_DREAMER)

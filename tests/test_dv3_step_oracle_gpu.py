@@ -1,5 +1,8 @@
 """Whole-train-step oracle at the headline bench shape (B 16 x T 64, H 15, dense 512, cnn mult 32, deter 512,
-stoch 32x32, 9 actions; ``exp=dreamer_v3_100k_ms_pacman``).
+stoch 32x32, 9 actions; ``exp=dreamer_v3_100k_ms_pacman``), and the same step with a multi-discrete [3, 2] action
+space (two actor heads: the ``nh > 1`` branches of the imagination kernels, the per-head unimix and the
+multi-head actor loss; reference ``tests/test_algos/test_algos.py:562-564`` runs every algorithm on
+``multidiscrete_dummy``).
 
 The fused + hipGraph-replayed ``DreamerV3Trainer`` step (HIP kernels, recorded-forward reuse, one-hot
 gathers, device-side clipping) is compared with the SAME step run eagerly through the fp32 reference
@@ -23,7 +26,7 @@ pytestmark = pytest.mark.gpu
 T, B = 64, 16
 
 
-def _build():
+def _build(adim):
     from sheeprl_prey_amd.algos.dreamer_v3.agent import build_models
     from sheeprl_prey_amd.algos.dreamer_v3.dreamer_v3 import DreamerV3Trainer
     from sheeprl_prey_amd.algos.dreamer_v3.utils import Moments
@@ -38,20 +41,22 @@ def _build():
     runner = Runner(**dict(cfg.fabric))
     torch.manual_seed(0)
     obs_space = spaces.Dict({"rgb": spaces.Box(0, 255, (3, 64, 64), "uint8")})
-    wm, actor, critic, target = build_models(runner, [9], False, cfg, obs_space)
+    wm, actor, critic, target = build_models(runner, adim, False, cfg, obs_space)
     opts = [build_optimizer(c, m.parameters()) for c, m in
             ((cfg.algo.world_model.optimizer, wm), (cfg.algo.actor.optimizer, actor), (cfg.algo.critic.optimizer, critic))]
     moments = Moments(None, cfg.algo.actor.moments.decay, cfg.algo.actor.moments.max,
                       cfg.algo.actor.moments.percentile.low, cfg.algo.actor.moments.percentile.high).cuda()
-    tr = DreamerV3Trainer(runner, cfg, wm, actor, critic, target, *opts, moments, False, [9])
+    tr = DreamerV3Trainer(runner, cfg, wm, actor, critic, target, *opts, moments, False, adim)
     return tr, opts, moments
 
 
-def _data():
+def _data(adim):
     g = torch.Generator(device="cuda").manual_seed(1)
+    acts = torch.cat([torch.nn.functional.one_hot(torch.randint(0, a, (T, B), device="cuda", generator=g), a).float()
+                      for a in adim], -1)
     return {
         "rgb": torch.randint(0, 255, (T, B, 3, 64, 64), dtype=torch.uint8, device="cuda", generator=g),
-        "actions": torch.nn.functional.one_hot(torch.randint(0, 9, (T, B), device="cuda", generator=g), 9).float(),
+        "actions": acts,
         "rewards": torch.randn(T, B, 1, device="cuda", generator=g),
         "dones": (torch.rand(T, B, 1, device="cuda", generator=g) < 0.02).float(),
         "is_first": (torch.rand(T, B, 1, device="cuda", generator=g) < 0.02).float(),
@@ -73,12 +78,13 @@ def _rel(a: torch.Tensor, b: torch.Tensor) -> float:
     return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
 
 
-def test_dv3_fused_graphed_step_matches_eager_reference_step():
+@pytest.mark.parametrize("adim", [[9], [3, 2]], ids=["discrete9", "multidiscrete3x2"])
+def test_dv3_fused_graphed_step_matches_eager_reference_step(adim):
     from sheeprl_prey_amd import ops
     from sheeprl_prey_amd.algos.dreamer_v3.dreamer_v3 import METRIC_KEYS
 
-    tr, opts, moments = _build()
-    data = _data()
+    tr, opts, moments = _build(adim)
+    data = _data(adim)
     tr.update_target(1.0)
     snap = {k: v.detach().clone() for k, v in _state(tr, opts, moments).items()}
     for _ in range(3):  # 2 warm-up steps, then capture (+ one replay)
