@@ -72,7 +72,6 @@ def _act_code(act: str) -> int:
 
 # =============================================================== Linear (library GEMMs, column-sum bias grad)
 _LIN2D = os.environ.get("SRL_LIN2D", "1") != "0"  # A/B switch
-_SIDE_LIN = os.environ.get("SRL_SIDE_LIN", "1") != "0"  # A/B switch: Linear parameter gradients on the side stream
 
 
 def _lin2d(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
@@ -137,11 +136,13 @@ def transpose_many(xs, outs=None):
     return res
 
 
-def wgrad(dz: Tensor, x: Optional[Tensor] = None, onehot=None, bias: bool = False):
+def wgrad(dz: Tensor, x: Optional[Tensor] = None, onehot=None, bias: bool = False, out=None):
     """``(dW, db)`` of a linear layer ``z = [onehot | x] W^T + b`` from ``dz`` = dL/dz over M rows:
     ``dW [N, Kone + Kd] = [onehot | x]^T dz``, ``db = dz.sum(0)`` (None unless ``bias``; needs ``x``).
     ``onehot = (idx, G, off, n_onehot)``: the first ``n_onehot = G*C`` input columns are exact one-hots whose hot
-    column is ``idx[m, g] - off`` (idx row-strided int32 [M, >= G]); they are scattered, not multiplied."""
+    column is ``idx[m, g] - off`` (idx row-strided int32 [M, >= G]); they are scattered, not multiplied.
+    ``out = (dW, db)``: preallocated results (``ops/sidestream.py`` deferral), filled in place where the
+    kernel path allows; the caller copies whatever else is returned."""
     dz2 = _rows2d(dz)
     M, N = dz2.shape
     x2 = _rows2d(x) if x is not None else None
@@ -162,8 +163,10 @@ def wgrad(dz: Tensor, x: Optional[Tensor] = None, onehot=None, bias: bool = Fals
         dWo = torch.empty(N, G * C, device=dz.device, dtype=torch.float32)
         _ext().wgrad(dz2, None, idx2, int(G), int(C), int(off), dWo, None, False)
         return torch.cat((dWo, dense), 1), db
-    dW = torch.empty(N, G * C + Kd, device=dz.device, dtype=torch.float32)
-    db = torch.empty(N, device=dz.device, dtype=torch.float32) if bias else None
+    dW = out[0] if out is not None and out[0] is not None else torch.empty(N, G * C + Kd, device=dz.device, dtype=torch.float32)
+    db = None
+    if bias:
+        db = out[1] if out is not None and out[1] is not None else torch.empty(N, device=dz.device, dtype=torch.float32)
     _ext().wgrad(dz2, x2, idx2, int(G), int(C), int(off), dW, db, False)
     return dW, db
 
@@ -186,26 +189,31 @@ class _Linear(torch.autograd.Function):
 
         x, w = ctx.saved_tensors
         g2 = gy.reshape(-1, gy.shape[-1])
-        dx = dw = db = None
+        dx = None
         if ctx.needs_input_grad[0]:
             dx = (g2 @ w).view(*gy.shape[:-1], w.shape[1])
-        if ss.active(gy.device) and ctx.needs_input_grad[1] and _SIDE_LIN:
-            # inside a side-stream scope (the world-model backward): the parameter gradients leave the data-gradient
-            # chain and run beside it (ops/sidestream.py)
-            with ss.on_side(gy.device, g2, x):
-                dw, db = _Linear._param_grads(ctx, g2, x)
-            return dx, ss.mark_main(dw), (ss.mark_main(db) if db is not None else None)
-        dw, db = _Linear._param_grads(ctx, g2, x)
+        if ss.active(gy.device) and ctx.needs_input_grad[1]:
+            # inside a deferral scope (the world-model backward): the parameter gradients leave the data-gradient
+            # chain and run beside the scan backward (ops/sidestream.py)
+            shapes = [tuple(w.shape), (w.shape[0],) if ctx.has_bias and ctx.needs_input_grad[2] else None]
+            meta = (tuple(ctx.needs_input_grad), ctx.has_bias)
+            dw, db = ss.param_grads(gy.device, lambda outs: _Linear._param_grads(meta, g2, x, outs), shapes, g2, x)
+            return dx, dw, db
+        dw, db = _Linear._param_grads((tuple(ctx.needs_input_grad), ctx.has_bias), g2, x)
         return dx, dw, db
 
     @staticmethod
-    def _param_grads(ctx, g2, x):
+    def _param_grads(meta, g2, x, out=None):
+        needs, has_bias = meta
         dw = db = None
-        if ctx.needs_input_grad[1] and wgrad_ok(g2):
-            return wgrad(g2, x, bias=ctx.has_bias and ctx.needs_input_grad[2])
-        if ctx.needs_input_grad[1]:
-            dw = g2.t() @ x.reshape(-1, x.shape[-1])
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if needs[1] and wgrad_ok(g2):
+            return wgrad(g2, x, bias=has_bias and needs[2], out=out)
+        if needs[1]:
+            if out is not None and out[0] is not None:
+                dw = torch.mm(g2.t(), x.reshape(-1, x.shape[-1]), out=out[0])
+            else:
+                dw = g2.t() @ x.reshape(-1, x.shape[-1])
+        if has_bias and needs[2]:
             db = _ext().colsum(g2 if g2.stride(-1) == 1 else g2.contiguous())
         return dw, db
 
@@ -506,6 +514,22 @@ def skipped_updates(reset: bool = False) -> int:
     return n
 
 
+def check_faults() -> None:
+    """Host health check shared by every algorithm loop (``algos/common.py:log_throughput``, log time; syncs):
+    words 0 / 1 of a device fault block are sticky and make every flat-optimiser update skip, so a fault
+    that no algorithm-specific check consumed (DreamerV3 reads and resets them itself first) must not leave
+    the run silently frozen - reset the words and raise."""
+    bad = []
+    for key, b in _FAULT.items():
+        w = b[:2].cpu()
+        if int(w[0]) | int(w[1]):
+            b[:2].zero_()
+            bad.append((key, int(w[0]), int(w[1])))
+    if bad:
+        raise RuntimeError("device fault block set (scan health word, replay-gather error word) on "
+                           f"{bad}: the optimiser updates of the affected steps were skipped")
+
+
 def _guard_tripped(guard: Optional[Tensor]) -> bool:
     if guard is None:
         return False
@@ -567,7 +591,7 @@ def flat_adam(p, g, m, v, scalars, lr, b1, b2, eps, wd, decoupled) -> None:
 
 __all__ = [
     "ln_act", "ln_act_nchw", "ln_gru", "unimix_sample", "twohot_nll", "twohot_mean", "twohot_bins", "kl_balance",
-    "lambda_returns", "gae_scan", "flat_grad_norm", "flat_advance", "flat_adam", "fault_block", "skipped_updates", "native_available", "set_fused",
+    "lambda_returns", "gae_scan", "flat_grad_norm", "flat_advance", "flat_adam", "fault_block", "skipped_updates", "check_faults", "native_available", "set_fused",
 ]
 
 

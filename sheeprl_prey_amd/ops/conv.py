@@ -199,8 +199,12 @@ def encoder_small(stages, x: Tensor, scale: float = 1.0) -> Tensor:
 
 
 def _wgrad(C, P: Tensor, Q: Tensor, cb: int, w: Tensor) -> Tensor:
-    """Decoder weight gradient (in line)."""
-    return C.conv_wgrad(P, Q, cb)
+    """Decoder weight gradient: in line, or deferred beside the scan backward inside a deferral scope
+    (``ops/sidestream.py``; written straight into the preallocated gradient)."""
+    dev = P.device
+    if not ss.active(dev):
+        return C.conv_wgrad(P, Q, cb)
+    return ss.param_grads(dev, lambda outs: (C.conv_wgrad(P, Q, cb, outs[0]),), [tuple(w.shape)], P, Q)[0]
 
 
 # ---------------------------------------------------------------------------------- decoder
@@ -254,11 +258,9 @@ class DecoderConvFn(torch.autograd.Function):
         dbias = dout.sum(dim=(0, 2, 3))
         dws: List[Optional[Tensor]] = [None] * (L + 1)
         cout_last = ws[L].shape[1]
-        # the weight gradients leave the critical path (data gradients -> scan backward -> encoder): each runs
-        # on the side stream as soon as its output gradient exists (ops/sidestream.py; joined by the optimiser)
-        dev = dout.device
-        with ss.on_side(dev, p_last, q):
-            dws[L] = _wgrad(C, p_last, q, cout_last, ws[L])
+        # the weight gradients leave the critical path (data gradients -> scan backward -> encoder): inside the
+        # world-model backward they are queued and run beside the scan backward (ops/sidestream.py)
+        dws[L] = _wgrad(C, p_last, q, cout_last, ws[L])
         wp = C.conv_pack_down(ws[L], q.shape[3])
         _, zp, mp, rp = acts[4 * (L - 1):4 * L]
         dz = C.conv_gemm(0, q, wp, ws[L].shape[0], 1, gs[L - 1], bs[L - 1], 0.0, act[L - 1], False, zp, mp, rp,
@@ -267,8 +269,7 @@ class DecoderConvFn(torch.autograd.Function):
         for i in range(L - 1, -1, -1):
             p = acts[4 * i]
             cout = ws[i].shape[1]
-            with ss.on_side(dev, p, dz):
-                dws[i] = _wgrad(C, p, dz, cout, ws[i])
+            dws[i] = _wgrad(C, p, dz, cout, ws[i])
             wp = C.conv_pack_down(ws[i], cout)
             cin = ws[i].shape[0]
             if i > 0:
@@ -279,8 +280,6 @@ class DecoderConvFn(torch.autograd.Function):
                 dh = C.conv_gemm(0, dz, wp, cin, 2, None, None, 0.0, 0, True, None, None, None, None, None, None,
                                  0.0, cin)[0]
         dh = dh.reshape(dh.shape[0], -1)
-        for d in dws:
-            ss.mark_main(d)
         return (dh, None, *dws, *[d.view_as(g) for d, g in zip(dgs, gs)], *[d.view_as(b) for d, b in zip(dbs, bs)],
                 dbias)
 

@@ -126,32 +126,31 @@ class _GatherFirstLayer(torch.autograd.Function):
             dx = dz.mm(W).view(xshape)
         from sheeprl_prey_amd.ops import sidestream as ss
 
-        if ss.active(dz.device) and ops._SIDE_LIN and ctx.needs_input_grad[2]:
-            # inside a side-stream scope (the world-model backward): parameter gradients beside the data chain
-            with ss.on_side(dz.device, dz, x2, idx2):
-                dW, dbias = _GatherFirstLayer._param_grads(ctx, dz, x2, idx2)
-            ss.mark_main(dW)
-            if dbias is not None:
-                ss.mark_main(dbias)
+        meta = (ctx.meta, tuple(ctx.needs_input_grad))
+        if ss.active(dz.device) and ctx.needs_input_grad[2]:
+            # inside a deferral scope (the world-model backward): parameter gradients beside the scan backward
+            shapes = [tuple(W.shape), (N,) if has_bias and ctx.needs_input_grad[3] else None]
+            dW, dbias = ss.param_grads(dz.device, lambda outs: _GatherFirstLayer._param_grads(meta, dz, x2, idx2, outs),
+                                       shapes, dz, x2, idx2)
         else:
-            dW, dbias = _GatherFirstLayer._param_grads(ctx, dz, x2, idx2)
+            dW, dbias = _GatherFirstLayer._param_grads(meta, dz, x2, idx2)
         return (dx, None, dW, dbias, dg if ctx.needs_input_grad[4] else None, db if ctx.needs_input_grad[5] else None,
                 None, None, None, None, None, None)
 
     @staticmethod
-    def _param_grads(ctx, dz, x2, idx2):
-        act, use_ln, has_bias, xshape, G, off, n_onehot = ctx.meta
+    def _param_grads(meta, dz, x2, idx2, out=None):
+        (act, use_ln, has_bias, xshape, G, off, n_onehot), needs = meta
         dW = dbias = None
-        if ctx.needs_input_grad[2] and ops.wgrad_ok(dz):
+        if needs[2] and ops.wgrad_ok(dz):
             # one-hot columns scattered, the dense tail by the split-K kernel, the bias sum on the side (wgrad.hip)
-            want_b = has_bias and ctx.needs_input_grad[3]
+            want_b = has_bias and needs[3]
             if x2.shape[1] > n_onehot and ops.wgrad_onehot_ok(dz, G, n_onehot):
-                dW, dbias = ops.wgrad(dz, x2[:, n_onehot:], onehot=(idx2, G, off, n_onehot), bias=want_b)
+                dW, dbias = ops.wgrad(dz, x2[:, n_onehot:], onehot=(idx2, G, off, n_onehot), bias=want_b, out=out)
             else:
-                dW, dbias = ops.wgrad(dz, x2, bias=want_b)
-        elif ctx.needs_input_grad[2]:
+                dW, dbias = ops.wgrad(dz, x2, bias=want_b, out=out)
+        elif needs[2]:
             dW = dz.t().mm(x2)  # x2 may be row-strided (a view into the trajectory buffer): mm takes the stride
-        if has_bias and ctx.needs_input_grad[3] and dbias is None:
+        if has_bias and needs[3] and dbias is None:
             dbias = ops._ext().colsum(dz)
         return dW, dbias
 

@@ -29,6 +29,7 @@ from typing import Tuple
 import torch
 from torch import Tensor
 
+from sheeprl_prey_amd.ops import sidestream
 from sheeprl_prey_amd.ops.reference import ACTS
 
 
@@ -170,6 +171,7 @@ class RSSMScanFn(torch.autograd.Function):
         p2b = torch.empty_like(p2g)
         pgg = torch.empty(T, gg, 3 * H, device=dev, dtype=f32)
         pgb = torch.empty_like(pgg)
+        sidestream.flush(dev)
         sk = _use_skinny(B, H)
         if sk:  # the adjoint GEMMs stream W^T: one transposed copy of each weight per backward
             WzT, WgT, W1T, W2T = (Wz.t().contiguous(), Wg.t().contiguous(), W1.t().contiguous(),
@@ -283,6 +285,7 @@ class RSSMScan4Fn(torch.autograd.Function):
         bwd = [WzT, Wg.t().contiguous(), W1.t().contiguous(), W2.transpose(1, 2).contiguous(), dpost,
                dmixed, DH, dlog, dv, du, dgx, dx, e(B, H + D), e(B, H), p1g, p1b, pgg, pgb, p2g, p2b]
         C.scan4_bwd(fwd + bwd, ctx.dims, ctx.fl)
+        sidestream.flush(dev)
         cat, zm, hs, v = fwd[16], fwd[17], fwd[24], fwd[26]
         TB = T * B
         dWz = dx.reshape(TB, D).t().mm(zm.reshape(TB, S))
@@ -377,6 +380,8 @@ class RSSMPersistFn(torch.autograd.Function):
                dx, p1g, p1b, pgg, pgb, p2g, p2b, e(T, B, 3 * H), e(T, H // 16, 16, 2)]
         _scan_health_word(dev)
         C.scanp_bwd(fwd + bwd, ctx.dims, ctx.fl)
+        # the queued decoder / head parameter gradients run beside the scan backward (ops/sidestream.py)
+        sidestream.flush(dev)
         cat, zm, hs, v = fwd[17], fwd[18], fwd[25], fwd[27]
         TB = T * B
         dWz = dx.reshape(TB, D).t().mm(zm.reshape(TB, S))
