@@ -21,6 +21,7 @@ bool launch_ln_act_bwd(const float*, int, const float*, int, float*, int, const 
 void launch_colsum2(const float*, const float*, float*, float*, int, int, int, hipStream_t);
 void launch_colsum1(const float*, int, float*, int, int, hipStream_t);
 void set_colsum_workspace(float*, int64_t, int*, int64_t);
+void set_colsum_side_stream(hipStream_t);
 void launch_cartpole_step(float*, int*, float*, const int64_t*, const float*, float*, float*, float*, float*, float*, float*,
                           float*, int, int, hipStream_t);
 void launch_rssm_mask_fwd(const float*, int, const float*, const float*, const float*, float*, int, float*, int, int, int,
@@ -1178,6 +1179,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_act_bwd_into", &ln_act_bwd_into);
   m.def("ln_bwd_grid", &ln_bwd_grid_py);
   m.def("set_colsum_workspace", &set_colsum_workspace_py);
+  m.def("set_colsum_side_stream", [](int64_t st) { set_colsum_side_stream(reinterpret_cast<hipStream_t>(st)); });
   m.def("ln_gru_bwd_grid", &ln_gru_bwd_grid_py);
   m.def("ln_gru_fwd_into", &ln_gru_fwd_into);
   m.def("ln_gru_bwd_into", &ln_gru_bwd_into, pybind11::arg("x"), pybind11::arg("h"), pybind11::arg("ldh"), pybind11::arg("gamma"),

@@ -798,38 +798,63 @@ static void launch_zero2(float* a, float* b, int n, hipStream_t st) {
 
 // Workspace + ticket counters of colsum_t_kernel (set once per process by ops.init_reduce_workspace on the device
 // it trains on; until then - or on another device - the zero kernel + atomic form runs).  Launches take rotating
-// slices so launches close together (e.g. on a side stream) never share one.
+// slices so launches close together never share one, and the pool is split in two halves by stream: launches on
+// the registered side stream (ops/sidestream.py: parameter gradients beside the scan backward) rotate through the
+// second half, so a side launch can never share a slice with a main-stream launch running at the same time, however
+// often either cursor wraps.
 static float* g_cs_ws = nullptr;
 static int* g_cs_cnt = nullptr;
-static int64_t g_cs_ws_n = 0, g_cs_cnt_n = 0, g_cs_ws_cur = 0, g_cs_cnt_cur = 0;
+static int64_t g_cs_ws_n = 0, g_cs_cnt_n = 0, g_cs_ws_cur[2] = {0, 0}, g_cs_cnt_cur[2] = {0, 0};
 static int g_cs_dev = -1;
+static hipStream_t g_cs_side = nullptr;
 
 void set_colsum_workspace(float* ws, int64_t ws_n, int* cnt, int64_t cnt_n) {
+  // the cursors survive a re-init with the same buffers (captured graphs keep their slices; a reset would hand
+  // a live slice out again)
+  if (ws != g_cs_ws || cnt != g_cs_cnt) g_cs_ws_cur[0] = g_cs_ws_cur[1] = g_cs_cnt_cur[0] = g_cs_cnt_cur[1] = 0;
   g_cs_ws = ws;
   g_cs_ws_n = ws_n;
   g_cs_cnt = cnt;
   g_cs_cnt_n = cnt_n;
-  g_cs_ws_cur = g_cs_cnt_cur = 0;
   g_cs_dev = -1;
   if (ws != nullptr) (void)hipGetDevice(&g_cs_dev);
+}
+
+void set_colsum_side_stream(hipStream_t st) { g_cs_side = st; }
+
+static int colsum_S2(int rows, int G) {
+  const int Rg = cdiv(rows, G > 0 ? G : 1);
+  int S = cdiv(Rg, 64);
+  if (S > 32) S = 32;
+  if (S < 1) S = 1;
+  return S;
+}
+
+// slice sizes of one ticket launch; false when the workspace is absent / on another device / too small
+static bool colsum_ticket_fits(int N, int G, int S, int64_t& need, int64_t& nc) {
+  if (g_cs_ws == nullptr) return false;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != g_cs_dev) return false;
+  const int nx = cdiv(N, 64);
+  need = S > 1 ? 2LL * S * G * N : 0;
+  nc = S > 1 ? (int64_t)G * nx : 0;
+  return need <= g_cs_ws_n / 2 && nc <= g_cs_cnt_n / 2;
 }
 
 // true: launched the ticket form (out written directly, no zeroing needed)
 static bool colsum_ticket(const float* pa, const float* pb, int ld, float* oa, float* ob, int rows, int N, int G, int S,
                           hipStream_t st) {
-  if (g_cs_ws == nullptr) return false;
-  int dev = -1;
-  if (hipGetDevice(&dev) != hipSuccess || dev != g_cs_dev) return false;
-  const int nx = cdiv(N, 64);
-  const int64_t need = S > 1 ? 2LL * S * G * N : 0, nc = S > 1 ? (int64_t)G * nx : 0;
-  if (need > g_cs_ws_n || nc > g_cs_cnt_n) return false;
-  if (g_cs_ws_cur + need > g_cs_ws_n) g_cs_ws_cur = 0;
-  if (g_cs_cnt_cur + nc > g_cs_cnt_n) g_cs_cnt_cur = 0;
-  float* ws = g_cs_ws + g_cs_ws_cur;
-  int* cnt = g_cs_cnt + g_cs_cnt_cur;
-  g_cs_ws_cur += (need + 63) / 64 * 64;
-  g_cs_cnt_cur += (nc + 63) / 64 * 64;
-  hipLaunchKernelGGL(colsum_t_kernel, dim3(nx, G, S), dim3(256), 0, st, pa, pb, ld, oa, ob, rows, N, G, ws, cnt);
+  int64_t need, nc;
+  if (!colsum_ticket_fits(N, G, S, need, nc)) return false;
+  const int h = (g_cs_side != nullptr && st == g_cs_side) ? 1 : 0;
+  const int64_t wsh = g_cs_ws_n / 2, cnh = g_cs_cnt_n / 2;
+  if (g_cs_ws_cur[h] + need > wsh) g_cs_ws_cur[h] = 0;
+  if (g_cs_cnt_cur[h] + nc > cnh) g_cs_cnt_cur[h] = 0;
+  float* ws = g_cs_ws + h * wsh + g_cs_ws_cur[h];
+  int* cnt = g_cs_cnt + h * cnh + g_cs_cnt_cur[h];
+  g_cs_ws_cur[h] += (need + 63) / 64 * 64;
+  g_cs_cnt_cur[h] += (nc + 63) / 64 * 64;
+  hipLaunchKernelGGL(colsum_t_kernel, dim3(cdiv(N, 64), G, S), dim3(256), 0, st, pa, pb, ld, oa, ob, rows, N, G, ws, cnt);
   return true;
 }
 
@@ -852,12 +877,9 @@ static void launch_colsum2_nz(const float* pa, const float* pb, float* oa, float
 }
 
 void launch_colsum2(const float* pa, const float* pb, float* oa, float* ob, int rows, int N, int G, hipStream_t st) {
-  // ticket form (one launch), else zero kernel + one atomic reduction kernel (graph-capturable); ~64 partial rows
-  // per split
-  const int Rg = cdiv(rows, G > 0 ? G : 1);
-  int S = cdiv(Rg, 64);
-  if (S > 32) S = 32;
-  if (S < 1) S = 1;
+  // ticket form (one launch, deterministic), else zero kernel + one atomic reduction kernel (graph-capturable); ~64
+  // partial rows per split
+  const int S = colsum_S2(rows, G);
   if (colsum_ticket(pa, pb, N, oa, ob, rows, N, G, S, st)) return;
   launch_zero2(oa, ob, G * N, st);
   hipLaunchKernelGGL(colsum2_kernel, dim3(cdiv(N, 64), G, S), dim3(256), 0, st, pa, pb, oa, ob, rows, N, G);
@@ -877,9 +899,13 @@ bool launch_ln_act_bwd(const float* x, int ldx, const float* dy, int lddy, float
     const bool al16 = ((uintptr_t)x | (uintptr_t)dy | (uintptr_t)dx | (uintptr_t)gamma | (uintptr_t)beta) % 16 == 0;
     if ((G == 1 || (g_ln_vec_groups && (G == 2 || G == 4) && M % G == 0)) && N % 4 == 0 && ldx % 4 == 0 &&
         lddy % 4 == 0 && lddx % 4 == 0 && al16 && (gamma != nullptr) == (beta != nullptr) && maxv <= 16) {
-      float* za = (gamma && dgamma) ? dgamma : nullptr;
-      float* zb = (gamma && dgamma) ? dbeta : nullptr;
-#define F4(NV) if (maxv == 4 * NV) { SRL_ACT_SPECIALIZE(act, hipLaunchKernelGGL((ln_wave4_bwd_kernel<NV, ACTC>), dim3(grid), dim3(256), 0, st, x, ldx, dy, lddy, dx, lddx, gamma, beta, mean, rstd, pg, pb, M, N, act, za, zb, G)); goto reduce_zeroed; }
+      // the deterministic one-launch ticket reduction when its workspace is set (no zeroing needed); else the LN
+      // kernel zeroes dgamma / dbeta itself and the atomic reduction follows
+      int64_t tneed, tnc;
+      const bool tk = gamma && dgamma && colsum_ticket_fits(N, G, colsum_S2(grid * G, G), tneed, tnc);
+      float* za = (gamma && dgamma && !tk) ? dgamma : nullptr;
+      float* zb = (gamma && dgamma && !tk) ? dbeta : nullptr;
+#define F4(NV) if (maxv == 4 * NV) { SRL_ACT_SPECIALIZE(act, hipLaunchKernelGGL((ln_wave4_bwd_kernel<NV, ACTC>), dim3(grid), dim3(256), 0, st, x, ldx, dy, lddy, dx, lddx, gamma, beta, mean, rstd, pg, pb, M, N, act, za, zb, G)); if (tk) goto reduce; goto reduce_zeroed; }
       F4(1) F4(2) F4(4)
 #undef F4
     }

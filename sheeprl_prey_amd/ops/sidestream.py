@@ -61,6 +61,10 @@ def _stream(i: int) -> "torch.cuda.Stream":
     s = _streams.get(i)
     if s is None:
         s = _streams[i] = torch.cuda.Stream(device=i)
+        from sheeprl_prey_amd import ops
+
+        # column-sum launches on this stream rotate through their own half of the ticket workspace (norm.hip)
+        ops._ext().set_colsum_side_stream(int(s.cuda_stream))
     return s
 
 
