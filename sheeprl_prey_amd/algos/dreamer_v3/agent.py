@@ -296,27 +296,27 @@ class RSSM(nn.Module):
         return imagined_prior, recurrent_state
 
     # ---- MI355X imagination: buffer-resident no-grad rollout ---------------------------
-    _actor_tail_ok = os.environ.get("SRL_ACTOR_TAIL", "1") != "0"  # A/B switch of the fused rollout actor tail
+    _actor_tail_ok = True  # the fused rollout actor tail (tests toggle it)
     # merged h_{t+1} GEMM of the imagination step (every GEMM over h_{t+1} as one, 505 -> 463 dispatches per Atari
     # step).  Untuned it was slower (313.0 / 313.5 vs 323.3 env-steps/s; profiles/r4_imag_merge.md); with its shapes
     # in the committed TunableOp results it is equal (323.0 vs 323.2 mean of three interleaved 150-step runs,
     # profiles/r4_merge_ab.md), so the rollouts use it by default for recurrent states up to 1024 wide; the continuous
     # rollout (imagine_cont.py) measured 123.6 / 123.7 vs 123.3 / 123.6 env-steps/s with / without.  For the XL state
     # (deter 4096) the unmerged K = Hd + D GRU projection is a ~150 TF/s library GEMM and splitting it costs more
-    # than the launches saved (47.8 / 47.6 vs 48.2 / 48.3 env-steps/s, merged shapes tuned).  SRL_IMAG_MERGE /
-    # SRL_IMAG_MERGE_CONT = 1 / 0 force it on / off.
-    _merge_h_ok = os.environ.get("SRL_IMAG_MERGE", "auto")
-    _merge_h_cont_ok = os.environ.get("SRL_IMAG_MERGE_CONT", os.environ.get("SRL_IMAG_MERGE", "auto"))
+    # than the launches saved (47.8 / 47.6 vs 48.2 / 48.3 env-steps/s, merged shapes tuned).  Tests force it with
+    # True / False.
+    _merge_h_ok = "auto"
+    _merge_h_cont_ok = "auto"
     MERGE_MAX_H = 1024
 
     @staticmethod
     def merge_enabled(flag, Hd: int) -> bool:
-        """The SRL_IMAG_MERGE policy: "1" on, "0" off, "auto" (default) for recurrent states <= MERGE_MAX_H."""
+        """The merge policy: "1" / True on, "0" / False off, "auto" (default) for recurrent states <= MERGE_MAX_H."""
         if flag is True or flag is False:
             return flag
         return flag == "1" or (flag == "auto" and Hd <= RSSM.MERGE_MAX_H)
     # one-launch prior head (prior_head.hip; used on the merged path): 30.6 us vs ~28 us for LayerNorm + GEMM + sampler
-    _prior_head_ok = os.environ.get("SRL_PRIOR_HEAD", "1") != "0"
+    _prior_head_ok = True
 
     def imagine_fast_ok(self, actor) -> bool:
         gru = self.recurrent_model.rnn

@@ -100,13 +100,13 @@ class DreamerV3Trainer:
         self.actions_dim = list(actions_dim)
         self.target_flat = flatten_like(target_critic, critic_optimizer)
         # discrete fast path: record the rollout's actor forward and keep the imagination critic forward's
-        # graph, so the actor / critic losses skip their second forwards (A/B switch SRL_REUSE_FWD=0)
-        self.reuse_forwards = os.environ.get("SRL_REUSE_FWD", "1") != "0"
-        # first layers over the one-hot posteriors / priors as row gathers (ops/onehot.py; A/B switch SRL_ONEHOT=0)
-        self.onehot_heads = os.environ.get("SRL_ONEHOT", "1") != "0"
+        # graph, so the actor / critic losses skip their second forwards (attribute: tests toggle it)
+        self.reuse_forwards = True
+        # first layers over the one-hot posteriors / priors as row gathers (ops/onehot.py)
+        self.onehot_heads = True
         # continuous actors: the imagined rollout + its backward as one hand-written autograd node
-        # (algos/dreamer_v3/imagine_cont.py); 0 = the reference-shaped eager loop
-        self.cont_fast = os.environ.get("SRL_CONT_FAST", "1") != "0"
+        # (algos/dreamer_v3/imagine_cont.py); False = the reference-shaped eager loop
+        self.cont_fast = True
         self._st: Dict[str, Any] = {}
         self._gather_buf = None
         # teacher forcing of the eager oracle (tests/test_dv3_step_oracle_gpu.py): {"posteriors" [T,B,S],
@@ -152,8 +152,7 @@ class DreamerV3Trainer:
         (``sample_into``) and the step replayed - None (caller samples + calls ``train_step``) otherwise."""
         g = self.seg if self.segmented else self.graphed
         ready = g.graphs is not None if self.segmented else g.graph is not None
-        if (not ready or g.static_in is None or not hasattr(rb, "sample_into")
-                or os.environ.get("SRL_FUSED_SAMPLE", "1") == "0"):
+        if not ready or g.static_in is None or not hasattr(rb, "sample_into"):
             return None
         if not rb.sample_into(g.static_in, batch_size, sequence_length):
             return None

@@ -203,7 +203,7 @@ class NatureCNN(CNN):
         x = cnn_forward(self.model, x, input_dim=x.shape[-3:], output_dim=(-1,))
         return F.relu(self.fc(x)) if self.fc is not None else x
 
-    training_eager = os.environ.get("SRL_NATCNN", "1") == "0"  # stock conv path (A/B measurements)
+    training_eager = False  # True: the stock conv path (tests toggle it)
 
 
 class LayerNormGRUCell(nn.Module):

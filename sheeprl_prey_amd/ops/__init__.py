@@ -71,7 +71,7 @@ def _act_code(act: str) -> int:
 
 
 # =============================================================== Linear (library GEMMs, column-sum bias grad)
-_LIN2D = os.environ.get("SRL_LIN2D", "1") != "0"  # A/B switch
+_LIN2D = True  # row-strided 2-D linear forward (tests toggle it)
 
 
 def _lin2d(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
@@ -89,7 +89,7 @@ def _lin2d(x: Tensor, weight: Tensor, bias: Optional[Tensor]) -> Tensor:
 
 
 # =============================================================== tall-layer weight gradients (wgrad.hip)
-WGRAD_MIN_ROWS = int(os.environ.get("SRL_WGRAD_MIN_ROWS", "4096"))  # 0 disables (A/B switch)
+WGRAD_MIN_ROWS = 4096  # below this many rows the library GEMM takes the weight gradient (0 disables the kernel)
 WGRAD_MAX_TILES = 32  # dense parts with more 128 x 128 output tiles go to the library GEMM
 
 
@@ -181,6 +181,7 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)  # the leaves a deferred weight gradient is assigned to (ops/sidestream.py)
         return _lin2d(x, weight, bias)
 
     @staticmethod
@@ -195,9 +196,8 @@ class _Linear(torch.autograd.Function):
         if ss.active(gy.device) and ctx.needs_input_grad[1]:
             # inside a deferral scope (the world-model backward): the parameter gradients leave the data-gradient
             # chain and run beside the scan backward (ops/sidestream.py)
-            shapes = [tuple(w.shape), (w.shape[0],) if ctx.has_bias and ctx.needs_input_grad[2] else None]
             meta = (tuple(ctx.needs_input_grad), ctx.has_bias)
-            dw, db = ss.param_grads(gy.device, lambda outs: _Linear._param_grads(meta, g2, x, outs), shapes, g2, x)
+            dw, db = ss.param_grads(gy.device, lambda: _Linear._param_grads(meta, g2, x), ctx.params, g2, x)
             return dx, dw, db
         dw, db = _Linear._param_grads((tuple(ctx.needs_input_grad), ctx.has_bias), g2, x)
         return dx, dw, db
@@ -743,7 +743,7 @@ def skinny_nt(A: Tensor, W: Tensor, out: Tensor, add: Optional[Tensor] = None) -
     Z = A.shape[0] if A.dim() == 3 else 1
     need = C.skinny_workspace(W.shape[-2], A.shape[-1], Z)
     part = torch.empty(need, device=A.device, dtype=torch.float32) if need else None
-    C.skinny_nt(A, W, out, add, part, _skinny_tickets(A.device, Z * (W.shape[-2] // 128)) if need else None)
+    C.skinny_nt(A, W, out, add, part)
     return True
 
 
@@ -754,8 +754,6 @@ _reduce_ws: dict = {}
 
 
 def init_reduce_workspace(device, floats: int = 1 << 22, counters: int = 1 << 16) -> bool:
-    if os.environ.get("SRL_COLSUM_TICKET", "1") == "0":  # A/B: the two-launch (zero + atomic) column sums
-        return False
     if not (torch.cuda.is_available() and native_available()) or torch.cuda.is_current_stream_capturing():
         return False
     device = torch.device(device)
@@ -772,27 +770,6 @@ def init_reduce_workspace(device, floats: int = 1 << 22, counters: int = 1 << 16
             _reduce_ws[device.index] = (ws, cnt)  # never freed: a graph captured with it may replay at any time
         _ext().set_colsum_workspace(ws, cnt)
     return True
-
-
-# Ticket counters of skinny_nt's in-launch split combine: one zeroed int32 pool per device, created on first use
-# (the first calls run eagerly, before any step is captured), handed out in rotating slices so that launches close
-# together never share a counter; each launch's last-arriving workgroup returns its counters to zero.
-_SKINNY_POOL = 1 << 16
-_skinny_pool: dict = {}
-
-
-def _skinny_tickets(device, n: int) -> Optional[Tensor]:
-    key = device.index if device.index is not None else torch.cuda.current_device()
-    pool = _skinny_pool.get(key)
-    if pool is None:
-        if torch.cuda.is_current_stream_capturing():
-            return None  # never allocate the pool inside a capture (graph-private memory): separate reduce launch
-        pool = _skinny_pool[key] = [torch.zeros(_SKINNY_POOL, device=device, dtype=torch.int32), 0]
-    if pool[1] + n > _SKINNY_POOL:
-        pool[1] = 0
-    sl = pool[0][pool[1]:pool[1] + n]
-    pool[1] += (n + 63) // 64 * 64  # slices start on separate 256-byte lines
-    return sl
 
 
 # =============================================================== P2E disagreement (K20)

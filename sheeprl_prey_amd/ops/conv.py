@@ -29,7 +29,7 @@ ENABLED = True  # A/B switch: False routes the stacks through the per-layer modu
 # too few output rows to fill the chip (E4: 16 rows per frame) and a single workgroup walks all of K:
 # no-grad calls there take the split-K small-batch stack (csrc/conv_small.hip, ``encoder_small``).
 MIN_FRAMES = 64
-SMALL_ENABLED = os.environ.get("SRL_SMALL_ENCODER", "1") != "0"  # A/B switch: False sends the small no-grad batches to the per-layer modules (MIOpen)
+SMALL_ENABLED = True  # False sends the small no-grad batches to the per-layer modules (MIOpen; tests toggle it)
 
 
 def _C():
@@ -198,13 +198,10 @@ def encoder_small(stages, x: Tensor, scale: float = 1.0) -> Tensor:
                                    [act_code(ln.act) for ln in lns], float(scale))
 
 
-def _wgrad(C, P: Tensor, Q: Tensor, cb: int, w: Tensor) -> Tensor:
-    """Decoder weight gradient: in line, or deferred beside the scan backward inside a deferral scope
-    (``ops/sidestream.py``; written straight into the preallocated gradient)."""
-    dev = P.device
-    if not ss.active(dev):
-        return C.conv_wgrad(P, Q, cb)
-    return ss.param_grads(dev, lambda outs: (C.conv_wgrad(P, Q, cb, outs[0]),), [tuple(w.shape)], P, Q)[0]
+def _wgrad(C, P: Tensor, Q: Tensor, cb: int, w: Tensor) -> Optional[Tensor]:
+    """Decoder weight gradient of parameter ``w``: in line, or (inside a deferral scope) queued to run beside the
+    scan backward and None returned (``ops/sidestream.py`` assigns it to ``w.grad``)."""
+    return ss.param_grads(P.device, lambda: (C.conv_wgrad(P, Q, cb),), [w], P, Q)[0]
 
 
 # ---------------------------------------------------------------------------------- decoder
@@ -234,6 +231,7 @@ class DecoderConvFn(torch.autograd.Function):
         saved.append(p)
         ctx.save_for_backward(*saved, *params)
         ctx.meta, ctx.L = meta, L
+        ctx.wparams = params[:L + 1]  # the conv weights (leaves) a deferred weight gradient is assigned to
         return out
 
     @staticmethod
@@ -260,7 +258,7 @@ class DecoderConvFn(torch.autograd.Function):
         cout_last = ws[L].shape[1]
         # the weight gradients leave the critical path (data gradients -> scan backward -> encoder): inside the
         # world-model backward they are queued and run beside the scan backward (ops/sidestream.py)
-        dws[L] = _wgrad(C, p_last, q, cout_last, ws[L])
+        dws[L] = _wgrad(C, p_last, q, cout_last, ctx.wparams[L])
         wp = C.conv_pack_down(ws[L], q.shape[3])
         _, zp, mp, rp = acts[4 * (L - 1):4 * L]
         dz = C.conv_gemm(0, q, wp, ws[L].shape[0], 1, gs[L - 1], bs[L - 1], 0.0, act[L - 1], False, zp, mp, rp,
@@ -269,7 +267,7 @@ class DecoderConvFn(torch.autograd.Function):
         for i in range(L - 1, -1, -1):
             p = acts[4 * i]
             cout = ws[i].shape[1]
-            dws[i] = _wgrad(C, p, dz, cout, ws[i])
+            dws[i] = _wgrad(C, p, dz, cout, ctx.wparams[i])
             wp = C.conv_pack_down(ws[i], cout)
             cin = ws[i].shape[0]
             if i > 0:

@@ -77,9 +77,9 @@ int scan4_fwd_lds(int, int, int, int);
 int scan4_bwd_lds(int, int, int, int);
 void launch_scanp_fwd(const srl::scanp::PP&, hipStream_t);
 void launch_scanp_bwd(const srl::scanp::PP&, hipStream_t);
-bool scanp_supported(int, int, int, int, int, int, int);
+bool scanp_supported(int, int, int, int, int, int);
 int scanp_sync_words();
-int scanp_fwd_grid(int, int, int, int);
+int scanp_fwd_grid(int, int, int);
 int scanp_bwd_grid(int, int, int, int);
 
 namespace {
@@ -606,13 +606,6 @@ int64_t scan4_lds(int64_t S, int64_t D, int64_t H, int64_t hid) {
 
 // ------------------------------------------------------------------ persistent RSSM posterior scan
 // tensors (fixed order, see ops/rssm.py RSSMPersistFn): 33 forward buffers + the int32 sample table and hand-off
-// forward form of the persistent scan (rssm_persist.hip PP::ag): 1 = "A owns the gates" (SRL_SCANP_AG=1)
-int g_scanp_ag = [] {
-  const char* e = getenv("SRL_SCANP_AG");
-  return e ? atoi(e) : 0;
-}();
-void set_scanp_ag(int64_t v) { g_scanp_ag = (int)v; }
-
 // counter block, then 20 backward ones; an undefined / empty tensor is a null pointer.
 srl::scanp::PP scanp_params(const std::vector<torch::Tensor>& ts, const std::vector<int64_t>& ints,
                             const std::vector<double>& fl) {
@@ -621,8 +614,7 @@ srl::scanp::PP scanp_params(const std::vector<torch::Tensor>& ts, const std::vec
   p.T = ints[0]; p.B = ints[1]; p.S = ints[2]; p.D = ints[3]; p.H = ints[4]; p.hid = ints[5]; p.C = ints[6];
   p.act1 = ints[7]; p.act2 = ints[8];
   p.alpha = fl[0]; p.eps1 = fl[1]; p.epsg = fl[2]; p.eps2 = fl[3];
-  p.ag = g_scanp_ag;
-  TORCH_CHECK(scanp_supported(p.B, p.S, p.D, p.H, p.hid, p.C, p.ag), "scanp: unsupported shape B=", p.B, " S=", p.S, " D=", p.D,
+  TORCH_CHECK(scanp_supported(p.B, p.S, p.D, p.H, p.hid, p.C), "scanp: unsupported shape B=", p.B, " S=", p.S, " D=", p.D,
               " H=", p.H, " hid=", p.hid, " C=", p.C);
   auto P = [&](size_t i) -> float* {
     if (i >= ts.size() || !ts[i].defined() || ts[i].numel() == 0) return nullptr;
@@ -667,6 +659,7 @@ srl::scanp::PP scanp_params(const std::vector<torch::Tensor>& ts, const std::vec
 
 long long* g_scanp_prof = nullptr;  // debug phase timestamps (set_scanp_prof)
 unsigned* g_scanp_health = nullptr;  // sticky timeout word shared by every launch (set_scanp_health)
+
 unsigned g_scanp_spin = 0;           // spin bound of the hand-off waits (0 = kernel default; tests force timeouts)
 
 void set_scanp_health(c10::optional<torch::Tensor> buf, int64_t spin_max) {
@@ -803,7 +796,7 @@ torch::Tensor tn_head_sample_bwd(torch::Tensor loc, torch::Tensor scale, torch::
 std::vector<int64_t> scanp_info(int64_t B, int64_t S, int64_t D, int64_t H, int64_t hid, int64_t C) {
   // [supported, sync words, error word index, forward grid, backward grid]
   const int words = scanp_sync_words();
-  return {scanp_supported(B, S, D, H, hid, C, g_scanp_ag) ? 1 : 0, words, words - 32, scanp_fwd_grid(S, H, hid, g_scanp_ag),
+  return {scanp_supported(B, S, D, H, hid, C) ? 1 : 0, words, words - 32, scanp_fwd_grid(S, H, hid),
           scanp_bwd_grid(S, D, H, hid)};
 }
 
@@ -1197,7 +1190,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scanp_fwd", &scanp_fwd);
   m.def("scanp_bwd", &scanp_bwd);
   m.def("scanp_info", &scanp_info);
-  m.def("set_scanp_ag", &set_scanp_ag);  // persistent-scan forward form (0 = A/B, 1 = A owns the gates)
   m.def("truncnorm_rsample_fwd", &truncnorm_rsample_fwd);
   m.def("truncnorm_rsample_bwd", &truncnorm_rsample_bwd);
   m.def("truncnorm_logprob_fwd", &truncnorm_logprob_fwd);

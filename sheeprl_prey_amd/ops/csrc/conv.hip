@@ -25,9 +25,6 @@
 #include "conv.h"
 #include <string>
 
-#ifndef NARROW_DEFAULT
-#define NARROW_DEFAULT 1  // measured: 128x64 tiles for 64 channels -1.4% on the stack, 128x32 no gain
-#endif
 
 namespace srl {
 namespace conv {
@@ -567,14 +564,13 @@ struct EpiPlain : EpiPlainP {  // out = acc + bias[c] + c0 for c < Nreal; NHWC (
 
 // --------------------------------------------------------------------------- GEMM main loops
 // Tile BM x BN, WM x WN waves of (TM*32) x (TN*32); 64*WM*WN threads; one LDS stage + register
-// prefetch of the next stage.
-// DB: two LDS stages - the next stage's registers are stored into the other buffer right after this
-// stage's MFMAs, so each K stage needs ONE workgroup barrier instead of two (A/B: SRL_CONV_DB).
-template <int BM, int BN, int WM, int WN, class LA, class LB, class EP, class RM, bool DB = false>
+// prefetch of the next stage (a double-buffered form with one barrier per stage measured no gain:
+// profiles/r4_conv_ab.md, profiles/r4_conv_db_wide.md; removed).
+template <int BM, int BN, int WM, int WN, class LA, class LB, class EP, class RM>
 __global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep, RM rm, int K, int ncls, int remap) {
   constexpr int NTH = 64 * WM * WN, TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(TM >= 1 && TN >= 1 && TM * WM * 32 == BM && TN * WN * 32 == BN, "bad tile");
-  constexpr int LDS_MAIN = (DB ? 2 : 1) * (BM + BN) * LDK;
+  constexpr int LDS_MAIN = (BM + BN) * LDK;
   constexpr int LDS_EPI = WM * 32 * (BN + 4) > 2 * WM * WN * BN ? WM * 32 * (BN + 4) : 2 * WM * WN * BN;
   __shared__ float lds[LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI];
   float* As = lds;
@@ -626,41 +622,18 @@ __global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep,
           for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q], b[j][q], acc[i][j], 0, 0, 0);
     }
   };
-  if constexpr (DB) {
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    __syncthreads();
     la.store(ra, As);
     lb.store(rb, Bs);
     __syncthreads();
-    int buf = 0;
-    for (int k0 = 0; k0 < K; k0 += BK) {
-      const bool more = k0 + BK < K;
-      if (more) {
-        la.load(k0 + BK, ra);
-        lb.load(k0 + BK, rb);
-      }
-      const float* Ac = lds + buf * (BM + BN) * LDK;
-      stage_mfma(Ac, Ac + BM * LDK);
-      if (more) {  // the other buffer was last read in the previous stage, which every wave has left (barrier)
-        float* An = lds + (buf ^ 1) * (BM + BN) * LDK;
-        la.store(ra, An);
-        lb.store(rb, An + BM * LDK);
-      }
-      __syncthreads();
-      buf ^= 1;
+    if (k0 + BK < K) {
+      la.load(k0 + BK, ra);
+      lb.load(k0 + BK, rb);
     }
-  } else {
-    for (int k0 = 0; k0 < K; k0 += BK) {
-      __syncthreads();
-      la.store(ra, As);
-      lb.store(rb, Bs);
-      __syncthreads();
-      if (k0 + BK < K) {
-        la.load(k0 + BK, ra);
-        lb.load(k0 + BK, rb);
-      }
-      stage_mfma(As, Bs);
-    }
-    __syncthreads();
+    stage_mfma(As, Bs);
   }
+  __syncthreads();
   ep.template run<BM, BN, TM, TN, WM, WN>(acc, f, m0, lds, rm);
 }
 
@@ -947,7 +920,7 @@ void launch(K kernel, dim3 grid, dim3 block, hipStream_t st, Args... args) {
 }
 }  // namespace
 
-template <int BM, int BN, int WM, int WN, bool DB, class LA, class RM>
+template <int BM, int BN, int WM, int WN, class LA, class RM>
 static void dispatch_epi(const LA& la, const Dense<BN, 64 * WM * WN>& lb, const ConvEpi& e, const RM& rm, int K, int mtiles,
                          int ncls, hipStream_t st) {
   dim3 block(64 * WM * WN);
@@ -956,37 +929,16 @@ static void dispatch_epi(const LA& la, const Dense<BN, 64 * WM * WN>& lb, const 
   if (e.mode == 0) {
     EpiLNAct ep;
     static_cast<EpiLNActP&>(ep) = e.ln;
-    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNAct, RM, DB>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNAct, RM>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
   } else if (e.mode == 1) {
     EpiLNBwd ep;
     static_cast<EpiLNBwdP&>(ep) = e.lb;
-    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNBwd, RM, DB>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNBwd, RM>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
   } else {
     EpiPlain ep;
     static_cast<EpiPlainP&>(ep) = e.pl;
-    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiPlain, RM, DB>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
+    launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiPlain, RM>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
   }
-}
-
-// Tile choice for the narrow (32 / 64 output channel) layers; SRL_CONV_NARROW bit 0: 128x64 (2x2
-// waves) for 64 channels, bit 1: 128x32 for 32 channels (A/B knob, read once).
-static int narrow_tiles() {
-  static const int v = [] {
-    const char* e = getenv("SRL_CONV_NARROW");
-    return e ? atoi(e) : NARROW_DEFAULT;
-  }();
-  return v;
-}
-
-// Double-buffered main loop (one barrier per K stage); SRL_CONV_DB bit 0: 128x32 tiles (32 channels), bit 1: 128x64
-// (64), bit 2: 128x96, bit 3: 128x128, bit 4: 128x192, bit 5: 64x256, bit 6: 64x384 (A/B knob, read once; default
-// off: profiles/r4_conv_ab.md for the narrow tiles)
-static int conv_db() {
-  static const int v = [] {
-    const char* e = getenv("SRL_CONV_DB");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
 }
 
 // Output-channel tiles: the workgroup tile spans the whole channel row (the LayerNorm epilogues need
@@ -998,38 +950,15 @@ static int conv_db() {
 //   512 / 768   64 x C, 1 x 8 waves (TM 2, TN 2 / 3; 512 threads keep the B-tile prefetch at 8 / 12
 //               float4 per thread; LDS 83 / 120 KB)
 //   1024        32 x C, 1 x 8 waves (TM 1, TN 4: no register spill; LDS 152 KB)
-#define SRL_CONV_TILES(X, ...)                                                                     \
+#define CONV_TILES(X, ...)                                                                         \
   switch (Nc) {                                                                                     \
-    case 32:                                                                                        \
-      if (conv_db() & 1) X<128, 32, 4, 1, true>(__VA_ARGS__);                                       \
-      else if (narrow_tiles() & 2) X<128, 32, 4, 1>(__VA_ARGS__);                                   \
-      else X<256, 32, 4, 1>(__VA_ARGS__);                                                           \
-      return true;                                                                                  \
-    case 64:                                                                                        \
-      if (conv_db() & 2) X<128, 64, 2, 2, true>(__VA_ARGS__);                                       \
-      else if (narrow_tiles() & 1) X<128, 64, 2, 2>(__VA_ARGS__);                                   \
-      else X<256, 64, 4, 1>(__VA_ARGS__);                                                           \
-      return true;                                                                                  \
-    case 96:                                                                                        \
-      if (conv_db() & 4) X<128, 96, 4, 1, true>(__VA_ARGS__);                                       \
-      else X<128, 96, 4, 1>(__VA_ARGS__);                                                           \
-      return true;                                                                                  \
-    case 128:                                                                                       \
-      if (conv_db() & 8) X<128, 128, 2, 2, true>(__VA_ARGS__);                                      \
-      else X<128, 128, 2, 2>(__VA_ARGS__);                                                          \
-      return true;                                                                                  \
-    case 192:                                                                                       \
-      if (conv_db() & 16) X<128, 192, 2, 2, true>(__VA_ARGS__);                                     \
-      else X<128, 192, 2, 2>(__VA_ARGS__);                                                          \
-      return true;                                                                                  \
-    case 256:                                                                                       \
-      if (conv_db() & 32) X<64, 256, 1, 4, true>(__VA_ARGS__);                                      \
-      else X<64, 256, 1, 4>(__VA_ARGS__);                                                           \
-      return true;                                                                                  \
-    case 384:                                                                                       \
-      if (conv_db() & 64) X<64, 384, 1, 4, true>(__VA_ARGS__);                                      \
-      else X<64, 384, 1, 4>(__VA_ARGS__);                                                           \
-      return true;                                                                                  \
+    case 32: X<256, 32, 4, 1>(__VA_ARGS__); return true;                                            \
+    case 64: X<128, 64, 2, 2>(__VA_ARGS__); return true;                                            \
+    case 96: X<128, 96, 4, 1>(__VA_ARGS__); return true;                                            \
+    case 128: X<128, 128, 2, 2>(__VA_ARGS__); return true;                                          \
+    case 192: X<128, 192, 2, 2>(__VA_ARGS__); return true;                                          \
+    case 256: X<64, 256, 1, 4>(__VA_ARGS__); return true;                                           \
+    case 384: X<64, 384, 1, 4>(__VA_ARGS__); return true;                                           \
     case 512: X<64, 512, 1, 8>(__VA_ARGS__); return true;                                           \
     case 768: X<64, 768, 1, 8>(__VA_ARGS__); return true;                                           \
     case 1024: X<32, 1024, 1, 8>(__VA_ARGS__); return true;                                         \
@@ -1045,7 +974,7 @@ bool conv_channels_supported(int Nc) {
 
 // DOWN: out grid (N, SH, SW) with Nc output channels, input Q NHWC (N, 2SH, 2SW, Cb); Cb is a
 // multiple of 32 or a power of two below 32
-template <int BM, int BN, int WM, int WN, bool DB = false>
+template <int BM, int BN, int WM, int WN>
 static void down_cfg(const float* Q, const float* Wp, int N, int SH, int SW, int Cb, const ConvEpi& e, hipStream_t st) {
   constexpr int NTH = 64 * WM * WN;
   const int M = N * SH * SW;
@@ -1060,16 +989,16 @@ static void down_cfg(const float* Q, const float* Wp, int N, int SH, int SW, int
   lb.W = Wp;
   lb.K = 16 * Cb;
   lb.cls_stride = 0;
-  dispatch_epi<BM, BN, WM, WN, DB>(la, lb, e, RowDown{0}, 16 * Cb, (M + BM - 1) / BM, 1, st);
+  dispatch_epi<BM, BN, WM, WN>(la, lb, e, RowDown{0}, 16 * Cb, (M + BM - 1) / BM, 1, st);
 }
 
 bool launch_conv_down(const float* Q, const float* Wp, int N, int SH, int SW, int Cb, int Nc, const ConvEpi& e,
                       hipStream_t st) {
   if (!(Cb % 32 == 0 || (Cb >= 4 && Cb < 32 && (Cb & (Cb - 1)) == 0))) return false;
-  SRL_CONV_TILES(down_cfg, Q, Wp, N, SH, SW, Cb, e, st)
+  CONV_TILES(down_cfg, Q, Wp, N, SH, SW, Cb, e, st)
 }
 
-template <int BM, int BN, int WM, int WN, bool DB = false>
+template <int BM, int BN, int WM, int WN>
 static void up_cfg(const float* P, const float* Wp, int N, int SH, int SW, int Ca, int Bp, const ConvEpi& e, hipStream_t st) {
   constexpr int NTH = 64 * WM * WN;
   const int M = N * SH * SW;
@@ -1084,7 +1013,7 @@ static void up_cfg(const float* P, const float* Wp, int N, int SH, int SW, int C
   lb.K = 4 * Ca;
   lb.cls_stride = (size_t)Bp * 4 * Ca;
   RowUp rm{ilog2(SH), ilog2(SW), 0};
-  dispatch_epi<BM, BN, WM, WN, DB>(la, lb, e, rm, 4 * Ca, (M + BM - 1) / BM, 4, st);
+  dispatch_epi<BM, BN, WM, WN>(la, lb, e, rm, 4 * Ca, (M + BM - 1) / BM, 4, st);
 }
 
 // UP: P NHWC (N, SH, SW, Ca) -> out grid (N, 2SH, 2SW) with Bp output channels (pack padding)
@@ -1092,14 +1021,8 @@ bool launch_conv_up(const float* P, const float* Wp, int N, int SH, int SW, int 
                     hipStream_t st) {
   if (Ca % 32 != 0) return false;
   const int Nc = Bp;
-  SRL_CONV_TILES(up_cfg, P, Wp, N, SH, SW, Ca, Bp, e, st)
+  CONV_TILES(up_cfg, P, Wp, N, SH, SW, Ca, Bp, e, st)
 }
-
-// SRL_WGRAD_REMAP=0: hardware workgroup order (A/B)
-static const bool g_wgrad_remap = [] {
-  const char* e = getenv("SRL_WGRAD_REMAP");
-  return !(e && e[0] == '0');
-}();
 
 template <int BM, int BN, int WM, int WN>
 static void wgrad_cfg(const float* P, const float* Q, float* slab, int S, int kper, int N, int SH, int SW, int Ca, int Cbp,
@@ -1117,7 +1040,8 @@ static void wgrad_cfg(const float* P, const float* Q, float* slab, int S, int kp
   lb.lSW = ilog2(SW);
   lb.M = M;
   dim3 grid(Ca / BM, 16 * Cbp / BN, S);
-  const int remap = g_wgrad_remap && (grid.x * grid.y * grid.z) % 8 == 0;
+  // XCD-ordered splits (profiles/r4_wgrad_remap_{on,off}.txt: Atari layers 1.165 -> 1.126 ms)
+  const int remap = (grid.x * grid.y * grid.z) % 8 == 0;
   hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN>), grid, dim3(NTH), 0, st, la, lb, slab, 16 * Cbp, Ca, kper, remap);
 }
 
@@ -1162,12 +1086,6 @@ static int num_cus() {
   return n;
 }
 
-// SRL_WGRAD_PLAN=0: the previous split rule (~512 workgroups whatever the residency)
-static const bool g_wgrad_rounds = [] {
-  const char* e = getenv("SRL_WGRAD_PLAN");
-  return !(e && e[0] == '0');
-}();
-
 // number of K splits (and pixels per split) for a WGRAD problem; slab = S * Ca * 16 * Cbp floats.
 // Rounds-aware: with T output tiles and R resident slots (occupancy x CUs) a launch of T * S workgroups runs
 // ceil(T * S / R) rounds of M / S pixels each, so its time goes as ceil(T S / R) / S: a grid just over a
@@ -1183,7 +1101,7 @@ void conv_wgrad_plan(int N, int SH, int SW, int Ca, int Cbp, int* S, int* kper) 
   int kp = (M + want - 1) / want;
   kp = ((kp + 31) / 32) * 32;
   if (kp < 1024) kp = 1024;
-  if (g_wgrad_rounds) {
+  {
     const int occ = wgrad_occ(BM, BN);
     const int R = occ * num_cus();
     const int smax = std::max(1, M / 1024);
@@ -1482,11 +1400,8 @@ __global__ __launch_bounds__(256) void up_last_mfma_kernel(const float* __restri
 }
 
 // final-layer form: 0 = MFMA (default: 96.6 vs 120.2 us at the Atari-100k shape, profiles/r4_up_last.json),
-// 1 = the VALU kernels below (SRL_UP_LAST=valu)
-static int g_up_last_form = [] {
-  const char* e = getenv("SRL_UP_LAST");
-  return (e && std::string(e) == "valu") ? 1 : 0;
-}();
+// 1 = the VALU kernels below (tests only: set_up_last_form)
+static int g_up_last_form = 0;
 void set_up_last_form(int f) { g_up_last_form = f; }
 
 bool launch_up_small(const float* P, const float* W, const float* bias, float c0, float* out, int N, int SH, int SW, int Ca,

@@ -16,9 +16,8 @@ void launch_moments(const float* x, int n, int r0, int r1, int r2, int r3, float
                     float om, float inv_max, float* low, float* high, float* inv, hipStream_t st);
 
 int skinny_plan(int N, int K, int Z, int* kc);
-void set_skinny_fused(int on);
 void launch_skinny_nt(const float* A, long lda, long sA, const float* W, long ldw, long sW, float* out, long ldo, long sO,
-                      const float* add, long ldadd, long sAdd, float* part, int* cnt, int M, int N, int K, int Z, hipStream_t st);
+                      const float* add, long ldadd, long sAdd, float* part, int M, int N, int K, int Z, hipStream_t st);
 void launch_sac_target(const float* obs, const float* act, const float* logp, const float* rew, const float* done,
                        const float* log_alpha, const float* W1, const float* b1, const float* W2, const float* b2,
                        const float* W3, const float* b3, float* y, int M, int OD, int AD, int H, int n, float gamma,
@@ -276,9 +275,8 @@ static void skinny_dims(const torch::Tensor& t, int64_t& Z, int64_t& R, int64_t&
   sz = t.dim() == 3 ? t.stride(0) : 0;
 }
 
-// cnt (optional, int32, >= Z * N / 128 entries, zero between launches): ticket counters of the in-launch split combine
 int64_t skinny_nt(torch::Tensor A, torch::Tensor W, torch::Tensor out, c10::optional<torch::Tensor> add,
-                  c10::optional<torch::Tensor> part, c10::optional<torch::Tensor> cnt) {
+                  c10::optional<torch::Tensor> part) {
   int64_t Za, M, K, lda, sA, Zw, N, Kw, ldw, sW, Zo, Mo, No, ldo, sO;
   skinny_dims(A, Za, M, K, lda, sA);
   skinny_dims(W, Zw, N, Kw, ldw, sW);
@@ -312,14 +310,8 @@ int64_t skinny_nt(torch::Tensor A, torch::Tensor W, torch::Tensor out, c10::opti
                 "skinny_nt: workspace too small");
     pp = part->data_ptr<float>();
   }
-  int* cp = nullptr;
-  if (cnt.has_value() && cnt->defined()) {
-    TORCH_CHECK(cnt->is_cuda() && cnt->scalar_type() == torch::kInt32 && cnt->is_contiguous() && cnt->numel() >= Za * (N / 128),
-                "skinny_nt: cnt must be a contiguous int32 GPU tensor of >= Z * N / 128 zeros");
-    cp = cnt->data_ptr<int>();
-  }
   launch_skinny_nt(A.data_ptr<float>(), lda, sA, W.data_ptr<float>(), ldw, sW, out.data_ptr<float>(), ldo, sO, addp, ldadd,
-                   sAdd, pp, cp, (int)M, (int)N, (int)K, (int)Za, stream());
+                   sAdd, pp, (int)M, (int)N, (int)K, (int)Za, stream());
   return 0;
 }
 
@@ -753,6 +745,7 @@ bool launch_transpose_many(int nj, const float* const* src, const long* lds, con
 
 // contiguous transposes of up to 8 row-strided fp32 matrices (unit column stride) in one launch
 // (outs: optional contiguous [cols, rows] destinations, e.g. row blocks of one table; None entries allocate)
+void launch_side_delay(float us, hipStream_t st);
 std::vector<torch::Tensor> transpose_many(std::vector<torch::Tensor> xs, c10::optional<std::vector<c10::optional<torch::Tensor>>> outs) {
   TORCH_CHECK(!xs.empty() && xs.size() <= 8, "transpose_many: 1..8 matrices");
   std::vector<torch::Tensor> out;
@@ -792,6 +785,7 @@ void register_ext(pybind11::module& m) {
   m.def("onehot_index", &onehot_index);
   m.def("seq_sample_into", &seq_sample_into);
   m.def("transpose_many", &transpose_many, pybind11::arg("xs"), pybind11::arg("outs") = pybind11::none());
+  m.def("side_delay", [](double us) { launch_side_delay((float)us, stream()); });
   m.def("actor_tail", &actor_tail, pybind11::arg("pre"), pybind11::arg("y"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("eps"), pybind11::arg("act"), pybind11::arg("Wh"),
         pybind11::arg("bh"), pybind11::arg("uniform"), pybind11::arg("alpha"), pybind11::arg("sample"), pybind11::arg("idx"),
@@ -819,10 +813,8 @@ void register_ext(pybind11::module& m) {
   m.def("obs_mse_bwd", &obs_mse_bwd);
   m.def("sac_twin_q_target", &sac_twin_q_target);
   m.def("skinny_nt", &skinny_nt, pybind11::arg("A"), pybind11::arg("W"), pybind11::arg("out"),
-        pybind11::arg("add") = pybind11::none(), pybind11::arg("part") = pybind11::none(),
-        pybind11::arg("cnt") = pybind11::none());
+        pybind11::arg("add") = pybind11::none(), pybind11::arg("part") = pybind11::none());
   m.def("skinny_workspace", &skinny_workspace);
-  m.def("set_skinny_fused", &set_skinny_fused);  // 1 = in-launch split combine (opt-in A/B), 0 = reduce kernel
   m.def("actor_loss_discrete", &actor_loss_discrete);
   m.def("moments_update", &moments_update);
   m.def("nc_conv_fwd", &nc_conv_fwd);

@@ -277,11 +277,9 @@ __global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict
 
 using namespace srl;
 
-// A/B switch of the float4 wide-row forward / backward (SRL_GRU_VEC=0: the scalar kernels for every H)
-static bool g_gru_vec = [] {
-  const char* e = getenv("SRL_GRU_VEC");
-  return !(e && e[0] == '0');
-}();
+// the float4 wide-row forward / backward where the shape allows (set_gru_vec(false): the scalar kernels for every H,
+// tests only)
+static bool g_gru_vec = true;
 void set_gru_vec(bool on) { g_gru_vec = on; }
 
 static int gru_maxh(int H) {

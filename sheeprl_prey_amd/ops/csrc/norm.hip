@@ -748,11 +748,8 @@ int ln_bwd_grid(int M, int N, int G) {
   return M < 512 ? M : 512;
 }
 
-// SRL_LN_VEC_GROUPS=0: grouped (G > 1) rows on the scalar wave kernels (A/B)
-static const bool g_ln_vec_groups = [] {
-  const char* e = getenv("SRL_LN_VEC_GROUPS");
-  return !(e && e[0] == '0');
-}();
+// grouped (G = 2 / 4) rows on the 16-byte wave kernels (profiles/r4_ln_grouped.md)
+static constexpr bool g_ln_vec_groups = true;
 
 bool launch_ln_act_fwd(const float* x, int ldx, float* y, int ldy, const float* gamma, const float* beta, float* mean,
                        float* rstd, int M, int N, int G, float eps, int act, hipStream_t st) {

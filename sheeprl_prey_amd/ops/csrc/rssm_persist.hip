@@ -51,7 +51,7 @@ typedef unsigned long long u64;
 
 constexpr int NSH = 8;                // shards per arrival counter
 constexpr int SHW = 32;               // u32 words between shards (128 B)
-constexpr int NCTR = 6;               // counters per direction (ag form: 4 = A row statistics, 5 = h tiles)
+constexpr int NCTR = 4;               // counters per direction
 constexpr int ERRW = NCTR * NSH * SHW;  // index of the error word
 constexpr u32 SPIN_MAX = 1u << 20;
 
@@ -236,8 +236,6 @@ __device__ __forceinline__ void gemm_reg(const WTile<NT, U>& wt, const float* As
 // One role per workgroup; each role carves the dynamic LDS its own way (floats).
 __host__ __device__ inline int lds_A(int D, int H) { return 16 * (H + D + 4) + 2 * D + 4096 + 256 + 32 + 16; }
 __host__ __device__ inline int lds_B(int H) { return 16 * (H + 4) + 6 * H + 4096 + 256 + 32 + 16; }
-__host__ __device__ inline int lds_AG(int D, int H) { return 16 * (H + D + 4) + 2 * D + 96 + 8 * 16 * 48 + 768 + 64 + 16 + 48 * 260; }
-__host__ __device__ inline int lds_BU(int H) { return 16 * (H + 4) + 4096 + 256 + 16; }
 __host__ __device__ inline int lds_C_base(int hid, int S, int C) { return 16 * (hid + 4) + 2 * hid + 8192 + 512 + 16 + 16 * (S / C) + 32 + 1024 + 512; }
 // C also keeps its Wz^T column tiles (S rows x 16 columns each, ceil(D/16 / nC) of them) in LDS when they fit:
 // the per-step posterior gather then reads LDS instead of L2
@@ -433,7 +431,7 @@ __device__ __forceinline__ void fwd_B(const PP& p, int bI, float* sm) {
 __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
   const bool first_wg = cI == 0;
   const int B = p.B, S = p.S, D = p.D, H = p.H, hid = p.hid, C = p.C, T = p.T;
-  const int nA = (p.ag ? H : 3 * H) / 16, nB = hid / 16, nC = S / 32, nseg = S / C;
+  const int nA = 3 * H / 16, nB = hid / 16, nC = S / 32, nseg = S / C;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lda = hid + 4, n0 = cI * 32;
   float* As = sm;
   float* l2w = As + 16 * lda;
@@ -597,269 +595,6 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
       for (int e = lo + threadIdx.x; e < hi; e += NTH) v[e] = As[(e / hid) * lda + e % hid];
     }
   }
-}
-
-// ======================================================================= forward, "A owns the gates" form
-// A' (H/16 workgroups): the 16 h columns j of all three gates - gx columns {16a + j} of r, c, u - so after the
-// GEMM a workgroup holds every input of its 16 x 16 LN-GRU tile except the row statistics over 3H: each
-// publishes per-row (mean, M2) of its 48 columns, ONE hand-off among the A' workgroups (small), then the tile's
-// h_t is formed in place and published (h tiles hand-off to B' and the next step's A').  The h half of the GEMM
-// (K = H) needs only h_{t-1}, so it runs before the wait for C's xr_t.  B' (hid/16) only stages h_t and forms
-// its u tile.  Removes the full-row gx read (+ the redundant LN-GRU of every B workgroup) from the critical path.
-// Counters: 4 = A' row statistics, 5 = h tiles, 1 = B' (u), 2 / 3 = C as in the A/B form.
-__device__ __forceinline__ void fwd_AG(const PP& p, int a, float* sm) {
-  const bool first_wg = a == 0;
-  const int B = p.B, D = p.D, H = p.H, HD = H + D, N3 = 3 * H, T = p.T;
-  const int nA = H / 16, nB = p.hid / 16, nC = p.S / 32;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lda = HD + 4;
-  const int li = lane & 15, lg4 = lane >> 4;
-  float* As = sm;
-  float* l1w = As + 16 * lda;
-  float* l1b = l1w + D;
-  float* lgp = l1b + D;            // [2][48]: LN-GRU gamma / beta of this workgroup's gx columns (gate-major)
-  float* red = lgp + 96;           // [8 waves][16][48]: two-stage cross-wave reduction (waves 8..15 store, 0..7 add)
-  float* ct = red + 8 * 16 * 48;   // [16][48] gx tile
-  float* rowst = ct + 768;         // [16][2] LN-GRU row mean / rstd; [32..64): LN1 row statistics (workgroup 0)
-  int* flag = (int*)(rowst + 64);
-  float* wl = (float*)(flag + 16);  // [48 rows][260]: the second x-half weight chunk of every wave (K columns H + 256 ..)
-  // weight fragments (rows g*H + 16a + (lane & 15) of Wg, g = 0..2) for the x half (K = D, after the wait for C): the
-  // first chunk of each wave in registers, the second (K columns H + 256 ..) in LDS, both resident for the whole scan;
-  // the h half (K = H, before the wait) is streamed from L2 each step - its latency is off the critical path, and three
-  // register tiles of the whole K would not fit the 128-VGPR budget.  D <= 512 (host gate).
-  WTile<3, 1> wt;
-  const int nch = HD >> 4, nH = H >> 4;
-  const float* wrow = p.Wg + (size_t)(16 * a + li) * HD + 4 * lg4;
-  if (nH + w < nch) {
-#pragma unroll
-    for (int g = 0; g < 3; ++g) wt.b[0][g] = *(const f4*)(wrow + (size_t)g * H * HD + ((nH + w) << 4));
-  }
-  for (int e = threadIdx.x; e < 48 * 64; e += NTH) {  // 48 rows x 256 columns as float4
-    const int r = e >> 6, k4 = (e & 63) << 2, g = r >> 4, i = r & 15;
-    const int col = H + 256 + k4;
-    *(f4*)(wl + r * 260 + k4) = col < HD ? *(const f4*)(p.Wg + (size_t)(g * H + 16 * a + i) * HD + col) : f4{0.f, 0.f, 0.f, 0.f};
-  }
-  stage_vec(l1w, p.ln1w, D);
-  stage_vec(l1b, p.ln1b, D);
-  if (threadIdx.x < 48) {
-    const int g = threadIdx.x >> 4, c = threadIdx.x & 15;
-    lgp[threadIdx.x] = p.lngw[g * H + 16 * a + c];
-    lgp[48 + threadIdx.x] = p.lngb[g * H + 16 * a + c];
-  }
-  const u32 eA = shard_count(0, nA), eC = shard_count(nA + nB, nC);
-  for (int e = threadIdx.x; e < 16 * H; e += NTH) As[(e / H) * lda + e % H] = 0.f;  // h_{-1} = 0
-  __syncthreads();
-  const float* arow = As + li * lda + 4 * lg4;
-  for (int t = 0; t < T; ++t) {
-    PROF(0, 0);
-    f4 acc[3];
-#pragma unroll
-    for (int g = 0; g < 3; ++g) acc[g] = f4{0.f, 0.f, 0.f, 0.f};
-    if (t > 0) {
-      // every A' workgroup's h_{t-1} tile
-      if (!wait_ctr(p, 5, eA, t, 1, flag)) return;
-      stage_wt<2>(As, lda, p.hs + (size_t)(t - 1) * B * H, H, B, H, p.first + (size_t)t * B);
-      __syncthreads();
-    }
-    // h half of the GEMM (chunks c < nH, weights streamed) while C finishes the previous step
-    for (int c = w; c < nH; c += NWV) {
-      f4 bw[3];
-#pragma unroll
-      for (int g = 0; g < 3; ++g) bw[g] = *(const f4*)(wrow + (size_t)g * H * HD + (c << 4));
-      const f4 av = *(const f4*)(arow + (c << 4));
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bw[g][0], acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bw[g][1], acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bw[g][2], acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bw[g][3], acc[g], 0, 0, 0);
-      }
-    }
-    // park the h-half partial sums in the reduction buffer (slot w & 7: waves 0..7 store, then waves 8..15 add): no
-    // accumulator registers live across the wait and the LN1 prologue
-    if (w < 8) {
-#pragma unroll
-      for (int g = 0; g < 3; ++g)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[(w * 16 + 4 * lg4 + r) * 48 + 16 * g + li] = acc[g][r];
-    }
-    __syncthreads();
-    if (w >= 8) {
-#pragma unroll
-      for (int g = 0; g < 3; ++g)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[((w - 8) * 16 + 4 * lg4 + r) * 48 + 16 * g + li] += acc[g][r];
-    }
-    if (t > 0 && !wait_ctr(p, 2, eC, t, 2, flag)) return;
-    PROF(0, 1);
-    stage_wt<2>(As + H, lda, p.xr + (size_t)t * B * D, D, B, D);
-    __syncthreads();
-    PROF(0, 5);
-    if (w < B) {
-      float mu, rs;
-      wave_ln_act_row<LN_M>(As + w * lda + H, D, p.eps1, l1w, l1b, p.act1, mu, rs);
-      if (a == 0 && lane == 0) {
-        rowst[32 + w] = mu;
-        rowst[48 + w] = rs;
-      }
-    }
-    __syncthreads();
-    PROF(0, 2);
-    // x half (chunks nH <= c < nch, resident weights), then the cross-wave reduction of the 16 x 48 tile
-#pragma unroll
-    for (int g = 0; g < 3; ++g) acc[g] = f4{0.f, 0.f, 0.f, 0.f};
-    if (nH + w < nch) {  // first chunk: register weights
-      const f4 av = *(const f4*)(arow + ((nH + w) << 4));
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], wt.b[0][g][0], acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], wt.b[0][g][1], acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], wt.b[0][g][2], acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], wt.b[0][g][3], acc[g], 0, 0, 0);
-      }
-    }
-    if (nH + w + NWV < nch) {  // second chunk: LDS weights
-      const f4 av = *(const f4*)(arow + ((nH + w + NWV) << 4));
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        const f4 bw = *(const f4*)(wl + (16 * g + li) * 260 + (w << 4) + 4 * lg4);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[0], bw[0], acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[1], bw[1], acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[2], bw[2], acc[g], 0, 0, 0);
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[3], bw[3], acc[g], 0, 0, 0);
-      }
-    }
-    // x-half partials onto the parked h-half sums: waves 8..15 add into slot w - 8, then waves 0..7 into slot w
-    __syncthreads();
-    if (w >= 8) {
-#pragma unroll
-      for (int g = 0; g < 3; ++g)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[((w - 8) * 16 + 4 * lg4 + r) * 48 + 16 * g + li] += acc[g][r];
-    }
-    __syncthreads();
-    if (w < 8) {
-#pragma unroll
-      for (int g = 0; g < 3; ++g)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[(w * 16 + 4 * lg4 + r) * 48 + 16 * g + li] += acc[g][r];
-    }
-    __syncthreads();
-    if (threadIdx.x < 768) {
-      float v = 0.f;
-#pragma unroll
-      for (int ww = 0; ww < 8; ++ww) v += red[ww * 768 + threadIdx.x];
-      ct[threadIdx.x] = v;
-    }
-    __syncthreads();
-    PROF(0, 3);
-    // per-row (mean, M2) of the tile's 48 columns -> the other A' workgroups
-    const int eb = threadIdx.x >> 4, ec = threadIdx.x & 15;
-    if (threadIdx.x < 256) {
-      const float x0 = ct[eb * 48 + ec], x1 = ct[eb * 48 + 16 + ec], x2 = ct[eb * 48 + 32 + ec];
-      const float m = row16_sum(x0 + x1 + x2) * (1.f / 48.f);
-      const float q = row16_sum((x0 - m) * (x0 - m) + (x1 - m) * (x1 - m) + (x2 - m) * (x2 - m));
-      if (eb < B && ec == 0) st_wt2(p.gst + (((size_t)t * nA + a) * 16 + eb) * 2, m, q);
-    }
-    arrive(p.sync + 4 * NSH * SHW);
-    {  // the gx tile (weight-gradient input of the backward) behind the hand-off
-      if (threadIdx.x < 768) {
-        const int b = threadIdx.x / 48, cc = threadIdx.x - 48 * b, g = cc >> 4, c = cc & 15;
-        if (b < B) p.gx[((size_t)t * B + b) * N3 + g * H + 16 * a + c] = ct[threadIdx.x];
-      }
-    }
-    if (!wait_ctr(p, 4, eA, t + 1, 6, flag)) return;
-    PROF(0, 6);
-    if (w < B) {  // row statistics of gx over 3H: Chan's combine of the nA partials (48 columns each)
-      float2 pr[2];
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int i = lane + 64 * k;
-        pr[k] = i < nA ? ld_wt2(p.gst + (((size_t)t * nA + i) * 16 + w) * 2) : make_float2(0.f, 0.f);
-      }
-      const float mu = wave_sum_dpp(pr[0].x + pr[1].x) / nA;
-      float q = 0.f;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int i = lane + 64 * k;
-        if (i < nA) q += pr[k].y + 48.f * (pr[k].x - mu) * (pr[k].x - mu);
-      }
-      const float rs = rsqrtf(wave_sum_dpp(q) / N3 + p.epsg);
-      if (lane == 0) {
-        rowst[2 * w] = mu;
-        rowst[2 * w + 1] = rs;
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x < 256 && eb < B) {  // the LN-GRU of the tile: h column 16a + ec of row eb
-      const float mu = rowst[2 * eb], rs = rowst[2 * eb + 1];
-      const float x0 = ct[eb * 48 + ec], x1 = ct[eb * 48 + 16 + ec], x2 = ct[eb * 48 + 32 + ec];  // re-read: not live across the wait
-      const float zr = (x0 - mu) * rs * lgp[ec] + lgp[48 + ec];
-      const float zc = (x1 - mu) * rs * lgp[16 + ec] + lgp[64 + ec];
-      const float zu = (x2 - mu) * rs * lgp[32 + ec] + lgp[80 + ec];
-      const float r = fsig(zr), c = ftanh(r * zc), uu = fsig(zu - 1.f);
-      const float hp = As[eb * lda + 16 * a + ec];  // (1 - first) h_{t-1} as staged
-      st_wt(p.hs + ((size_t)t * B + eb) * H + 16 * a + ec, uu * c + (1.f - uu) * hp);
-    }
-    arrive(p.sync + 5 * NSH * SHW);
-    PROF(0, 4);
-    if (a == 0 && threadIdx.x < B) {  // row statistics for the backward, behind the hand-off
-      p.m1[(size_t)t * B + threadIdx.x] = rowst[32 + threadIdx.x];
-      p.r1[(size_t)t * B + threadIdx.x] = rowst[48 + threadIdx.x];
-      p.mg[(size_t)t * B + threadIdx.x] = rowst[2 * threadIdx.x];
-      p.rg[(size_t)t * B + threadIdx.x] = rowst[2 * threadIdx.x + 1];
-    }
-    {  // the GRU input of step t, read only by the backward
-      int lo, hi;
-      part_range(B * HD, a, nA, lo, hi);
-      float* cat = p.cat + (size_t)t * B * HD;
-      for (int e = lo + threadIdx.x; e < hi; e += NTH) cat[e] = As[(e / HD) * lda + e % HD];
-    }
-  }
-}
-
-// B' (ag form): u tile = h_t Wr1^T + P_t from the A' h tiles.
-__device__ __forceinline__ void fwd_BU(const PP& p, int bI, float* sm) {
-  const bool first_wg = bI == 0;
-  const int B = p.B, H = p.H, T = p.T, hid = p.hid;
-  const int nA = H / 16;
-  const int w = threadIdx.x >> 6, lda = H + 4;
-  float* As = sm;
-  float* red = As + 16 * lda;
-  float* ct = red + 4096;
-  int* flag = (int*)(ct + 256);
-  WTile<1, UB> wt;
-  wload<1, UB>(wt, p.W1 + (size_t)bI * 16 * H, H, H, w);
-  const u32 eA = shard_count(0, nA);
-  __syncthreads();
-  for (int t = 0; t < T; ++t) {
-    PROF(1, 0);
-    const int eb = threadIdx.x >> 4, ec = threadIdx.x & 15;
-    const size_t eo = ((size_t)t * B + eb) * hid + bI * 16 + ec;
-    const float pre = (threadIdx.x < 256 && eb < B) ? p.P[eo] : 0.f;  // epilogue input, loaded behind the wait
-    if (!wait_ctr(p, 5, eA, t + 1, 3, flag)) return;
-    PROF(1, 1);
-    stage_wt(As, lda, p.hs + (size_t)t * B * H, H, B, H);
-    __syncthreads();
-    PROF(1, 2);
-    gemm_reg<1, UB>(wt, As, lda, H, red, ct);
-    PROF(1, 3);
-    if (threadIdx.x < 256 && eb < B) st_wt(p.u + eo, ct[threadIdx.x] + pre);
-    arrive(p.sync + 1 * NSH * SHW);
-    PROF(1, 4);
-  }
-}
-
-// the ag form as its own kernel: its register allocation does not touch the A/B form's
-__global__ void __launch_bounds__(NTH) fwd_ag_kernel(PP p) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int bid = blockIdx.x;
-  const int nA = p.H / 16, nB = p.hid / 16;
-  if (bid < nA)
-    fwd_AG(p, bid, sm);
-  else if (bid < nA + nB)
-    fwd_BU(p, bid - nA, sm);
-  else
-    fwd_C(p, bid - nA - nB, sm);
 }
 
 __global__ void __launch_bounds__(NTH) fwd_kernel(PP p) {
@@ -1262,11 +997,10 @@ using namespace srl::scanp;
 // Words of the hand-off counter block (counters + error word, padded).
 int scanp_sync_words() { return ERRW + SHW; }
 
-int scanp_fwd_grid(int S, int H, int hid, int ag) { return (ag ? H : 3 * H) / 16 + hid / 16 + S / 32; }
+int scanp_fwd_grid(int S, int H, int hid) { return 3 * H / 16 + hid / 16 + S / 32; }
 int scanp_bwd_grid(int S, int D, int H, int hid) { return hid / 16 + H / 16 + (H + D) / 16 + S / 32; }
 
-int scanp_fwd_lds(int S, int D, int H, int hid, int C, int ag) {
-  if (ag) return 4 * std::max(std::max(lds_AG(D, H), lds_BU(H)), lds_C(hid, S, C, D));
+int scanp_fwd_lds(int S, int D, int H, int hid, int C) {
   return 4 * std::max(std::max(lds_A(D, H), lds_B(H)), lds_C(hid, S, C, D));
 }
 
@@ -1275,15 +1009,14 @@ int scanp_bwd_lds(int S, int D, int H, int hid) {
 }
 
 // Shape gate (register tile caps, LDS, residency of every workgroup): mirrors the kernels.
-bool scanp_supported(int B, int S, int D, int H, int hid, int C, int ag) {
+bool scanp_supported(int B, int S, int D, int H, int hid, int C) {
   if (B < 1 || B > 16 || C < 1 || C > 32 || (32 % C) != 0 || S % 32 || D % 16 || H % 16 || hid % 16) return false;
   if (H + D > 16 * 16 * UA || H > 16 * 16 * UB || hid > 16 * 16 * UC) return false;
   if (S > 16 * 16 * U1 || hid > 16 * 16 * U2 || 3 * H > 16 * 16 * U3 || D > 16 * 16 * U4 || H > 64 * GRU_M) return false;
   if (D > 64 * LN_M || hid > 64 * LN_M) return false;
   if (3 * H / 16 > 128) return false;  // Chan combine: two partials per lane
   const int mx = 160 * 1024;
-  if (ag && D > 16 * 16 * 2) return false;  // fwd_AG: x-half weight tiles UX = 2
-  if (scanp_fwd_lds(S, D, H, hid, C, ag) > mx || scanp_bwd_lds(S, D, H, hid) > mx) return false;
+  if (scanp_fwd_lds(S, D, H, hid, C) > mx || scanp_bwd_lds(S, D, H, hid) > mx) return false;
   int dev = 0, cus = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1291,32 +1024,27 @@ bool scanp_supported(int B, int S, int D, int H, int hid, int C, int ag) {
   // must fit the occupancy the compiler/runtime report for these kernels at their LDS size - not just
   // the CU count.  Another process or stream sharing the CUs can still starve a wave: the bounded
   // waits + the sticky health word (check_scan_health on the host) catch that at run time.
-  const void* fk = ag ? (const void*)fwd_ag_kernel : (const void*)fwd_kernel;
+  const void* fk = (const void*)fwd_kernel;
   set_lds(fk, 160 * 1024);
   set_lds((const void*)bwd_kernel, 160 * 1024);
   int occ_f = 0, occ_b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, fk, NTH, scanp_fwd_lds(S, D, H, hid, C, ag)) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, fk, NTH, scanp_fwd_lds(S, D, H, hid, C)) !=
           hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_b, (const void*)bwd_kernel, NTH, scanp_bwd_lds(S, D, H, hid)) !=
           hipSuccess)
     return false;
-  return scanp_fwd_grid(S, H, hid, ag) <= cus * occ_f && scanp_bwd_grid(S, D, H, hid) <= cus * occ_b;
+  return scanp_fwd_grid(S, H, hid) <= cus * occ_f && scanp_bwd_grid(S, D, H, hid) <= cus * occ_b;
 }
 
 void launch_scanp_fwd(const PP& p, hipStream_t st) {
   static bool init = false;
   if (!init) {
     set_lds((const void*)fwd_kernel, 160 * 1024);
-    set_lds((const void*)fwd_ag_kernel, 160 * 1024);
     init = true;
   }
   hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(256), 0, st, p.sync, scanp_sync_words());
-  if (p.ag)
-    hipLaunchKernelGGL(fwd_ag_kernel, dim3(scanp_fwd_grid(p.S, p.H, p.hid, 1)), dim3(NTH),
-                       scanp_fwd_lds(p.S, p.D, p.H, p.hid, p.C, 1), st, p);
-  else
-    hipLaunchKernelGGL(fwd_kernel, dim3(scanp_fwd_grid(p.S, p.H, p.hid, 0)), dim3(NTH),
-                       scanp_fwd_lds(p.S, p.D, p.H, p.hid, p.C, 0), st, p);
+  hipLaunchKernelGGL(fwd_kernel, dim3(scanp_fwd_grid(p.S, p.H, p.hid)), dim3(NTH), scanp_fwd_lds(p.S, p.D, p.H, p.hid, p.C),
+                     st, p);
 }
 
 void launch_scanp_bwd(const PP& p, hipStream_t st) {

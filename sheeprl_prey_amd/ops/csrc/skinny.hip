@@ -12,13 +12,7 @@
 //  * split-K over the grid: N/128 row blocks x ~K/kc chunks ~ 640 workgroups so every CU streams; the
 //    per-chunk partials (~WGs x 8 KiB) are summed, with the addend (bias / action projection), by a
 //    second small kernel that spreads the chunks over 4 waves per output tile.
-//  * opt-in (SRL_SKINNY_FUSED=1; the default is the separate reduce kernel, measured faster): the split partials are
-//    combined INSIDE the launch:
-//    each split workgroup stores its [128 weight rows x 16] partial tile write-through (sc1 buffer stores, no
-//    release fence), drains, joins, and one lane draws a ticket from the tile's counter (relaxed, agent scope);
-//    the workgroup drawing splits - 1 sums the tile's partials with sc1 loads in split order (deterministic,
-//    whichever workgroup is last), adds the addend and writes the output, and resets the counter for the next
-//    launch (cdna_hip_programming.md section 6 Guideline 16, split-K counter form).
+//    (an in-launch ticket combine of the partials measured slower - profiles/r4_skinny_fused.md - and was removed)
 //  * the A chunk (16 x kc) is staged once per workgroup in LDS (row stride kc+4) and shared by its 4 waves.
 //  * v_mfma_f32_16x16x4_f32 with a permuted K order: lane (j, q) of float4 i, component e feeds MFMA
 //    k = 16 i + 4 q + e for both operands, so one 64 B load per row maps onto the MFMA B layout
@@ -49,7 +43,6 @@ struct SP {
   const float* add;
   long ldadd, sAdd;
   float* part;
-  int* cnt;  // fused combine: one ticket counter per (z, row block), zero between launches (or null)
   int M, N, K, kc, splits, Z;
 };
 
@@ -121,47 +114,6 @@ __global__ __launch_bounds__(NTH) void skinny_nt_kernel(SP p) {
     }
   }
   // D layout: col = lane & 15 (weight row), row = 4 * (lane >> 4) + e (activation row)
-  if (p.splits > 1 && p.cnt != nullptr) {
-    // fused combine.  Partial tile layout [s][z][n][16 rows]: a lane's 4 rows (4q .. 4q+3) of weight row n are one
-    // 16-byte write-through store
-    const long tbase = ((long)s * p.Z + z) * p.N;
-    const int tot = p.splits * p.Z * p.N * 16;
-    const auto prs = __builtin_amdgcn_make_buffer_rsrc(p.part, (short)0, tot * 4, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc0), prs, (int)(((tbase + n0 + j) * 16 + 4 * q) * 4), 0, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc1), prs, (int)(((tbase + n0 + 16 + j) * 16 + 4 * q) * 4), 0, 16);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
-    __shared__ int last;
-    __syncthreads();
-    int* ctr = p.cnt + (long)z * gridDim.x + nb;
-    if (threadIdx.x == 0) last = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.splits - 1;
-    __syncthreads();
-    if (!last) return;
-    if (threadIdx.x == 0) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // the tile's 128 x 16 outputs as 512 float4 (weight row n, rows 4c .. 4c + 3): two per thread, every partial
-    // read with sc1 loads (the other splits' stores bypassed this CU's L1 / this XCD's L2 copy)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the loads stay below the ticket
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int f = threadIdx.x + NTH * h;
-      const int nl = f >> 2, c = f & 3;
-      const int n = nb * WG_ROWS + nl;
-      floatx4 r = {0.f, 0.f, 0.f, 0.f};
-      for (int ss = 0; ss < p.splits; ++ss) {
-        const long off = ((((long)ss * p.Z + z) * p.N + n) * 16 + 4 * c) * 4;
-        r += __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(prs, (int)off, 0, 16));
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = 4 * c + e;
-        if (m < p.M) {
-          float* o = p.out + (long)z * p.sO + (long)m * p.ldo;
-          const float* ad = p.add ? p.add + (long)z * p.sAdd + (long)m * p.ldadd : nullptr;
-          o[n] = r[e] + (ad ? ad[n] : 0.f);
-        }
-      }
-    }
-    return;
-  }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const int m = 4 * q + e;
@@ -217,15 +169,9 @@ __global__ __launch_bounds__(NTH) void skinny_reduce_kernel(SP p) {
 }  // namespace skinny
 }  // namespace srl
 
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-
-// Split plan: returns the number of K chunks (and the chunk width in *kc).  SRL_SKINNY_WGS overrides
-// the target grid size (tuning experiments).
+// Split plan: returns the number of K chunks (and the chunk width in *kc).
 int skinny_plan(int N, int K, int Z, int* kc) {
-  static const int target = env_int("SRL_SKINNY_WGS", srl::skinny::TARGET_WGS);
+  constexpr int target = srl::skinny::TARGET_WGS;
   const int nblk = std::max(1, N / srl::skinny::WG_ROWS * Z);
   int splits = std::max(1, std::min(K / srl::skinny::KSTEP, (target + nblk - 1) / nblk));
   int c = (K + splits - 1) / splits;
@@ -235,15 +181,8 @@ int skinny_plan(int N, int K, int Z, int* kc) {
   return (K + c - 1) / c;
 }
 
-// in-launch combine of the split partials: opt-in (SRL_SKINNY_FUSED=1 or set_skinny_fused).  Measured slower than
-// the separate reduce kernel at the XL shapes (profiles/r4_skinny_fused.md: W1 forward 31.5 vs 15.1 us - the last
-// workgroup of a tile reads its 16-32 partial slabs serially; XL bench 46.5 vs 48.4)
-static int g_skinny_fused = env_int("SRL_SKINNY_FUSED", 0);
-void set_skinny_fused(int on) { g_skinny_fused = on; }
-static bool skinny_fused() { return g_skinny_fused != 0; }
-
 void launch_skinny_nt(const float* A, long lda, long sA, const float* W, long ldw, long sW, float* out, long ldo, long sO,
-                      const float* add, long ldadd, long sAdd, float* part, int* cnt, int M, int N, int K, int Z,
+                      const float* add, long ldadd, long sAdd, float* part, int M, int N, int K, int Z,
                       hipStream_t st) {
   srl::skinny::SP p;
   p.A = A;
@@ -259,7 +198,6 @@ void launch_skinny_nt(const float* A, long lda, long sA, const float* W, long ld
   p.ldadd = ldadd;
   p.sAdd = sAdd;
   p.part = part;
-  p.cnt = skinny_fused() ? cnt : nullptr;
   p.M = M;
   p.N = N;
   p.K = K;
@@ -275,6 +213,6 @@ void launch_skinny_nt(const float* A, long lda, long sA, const float* W, long ld
   }
   const dim3 grid(N / srl::skinny::WG_ROWS, p.splits, Z);
   hipLaunchKernelGGL(srl::skinny::skinny_nt_kernel<false>, grid, dim3(srl::skinny::NTH), lds, st, p);
-  if (p.splits > 1 && p.cnt == nullptr)
+  if (p.splits > 1)
     hipLaunchKernelGGL(srl::skinny::skinny_reduce_kernel, dim3((N / 4 + 63) / 64, M, Z), dim3(srl::skinny::NTH), 0, st, p);
 }

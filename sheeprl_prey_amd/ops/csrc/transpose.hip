@@ -76,3 +76,23 @@ bool launch_transpose_many(int nj, const float* const* src, const long* lds, con
   if (tiles > 0) hipLaunchKernelGGL(tr::transpose_kernel, dim3(tiles), dim3(256), 0, st, p);
   return true;
 }
+
+// One-wave delay at the head of a side-stream branch (ops/sidestream.py): holds the branch ~us microseconds of wall
+// clock (s_memrealtime, 100 MHz) so that the persistent scan launched beside it claims its CUs first.
+namespace srl {
+__global__ void __launch_bounds__(64) side_delay_kernel(long long ticks) {
+  long long t0;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  for (int i = 0; i < (1 << 20); ++i) {  // bounded: ends within ~10 ms whatever the clock does
+    long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    if (t - t0 >= ticks) break;
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+}  // namespace srl
+
+void launch_side_delay(float us, hipStream_t st) {
+  const long long ticks = (long long)(us * 100.f);
+  if (ticks > 0) hipLaunchKernelGGL(srl::side_delay_kernel, dim3(1), dim3(64), 0, st, ticks);
+}

@@ -572,14 +572,9 @@ using namespace srl;
 
 // Chunks for the dense split: ~2 workgroups per CU over the output tiles, chunks of >= 256 rows, a
 // multiple of 16 rows (one register batch).
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-
 int wgrad_dense_chunks(int M, int N, int K) {
   const int tiles = cdiv(N, wgrad::BT) * cdiv(K, wgrad::BT);
-  static const int target = env_int("SRL_WGRAD_WGS", 512);  // tuning knob (scripts/wgrad_timing.py)
+  constexpr int target = 512;  // tuned with scripts/wgrad_timing.py
   int S = cdiv(target, tiles);
   const int maxS = cdiv(M, 256);
   if (S > maxS) S = maxS;
@@ -629,7 +624,7 @@ void launch_wgrad_dense(const float* dz, long ldz, const float* x, long ldx, flo
 int wgrad_onehot_chunks(int M, int N, int G, int C) {
   if (C > wgrad::OH_CMAX || C < 1 || (N & 1)) return 0;
   const int blocks = cdiv(N, wgrad::OH_COLS) * cdiv(G, wgrad::OH_WAVES);
-  static const int target = env_int("SRL_WGRAD_OH_WGS", 256);  // tuning knob
+  constexpr int target = 256;
   int S = cdiv(target, blocks);  // one 133 KB-LDS workgroup per CU
   const int maxS = cdiv(M, 256);
   if (S > maxS) S = maxS;
@@ -654,8 +649,7 @@ bool launch_wgrad_onehot(const float* dz, long ldz, const int* idx, long ldi, in
   p.S = S;
   p.KO = G * C;
   const dim3 grid(cdiv(N, wgrad::OH_COLS), cdiv(G, wgrad::OH_WAVES), S);
-  static const bool staged = env_int("SRL_WGRAD_OH_STAGED", 1) != 0;  // A/B switch
-  if (staged && (N & 3) == 0 && (ldz & 3) == 0 && ((uintptr_t)dz & 15) == 0) {
+  if ((N & 3) == 0 && (ldz & 3) == 0 && ((uintptr_t)dz & 15) == 0) {
     p.rows = cdiv(cdiv(M, S), wgrad::OS_RU) * wgrad::OS_RU;
     hipLaunchKernelGGL(wgrad::onehot_stg_kernel, grid, dim3(wgrad::OH_WAVES * 64), 0, st, p);
     return true;

@@ -101,6 +101,7 @@ class _GatherFirstLayer(torch.autograd.Function):
         if not ok:
             raise RuntimeError(f"onehot_gather_ln: unsupported layer width {N}")
         ctx.save_for_backward(x2, idx2, W, gamma, beta, z, mean, rstd)
+        ctx.params = (W, bias)  # the leaves a deferred weight gradient is assigned to (ops/sidestream.py)
         ctx.meta = (act, use_ln, bias is not None, x.shape, int(G), int(off), int(n_onehot))
         return y.view(*x.shape[:-1], N)
 
@@ -129,9 +130,8 @@ class _GatherFirstLayer(torch.autograd.Function):
         meta = (ctx.meta, tuple(ctx.needs_input_grad))
         if ss.active(dz.device) and ctx.needs_input_grad[2]:
             # inside a deferral scope (the world-model backward): parameter gradients beside the scan backward
-            shapes = [tuple(W.shape), (N,) if has_bias and ctx.needs_input_grad[3] else None]
-            dW, dbias = ss.param_grads(dz.device, lambda outs: _GatherFirstLayer._param_grads(meta, dz, x2, idx2, outs),
-                                       shapes, dz, x2, idx2)
+            dW, dbias = ss.param_grads(dz.device, lambda: _GatherFirstLayer._param_grads(meta, dz, x2, idx2),
+                                       ctx.params, dz, x2, idx2)
         else:
             dW, dbias = _GatherFirstLayer._param_grads(meta, dz, x2, idx2)
         return (dx, None, dW, dbias, dg if ctx.needs_input_grad[4] else None, db if ctx.needs_input_grad[5] else None,

@@ -35,7 +35,7 @@ from sheeprl_prey_amd.ops.reference import ACTS
 
 def _use_skinny(B: int, H: int) -> bool:
     """Large recurrent states (XL: deter 4096): the per-step GEMMs take a weight-streaming route."""
-    return B <= 16 and H >= 1024 and os.environ.get("SRL_SKINNY", "1") != "0"
+    return B <= 16 and H >= 1024
 
 
 # Measured on MI355X (scripts/skinny_sweep.py, 16 rows): hipBLASLt's NT kernels stream the big GRU
@@ -284,8 +284,9 @@ class RSSMScan4Fn(torch.autograd.Function):
         p1g, p1b, pgg, pgb, p2g, p2b = e(T, D), e(T, D), e(T, 3 * H), e(T, 3 * H), e(T, 2 * hid), e(T, 2 * hid)
         bwd = [WzT, Wg.t().contiguous(), W1.t().contiguous(), W2.transpose(1, 2).contiguous(), dpost,
                dmixed, DH, dlog, dv, du, dgx, dx, e(B, H + D), e(B, H), p1g, p1b, pgg, pgb, p2g, p2b]
+        fork = sidestream.fork_point(dev)
         C.scan4_bwd(fwd + bwd, ctx.dims, ctx.fl)
-        sidestream.flush(dev)
+        sidestream.flush(dev, fork=fork)
         cat, zm, hs, v = fwd[16], fwd[17], fwd[24], fwd[26]
         TB = T * B
         dWz = dx.reshape(TB, D).t().mm(zm.reshape(TB, S))
@@ -379,9 +380,10 @@ class RSSMPersistFn(torch.autograd.Function):
         bwd = [W2T, W1T, WgT, dpost, dmixed, DH, dlog, dv, du, dgx, dcat,
                dx, p1g, p1b, pgg, pgb, p2g, p2b, e(T, B, 3 * H), e(T, H // 16, 16, 2)]
         _scan_health_word(dev)
+        fork = sidestream.fork_point(dev)
         C.scanp_bwd(fwd + bwd, ctx.dims, ctx.fl)
         # the queued decoder / head parameter gradients run beside the scan backward (ops/sidestream.py)
-        sidestream.flush(dev)
+        sidestream.flush(dev, fork=fork)
         cat, zm, hs, v = fwd[17], fwd[18], fwd[25], fwd[27]
         TB = T * B
         dWz = dx.reshape(TB, D).t().mm(zm.reshape(TB, S))

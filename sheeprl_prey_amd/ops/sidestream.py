@@ -10,20 +10,18 @@ so nothing on that chain waits for them.  The persistent scan backward holds ~16
 ~1.7 ms while its workgroups mostly wait on each other's hand-offs; the other CUs are idle.
 
 Protocol (``with scope(): loss.backward()``):
-* ``param_grads(dev, fn, shapes, *reads)``: inside a scope, the gradient tensors are allocated now (on the
-  main stream, so autograd can hand them to the parameters) and ``fn(outs)`` - which fills ``outs`` or
-  returns tensors to copy into them - is QUEUED; outside a scope it runs in line and its result is returned.
-* ``flush(dev)``: the scan backward calls it right after launching its kernel.  The queue then runs on a
-  side stream forked off the main stream (so it sees every data gradient queued so far), behind a short
+* ``param_grads(dev, fn, params, *reads)``: outside a scope ``fn()`` runs in line and its gradient tensors are
+  returned; inside a scope it is QUEUED and None is returned for those parameters (the autograd Function hands
+  autograd no gradient for them, so no AccumulateGrad runs - autograd would clone a buffer that is still
+  being written on another stream).
+* ``fork_point(dev)`` / ``flush(dev, fork=...)``: the scan backward records the fork point on the main stream,
+  enqueues its kernel, then flushes.  The queue then runs on a side stream forked off the main stream at that
+  point (so it sees every data gradient queued before the scan and does NOT wait for the scan), behind a short
   spin kernel so that the scan's workgroups are resident before the weight-gradient grids fill the chip (a
-  persistent grid needs whole free CUs; the side kernels then run on the CUs the scan leaves idle).
-  Reads are marked used by the side stream (``record_stream``) so the caching allocator cannot recycle them.
-* the join: the first queued item registers an autograd final callback that flushes whatever is still
-  queued (a backward without a scan) and makes the main stream wait for the side stream; the flat
-  optimisers also call ``join()`` before they read a gradient (``parallel/flat_optim.py``).  hipGraph
-  capture records the fork / join as graph edges (branches replay concurrently:
-  ``scripts/overlap_probe.py``).
-
+  persistent grid needs whole free CUs; the side kernels then run on the CUs the scan leaves idle).  Each
+  result becomes its parameter's ``.grad`` (or is added to one already there, on the side stream).  Reads
+  and results are marked used by the side / main stream (``record_stream``) so the caching allocator cannot
+  recycle them early.
 Same gradients as the in-line backward, joined before anything reads them.  ``SRL_DEFER_WGRAD=0`` runs
 everything in line (A/B).  History: round 4 forked each weight gradient onto the side stream as soon as its
 output gradient existed; those kernels then competed with the decoder's data-gradient convolutions instead
@@ -38,8 +36,8 @@ import torch
 from torch import Tensor
 
 ENABLED = os.environ.get("SRL_DEFER_WGRAD", "1") != "0"
-# cycles of the spin kernel at the head of the side branch (~8 us at the gfx950 shader clock)
-DELAY_CYCLES = 20000
+# microseconds the side branch waits (one-wave delay kernel) before its first weight-gradient grid
+DELAY_US = float(os.environ.get("SRL_SIDE_DELAY_US", "8"))
 _streams: Dict[int, "torch.cuda.Stream"] = {}
 _queue: Dict[int, List] = {}
 _pending: Dict[int, bool] = {}
@@ -60,7 +58,7 @@ def scope() -> Iterator[None]:
 def _stream(i: int) -> "torch.cuda.Stream":
     s = _streams.get(i)
     if s is None:
-        s = _streams[i] = torch.cuda.Stream(device=i)
+        s = _streams[i] = torch.cuda.Stream(device=i, priority=int(os.environ.get("SRL_SIDE_PRIO", "0")))
         from sheeprl_prey_amd import ops
 
         # column-sum launches on this stream rotate through their own half of the ticket workspace (norm.hip)
@@ -76,24 +74,34 @@ def active(dev: torch.device) -> bool:
     return ENABLED and _depth > 0 and dev.type == "cuda"
 
 
-def param_grads(dev: torch.device, fn: Callable[[Optional[List[Optional[Tensor]]]], Sequence[Optional[Tensor]]],
-                shapes: Sequence, *reads: Tensor) -> List[Optional[Tensor]]:
-    """``fn(outs)`` now (``outs=None``: fn allocates) or, inside a scope, queued until ``flush``; returns the
-    gradient tensors (entries of ``shapes`` that are None give None)."""
+def param_grads(dev: torch.device, fn: Callable[[], Sequence[Optional[Tensor]]], params: Sequence[Optional[Tensor]],
+                *reads: Tensor) -> List[Optional[Tensor]]:
+    """``fn()`` -> the gradients of ``params``: computed now and returned, or (inside a scope) queued until
+    ``flush`` and None returned."""
     if not active(dev):
-        return list(fn(None))
-    outs = [torch.empty(tuple(s), device=dev, dtype=torch.float32) if s is not None else None for s in shapes]
+        return list(fn())
     i = _index(dev)
-    _queue.setdefault(i, []).append((fn, outs, reads))
+    _queue.setdefault(i, []).append((fn, list(params), reads))
     if not _armed.get(i):
         _armed[i] = True
         main = torch.cuda.current_stream(dev)
         torch.autograd.Variable._execution_engine.queue_callback(lambda: _finish(i, main))
-    return outs
+    return [None] * len(params)
 
 
-def flush(dev: torch.device, delay: bool = True) -> None:
-    """Run the queued parameter-gradient work on the side stream, forked off the current stream now."""
+def fork_point(dev: torch.device) -> Optional["torch.cuda.Event"]:
+    """An event on the current stream marking where the side branch forks (recorded BEFORE the kernel it should
+    run beside is enqueued: a fork after it would make the branch wait for that kernel to finish)."""
+    if dev.type != "cuda" or not _queue.get(_index(dev)):
+        return None
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    return ev
+
+
+def flush(dev: torch.device, delay: bool = True, fork: Optional["torch.cuda.Event"] = None) -> None:
+    """Run the queued parameter-gradient work on the side stream, forked off the current stream at ``fork``
+    (a ``fork_point`` event) or now."""
     if dev.type != "cuda":
         return
     i = _index(dev)
@@ -102,20 +110,37 @@ def flush(dev: torch.device, delay: bool = True) -> None:
         return
     main = torch.cuda.current_stream(dev)
     s = _stream(i)
-    s.wait_stream(main)
+    if fork is not None:
+        s.wait_event(fork)
+    else:
+        s.wait_stream(main)
     with torch.cuda.stream(s):
-        if delay and DELAY_CYCLES > 0:
-            torch.cuda._sleep(DELAY_CYCLES)
-        for fn, outs, _ in q:
-            res = fn(outs)
-            for o, r in zip(outs, res):
-                if o is not None and r is not None and r.data_ptr() != o.data_ptr():
-                    o.copy_(r.view_as(o))
-    for _, outs, reads in q:
-        for t in list(reads) + list(outs):
-            if t is not None and t.is_cuda:
-                t.record_stream(s)
+        if delay and DELAY_US > 0:
+            from sheeprl_prey_amd import ops
+
+            ops._ext().side_delay(DELAY_US)
+        for fn, params, reads in q:
+            res = fn()
+            for p, r in zip(params, res):
+                if p is None or r is None:
+                    continue
+                if p.grad is None:
+                    p.grad = r.view_as(p) if r.shape != p.shape else r
+                else:
+                    p.grad.add_(r.view_as(p))
+                r.record_stream(main)  # read there after the join (flat optimiser gather)
+            for t in reads:
+                if t is not None and t.is_cuda:
+                    t.record_stream(s)
     _pending[i] = True
+    # the post-accumulate-grad hooks autograd did not run for these parameters (the flat optimisers' overlapped
+    # all-reduce buckets, parallel/flat_optim.py): they join the side stream before they read the gradient
+    for _, params, _ in q:
+        for p in params:
+            hooks = getattr(p, "_post_accumulate_grad_hooks", None) if p is not None else None
+            if hooks and p.grad is not None:
+                for h in list(hooks.values()):
+                    h(p)
 
 
 def _finish(i: int, main: "torch.cuda.Stream") -> None:

@@ -320,12 +320,13 @@ class FlatOptimizer:
 
     def _ov_finish(self, wait: bool = True) -> None:
         ov = self._ov
-        # parameters that got no gradient in this backward: a zero slab view (set_to_none) or the
-        # accumulated one already there
+        _side_join()  # deferred parameter gradients (ops/sidestream.py) land in .grad without a hook
+        # parameters whose hook did not fire in this backward: no gradient (a zero slab view), a deferred one set
+        # by the side stream, or the accumulated one already in the slab
         for i, p in enumerate(self.params):
             if not ov["seen"][i]:
                 v = self._ov_view(i)
-                if self._detached or p.grad is None:
+                if p.grad is None:
                     v.zero_()
                 elif p.grad.data_ptr() != v.data_ptr():
                     v.copy_(p.grad)

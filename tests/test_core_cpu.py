@@ -413,16 +413,19 @@ def test_built_extension_links():
 
 
 def test_sidestream_scope_is_inert_on_cpu_and_outside_scopes():
-    """ops/sidestream.py: on CPU tensors and outside a scope ``on_side`` runs the block in line and nothing is left to
-    join; the scope counter nests and unwinds on exceptions."""
+    """ops/sidestream.py: on CPU tensors and outside a scope ``param_grads`` runs its function in line and returns
+    its gradients, nothing is queued or left to join; the scope counter nests and unwinds on exceptions."""
     import torch
 
     from sheeprl_prey_amd.ops import sidestream as ss
 
     x = torch.ones(3)
-    with ss.on_side(x.device, x):
-        y = x * 2
-    assert torch.equal(y, torch.full((3,), 2.0)) and not ss._pending
+    p = torch.nn.Parameter(torch.zeros(3))
+    (g,) = ss.param_grads(x.device, lambda: (x * 2,), [p], x)
+    assert torch.equal(g, torch.full((3,), 2.0)) and not ss._pending and not ss._queue
+    with ss.scope():
+        (g,) = ss.param_grads(x.device, lambda: (x * 3,), [p], x)  # CPU inside a scope: still in line
+    assert torch.equal(g, torch.full((3,), 3.0)) and not ss._queue and p.grad is None
     ss.join()
     assert not ss.active(torch.device("cpu"))
     with ss.scope():

@@ -80,24 +80,6 @@ def test_fused_rssm_scan_matches_python_scan(H, D, hid, B, T, impl):
     _check_scan_vs_python(H, D, hid, B, T, impl, expect="scan4" if (impl == "persist" and D > 512) else None)
 
 
-@pytest.mark.parametrize("H,D,hid,B,T", [(64, 64, 64, 4, 16), (512, 512, 512, 16, 8), (96, 80, 48, 3, 5),
-                                         (512, 512, 512, 16, 64)])
-def test_persistent_scan_ag_form_matches_python_scan(H, D, hid, B, T):
-    """The persistent scan's "A owns the gates" forward form (``fwd_ag_kernel``: A' workgroups own 16 h columns of
-    all three GRU gates, one row-statistics hand-off among them, the LN-GRU tile formed in place; B' only stages h)
-    vs the python step loop, forward and backward (the backward reads what the new forward saved)."""
-    from sheeprl_prey_amd import ops
-
-    C = ops._ext()
-    C.set_scanp_ag(1)
-    try:
-        tol = (5e-3, 5e-4) if T == 64 else (2e-3, 2e-4)
-        gtol = (5e-3, 5e-3) if T == 64 else (3e-3, 3e-3)
-        _check_scan_vs_python(H, D, hid, B, T, "persist", tol=tol, gtol=gtol)
-    finally:
-        C.set_scanp_ag(0)
-
-
 @pytest.mark.parametrize("impl", ["persist", "scan4"])
 def test_fused_rssm_scan_full_shape_T64(impl):
     """Atari-100k shape over the whole sequence (B 16, T 64, H = D = hid = 512): the fast

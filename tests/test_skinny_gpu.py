@@ -44,43 +44,3 @@ def test_skinny_in_place_accumulate_and_gate():
     assert not ops.skinny_nt(A, torch.randn(100, 1024, device="cuda"), torch.empty(16, 100, device="cuda"))
 
 
-def test_skinny_fused_combine_repeat_and_graph():
-    """The opt-in in-launch split combine (ticket counters returned to zero by each tile's last workgroup): repeated eager
-    calls, and the same call captured in a hipGraph and replayed, give the deterministic result every time and
-    leave every counter of the pool at zero."""
-    C = ops._ext()
-    C.set_skinny_fused(1)
-    try:
-        _fused_combine_checks(C)
-    finally:
-        C.set_skinny_fused(0)
-
-
-def _fused_combine_checks(C):
-    torch.manual_seed(0)
-    A = torch.randn(2, 16, 1024, device="cuda")
-    W = torch.randn(2, 1024, 1024, device="cuda") / 32
-    bias = torch.randn(2, 1, 1024, device="cuda")
-    assert C.skinny_workspace(1024, 1024, 2) > 0  # split-K: the combine path runs
-    out = torch.empty(2, 16, 1024, device="cuda")
-    assert ops.skinny_nt(A, W, out, bias)
-    first = out.clone()
-    torch.testing.assert_close(first.double(), torch.matmul(A.double(), W.double().transpose(1, 2)) + bias.double(),
-                               rtol=1e-4, atol=1e-4)
-    for _ in range(5):
-        assert ops.skinny_nt(A, W, out, bias)
-        assert torch.equal(out, first)
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(s):
-        with torch.cuda.graph(g):
-            ops.skinny_nt(A, W, out, bias)
-    torch.cuda.current_stream().wait_stream(s)
-    for _ in range(4):
-        out.zero_()
-        g.replay()
-        torch.cuda.synchronize()
-        assert torch.equal(out, first)
-    pool = ops._skinny_pool[torch.cuda.current_device()][0]
-    assert int(pool.abs().sum()) == 0
