@@ -37,7 +37,7 @@ from torch import Tensor
 
 ENABLED = os.environ.get("SRL_DEFER_WGRAD", "1") != "0"
 # microseconds the side branch waits (one-wave delay kernel) before its first weight-gradient grid
-DELAY_US = float(os.environ.get("SRL_SIDE_DELAY_US", "8"))
+DELAY_US = 8.0
 _streams: Dict[int, "torch.cuda.Stream"] = {}
 _queue: Dict[int, List] = {}
 _pending: Dict[int, bool] = {}
@@ -58,7 +58,7 @@ def scope() -> Iterator[None]:
 def _stream(i: int) -> "torch.cuda.Stream":
     s = _streams.get(i)
     if s is None:
-        s = _streams[i] = torch.cuda.Stream(device=i, priority=int(os.environ.get("SRL_SIDE_PRIO", "0")))
+        s = _streams[i] = torch.cuda.Stream(device=i)
         from sheeprl_prey_amd import ops
 
         # column-sum launches on this stream rotate through their own half of the ticket workspace (norm.hip)
