@@ -161,11 +161,12 @@ def main():
 
     grad_steps = 0
     last_batch = [None]
+    unsampled = [False]  # profile passes: the eager train step (graphs off) instead of the captured sampled replay
 
     def train_once():
         nonlocal grad_steps
         trainer.update_target(1.0 if grad_steps == 0 else cfg.algo.critic.tau)
-        if not args.eager_ops and not args.check_finite:
+        if not args.eager_ops and not args.check_finite and not unsampled[0]:
             # captured step: the sample is drawn into the graph's inputs by one launch (dreamer_v3.main does the same)
             out = trainer.train_step_sampled(rb, cfg.per_rank_batch_size, cfg.per_rank_sequence_length)
             if out is not None:
@@ -223,6 +224,7 @@ def main():
         from torch.profiler import ProfilerActivity, profile
 
         trainer.graphed.enabled = False
+        unsampled[0] = True
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
             for _ in range(args.torch_profile):
                 one_step()
@@ -260,6 +262,7 @@ def main():
             for (name, site), n in sm.c.most_common(int(os.environ.get("SRL_PROFILE_TOP", 60))):
                 print(f"SITE {n:4d} {name:28s} {site}", file=sys.stderr, flush=True)
         trainer.graphed.enabled = True
+        unsampled[0] = False
         small = ("aten::cat", "aten::copy_", "aten::fill_", "aten::zero_", "aten::add", "aten::add_", "aten::sum",
                  "aten::mean", "aten::mul", "aten::sub", "aten::rand", "aten::zeros", "aten::clone", "aten::div",
                  "aten::neg", "aten::exp", "aten::where", "aten::stack", "aten::contiguous", "aten::index_select",

@@ -72,6 +72,10 @@ __device__ __forceinline__ long long prof_clock() {
 constexpr int UA = 4, UB = 2, UC = 2;           // K = H+D <= 1024, H <= 512, hid <= 512
 constexpr int U1 = 4, U2 = 2, U3 = 6, U4 = 2;   // K = S <= 1024, hid <= 512, 3H <= 1536, D <= 512
 constexpr int GRU_M = 8;                        // H <= 64 * GRU_M
+// "big" form for a wide recurrent input (exp=dreamer_v3_prey: dense 1024, deter / hidden 256): the A tile takes
+// K = H + D <= 1280, its LN1 row up to 1024 wide, and G4 (dz = dx Wz, K = D <= 1024) keeps its LN1 adjoint in LDS
+// (two passes) with the GEMM reduction aliased onto the dead xh tile (bwd_G4_big)
+constexpr int UA_BIG = 5, LN_BIG = 16, U4_BIG = 4;
 constexpr int LN_M = 8;                         // D, hid <= 64 * LN_M (row LayerNorms in registers)
 
 // ------------------------------------------------------------------ write-through accesses
@@ -255,6 +259,7 @@ __host__ __device__ inline int lds_G4(int D) { return 48 * (D + 4) + 2 * D + 48 
 // Block ids: A = [0, nA), B = [nA, nA + nB), C = [nA + nB, nA + nB + nC).  Counters: 0 = A, 1 = B, 2 = C.
 
 // A: gx tile = [(1-first) h_{t-1}, act(LN1(xr_t))] Wg^T, plus per-row (mean, M2) of the tile.
+template <int UA_, int LNA_>
 __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
   const bool first_wg = a == 0;
   const int B = p.B, D = p.D, H = p.H, HD = H + D, N3 = 3 * H, T = p.T;
@@ -266,8 +271,8 @@ __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
   float* red = l1b + D;
   float* ct = red + 4096;         // [256] GEMM tile + [32] this step's LN1 row statistics (workgroup 0)
   int* flag = (int*)(ct + 256 + 32);
-  WTile<1, UA> wt;
-  wload<1, UA>(wt, p.Wg + (size_t)a * 16 * HD, HD, HD, w);
+  WTile<1, UA_> wt;
+  wload<1, UA_>(wt, p.Wg + (size_t)a * 16 * HD, HD, HD, w);
   stage_vec(l1w, p.ln1w, D);
   stage_vec(l1b, p.ln1b, D);
   const u32 eB = shard_count(nA, nB), eC = shard_count(nA + nB, nC);
@@ -287,7 +292,7 @@ __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
     PROF(0, 5);
     if (w < B) {
       float mu, rs;
-      wave_ln_act_row<LN_M>(As + w * lda + H, D, p.eps1, l1w, l1b, p.act1, mu, rs);
+      wave_ln_act_row<LNA_>(As + w * lda + H, D, p.eps1, l1w, l1b, p.act1, mu, rs);
       if (a == 0 && lane == 0) {  // stored after the hand-off: a global store before a barrier would be drained there
         ct[256 + w] = mu;
         ct[272 + w] = rs;
@@ -295,7 +300,7 @@ __device__ __forceinline__ void fwd_A(const PP& p, int a, float* sm) {
     }
     __syncthreads();
     PROF(0, 2);
-    gemm_reg<1, UA>(wt, As, lda, HD, red, ct);
+    gemm_reg<1, UA_>(wt, As, lda, HD, red, ct);
     PROF(0, 3);
     if (threadIdx.x < 256) {
       const int b = threadIdx.x >> 4, c = threadIdx.x & 15;
@@ -597,16 +602,26 @@ __device__ __forceinline__ void fwd_C(const PP& p, int cI, float* sm) {
   }
 }
 
-__global__ void __launch_bounds__(NTH) fwd_kernel(PP p) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+template <int UA_, int LNA_>
+__device__ __forceinline__ void fwd_body(const PP& p, float* sm) {
   const int bid = blockIdx.x;
   const int nA = 3 * p.H / 16, nB = p.hid / 16;
   if (bid < nA)
-    fwd_A(p, bid, sm);
+    fwd_A<UA_, LNA_>(p, bid, sm);
   else if (bid < nA + nB)
     fwd_B(p, bid - nA, sm);
   else
     fwd_C(p, bid - nA - nB, sm);
+}
+
+__global__ void __launch_bounds__(NTH) fwd_kernel(PP p) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  fwd_body<UA, LN_M>(p, sm);
+}
+
+__global__ void __launch_bounds__(NTH) fwd_kernel_big(PP p) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  fwd_body<UA_BIG, LN_BIG>(p, sm);
 }
 
 // ======================================================================= backward roles
@@ -968,8 +983,134 @@ __device__ __forceinline__ void bwd_G4(const PP& p, int i4, float* sm) {
   }
 }
 
-__global__ void __launch_bounds__(NTH) bwd_kernel(PP p) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+// G4 for a wide recurrent input (D <= 1024): the same adjoint as bwd_G4, laid out for 160 KB of LDS -
+//   LN1' in two LDS passes (wave_ln_bwd_prep: x <- xh, dy <- dz in place) instead of registers, the LN1 parameter
+//   partials taken before the GEMM, dx written over dz in R (the GEMM's A operand and, behind the hand-off, the
+//   stored weight-gradient input), the GEMM's cross-wave reduction in the then-dead xh tile As.
+// LDS (floats): As [16][D+4] | R [16][D+4] | l1w [D] | l1b [D] | st 48 | ct 512 | flag 16 | fpre 7 * 512 + 32.
+__host__ __device__ inline int lds_G4_big(int D) { return 32 * (D + 4) + 2 * D + 48 + 512 + 16 + 7 * 512 + 32; }
+
+__device__ __forceinline__ void bwd_G4_big(const PP& p, int i4, float* sm) {
+  const bool first_wg = i4 == 0;
+  const int B = p.B, S = p.S, D = p.D, H = p.H, HD = H + D, C = p.C, T = p.T;
+  const int n3 = HD / 16, n4 = S / 32;
+  const int w = threadIdx.x >> 6, lda = D + 4, n0 = i4 * 32;
+  float* As = sm;
+  float* R = As + 16 * lda;
+  float* l1w = R + 16 * lda;
+  float* l1b = l1w + D;
+  float* st = l1b + D;
+  float* ct = st + 48;
+  int* flag = (int*)(ct + 512);
+  float* fpre = (float*)(flag + 16);  // as bwd_G4: [7][512] unimix-adjoint terms, [32] LN1 row statistics
+  float* red = As;                    // [16 waves][16][32]: 8192 floats <= 16 (D + 4)
+  WTile<2, U4_BIG> wt;
+  wload<2, U4_BIG>(wt, p.WzT + (size_t)n0 * D, D, D, w);
+  stage_vec(l1w, p.ln1w, D);
+  stage_vec(l1b, p.ln1b, D);
+  const u32 e3 = shard_count(p.hid / 16 + H / 16, n3);
+  if (threadIdx.x < B) {
+    fpre[3584 + threadIdx.x] = p.m1[(size_t)(T - 1) * B + threadIdx.x];
+    fpre[3600 + threadIdx.x] = p.r1[(size_t)(T - 1) * B + threadIdx.x];
+  }
+  __syncthreads();
+  for (int t = T - 1; t >= 0; --t) {
+    PROF(6, 0);
+    stage(As, lda, p.xr + (size_t)t * B * D, D, B, D);
+    const int eb = threadIdx.x >> 5, ec = threadIdx.x & 31, ebb = eb < B ? eb : 0;
+    const size_t eo = (size_t)(t > 0 ? t - 1 : 0) * B * S + (size_t)ebb * S + n0 + ec;
+    const bool eok = threadIdx.x < 512 && t > 0;
+    const float el = eok ? p.logits[eo] : 0.f;
+    if (threadIdx.x < 512) {
+      fpre[2048 + threadIdx.x] = eok ? p.dmixed[eo] : 0.f;
+      fpre[2560 + threadIdx.x] = (eok && p.dpost) ? p.dpost[eo] : 0.f;
+      fpre[3072 + threadIdx.x] = eok ? 1.f - p.first[(size_t)t * B + ebb] : 0.f;
+    }
+    if (threadIdx.x < 512 && t > 0) {
+      float q = 0.f, pm = 0.f, m = el, cl = 0.f;
+      if (p.alpha > 0.f) {
+        const float mx = seg_max_f(el, C);
+        const float e = __expf(el - mx);
+        q = e / seg_sum_f(e, C);
+        pm = (1.f - p.alpha) * q + p.alpha / C;
+        cl = (pm <= FEPS || pm >= 1.f - FEPS) ? 1.f : 0.f;
+        m = logf(fminf(fmaxf(pm, FEPS), 1.f - FEPS));
+      }
+      const float mx2 = seg_max_f(m, C);
+      const float e2 = __expf(m - mx2);
+      fpre[threadIdx.x] = q;
+      fpre[512 + threadIdx.x] = pm;
+      fpre[1024 + threadIdx.x] = e2 / seg_sum_f(e2, C);
+      fpre[1536 + threadIdx.x] = cl;
+    }
+    if (!wait_ctr(p, 2, e3, T - t, 14, flag)) return;
+    PROF(6, 1);
+    stage_wt(R, lda, p.dcat + (size_t)t * B * HD + H, HD, B, D);
+    __syncthreads();
+    PROF(6, 5);
+    float s1 = 0.f, s2 = 0.f, rsw = 0.f;
+    if (w < B) {
+      rsw = fpre[3600 + w];
+      wave_ln_bwd_prep(As + w * lda, R + w * lda, l1w, l1b, D, p.act1, fpre[3584 + w], rsw, s1, s2);
+    }
+    __syncthreads();
+    {  // LN1 parameter partials of this workgroup's column range (xh in As, dz in R), then dx over dz
+      int lo, hi;
+      part_range(D, i4, n4, lo, hi);
+      ln_param_partials(As, lda, R, lda, B, lo, hi, p.p1g + (size_t)t * p.ldp, p.p1b + (size_t)t * p.ldp);
+    }
+    __syncthreads();
+    if (w < B) {
+      const int s = threadIdx.x & 63;
+      float* xr = As + w * lda;
+      float* dr = R + w * lda;
+      for (int k = s; k < D; k += 64) dr[k] = rsw * (dr[k] * l1w[k] - s1 - xr[k] * s2);
+    }
+    __syncthreads();
+    PROF(6, 6);
+    auto tail = [&]() {  // dx (weight-gradient input) behind the hand-off
+      int lo, hi;
+      part_range(B * D, i4, n4, lo, hi);
+      float* dx = p.dx + (size_t)t * B * D;
+      for (int e = lo + threadIdx.x; e < hi; e += NTH) dx[e] = R[(e / D) * lda + e % D];
+      __syncthreads();  // As / R are rewritten by the next step
+    };
+    if (t == 0) {
+      tail();
+      break;
+    }
+    PROF(6, 2);
+    gemm_reg<2, U4_BIG>(wt, R, lda, D, red, ct);
+    PROF(6, 3);
+    if (threadIdx.x < 512) {
+      const float ds = fpre[2560 + threadIdx.x] + fpre[3072 + threadIdx.x] * ct[threadIdx.x];
+      const float q = fpre[threadIdx.x], pm = fpre[512 + threadIdx.x], pr = fpre[1024 + threadIdx.x];
+      const bool clamped = fpre[1536 + threadIdx.x] != 0.f;
+      float gm = fpre[2048 + threadIdx.x];
+      const float dot = seg_sum_f(pr * ds, C);
+      gm += pr * (ds - dot);
+      float dl;
+      if (p.alpha > 0.f) {
+        const float wv = clamped ? 0.f : (1.f - p.alpha) * gm / pm;
+        dl = q * (wv - seg_sum_f(q * wv, C));
+      } else {
+        dl = gm;
+      }
+      if (eb < B) st_wt(p.dlog + eo, dl);
+    }
+    PROF(6, 7);
+    arrive(p.sync + 3 * NSH * SHW);
+    PROF(6, 4);
+    tail();
+    if (threadIdx.x < B) {
+      fpre[3584 + threadIdx.x] = p.m1[(size_t)(t - 1) * B + threadIdx.x];
+      fpre[3600 + threadIdx.x] = p.r1[(size_t)(t - 1) * B + threadIdx.x];
+    }
+  }
+}
+
+template <bool BIG>
+__device__ __forceinline__ void bwd_body(const PP& p, float* sm) {
   const int n1 = p.hid / 16, n2 = p.H / 16, n3 = (p.H + p.D) / 16;
   const int bid = blockIdx.x;
   if (bid < n1)
@@ -978,8 +1119,20 @@ __global__ void __launch_bounds__(NTH) bwd_kernel(PP p) {
     bwd_G2(p, bid - n1, sm);
   else if (bid < n1 + n2 + n3)
     bwd_G3(p, bid - n1 - n2, sm);
+  else if constexpr (BIG)
+    bwd_G4_big(p, bid - n1 - n2 - n3, sm);
   else
     bwd_G4(p, bid - n1 - n2 - n3, sm);
+}
+
+__global__ void __launch_bounds__(NTH) bwd_kernel(PP p) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  bwd_body<false>(p, sm);
+}
+
+__global__ void __launch_bounds__(NTH) bwd_kernel_big(PP p) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  bwd_body<true>(p, sm);
 }
 
 __global__ void zero_kernel(u32* w, int n) {
@@ -1000,23 +1153,33 @@ int scanp_sync_words() { return ERRW + SHW; }
 int scanp_fwd_grid(int S, int H, int hid) { return 3 * H / 16 + hid / 16 + S / 32; }
 int scanp_bwd_grid(int S, int D, int H, int hid) { return hid / 16 + H / 16 + (H + D) / 16 + S / 32; }
 
+// Form of a shape: 0 = the register-tile form (D <= 512), 1 = the wide-input form (fwd_kernel_big / bwd_kernel_big,
+// H + D <= 1280, D <= 1024), -1 = not covered.
+static bool scanp_caps(int B, int S, int D, int H, int hid, int C, bool big) {
+  if (B < 1 || B > 16 || C < 1 || C > 32 || (32 % C) != 0 || S % 32 || D % 16 || H % 16 || hid % 16) return false;
+  if (H > 16 * 16 * UB || hid > 16 * 16 * UC) return false;
+  if (S > 16 * 16 * U1 || hid > 16 * 16 * U2 || 3 * H > 16 * 16 * U3 || H > 64 * GRU_M) return false;
+  if (hid > 64 * LN_M) return false;
+  if (3 * H / 16 > 128) return false;  // Chan combine: two partials per lane
+  if (!big) return H + D <= 16 * 16 * UA && D <= 16 * 16 * U4 && D <= 64 * LN_M;
+  return H + D <= 16 * 16 * UA_BIG && D <= 16 * 16 * U4_BIG && D <= 64 * LN_BIG && 16 * (D + 4) >= 8192;
+}
+
 int scanp_fwd_lds(int S, int D, int H, int hid, int C) {
   return 4 * std::max(std::max(lds_A(D, H), lds_B(H)), lds_C(hid, S, C, D));
 }
 
-int scanp_bwd_lds(int S, int D, int H, int hid) {
-  return 4 * std::max(std::max(lds_G1(S), lds_G2(hid)), std::max(lds_G3(H), lds_G4(D)));
+static int scanp_bwd_lds_form(int S, int D, int H, int hid, bool big) {
+  return 4 * std::max(std::max(lds_G1(S), lds_G2(hid)), std::max(lds_G3(H), big ? lds_G4_big(D) : lds_G4(D)));
 }
 
-// Shape gate (register tile caps, LDS, residency of every workgroup): mirrors the kernels.
-bool scanp_supported(int B, int S, int D, int H, int hid, int C) {
-  if (B < 1 || B > 16 || C < 1 || C > 32 || (32 % C) != 0 || S % 32 || D % 16 || H % 16 || hid % 16) return false;
-  if (H + D > 16 * 16 * UA || H > 16 * 16 * UB || hid > 16 * 16 * UC) return false;
-  if (S > 16 * 16 * U1 || hid > 16 * 16 * U2 || 3 * H > 16 * 16 * U3 || D > 16 * 16 * U4 || H > 64 * GRU_M) return false;
-  if (D > 64 * LN_M || hid > 64 * LN_M) return false;
-  if (3 * H / 16 > 128) return false;  // Chan combine: two partials per lane
+int scanp_bwd_lds(int S, int D, int H, int hid) {
+  return scanp_bwd_lds_form(S, D, H, hid, !scanp_caps(1, S, D, H, hid, 1, false));
+}
+
+static bool scanp_resident(int S, int D, int H, int hid, int C, bool big) {
   const int mx = 160 * 1024;
-  if (scanp_fwd_lds(S, D, H, hid, C) > mx || scanp_bwd_lds(S, D, H, hid) > mx) return false;
+  if (scanp_fwd_lds(S, D, H, hid, C) > mx || scanp_bwd_lds_form(S, D, H, hid, big) > mx) return false;
   int dev = 0, cus = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1024,36 +1187,49 @@ bool scanp_supported(int B, int S, int D, int H, int hid, int C) {
   // must fit the occupancy the compiler/runtime report for these kernels at their LDS size - not just
   // the CU count.  Another process or stream sharing the CUs can still starve a wave: the bounded
   // waits + the sticky health word (check_scan_health on the host) catch that at run time.
-  const void* fk = (const void*)fwd_kernel;
+  const void* fk = big ? (const void*)fwd_kernel_big : (const void*)fwd_kernel;
+  const void* bk = big ? (const void*)bwd_kernel_big : (const void*)bwd_kernel;
   set_lds(fk, 160 * 1024);
-  set_lds((const void*)bwd_kernel, 160 * 1024);
+  set_lds(bk, 160 * 1024);
   int occ_f = 0, occ_b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, fk, NTH, scanp_fwd_lds(S, D, H, hid, C)) !=
-          hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_b, (const void*)bwd_kernel, NTH, scanp_bwd_lds(S, D, H, hid)) !=
-          hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_f, fk, NTH, scanp_fwd_lds(S, D, H, hid, C)) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_b, bk, NTH, scanp_bwd_lds_form(S, D, H, hid, big)) != hipSuccess)
     return false;
   return scanp_fwd_grid(S, H, hid) <= cus * occ_f && scanp_bwd_grid(S, D, H, hid) <= cus * occ_b;
 }
 
+int scanp_form(int B, int S, int D, int H, int hid, int C) {
+  // memo of the last shapes asked (every launch asks; the residency query is a host API round trip)
+  struct Q { int key[7]; int form; };
+  static Q memo[8];
+  static int nmemo = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const int key[7] = {B, S, D, H, hid, C, dev};
+  for (int i = 0; i < nmemo; ++i)
+    if (std::equal(key, key + 7, memo[i].key)) return memo[i].form;
+  int form = -1;
+  for (int f = 0; f < 2 && form < 0; ++f)
+    if (scanp_caps(B, S, D, H, hid, C, f == 1) && scanp_resident(S, D, H, hid, C, f == 1)) form = f;
+  Q& q = memo[nmemo < 8 ? nmemo++ : 7];
+  std::copy(key, key + 7, q.key);
+  q.form = form;
+  return form;
+}
+
+// Shape gate (register tile caps, LDS, residency of every workgroup): mirrors the kernels.
+bool scanp_supported(int B, int S, int D, int H, int hid, int C) { return scanp_form(B, S, D, H, hid, C) >= 0; }
+
 void launch_scanp_fwd(const PP& p, hipStream_t st) {
-  static bool init = false;
-  if (!init) {
-    set_lds((const void*)fwd_kernel, 160 * 1024);
-    init = true;
-  }
+  const bool big = scanp_form(p.B, p.S, p.D, p.H, p.hid, p.C) == 1;
   hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(256), 0, st, p.sync, scanp_sync_words());
-  hipLaunchKernelGGL(fwd_kernel, dim3(scanp_fwd_grid(p.S, p.H, p.hid)), dim3(NTH), scanp_fwd_lds(p.S, p.D, p.H, p.hid, p.C),
-                     st, p);
+  hipLaunchKernelGGL(big ? fwd_kernel_big : fwd_kernel, dim3(scanp_fwd_grid(p.S, p.H, p.hid)), dim3(NTH),
+                     scanp_fwd_lds(p.S, p.D, p.H, p.hid, p.C), st, p);
 }
 
 void launch_scanp_bwd(const PP& p, hipStream_t st) {
-  static bool init = false;
-  if (!init) {
-    set_lds((const void*)bwd_kernel, 160 * 1024);
-    init = true;
-  }
+  const bool big = scanp_form(p.B, p.S, p.D, p.H, p.hid, p.C) == 1;
   hipLaunchKernelGGL(zero_kernel, dim3(1), dim3(256), 0, st, p.sync, scanp_sync_words());
-  hipLaunchKernelGGL(bwd_kernel, dim3(scanp_bwd_grid(p.S, p.D, p.H, p.hid)), dim3(NTH), scanp_bwd_lds(p.S, p.D, p.H, p.hid),
-                     st, p);
+  hipLaunchKernelGGL(big ? bwd_kernel_big : bwd_kernel, dim3(scanp_bwd_grid(p.S, p.D, p.H, p.hid)), dim3(NTH),
+                     scanp_bwd_lds_form(p.S, p.D, p.H, p.hid, big), st, p);
 }

@@ -75,9 +75,15 @@ def test_dv3_graph_matches_eager_losses():
                                          (256, 1024, 256, 16, 8)])  # the prey preset: deter 256, dense 1024
 def test_fused_rssm_scan_matches_python_scan(H, D, hid, B, T, impl):
     """The fused scans (persist: one persistent launch per direction; scan4: 4+4 MFMA launches/step;
-    scan9: 9+9 launches/step; batched weight grads) vs the python step loop, same noise.  D = 1024 is beyond the
-    persistent scan's register tiles: "persist" falls back to scan4 there."""
-    _check_scan_vs_python(H, D, hid, B, T, impl, expect="scan4" if (impl == "persist" and D > 512) else None)
+    scan9: 9+9 launches/step; batched weight grads) vs the python step loop, same noise.  D = 1024 (the prey
+    preset) runs the persistent scan's wide-input form (fwd_kernel_big / bwd_kernel_big)."""
+    _check_scan_vs_python(H, D, hid, B, T, impl)
+
+
+def test_persistent_scan_prey_shape_T64():
+    """The fork's own preset (exp=dreamer_v3_prey: deter 256, dense 1024, hidden 256, stoch 32x32) through the
+    persistent scan's wide-input form over a whole B 16 x T 64 sequence, fwd + bwd vs the python loop."""
+    _check_scan_vs_python(256, 1024, 256, 16, 64, "persist", tol=(5e-3, 5e-4), gtol=(5e-3, 5e-3))
 
 
 @pytest.mark.parametrize("impl", ["persist", "scan4"])
