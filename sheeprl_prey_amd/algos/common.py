@@ -129,6 +129,16 @@ def episode_stats(infos: Dict[str, Any]):
             yield i, ep["episode"]["r"], ep["episode"]["l"]
 
 
+def episode_success(infos: Dict[str, Any]):
+    """Yield (env_idx, 1.0 / 0.0) for finished episodes whose final info carries the env's ``is success`` flag (the
+    prey env's goal-reached flag, ``prey_env/gymnasium_env_bins.py:195``); nothing for envs without one."""
+    if "final_info" not in infos:
+        return
+    for i, ep in enumerate(infos["final_info"]):
+        if ep is not None and "episode" in ep and "is success" in ep:
+            yield i, float(bool(np.asarray(ep["is success"]).reshape(-1)[0]))
+
+
 class PolynomialLR:
     """``torch.optim.lr_scheduler.PolynomialLR`` for the flat optimisers (state-dict compatible)."""
 

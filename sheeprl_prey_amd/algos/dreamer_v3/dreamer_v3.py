@@ -34,6 +34,7 @@ from sheeprl_prey_amd.algos.common import (
     build_envs,
     check_obs_keys,
     episode_stats,
+    episode_success,
     load_resume,
     log_throughput,
     setup_logger,
@@ -485,7 +486,7 @@ class DreamerV3Trainer:
 
 def make_aggregator(cfg) -> MetricAggregator:
     sync = cfg.metric.sync_on_compute
-    names = ["Rewards/rew_avg", "Game/ep_len_avg", "Params/exploration_amout", *METRIC_KEYS]
+    names = ["Rewards/rew_avg", "Game/ep_len_avg", "Game/success_rate", "Params/exploration_amout", *METRIC_KEYS]
     return MetricAggregator({n: MeanMetric(sync_on_compute=sync) for n in names})
 
 
@@ -641,6 +642,8 @@ def main(runner, cfg: Dict[str, Any]):
             aggregator.update("Rewards/rew_avg", ep_rew)
             aggregator.update("Game/ep_len_avg", ep_len)
             runner.print(f"Rank-0: policy_step={policy_step}, reward_env_{i}={ep_rew[-1]}")
+        for _, ok in episode_success(infos):
+            aggregator.update("Game/success_rate", ok)  # goal reached (prey env ``is success``), not in the reference
 
         updates_before_training -= 1
         if train_now:
