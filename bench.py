@@ -627,7 +627,7 @@ def bench_sac(args):
     trainer = SACTrainer(runner, cfg, agent, actor_opt, qf_opt, alpha_opt)
     aggregator = make_aggregator(cfg)
     rb = ReplayBuffer(cfg.buffer.size // (ne * world), ne, device=device)
-    loop = SACInteraction(runner, cfg, envs, agent, rb, obs_dim)
+    loop = SACInteraction(runner, cfg, envs, agent, rb, obs_dim, policy=trainer.policy())
     loop.reset(cfg.seed + rank)
     learning_starts = max(int(cfg.algo.learning_starts) // (ne * world), 1)
     ema_every = cfg.algo.critic.target_network_frequency // (ne * world) + 1
@@ -681,7 +681,8 @@ def bench_sac(args):
             "data": "synthetic walker_walk-shaped control env (24-dim state, 6-dim action; envs/synthetic.py), random-init weights",
             "config": {"model": "SAC actor 2x256 + 2 critics 2x256 (exp=sac)", "global_batch": cfg.per_rank_batch_size * world,
                        "num_envs_per_rank": ne, "gradient_steps_per_env_step": cfg.algo.per_rank_gradient_steps,
-                       "parallelism": f"dp{world}", "update_mode": trainer.critic_step.mode},
+                       "parallelism": f"dp{world}", "update_mode": trainer.critic_step.mode,
+                       "fused_update": trainer.fused is not None},
             "dp_param_spread": spread,
         }), flush=True)
     envs.close()

@@ -59,7 +59,7 @@ try:
         CppExtension(
             name="sheeprl_prey_amd.ops._C",
             sources=[os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "conv_bindings.cpp"),
-                     os.path.join(CSRC, "ext_bindings.cpp")],
+                     os.path.join(CSRC, "ext_bindings.cpp"), os.path.join(CSRC, "sac_bindings.cpp")],
             include_dirs=[os.path.join(HERE, CSRC), os.path.join(ROCM, "include")],
             library_dirs=[os.path.join(ROCM, "lib")],
             libraries=["amdhip64", "c10_hip", "torch_hip"],

@@ -56,6 +56,13 @@ class SACTrainer:
         self.actor_q_reduce = actor_q_reduce
         self.fused_critic = os.environ.get("SRL_SAC_FUSED", "1") != "0"
         agent.bind_target_slab(qf_optimizer)
+        # the whole gradient step as seven fused launches (algos/sac/fused.py) when the agent fits its kernels
+        from sheeprl_prey_amd.algos.sac.fused import SACFusedUpdate
+
+        opts = (actor_optimizer, qf_optimizer, alpha_optimizer)
+        self.fused = (SACFusedUpdate(agent, actor_optimizer, qf_optimizer, alpha_optimizer, self.gamma,
+                                     reduce_min=actor_q_reduce == "min")
+                      if self.fused_critic and SACFusedUpdate.supported(agent, opts) else None)
         self.critic_params = list(agent.critic.parameters())
         self.actor_params = [p for p in agent.actor.parameters() if p.requires_grad]
         self._st: Dict[str, Tensor] = {}
@@ -68,6 +75,9 @@ class SACTrainer:
 
     # ------------------------------------------------------------------ critic
     def _critic_fwd_bwd(self, d: Dict[str, Tensor]) -> None:
+        if self.fused is not None:
+            self._st["qf_loss"] = self.fused.critic(d)
+            return
         a = self.agent
         target = a.get_next_target_q_values(d["next_observations"], d["rewards"], d["dones"], self.gamma)
         # the twin-Q forward, loss and backward as two kernels (K15) when the critic layout allows
@@ -87,12 +97,19 @@ class SACTrainer:
             self.runner.sync_gradients(self.qf_optimizer)
 
     def _critic_apply(self, d: Dict[str, Tensor]) -> Dict[str, Tensor]:
-        self.qf_optimizer.step()
-        self.agent.qfs_target_ema(d["ema_w"])
+        if self.fused is not None:
+            self.fused.critic_apply(d["ema_w"])
+        else:
+            self.qf_optimizer.step()
+            self.agent.qfs_target_ema(d["ema_w"])
         return {"Loss/value_loss": self._st["qf_loss"]}
 
     # ------------------------------------------------------------------ actor + alpha
     def _actor_fwd_bwd(self, d: Dict[str, Tensor]) -> None:
+        if self.fused is not None:
+            losses = self.fused.actor(d["observations"])
+            self._st["actor_loss"], self._st["alpha_loss"] = losses[0], losses[1]
+            return
         a = self.agent
         obs = d["observations"]
         actions, logp = a.get_actions_and_log_probs(obs)
@@ -114,8 +131,11 @@ class SACTrainer:
             self.runner.sync_gradients(self.alpha_optimizer)
 
     def _actor_apply(self, d: Dict[str, Tensor]) -> Dict[str, Tensor]:
-        self.actor_optimizer.step()
-        self.alpha_optimizer.step()
+        if self.fused is not None:
+            self.fused.actor_apply()
+        else:
+            self.actor_optimizer.step()
+            self.alpha_optimizer.step()
         return {"Loss/policy_loss": self._st["actor_loss"], "Loss/alpha_loss": self._st["alpha_loss"]}
 
     # ------------------------------------------------------------------ API
@@ -131,12 +151,24 @@ class SACTrainer:
         dev = data["rewards"].device
         d = dict(data)
         d["ema_w"] = self.ema_weight(do_ema, dev)
+        if self.fused is not None:
+            self.fused.attach(aggregator)
         out = dict(self.critic_step(d))
         out.update(self.actor_step({"observations": data["observations"]}))
-        if aggregator is not None:
-            for k, v in out.items():
-                if k in aggregator:
-                    aggregator.update(k, v)
+        self.record(out, aggregator)
+
+    def record(self, out: Dict[str, Tensor], aggregator: Optional[MetricAggregator]) -> None:
+        """Loss metrics into ``aggregator`` (the fused update accumulates its own on the device)."""
+        if aggregator is None:
+            return
+        for k, v in out.items():
+            if k in aggregator and not (self.fused is not None and k in self.fused.KEYS):
+                aggregator.update(k, v)
+
+    def policy(self):
+        """The player's action function: the fused one-launch sampler when the update is fused, else None
+        (``SACInteraction`` then runs ``agent.actor``)."""
+        return self.fused.act if self.fused is not None else None
 
 
 def make_aggregator(cfg) -> MetricAggregator:
@@ -226,7 +258,7 @@ class SACInteraction:
     pinned copy sliced on the device (instead of five synchronous pageable copies); the staging buffer
     is rewritten only after an event recorded behind its last copy has completed."""
 
-    def __init__(self, runner, cfg, envs, agent, rb, obs_dim: int):
+    def __init__(self, runner, cfg, envs, agent, rb, obs_dim: int, policy=None):
         self.runner, self.cfg, self.envs, self.agent, self.rb = runner, cfg, envs, agent, rb
         self.obs_dim = obs_dim
         self.n_env = int(cfg.env.num_envs)
@@ -238,7 +270,8 @@ class SACInteraction:
 
             self.stage = torch.empty((self.n_env, 2 * obs_dim + self.act_dim + 2), dtype=torch.float32).pin_memory()
             self.staged = torch.cuda.Event()  # the last copy out of `stage` (random-action steps have no readback)
-            self.player = GraphedStep(lambda d: {"a": agent.actor(d["obs"])[0]}, warmup=2, enabled=runner.cuda_graphs,
+            act = policy if policy is not None else (lambda o: agent.actor(o)[0])
+            self.player = GraphedStep(lambda d: {"a": act(d["obs"])}, warmup=2, enabled=runner.cuda_graphs,
                                       name="sac_player")
         self._last = None
 
@@ -357,7 +390,7 @@ def run_sac_family(runner, cfg: Dict[str, Any], variant: str = "sac"):
     warn_log_ckpt_every(cfg, policy_steps_per_update)
     ema_every = cfg.algo.critic.target_network_frequency // policy_steps_per_update + 1
 
-    loop = SACInteraction(runner, cfg, envs, agent, rb, obs_dim)
+    loop = SACInteraction(runner, cfg, envs, agent, rb, obs_dim, policy=trainer.policy())
     loop.reset(cfg.seed)
 
     for update in range(start_step, num_updates + 1):
@@ -422,7 +455,6 @@ def _eager_train(trainer: SACTrainer, bd, do_ema, aggregator) -> None:
     trainer._actor_fwd_bwd(d)
     trainer._coll_actor()
     out.update(trainer._actor_apply(d))
-    if aggregator is not None:
-        for k, v in out.items():
-            if k in aggregator:
-                aggregator.update(k, v)
+    if trainer.fused is not None:
+        trainer.fused.attach(aggregator)
+    trainer.record(out, aggregator)

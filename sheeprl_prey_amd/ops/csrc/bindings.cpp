@@ -1129,10 +1129,12 @@ void ppo_mlp_train(std::vector<std::vector<int64_t>> layers, std::vector<int64_t
 
 void register_conv(pybind11::module& m);
 void register_ext(pybind11::module& m);
+void register_sac(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_conv(m);
   register_ext(m);
+  register_sac(m);
   m.def("set_gru_vec", &set_gru_vec);  // float4 wide-row LN-GRU forward on (default) / off (A/B, tests)
   m.def("ln_gru_into", &ln_gru_into, pybind11::arg("x"), pybind11::arg("h"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("eps"), pybind11::arg("out"), pybind11::arg("mean") = pybind11::none(),

@@ -30,7 +30,8 @@ void launch_sac_critic_fwd(const float* obs, const float* act, const float* y, c
                            hipStream_t st);
 void launch_sac_critic_wgrad(const float* X, const float* H1, const float* H2, const float* DH1, const float* DH2,
                              const float* DQ, const float* g, float* dW1, float* db1, float* dW2, float* db2, float* dW3,
-                             float* db3, int M, int IN, int H, int n, hipStream_t st);
+                             float* db3, int M, int IN, int H, int n, const float* lossp, int nlp, float* loss,
+                             hipStream_t st);
 void launch_wm_loss_fwd(const float* kl_loss, const float* obs, const float* rew, const float* logit, const float* done,
                         const float* kl, int R, float kl_reg, float scale, float* total, float* means, hipStream_t st);
 void launch_wm_loss_bwd(const float* logit, const float* done, const float* g, int R, float kl_reg, float scale, float* d_kll,
@@ -386,7 +387,7 @@ std::vector<torch::Tensor> sac_critic_wgrad(torch::Tensor X, torch::Tensor H1, t
   launch_sac_critic_wgrad(X.data_ptr<float>(), H1.data_ptr<float>(), H2.data_ptr<float>(), DH1.data_ptr<float>(),
                           DH2.data_ptr<float>(), DQ.data_ptr<float>(), g.data_ptr<float>(), dW1.data_ptr<float>(),
                           db1.data_ptr<float>(), dW2.data_ptr<float>(), db2.data_ptr<float>(), dW3.data_ptr<float>(),
-                          db3.data_ptr<float>(), (int)M, (int)IN, (int)H, (int)n, stream());
+                          db3.data_ptr<float>(), (int)M, (int)IN, (int)H, (int)n, nullptr, 0, nullptr, stream());
   return {dW1, db1, dW2, db2, dW3, db3};
 }
 

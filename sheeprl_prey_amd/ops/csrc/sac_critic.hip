@@ -16,6 +16,7 @@
 //                scalar: the launch is graph-capturable).
 // Weights are the stacked ensemble layout [n, out, in] (models/ensemble.py).
 #include "common.h"
+#include "sac_tiles.h"
 
 namespace srl {
 namespace saccrit {
@@ -24,7 +25,7 @@ constexpr int NTH = 512;
 constexpr int NW = NTH / 64;
 constexpr int ROWS = 16;
 
-typedef float floatx4 __attribute__((ext_vector_type(4)));
+using namespace sactile;
 
 struct FP {
   const float* obs;
@@ -46,62 +47,6 @@ struct FP {
   float* lossp;     // [n * blocks] partial losses
   int M, OD, AD, IN, INp, H, n;
 };
-
-__device__ __forceinline__ float comp(const float4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; }
-
-// The weight operands stream from L2: each helper issues a chunk of KC K-steps of loads before the
-// MFMAs that consume them (one load latency per chunk, not per K-step: the first version waited on
-// every 16-wide K step and spent ~30 us in the forward at M = 256, H = 256).
-constexpr int KC = 8;
-
-// acc (16 rows x 16 cols from weight row n0) += act[16][K] . W[n0.., K]^T ; act in LDS (stride lda), W row-major.
-__device__ __forceinline__ floatx4 tile_gemm_nt(const float* act, int lda, const float* W, int ldw, int n0, int K, int lane) {
-  const int j = lane & 15, q = lane >> 4;
-  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  const float* wr = W + (long)(n0 + j) * ldw + 4 * q;
-  const float* ar = act + j * lda + 4 * q;
-  for (int kb = 0; kb < K; kb += 16 * KC) {
-    float4 w[KC], a[KC];
-#pragma unroll
-    for (int u = 0; u < KC; ++u)
-      if (kb + 16 * u < K) w[u] = *reinterpret_cast<const float4*>(wr + kb + 16 * u);
-#pragma unroll
-    for (int u = 0; u < KC; ++u)
-      if (kb + 16 * u < K) a[u] = *reinterpret_cast<const float4*>(ar + kb + 16 * u);
-#pragma unroll
-    for (int u = 0; u < KC; ++u) {
-      if (kb + 16 * u < K) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a[u], e), comp(w[u], e), acc, 0, 0, 0);
-      }
-    }
-  }
-  return acc;
-}
-
-// acc (16 rows x 16 cols from column n0) += act[16][K] . W[K, n0..]   (W row-major [K][ldw]: read K-major)
-__device__ __forceinline__ floatx4 tile_gemm_nn(const float* act, int lda, const float* W, int ldw, int n0, int K, int lane) {
-  const int j = lane & 15, q = lane >> 4;
-  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  const float* wc = W + n0 + j;
-  const float* ar = act + j * lda + 4 * q;
-  for (int kb = 0; kb < K; kb += 16 * KC) {
-    float w[KC][4];
-#pragma unroll
-    for (int u = 0; u < KC; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) w[u][e] = kb + 16 * u < K ? wc[(long)(kb + 16 * u + 4 * q + e) * ldw] : 0.f;
-#pragma unroll
-    for (int u = 0; u < KC; ++u) {
-      if (kb + 16 * u < K) {
-        const float4 a = *reinterpret_cast<const float4*>(ar + kb + 16 * u);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(comp(a, e), w[u][e], acc, 0, 0, 0);
-      }
-    }
-  }
-  return acc;
-}
 
 __global__ __launch_bounds__(NTH) void critic_fwd_kernel(FP p) {
   extern __shared__ float sm[];
@@ -227,36 +172,11 @@ struct GP {
   float* db2;      // [n, H]
   float* dW3;      // [n, 1, H]
   float* db3;      // [n, 1]
-  int M, IN, INp, H, n;
+  const float* lossp;  // [nlp] partial losses of the forward kernel, or null
+  float* loss;         // their sum (the loss value), written by one extra workgroup when lossp is set
+  int M, IN, INp, H, n, nlp;
   int nb2, nb1;    // workgroups of the dW2 / dW1 roles
 };
-
-// out tile (16 x 16) = sum_r G[r][i0 + i] * A[r][j0 + jj]  (both row-major, row strides ldg / lda); KC/2
-// row steps of loads in flight per chunk
-__device__ __forceinline__ floatx4 tile_wgrad(const float* G, int ldg, const float* A, int lda, int i0, int j0, int M,
-                                              int lane) {
-  const int j = lane & 15, q = lane >> 4;
-  constexpr int RC = KC / 2;
-  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  const float* gc = G + i0 + j;
-  const float* ac = A + j0 + j;
-  for (int kb = 0; kb < M; kb += 16 * RC) {
-    float a[RC][4], b[RC][4];
-#pragma unroll
-    for (int u = 0; u < RC; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = kb + 16 * u + 4 * q + e;
-        a[u][e] = r < M ? gc[(long)r * ldg] : 0.f;
-        b[u][e] = r < M ? ac[(long)r * lda] : 0.f;
-      }
-#pragma unroll
-    for (int u = 0; u < RC; ++u)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][e], b[u][e], acc, 0, 0, 0);
-  }
-  return acc;
-}
 
 __global__ __launch_bounds__(NTH) void critic_wgrad_kernel(GP p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -289,6 +209,15 @@ __global__ __launch_bounds__(NTH) void critic_wgrad_kernel(GP p) {
   b -= p.nb1;  // bias / head workgroups (critic, 64 columns): column sums over the batch, rows split over waves
   __shared__ float red[NW][3][64];
   const int nch = H / 64;
+  if (b == p.n * nch) {  // loss workgroup: the forward's partial losses summed in a fixed order (one wave)
+    if (wave == 0) {
+      float s = 0.f;
+      for (int i = lane; i < p.nlp; i += 64) s += p.lossp[i];
+      s = wave_sum(s);
+      if (lane == 0) *p.loss = s;
+    }
+    return;
+  }
   const int c = b / nch, k = (b - c * nch) * 64 + lane;
   const float* DH1 = p.DH1 + (long)c * M * H;
   const float* DH2 = p.DH2 + (long)c * M * H;
@@ -379,7 +308,8 @@ void launch_sac_critic_fwd(const float* obs, const float* act, const float* y, c
 
 void launch_sac_critic_wgrad(const float* X, const float* H1, const float* H2, const float* DH1, const float* DH2,
                              const float* DQ, const float* g, float* dW1, float* db1, float* dW2, float* db2, float* dW3,
-                             float* db3, int M, int IN, int H, int n, hipStream_t st) {
+                             float* db3, int M, int IN, int H, int n, const float* lossp, int nlp, float* loss,
+                             hipStream_t st) {
   GP p;
   p.X = X;
   p.H1 = H1;
@@ -399,8 +329,11 @@ void launch_sac_critic_wgrad(const float* X, const float* H1, const float* H2, c
   p.INp = (IN + 15) / 16 * 16;
   p.H = H;
   p.n = n;
+  p.lossp = lossp;
+  p.loss = loss;
+  p.nlp = nlp;
   const int nt = H / 16;
   p.nb2 = (n * nt * nt + NW - 1) / NW;
   p.nb1 = (n * nt * (p.INp / 16) + NW - 1) / NW;
-  hipLaunchKernelGGL(critic_wgrad_kernel, dim3(p.nb2 + p.nb1 + n * (H / 64)), dim3(NTH), 0, st, p);
+  hipLaunchKernelGGL(critic_wgrad_kernel, dim3(p.nb2 + p.nb1 + n * (H / 64) + (lossp && loss ? 1 : 0)), dim3(NTH), 0, st, p);
 }

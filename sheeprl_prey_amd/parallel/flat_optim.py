@@ -141,6 +141,16 @@ class FlatOptimizer:
             if p.grad is None or p.grad.data_ptr() != self.flat_grad[off:].data_ptr():
                 p.grad = self.flat_grad[off : off + p.numel()].view_as(p)
 
+    def grad_views(self, params: Iterable[Tensor]) -> List[Tensor]:
+        """The slab views of ``params``' gradients, with every ``.grad`` linked to its view: for kernels that
+        write complete gradients straight into the slab (the fused SAC update) - nothing is zeroed or gathered
+        before the optimiser reads it."""
+        self.wait_grads()
+        self._relink()
+        self._detached = False
+        index = {id(p): i for i, p in enumerate(self.params)}
+        return [self._ov_view(index[id(p)]) for p in params]
+
     def zero_grad(self, set_to_none: bool = True, arm: bool = True) -> None:
         """``set_to_none`` (default): the next backward lets autograd hand each parameter its freshly
         computed gradient (AccumulateGrad steals the buffer: no per-parameter accumulate kernel), and

@@ -17,7 +17,13 @@ from torch import Tensor
 class MeanMetric:
     def __init__(self, sync_on_compute: bool = False, **_):
         self.sync_on_compute = sync_on_compute
+        self._acc: Optional[Tensor] = None
         self.reset()
+
+    def attach(self, acc: Tensor) -> None:
+        """A device accumulator ``[sum, count]`` (float64) that kernels add to every step (the fused SAC update,
+        ``algos/sac/fused.py``): ``compute`` adds it, ``reset`` zeroes it - no per-step copy launch."""
+        self._acc = acc
 
     SLOTS = 512  # device scalars staged before one NaN-filtered reduction
 
@@ -28,6 +34,8 @@ class MeanMetric:
         self._dev_n: Optional[Tensor] = None
         self._slots: Optional[Tensor] = None
         self._used = 0
+        if self._acc is not None:
+            self._acc.zero_()
 
     def _flush(self) -> None:
         if not self._used:
@@ -76,6 +84,10 @@ class MeanMetric:
             self._flush()
             s += float(self._dev_sum.item())
             n += float(self._dev_n.item())
+        if self._acc is not None:
+            a_s, a_n = self._acc.tolist()
+            s += a_s
+            n += a_n
         if self.sync_on_compute and torch.distributed.is_available() and torch.distributed.is_initialized():
             t = torch.tensor([s, n], dtype=torch.float64)
             torch.distributed.all_reduce(t)
