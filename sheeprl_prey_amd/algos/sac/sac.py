@@ -68,10 +68,18 @@ class SACTrainer:
         self._st: Dict[str, Tensor] = {}
         self._ema_w: Dict[Any, Tensor] = {}
         use_graphs = bool(cfg.fabric.get("cuda_graphs", False)) if graphs is None else graphs
-        self.critic_step = PhasedStep(runner, [self._critic_fwd_bwd, self._critic_apply], [self._coll_critic],
-                                      graphs=use_graphs, name="sac_critic")
-        self.actor_step = PhasedStep(runner, [self._actor_fwd_bwd, self._actor_apply], [self._coll_actor],
-                                     graphs=use_graphs, name="sac_actor")
+        if self.fused is not None:
+            # the whole gradient step is one captured graph (one replay, one set of static inputs)
+            self.step = PhasedStep(runner, [self._critic_fwd_bwd, self._critic_apply, self._actor_fwd_bwd,
+                                            self._actor_apply], [self._coll_critic, _no_coll, self._coll_actor],
+                                   graphs=use_graphs, name="sac_step")
+            self.critic_step = self.actor_step = self.step
+        else:
+            self.critic_step = PhasedStep(runner, [self._critic_fwd_bwd, self._critic_apply], [self._coll_critic],
+                                          graphs=use_graphs, name="sac_critic")
+            self.actor_step = PhasedStep(runner, [self._actor_fwd_bwd, self._actor_apply], [self._coll_actor],
+                                         graphs=use_graphs, name="sac_actor")
+        self._ema_static: Optional[Tensor] = None
 
     # ------------------------------------------------------------------ critic
     def _critic_fwd_bwd(self, d: Dict[str, Tensor]) -> None:
@@ -133,6 +141,8 @@ class SACTrainer:
     def _actor_apply(self, d: Dict[str, Tensor]) -> Dict[str, Tensor]:
         if self.fused is not None:
             self.fused.actor_apply()
+            return {"Loss/value_loss": self._st["qf_loss"], "Loss/policy_loss": self._st["actor_loss"],
+                    "Loss/alpha_loss": self._st["alpha_loss"]}
         else:
             self.actor_optimizer.step()
             self.alpha_optimizer.step()
@@ -151,11 +161,43 @@ class SACTrainer:
         dev = data["rewards"].device
         d = dict(data)
         d["ema_w"] = self.ema_weight(do_ema, dev)
+        self._ema_static = None  # the copy-in below rewrites the static EMA weight
         if self.fused is not None:
             self.fused.attach(aggregator)
-        out = dict(self.critic_step(d))
-        out.update(self.actor_step({"observations": data["observations"]}))
+            out = dict(self.step(d))
+        else:
+            out = dict(self.critic_step(d))
+            out.update(self.actor_step({"observations": data["observations"]}))
         self.record(out, aggregator)
+
+    TRAIN_KEYS = ("observations", "next_observations", "actions", "rewards", "dones")
+
+    def train_from_buffer(self, rb, batch_size: int, n_batches: int, do_ema: bool,
+                          aggregator: Optional[MetricAggregator] = None) -> bool:
+        """``n_batches`` SAC updates on minibatches drawn by ONE device launch each straight into the captured
+        step's static inputs (``ReplayBuffer.sample_rows_into``): per update one sampling kernel + one graph replay,
+        no host-side index draw / gather / copy-in.  One GPU, fused update, captured step, replay keys exactly the
+        train keys; False (nothing done) otherwise - the caller takes the regular path."""
+        impl = getattr(self.critic_step, "_impl", None)
+        if (self.fused is None or self.critic_step.mode != "single" or impl is None or impl.graph is None
+                or set(rb.keys()) != set(self.TRAIN_KEYS)):
+            return False
+        st = impl.static_in
+        out = {k: st[k] for k in self.TRAIN_KEYS}
+        if any(v.shape[0] != batch_size for v in out.values()):
+            return False
+        ema = self.ema_weight(do_ema, st["ema_w"].device)
+        if self._ema_static is not ema:
+            st["ema_w"].copy_(ema)
+            self._ema_static = ema
+        self.fused.attach(aggregator)
+        for i in range(n_batches):
+            if not rb.sample_rows_into(out, batch_size):
+                if i == 0:
+                    return False
+                raise RuntimeError("SAC: the device replay draw stopped applying mid-update")
+            impl.replay_static()
+        return True
 
     def record(self, out: Dict[str, Tensor], aggregator: Optional[MetricAggregator]) -> None:
         """Loss metrics into ``aggregator`` (the fused update accumulates its own on the device)."""
@@ -169,6 +211,10 @@ class SACTrainer:
         """The player's action function: the fused one-launch sampler when the update is fused, else None
         (``SACInteraction`` then runs ``agent.actor``)."""
         return self.fused.act if self.fused is not None else None
+
+
+def _no_coll(dry: bool = False) -> None:
+    pass
 
 
 def make_aggregator(cfg) -> MetricAggregator:
@@ -233,11 +279,16 @@ def sac_train_update(trainer: SACTrainer, runner, cfg, rb, update: int, learning
     if update < learning_starts:
         return False
     training_steps = learning_starts if update == learning_starts else 1
+    do_ema = update % ema_every == 0
+    if runner.world_size == 1 and not cfg.buffer.sample_next_obs:
+        with timer("Time/train_time"):
+            if trainer.train_from_buffer(rb, cfg.per_rank_batch_size,
+                                         max(training_steps, 1) * cfg.algo.per_rank_gradient_steps, do_ema, aggregator):
+                return True
     sample = rb.sample(max(training_steps, 1) * cfg.algo.per_rank_gradient_steps * cfg.per_rank_batch_size,
                        sample_next_obs=cfg.buffer.sample_next_obs)
     data = gather_and_shard(runner, sample, cfg).to(runner.device)
     with timer("Time/train_time"):
-        do_ema = update % ema_every == 0
         for start in range(0, data.shape[0], cfg.per_rank_batch_size):
             batch = data[start : start + cfg.per_rank_batch_size]
             bd = {k: batch[k] for k in ("observations", "next_observations", "actions", "rewards", "dones")}
@@ -314,12 +365,13 @@ class SACInteraction:
             row = self.stage.to(rb.device, non_blocking=True)
             self.staged.record()
             next_obs = row[:, :obs_dim]
-            sd["dones"] = row[:, -1:]
-            sd["actions"] = row[:, 2 * obs_dim:2 * obs_dim + act_dim]
-            sd["observations"] = self.obs
+            step = {"observations": self.obs, "actions": row[:, 2 * obs_dim:2 * obs_dim + act_dim],
+                    "rewards": row[:, -2:-1], "dones": row[:, -1:]}
             if not cfg.buffer.sample_next_obs:
-                sd["next_observations"] = row[:, obs_dim:2 * obs_dim]
-            sd["rewards"] = row[:, -2:-1]
+                step["next_observations"] = row[:, obs_dim:2 * obs_dim]
+            rb.add_step(step)  # one multi-tensor copy, no TensorDict round trip
+            self.obs = next_obs
+            return
         else:
             next_obs = obs_to_tensor(next_o, cfg.mlp_keys.encoder, rb.device, n_env)
             sd["dones"] = torch.as_tensor(dones, dtype=torch.float32).view(n_env, -1).to(rb.device)

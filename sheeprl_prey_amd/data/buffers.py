@@ -198,6 +198,29 @@ class ReplayBuffer:
             self._full = True
         self._pos = next_pos
 
+    def add_step(self, rows: Dict[str, Tensor]) -> None:
+        """Add ONE time step, ``rows[k]`` [n_envs, ...]: ``add`` of the [1, n_envs] TensorDict without building it.
+        Device-resident storage fed with device tensors of the stored dtypes and shapes (e.g. SAC's staged
+        transition row, sliced per key) takes one multi-tensor copy launch; anything else goes through ``add``."""
+        buf = self._buf
+        if buf is not None and len(rows) == len(buf._data) and self._first_device().type != "cpu":
+            pos = self._pos
+            dsts, srcs = [], []
+            for k, v in rows.items():
+                store = buf._data.get(k)
+                if store is None or v.dtype != store.dtype or v.device != store.device or v.shape != store.shape[1:]:
+                    break
+                dsts.append(store[pos])
+                srcs.append(v)
+            else:
+                torch._foreach_copy_(dsts, srcs)
+                self._pos = (pos + 1) % self._buffer_size
+                if pos + 1 >= self._buffer_size:
+                    self._full = True
+                return
+        self.add(TensorDict({k: v.unsqueeze(0) for k, v in rows.items()}, batch_size=[1, self._n_envs],
+                            device=next(iter(rows.values())).device))
+
     def _first_device(self):
         for v in self._buf.values():
             return v.device
@@ -237,6 +260,45 @@ class ReplayBuffer:
             for k in self.obs_keys:
                 out.set(f"next_{k}", self._buf[k][(batch_idxes + 1) % self._buffer_size, env_idxes])
         return out
+
+    def sample_rows_into(self, out: Dict[str, Tensor], batch_size: int) -> bool:
+        """``sample(batch_size)`` (without next observations) written straight into the preallocated contiguous
+        ``out[k]`` [batch_size, ...] - e.g. a captured train step's static inputs - by ONE device launch (rows
+        uniform over the filled store, envs uniform: the distribution of ``sample``).  The regular path's index
+        draws, per-key gathers and copy-ins become one kernel.  False (nothing written) when not applicable."""
+        return self._fused_draw({k: v.unsqueeze(0) for k, v in out.items()}, batch_size, 1)
+
+    def _fused_draw(self, out: Dict[str, Tensor], batch_size: int, sequence_length: int) -> bool:
+        """One-launch device draw of ``batch_size`` windows of ``sequence_length`` rows into ``out[k]``
+        [sequence_length, batch_size, ...] (``sample_into`` / ``sample_rows_into``)."""
+        if self._buf is None or not ops.fused_enabled() or set(out) != set(self._buf.keys()):
+            return False
+        dev = self._first_device()
+        if dev.type != "cuda" or sequence_length < 1:
+            return False
+        for k, o in out.items():
+            # the kernel copies rows verbatim: each destination must have the stored dtype and feature shape
+            # (the regular path casts non-uint8 keys to fp32) - otherwise the caller takes the regular path
+            b = self._buf[k]
+            if (o.dtype != b.dtype or tuple(o.shape) != (sequence_length, batch_size) + tuple(b.shape[2:])
+                    or not o.is_contiguous() or o.device != b.device):
+                return False
+        if not self._full and self._pos - sequence_length + 1 < 1:
+            raise ValueError(f"too long sequence length ({sequence_length})")
+        if self._full:
+            first_end = self._pos - sequence_length + 1
+            second_end = self.buffer_size if first_end >= 0 else self.buffer_size + first_end
+            n1, start2, n2 = max(first_end, 0), self._pos, max(second_end - self._pos, 0)
+        else:
+            n1, start2, n2 = self._pos - sequence_length + 1, 0, 0
+        if not hasattr(self, "_draw_seed"):
+            self._draw_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            self._draw_counter = 0
+        keys = list(self._buf.keys())
+        self._draw_counter += 1
+        return bool(ops._ext().seq_sample_into([self._buf[k] for k in keys], [out[k] for k in keys], int(batch_size),
+                                               int(sequence_length), int(n1), int(start2), int(n2), self._draw_seed,
+                                               self._draw_counter))
 
     # ------------------------------------------------------------------ item access
     def __getitem__(self, key: str) -> Tensor:
@@ -323,34 +385,7 @@ class SequentialReplayBuffer(ReplayBuffer):
         launch (``gather.hip`` seq_sample_kernel): the start rows and envs are drawn on the device - same
         distribution as ``sample``, a counter-based generator seeded from torch's - so the host does not issue the
         ~15 small ops of the index draw, gather and copy-in.  False (nothing written) when not applicable."""
-        if self._buf is None or not ops.fused_enabled() or set(out) != set(self._buf.keys()):
-            return False
-        dev = self._first_device()
-        if dev.type != "cuda" or sequence_length < 1:
-            return False
-        for k, o in out.items():
-            # the kernel copies rows verbatim: each destination must have the stored dtype and feature shape
-            # (the regular path casts non-uint8 keys to fp32) - otherwise the caller takes the regular path
-            b = self._buf[k]
-            if (o.dtype != b.dtype or tuple(o.shape) != (sequence_length, batch_size) + tuple(b.shape[2:])
-                    or not o.is_contiguous() or o.device != b.device):
-                return False
-        if not self._full and self._pos - sequence_length + 1 < 1:
-            raise ValueError(f"too long sequence length ({sequence_length})")
-        if self._full:
-            first_end = self._pos - sequence_length + 1
-            second_end = self.buffer_size if first_end >= 0 else self.buffer_size + first_end
-            n1, start2, n2 = max(first_end, 0), self._pos, max(second_end - self._pos, 0)
-        else:
-            n1, start2, n2 = self._pos - sequence_length + 1, 0, 0
-        if not hasattr(self, "_draw_seed"):
-            self._draw_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-            self._draw_counter = 0
-        keys = list(self._buf.keys())
-        self._draw_counter += 1
-        return bool(ops._ext().seq_sample_into([self._buf[k] for k in keys], [out[k] for k in keys], int(batch_size),
-                                               int(sequence_length), int(n1), int(start2), int(n2), self._draw_seed,
-                                               self._draw_counter))
+        return self._fused_draw(out, batch_size, sequence_length)
 
     def _get_samples(self, batch_idxes: Tensor, sample_next_obs: bool = False) -> TensorDict:
         shape = batch_idxes.shape

@@ -39,6 +39,13 @@ unsigned long long* ctr_ptr(const torch::Tensor& t) {
   return reinterpret_cast<unsigned long long*>(t.data_ptr<int64_t>());
 }
 
+long long* ts_ptr(const c10::optional<torch::Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kInt64 && t->is_contiguous() && t->numel() >= 16,
+              "sac_fused: timestamps must be a contiguous int64 GPU tensor of >= 16 values");
+  return reinterpret_cast<long long*>(t->data_ptr<int64_t>());
+}
+
 int* int_ptr(const torch::Tensor& t, int64_t numel, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kInt32 && t.is_contiguous() && t.numel() >= numel, "sac_fused: ",
               name, " must be a contiguous int32 GPU tensor of >= ", numel, " values");
@@ -125,7 +132,8 @@ void sac_fused_act(torch::Tensor obs, std::vector<torch::Tensor> actor, double l
 void sac_fused_target(torch::Tensor obs, torch::Tensor rew, torch::Tensor done, torch::Tensor log_alpha,
                       std::vector<torch::Tensor> actor, double lo, double hi, std::vector<torch::Tensor> target,
                       torch::Tensor ctr, int64_t seed, double gamma, torch::Tensor y, c10::optional<torch::Tensor> act,
-                      c10::optional<torch::Tensor> logp, c10::optional<torch::Tensor> eps) {
+                      c10::optional<torch::Tensor> logp, c10::optional<torch::Tensor> eps,
+                      c10::optional<torch::Tensor> ts) {
   TgtP p;
   p.a = actor_w(actor, lo, hi);
   p.c = critic_w(target, p.a);
@@ -145,6 +153,7 @@ void sac_fused_target(torch::Tensor obs, torch::Tensor rew, torch::Tensor done, 
   p.act = optf(act, "act", M * p.a.A);
   p.logp = optf(logp, "logp", M);
   p.eps = optf(eps, "eps", M * p.a.A);
+  p.ts = ts_ptr(ts);
   p.M = (int)M;
   p.gamma = (float)gamma;
   launch_tgt(p, stream());
@@ -181,7 +190,8 @@ void sac_fused_actor(torch::Tensor obs, torch::Tensor log_alpha, torch::Tensor t
                      torch::Tensor ctr, int64_t seed, bool reduce_min, std::vector<torch::Tensor> ws, torch::Tensor cnt,
                      std::vector<torch::Tensor> grads, c10::optional<torch::Tensor> qf_loss, torch::Tensor losses,
                      c10::optional<torch::Tensor> acc, c10::optional<torch::Tensor> act, c10::optional<torch::Tensor> logp,
-                     c10::optional<torch::Tensor> eps, c10::optional<torch::Tensor> q) {
+                     c10::optional<torch::Tensor> eps, c10::optional<torch::Tensor> q,
+                     c10::optional<torch::Tensor> ts) {
   UpdP u;
   u.a = actor_w(actor, lo, hi);
   u.c = critic_w(critic, u.a);
@@ -218,6 +228,7 @@ void sac_fused_actor(torch::Tensor obs, torch::Tensor log_alpha, torch::Tensor t
   u.eps = optf(eps, "eps", M * A);
   u.q = optf(q, "q", M * n);
   u.cnt = int_ptr(cnt, nblk, "tickets");
+  u.ts = ts_ptr(ts);
   u.M = (int)M;
   u.reduce_min = reduce_min ? 1 : 0;
   hipStream_t st = stream();
@@ -302,9 +313,17 @@ void sac_adam_multi(std::vector<std::vector<torch::Tensor>> tensors, std::vector
 
 void register_sac(pybind11::module& m) {
   m.def("sac_fused_act", &sac_fused_act);
-  m.def("sac_fused_target", &sac_fused_target);
+  m.def("sac_fused_target", &sac_fused_target, pybind11::arg("obs"), pybind11::arg("rew"), pybind11::arg("done"),
+        pybind11::arg("log_alpha"), pybind11::arg("actor"), pybind11::arg("lo"), pybind11::arg("hi"), pybind11::arg("target"),
+        pybind11::arg("ctr"), pybind11::arg("seed"), pybind11::arg("gamma"), pybind11::arg("y"), pybind11::arg("act"),
+        pybind11::arg("logp"), pybind11::arg("eps"), pybind11::arg("ts") = pybind11::none());
   m.def("sac_fused_critic_wgrad", &sac_fused_critic_wgrad);
-  m.def("sac_fused_actor", &sac_fused_actor);
+  m.def("sac_fused_actor", &sac_fused_actor, pybind11::arg("obs"), pybind11::arg("log_alpha"),
+        pybind11::arg("target_entropy"), pybind11::arg("actor"), pybind11::arg("lo"), pybind11::arg("hi"),
+        pybind11::arg("critic"), pybind11::arg("ctr"), pybind11::arg("seed"), pybind11::arg("reduce_min"), pybind11::arg("ws"),
+        pybind11::arg("cnt"), pybind11::arg("grads"), pybind11::arg("qf_loss"), pybind11::arg("losses"), pybind11::arg("acc"),
+        pybind11::arg("act"), pybind11::arg("logp"), pybind11::arg("eps"), pybind11::arg("q"),
+        pybind11::arg("ts") = pybind11::none());
   m.def("sac_adam_multi", &sac_adam_multi);
   m.def("sac_fused_zp", [](int64_t A) { return (int64_t)zp_of((int)A); });
   m.def("sac_fused_blocks", [](int64_t M) { return (int64_t)upd_blocks((int)M); });

@@ -70,18 +70,8 @@ __global__ __launch_bounds__(NTH) void critic_fwd_kernel(FP p) {
   const int tiles = H / (16 * NW);
   const float* W1 = p.W1 + (long)c * H * p.IN;
   float* H1 = p.H1 + (long)c * M * H;
-  for (int t = 0; t < tiles; ++t) {
-    const int n0 = (wave * tiles + t) * 16;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    if ((p.IN & 15) == 0) {
-      acc = tile_gemm_nt(xs, ldx, W1, p.IN, n0, p.IN, lane);
-    } else {
-      for (int k0 = 0; k0 < p.INp; k0 += 4) {
-        const int k = k0 + q;
-        const float w = k < p.IN ? W1[(long)(n0 + j) * p.IN + k] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xs[j * ldx + k], w, acc, 0, 0, 0);
-      }
-    }
+  // first layer: the whole (small) K of both tiles' weights in flight at once
+  wave_tiles<2, NW>(xs, ldx, W1, p.IN, H, p.IN, lane, wave, [&](int n0, const floatx4& acc) {
     const float bb = p.b1[c * H + n0 + j];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -89,14 +79,12 @@ __global__ __launch_bounds__(NTH) void critic_fwd_kernel(FP p) {
       h1s[(4 * q + e) * ldh + n0 + j] = h;
       if (r0 + 4 * q + e < M) H1[(long)(r0 + 4 * q + e) * H + n0 + j] = h;
     }
-  }
+  });
   __syncthreads();
   const float* W2 = p.W2 + (long)c * H * H;
   float* H2 = p.H2 + (long)c * M * H;
   float part[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int t = 0; t < tiles; ++t) {
-    const int n0 = (wave * tiles + t) * 16;
-    const floatx4 acc = tile_gemm_nt(h1s, ldh, W2, H, n0, H, lane);
+  wave_tiles<0, NW>(h1s, ldh, W2, H, H, H, lane, wave, [&](int n0, const floatx4& acc) {
     const float bb = p.b2[c * H + n0 + j], w3 = p.W3[c * H + n0 + j];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -105,7 +93,7 @@ __global__ __launch_bounds__(NTH) void critic_fwd_kernel(FP p) {
       h2s[(4 * q + e) * ldh + n0 + j] = h;
       if (r0 + 4 * q + e < M) H2[(long)(r0 + 4 * q + e) * H + n0 + j] = h;
     }
-  }
+  });
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     float v = part[e];
@@ -147,15 +135,13 @@ __global__ __launch_bounds__(NTH) void critic_fwd_kernel(FP p) {
   __syncthreads();
   // dh1 = (dh2 W2) * [h1 > 0]
   float* DH1 = p.DH1 + (long)c * M * H;
-  for (int t = 0; t < tiles; ++t) {
-    const int n0 = (wave * tiles + t) * 16;
-    const floatx4 acc = tile_gemm_nn(h2s, ldh, W2, H, n0, H, lane);
+  wave_tiles<1, NW>(h2s, ldh, W2, H, H, H, lane, wave, [&](int n0, const floatx4& acc) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int r = 4 * q + e;
       if (r0 + r < M) DH1[(long)(r0 + r) * H + n0 + j] = h1s[r * ldh + n0 + j] > 0.f ? acc[e] : 0.f;
     }
-  }
+  });
 }
 
 struct GP {

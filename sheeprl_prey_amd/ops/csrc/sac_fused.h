@@ -46,6 +46,7 @@ struct TgtP {
   float* act;   // [M, A] or null
   float* logp;  // [M] or null
   float* eps;   // [M, A] or null
+  long long* ts;  // phase timestamps of workgroup 0 (s_memrealtime, 100 MHz) or null
   int M;
   float gamma;
 };
@@ -63,6 +64,7 @@ struct UpdP {
   float* part;                               // [blocks, 2] loss partials
   float *act, *logp, *eps, *q;               // [M, A] [M] [M, A] [M, n]: optional (tests / metrics)
   int* cnt;                                  // [blocks] tickets, zero at rest
+  long long* ts;                             // phase timestamps of row block 0 (s_memrealtime) or null
   int M, reduce_min;
 };
 

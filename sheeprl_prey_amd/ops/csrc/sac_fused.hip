@@ -52,6 +52,15 @@ __device__ __forceinline__ float gauss(unsigned long long seed, unsigned long lo
   return sqrtf(-2.f * logf(u1)) * cosf(6.283185307179586f * u2);
 }
 
+// phase timestamp i (s_memrealtime, 100 MHz) from thread 0 of a chosen workgroup: kernel-internal profiling
+__device__ __forceinline__ void stamp(long long* ts, bool who, int i) {
+  if (ts && who && threadIdx.x == 0) {
+    long long c;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c)::"memory");
+    ts[i] = c;
+  }
+}
+
 __device__ __forceinline__ int zp_dev(int A) { return (2 * A + 15) / 16 * 16; }
 __device__ __forceinline__ int pad16(int v) { return (v + 15) / 16 * 16; }
 
@@ -92,13 +101,11 @@ __device__ __forceinline__ void load_rows(float* xs, int ldx, int width, const f
 
 // h1 = relu(x W1^T + b1), h2 = relu(h1 W2^T + b2), z = h2 [Wm; Ws]^T + [bm; bs] for the 16 rows in xs (columns < OD
 // are read).  H1g / H2g: optional global copies of the hidden rows (the weight-gradient operands).
+template <int FIRST = 2>  // wave_tiles form of the first layer (3 in kernels at their register limit)
 __device__ void actor_fwd(const ActorW& a, const float* xs, int ldx, const ALds& L, float* H1g, float* H2g, int r0, int M) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, j = lane & 15, q = lane >> 4;
-  const int H = a.H, tiles = H / (16 * NW);
-  for (int t = 0; t < tiles; ++t) {
-    const int n0 = (wave * tiles + t) * 16;
-    const floatx4 acc = (a.OD & 15) == 0 ? tile_gemm_nt(xs, ldx, a.W1, a.OD, n0, a.OD, lane)
-                                         : tile_gemm_nt_small(xs, ldx, a.W1, a.OD, n0, a.OD, lane);
+  const int H = a.H;
+  wave_tiles<FIRST, NW>(xs, ldx, a.W1, a.OD, H, a.OD, lane, wave, [&](int n0, const floatx4& acc) {
     const float bb = a.b1[n0 + j];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -106,11 +113,9 @@ __device__ void actor_fwd(const ActorW& a, const float* xs, int ldx, const ALds&
       L.h1[(4 * q + e) * L.ldh + n0 + j] = h;
       if (H1g && r0 + 4 * q + e < M) H1g[(long)(r0 + 4 * q + e) * H + n0 + j] = h;
     }
-  }
+  });
   __syncthreads();
-  for (int t = 0; t < tiles; ++t) {
-    const int n0 = (wave * tiles + t) * 16;
-    const floatx4 acc = tile_gemm_nt(L.h1, L.ldh, a.W2, H, n0, H, lane);
+  wave_tiles<0, NW>(L.h1, L.ldh, a.W2, H, H, H, lane, wave, [&](int n0, const floatx4& acc) {
     const float bb = a.b2[n0 + j];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -118,7 +123,7 @@ __device__ void actor_fwd(const ActorW& a, const float* xs, int ldx, const ALds&
       L.h2[(4 * q + e) * L.ldh + n0 + j] = h;
       if (H2g && r0 + 4 * q + e < M) H2g[(long)(r0 + 4 * q + e) * H + n0 + j] = h;
     }
-  }
+  });
   __syncthreads();
   const int A = a.A, nz = zp_dev(A) / 16;
   for (int t = wave; t < nz; t += NW) {  // head tiles: columns [mean 0..A) | [log-std A..2A) | zero padding
@@ -200,33 +205,33 @@ __global__ __launch_bounds__(NTH) void tgt_kernel(TgtP p) {
   float* qp = hc + ROWS * ldc;               // [NW][16]
   float* qmin = qp + NW * ROWS;              // [16]
   const int r0 = blockIdx.x * ROWS;
+  const bool b0 = blockIdx.x == 0;
+  stamp(p.ts, b0, 0);
   const unsigned long long ctr = *p.ctr;
   load_rows(xs, ldx, INp, p.obs, a.OD, r0, p.M);
   if (tid < ROWS) qmin[tid] = INFINITY;
   __syncthreads();
+  stamp(p.ts, b0, 1);
   actor_fwd(a, xs, ldx, L, nullptr, nullptr, r0, p.M);
+  stamp(p.ts, b0, 2);
   actor_sample(a, L, xs + a.OD, ldx, p.seed, ctr, SALT_TARGET, r0, p.M, p.act, p.logp, p.eps);
-  const int tiles = c.H / (16 * NW);
+  stamp(p.ts, b0, 3);
   for (int ci = 0; ci < c.n; ++ci) {
     const float* W1 = c.W1 + (long)ci * c.H * IN;
-    for (int t = 0; t < tiles; ++t) {
-      const int n0 = (wave * tiles + t) * 16;
-      const floatx4 acc = (IN & 15) == 0 ? tile_gemm_nt(xs, ldx, W1, IN, n0, IN, lane)
-                                         : tile_gemm_nt_small(xs, ldx, W1, IN, n0, IN, lane);
+    wave_tiles<2, NW>(xs, ldx, W1, IN, c.H, IN, lane, wave, [&](int n0, const floatx4& acc) {
       const float bb = c.b1[ci * c.H + n0 + j];
 #pragma unroll
       for (int e = 0; e < 4; ++e) hc[(4 * q + e) * ldc + n0 + j] = fmaxf(acc[e] + bb, 0.f);
-    }
+    });
     __syncthreads();
+    stamp(p.ts, b0 && ci < 2, 4 + 2 * ci);
     const float* W2 = c.W2 + (long)ci * c.H * c.H;
     float part[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < tiles; ++t) {
-      const int n0 = (wave * tiles + t) * 16;
-      const floatx4 acc = tile_gemm_nt(hc, ldc, W2, c.H, n0, c.H, lane);
+    wave_tiles<0, NW>(hc, ldc, W2, c.H, c.H, c.H, lane, wave, [&](int n0, const floatx4& acc) {
       const float bb = c.b2[ci * c.H + n0 + j], w3 = c.W3[ci * c.H + n0 + j];
 #pragma unroll
       for (int e = 0; e < 4; ++e) part[e] += fmaxf(acc[e] + bb, 0.f) * w3;
-    }
+    });
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float v = part[e];
@@ -241,12 +246,14 @@ __global__ __launch_bounds__(NTH) void tgt_kernel(TgtP p) {
       qmin[tid] = fminf(qmin[tid], s);
     }
     __syncthreads();
+    stamp(p.ts, b0 && ci < 2, 5 + 2 * ci);
   }
   if (tid < ROWS && r0 + tid < p.M) {
     const int row = r0 + tid;
     const float alpha = expf(*p.log_alpha);
     p.y[row] = p.rew[row] + (1.f - p.done[row]) * p.gamma * (qmin[tid] - alpha * L.lp[tid]);
   }
+  stamp(p.ts, b0, 8);
 }
 
 // ---------------------------------------------------------------- actor / alpha objective, forward + data backward
@@ -268,6 +275,8 @@ __global__ __launch_bounds__(NTH) void upd_kernel(UpdP p) {
   int* sel = reinterpret_cast<int*>(qred + ROWS);  // [16]
   const int rb = blockIdx.x, ci = blockIdx.y, r0 = rb * ROWS;
   const bool lead = ci == 0;  // writes the actor's weight-gradient operands
+  const bool b0 = rb == 0 && ci == 0;
+  stamp(p.ts, b0, 0);
   const unsigned long long ctr = *p.ctr;
   load_rows(xs, ldx, INp, p.obs, OD, r0, M);
   if (lead)
@@ -276,7 +285,9 @@ __global__ __launch_bounds__(NTH) void upd_kernel(UpdP p) {
       if (row < M) p.Xa[(long)row * ODp + k] = k < OD ? p.obs[(long)row * OD + k] : 0.f;
     }
   __syncthreads();
-  actor_fwd(a, xs, ldx, L, lead ? p.H1a : nullptr, lead ? p.H2a : nullptr, r0, M);
+  stamp(p.ts, b0, 1);
+  actor_fwd<3>(a, xs, ldx, L, lead ? p.H1a : nullptr, lead ? p.H2a : nullptr, r0, M);
+  stamp(p.ts, b0, 2);
   actor_sample(a, L, xs + OD, ldx, p.seed, ctr, SALT_ACTOR, r0, M, lead ? p.act : nullptr, lead ? p.logp : nullptr,
                lead ? p.eps : nullptr);
 
@@ -284,20 +295,15 @@ __global__ __launch_bounds__(NTH) void upd_kernel(UpdP p) {
   const float* W1 = c.W1 + (long)ci * Hc * IN;
   const float* W2 = c.W2 + (long)ci * Hc * Hc;
   const float* w3 = c.W3 + (long)ci * Hc;
-  const int tiles = Hc / (16 * NW);
-  for (int t = 0; t < tiles; ++t) {
-    const int n0 = (wave * tiles + t) * 16;
-    const floatx4 acc = (IN & 15) == 0 ? tile_gemm_nt(xs, ldx, W1, IN, n0, IN, lane)
-                                       : tile_gemm_nt_small(xs, ldx, W1, IN, n0, IN, lane);
+  wave_tiles<3, NW>(xs, ldx, W1, IN, Hc, IN, lane, wave, [&](int n0, const floatx4& acc) {
     const float bb = c.b1[ci * Hc + n0 + j];
 #pragma unroll
     for (int e = 0; e < 4; ++e) h1c[(4 * q + e) * ldc + n0 + j] = fmaxf(acc[e] + bb, 0.f);
-  }
+  });
   __syncthreads();
+  stamp(p.ts, b0, 3);
   float part[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int t = 0; t < tiles; ++t) {
-    const int n0 = (wave * tiles + t) * 16;
-    const floatx4 acc = tile_gemm_nt(h1c, ldc, W2, Hc, n0, Hc, lane);
+  wave_tiles<0, NW>(h1c, ldc, W2, Hc, Hc, Hc, lane, wave, [&](int n0, const floatx4& acc) {
     const float bb = c.b2[ci * Hc + n0 + j], wv = w3[n0 + j];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -305,7 +311,7 @@ __global__ __launch_bounds__(NTH) void upd_kernel(UpdP p) {
       part[e] += h * wv;
       h2c[(4 * q + e) * ldc + n0 + j] = h;
     }
-  }
+  });
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     float v = part[e];
@@ -319,6 +325,7 @@ __global__ __launch_bounds__(NTH) void upd_kernel(UpdP p) {
     for (int w = 0; w < NW; ++w) s += qp[w * ROWS + tid];
     qv[tid] = s;
   }
+  stamp(p.ts, b0, 4);
   // dq/da with a unit output gradient: dh2 = w3 [h2 > 0] (in place), dh1 = (dh2 W2) [h1 > 0] (in place: each lane
   // masks and overwrites only its own output elements), da = dh1 W1[:, OD:OD+A]
   for (int i = tid; i < ROWS * Hc; i += NTH) {
@@ -327,15 +334,13 @@ __global__ __launch_bounds__(NTH) void upd_kernel(UpdP p) {
     *hp = *hp > 0.f ? w3[k] : 0.f;
   }
   __syncthreads();
-  for (int t = 0; t < tiles; ++t) {
-    const int n0 = (wave * tiles + t) * 16;
-    const floatx4 acc = tile_gemm_nn(h2c, ldc, W2, Hc, n0, Hc, lane);
+  wave_tiles<1, NW>(h2c, ldc, W2, Hc, Hc, Hc, lane, wave, [&](int n0, const floatx4& acc) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float* hp = h1c + (4 * q + e) * ldc + n0 + j;
       *hp = *hp > 0.f ? acc[e] : 0.f;
     }
-  }
+  });
   __syncthreads();
   // hand-off to the row block's finishing workgroup: write-through stores, drained before the ticket
   const int na = (A + 15) / 16;
@@ -353,11 +358,15 @@ __global__ __launch_bounds__(NTH) void upd_kernel(UpdP p) {
     __hip_atomic_store(p.QX + (long)ci * M + r0 + tid, qv[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (p.q) p.q[(long)(r0 + tid) * n + ci] = qv[tid];
   }
+  stamp(p.ts, b0, 5);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) last = __hip_atomic_fetch_add(p.cnt + rb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
   __syncthreads();
+  stamp(p.ts, b0, 6);
   if (!last) return;
+  const bool bl = rb == 0;
+  stamp(p.ts, bl, 7);
   if (tid == 0) __hip_atomic_store(p.cnt + rb, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: the hand-off reads are sc1
 
@@ -411,6 +420,7 @@ __global__ __launch_bounds__(NTH) void upd_kernel(UpdP p) {
     L.z[r * L.ldz + col] = 0.f;
   }
   __syncthreads();
+  stamp(p.ts, bl, 8);
   for (int i = tid; i < ROWS * ZP; i += NTH) {
     const int r = i / ZP, col = i - r * ZP;
     if (r0 + r < M) p.DZ[(long)(r0 + r) * ZP + col] = L.z[r * L.ldz + col];
@@ -426,17 +436,15 @@ __global__ __launch_bounds__(NTH) void upd_kernel(UpdP p) {
     if (r0 + r < M) p.DH2a[(long)(r0 + r) * H + h] = v;
   }
   __syncthreads();
+  stamp(p.ts, bl, 9);
   // dh1 = (dh2 W2) [h1 > 0]
-  const int ta = H / (16 * NW);
-  for (int t = 0; t < ta; ++t) {
-    const int n0 = (wave * ta + t) * 16;
-    const floatx4 acc = tile_gemm_nn(L.h2, L.ldh, a.W2, H, n0, H, lane);
+  wave_tiles<1, NW>(L.h2, L.ldh, a.W2, H, H, H, lane, wave, [&](int n0, const floatx4& acc) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int r = 4 * q + e;
       if (r0 + r < M) p.DH1a[(long)(r0 + r) * H + n0 + j] = L.h1[r * L.ldh + n0 + j] > 0.f ? acc[e] : 0.f;
     }
-  }
+  });
   if (wave == 0) {  // loss partials: sum_b (alpha logp - q_red), sum_b logp
     const bool ok = lane < ROWS && r0 + lane < M;
     float v1 = ok ? alpha * L.lp[lane] - qred[lane] : 0.f, v2 = ok ? L.lp[lane] : 0.f;
@@ -447,6 +455,7 @@ __global__ __launch_bounds__(NTH) void upd_kernel(UpdP p) {
       p.part[2 * rb + 1] = v2;
     }
   }
+  stamp(p.ts, bl, 10);
 }
 
 // ---------------------------------------------------------------- actor weight gradients, alpha gradient, losses
