@@ -411,6 +411,16 @@ class DreamerV3Trainer:
         lambda_values = st["lambda_values"]
         baseline = st["predicted_values"][:-1]
         offset, invscale = self.moments.update(st["gathered"])
+        if pre is not None and self.actor.distribution == "trunc_normal":
+            # advantage, closed-form truncated-normal entropies, discounting and the mean in one kernel
+            T = pre.shape[0]
+            policy_loss = ops.actor_loss_cont(pre, lambda_values.reshape(T - 1, -1), baseline.reshape(T - 1, -1),
+                                              st["discount"].detach().reshape(T, -1), offset, invscale,
+                                              cfg.algo.actor.ent_coef, self.actor.init_std, self.actor.min_std)
+            if policy_loss is not None:
+                policy_loss.backward()
+                st["out"]["Loss/policy_loss"] = policy_loss.detach()
+                return
         if not self.is_continuous:
             # advantage, log-probs, entropies, discounting and the mean in one kernel (actor_loss.hip)
             z = torch.cat(mixed, -1) if len(mixed) > 1 else mixed[0]

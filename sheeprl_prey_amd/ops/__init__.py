@@ -717,6 +717,42 @@ def actor_loss_discrete(z: Tensor, actions: Tensor, lam: Tensor, base: Tensor, d
                                     invscale.detach(), tuple(int(h) for h in heads), float(ent_coef))
 
 
+# =============================================================== DreamerV3 continuous actor objective
+class _ActorLossCont(torch.autograd.Function):
+    """``csrc/actor_loss.hip`` actor_loss_cont_kernel: the loss and its gradients w.r.t. the head outputs, the
+    lambda returns and the baseline in one pass (packed); the backward scales them by the upstream scalar."""
+
+    @staticmethod
+    def forward(ctx, pre, lam, base, disc, offset, invscale, ent_coef, init_std, min_std):
+        loss, g = _ext().actor_loss_cont(pre.contiguous(), lam.contiguous(), base.contiguous(), disc.contiguous(),
+                                         offset.reshape(1).contiguous(), invscale.reshape(1).contiguous(), float(ent_coef),
+                                         float(init_std), float(min_std), -1.0, 1.0)
+        ctx.save_for_backward(g)
+        ctx.shapes = (pre.shape, lam.shape, base.shape)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        (g,) = ctx.saved_tensors
+        sp, sl, sb = ctx.shapes
+        gs = g * gl
+        n0, n1 = sp.numel(), sl.numel()
+        return (gs[:n0].view(sp), gs[n0:n0 + n1].view(sl), gs[n0 + n1:].view(sb), None, None, None, None, None, None)
+
+
+def actor_loss_cont(pre: Tensor, lam: Tensor, base: Tensor, disc: Tensor, offset: Tensor, invscale: Tensor,
+                    ent_coef: float, init_std: float, min_std: float) -> Optional[Tensor]:
+    """DreamerV3 continuous (trunc-normal, bounds [-1, 1]) policy loss (reference ``dreamer_v3.py:258-301``) from the
+    actor head outputs ``pre`` [T, M, 2A]: ``-mean_{t<T-1} disc (advantage + ent_coef H)`` with the closed-form
+    truncated-normal entropy; one launch forward (+ a fixed-order sum), one backward.  None when the kernel does
+    not apply (the caller keeps the eager distribution objective)."""
+    if not (_native(pre) and pre.dim() == 3 and pre.shape[-1] % 2 == 0
+            and all(t.dtype == torch.float32 for t in (pre, lam, base, disc, offset, invscale))):
+        return None
+    return _ActorLossCont.apply(pre, lam, base, disc.detach(), offset.detach(), invscale.detach(), float(ent_coef),
+                                float(init_std), float(min_std))
+
+
 # =============================================================== skinny weight-streaming GEMM
 def skinny_ok(A: Tensor, W: Tensor) -> bool:
     """Shape/alignment gate of ``skinny_nt`` (M <= 16 rows, K % 128, N % 128, 16-byte strides)."""

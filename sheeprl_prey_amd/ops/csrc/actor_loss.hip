@@ -75,6 +75,70 @@ __global__ __launch_bounds__(NTH) void actor_loss_kernel(const float* __restrict
   if (threadIdx.x == 0) partial[blockIdx.x] = acc;
 }
 
+// Continuous (truncated-normal) actor objective (reference dreamer_v3.py:258-301 with agent.py:685-700):
+//
+//   loc = tanh(p_mean), std = 2 sigmoid((p_std + init_std) / 2) + min_std             (the actor head transform)
+//   H_k = log(sqrt(2 pi e)) + log Z - (b phi(b) - a phi(a)) / (2 Z) + log std,  a = (lo - loc) / std,
+//         b = (hi - loc) / std, Z = max(Phi(b) - Phi(a), eps)                        (truncated-normal entropy)
+//   loss = -mean_{t < T-1, m} disc[t,m] ((lam - off) / inv - (base - off) / inv + ent_coef sum_k H_k)
+//
+// One thread per (t, m) row; the gradients w.r.t. the head outputs (through the closed-form entropy derivative),
+// the lambda returns and the baseline are written with the loss partials (unscaled: the backward multiplies by the
+// upstream scalar).  Z's clamp passes no gradient where it is active, as torch's clamp_min.
+__global__ __launch_bounds__(NTH) void actor_loss_cont_kernel(const float* __restrict__ pre, const float* __restrict__ lam,
+                                                              const float* __restrict__ base, const float* __restrict__ disc,
+                                                              const float* __restrict__ offp, const float* __restrict__ invp,
+                                                              int A, int T, int M, float ent_coef, float init_std,
+                                                              float min_std, float lo, float hi, float* __restrict__ dpre,
+                                                              float* __restrict__ dlam, float* __restrict__ dbase,
+                                                              float* __restrict__ partial) {
+  __shared__ float red[NTH / 64];
+  const int rows = T * M, last = (T - 1) * M;
+  const float off = *offp, inv = *invp;
+  const float scale = -1.f / (float)last;
+  const float EPS = 1.1920928955078125e-07f, INV_SQRT2 = 0.70710678118654752f, INV_SQRT_2PI = 0.3989422804014327f;
+  const float LOG_SQRT_2PI_E = 1.4189385332046727f;
+  float acc = 0.f;
+  for (int r = blockIdx.x * NTH + threadIdx.x; r < rows; r += gridDim.x * NTH) {
+    const float* pr = pre + (size_t)r * 2 * A;
+    float* gr = dpre + (size_t)r * 2 * A;
+    if (r >= last) {  // the last imagined step enters neither the objective nor the entropy term
+      for (int k = 0; k < 2 * A; ++k) gr[k] = 0.f;
+      continue;
+    }
+    const float d = disc[r];
+    const float adv = (lam[r] - off) / inv - (base[r] - off) / inv;
+    dlam[r] = scale * d / inv;
+    dbase[r] = -scale * d / inv;
+    const float ge = scale * d * ent_coef;  // d loss / d H_k
+    float hs = 0.f;
+    for (int k = 0; k < A; ++k) {
+      const float loc = tanhf(pr[k]);
+      const float sg = 1.f / (1.f + expf(-0.5f * (pr[A + k] + init_std)));
+      const float sd = 2.f * sg + min_std;
+      const float a = (lo - loc) / sd, b = (hi - loc) / sd;
+      const float pa = expf(-0.5f * a * a) * INV_SQRT_2PI, pb = expf(-0.5f * b * b) * INV_SQRT_2PI;
+      const float zr = 0.5f * (1.f + erff(b * INV_SQRT2)) - 0.5f * (1.f + erff(a * INV_SQRT2));
+      const bool clamped = zr < EPS;
+      const float Z = clamped ? EPS : zr;
+      const float N = b * pb - a * pa;
+      hs += LOG_SQRT_2PI_E + logf(Z) - 0.5f * N / Z + logf(sd);
+      // dH/da, dH/db (Z held constant where its clamp is active)
+      const float dZa = clamped ? 0.f : -pa, dZb = clamped ? 0.f : pb;
+      const float dNa = -pa * (1.f - a * a), dNb = pb * (1.f - b * b);
+      const float dHa = dZa / Z - 0.5f * (dNa / Z - N * dZa / (Z * Z));
+      const float dHb = dZb / Z - 0.5f * (dNb / Z - N * dZb / (Z * Z));
+      const float dloc = -(dHa + dHb) / sd;
+      const float dsd = -(a * dHa + b * dHb) / sd + 1.f / sd;
+      gr[k] = ge * dloc * (1.f - loc * loc);
+      gr[A + k] = ge * dsd * sg * (1.f - sg);
+    }
+    acc += d * (adv + ent_coef * hs);
+  }
+  acc = block_sum<NTH / 64>(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = acc;
+}
+
 __global__ void actor_loss_final(const float* __restrict__ partial, int n, float scale, float* __restrict__ loss) {
   if (threadIdx.x == 0) {
     float s = 0.f;
@@ -114,6 +178,15 @@ void launch_imag_discount(const float* clog, const float* dones, int T1, int M, 
 }
 
 int actor_loss_blocks(int rows) { return std::min(256, std::max(1, (rows + srl::aloss::NTH - 1) / srl::aloss::NTH)); }
+
+void launch_actor_loss_cont(const float* pre, const float* lam, const float* base, const float* disc, const float* offp,
+                            const float* invp, int A, int T, int M, float ent_coef, float init_std, float min_std, float lo,
+                            float hi, float* dpre, float* dlam, float* dbase, float* partial, float* loss, hipStream_t st) {
+  const int nb = actor_loss_blocks(T * M);
+  hipLaunchKernelGGL(srl::aloss::actor_loss_cont_kernel, dim3(nb), dim3(srl::aloss::NTH), 0, st, pre, lam, base, disc, offp,
+                     invp, A, T, M, ent_coef, init_std, min_std, lo, hi, dpre, dlam, dbase, partial);
+  hipLaunchKernelGGL(srl::aloss::actor_loss_final, dim3(1), dim3(64), 0, st, partial, nb, -1.f / (float)((T - 1) * M), loss);
+}
 
 void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,

@@ -54,6 +54,9 @@ void launch_gru_cell_bwd(const float* gh, const float* h, const float* rzn, cons
 void launch_gather_rows(const void* const* src, void* const* dst, const long* row_bytes, int nk, int n_envs, long cap, int N,
                         const long* row, const long* env, int* err, hipStream_t st);
 int actor_loss_blocks(int rows);
+void launch_actor_loss_cont(const float* pre, const float* lam, const float* base, const float* disc, const float* offp,
+                            const float* invp, int A, int T, int M, float ent_coef, float init_std, float min_std, float lo,
+                            float hi, float* dpre, float* dlam, float* dbase, float* partial, float* loss, hipStream_t st);
 void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
                        const float* offp, const float* invp, const int* heads, int nh, int A, int T, int M, float ent_coef,
                        float* dz, float* partial, float* loss, hipStream_t st);
@@ -260,6 +263,29 @@ std::vector<torch::Tensor> actor_loss_discrete(torch::Tensor z, torch::Tensor ac
                     (int)A, (int)T, (int)M, (float)ent_coef, dz.data_ptr<float>(), partial.data_ptr<float>(),
                     loss.data_ptr<float>(), stream());
   return {loss, dz};
+}
+
+// ------------------------------------------------------------------ DreamerV3 continuous actor objective (actor_loss.hip)
+// pre [T, M, 2A] (the trunc-normal head outputs); lam, base [T-1, M]; disc [T, M] (first T-1 rows read); offset /
+// invscale scalars.  Returns {loss (0-dim), grads [T*M*2A | (T-1)M | (T-1)M] packed: d pre, d lambda, d baseline}.
+std::vector<torch::Tensor> actor_loss_cont(torch::Tensor pre, torch::Tensor lam, torch::Tensor base, torch::Tensor disc,
+                                           torch::Tensor offset, torch::Tensor invscale, double ent_coef, double init_std,
+                                           double min_std, double lo, double hi) {
+  for (auto* t : {&pre, &lam, &base, &disc, &offset, &invscale}) nc_check(*t, "actor_loss_cont operand");
+  TORCH_CHECK(pre.dim() == 3 && pre.size(2) % 2 == 0, "actor_loss_cont: pre must be [T, M, 2A]");
+  const int64_t T = pre.size(0), M = pre.size(1), A = pre.size(2) / 2;
+  TORCH_CHECK(T >= 2 && A >= 1 && lam.numel() == (T - 1) * M && base.numel() == (T - 1) * M && disc.numel() >= (T - 1) * M,
+              "actor_loss_cont: lambda / baseline [T-1, M], discount [T, M]");
+  TORCH_CHECK(offset.numel() == 1 && invscale.numel() == 1, "actor_loss_cont: scalar offset / invscale");
+  auto grads = torch::empty({T * M * 2 * A + 2 * (T - 1) * M}, pre.options());
+  auto loss = torch::empty({}, pre.options());
+  auto partial = torch::empty({actor_loss_blocks((int)(T * M))}, pre.options());
+  float* g = grads.data_ptr<float>();
+  launch_actor_loss_cont(pre.data_ptr<float>(), lam.data_ptr<float>(), base.data_ptr<float>(), disc.data_ptr<float>(),
+                         offset.data_ptr<float>(), invscale.data_ptr<float>(), (int)A, (int)T, (int)M, (float)ent_coef,
+                         (float)init_std, (float)min_std, (float)lo, (float)hi, g, g + T * M * 2 * A,
+                         g + T * M * 2 * A + (T - 1) * M, partial.data_ptr<float>(), loss.data_ptr<float>(), stream());
+  return {loss, grads};
 }
 
 // ------------------------------------------------------------------ skinny weight-streaming GEMM (skinny.hip)
@@ -779,6 +805,7 @@ std::vector<torch::Tensor> transpose_many(std::vector<torch::Tensor> xs, c10::op
 }
 
 void register_ext(pybind11::module& m) {
+  m.def("actor_loss_cont", &actor_loss_cont);
   m.def("sac_critic_fwd", &sac_critic_fwd);
   m.def("sac_critic_wgrad", &sac_critic_wgrad);
   m.def("gather_rows", &gather_rows, pybind11::arg("srcs"), pybind11::arg("row"), pybind11::arg("env"),
