@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--vector", type=int, default=0, help="vector observation size (0: 64x64 rgb frames)")
+    ap.add_argument("--marker", action="store_true", help="a sleep kernel before the timed steps (scripts/trace_window.py)")
     ap.add_argument("overrides", nargs="*")
     a = ap.parse_args()
     from sheeprl_prey_amd.algos.dreamer_v3.agent import build_models
@@ -58,6 +59,8 @@ def main():
     for _ in range(a.warmup):
         out = tr.train_step(data)
     torch.cuda.synchronize()
+    if a.marker:
+        torch.cuda._sleep(1000)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         out = tr.train_step(data)
