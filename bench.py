@@ -225,7 +225,8 @@ def main():
 
         trainer.graphed.enabled = False
         unsampled[0] = True
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True,
+                     record_shapes=bool(os.environ.get("SRL_PROFILE_SHAPES"))) as prof:
             for _ in range(args.torch_profile):
                 one_step()
             torch.cuda.synchronize()
@@ -242,6 +243,8 @@ def main():
                     "mm", "addmm", "bmm", "baddbmm", "convolution", "miopen_convolution", "record_stream", "set_",
                     "new_empty", "new_empty_strided", "resize_", "_has_compatible_shallow_copy_type", "numpy_T"}
 
+            gemm_mode = os.environ.get("SRL_PROFILE_SITES") == "gemm"
+
             class _Sites(TorchDispatchMode):
                 def __init__(self):
                     super().__init__()
@@ -249,7 +252,13 @@ def main():
 
                 def __torch_dispatch__(self, func, types, args=(), kwargs=None):
                     name = func.overloadpacket.__name__
-                    if name not in skip:
+                    if gemm_mode:  # SRL_PROFILE_SITES=gemm: library GEMM calls by site, operand shapes and strides
+                        if name in ("mm", "addmm", "addmm_", "bmm", "baddbmm"):
+                            fr = [f for f in traceback.extract_stack()[:-1] if "sheeprl_prey_amd" in f.filename]
+                            site = f"{fr[-1].filename.split('sheeprl_prey_amd/')[-1]}:{fr[-1].lineno}" if fr else "<autograd>"
+                            ops_ = ";".join(f"{tuple(a.shape)}/{a.stride()}" for a in args if isinstance(a, torch.Tensor))
+                            self.c[(name, f"{site} {ops_}")] += 1
+                    elif name not in skip:
                         fr = [f for f in traceback.extract_stack()[:-1] if "sheeprl_prey_amd" in f.filename]
                         site = f"{fr[-1].filename.split('sheeprl_prey_amd/')[-1]}:{fr[-1].lineno}" if fr else "<autograd>"
                         self.c[(name, site)] += 1
@@ -260,7 +269,7 @@ def main():
                 one_step()
             torch.cuda.synchronize()
             for (name, site), n in sm.c.most_common(int(os.environ.get("SRL_PROFILE_TOP", 60))):
-                print(f"SITE {n:4d} {name:28s} {site}", file=sys.stderr, flush=True)
+                print(f"SITE {n:4d} {name:10s} {site}", file=sys.stderr, flush=True)
         trainer.graphed.enabled = True
         unsampled[0] = False
         small = ("aten::cat", "aten::copy_", "aten::fill_", "aten::zero_", "aten::add", "aten::add_", "aten::sum",
@@ -272,6 +281,12 @@ def main():
         rows = [e for e in prof.key_averages(group_by_stack_n=5)
                 if e.key in small or (os.environ.get("SRL_PROFILE_ALL") and e.key.startswith("aten::") and e.key not in big
                                       and getattr(e, "self_device_time_total", 0) > 0)]
+        if os.environ.get("SRL_PROFILE_SHAPES"):  # library GEMMs by operand shapes, device time per call
+            for e in sorted((e for e in prof.key_averages(group_by_input_shape=True) if e.key in big),
+                            key=lambda e: -getattr(e, "device_time_total", 0))[:40]:
+                print(f"GEMM {e.key:12s} n={e.count / args.torch_profile:5.1f}/step "
+                      f"{getattr(e, 'device_time_total', 0) / max(e.count, 1):8.1f} us/call  {e.input_shapes}",
+                      file=sys.stderr, flush=True)
         rows.sort(key=lambda e: -e.count)
         for e in rows[:int(os.environ.get('SRL_PROFILE_TOP', 60))]:
             stack = " <- ".join(f.split("/")[-1] for f in e.stack[:5])

@@ -131,6 +131,7 @@ class ContinuousRollout:
         self.logits = post.new_empty(horizon, M, S)
         W = rec_lin.weight  # columns: (prior | action)
         self.rec_table = W[:, :S].t().contiguous()
+        self.act_table = W[:, S:].t().contiguous()  # [A, D]: the action columns, added inside the gather kernel
         self.a_table = self.layers[0][0].weight[:, :S].t().contiguous()
         self.buf[0, :, :S].copy_(post)
         self.buf[0, :, S:S + Hd].copy_(h)
@@ -150,8 +151,6 @@ class ContinuousRollout:
         M, S, Hd, A, G = self.M, self.S, self.Hd, self.A, self.G
         actor, buf = self.actor, self.buf
         init_std, min_std = float(actor.init_std), float(actor.min_std)
-        Wr = self.rec_lin.weight
-        Wr_a = Wr[:, S:]
         Wg = self.gru.linear.weight  # columns: (h | feat)
         gln = self.gru.layer_norm
         rln, tln = self.rec_ln, self.tr_ln
@@ -164,16 +163,18 @@ class ContinuousRollout:
         for t in range(self.H + 1):
             ga = (self.IDX[t], G, 0, S, self.a_table) + ((self.hm[t][:, hidm:hidm + Na],) if merge else ())
             out = self.trunk.step(t, buf[t, :, :S + Hd], gather=ga)
-            torch.addmm(self.head.bias, out, self.head.weight.t(), out=self.pre[t])
-            C.tn_head_sample_fwd(self.pre[t], self.u_act[t], init_std, min_std, -1.0, 1.0, self.loc[t], self.scale[t],
-                                 self.acts[t])
+            # head Linear + truncated-normal sample in one launch (the N = 2A GEMM folded into the sampler)
+            if not C.tn_head_linear_sample_fwd(out, self.head.weight, self.head.bias, self.u_act[t], init_std, min_std, -1.0,
+                                               1.0, self.pre[t], self.loc[t], self.scale[t], self.acts[t]):
+                torch.addmm(self.head.bias, out, self.head.weight.t(), out=self.pre[t])
+                C.tn_head_sample_fwd(self.pre[t], self.u_act[t], init_std, min_std, -1.0, 1.0, self.loc[t], self.scale[t],
+                                     self.acts[t])
             if t == self.H:
                 break
-            # recurrent MLP: action columns by a K = A GEMM, prior columns gathered, LayerNorm + act fused
-            Y = torch.mm(self.acts[t], Wr_a.t())
-            ok = C.onehot_gather_ln(Y, self.IDX[t], G, 0, self.rec_table, None, rln.weight, rln.bias, float(rln.eps),
+            # recurrent MLP in one launch: prior columns gathered, action columns as dense products, LayerNorm + act
+            ok = C.onehot_gather_ln(None, self.IDX[t], G, 0, self.rec_table, None, rln.weight, rln.bias, float(rln.eps),
                                     ops._act_code(rln.act), True, self.rec_z[t], buf[t, :, S + Hd:], self.rec_mean[t],
-                                    self.rec_rstd[t], err)
+                                    self.rec_rstd[t], err, self.acts[t], self.act_table)
             if not ok:
                 raise RuntimeError("onehot_gather_ln: unsupported recurrent layer width")
             gx = self.gx[t]
@@ -233,7 +234,9 @@ class ContinuousRollout:
         ldtr = self.tr_pre.stride(1)  # merged form: a column block of the per-step h products
         dtr = torch.empty(M, hid, device=dev)
         D = self.D
-        dz = torch.empty(M, D, device=dev)
+        # every step's recurrent-layer adjoint, so the action gradients take ONE [H M, D] x [D, A] GEMM after the
+        # chain (a per-step K = D, N = A product is a 32 x 32-tile library kernel at ~26 us each)
+        dz_all = torch.empty(H, M, D, device=dev)
         t_act, r_act = ops._act_code(tln.act), ops._act_code(rln.act)
         for t in range(H, 0, -1):
             s = t - 1  # the step that produced (prior_t, h_t)
@@ -250,16 +253,19 @@ class ContinuousRollout:
                               dadd=d_traj[s, :, S:] if (d_traj is not None and s > 0) else None)
             dcat = torch.mm(dgx, Wg)  # [M, Hd + D]: (h | x)
             # x_s = act(LN([prior_s | a_s] Wr^T)) (no bias)
+            dz = dz_all[s]
             C.ln_act_bwd_into(self.rec_z[s], D, dcat[:, Hd:], Hd + D, dz, D, rln.weight, rln.bias, self.rec_mean[s],
                               self.rec_rstd[s], None, None, None, None, M, D, 1, r_act)
-            d_a[s].addmm_(dz, Wr[:, S:])
             if s == 0:
                 break  # (prior_0, h_0) are the detached posteriors
-            dp = torch.mm(dz, Wr[:, :S])
-            if d_traj is not None:
-                dp += d_traj[s, :, :S]
+            # d prior_s = dz Wr_prior (+ the trajectory gradient of prior_s, as the GEMM's addend).  Wr_prior read as the
+            # contiguous [S, D] table of the forward's gathers: the [D, S] column slice of Wr has row stride S + A (not
+            # 16-byte aligned), which sends the library to a 32 x 32-tile kernel (~26 us vs ~10 us per step)
+            wp = self.rec_table.t()
+            dp = torch.mm(dz, wp) if d_traj is None else torch.addmm(d_traj[s, :, :S], dz, wp)
             # dh_s = (direct + d_traj) + the h half of d(h | x); the consumed dh buffer becomes the next dh_prev
             dh, dh_prev = dh_prev.add_(dcat[:, :Hd]), dh
+        d_a[:H].view(H * M, A).addmm_(dz_all.view(H * M, D), Wr[:, S:])
         # one batched actor backward over all (H+1) M rows
         R = (H + 1) * M
         dpre = C.tn_head_sample_bwd(self.loc.view(R, A), self.scale.view(R, A), self.u_act.view(R, A), d_a.view(R, A),

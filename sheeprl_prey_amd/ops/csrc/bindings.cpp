@@ -66,6 +66,8 @@ void launch_truncnorm_logprob_fwd(const float*, const float*, const float*, cons
                                   int, hipStream_t);
 void launch_truncnorm_logprob_bwd(const float*, const float*, const float*, const float*, int, const float*, int, const float*,
                                   float*, float*, float*, int, int, hipStream_t);
+bool launch_tn_head_linear_sample_fwd(const float*, int, const float*, const float*, const float*, float, float, float, float,
+                                      float*, float*, float*, float*, int, int, int, int, hipStream_t);
 void launch_tn_head_sample_fwd(const float*, int, const float*, float, float, float, float, float*, float*, float*, int, int, int,
                                hipStream_t);
 void launch_tn_head_sample_bwd(const float*, const float*, const float*, const float*, const float*, float, float, float, float*,
@@ -776,6 +778,26 @@ void tn_head_sample_fwd(torch::Tensor pre, torch::Tensor u, double init_std, dou
                             mp(scale), mp(x), x.stride(0), M, A, cur_stream());
 }
 
+// The same with the head Linear folded in: y [M, K] (row-strided), W [2A, K], b [2A] (optional) -> pre [M, 2A]
+// (contiguous), loc, scale [M, A], the sample into x.  False: shape outside the kernel (caller keeps GEMM + sample).
+bool tn_head_linear_sample_fwd(torch::Tensor y, torch::Tensor W, c10::optional<torch::Tensor> b, torch::Tensor u,
+                               double init_std, double min_std, double lo, double hi, torch::Tensor pre, torch::Tensor loc,
+                               torch::Tensor scale, torch::Tensor x) {
+  check_f32(W, "W");
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == torch::kFloat32 && y.dim() == 2 && y.stride(1) == 1 && W.dim() == 2 &&
+                  x.dim() == 2 && x.stride(1) == 1,
+              "tn_head_linear_sample: 2-D row-strided float32 y / x, contiguous W");
+  const int M = y.size(0), K = y.size(1), A = W.size(0) / 2;
+  TORCH_CHECK(W.size(0) == 2 * A && W.size(1) == K && pre.is_contiguous() && pre.numel() == (int64_t)M * 2 * A &&
+                  x.size(0) == M && x.size(1) == A && u.is_contiguous() && u.numel() == (int64_t)M * A && loc.is_contiguous() &&
+                  scale.is_contiguous() && loc.numel() == (int64_t)M * A && scale.numel() == (int64_t)M * A,
+              "tn_head_linear_sample_fwd: shapes");
+  if (b.has_value() && b->defined()) TORCH_CHECK(b->is_contiguous() && b->numel() == 2 * A, "tn_head_linear_sample_fwd: bias");
+  return launch_tn_head_linear_sample_fwd(fp(y), y.stride(0), fp(W), b.has_value() && b->defined() ? fp(*b) : nullptr, fp(u),
+                                          (float)init_std, (float)min_std, (float)lo, (float)hi, mp(pre), mp(loc), mp(scale),
+                                          mp(x), x.stride(0), M, K, A, cur_stream());
+}
+
 // d pre [M, 2A] of the head + sample above: gx = d sample (optional), dpre_in = a gradient reaching pre directly
 // (optional, [M, 2A] contiguous).
 torch::Tensor tn_head_sample_bwd(torch::Tensor loc, torch::Tensor scale, torch::Tensor u, c10::optional<torch::Tensor> gx,
@@ -1197,6 +1219,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("truncnorm_logprob_fwd", &truncnorm_logprob_fwd);
   m.def("truncnorm_logprob_bwd", &truncnorm_logprob_bwd);
   m.def("tn_head_sample_fwd", &tn_head_sample_fwd);
+  m.def("tn_head_linear_sample_fwd", &tn_head_linear_sample_fwd);
   m.def("tn_head_sample_bwd", &tn_head_sample_bwd);
   m.def("set_scanp_prof", &set_scanp_prof);
   m.def("set_scanp_health", &set_scanp_health);

@@ -87,7 +87,7 @@ void launch_onehot_index(const float* x, int ldx, int M, int G, int C, int* idx,
 bool launch_onehot_gather_ln(const float* Y, int ldy, const int* idx, int ldi, int G, int off, const float* T, int K,
                              const float* bias, const float* gamma, const float* beta, float eps, int act, int ln,
                              float* z_out, int ldz, float* y_out, int ldo, float* mean, float* rstd, int M, int N, int* err,
-                             hipStream_t st);
+                             hipStream_t st, const float* xa = nullptr, int ldxa = 0, int nA = 0, const float* Wa = nullptr);
 
 namespace {
 
@@ -123,7 +123,8 @@ void onehot_index(torch::Tensor x, int64_t C, torch::Tensor idx, int64_t off) {
 bool onehot_gather_ln(c10::optional<torch::Tensor> Y, torch::Tensor idx, int64_t G, int64_t off, torch::Tensor table,
                       c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta,
                       double eps, int64_t act, bool ln, c10::optional<torch::Tensor> z_out, torch::Tensor y_out,
-                      c10::optional<torch::Tensor> mean, c10::optional<torch::Tensor> rstd, c10::optional<torch::Tensor> err) {
+                      c10::optional<torch::Tensor> mean, c10::optional<torch::Tensor> rstd, c10::optional<torch::Tensor> err,
+                      c10::optional<torch::Tensor> xa, c10::optional<torch::Tensor> Wa) {
   TORCH_CHECK(table.is_cuda() && table.scalar_type() == torch::kFloat32 && table.dim() == 2 && table.is_contiguous(),
               "onehot_gather_ln: table [K, N] contiguous float32");
   const int64_t K = table.size(0), N = table.size(1), M = y_out.size(0);
@@ -150,9 +151,24 @@ bool onehot_gather_ln(c10::optional<torch::Tensor> Y, torch::Tensor idx, int64_t
   }
   float* mp_ = mean.has_value() && mean->defined() ? const_cast<float*>(optf(mean, "mean", M)) : nullptr;
   float* rp_ = rstd.has_value() && rstd->defined() ? const_cast<float*>(optf(rstd, "rstd", M)) : nullptr;
+  // optional dense input columns: xa [M, nA] row-strided, Wa [nA, N] contiguous (acc += xa Wa)
+  const float* xap = nullptr;
+  const float* wap = nullptr;
+  int64_t ldxa = 0, nA = 0;
+  if (xa.has_value() && xa->defined()) {
+    TORCH_CHECK(Wa.has_value() && Wa->defined() && Wa->is_cuda() && Wa->scalar_type() == torch::kFloat32 && Wa->dim() == 2 &&
+                    Wa->is_contiguous() && Wa->size(1) == N,
+                "onehot_gather_ln: Wa [nA, N] contiguous float32");
+    nA = Wa->size(0);
+    rowview(*xa, "xa", M, nA, torch::kFloat32);
+    xap = xa->data_ptr<float>();
+    ldxa = xa->stride(0);
+    wap = Wa->data_ptr<float>();
+  }
   return launch_onehot_gather_ln(yp, ldy, idx.data_ptr<int>(), idx.stride(0), G, off, table.data_ptr<float>(), K,
                                  optf(bias, "bias", N), optf(gamma, "gamma", N), optf(beta, "beta", N), (float)eps, act,
-                                 ln ? 1 : 0, zp, ldz, y_out.data_ptr<float>(), y_out.stride(0), mp_, rp_, M, N, ep, stream());
+                                 ln ? 1 : 0, zp, ldz, y_out.data_ptr<float>(), y_out.stride(0), mp_, rp_, M, N, ep, stream(),
+                                 xap, (int)ldxa, (int)nA, wap);
 }
 
 
@@ -826,7 +842,8 @@ void register_ext(pybind11::module& m) {
   m.def("onehot_gather_ln", &onehot_gather_ln, pybind11::arg("Y"), pybind11::arg("idx"), pybind11::arg("G"), pybind11::arg("off"),
         pybind11::arg("table"), pybind11::arg("bias"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("eps"),
         pybind11::arg("act"), pybind11::arg("ln"), pybind11::arg("z_out"), pybind11::arg("y_out"), pybind11::arg("mean"),
-        pybind11::arg("rstd"), pybind11::arg("err") = pybind11::none());
+        pybind11::arg("rstd"), pybind11::arg("err") = pybind11::none(), pybind11::arg("xa") = pybind11::none(),
+        pybind11::arg("Wa") = pybind11::none());
   m.def("gru_cell_fwd", &gru_cell_fwd);
   m.def("gru_cell_bwd", &gru_cell_bwd);
   m.def("lstm_fwd", &lstm_fwd);

@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
     const float* __restrict__ T, int K, const float* __restrict__ bias, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, int act, int ln, float* __restrict__ z_out, int ldz,
     float* __restrict__ y_out, int ldo, float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, int N,
-    int* __restrict__ err) {
+    int* __restrict__ err, const float* __restrict__ xa, int ldxa, int nA, const float* __restrict__ Wa) {
   static_assert(WPR == 1 || WPR == 2, "onehot_gather_ln: 1 or 2 waves per row");
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, part = wave % WPR;
@@ -84,6 +84,16 @@ __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
     const int i4 = c4 + lane + 64 * v;
     acc[v] = (live && Y != nullptr && i4 < N4) ? reinterpret_cast<const f4*>(Y + (int64_t)r * ldy)[i4] : zero4();
     if (live && bias != nullptr && i4 < N4) acc[v] += reinterpret_cast<const f4*>(bias)[i4];
+  }
+  // dense columns of the layer's input (the action part of the recurrent input: nA <= 64 small products per
+  // element, in place of a K = nA library GEMM launch): acc += sum_a xa[r, a] Wa[a, :]
+  for (int a = 0; a < nA; ++a) {
+    const float w = live ? xa[(int64_t)r * ldxa + a] : 0.f;
+#pragma unroll
+    for (int v = 0; v < NV4; ++v) {
+      const int i4 = c4 + lane + 64 * v;
+      if (i4 < N4) acc[v] += w * reinterpret_cast<const f4*>(Wa + (int64_t)a * N)[i4];
+    }
   }
   const int* ir = idx + (int64_t)(live ? r : 0) * ldi;
   // the row's hot indices: lanes < G load one each, then broadcast (wave-uniform loop below)
@@ -166,20 +176,21 @@ void launch_onehot_index(const float* x, int ldx, int M, int G, int C, int* idx,
 bool launch_onehot_gather_ln(const float* Y, int ldy, const int* idx, int ldi, int G, int off, const float* T, int K,
                              const float* bias, const float* gamma, const float* beta, float eps, int act, int ln,
                              float* z_out, int ldz, float* y_out, int ldo, float* mean, float* rstd, int M, int N, int* err,
-                             hipStream_t st) {
+                             hipStream_t st, const float* xa, int ldxa, int nA, const float* Wa) {
+  if (nA < 0 || nA > 64 || (nA > 0 && (xa == nullptr || Wa == nullptr))) return false;
   if (N % 4 != 0 || N > 4096 || G > 64 || M <= 0) return false;
   const int nv = (N + 255) / 256;
   const dim3 block(256);
   if (nv == 2 && M <= 4096) {  // latency-bound rollout sizes: two waves per 512-wide row
     hipLaunchKernelGGL((srl::onehot::onehot_gather_ln_kernel<1, 2>), dim3((M + 1) / 2), block, 0, st, Y, ldy, idx, ldi, G, off,
-                       T, K, bias, gamma, beta, eps, act, ln, z_out, ldz, y_out, ldo, mean, rstd, M, N, err);
+                       T, K, bias, gamma, beta, eps, act, ln, z_out, ldz, y_out, ldo, mean, rstd, M, N, err, xa, ldxa, nA, Wa);
     return true;
   }
   const dim3 grid((M + 3) / 4);
 #define OG(NV)                                                                                                          \
   if (nv <= NV) {                                                                                                       \
     hipLaunchKernelGGL((srl::onehot::onehot_gather_ln_kernel<NV, 1>), grid, block, 0, st, Y, ldy, idx, ldi, G, off, T, K, \
-                       bias, gamma, beta, eps, act, ln, z_out, ldz, y_out, ldo, mean, rstd, M, N, err);                   \
+                       bias, gamma, beta, eps, act, ln, z_out, ldz, y_out, ldo, mean, rstd, M, N, err, xa, ldxa, nA, Wa); \
     return true;                                                                                                        \
   }
   OG(1) OG(2) OG(4) OG(8) OG(16)

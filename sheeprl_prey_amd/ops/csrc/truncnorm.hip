@@ -125,6 +125,52 @@ __global__ void head_sample_fwd(const float* __restrict__ pre, int ldp, const fl
   }
 }
 
+// The head Linear folded in: pre = y W^T + b (y [M, K] row-strided, W [2A, K], 2A <= 64, K = 64 KM) computed per
+// row by one wave (K products per lane, one DPP wave reduction per head column, W staged per 4-row workgroup in
+// LDS under the row loads), written out for the backward, then sampled as head_sample_fwd.  At the continuous imagination shape
+// (M = 1024, K = 512, 2A = 12) the library ran this N = 12 GEMM as a 32 x 32-tile kernel at ~26 us per step.
+template <int KM>
+__global__ void __launch_bounds__(256) head_linear_sample_fwd(const float* __restrict__ y, int ldy, const float* __restrict__ W,
+                                                             const float* __restrict__ b, const float* __restrict__ u,
+                                                             float init_std, float min_std, float lo, float hi,
+                                                             float* __restrict__ pre, float* __restrict__ loc_out,
+                                                             float* __restrict__ scale_out, float* __restrict__ x, int ldx,
+                                                             int M, int A) {
+  extern __shared__ float ws[];  // [2A][64 KM]
+  const int K = 64 * KM, NA = 2 * A;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = blockIdx.x * 4 + wave;  // one row per wave: M / 4 workgroups
+  float v[KM];
+#pragma unroll
+  for (int m = 0; m < KM; ++m) v[m] = r < M ? y[(int64_t)r * ldy + lane + 64 * m] : 0.f;  // in flight under the staging
+  for (int i = threadIdx.x; i < NA * K; i += 256) ws[i] = W[i];
+  __syncthreads();
+  if (r < M) {
+    float mine = 0.f;  // lane j keeps head column j
+#pragma unroll 4
+    for (int j = 0; j < NA; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int m = 0; m < KM; ++m) s += v[m] * ws[j * K + lane + 64 * m];
+      s = wave_sum_dpp(s) + (b ? b[j] : 0.f);
+      if (lane == j) mine = s;
+    }
+    if (lane < NA) pre[(int64_t)r * NA + lane] = mine;
+    const float ps = __shfl(mine, lane + A, 64);  // the log-std column of action `lane`
+    if (lane < A) {
+      const int i = r * A + lane;
+      const float l = tanhf(mine);
+      const float sg = 1.f / (1.f + __expf(-0.5f * (ps + init_std)));
+      const float sc = 2.f * sg + min_std;
+      const Trunc t = bounds(l, sc, lo, hi);
+      const float xi = cdf(t.alpha) + u[i] * t.Z;
+      loc_out[i] = l;
+      scale_out[i] = sc;
+      x[(int64_t)r * ldx + lane] = l + sc * (SQRT_2 * erfinvf(2.f * xi - 1.f));
+    }
+  }
+}
+
 // d pre [M, 2A] = (d loc * (1 - loc^2) | d scale * sg (1 - sg)) (+ dpre_in), with (d loc, d scale) the
 // rsample backward of gx (gx may be null: only dpre_in), sg = (scale - min_std) / 2.
 __global__ void head_sample_bwd(const float* __restrict__ loc, const float* __restrict__ scale, const float* __restrict__ u,
@@ -193,6 +239,21 @@ void launch_tn_head_sample_fwd(const float* pre, int ldp, const float* u, float 
   if (M * A > 0)
     hipLaunchKernelGGL(head_sample_fwd, dim3(grid_for(M * A)), dim3(256), 0, st, pre, ldp, u, init_std, min_std, lo, hi, loc,
                        scale, x, ldx, M, A);
+}
+
+bool launch_tn_head_linear_sample_fwd(const float* y, int ldy, const float* W, const float* b, const float* u, float init_std,
+                                      float min_std, float lo, float hi, float* pre, float* loc, float* scale, float* x, int ldx,
+                                      int M, int K, int A, hipStream_t st) {
+  if (M <= 0 || A < 1 || 2 * A > 64 || K % 64 != 0 || K > 1024 || (size_t)2 * A * K * 4 > 64 * 1024) return false;
+  const dim3 grid((M + 3) / 4);
+  const size_t shm = (size_t)2 * A * K * sizeof(float);
+  switch (K / 64) {
+#define HL(KM) \
+  case KM: hipLaunchKernelGGL(head_linear_sample_fwd<KM>, grid, dim3(256), shm, st, y, ldy, W, b, u, init_std, min_std, lo, hi, pre, loc, scale, x, ldx, M, A); return true;
+    HL(1) HL(2) HL(4) HL(8) HL(16)
+#undef HL
+    default: return false;
+  }
 }
 
 void launch_tn_head_sample_bwd(const float* loc, const float* scale, const float* u, const float* gx, const float* dpre_in,

@@ -41,3 +41,68 @@ def test_actor_loss_cont_matches_fp64_eager(T, M, A, spread):
     scale = float(p64.grad.abs().max())
     torch.testing.assert_close(pre.grad.double(), p64.grad, rtol=1e-3, atol=1e-4 * scale)
     assert float(pre.grad[-1].abs().max()) == 0.0  # the last imagined step is outside the objective
+
+
+@pytest.mark.parametrize("M,K,A,bias", [(1024, 512, 6, True), (37, 256, 1, False), (100, 1024, 8, True)])
+def test_head_linear_sample_matches_gemm_then_sample(M, K, A, bias):
+    """``tn_head_linear_sample_fwd`` (head Linear folded into the truncated-normal sampler, csrc/truncnorm.hip) vs
+    the library GEMM + ``tn_head_sample_fwd``, on the same uniforms; the head product against fp64."""
+    from sheeprl_prey_amd import ops
+
+    C = ops._ext()
+    torch.manual_seed(M + K)
+    ys = torch.randn(M, K + 8, device="cuda")
+    y = ys[:, :K]  # row-strided
+    W = torch.randn(2 * A, K, device="cuda") / K ** 0.5
+    b = torch.randn(2 * A, device="cuda") if bias else None
+    u = torch.rand(M, A, device="cuda").clamp(1e-6, 1 - 1e-6)
+    outs = []
+    for fused in (True, False):
+        pre = torch.empty(M, 2 * A, device="cuda")
+        loc, scale = torch.empty(M, A, device="cuda"), torch.empty(M, A, device="cuda")
+        x = torch.full((M, A + 3), -9.0, device="cuda")[:, :A]
+        if fused:
+            assert C.tn_head_linear_sample_fwd(y, W, b, u, 0.0, 0.1, -1.0, 1.0, pre, loc, scale, x)
+        else:
+            torch.addmm(b if bias else torch.zeros(2 * A, device="cuda"), y, W.t(), out=pre)
+            C.tn_head_sample_fwd(pre, u, 0.0, 0.1, -1.0, 1.0, loc, scale, x)
+        outs.append((pre, loc, scale, x))
+    (p1, l1, s1, x1), (p0, l0, s0, x0) = outs
+    ref = y.double() @ W.double().t() + (b.double() if bias else 0.0)
+    torch.testing.assert_close(p1.double(), ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(l1, l0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x1, x0, rtol=1e-4, atol=1e-4)
+    # outside the kernel's LDS budget (2A x K fp32 > 64 KB): nothing launched, the caller keeps GEMM + sample
+    W2 = torch.randn(2 * 9, 1024, device="cuda")
+    y2 = torch.randn(4, 1024, device="cuda")
+    p2, l2, s2, x2 = (torch.empty(4, 18, device="cuda"), torch.empty(4, 9, device="cuda"), torch.empty(4, 9, device="cuda"),
+                      torch.empty(4, 9, device="cuda"))
+    assert not C.tn_head_linear_sample_fwd(y2, W2, None, torch.rand(4, 9, device="cuda"), 0.0, 0.1, -1.0, 1.0, p2, l2, s2, x2)
+
+
+@pytest.mark.parametrize("M,N,G,nA", [(1024, 512, 32, 6), (33, 256, 8, 1), (64, 1024, 16, 12)])
+def test_onehot_gather_ln_dense_columns(M, N, G, nA):
+    """``onehot_gather_ln`` with dense input columns (``xa @ Wa`` added in-kernel: the recurrent layer's action part
+    of the continuous rollout) vs the one-hot-expanded dense layer in fp64: pre-norm values, statistics, output."""
+    import torch.nn.functional as F
+
+    from sheeprl_prey_amd import ops
+
+    C = ops._ext()
+    torch.manual_seed(M + N)
+    K = G * 32
+    table = torch.randn(K, N, device="cuda") / 8
+    idx = (torch.randint(0, 32, (M, G), device="cuda") + torch.arange(G, device="cuda") * 32).int()
+    xa = torch.randn(M, nA + 2, device="cuda")[:, :nA]
+    Wa = torch.randn(nA, N, device="cuda") / 3
+    gamma, beta = 1 + 0.1 * torch.randn(N, device="cuda"), 0.1 * torch.randn(N, device="cuda")
+    z, y = torch.empty(M, N, device="cuda"), torch.empty(M, N, device="cuda")
+    mean, rstd = torch.empty(M, device="cuda"), torch.empty(M, device="cuda")
+    assert C.onehot_gather_ln(None, idx, G, 0, table, None, gamma, beta, 1e-3, ops._act_code("silu"), True, z, y, mean,
+                              rstd, None, xa, Wa)
+    onehot = torch.zeros(M, K, device="cuda", dtype=torch.float64).scatter_(1, idx.long(), 1.0)
+    zr = onehot @ table.double() + xa.double() @ Wa.double()
+    yr = F.silu(F.layer_norm(zr, (N,), gamma.double(), beta.double(), 1e-3))
+    torch.testing.assert_close(z.double(), zr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(y.double(), yr, rtol=1e-4, atol=1e-4)
