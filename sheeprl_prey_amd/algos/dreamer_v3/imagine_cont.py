@@ -162,10 +162,10 @@ class ContinuousRollout:
             Wgx_t = Wg[:, Hd:].t()
         for t in range(self.H + 1):
             ga = (self.IDX[t], G, 0, S, self.a_table) + ((self.hm[t][:, hidm:hidm + Na],) if merge else ())
-            out = self.trunk.step(t, buf[t, :, :S + Hd], gather=ga)
-            # head Linear + truncated-normal sample in one launch (the N = 2A GEMM folded into the sampler)
-            if not C.tn_head_linear_sample_fwd(out, self.head.weight, self.head.bias, self.u_act[t], init_std, min_std, -1.0,
-                                               1.0, self.pre[t], self.loc[t], self.scale[t], self.acts[t]):
+            # the trunk's last LayerNorm + the head Linear + the truncated-normal sample in one launch when it fits
+            tn = (self.head, self.u_act[t], init_std, min_std, self.pre[t], self.loc[t], self.scale[t], self.acts[t])
+            out = self.trunk.step(t, buf[t, :, :S + Hd], gather=ga, tail_tn=tn)
+            if out is not None:
                 torch.addmm(self.head.bias, out, self.head.weight.t(), out=self.pre[t])
                 C.tn_head_sample_fwd(self.pre[t], self.u_act[t], init_std, min_std, -1.0, 1.0, self.loc[t], self.scale[t],
                                      self.acts[t])

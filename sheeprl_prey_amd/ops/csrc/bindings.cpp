@@ -67,7 +67,8 @@ void launch_truncnorm_logprob_fwd(const float*, const float*, const float*, cons
 void launch_truncnorm_logprob_bwd(const float*, const float*, const float*, const float*, int, const float*, int, const float*,
                                   float*, float*, float*, int, int, hipStream_t);
 bool launch_tn_head_linear_sample_fwd(const float*, int, const float*, const float*, const float*, float, float, float, float,
-                                      float*, float*, float*, float*, int, int, int, int, hipStream_t);
+                                      float*, float*, float*, float*, int, int, int, int, hipStream_t, const float*,
+                                      const float*, float, int, float*, int, float*, float*);
 void launch_tn_head_sample_fwd(const float*, int, const float*, float, float, float, float, float*, float*, float*, int, int, int,
                                hipStream_t);
 void launch_tn_head_sample_bwd(const float*, const float*, const float*, const float*, const float*, float, float, float, float*,
@@ -782,7 +783,9 @@ void tn_head_sample_fwd(torch::Tensor pre, torch::Tensor u, double init_std, dou
 // (contiguous), loc, scale [M, A], the sample into x.  False: shape outside the kernel (caller keeps GEMM + sample).
 bool tn_head_linear_sample_fwd(torch::Tensor y, torch::Tensor W, c10::optional<torch::Tensor> b, torch::Tensor u,
                                double init_std, double min_std, double lo, double hi, torch::Tensor pre, torch::Tensor loc,
-                               torch::Tensor scale, torch::Tensor x) {
+                               torch::Tensor scale, torch::Tensor x, c10::optional<torch::Tensor> ln_w,
+                               c10::optional<torch::Tensor> ln_b, double ln_eps, int64_t act, c10::optional<torch::Tensor> y_out,
+                               c10::optional<torch::Tensor> mean, c10::optional<torch::Tensor> rstd) {
   check_f32(W, "W");
   TORCH_CHECK(y.is_cuda() && y.scalar_type() == torch::kFloat32 && y.dim() == 2 && y.stride(1) == 1 && W.dim() == 2 &&
                   x.dim() == 2 && x.stride(1) == 1,
@@ -793,9 +796,20 @@ bool tn_head_linear_sample_fwd(torch::Tensor y, torch::Tensor W, c10::optional<t
                   scale.is_contiguous() && loc.numel() == (int64_t)M * A && scale.numel() == (int64_t)M * A,
               "tn_head_linear_sample_fwd: shapes");
   if (b.has_value() && b->defined()) TORCH_CHECK(b->is_contiguous() && b->numel() == 2 * A, "tn_head_linear_sample_fwd: bias");
+  // optional LayerNorm + activation of y first (y = the trunk's last pre-activation): weights [K], the normalised
+  // row into y_out (row-strided [M, K]), statistics into mean / rstd [M]
+  const bool ln = ln_w.has_value() && ln_w->defined();
+  if (ln) {
+    TORCH_CHECK(ln_b.has_value() && ln_b->defined() && ln_w->numel() == K && ln_b->numel() == K && y_out.has_value() &&
+                    y_out->defined() && y_out->dim() == 2 && y_out->stride(1) == 1 && y_out->size(0) == M && y_out->size(1) == K &&
+                    mean.has_value() && rstd.has_value() && mean->numel() == M && rstd->numel() == M,
+                "tn_head_linear_sample_fwd: LayerNorm operands");
+  }
   return launch_tn_head_linear_sample_fwd(fp(y), y.stride(0), fp(W), b.has_value() && b->defined() ? fp(*b) : nullptr, fp(u),
                                           (float)init_std, (float)min_std, (float)lo, (float)hi, mp(pre), mp(loc), mp(scale),
-                                          mp(x), x.stride(0), M, K, A, cur_stream());
+                                          mp(x), x.stride(0), M, K, A, cur_stream(), ln ? fp(*ln_w) : nullptr,
+                                          ln ? fp(*ln_b) : nullptr, (float)ln_eps, (int)act, ln ? mp(*y_out) : nullptr,
+                                          ln ? y_out->stride(0) : 0, ln ? mp(*mean) : nullptr, ln ? mp(*rstd) : nullptr);
 }
 
 // d pre [M, 2A] of the head + sample above: gx = d sample (optional), dpre_in = a gradient reaching pre directly
@@ -1219,7 +1233,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("truncnorm_logprob_fwd", &truncnorm_logprob_fwd);
   m.def("truncnorm_logprob_bwd", &truncnorm_logprob_bwd);
   m.def("tn_head_sample_fwd", &tn_head_sample_fwd);
-  m.def("tn_head_linear_sample_fwd", &tn_head_linear_sample_fwd);
+  m.def("tn_head_linear_sample_fwd", &tn_head_linear_sample_fwd, pybind11::arg("y"), pybind11::arg("W"), pybind11::arg("b"),
+        pybind11::arg("u"), pybind11::arg("init_std"), pybind11::arg("min_std"), pybind11::arg("lo"), pybind11::arg("hi"),
+        pybind11::arg("pre"), pybind11::arg("loc"), pybind11::arg("scale"), pybind11::arg("x"),
+        pybind11::arg("ln_w") = pybind11::none(), pybind11::arg("ln_b") = pybind11::none(), pybind11::arg("ln_eps") = 0.0,
+        pybind11::arg("act") = 0, pybind11::arg("y_out") = pybind11::none(), pybind11::arg("mean") = pybind11::none(),
+        pybind11::arg("rstd") = pybind11::none());
   m.def("tn_head_sample_bwd", &tn_head_sample_bwd);
   m.def("set_scanp_prof", &set_scanp_prof);
   m.def("set_scanp_health", &set_scanp_health);

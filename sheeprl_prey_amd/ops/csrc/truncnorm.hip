@@ -135,7 +135,10 @@ __global__ void __launch_bounds__(256) head_linear_sample_fwd(const float* __res
                                                              float init_std, float min_std, float lo, float hi,
                                                              float* __restrict__ pre, float* __restrict__ loc_out,
                                                              float* __restrict__ scale_out, float* __restrict__ x, int ldx,
-                                                             int M, int A) {
+                                                             int M, int A, const float* __restrict__ lng,
+                                                             const float* __restrict__ lnb, float lneps, int act,
+                                                             float* __restrict__ yo, int ldyo, float* __restrict__ mean_out,
+                                                             float* __restrict__ rstd_out) {
   extern __shared__ float ws[];  // [2A][64 KM]
   const int K = 64 * KM, NA = 2 * A;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -144,6 +147,28 @@ __global__ void __launch_bounds__(256) head_linear_sample_fwd(const float* __res
 #pragma unroll
   for (int m = 0; m < KM; ++m) v[m] = r < M ? y[(int64_t)r * ldy + lane + 64 * m] : 0.f;  // in flight under the staging
   for (int i = threadIdx.x; i < NA * K; i += 256) ws[i] = W[i];
+  if (lng != nullptr && r < M) {
+    // y holds the trunk's last pre-activation: its LayerNorm + activation first (the row is in registers), the
+    // normalised row and its statistics written out for the trunk backward
+    float a = 0.f;
+#pragma unroll
+    for (int m = 0; m < KM; ++m) a += v[m];
+    const float mu = wave_sum_dpp(a) / K;
+    float q = 0.f;
+#pragma unroll
+    for (int m = 0; m < KM; ++m) q += (v[m] - mu) * (v[m] - mu);
+    const float rs = rsqrtf(wave_sum_dpp(q) / K + lneps);
+#pragma unroll
+    for (int m = 0; m < KM; ++m) {
+      const int k = lane + 64 * m;
+      v[m] = act_fwd((v[m] - mu) * rs * lng[k] + lnb[k], act);
+      yo[(int64_t)r * ldyo + k] = v[m];
+    }
+    if (lane == 0) {
+      mean_out[r] = mu;
+      rstd_out[r] = rs;
+    }
+  }
   __syncthreads();
   if (r < M) {
     float mine = 0.f;  // lane j keeps head column j
@@ -243,13 +268,15 @@ void launch_tn_head_sample_fwd(const float* pre, int ldp, const float* u, float 
 
 bool launch_tn_head_linear_sample_fwd(const float* y, int ldy, const float* W, const float* b, const float* u, float init_std,
                                       float min_std, float lo, float hi, float* pre, float* loc, float* scale, float* x, int ldx,
-                                      int M, int K, int A, hipStream_t st) {
+                                      int M, int K, int A, hipStream_t st, const float* lng, const float* lnb, float lneps,
+                                      int act, float* yo, int ldyo, float* mean_out, float* rstd_out) {
+  if (lng != nullptr && (lnb == nullptr || yo == nullptr || mean_out == nullptr || rstd_out == nullptr)) return false;
   if (M <= 0 || A < 1 || 2 * A > 64 || K % 64 != 0 || K > 1024 || (size_t)2 * A * K * 4 > 64 * 1024) return false;
   const dim3 grid((M + 3) / 4);
   const size_t shm = (size_t)2 * A * K * sizeof(float);
   switch (K / 64) {
 #define HL(KM) \
-  case KM: hipLaunchKernelGGL(head_linear_sample_fwd<KM>, grid, dim3(256), shm, st, y, ldy, W, b, u, init_std, min_std, lo, hi, pre, loc, scale, x, ldx, M, A); return true;
+  case KM: hipLaunchKernelGGL(head_linear_sample_fwd<KM>, grid, dim3(256), shm, st, y, ldy, W, b, u, init_std, min_std, lo, hi, pre, loc, scale, x, ldx, M, A, lng, lnb, lneps, act, yo, ldyo, mean_out, rstd_out); return true;
     HL(1) HL(2) HL(4) HL(8) HL(16)
 #undef HL
     default: return false;

@@ -58,7 +58,7 @@ class TrunkRecord:
         self.onehot = None
 
     @torch.no_grad()
-    def step(self, t: int, x: Tensor, gather=None, tail=None) -> Optional[Tensor]:
+    def step(self, t: int, x: Tensor, gather=None, tail=None, tail_tn=None) -> Optional[Tensor]:
         """Forward of step ``t`` on ``x`` [M, K0] (row stride allowed); returns the trunk output [M, N].
         ``gather`` = (idx, G, off, n_onehot, table[, Y]): the first ``n_onehot`` input columns are one-hot with hot
         columns ``idx - off`` - the first layer is then a GEMM over the dense columns (or ``Y``, that product
@@ -66,7 +66,10 @@ class TrunkRecord:
         LayerNorm fused (``ops/onehot.py``).
         ``tail`` = (head Linear, uniforms [M], unimix, sample_out, idx_out, idx_off): the last LayerNorm, the head
         and the unimix one-hot sample run as one kernel (``csrc/actor_tail.hip``); returns None when it did (the
-        sample is in ``sample_out``), else the trunk output as without ``tail``."""
+        sample is in ``sample_out``), else the trunk output as without ``tail``.
+        ``tail_tn`` = (head Linear, uniforms [M, A], init_std, min_std, pre_out, loc, scale, sample_out): the continuous
+        form - the last LayerNorm, the head and the truncated-normal sample as one kernel
+        (``csrc/truncnorm.hip`` head_linear_sample_fwd); None when it did."""
         C = ops._ext()
         M = self.M
         for i, (lin, ln) in enumerate(self.layers):
@@ -90,6 +93,13 @@ class TrunkRecord:
                 if C.actor_tail(pre, self.y[i][t], ln.weight, ln.bias, self.mean[i][t], self.rstd[i][t], float(ln.eps),
                                 ops._act_code(ln.act), head.weight, head.bias, uni, float(alpha), sample_out, idx_out,
                                 int(ioff)):
+                    return None
+            if tail_tn is not None and i == len(self.layers) - 1:
+                head, u, init_std, min_std, pre_out, loc, scale, sample_out = tail_tn
+                if C.tn_head_linear_sample_fwd(pre, head.weight, head.bias, u, float(init_std), float(min_std), -1.0, 1.0,
+                                               pre_out, loc, scale, sample_out, ln_w=ln.weight, ln_b=ln.bias,
+                                               ln_eps=float(ln.eps), act=ops._act_code(ln.act), y_out=self.y[i][t],
+                                               mean=self.mean[i][t], rstd=self.rstd[i][t]):
                     return None
             C.ln_act_fwd_into(pre, N, self.y[i][t], N, ln.weight, ln.bias, self.mean[i][t], self.rstd[i][t], M, N, 1,
                               float(ln.eps), ops._act_code(ln.act))

@@ -106,3 +106,32 @@ def test_onehot_gather_ln_dense_columns(M, N, G, nA):
     yr = F.silu(F.layer_norm(zr, (N,), gamma.double(), beta.double(), 1e-3))
     torch.testing.assert_close(z.double(), zr, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(y.double(), yr, rtol=1e-4, atol=1e-4)
+
+
+def test_head_linear_sample_with_layernorm_prologue():
+    """The trunk's last LayerNorm + SiLU folded in front of the head (``ln_w`` ...): normalised row, statistics,
+    head outputs and samples vs ``ln_act_fwd_into`` + the unfused head."""
+    from sheeprl_prey_amd import ops
+
+    C = ops._ext()
+    torch.manual_seed(11)
+    M, K, A = 1024, 512, 6
+    z = torch.randn(M, K + 16, device="cuda")[:, :K] * 2 + 0.5
+    g, bb = 1 + 0.1 * torch.randn(K, device="cuda"), 0.1 * torch.randn(K, device="cuda")
+    W, b = torch.randn(2 * A, K, device="cuda") / K ** 0.5, torch.randn(2 * A, device="cuda")
+    u = torch.rand(M, A, device="cuda").clamp(1e-6, 1 - 1e-6)
+    act = ops._act_code("silu")
+    y1, m1, r1 = torch.empty(M, K, device="cuda"), torch.empty(M, device="cuda"), torch.empty(M, device="cuda")
+    p1, l1, s1, x1 = (torch.empty(M, 2 * A, device="cuda"), torch.empty(M, A, device="cuda"), torch.empty(M, A, device="cuda"),
+                      torch.empty(M, A, device="cuda"))
+    assert C.tn_head_linear_sample_fwd(z, W, b, u, 0.0, 0.1, -1.0, 1.0, p1, l1, s1, x1, ln_w=g, ln_b=bb, ln_eps=1e-3, act=act,
+                                       y_out=y1, mean=m1, rstd=r1)
+    y0, m0, r0 = torch.empty(M, K, device="cuda"), torch.empty(M, device="cuda"), torch.empty(M, device="cuda")
+    C.ln_act_fwd_into(z, z.stride(0), y0, K, g, bb, m0, r0, M, K, 1, 1e-3, act)
+    p0, l0, s0, x0 = (torch.empty(M, 2 * A, device="cuda"), torch.empty(M, A, device="cuda"), torch.empty(M, A, device="cuda"),
+                      torch.empty(M, A, device="cuda"))
+    torch.addmm(b, y0, W.t(), out=p0)
+    C.tn_head_sample_fwd(p0, u, 0.0, 0.1, -1.0, 1.0, l0, s0, x0)
+    for a_, b_ in ((y1, y0), (m1, m0), (r1, r0), (p1, p0), (l1, l0), (s1, s0)):
+        torch.testing.assert_close(a_, b_, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(x1, x0, rtol=1e-3, atol=1e-3)
