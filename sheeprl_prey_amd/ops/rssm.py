@@ -171,7 +171,7 @@ class RSSMScanFn(torch.autograd.Function):
         p2b = torch.empty_like(p2g)
         pgg = torch.empty(T, gg, 3 * H, device=dev, dtype=f32)
         pgb = torch.empty_like(pgg)
-        sidestream.flush(dev)
+        sidestream.flush(dev, inline=True)
         sk = _use_skinny(B, H)
         if sk:  # the adjoint GEMMs stream W^T: one transposed copy of each weight per backward
             WzT, WgT, W1T, W2T = (Wz.t().contiguous(), Wg.t().contiguous(), W1.t().contiguous(),
