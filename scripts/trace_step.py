@@ -1,5 +1,5 @@
 """Dump the kernel sequence of ONE timed step from a rocprofv3 kernel-trace CSV (after bench.py's
-marker kernel): index, start offset (us), duration (us), name.  Usage: trace_step.py <csv> <steps>"""
+marker kernel): index, start offset (us), duration (us), stream (or queue) id, name.  Usage: trace_step.py <csv> <steps>"""
 import csv
 import sys
 
@@ -14,7 +14,8 @@ def main(path, steps):
     t0 = int(step[0]["Start_Timestamp"])
     for i, r in enumerate(step):
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        print(f"{i}\t{(s - t0) / 1e3:.1f}\t{(e - s) / 1e3:.1f}\t{r['Kernel_Name'][:110]}")
+        q = r.get("Stream_Id", r.get("Queue_Id", ""))
+        print(f"{i}\t{(s - t0) / 1e3:.1f}\t{(e - s) / 1e3:.1f}\t{q}\t{r['Kernel_Name'][:110]}")
 
 
 if __name__ == "__main__":

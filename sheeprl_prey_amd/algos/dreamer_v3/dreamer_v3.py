@@ -122,6 +122,13 @@ class DreamerV3Trainer:
         self.graph_mode = "segmented" if self.segmented else (("single+rccl" if ws > 1 else "single") if single else "eager")
         # the actor all-reduce overlaps the critic phase wherever the step is not cut between phases
         self.defer_actor_sync = not self.segmented
+        # discrete single-graph step on one rank: the actor phase on a side stream beside the critic phase, joined
+        # before the final phase.  A backward runs on the stream its forward ran on: the actor's loss graph is built
+        # inside its phase (side stream), the critic reuses the imagination's forward graph (main stream).  Measured
+        # +0.4 % (the two phases' GEMMs slow each other, profiles/r5_ac_overlap.md); the continuous step (critic on
+        # the side beside the rollout backward) measured 1.4 % slower and stays in line.  SRL_DV3_AC_OVERLAP=0: in line
+        self.overlap_ac = (not self.segmented and ws == 1 and not is_continuous
+                           and os.environ.get("SRL_DV3_AC_OVERLAP", "1") != "0")
         self.graphed = GraphedStep(self._full_step, warmup=2, enabled=single, name="dreamer_v3_train")
         if self.segmented:
             from sheeprl_prey_amd.parallel.graphs import SegmentedGraph
@@ -165,6 +172,20 @@ class DreamerV3Trainer:
         self._coll_wm()
         self._phase_imagine(data)
         self._coll_lambda()
+        dev = data["rewards"].device
+        if self.overlap_ac and dev.type == "cuda":
+            main = torch.cuda.current_stream(dev)
+            side = sidestream._stream(sidestream._index(dev))  # its own half of the column-sum tickets
+            side.wait_stream(main)
+            # the recorded rollout activations (allocated on the main stream) stay referenced until the join: the
+            # actor phase drops them while its backward may still be reading them on the side stream
+            keep = self._st.get("actor_rec")
+            with torch.cuda.stream(side):
+                self._phase_actor(data)
+            self._phase_critic(data)
+            main.wait_stream(side)
+            del keep
+            return self._phase_final(data)
         self._phase_actor(data)
         self._coll_actor()
         self._phase_critic(data)
