@@ -156,7 +156,7 @@ def main():
     from sheeprl_prey_amd.algos.dreamer_v3.interaction import InteractionLoop
 
     loop = InteractionLoop(runner, cfg, envs, player, rb, actions_dim, is_continuous)
-    player.use_graphs = runner.cuda_graphs
+    player.use_graphs = runner.cuda_graphs and os.environ.get("SRL_PLAYER_GRAPH", "1") != "0"
     loop.reset(cfg.seed + rank)
 
     grad_steps = 0
@@ -300,11 +300,16 @@ def main():
     if args.profile_steps:
         torch.cuda._sleep(1000)  # marker kernel: scripts/trace_window.py aggregates the dispatches after it
         torch.cuda.synchronize()
+    if os.environ.get("SRL_HOST_TIMES"):
+        loop.host_ms = {}  # host-side breakdown of the interaction step (interaction.py)
     t0 = time.perf_counter()
     for i in range(args.steps):
         out = one_step()
         heart.beat(f"timed step {i}")
     torch.cuda.synchronize()
+    if loop.host_ms and rank == 0:
+        n = max(1, loop.host_ms.pop("steps", 1))
+        print("host ms/step: " + ", ".join(f"{k} {v / n:.3f}" for k, v in loop.host_ms.items()), file=sys.stderr, flush=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

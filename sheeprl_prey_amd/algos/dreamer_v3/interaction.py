@@ -54,6 +54,7 @@ class InteractionLoop:
         self._slot = 0
         self._ring: List[Dict[str, torch.Tensor]] = []
         self.last_train_host_s = 0.0
+        self.host_ms: Optional[Dict[str, float]] = None  # host-side breakdown of ``step`` when a dict
 
     # ------------------------------------------------------------------ setup
     def _obs_tensor(self, k: str, v) -> torch.Tensor:
@@ -154,6 +155,8 @@ class InteractionLoop:
         cfg, ne = self.cfg, self.ne
         train_fn = self._timed(train_fn)
         self.last_train_host_s = 0.0
+        hp = self.host_ms  # optional host-side breakdown (bench.py SRL_HOST_TIMES=1)
+        t0 = time.perf_counter() if hp is not None else 0.0
         deferred = None
         if self.serial_order:
             deferred, train_fn = train_fn, None
@@ -164,8 +167,16 @@ class InteractionLoop:
             out = train_fn() if train_fn is not None else None
         elif self.pipelined:
             self._policy_pipelined()
+            if hp is not None:
+                t1 = time.perf_counter()
+                hp["player_launch"] = hp.get("player_launch", 0.0) + (t1 - t0) * 1e3
             out = train_fn() if train_fn is not None else None
+            if hp is not None:
+                t2 = time.perf_counter()
             self._act_ev.synchronize()
+            if hp is not None:
+                t0 = time.perf_counter()
+                hp["action_wait"] = hp.get("action_wait", 0.0) + (t0 - t2) * 1e3
             real = self._real_pin.numpy().copy()
         else:
             real, acts = self._policy_serial()
@@ -176,6 +187,9 @@ class InteractionLoop:
 
         o, rewards, dones, truncated, infos = self.envs.step(np.asarray(real).reshape(self.envs.action_space.shape))
         dones = np.logical_or(dones, truncated)
+        if hp is not None:
+            t1 = time.perf_counter()
+            hp["env_step"] = hp.get("env_step", 0.0) + (t1 - t0) * 1e3
 
         sd = self.step_data
         sd["is_first"] = torch.zeros_like(sd["dones"])
@@ -217,6 +231,12 @@ class InteractionLoop:
             sd["dones"][idxes] = 0.0
             sd["is_first"][idxes] = 1.0
             self.player.init_states(idxes)
+        if hp is not None:
+            t0 = time.perf_counter()
+            hp["bookkeeping"] = hp.get("bookkeeping", 0.0) + (t0 - t1) * 1e3
         if deferred is not None:
             self.last_train_out = deferred()
+        if hp is not None:
+            hp["train_launch"] = hp.get("train_launch", 0.0) + (time.perf_counter() - t0) * 1e3
+            hp["steps"] = hp.get("steps", 0) + 1
         return infos
