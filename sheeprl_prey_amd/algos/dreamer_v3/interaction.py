@@ -25,6 +25,7 @@ timing the env interaction subtract it (the reference times interaction and trai
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
@@ -32,6 +33,8 @@ import numpy as np
 import torch
 
 from sheeprl_prey_amd.data.tensordict import TensorDict
+
+_SPIN = os.environ.get("SRL_SPIN_WAIT", "1") != "0"
 
 
 class InteractionLoop:
@@ -173,7 +176,11 @@ class InteractionLoop:
             out = train_fn() if train_fn is not None else None
             if hp is not None:
                 t2 = time.perf_counter()
-            self._act_ev.synchronize()
+            if _SPIN:
+                while not self._act_ev.query():  # poll: lower wake-up latency than the blocking event wait
+                    pass
+            else:
+                self._act_ev.synchronize()
             if hp is not None:
                 t0 = time.perf_counter()
                 hp["action_wait"] = hp.get("action_wait", 0.0) + (t0 - t2) * 1e3
