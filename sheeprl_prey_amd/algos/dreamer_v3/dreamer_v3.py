@@ -109,6 +109,7 @@ class DreamerV3Trainer:
         # (algos/dreamer_v3/imagine_cont.py); False = the reference-shaped eager loop
         self.cont_fast = True
         self._st: Dict[str, Any] = {}
+        self._consts: Dict[Any, Tensor] = {}
         self._gather_buf = None
         # teacher forcing of the eager oracle (tests/test_dv3_step_oracle_gpu.py): {"posteriors" [T,B,S],
         # "priors" [H+1,M,S], "actions" [H+1,M,A]} one-hot samples of a fused run, taken instead of drawing
@@ -138,6 +139,15 @@ class DreamerV3Trainer:
                 [self._coll_wm, self._coll_lambda, self._coll_actor, self._coll_critic],
                 warmup=2,
             )
+
+    def _const(self, like: Tensor, value: float) -> Tensor:
+        """A cached tensor shaped like ``like`` filled with ``value`` (backward seeds, constant rows): made once,
+        outside the captured replays, instead of a fill launch per step."""
+        key = (tuple(like.shape), like.dtype, str(like.device), float(value))
+        t = self._consts.get(key)
+        if t is None:
+            t = self._consts[key] = torch.full(like.shape, float(value), dtype=like.dtype, device=like.device)
+        return t
 
     @property
     def uses_graphs(self) -> bool:
@@ -256,9 +266,9 @@ class DreamerV3Trainer:
         # fused conv stack's NHWC conversion), the reference divides here (dreamer_v3.py:169)
         batch_obs = {k: data[k] if data[k].dtype == torch.uint8 else data[k] / 255.0 for k in cfg.cnn_keys.encoder}
         batch_obs.update({k: data[k] for k in cfg.mlp_keys.encoder})
-        is_first = data["is_first"].clone()
-        is_first[0] = 1.0
-        batch_actions = torch.cat((torch.zeros_like(data["actions"][:1]), data["actions"][:-1]), dim=0)
+        # first row forced to a reset, actions shifted by one step: one concatenation each with a cached constant row
+        is_first = torch.cat((self._const(data["is_first"][:1], 1.0), data["is_first"][1:]), dim=0)
+        batch_actions = torch.cat((self._const(data["actions"][:1], 0.0), data["actions"][:-1]), dim=0)
         embedded_obs = wm.encoder(batch_obs)
         forced = self.teacher["posteriors"] if self.teacher is not None else None
         recurrent_states, posteriors, posteriors_logits, priors_logits = wm.rssm.scan_dynamic(
@@ -275,12 +285,12 @@ class DreamerV3Trainer:
             oh = (idx.view(T, B, G), G, 0, stoch * disc)
         reconstructed = wm.observation_model(latent_states, onehot=oh) if oh is not None else wm.observation_model(latent_states)
         # image MSE against the raw uint8 frames and vector symlog MSE, one fused kernel each way (K6)
-        obs_loss = 0
-        for k in cfg.cnn_keys.decoder:
-            raw = data[k].dtype == torch.uint8
-            obs_loss = obs_loss + ops.obs_mse(reconstructed[k], data[k] if raw else batch_obs[k], 1.0 / 255.0 if raw else 1.0)
-        for k in cfg.mlp_keys.decoder:
-            obs_loss = obs_loss + ops.obs_mse(reconstructed[k], batch_obs[k], symlog=True)
+        terms = [ops.obs_mse(reconstructed[k], data[k] if data[k].dtype == torch.uint8 else batch_obs[k],
+                             1.0 / 255.0 if data[k].dtype == torch.uint8 else 1.0) for k in cfg.cnn_keys.decoder]
+        terms += [ops.obs_mse(reconstructed[k], batch_obs[k], symlog=True) for k in cfg.mlp_keys.decoder]
+        obs_loss = terms[0] if terms else 0  # no "0 + term" launch for the single-key case
+        for t_ in terms[1:]:
+            obs_loss = obs_loss + t_
         reward_logits = self._head(wm.reward_model, latent_states, oh)
         continue_logits = self._head(wm.continue_model, latent_states, oh)
         ents: List[Tensor] = []  # posterior / prior entropies: a by-product of the KL kernel
@@ -291,7 +301,7 @@ class DreamerV3Trainer:
         )
         self.world_optimizer.zero_grad(set_to_none=True)
         with sidestream.scope():  # decoder weight gradients beside the scan backward (ops/sidestream.py)
-            rec_loss.backward()
+            rec_loss.backward(self._const(rec_loss, 1.0))
         out["Loss/world_model_loss"] = rec_loss.detach()
         out["Loss/observation_loss"] = observation_loss.detach()
         out["Loss/reward_loss"] = reward_loss.detach()
@@ -439,7 +449,7 @@ class DreamerV3Trainer:
                                               st["discount"].detach().reshape(T, -1), offset, invscale,
                                               cfg.algo.actor.ent_coef, self.actor.init_std, self.actor.min_std)
             if policy_loss is not None:
-                policy_loss.backward()
+                policy_loss.backward(self._const(policy_loss, 1.0))
                 st["out"]["Loss/policy_loss"] = policy_loss.detach()
                 return
         if not self.is_continuous:
@@ -450,7 +460,7 @@ class DreamerV3Trainer:
                 z, st["imagined_actions"], lambda_values.reshape(T - 1, -1), baseline.reshape(T - 1, -1),
                 st["discount"].detach().reshape(T, -1), offset, invscale, self.actions_dim, cfg.algo.actor.ent_coef)
             if policy_loss is not None:
-                policy_loss.backward()
+                policy_loss.backward(self._const(policy_loss, 1.0))
                 st["out"]["Loss/policy_loss"] = policy_loss.detach()
                 return
         if policies is None:
@@ -468,7 +478,7 @@ class DreamerV3Trainer:
         except NotImplementedError:
             entropy = torch.zeros_like(objective[..., 0])
         policy_loss = -torch.mean(st["discount"][:-1].detach() * (objective + entropy.unsqueeze(-1)[:-1]))
-        policy_loss.backward()
+        policy_loss.backward(self._const(policy_loss, 1.0))
         st["out"]["Loss/policy_loss"] = policy_loss.detach()
 
     def _phase_critic(self, data: Dict[str, Tensor]) -> None:
@@ -483,7 +493,7 @@ class DreamerV3Trainer:
         self.critic_optimizer.zero_grad(set_to_none=True)
         value_loss = ops.twohot_nll(qv_logits, st["lambda_values"].detach()) + ops.twohot_nll(qv_logits, target_values)
         value_loss = torch.mean(value_loss * st["discount"][:-1].squeeze(-1))
-        value_loss.backward()
+        value_loss.backward(self._const(value_loss, 1.0))
         st["out"]["Loss/value_loss"] = value_loss.detach()
 
     def _phase_final(self, data: Dict[str, Tensor]) -> Dict[str, Tensor]:

@@ -327,7 +327,7 @@ class RSSMPersistFn(torch.autograd.Function):
         # recurrent input before the posterior gathers: action part + z0 Wz^T of reset rows
         xr = torch.addcmul(a_proj, first.unsqueeze(-1), torch.mv(Wz_c, z0))
         zm = e(T, B, S)
-        zm[0] = first[0].unsqueeze(-1) * z0
+        torch.mul(first[0].unsqueeze(-1), z0, out=zm[0])
         ok, words, _, _, _ = C.scanp_info(B, S, D, H, hid, disc)
         assert ok, "scanp: unsupported shape"
         sync = torch.empty(words, device=dev, dtype=torch.int32)
@@ -542,7 +542,7 @@ def fused_scan(rssm, embedded_obs: Tensor, actions: Tensor, is_first: Tensor, z0
     S = tr[3].out_features
     rec_lin = rec[0]
     Wz, Wa = _split_cols(rec_lin.weight, S)
-    a_proj = torch.nn.functional.linear((1 - is_first) * actions, Wa)
+    a_proj = torch.nn.functional.linear(torch.addcmul(actions, is_first, actions, value=-1.0), Wa)  # (1 - first) a
     Wh_rep, We = _split_cols(rep[0].weight, H)
     e_proj = torch.nn.functional.linear(embedded_obs, We, rep[0].bias)
     hid = tr[0].out_features
