@@ -491,8 +491,8 @@ class DreamerV3Trainer:
             oh = st.get("traj_onehot")
             target_values = ops.twohot_mean(self._head(self.target_critic, traj, (oh[0][:-1],) + oh[1:] if oh else None))
         self.critic_optimizer.zero_grad(set_to_none=True)
-        value_loss = ops.twohot_nll(qv_logits, st["lambda_values"].detach()) + ops.twohot_nll(qv_logits, target_values)
-        value_loss = torch.mean(value_loss * st["discount"][:-1].squeeze(-1))
+        # mean(discount * (nll(lambda returns) + nll(target values))): one kernel writing the loss and its logits gradient
+        value_loss = ops.twohot_value_loss(qv_logits, st["lambda_values"].detach(), target_values, st["discount"][:-1].detach())
         value_loss.backward(self._const(value_loss, 1.0))
         st["out"]["Loss/value_loss"] = value_loss.detach()
 

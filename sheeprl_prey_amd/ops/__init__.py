@@ -380,6 +380,37 @@ def twohot_nll(logits: Tensor, target: Tensor, low: float = -20.0, high: float =
     return ref.twohot_nll(logits, target, bins)
 
 
+class _ValueLoss2(torch.autograd.Function):
+    """Critic objective with its logits gradient computed in the forward pass (``csrc/dist.hip`` value_loss2_kernel)."""
+
+    @staticmethod
+    def forward(ctx, logits, y1, y2, w, bins):
+        loss, dl = _ext().value_loss2(logits.contiguous(), y1.detach().contiguous().float(), y2.detach().contiguous().float(),
+                                      w.detach().contiguous().float(), bins)
+        ctx.save_for_backward(dl)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        return dl * g, None, None, None, None
+
+
+def twohot_value_loss(logits: Tensor, y1: Tensor, y2: Tensor, w: Tensor, low: float = -20.0, high: float = 20.0) -> Tensor:
+    """``mean(w * (twohot_nll(logits, y1) + twohot_nll(logits, y2)))`` (DreamerV3 critic loss, reference
+    ``dreamer_v3.py:327-336``): one forward pass writing the loss and the logits gradient, one scaling launch backward.
+    ``y1``, ``y2``, ``w`` hold one value per logits row (no gradient flows into them)."""
+    K = logits.shape[-1]
+    R = logits.numel() // K
+    bins = twohot_bins(K, low, high, device=logits.device)
+    if (_native(logits) and logits.dtype == torch.float32 and K <= 512 and y1.numel() == R and y2.numel() == R
+            and w.numel() == R):
+        return _ValueLoss2.apply(logits, y1.reshape(-1), y2.reshape(-1), w.reshape(-1), bins)
+    lead = logits.shape[:-1]
+    nll = twohot_nll(logits, y1.reshape(lead)) + twohot_nll(logits, y2.reshape(lead))
+    return torch.mean(nll * w.reshape(lead))
+
+
 class _TwoHotMean(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, bins):
@@ -591,7 +622,7 @@ def flat_adam(p, g, m, v, scalars, lr, b1, b2, eps, wd, decoupled) -> None:
 
 __all__ = [
     "ln_act", "ln_act_nchw", "ln_gru", "unimix_sample", "twohot_nll", "twohot_mean", "twohot_bins", "kl_balance",
-    "lambda_returns", "gae_scan", "flat_grad_norm", "flat_advance", "flat_adam", "fault_block", "skipped_updates", "check_faults", "native_available", "set_fused",
+    "lambda_returns", "twohot_value_loss", "gae_scan", "flat_grad_norm", "flat_advance", "flat_adam", "fault_block", "skipped_updates", "check_faults", "native_available", "set_fused",
 ]
 
 

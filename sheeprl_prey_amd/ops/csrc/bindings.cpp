@@ -44,6 +44,8 @@ bool launch_unimix_sample_fwd(const float*, const float*, float*, float*, int, i
 bool launch_unimix_sample_bwd(const float*, const float*, const float*, float*, int, int, float, hipStream_t);
 bool launch_twohot_nll_fwd(const float*, const float*, const float*, float*, int, int, hipStream_t);
 bool launch_twohot_nll_bwd(const float*, const float*, const float*, const float*, float*, int, int, hipStream_t);
+bool launch_value_loss2(const float*, const float*, const float*, const float*, const float*, float*, float*, float*, int, int,
+                        hipStream_t);
 bool launch_twohot_mean_fwd(const float*, const float*, float*, float*, int, int, hipStream_t);
 bool launch_twohot_mean_bwd(const float*, const float*, const float*, const float*, float*, int, int, hipStream_t);
 bool launch_kl_fwd(const float*, const float*, float*, float*, float*, float*, int, int, int, float, float, float, hipStream_t);
@@ -334,6 +336,23 @@ torch::Tensor twohot_nll_fwd(torch::Tensor logits, torch::Tensor y, torch::Tenso
                                   loss.data_ptr<float>(), R, K, cur_stream());
   TORCH_CHECK(ok, "twohot: too many bins ", K);
   return loss;
+}
+
+// critic objective mean_r w_r (nll(l_r, y1_r) + nll(l_r, y2_r)) and its logits gradient, one pass (dist.hip)
+std::vector<torch::Tensor> value_loss2(torch::Tensor logits, torch::Tensor y1, torch::Tensor y2, torch::Tensor w,
+                                       torch::Tensor bins) {
+  for (auto* t : {&logits, &y1, &y2, &w, &bins})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kFloat32 && t->is_contiguous(), "value_loss2: contiguous fp32 GPU tensors");
+  const int64_t K = logits.size(-1), R = logits.numel() / K;
+  TORCH_CHECK(y1.numel() == R && y2.numel() == R && w.numel() == R && bins.numel() == K, "value_loss2: shape mismatch");
+  auto dl = torch::empty_like(logits);
+  auto partial = torch::empty({(R + 3) / 4}, logits.options());
+  auto loss = torch::empty({}, logits.options());
+  bool ok = launch_value_loss2(logits.data_ptr<float>(), y1.data_ptr<float>(), y2.data_ptr<float>(), w.data_ptr<float>(),
+                               bins.data_ptr<float>(), dl.data_ptr<float>(), partial.data_ptr<float>(), loss.data_ptr<float>(),
+                               (int)R, (int)K, cur_stream());
+  TORCH_CHECK(ok, "value_loss2: K > 512");
+  return {loss, dl};
 }
 
 torch::Tensor twohot_nll_bwd(torch::Tensor logits, torch::Tensor y, torch::Tensor bins, torch::Tensor gl) {
@@ -1197,6 +1216,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("unimix_sample_bwd", &unimix_sample_bwd);
   m.def("twohot_nll_fwd", &twohot_nll_fwd);
   m.def("twohot_nll_bwd", &twohot_nll_bwd);
+  m.def("value_loss2", &value_loss2);
   m.def("twohot_mean_fwd", &twohot_mean_fwd);
   m.def("twohot_mean_bwd", &twohot_mean_bwd);
   m.def("kl_fwd", &kl_fwd);

@@ -607,6 +607,91 @@ bool launch_unimix_sample_bwd(const float* logits, const float* g_mixed, const f
   return true;
 }
 
+// DreamerV3 critic objective (reference dreamer_v3.py:327-336): loss = mean_r w_r (nll(l_r, y1_r) + nll(l_r, y2_r)) over
+// the two-hot encodings of the lambda returns y1 and the target critic's values y2, one wave per row.  The logits
+// gradient is written in the same pass (d/dl_rk = scale w_r (2 softmax_rk - t1_rk - t2_rk)); the autograd backward only
+// scales it by the incoming gradient.  Per-block partials (4 rows, fixed order) -> fixed-order final sum (value_loss_final).
+__device__ __forceinline__ void th_interp(const float* __restrict__ bins, int K, float x, int cle, int cgt, int& below,
+                                          int& above, float& wb, float& wa) {
+  below = cle - 1;
+  above = K - cgt;
+  below = below < 0 ? 0 : (below > K - 1 ? K - 1 : below);
+  above = above < 0 ? 0 : (above > K - 1 ? K - 1 : above);
+  const float bb = bins[below], ba = bins[above];
+  const bool eq = below == above;
+  const float db = eq ? 1.f : fabsf(bb - x), da = eq ? 1.f : fabsf(ba - x);
+  const float tot = db + da;
+  wb = da / tot;
+  wa = db / tot;
+}
+
+template <int MAXK>
+__global__ void __launch_bounds__(256) value_loss2_kernel(const float* __restrict__ logits, const float* __restrict__ y1,
+                                                          const float* __restrict__ y2, const float* __restrict__ w,
+                                                          const float* __restrict__ bins, float* __restrict__ dlogits,
+                                                          float* __restrict__ partial, int R, int K, float scale) {
+  __shared__ float rowv[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = blockIdx.x * 4 + wv;
+  float v = 0.f;
+  if (r < R) {
+    const float* lr = logits + (int64_t)r * K;
+    const float a = y1[r], b = y2[r];
+    const float x1 = copysignf(log1pf(fabsf(a)), a), x2 = copysignf(log1pf(fabsf(b)), b);
+    float lv[MAXK];
+    float mx = -INFINITY;
+    int c1le = 0, c1gt = 0, c2le = 0, c2gt = 0;
+#pragma unroll
+    for (int i = 0; i < MAXK; ++i) {
+      const int k = lane + 64 * i;
+      const bool ok = k < K;
+      lv[i] = ok ? lr[k] : -INFINITY;
+      const float bk = ok ? bins[k] : 0.f;
+      mx = fmaxf(mx, lv[i]);
+      c1le += (ok && bk <= x1) ? 1 : 0;
+      c1gt += (ok && bk > x1) ? 1 : 0;
+      c2le += (ok && bk <= x2) ? 1 : 0;
+      c2gt += (ok && bk > x2) ? 1 : 0;
+    }
+    mx = wave_max(mx);
+    float se = 0.f;
+#pragma unroll
+    for (int i = 0; i < MAXK; ++i) se += (lane + 64 * i < K) ? __expf(lv[i] - mx) : 0.f;
+    se = wave_sum(se);
+    const float lse = mx + logf(se);
+    int b1, a1, b2, a2;
+    float wb1, wa1, wb2, wa2;
+    th_interp(bins, K, x1, (int)wave_sum((float)c1le), (int)wave_sum((float)c1gt), b1, a1, wb1, wa1);
+    th_interp(bins, K, x2, (int)wave_sum((float)c2le), (int)wave_sum((float)c2gt), b2, a2, wb2, wa2);
+    const float wr = w[r];
+    // the same per-term arithmetic as twohot_nll_fwd_kernel, then w * (nll1 + nll2) as the torch composite
+    const float n1 = -(wb1 * (lr[b1] - lse) + wa1 * (lr[a1] - lse));
+    const float n2 = -(wb2 * (lr[b2] - lse) + wa2 * (lr[a2] - lse));
+    v = (n1 + n2) * wr;
+    const float g = scale * wr;
+    float* dr = dlogits + (int64_t)r * K;
+#pragma unroll
+    for (int i = 0; i < MAXK; ++i) {
+      const int k = lane + 64 * i;
+      if (k < K) {
+        const float t = (k == b1 ? wb1 : 0.f) + (k == a1 ? wa1 : 0.f) + (k == b2 ? wb2 : 0.f) + (k == a2 ? wa2 : 0.f);
+        dr[k] = g * (2.f * (__expf(lv[i] - mx) / se) - t);
+      }
+    }
+  }
+  if (lane == 0) rowv[wv] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = (rowv[0] + rowv[1]) + (rowv[2] + rowv[3]);
+}
+
+__global__ void value_loss_final(const float* __restrict__ partial, int n, float scale, float* __restrict__ loss) {
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int i = 0; i < n; ++i) s += partial[i];
+    *loss = s * scale;
+  }
+}
+
 #define TH_DISPATCH(KERNEL, ...)                                                                       \
   do {                                                                                                 \
     dim3 g(cdiv(R, 4)), b(256);                                                                        \
@@ -625,6 +710,13 @@ bool launch_twohot_nll_fwd(const float* logits, const float* y, const float* bin
 bool launch_twohot_nll_bwd(const float* logits, const float* y, const float* bins, const float* gl, float* dlogits, int R,
                            int K, hipStream_t st) {
   TH_DISPATCH(twohot_nll_bwd_kernel, logits, y, bins, gl, dlogits, R, K);
+  return true;
+}
+bool launch_value_loss2(const float* logits, const float* y1, const float* y2, const float* w, const float* bins,
+                        float* dlogits, float* partial, float* loss, int R, int K, hipStream_t st) {
+  const float scale = 1.f / (float)R;
+  TH_DISPATCH(value_loss2_kernel, logits, y1, y2, w, bins, dlogits, partial, R, K, scale);
+  hipLaunchKernelGGL(value_loss_final, dim3(1), dim3(64), 0, st, partial, cdiv(R, 4), scale, loss);
   return true;
 }
 bool launch_twohot_mean_fwd(const float* logits, const float* bins, float* out, float* s, int R, int K, hipStream_t st) {
