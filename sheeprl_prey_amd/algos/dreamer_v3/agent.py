@@ -420,9 +420,12 @@ class RSSM(nn.Module):
             # the transition layer's bias rides in the GEMM epilogue (zero on the actor / GRU columns: the actor's bias
             # is added by the gather kernel, the GRU projection has none)
             bm = None
-            if tr_lin.bias is not None:
-                bm = torch.zeros(Wm.shape[0], device=dev, dtype=Wm.dtype)
-                bm[:Ntr] = tr_lin.bias
+            if tr_lin.bias is not None:  # one concatenation with a cached zero tail (no fill + copy per step)
+                nz = Wm.shape[0] - Ntr
+                zt = getattr(self, "_bm_zeros", None)
+                if zt is None or zt.numel() != nz or zt.device != dev:
+                    zt = self._bm_zeros = torch.zeros(nz, device=dev, dtype=Wm.dtype)
+                bm = torch.cat((tr_lin.bias.detach(), zt))
             hm = torch.addmm(bm, h, Wm.t()) if bm is not None else torch.mm(h, Wm.t())
             ytr, mtr, rtr = post.new_empty(M, Ntr), post.new_empty(M), post.new_empty(M)
             tr_act = ops._act_code(tr_ln.act)

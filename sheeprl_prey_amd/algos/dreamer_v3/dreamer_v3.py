@@ -20,7 +20,7 @@ import copy
 import os
 import time
 import warnings
-from typing import Any, Dict, List, Sequence
+from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -240,17 +240,38 @@ class DreamerV3Trainer:
         self._st["gathered"] = self._gather_buf
 
     @staticmethod
-    def _head(mlp, x: Tensor, onehot) -> Tensor:
+    def _head(mlp, x: Tensor, onehot, table: Optional[Tensor] = None) -> Tensor:
         """``mlp(x)``; with ``onehot = (idx, G, off, S)`` the first layer's one-hot prior columns are row
-        gathers (``ops/onehot.py``) instead of GEMM columns."""
+        gathers (``ops/onehot.py``) instead of GEMM columns (``table``: their transposed weight, if made already)."""
         if onehot is not None:
             from sheeprl_prey_amd.ops.onehot import mlp_forward
 
             idx, G, off, S = onehot
-            y = mlp_forward(mlp, x, idx, G, off, S)
+            y = mlp_forward(mlp, x, idx, G, off, S, table=table)
             if y is not None:
                 return y
         return mlp(x)
+
+    def _head_tables(self, oh) -> Dict[str, Tensor]:
+        """The transposed one-hot columns of the imagination heads' first layers (critic, reward, continue and the
+        target critic of the critic phase) in ONE transpose launch instead of one per head."""
+        if not (ops.fused_enabled() and self.onehot_heads):
+            return {}
+        from sheeprl_prey_amd.ops.onehot import head_table
+
+        S = oh[3]
+        heads = {"critic": self.critic, "reward": self.world_model.reward_model,
+                 "continue": self.world_model.continue_model, "target": self.target_critic}
+        srcs = {k: head_table(m, S) for k, m in heads.items()}
+        srcs = {k: v for k, v in srcs.items() if v is not None and v.is_cuda}
+        if not srcs:
+            return {}
+        with torch.no_grad():
+            outs = dict(zip(srcs, ops.transpose_many(list(srcs.values()))))
+        for k in ("target", "critic"):  # read again by the critic phase (same weights until the final phase)
+            if k in outs:
+                self._st[k + "_table"] = outs[k]
+        return outs
 
     # ------------------------------------------------------------------ phases
     def _phase_wm(self, data: Dict[str, Tensor]) -> None:
@@ -394,23 +415,24 @@ class DreamerV3Trainer:
                 imagined_trajectories = torch.stack(trajectories)
                 imagined_actions_t = torch.stack(imagined_actions)
             oh = st.get("traj_onehot")
+            tabs = self._head_tables(oh) if oh is not None else {}
             if fast and self.reuse_forwards:
                 # the critic's forward over the trajectories, WITH its graph: the critic loss of this step
                 # (same weights - the critic steps in the final phase - same detached inputs) reuses it
                 # instead of running the critic forward a second time (reference dreamer_v3.py:260, :327)
                 with torch.enable_grad():
-                    st["critic_logits"] = self._head(critic, imagined_trajectories, oh)
+                    st["critic_logits"] = self._head(critic, imagined_trajectories, oh, tabs.get("critic"))
                 predicted_values = ops.twohot_mean(st["critic_logits"].detach())
             else:
-                predicted_values = ops.twohot_mean(self._head(critic, imagined_trajectories, oh))
+                predicted_values = ops.twohot_mean(self._head(critic, imagined_trajectories, oh, tabs.get("critic")))
             # the reward and continue heads only on the imagined steps 1..H: the losses never read row 0 (reference
             # dreamer_v3.py:261-276 uses rewards[1:] and replaces continues[0] by 1 - done)
             traj1 = imagined_trajectories[1:]
             oh1 = (oh[0][1:],) + tuple(oh[1:]) if oh is not None else None
-            predicted_rewards = ops.twohot_mean(self._head(wm.reward_model, traj1, oh1))
+            predicted_rewards = ops.twohot_mean(self._head(wm.reward_model, traj1, oh1, tabs.get("reward")))
             # continuation flags, their gamma-discounts and the cumulative discount: one kernel (K11)
-            cont_g, discount = ops.imag_discount(self._head(wm.continue_model, traj1, oh1), data["dones"],
-                                                 cfg.algo.gamma, skip_first=True)
+            cont_g, discount = ops.imag_discount(self._head(wm.continue_model, traj1, oh1, tabs.get("continue")),
+                                                 data["dones"], cfg.algo.gamma, skip_first=True)
             lambda_values = compute_lambda_values(predicted_rewards, predicted_values[1:], cont_g,
                                                   lmbda=cfg.algo.lmbda)
         st["discount"] = discount.detach()
@@ -486,10 +508,15 @@ class DreamerV3Trainer:
         cfg, st = self.cfg, self._st
         traj = st["imagined_trajectories"].detach()[:-1]
         qv_full = st.pop("critic_logits", None)
-        qv_logits = qv_full[:-1] if qv_full is not None else self.critic(traj)
+        oh = st.get("traj_onehot")
+        ctab = st.pop("critic_table", None)
+        if qv_full is not None:
+            qv_logits = qv_full[:-1]
+        else:  # (continuous) the critic's first layer gathers the one-hot prior columns too
+            qv_logits = self._head(self.critic, traj, (oh[0][:-1],) + oh[1:] if oh else None, ctab)
         with torch.no_grad():
-            oh = st.get("traj_onehot")
-            target_values = ops.twohot_mean(self._head(self.target_critic, traj, (oh[0][:-1],) + oh[1:] if oh else None))
+            target_values = ops.twohot_mean(self._head(self.target_critic, traj, (oh[0][:-1],) + oh[1:] if oh else None,
+                                                        st.pop("target_table", None)))
         self.critic_optimizer.zero_grad(set_to_none=True)
         # mean(discount * (nll(lambda returns) + nll(target values))): one kernel writing the loss and its logits gradient
         value_loss = ops.twohot_value_loss(qv_logits, st["lambda_values"].detach(), target_values, st["discount"][:-1].detach())

@@ -85,12 +85,13 @@ class _GatherFirstLayer(torch.autograd.Function):
     """``act(LN(lin(x)))`` with the one-hot columns gathered (forward) and the dense backward."""
 
     @staticmethod
-    def forward(ctx, x, idx, W, bias, gamma, beta, G, off, n_onehot, eps, act, use_ln):
+    def forward(ctx, x, idx, W, bias, gamma, beta, G, off, n_onehot, eps, act, use_ln, table=None):
         C = ops._ext()
         x2 = x.reshape(-1, x.shape[-1])
         idx2 = idx.reshape(-1, idx.shape[-1])
         M, N = x2.shape[0], W.shape[0]
-        table = ops.transpose_many([W[:, :n_onehot]])[0]
+        if table is None:
+            table = ops.transpose_many([W[:, :n_onehot]])[0]
         Y = torch.mm(x2[:, n_onehot:], W[:, n_onehot:].t()) if x2.shape[1] > n_onehot else None
         z = torch.empty(M, N, device=x.device, dtype=x.dtype)
         y = torch.empty(M, N, device=x.device, dtype=x.dtype)
@@ -135,7 +136,7 @@ class _GatherFirstLayer(torch.autograd.Function):
         else:
             dW, dbias = _GatherFirstLayer._param_grads(meta, dz, x2, idx2)
         return (dx, None, dW, dbias, dg if ctx.needs_input_grad[4] else None, db if ctx.needs_input_grad[5] else None,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
     @staticmethod
     def _param_grads(meta, dz, x2, idx2, out=None):
@@ -155,10 +156,12 @@ class _GatherFirstLayer(torch.autograd.Function):
         return dW, dbias
 
 
-def first_layer(x: Tensor, idx: Tensor, G: int, off: int, lin: nn.Linear, ln: Optional[nn.Module], n_onehot: int) -> Tensor:
-    """Autograd form of ``gather_first_layer`` (any leading dims; x may be row-strided)."""
+def first_layer(x: Tensor, idx: Tensor, G: int, off: int, lin: nn.Linear, ln: Optional[nn.Module], n_onehot: int,
+                table: Optional[Tensor] = None) -> Tensor:
+    """Autograd form of ``gather_first_layer`` (any leading dims; x may be row-strided; ``table`` as there)."""
     g, b, eps, act, use_ln = _ln_parts(ln)
-    return _GatherFirstLayer.apply(x, idx, lin.weight, lin.bias, g, b, int(G), int(off), int(n_onehot), eps, act, use_ln)
+    return _GatherFirstLayer.apply(x, idx, lin.weight, lin.bias, g, b, int(G), int(off), int(n_onehot), eps, act, use_ln,
+                                   table)
 
 
 def mlp_split(mlp: nn.Module):
@@ -180,9 +183,20 @@ def mlp_split(mlp: nn.Module):
     return None
 
 
-def mlp_forward(mlp: nn.Module, x: Tensor, idx: Tensor, G: int, off: int, n_onehot: int) -> Optional[Tensor]:
+def head_table(mlp: nn.Module, n_onehot: int) -> Optional[Tensor]:
+    """The one-hot columns of ``mlp``'s first Linear (``W[:, :n_onehot]``, a source for ``ops.transpose_many``: several
+    heads' tables in one launch) or None when ``mlp_forward`` would not gather."""
+    sp = mlp_split(mlp)
+    if sp is None or not layer_supported(sp[0], n_onehot):
+        return None
+    return sp[0].weight[:, :n_onehot]
+
+
+def mlp_forward(mlp: nn.Module, x: Tensor, idx: Tensor, G: int, off: int, n_onehot: int,
+                table: Optional[Tensor] = None) -> Optional[Tensor]:
     """``mlp(x)`` with the first layer's one-hot columns gathered; None when the MLP layout or the layer
-    width is not covered (the caller runs ``mlp(x)``)."""
+    width is not covered (the caller runs ``mlp(x)``).  ``table``: the transposed one-hot columns, when the
+    caller made them (``head_table``)."""
     sp = mlp_split(mlp)
     if sp is None or not ops._native(x) or x.dtype != torch.float32:
         return None
@@ -191,11 +205,11 @@ def mlp_forward(mlp: nn.Module, x: Tensor, idx: Tensor, G: int, off: int, n_oneh
         return None
     need_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in mlp.parameters()))
     if need_grad:
-        h = first_layer(x, idx, G, off, lin, ln, n_onehot)
+        h = first_layer(x, idx, G, off, lin, ln, n_onehot, table=table)
     else:
         lead = x.shape[:-1]
         h = gather_first_layer(x.reshape(-1, x.shape[-1]), idx.reshape(-1, idx.shape[-1]), G, off, lin, ln,
-                               n_onehot).view(*lead, lin.out_features)
+                               n_onehot, table=table).view(*lead, lin.out_features)
     for m in rest:
         h = m(h)
     return h
