@@ -181,9 +181,10 @@ class ContinuousRollout:
             hid = self.tr_y.shape[-1]
             if merge:
                 # gx = x Wg_x^T + (h_t Wg_h^T from the merged GEMM): materialised - the backward reads the whole gx
-                torch.addmm(self.hm[t][:, hidm + Na:], buf[t, :, S + Hd:], Wgx_t, out=gx)
+                # (the LN-GRU kernel adds the h part and writes the sum back: no addend copy ahead of the GEMM)
+                torch.mm(buf[t, :, S + Hd:], Wgx_t, out=gx)
                 C.ln_gru_into(gx, buf[t, :, S:S + Hd], gln.weight, gln.bias, float(gln.eps), buf[t + 1, :, S:S + Hd],
-                              self.g_mean[t], self.g_rstd[t])
+                              mean=self.g_mean[t], rstd=self.g_rstd[t], x2=self.hm[t][:, hidm + Na:], write_sum=True)
                 self._hmm(buf[t + 1, :, S:S + Hd], self.hm[t + 1])
                 C.ln_act_fwd_into(self.hm[t + 1], self.hm.shape[-1], self.tr_y[t], hid, tln.weight, tln.bias,
                                   self.tr_mean[t], self.tr_rstd[t], M, hid, 1, float(tln.eps), ops._act_code(tln.act))

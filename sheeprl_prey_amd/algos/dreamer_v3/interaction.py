@@ -75,8 +75,22 @@ class InteractionLoop:
         self.player.init_states()
         if self.pipelined:
             sd = self.step_data
-            self._ring = [{k: torch.empty_like(sd[k]).pin_memory() for k in self.row_keys} for _ in range(2)]
-            self._dev_obs = {k: torch.empty_like(sd[k], device=self.device) for k in self.obs_keys}
+            # one staging row per slot: every row key packed into ONE pinned byte buffer (64-byte aligned views) and a
+            # device twin, so a step is one H2D copy; the player reads the observations from the device twin and the
+            # replay add is one device-to-device multi-tensor copy from it
+            offs, total = {}, 0
+            for k in self.row_keys:
+                nb = sd[k].numel() * sd[k].element_size()
+                offs[k] = (total, nb)
+                total += (nb + 63) // 64 * 64
+            self._pstage = [torch.empty(total, dtype=torch.uint8).pin_memory() for _ in range(2)]
+            self._dstage = [torch.empty(total, dtype=torch.uint8, device=self.device) for _ in range(2)]
+
+            def views(buf):
+                return {k: buf[o:o + nb].view(sd[k].dtype).view(sd[k].shape) for k, (o, nb) in offs.items()}
+
+            self._ring = [views(b) for b in self._pstage]
+            self._dring = [views(b) for b in self._dstage]
             width = sum(self.actions_dim) if self.is_continuous else len(self.actions_dim)
             dtype = torch.float32 if self.is_continuous else torch.int64
             shape = (self.ne, width) if self.is_continuous else (width, self.ne)
@@ -112,20 +126,20 @@ class InteractionLoop:
 
     def _policy_pipelined(self) -> None:
         """Stage the row, act, enqueue the row's replay add; the action comes back via ``_real_pin``."""
-        b = self._ring[self._slot]
+        slot = self._slot
+        b, d = self._ring[slot], self._dring[slot]
         self._slot ^= 1
         for k in self.row_keys:  # slot last read by work enqueued before the previous step's player
             b[k].copy_(self.step_data[k])
-        # the device obs buffer was last read by the previous player, which the host already waited for
-        # (its readback event): the copy may overlap the previous step's training on the main stream
+        # the slot's device twin was last read two steps ago (that step's player and replay add), which precede the
+        # previous step's player, whose readback the host already waited for: the copy may overlap the training
         main = torch.cuda.current_stream(self.device)
         with torch.cuda.stream(self._h2d):
-            for k in self.obs_keys:
-                self._dev_obs[k].copy_(b[k], non_blocking=True)
+            self._dstage[slot].copy_(self._pstage[slot], non_blocking=True)
             self._h2d_ev.record(self._h2d)
         main.wait_event(self._h2d_ev)
         with torch.no_grad():
-            pre = {k: (v[None] / 255.0 if k in self.cnn_keys else v[None]) for k, v in self._dev_obs.items()}
+            pre = {k: (d[k][None] / 255.0 if k in self.cnn_keys else d[k][None]) for k in self.obs_keys}
             mask = {k: v for k, v in pre.items() if k.startswith("mask")} or None
             actions = self.player.get_exploration_action(pre, self.is_continuous, mask)
             acts = torch.cat(actions, -1).view(self.ne, -1)
@@ -135,7 +149,7 @@ class InteractionLoop:
                 self._real_pin.copy_(torch.stack([a.argmax(-1) for a in actions]).view(len(self.actions_dim), -1),
                                      non_blocking=True)
             self._act_ev.record(main)
-        row = TensorDict({**{k: b[k] for k in self.row_keys}, "actions": acts}, batch_size=[self.ne])
+        row = TensorDict({**{k: d[k] for k in self.row_keys}, "actions": acts}, batch_size=[self.ne])
         self.rb.add(row[None, ...])
 
     # ------------------------------------------------------------------ one step

@@ -34,7 +34,7 @@ int ln_nchw_splits(int, int);
 void launch_ln_nchw_bwd(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
                         float*, float*, float*, int, int, int, int, hipStream_t);
 bool launch_ln_gru_fwd(const float*, const float*, int, const float*, const float*, float*, float*, float*, int, int, float,
-                       hipStream_t, int ldo = 0, const float* x2 = nullptr, int ldx2 = 0);
+                       hipStream_t, int ldo = 0, const float* x2 = nullptr, int ldx2 = 0, float* xsum = nullptr);
 int ln_gru_bwd_grid(int);
 bool launch_ln_gru_bwd(const float*, const float*, int, const float*, const float*, const float*, const float*, const float*,
                        float*, float*, float*, float*, float*, float*, int, int, hipStream_t, const float* dadd = nullptr,
@@ -864,7 +864,8 @@ std::vector<int64_t> scanp_info(int64_t B, int64_t S, int64_t D, int64_t H, int6
 void set_gru_vec(bool on);
 
 void ln_gru_into(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::Tensor beta, double eps, torch::Tensor out,
-                 c10::optional<torch::Tensor> mean_out, c10::optional<torch::Tensor> rstd_out, c10::optional<torch::Tensor> x2) {
+                 c10::optional<torch::Tensor> mean_out, c10::optional<torch::Tensor> rstd_out, c10::optional<torch::Tensor> x2,
+                 bool write_sum) {
   check_f32(x, "x");
   check_f32(gamma, "gamma");
   check_f32(beta, "beta");
@@ -887,7 +888,8 @@ void ln_gru_into(torch::Tensor x, torch::Tensor h, torch::Tensor gamma, torch::T
   auto rstd = keep ? *rstd_out : torch::empty({M}, x.options());
   bool ok = launch_ln_gru_fwd(x.data_ptr<float>(), h.data_ptr<float>(), h.stride(0), gamma.data_ptr<float>(),
                               beta.data_ptr<float>(), out.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                              M, H, (float)eps, cur_stream(), out.stride(0), x2p, (int)ldx2);
+                              M, H, (float)eps, cur_stream(), out.stride(0), x2p, (int)ldx2,
+                              (write_sum && x2p) ? x.data_ptr<float>() : nullptr);
   TORCH_CHECK(ok, "ln_gru_into: unsupported hidden size ", H);
 }
 
@@ -1193,7 +1195,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_gru_vec", &set_gru_vec);  // float4 wide-row LN-GRU forward on (default) / off (A/B, tests)
   m.def("ln_gru_into", &ln_gru_into, pybind11::arg("x"), pybind11::arg("h"), pybind11::arg("gamma"), pybind11::arg("beta"),
         pybind11::arg("eps"), pybind11::arg("out"), pybind11::arg("mean") = pybind11::none(),
-        pybind11::arg("rstd") = pybind11::none(), pybind11::arg("x2") = pybind11::none());
+        pybind11::arg("rstd") = pybind11::none(), pybind11::arg("x2") = pybind11::none(),
+        pybind11::arg("write_sum") = false);  // write_sum: x <- x + x2 (the whole GRU input, for a backward)
   m.def("colsum", &colsum);
   m.def("cartpole_step", &cartpole_step);
   m.def("ppo_cartpole_rollout", &ppo_cartpole_rollout);

@@ -12,11 +12,12 @@
 namespace srl {
 
 template <int MAXH>
-__global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict__ x, const float* __restrict__ h, int ldh,
+// xsum (may alias x): the summed input x + x2 written back (the split-GEMM caller whose backward reads the whole gx)
+__global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* x, const float* __restrict__ h, int ldh,
                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
                                                          float* __restrict__ hn, float* __restrict__ mean_out,
                                                          float* __restrict__ rstd_out, int M, int H, float eps,
-                                                         int ldo, const float* __restrict__ x2, int ldx2) {
+                                                         int ldo, const float* __restrict__ x2, int ldx2, float* xsum) {
   __shared__ float red[4];
   const int T = 256, N = 3 * H;
   for (int row = blockIdx.x; row < M; row += gridDim.x) {
@@ -31,6 +32,7 @@ __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict
       for (int g = 0; g < 3; ++g) {
         v[g][k] = j < H ? xr[g * H + j] + (x2r ? x2r[g * H + j] : 0.f) : 0.f;
         s += v[g][k];
+        if (xsum && j < H) xsum[(int64_t)row * N + g * H + j] = v[g][k];  // same element this thread just read
       }
     }
     const float mu = block_sum<4>(s, red) / N;
@@ -71,11 +73,11 @@ __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* __restrict
 // vector load issued before the row statistics reduce.  The scalar forms issue 3 * MAXH four-byte loads per
 // thread per row from 256 threads.
 template <int NW>
-__global__ void __launch_bounds__(64 * NW) ln_gru_fwd4_kernel(const float* __restrict__ x, const float* __restrict__ h, int ldh,
+__global__ void __launch_bounds__(64 * NW) ln_gru_fwd4_kernel(const float* x, const float* __restrict__ h, int ldh,
                                                               const float* __restrict__ gamma, const float* __restrict__ beta,
                                                               float* __restrict__ hn, float* __restrict__ mean_out,
                                                               float* __restrict__ rstd_out, int M, int H, float eps,
-                                                              int ldo, const float* __restrict__ x2, int ldx2) {
+                                                              int ldo, const float* __restrict__ x2, int ldx2, float* xsum) {
   __shared__ float red[NW];
   const int N = 3 * H, H4 = H >> 2, j4 = threadIdx.x;
   const float4* g4 = reinterpret_cast<const float4*>(gamma);
@@ -96,6 +98,7 @@ __global__ void __launch_bounds__(64 * NW) ln_gru_fwd4_kernel(const float* __res
       }
       v[g] = a;
       s += (a.x + a.y) + (a.z + a.w);
+      if (xsum) reinterpret_cast<float4*>(xsum + (int64_t)row * N)[g * H4 + j4] = a;
     }
     const float4 hp = reinterpret_cast<const float4*>(h + (int64_t)row * ldh)[j4];
     const float mu = block_sum<NW>(s, red) / N;
@@ -291,27 +294,28 @@ static int gru_maxh(int H) {
 }
 
 bool launch_ln_gru_fwd(const float* x, const float* h, int ldh, const float* gamma, const float* beta, float* hn,
-                       float* mean, float* rstd, int M, int H, float eps, hipStream_t st, int ldo, const float* x2, int ldx2) {
+                       float* mean, float* rstd, int M, int H, float eps, hipStream_t st, int ldo, const float* x2, int ldx2,
+                       float* xsum) {
   if (ldo <= 0) ldo = H;
   int mh = gru_maxh(H);
   dim3 g(M < 8192 ? M : 8192), b(256);
   const bool al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(h) | reinterpret_cast<uintptr_t>(hn) |
                     reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
-                    reinterpret_cast<uintptr_t>(x2)) & 15) == 0 && ldh % 4 == 0 && ldo % 4 == 0 && (!x2 || ldx2 % 4 == 0);
+                    reinterpret_cast<uintptr_t>(x2) | reinterpret_cast<uintptr_t>(xsum)) & 15) == 0 && ldh % 4 == 0 && ldo % 4 == 0 && (!x2 || ldx2 % 4 == 0);
   if (g_gru_vec && al && H % 1024 == 0 && H <= 4096) {
     const dim3 bw(H / 4);
     switch (H / 1024) {
-      case 1: hipLaunchKernelGGL(ln_gru_fwd4_kernel<4>, g, bw, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
-      case 2: hipLaunchKernelGGL(ln_gru_fwd4_kernel<8>, g, bw, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
-      case 4: hipLaunchKernelGGL(ln_gru_fwd4_kernel<16>, g, bw, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
+      case 1: hipLaunchKernelGGL(ln_gru_fwd4_kernel<4>, g, bw, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2, xsum); return true;
+      case 2: hipLaunchKernelGGL(ln_gru_fwd4_kernel<8>, g, bw, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2, xsum); return true;
+      case 4: hipLaunchKernelGGL(ln_gru_fwd4_kernel<16>, g, bw, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2, xsum); return true;
       default: break;
     }
   }
   switch (mh) {
-    case 2: hipLaunchKernelGGL(ln_gru_fwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
-    case 4: hipLaunchKernelGGL(ln_gru_fwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
-    case 8: hipLaunchKernelGGL(ln_gru_fwd_kernel<8>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
-    case 16: hipLaunchKernelGGL(ln_gru_fwd_kernel<16>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2); return true;
+    case 2: hipLaunchKernelGGL(ln_gru_fwd_kernel<2>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2, xsum); return true;
+    case 4: hipLaunchKernelGGL(ln_gru_fwd_kernel<4>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2, xsum); return true;
+    case 8: hipLaunchKernelGGL(ln_gru_fwd_kernel<8>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2, xsum); return true;
+    case 16: hipLaunchKernelGGL(ln_gru_fwd_kernel<16>, g, b, 0, st, x, h, ldh, gamma, beta, hn, mean, rstd, M, H, eps, ldo, x2, ldx2, xsum); return true;
     default: return false;
   }
 }

@@ -135,3 +135,25 @@ def test_head_linear_sample_with_layernorm_prologue():
     for a_, b_ in ((y1, y0), (m1, m0), (r1, r0), (p1, p0), (l1, l0), (s1, s0)):
         torch.testing.assert_close(a_, b_, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(x1, x0, rtol=1e-3, atol=1e-3)
+
+
+def test_ln_gru_into_writes_back_the_summed_input():
+    """``ln_gru_into(..., x2=, write_sum=True)`` (the continuous rollout's split GRU input GEMM): same next state and
+    statistics as the kernel on the materialised sum, and ``x`` holds the sum afterwards (the backward reads it)."""
+    from sheeprl_prey_amd import ops
+
+    C = ops._ext()
+    torch.manual_seed(3)
+    for M, H in ((1024, 512), (33, 256), (16, 1024)):
+        x = torch.randn(M, 3 * H, device="cuda")
+        x2s = torch.randn(M, 3 * H + 40, device="cuda")[:, 8:8 + 3 * H]  # row-strided addend
+        h = torch.randn(M, H, device="cuda")
+        g, b = 1 + 0.1 * torch.randn(3 * H, device="cuda"), 0.1 * torch.randn(3 * H, device="cuda")
+        ref_x = x + x2s
+        o0, m0, r0 = torch.empty(M, H, device="cuda"), torch.empty(M, device="cuda"), torch.empty(M, device="cuda")
+        C.ln_gru_into(ref_x.clone(), h, g, b, 1e-3, o0, mean=m0, rstd=r0)
+        o1, m1, r1 = torch.empty(M, H, device="cuda"), torch.empty(M, device="cuda"), torch.empty(M, device="cuda")
+        C.ln_gru_into(x, h, g, b, 1e-3, o1, mean=m1, rstd=r1, x2=x2s, write_sum=True)
+        torch.testing.assert_close(x, ref_x, rtol=0, atol=0)
+        for a_, b_ in ((o1, o0), (m1, m0), (r1, r0)):
+            torch.testing.assert_close(a_, b_, rtol=1e-6, atol=1e-6)
