@@ -183,7 +183,7 @@ class DreamerV3Trainer:
         self._phase_imagine(data)
         self._coll_lambda()
         dev = data["rewards"].device
-        if self.overlap_ac and dev.type == "cuda":
+        if self.overlap_ac and dev.type == "cuda" and self.runner.world_size == 1:
             main = torch.cuda.current_stream(dev)
             side = sidestream._stream(sidestream._index(dev))  # its own half of the column-sum tickets
             side.wait_stream(main)
@@ -192,7 +192,9 @@ class DreamerV3Trainer:
             keep = self._st.get("actor_rec")
             with torch.cuda.stream(side):
                 self._phase_actor(data)
+                self._coll_actor()  # (one rank: no communication; kept so the phase contract holds)
             self._phase_critic(data)
+            self._coll_critic()
             main.wait_stream(side)
             del keep
             return self._phase_final(data)
