@@ -218,10 +218,14 @@ class ContinuousRollout:
         Wg = self.gru.linear.weight
         gln, rln, tln = self.gru.layer_norm, self.rec_ln, self.tr_ln
         d_a = torch.zeros(H + 1, M, A, device=dev) if d_acts is None else d_acts.contiguous().clone()
+        dtp = None
         if d_traj is not None:
             d_traj = d_traj.reshape(H + 1, M, S + Hd)
             dh = d_traj[H, :, S:].contiguous()
-            dp = d_traj[H, :, :S].contiguous()
+            # the prior half of every step's trajectory gradient, contiguous in ONE copy: each step's dp then
+            # accumulates into its own row block in place (no per-step copy of a strided GEMM addend)
+            dtp = d_traj[:, :, :S].contiguous()
+            dp = dtp[H]
         else:
             dh = torch.zeros(M, Hd, device=dev)
             dp = torch.zeros(M, S, device=dev)
@@ -263,7 +267,7 @@ class ContinuousRollout:
             # contiguous [S, D] table of the forward's gathers: the [D, S] column slice of Wr has row stride S + A (not
             # 16-byte aligned), which sends the library to a 32 x 32-tile kernel (~26 us vs ~10 us per step)
             wp = self.rec_table.t()
-            dp = torch.mm(dz, wp) if d_traj is None else torch.addmm(d_traj[s, :, :S], dz, wp)
+            dp = torch.mm(dz, wp) if dtp is None else dtp[s].addmm_(dz, wp)
             # dh_s = (direct + d_traj) + the h half of d(h | x); the consumed dh buffer becomes the next dh_prev
             dh, dh_prev = dh_prev.add_(dcat[:, :Hd]), dh
         d_a[:H].view(H * M, A).addmm_(dz_all.view(H * M, D), Wr[:, S:])
