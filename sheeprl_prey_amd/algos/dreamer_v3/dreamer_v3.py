@@ -88,7 +88,9 @@ class DreamerV3Trainer:
       memory pool);
     * no graphs: eager."""
 
-    PHASES = ("wm", "imagine", "actor", "critic", "final")
+    # the segmented (multi-rank) form's graphs: the actor and critic phases share one (neither reads the other's
+    # all-reduce; both collectives run after it), one graph boundary fewer per step
+    PHASES = ("wm", "imagine", "actor+critic", "final")
 
     def __init__(self, runner, cfg, world_model, actor, critic, target_critic, world_optimizer, actor_optimizer,
                  critic_optimizer, moments: Moments, is_continuous: bool, actions_dim: Sequence[int],
@@ -135,8 +137,8 @@ class DreamerV3Trainer:
             from sheeprl_prey_amd.parallel.graphs import SegmentedGraph
 
             self.seg = SegmentedGraph(
-                [self._phase_wm, self._phase_imagine, self._phase_actor, self._phase_critic, self._phase_final],
-                [self._coll_wm, self._coll_lambda, self._coll_actor, self._coll_critic],
+                [self._phase_wm, self._phase_imagine, self._phase_actor_critic, self._phase_final],
+                [self._coll_wm, self._coll_lambda, self._coll_actor_critic],
                 warmup=2,
             )
 
@@ -220,6 +222,14 @@ class DreamerV3Trainer:
         set_phase("coll_critic")
         if not dry:
             self.runner.sync_gradients(self.critic_optimizer)
+
+    def _coll_actor_critic(self, dry: bool = False) -> None:
+        self._coll_actor(dry)
+        self._coll_critic(dry)
+
+    def _phase_actor_critic(self, data: Dict[str, Tensor]) -> None:
+        self._phase_actor(data)
+        self._phase_critic(data)
 
     def _coll_lambda(self, dry: bool = False) -> None:
         set_phase("coll_lambda")
