@@ -126,11 +126,14 @@ class DreamerV3Trainer:
         # the actor all-reduce overlaps the critic phase wherever the step is not cut between phases
         self.defer_actor_sync = not self.segmented
         # discrete single-graph step on one rank: the actor phase on a side stream beside the critic phase, joined
-        # before the final phase.  A backward runs on the stream its forward ran on: the actor's loss graph is built
+        # before the final phase (dense <= 512, see below).  A backward runs on the stream its forward ran on: the actor's loss graph is built
         # inside its phase (side stream), the critic reuses the imagination's forward graph (main stream).  Measured
         # +0.4 % (the two phases' GEMMs slow each other, profiles/r5_ac_overlap.md); the continuous step (critic on
         # the side beside the rollout backward) measured 1.4 % slower and stays in line.  SRL_DV3_AC_OVERLAP=0: in line
+        # Wider models fill the chip with either phase alone: XL (dense 1024, 5 layers) measured 47.0-47.3 overlapped
+        # vs 48.2-48.4 in line, so the overlap is kept to dense <= 512 (the Atari-100k recipe)
         self.overlap_ac = (not self.segmented and ws == 1 and not is_continuous
+                           and int(cfg.algo.get("dense_units", 512)) <= 512
                            and os.environ.get("SRL_DV3_AC_OVERLAP", "1") != "0")
         self.graphed = GraphedStep(self._full_step, warmup=2, enabled=single, name="dreamer_v3_train")
         if self.segmented:
