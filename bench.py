@@ -51,9 +51,6 @@ def parse():
     p.add_argument("--segmented", action="store_true",
                    help="use the multi-rank graph mode (one hipGraph per phase, collectives between replays) "
                         "on any N, to price it against the single-graph step at N=1")
-    p.add_argument("--graph-collectives", type=int, default=0, choices=[0, 1],
-                   help="N>1 over RCCL: 1 = capture the collectives in the one step graph (single+rccl), 0 = one graph "
-                        "per phase with the collectives issued eagerly between replays (segmented, default)")
     p.add_argument("--pg-timeout", type=float, default=300.0,
                    help="process-group timeout and host heartbeat (seconds): a stalled rank exits non-zero")
     p.add_argument("--check-finite", type=int, default=0,
@@ -116,7 +113,7 @@ def main():
                 "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]"]
     overrides = base + [
         "fabric.accelerator=cuda", f"fabric.cuda_graphs={not args.no_graphs}", "metric.log_every=1000000000",
-        f"fabric.fused_ops={not args.eager_ops}", f"fabric.graph_collectives={bool(args.graph_collectives)}",
+        f"fabric.fused_ops={not args.eager_ops}",
         f"fabric.pg_timeout_s={args.pg_timeout}",
     ] + ([f"fabric.tunable_gemm={args.gemm_tuning}"] if args.gemm_tuning else []) + (XL_OVERRIDES if args.xl else []) + list(
         args.overrides)

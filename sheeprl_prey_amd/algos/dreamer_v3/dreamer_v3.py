@@ -79,11 +79,9 @@ class DreamerV3Trainer:
 
     Execution:
     * one rank, graphs: ONE hipGraph for the whole step;
-    * N ranks over RCCL, graphs, ``fabric.graph_collectives=True`` (opt-in): still ONE hipGraph per rank -
-      the collectives are captured in it; the world-model buckets launch from the backward hooks and
-      overlap the rest of the world-model backward, the actor all-reduce overlaps the critic phase;
-    * N ranks otherwise (gloo, or ``graph_collectives=False``, the default): one hipGraph per phase with the
-      collectives issued eagerly between replays (for continuous actors the actor phase's backward
+    * N ranks, graphs: one hipGraph per phase with the collectives issued eagerly between replays (no
+      collective is ever captured: a capture holding RCCL work launched from the autograd thread aborted
+      the process on ROCm, profiles/r6_rccl_abort.md) (for continuous actors the actor phase's backward
       then runs through the imagination graph the previous capture recorded; both captures share one
       memory pool);
     * no graphs: eager."""
@@ -119,10 +117,9 @@ class DreamerV3Trainer:
         self.teacher: Dict[str, Tensor] = None
         ws = runner.world_size
         graphs = bool(runner.cuda_graphs)
-        capture_coll = ws > 1 and getattr(runner, "capture_collectives", False)
-        self.segmented = graphs and (force_segmented or (ws > 1 and not capture_coll))
+        self.segmented = graphs and (force_segmented or ws > 1)
         single = graphs and not self.segmented
-        self.graph_mode = "segmented" if self.segmented else (("single+rccl" if ws > 1 else "single") if single else "eager")
+        self.graph_mode = "segmented" if self.segmented else ("single" if single else "eager")
         # the actor all-reduce overlaps the critic phase wherever the step is not cut between phases
         self.defer_actor_sync = not self.segmented
         # discrete single-graph step on one rank: the actor phase on a side stream beside the critic phase, joined

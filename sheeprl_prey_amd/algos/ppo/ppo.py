@@ -215,9 +215,9 @@ class SegmentedPPOUpdate:
             torch.cuda.current_stream().wait_stream(s)
             return
         g = torch.cuda.CUDAGraph()
-        torch.cuda.synchronize()
-        from sheeprl_prey_amd.parallel.graphs import capture_error_mode
+        from sheeprl_prey_amd.parallel.graphs import capture_error_mode, quiesce_for_capture
 
+        quiesce_for_capture()
         with torch.cuda.graph(g, pool=self.pool, capture_error_mode=capture_error_mode()):
             fn()
         self.pool = g.pool()
@@ -276,10 +276,7 @@ class PPOTrainer:
         self.ent_t = torch.tensor(float(cfg.algo.ent_coef), device=dev)
         graphs = dev.type == "cuda" and bool(getattr(runner, "cuda_graphs", False)) and not cfg.algo.anneal_lr
         ws = runner.world_size
-        # N ranks over RCCL: the per-minibatch gradient all-reduces are captured inside the ONE update graph
-        self.capture_coll = graphs and ws > 1 and not force_segmented and bool(getattr(runner, "capture_collectives", False))
-        self.segmented = (SegmentedPPOUpdate(self) if graphs and (ws > 1 or force_segmented) and not self.capture_coll
-                          else None)
+        self.segmented = SegmentedPPOUpdate(self) if graphs and (ws > 1 or force_segmented) else None
         self.graphed = GraphedStep(self._train, warmup=2, enabled=graphs and self.segmented is None, name="ppo_train")
         # DistributedSampler permutations of the shared rollout (seeded per epoch, the same every update as in
         # the reference's sampler.set_epoch(epoch) loop): built once, static inputs of the captured update
@@ -299,7 +296,7 @@ class PPOTrainer:
         if self.segmented is not None:
             return "segmented"
         if self.graphed.enabled:
-            return "graph+rccl" if self.capture_coll else "graph"
+            return "graph"
         return "eager"
 
     def _train(self, data: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:

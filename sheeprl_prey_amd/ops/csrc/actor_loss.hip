@@ -139,12 +139,17 @@ __global__ __launch_bounds__(NTH) void actor_loss_cont_kernel(const float* __res
   if (threadIdx.x == 0) partial[blockIdx.x] = acc;
 }
 
-__global__ void actor_loss_final(const float* __restrict__ partial, int n, float scale, float* __restrict__ loss) {
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int i = 0; i < n; ++i) s += partial[i];
-    *loss = s * scale;
-  }
+// fixed-order tree over the block partials (lane-strided in index order, butterfly wave sum, 4 wave totals in order):
+// bitwise reproducible, n/256 dependent adds per lane instead of n in one lane
+__global__ void __launch_bounds__(256) actor_loss_final(const float* __restrict__ partial, int n, float scale,
+                                                        float* __restrict__ loss) {
+  __shared__ float wsum[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += partial[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *loss = ((wsum[0] + wsum[1]) + (wsum[2] + wsum[3])) * scale;
 }
 
 // Imagined continuation flags and discounts (reference dreamer_v3.py:680-700): c_0 = 1 - done,
@@ -185,7 +190,7 @@ void launch_actor_loss_cont(const float* pre, const float* lam, const float* bas
   const int nb = actor_loss_blocks(T * M);
   hipLaunchKernelGGL(srl::aloss::actor_loss_cont_kernel, dim3(nb), dim3(srl::aloss::NTH), 0, st, pre, lam, base, disc, offp,
                      invp, A, T, M, ent_coef, init_std, min_std, lo, hi, dpre, dlam, dbase, partial);
-  hipLaunchKernelGGL(srl::aloss::actor_loss_final, dim3(1), dim3(64), 0, st, partial, nb, -1.f / (float)((T - 1) * M), loss);
+  hipLaunchKernelGGL(srl::aloss::actor_loss_final, dim3(1), dim3(256), 0, st, partial, nb, -1.f / (float)((T - 1) * M), loss);
 }
 
 void launch_actor_loss(const float* z, const float* act, const float* lam, const float* base, const float* disc,
@@ -197,5 +202,5 @@ void launch_actor_loss(const float* z, const float* act, const float* lam, const
   const int nb = actor_loss_blocks(T * M);
   hipLaunchKernelGGL(srl::aloss::actor_loss_kernel, dim3(nb), dim3(srl::aloss::NTH), 0, st, z, act, lam, base, disc, offp,
                      invp, hd, A, T, M, ent_coef, dz, partial);
-  hipLaunchKernelGGL(srl::aloss::actor_loss_final, dim3(1), dim3(64), 0, st, partial, nb, -1.f / (float)((T - 1) * M), loss);
+  hipLaunchKernelGGL(srl::aloss::actor_loss_final, dim3(1), dim3(256), 0, st, partial, nb, -1.f / (float)((T - 1) * M), loss);
 }

@@ -684,12 +684,17 @@ __global__ void __launch_bounds__(256) value_loss2_kernel(const float* __restric
   if (threadIdx.x == 0) partial[blockIdx.x] = (rowv[0] + rowv[1]) + (rowv[2] + rowv[3]);
 }
 
-__global__ void value_loss_final(const float* __restrict__ partial, int n, float scale, float* __restrict__ loss) {
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int i = 0; i < n; ++i) s += partial[i];
-    *loss = s * scale;
-  }
+// fixed-order tree: lane-strided sums (each thread's elements in index order), a butterfly wave sum, then the 4 wave
+// totals in order - bitwise reproducible run to run, ~n/256 dependent adds per lane instead of n in one lane
+__global__ void __launch_bounds__(256) value_loss_final(const float* __restrict__ partial, int n, float scale,
+                                                        float* __restrict__ loss) {
+  __shared__ float wsum[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += partial[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *loss = ((wsum[0] + wsum[1]) + (wsum[2] + wsum[3])) * scale;
 }
 
 #define TH_DISPATCH(KERNEL, ...)                                                                       \
@@ -716,7 +721,7 @@ bool launch_value_loss2(const float* logits, const float* y1, const float* y2, c
                         float* dlogits, float* partial, float* loss, int R, int K, hipStream_t st) {
   const float scale = 1.f / (float)R;
   TH_DISPATCH(value_loss2_kernel, logits, y1, y2, w, bins, dlogits, partial, R, K, scale);
-  hipLaunchKernelGGL(value_loss_final, dim3(1), dim3(64), 0, st, partial, cdiv(R, 4), scale, loss);
+  hipLaunchKernelGGL(value_loss_final, dim3(1), dim3(256), 0, st, partial, cdiv(R, 4), scale, loss);
   return true;
 }
 bool launch_twohot_mean_fwd(const float* logits, const float* bins, float* out, float* s, int R, int K, hipStream_t st) {

@@ -221,7 +221,7 @@ class FlatOptimizer:
         return norm
 
     # ------------------------------------------------------------------ overlapped gradient all-reduce
-    def enable_overlap(self, group=None, world_size: int = 1, bucket_mb: float = 32, in_capture: bool = False) -> bool:
+    def enable_overlap(self, group=None, world_size: int = 1, bucket_mb: float = 32) -> bool:
         """Bucketed all-reduce overlapped with the backward (eager multi-rank paths).
 
         The slab is cut into buckets from its tail (parameters are laid out in forward order, so
@@ -235,14 +235,10 @@ class FlatOptimizer:
         backward between ``zero_grad`` (which arms) and the sync, as every algorithm here does.
         Reference counterpart: the per-model DDP reducers of ``dreamer_v3/agent.py:1054-1063``.
 
-        ``in_capture``: the hooks also launch their buckets while a hipGraph is being captured (RCCL
-        collectives are stream-capturable), so a graph-captured multi-rank step overlaps the gradient
-        all-reduce with the rest of its backward exactly like the eager path."""
+        Collectives never enter a hipGraph: inside a capture the hooks do nothing (the segmented graph
+        mode issues the whole-slab all-reduce eagerly between phase replays)."""
         if world_size <= 1 or getattr(self, "_ov", None) is not None:
-            ov = getattr(self, "_ov", None)
-            if ov is not None:
-                ov["in_capture"] = ov["in_capture"] or in_capture
-            return ov is not None
+            return getattr(self, "_ov", None) is not None
         if self.flat_grad._base is not None or any(
                 getattr(p, "_flat_slab", (None,))[0] is not None and p._flat_slab[0]() is not self for p in self.params):
             return False  # slab shared with another optimiser: keep the plain path
@@ -270,7 +266,7 @@ class FlatOptimizer:
         use_avg = g.is_cuda and dist.get_backend(group) == "nccl"
         self._ov = dict(group=group, ws=world_size, buckets=buckets, ranges=ranges, bucket_of=bucket_of,
                         op=dist.ReduceOp.AVG if use_avg else dist.ReduceOp.SUM, avg=use_avg, armed=False,
-                        pending=[], seen=[], works=[], next=0, in_capture=bool(in_capture))
+                        pending=[], seen=[], works=[], next=0)
         self._ov_handles = [p.register_post_accumulate_grad_hook(self._make_ov_hook(i)) for i, p in enumerate(self.params)]
         return True
 
@@ -279,11 +275,10 @@ class FlatOptimizer:
 
         def hook(p: Tensor) -> None:
             self_ = ref()
-            # inside a hipGraph capture the collectives are captured too only in the single-graph RCCL mode
-            # (``in_capture``); the segmented mode keeps them between replays
+            # no collective inside a hipGraph capture: the segmented mode issues them between replays
             if self_ is None or not self_._ov["armed"]:
                 return
-            if p.is_cuda and torch.cuda.is_current_stream_capturing() and not self_._ov["in_capture"]:
+            if p.is_cuda and torch.cuda.is_current_stream_capturing():
                 return
             self_._ov_ready(i, p)
 

@@ -27,6 +27,20 @@ def capture_error_mode() -> str:
     return "thread_local" if dist.is_available() and dist.is_initialized() else "global"
 
 
+def quiesce_for_capture(settle_s: float = 0.25) -> None:
+    """Called right before a capture begins: the device is drained and, with a process group up, the host
+    waits ``settle_s`` so the process group's watchdog reaps the (now complete) work of the eager warm-up
+    collectives before the capture opens - its next poll (every ~100 ms) then has no event left to query
+    while the capture is open.  A few captures per run: the wait costs well under a second in total."""
+    import time
+
+    import torch.distributed as dist
+
+    torch.cuda.synchronize()
+    if dist.is_available() and dist.is_initialized():
+        time.sleep(settle_s)
+
+
 class GraphedStep:
     def __init__(self, fn: Callable[[Dict[str, Tensor]], Dict[str, Tensor]], warmup: int = 2, enabled: bool = True,
                  name: str = "step"):
@@ -74,7 +88,7 @@ class GraphedStep:
             self._calls += 1
             return out
         g = torch.cuda.CUDAGraph()
-        torch.cuda.synchronize()
+        quiesce_for_capture()
         with torch.cuda.graph(g, pool=self.pool, capture_error_mode=capture_error_mode()):
             self.static_out = self.fn(self.static_in)
         self.graph = g
@@ -159,7 +173,7 @@ class SegmentedGraph:
                 out = self._run_eager(self.static_in)
             torch.cuda.current_stream().wait_stream(s)
             return out
-        torch.cuda.synchronize()
+        quiesce_for_capture()
         graphs = []
         pool = None
         out = None
@@ -188,10 +202,8 @@ class PhasedStep:
     """A training step given as ``phases`` separated by ``colls`` (gradient all-reduces etc.).
 
     * ``graphs`` and one rank: the whole step (phases + the no-op collectives) is ONE hipGraph;
-    * ``graphs`` and N ranks over RCCL (``runner.capture_collectives``): still ONE hipGraph per rank,
-      the collectives captured in it (``single+rccl``);
-    * ``graphs`` and N ranks otherwise (gloo): ``SegmentedGraph`` (per-phase graphs, collectives eagerly
-      in between);
+    * ``graphs`` and N ranks: ``SegmentedGraph`` (per-phase graphs, collectives eagerly in between -
+      no collective is ever captured);
     * otherwise eager.
     Phase/collective contract as in ``SegmentedGraph``."""
 
@@ -202,9 +214,6 @@ class PhasedStep:
         use = bool(graphs) and torch.cuda.is_available() and runner.device.type == "cuda"
         if not use:
             self.mode = "eager"
-        elif runner.world_size > 1 and not force_segmented and getattr(runner, "capture_collectives", False):
-            self.mode = "single+rccl"
-            self._impl = GraphedStep(self._run, warmup=warmup, enabled=True, name=name)
         elif runner.world_size > 1 or force_segmented:
             self.mode = "segmented"
             self._impl = SegmentedGraph(self.phases, self.colls, warmup=warmup)

@@ -158,7 +158,6 @@ class Runner:
         bucket_mb: float = 32,
         tunable_gemm: str = "use",
         overlap_grad_sync: bool = True,
-        graph_collectives: bool = False,
         pg_timeout_s: float = 1800,
         process_group=None,
         **_unused,
@@ -183,11 +182,6 @@ class Runner:
         self.bucket_mb = float(bucket_mb)
         # bucketed all-reduce launched from backward hooks (FlatOptimizer.enable_overlap)
         self.overlap_grad_sync = bool(overlap_grad_sync)
-        # multi-rank hipGraph steps: capture the RCCL collectives INSIDE the one step graph (N ranks replay
-        # one graph each, like N=1) instead of per-phase graphs with eager collectives in between.  Off by
-        # default: the segmented mode issues its collectives eagerly (the process group's timeout watches
-        # them); the captured mode has only run on 1-rank communicators (RCCL refuses 2 ranks on one GPU)
-        self.graph_collectives = bool(graph_collectives)
         # process-group timeout: a stalled collective ends the run with an error instead of holding the node
         self.pg_timeout_s = float(pg_timeout_s)
         # library-GEMM solution choice (parallel/gemm_tuning.py): committed TunableOp results
@@ -195,7 +189,7 @@ class Runner:
         self._kwargs = dict(
             devices=devices, num_nodes=num_nodes, strategy=strategy, accelerator=accelerator,
             precision=precision, callbacks=callbacks, cuda_graphs=cuda_graphs, fused_ops=fused_ops, bucket_mb=bucket_mb,
-            tunable_gemm=tunable_gemm, overlap_grad_sync=overlap_grad_sync, graph_collectives=graph_collectives,
+            tunable_gemm=tunable_gemm, overlap_grad_sync=overlap_grad_sync,
             pg_timeout_s=pg_timeout_s,
         )
         self.group = process_group  # None == WORLD
@@ -243,11 +237,6 @@ class Runner:
         if forced:
             return forced
         return "nccl" if self.accelerator == "cuda" else "gloo"
-
-    @property
-    def capture_collectives(self) -> bool:
-        """Graph-captured steps may record their gradient collectives (RCCL only: gloo is host-side)."""
-        return self.cuda_graphs and self.graph_collectives and self.backend == "nccl" and self.accelerator == "cuda"
 
     @property
     def logger(self):
@@ -409,8 +398,7 @@ class Runner:
             optimizer.all_reduce_grads(self.group, self.world_size, bucket_mb=self.bucket_mb, wait=wait)
             if self.overlap_grad_sync:
                 # from the next zero_grad on, buckets launch from the backward hooks (same call on every rank)
-                optimizer.enable_overlap(self.group, self.world_size, bucket_mb=self.bucket_mb,
-                                         in_capture=self.capture_collectives)
+                optimizer.enable_overlap(self.group, self.world_size, bucket_mb=self.bucket_mb)
             return
         grads = [p.grad for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
         if not grads:

@@ -28,3 +28,16 @@ def test_value_loss2_matches_fp64_composite(T, M, K, spread):
     r.backward()
     torch.testing.assert_close(loss.double(), r.detach(), rtol=2e-5, atol=1e-6)
     torch.testing.assert_close(logits.grad.double(), l64.grad, rtol=1e-4, atol=1e-9)
+
+
+def test_value_loss2_bitwise_reproducible():
+    """The final reduction is a fixed-order tree: two runs on the same inputs give bitwise-equal losses."""
+    from sheeprl_prey_amd import ops
+
+    torch.manual_seed(0)
+    logits = torch.randn(15, 1024, 255, device="cuda") * 2
+    y1, y2 = torch.randn(15, 1024, 1, device="cuda") * 3, torch.randn(15, 1024, 1, device="cuda") * 3
+    w = torch.rand(15, 1024, 1, device="cuda")
+    a = ops.twohot_value_loss(logits, y1, y2, w)
+    b = ops.twohot_value_loss(logits, y1, y2, w)
+    assert torch.equal(a, b)
