@@ -35,6 +35,9 @@ import torch
 from sheeprl_prey_amd.data.tensordict import TensorDict
 
 _SPIN = os.environ.get("SRL_SPIN_WAIT", "1") != "0"
+# the host polls the action event for at most this long, then blocks on it (a rank whose player sits behind a long
+# gradient step does not burn a core that CPU-heavy env workers need)
+_SPIN_S = float(os.environ.get("SRL_SPIN_WAIT_MS", "2")) * 1e-3
 
 
 class InteractionLoop:
@@ -98,6 +101,8 @@ class InteractionLoop:
             self._h2d = torch.cuda.Stream(device=self.device)
             self._h2d_ev = torch.cuda.Event()
             self._act_ev = torch.cuda.Event()
+            rb_dev = getattr(self.rb, "device", None)
+            self._rb_on_device = rb_dev is not None and torch.device(rb_dev).type == "cuda"
 
     # ------------------------------------------------------------------ acting
     def _random_actions(self):
@@ -149,7 +154,12 @@ class InteractionLoop:
                 self._real_pin.copy_(torch.stack([a.argmax(-1) for a in actions]).view(len(self.actions_dim), -1),
                                      non_blocking=True)
             self._act_ev.record(main)
-        row = TensorDict({**{k: d[k] for k in self.row_keys}, "actions": acts}, batch_size=[self.ne])
+        # device-resident replay storage: one device-to-device copy from the twin; host storage (buffer.device=cpu,
+        # memmap): the pinned host row (no H2D + blocking D2H round trip)
+        if self._rb_on_device:
+            row = TensorDict({**{k: d[k] for k in self.row_keys}, "actions": acts}, batch_size=[self.ne])
+        else:
+            row = TensorDict({**{k: b[k] for k in self.row_keys}, "actions": acts.cpu()}, batch_size=[self.ne])
         self.rb.add(row[None, ...])
 
     # ------------------------------------------------------------------ one step
@@ -191,8 +201,12 @@ class InteractionLoop:
             if hp is not None:
                 t2 = time.perf_counter()
             if _SPIN:
-                while not self._act_ev.query():  # poll: lower wake-up latency than the blocking event wait
-                    pass
+                # poll (lower wake-up latency than the blocking event wait), bounded by _SPIN_S
+                t_end = time.perf_counter() + _SPIN_S
+                while not self._act_ev.query():
+                    if time.perf_counter() > t_end:
+                        self._act_ev.synchronize()
+                        break
             else:
                 self._act_ev.synchronize()
             if hp is not None:

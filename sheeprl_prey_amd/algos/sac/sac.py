@@ -172,20 +172,34 @@ class SACTrainer:
 
     TRAIN_KEYS = ("observations", "next_observations", "actions", "rewards", "dones")
 
-    def train_from_buffer(self, rb, batch_size: int, n_batches: int, do_ema: bool,
-                          aggregator: Optional[MetricAggregator] = None) -> bool:
-        """``n_batches`` SAC updates on minibatches drawn by ONE device launch each straight into the captured
-        step's static inputs (``ReplayBuffer.sample_rows_into``): per update one sampling kernel + one graph replay,
-        no host-side index draw / gather / copy-in.  One GPU, fused update, captured step, replay keys exactly the
-        train keys; False (nothing done) otherwise - the caller takes the regular path."""
-        impl = getattr(self.critic_step, "_impl", None)
-        if (self.fused is None or self.critic_step.mode != "single" or impl is None or impl.graph is None
-                or set(rb.keys()) != set(self.TRAIN_KEYS)):
-            return False
-        st = impl.static_in
+    def buffer_draw_inputs(self, rb, batch_size: int) -> Optional[Dict[str, Tensor]]:
+        """The captured fused step's static train inputs when ``train_from_buffer`` applies to ``rb`` (one GPU,
+        fused update, captured step, device-resident replay holding exactly the train keys, static batch of
+        ``batch_size``); None otherwise - the caller then takes the regular path.  Checked before any timing."""
+        if self.fused is None or set(rb.keys()) != set(self.TRAIN_KEYS):
+            return None
+        dev = getattr(rb, "device", None)
+        if dev is None or torch.device(dev).type != "cuda":
+            return None
+        st = self.critic_step.captured_inputs()
+        if st is None:
+            return None
         out = {k: st[k] for k in self.TRAIN_KEYS}
         if any(v.shape[0] != batch_size for v in out.values()):
+            return None
+        return out
+
+    def train_from_buffer(self, rb, batch_size: int, n_batches: int, do_ema: bool,
+                          aggregator: Optional[MetricAggregator] = None,
+                          out: Optional[Dict[str, Tensor]] = None) -> bool:
+        """``n_batches`` SAC updates on minibatches drawn by ONE device launch each straight into the captured
+        step's static inputs (``ReplayBuffer.sample_rows_into``): per update one sampling kernel + one graph replay,
+        no host-side index draw / gather / copy-in.  ``out``: ``buffer_draw_inputs(rb, batch_size)`` (looked up
+        when omitted); False (nothing done) when the draw does not apply - the caller takes the regular path."""
+        out = out if out is not None else self.buffer_draw_inputs(rb, batch_size)
+        if out is None:
             return False
+        st = self.critic_step.captured_inputs()
         ema = self.ema_weight(do_ema, st["ema_w"].device)
         if self._ema_static is not ema:
             st["ema_w"].copy_(ema)
@@ -196,7 +210,7 @@ class SACTrainer:
                 if i == 0:
                     return False
                 raise RuntimeError("SAC: the device replay draw stopped applying mid-update")
-            impl.replay_static()
+            self.critic_step.replay()
         return True
 
     def record(self, out: Dict[str, Tensor], aggregator: Optional[MetricAggregator]) -> None:
@@ -280,10 +294,13 @@ def sac_train_update(trainer: SACTrainer, runner, cfg, rb, update: int, learning
         return False
     training_steps = learning_starts if update == learning_starts else 1
     do_ema = update % ema_every == 0
-    if runner.world_size == 1 and not cfg.buffer.sample_next_obs:
+    draw = (trainer.buffer_draw_inputs(rb, cfg.per_rank_batch_size)
+            if runner.world_size == 1 and not cfg.buffer.sample_next_obs else None)
+    if draw is not None:
         with timer("Time/train_time"):
             if trainer.train_from_buffer(rb, cfg.per_rank_batch_size,
-                                         max(training_steps, 1) * cfg.algo.per_rank_gradient_steps, do_ema, aggregator):
+                                         max(training_steps, 1) * cfg.algo.per_rank_gradient_steps, do_ema, aggregator,
+                                         out=draw):
                 return True
     sample = rb.sample(max(training_steps, 1) * cfg.algo.per_rank_gradient_steps * cfg.per_rank_batch_size,
                        sample_next_obs=cfg.buffer.sample_next_obs)

@@ -119,11 +119,14 @@ class Heartbeat:
     last beat's label and exits with status 3 (``os._exit``: a rank stuck in a device wait never
     returns to Python).  ``timeout_s <= 0`` disables it.  Until the first ``beat()`` the limit is
     ``max(timeout_s, startup_grace_s)``: model / env construction, the first graph captures, TunableOp
-    tuning and diagnostic passes run before any step completes and must not trip a short step timeout."""
+    tuning and diagnostic passes run before any step completes and must not trip a short step timeout.
+    The grace defaults to ``grace_factor * timeout_s`` (scaled to the run: a short step timeout keeps a short
+    start-up limit), and callers re-arm it around long passes with ``grace()``."""
 
-    def __init__(self, timeout_s: float, label: str = "start", startup_grace_s: float = 1800.0):
+    def __init__(self, timeout_s: float, label: str = "start", startup_grace_s: Optional[float] = None,
+                 grace_factor: float = 4.0):
         self.timeout_s = float(timeout_s)
-        self.startup_grace_s = float(startup_grace_s)
+        self.startup_grace_s = float(startup_grace_s) if startup_grace_s is not None else grace_factor * self.timeout_s
         self._beaten = False
         self.label = label
         self._last = time.monotonic()

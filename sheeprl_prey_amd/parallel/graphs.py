@@ -233,6 +233,17 @@ class PhasedStep:
                 self.colls[i]()
         return out
 
+    def captured_inputs(self) -> Optional[Dict[str, Tensor]]:
+        """The static inputs of the captured single-graph step (write a batch into them, then ``replay()``);
+        None before the capture or in the other modes."""
+        if self.mode != "single" or self._impl.graph is None:
+            return None
+        return self._impl.static_in
+
+    def replay(self) -> Optional[Dict[str, Tensor]]:
+        """Replay the captured step on what the caller wrote into ``captured_inputs()`` (no copy-in)."""
+        return self._impl.replay_static() if self.mode != "eager" else None
+
     def __call__(self, data: Dict[str, Tensor]):
         if self.mode == "eager":
             return self._run(data)
