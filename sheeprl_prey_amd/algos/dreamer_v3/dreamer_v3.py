@@ -86,9 +86,10 @@ class DreamerV3Trainer:
       memory pool);
     * no graphs: eager."""
 
-    # the segmented (multi-rank) form's graphs: the actor and critic phases share one (neither reads the other's
-    # all-reduce; both collectives run after it), one graph boundary fewer per step
-    PHASES = ("wm", "imagine", "actor+critic", "final")
+    # the segmented (multi-rank) form's graphs: the actor all-reduce is issued (async) between the actor and critic
+    # graphs and runs on the RCCL stream while the critic graph replays; the critic collective joins it before the
+    # final graph (round 5 merged actor+critic into one graph and lost that overlap)
+    PHASES = ("wm", "imagine", "actor", "critic", "final")
 
     def __init__(self, runner, cfg, world_model, actor, critic, target_critic, world_optimizer, actor_optimizer,
                  critic_optimizer, moments: Moments, is_continuous: bool, actions_dim: Sequence[int],
@@ -120,8 +121,9 @@ class DreamerV3Trainer:
         self.segmented = graphs and (force_segmented or ws > 1)
         single = graphs and not self.segmented
         self.graph_mode = "segmented" if self.segmented else ("single" if single else "eager")
-        # the actor all-reduce overlaps the critic phase wherever the step is not cut between phases
-        self.defer_actor_sync = not self.segmented
+        # the actor all-reduce overlaps the critic phase: inside the single graph as a deferred join, in the
+        # segmented form as an async collective between the actor and critic replays (joined by ``_coll_critic``)
+        self.defer_actor_sync = True
         # discrete single-graph step on one rank: the actor phase on a side stream beside the critic phase, joined
         # before the final phase (dense <= 512, see below).  A backward runs on the stream its forward ran on: the actor's loss graph is built
         # inside its phase (side stream), the critic reuses the imagination's forward graph (main stream).  Measured
@@ -137,8 +139,8 @@ class DreamerV3Trainer:
             from sheeprl_prey_amd.parallel.graphs import SegmentedGraph
 
             self.seg = SegmentedGraph(
-                [self._phase_wm, self._phase_imagine, self._phase_actor_critic, self._phase_final],
-                [self._coll_wm, self._coll_lambda, self._coll_actor_critic],
+                [self._phase_wm, self._phase_imagine, self._phase_actor, self._phase_critic, self._phase_final],
+                [self._coll_wm, self._coll_lambda, self._coll_actor, self._coll_critic],
                 warmup=2,
             )
 
@@ -222,14 +224,10 @@ class DreamerV3Trainer:
         set_phase("coll_critic")
         if not dry:
             self.runner.sync_gradients(self.critic_optimizer)
-
-    def _coll_actor_critic(self, dry: bool = False) -> None:
-        self._coll_actor(dry)
-        self._coll_critic(dry)
-
-    def _phase_actor_critic(self, data: Dict[str, Tensor]) -> None:
-        self._phase_actor(data)
-        self._phase_critic(data)
+            if self.segmented:
+                # the final graph's clip/step read the actor slab: its in-flight all-reduce is joined here, eagerly
+                # (a stream dependency on the RCCL stream, no host wait) - the captured join saw no pending work
+                self.actor_optimizer.wait_grads()
 
     def _coll_lambda(self, dry: bool = False) -> None:
         set_phase("coll_lambda")
