@@ -23,6 +23,7 @@
 // side: a power of two below 32); all host-checked.
 #include "common.h"
 #include "conv.h"
+#include <algorithm>
 #include <string>
 
 
@@ -823,6 +824,106 @@ __global__ __launch_bounds__(256) void ln_bwd_flat_kernel(const float* __restric
   }
 }
 
+// The same backward one IMAGE per iteration: the image's dy block (C x HW floats, contiguous in NCHW) is read with
+// coalesced loads and transposed through LDS ([hw][C + 1]: conflict-free both ways), so no load touches a cache
+// line per lane (ln_bwd_flat_kernel's dy reads stride HW floats across the lanes).  Every workgroup holds its
+// channel partials of dgamma / dbeta in registers over its images and writes them to part[block][2C]; a second
+// kernel (ln_part_reduce_kernel) sums the blocks in a fixed order - no float atomics, bitwise reproducible.
+template <int CPL, int ACTC>
+__global__ __launch_bounds__(256) void ln_bwd_img_kernel(const float* __restrict__ dy, const float* __restrict__ z,
+                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                         float* __restrict__ dz, float* __restrict__ part, int N, int C,
+                                                         int lHW, int act, int ipb) {
+  extern __shared__ float sm[];  // [HW][C + 1] dy tile, then [2][4][64 * CPL] partials
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int HW = 1 << lHW, ld = C + 1, CHW = C << lHW;
+  const float invC = 1.f / (float)C;
+  float cg[CPL], cb[CPL], g[CPL], bt[CPL];
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) {
+    const int c = lane + 64 * e;
+    cg[e] = cb[e] = 0.f;
+    g[e] = (c < C && gamma) ? gamma[c] : 1.f;
+    bt[e] = (c < C && beta) ? beta[c] : 0.f;
+  }
+  const int n0 = blockIdx.x * ipb, n1 = min(N, n0 + ipb);
+  for (int n = n0; n < n1; ++n) {
+    const float* dyn = dy + (size_t)n * CHW;
+    for (int e = threadIdx.x; e < CHW; e += 256) sm[(e & (HW - 1)) * ld + (e >> lHW)] = dyn[e];
+    __syncthreads();
+    for (int hw = w; hw < HW; hw += 4) {
+      const int m = (n << lHW) + hw;
+      const float mu = mean[m], rs = rstd[m];
+      float xh[CPL], dxh[CPL], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) {
+        const int c = lane + 64 * e;
+        xh[e] = dxh[e] = 0.f;
+        if (c < C) {
+          xh[e] = (z[(size_t)m * C + c] - mu) * rs;
+          const float da = sm[hw * ld + c] * cact_grad_c<ACTC>(xh[e] * g[e] + bt[e], act);
+          cg[e] += da * xh[e];
+          cb[e] += da;
+          dxh[e] = da * g[e];
+        }
+        s1 += dxh[e];
+        s2 += dxh[e] * xh[e];
+      }
+      s1 = wave_sum(s1) * invC;
+      s2 = wave_sum(s2) * invC;
+#pragma unroll
+      for (int e = 0; e < CPL; ++e)
+        if (lane + 64 * e < C) dz[(size_t)m * C + lane + 64 * e] = rs * (dxh[e] - s1 - xh[e] * s2);
+    }
+    __syncthreads();
+  }
+  float* cr = sm;  // [2][4][64 * CPL]
+#pragma unroll
+  for (int e = 0; e < CPL; ++e) {
+    cr[(0 * 4 + w) * 64 * CPL + lane + 64 * e] = cg[e];
+    cr[(1 * 4 + w) * 64 * CPL + lane + 64 * e] = cb[e];
+  }
+  __syncthreads();
+  float* pb = part + (size_t)blockIdx.x * 2 * C;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float* a = cr + c;
+    pb[c] = (a[0] + a[64 * CPL]) + (a[2 * 64 * CPL] + a[3 * 64 * CPL]);
+    pb[C + c] = (a[4 * 64 * CPL] + a[5 * 64 * CPL]) + (a[6 * 64 * CPL] + a[7 * 64 * CPL]);
+  }
+}
+
+// out[j] += sum_b part[b][j] (j < W) in a fixed order: 64 columns x 16 row groups per workgroup (each thread's rows
+// b = grp, grp + 16, ... summed in 4 independent chains so their loads are in flight together), LDS combine in order.
+__global__ __launch_bounds__(1024) void ln_part_reduce_kernel(const float* __restrict__ part, int nb, int W,
+                                                              float* __restrict__ out0, float* __restrict__ out1, int C) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6, col = blockIdx.x * 64 + cl;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (col < W) {
+    int b = grp;
+    for (; b + 48 < nb; b += 64) {
+      s0 += part[(size_t)b * W + col];
+      s1 += part[(size_t)(b + 16) * W + col];
+      s2 += part[(size_t)(b + 32) * W + col];
+      s3 += part[(size_t)(b + 48) * W + col];
+    }
+    for (; b < nb; b += 16) s0 += part[(size_t)b * W + col];
+  }
+  red[grp][cl] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (grp == 0 && col < W) {
+    float v = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) v += red[g][cl];
+    if (col < C) {
+      if (out0) out0[col] += v;
+    } else if (out1) {
+      out1[col - C] += v;
+    }
+  }
+}
+
 // ConvT forward to a tiny channel count (the decoder's last layer: 1 or 3 image channels), on VALU:
 // a workgroup owns a 16x16 tile of small-grid pixels of one image (+1 halo) staged in LDS (NHWC,
 // 32 input channels per pass, CA / 32 passes); thread = one small-grid pixel (u, v), producing its 2x2
@@ -1177,11 +1278,43 @@ void launch_to_nhwc4(const void* x, bool u8, float* out, int N, int C, int HW, f
 
 bool launch_ln_bwd_flat(const float* dy, const float* z, const float* mean, const float* rstd, const float* gamma,
                         const float* beta, float* dz, float* dgamma, float* dbeta, int M, int C, int HW, int act,
-                        hipStream_t st) {
+                        float* part, int part_blocks, hipStream_t st) {
   if (C % 32 != 0 || C > 1024) return false;
+  const int lHW = ilog2(HW);
+  // image-tiled form (coalesced dy, deterministic partials) whenever the caller gave a partial buffer and the
+  // [HW][C + 1] tile fits the default 64 KB of LDS
+  const int N = M / HW;
+  const size_t shm = std::max((size_t)HW * (C + 1), (size_t)8 * 64 * ((C + 63) / 64)) * sizeof(float);
+  if (part != nullptr && part_blocks > 0 && N * HW == M && shm <= 64 * 1024) {
+    const int ipb = (N + part_blocks - 1) / part_blocks;
+    const int nb = (N + ipb - 1) / ipb;
+    dim3 grid(nb);
+#define SRL_LNBI(K)                                                                                                    \
+  do {                                                                                                                 \
+    if (act == srl::ACT_SILU)                                                                                          \
+      hipLaunchKernelGGL((ln_bwd_img_kernel<K, srl::ACT_SILU>), grid, dim3(256), shm, st, dy, z, mean, rstd, gamma,   \
+                         beta, dz, part, N, C, lHW, act, ipb);                                                         \
+    else                                                                                                               \
+      hipLaunchKernelGGL((ln_bwd_img_kernel<K, -1>), grid, dim3(256), shm, st, dy, z, mean, rstd, gamma, beta, dz,     \
+                         part, N, C, lHW, act, ipb);                                                                   \
+  } while (0)
+    switch ((C + 63) / 64) {
+      case 1: SRL_LNBI(1); break;
+      case 2: SRL_LNBI(2); break;
+      case 3: SRL_LNBI(3); break;
+      case 4: SRL_LNBI(4); break;
+      case 5: case 6: SRL_LNBI(6); break;
+      case 7: case 8: SRL_LNBI(8); break;
+      case 9: case 10: case 11: case 12: SRL_LNBI(12); break;
+      default: SRL_LNBI(16); break;
+    }
+#undef SRL_LNBI
+    if (dgamma || dbeta)
+      hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, part, nb, 2 * C, dgamma, dbeta, C);
+    return true;
+  }
   const int rpb = 64;
   dim3 grid((M + rpb - 1) / rpb);
-  const int lHW = ilog2(HW);
 #define SRL_LNBF(K)                                                                                                    \
   do {                                                                                                                 \
     if (act == srl::ACT_SILU)                                                                                          \

@@ -18,7 +18,7 @@ void launch_pack_down(const float*, float*, int, int, int, hipStream_t);
 void launch_pack_up(const float*, float*, int, int, int, hipStream_t);
 void launch_to_nhwc4(const void*, bool, float*, int, int, int, float, hipStream_t);
 bool launch_ln_bwd_flat(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
-                        float*, int, int, int, int, hipStream_t);
+                        float*, int, int, int, int, float*, int, hipStream_t);
 bool launch_up_small(const float*, const float*, const float*, float, float*, int, int, int, int, int, hipStream_t);
 void set_up_last_form(int);
 bool conv_channels_supported(int);
@@ -217,9 +217,12 @@ torch::Tensor conv_ln_bwd_flat(torch::Tensor dy, torch::Tensor z, torch::Tensor 
   const int64_t N = z.size(0), HW = z.size(1) * z.size(2), C = z.size(3);
   TORCH_CHECK(dy.numel() == z.numel() && mean.numel() == N * HW, "ln_bwd_flat: sizes");
   auto dz = torch::empty_like(z);
+  // per-workgroup dgamma / dbeta partials of the image-tiled kernel (one image per workgroup up to 1024), reduced in a fixed order
+  const int64_t nblk = std::min<int64_t>(N, 1024);
+  auto part = torch::empty({nblk, 2 * C}, z.options());
   bool ok = launch_ln_bwd_flat(dy.data_ptr<float>(), z.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                                optp(gamma), optp(beta), dz.data_ptr<float>(), optw(dgamma), optw(dbeta), N * HW, C, HW,
-                               (int)act, stream());
+                               (int)act, part.data_ptr<float>(), (int)nblk, stream());
   TORCH_CHECK(ok, "ln_bwd_flat: channel count must be a multiple of 32 up to 1024");
   return dz;
 }

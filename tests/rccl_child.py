@@ -136,8 +136,9 @@ def case_dv3_segmented_step():
     from sheeprl_prey_amd.parallel.runner import Runner
     from tests.test_dreamer_gpu import _build, _data
 
+    fake = {"ws": 1}  # what Runner.world_size reports: 1 while the reference trainer runs, 2 for the segmented one
+    Runner.world_size = property(lambda self: fake["ws"])
     ref = _build(graphs=True, seed=5)
-    Runner.world_size = property(lambda self: 2)
     real_gather = dist.all_gather_into_tensor
 
     def gather_2(out, inp, group=None, async_op=False):  # the 2nd "rank" holds the same values
@@ -145,17 +146,21 @@ def case_dv3_segmented_step():
         out[1:].copy_(out[:1].expand_as(out[1:]))
 
     dist.all_gather_into_tensor = gather_2
+    fake["ws"] = 2
     tr = _build(graphs=True, seed=5)
-    assert tr.graph_mode == "segmented", tr.graph_mode
+    assert tr.graph_mode == "segmented" and ref.graph_mode == "single", (tr.graph_mode, ref.graph_mode)
     data = _data(seed=9)
     la, lb = [], []
-    with _CollectiveLog() as log:
-        for i in range(5):
-            torch.manual_seed(100 + i)
-            la.append(float(ref.train_step(data)["Loss/world_model_loss"]))
-            torch.manual_seed(100 + i)
+    log = _CollectiveLog()
+    for i in range(5):
+        fake["ws"] = 1
+        torch.manual_seed(100 + i)
+        la.append(float(ref.train_step(data)["Loss/world_model_loss"]))
+        fake["ws"] = 2
+        torch.manual_seed(100 + i)
+        with log:
             out = tr.train_step(data)
-            lb.append(float(out["Loss/world_model_loss"]))
+        lb.append(float(out["Loss/world_model_loss"]))
     assert tr.seg.graphs is not None
     assert log.calls and not any(cap for _, cap in log.calls), log.calls
     assert abs(la[1] - lb[1]) / abs(la[1]) < 1e-3, (la, lb)

@@ -142,3 +142,30 @@ def test_stack_ineligible_falls_back():
     assert conv_ops.encoder_spec(enc.model, (64, 64), 3) is None
     out = enc({"rgb": torch.rand(2, 3, 64, 64, device=DEV)})
     assert out.shape == (2, enc.output_dim)
+
+
+@pytest.mark.parametrize("n,hw,c", [(1024, 16, 256), (66, 16, 768), (7, 4, 32)])
+def test_ln_bwd_flat_matches_autograd_and_is_deterministic(n, hw, c):
+    """The encoder's last LayerNorm+SiLU backward with dy in NCHW-flat order (the image-tiled kernel: coalesced dy
+    through an LDS transpose, dgamma / dbeta as fixed-order block partials) against autograd in fp64; two runs give
+    bitwise-equal dgamma / dbeta."""
+    C = ops._ext()
+    torch.manual_seed(n + c)
+    z = torch.randn(n, hw, c, device=DEV)
+    gamma, beta = torch.rand(c, device=DEV) + 0.5, torch.randn(c, device=DEV) * 0.2
+    dy = torch.randn(n, c * hw, device=DEV)
+    z64 = z.double().requires_grad_()
+    g64, b64 = gamma.double().requires_grad_(), beta.double().requires_grad_()
+    y = torch.nn.functional.silu(torch.nn.functional.layer_norm(z64, (c,), g64, b64, 1e-5))
+    y.permute(0, 2, 1).reshape(n, c * hw).mul(dy.double()).sum().backward()
+    mean = z.mean(-1).reshape(-1)
+    rstd = torch.rsqrt(z.var(-1, unbiased=False) + 1e-5).reshape(-1)
+    outs = []
+    for _ in range(2):
+        dg, db = torch.zeros(c, device=DEV), torch.zeros(c, device=DEV)
+        dz = C.conv_ln_bwd_flat(dy, z.view(n, 1, hw, c), mean, rstd, gamma, beta, ops._act_code("silu"), dg, db)
+        outs.append((dz, dg, db))
+    torch.testing.assert_close(outs[0][0].view(n, hw, c).double(), z64.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(outs[0][1].double(), g64.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(outs[0][2].double(), b64.grad, rtol=1e-4, atol=1e-3)
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
