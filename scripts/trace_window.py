@@ -32,8 +32,19 @@ def main(path, steps, top=40):
         a[1] += 1
     busy = sum(a[0] for a in agg.values())
     n = sum(a[1] for a in agg.values())
+    # union of the kernel intervals: wall - union = time with NO kernel running (launch gaps, host waits)
+    iv = sorted((int(r[key_s]), int(r[key_e])) for r in win)
+    union, cs, ce = 0, iv[0][0], iv[0][1]
+    for s_, e_ in iv[1:]:
+        if s_ > ce:
+            union += ce - cs
+            cs, ce = s_, e_
+        else:
+            ce = max(ce, e_)
+    union += ce - cs
     print(f"timed window: {steps} steps, wall {(t1 - t0) / 1e6:.2f} ms ({(t1 - t0) / 1e6 / steps:.2f} ms/step), "
-          f"kernel busy {busy / 1e6:.2f} ms ({busy / 1e6 / steps:.2f} ms/step), {n / steps:.0f} dispatches/step\n")
+          f"kernel busy {busy / 1e6:.2f} ms ({busy / 1e6 / steps:.2f} ms/step), {n / steps:.0f} dispatches/step, "
+          f"GPU occupied (union) {union / 1e6 / steps:.2f} ms/step, idle {(t1 - t0 - union) / 1e6 / steps:.2f} ms/step\n")
     cats = collections.defaultdict(lambda: [0, 0])
     for name, (d, c) in agg.items():
         cat = next((k for k, pat in CATS if any(p in name for p in pat)), "other")
