@@ -75,7 +75,6 @@ bool launch_actor_tail(const float* pre, long ldp, float* y, long ldy, const flo
                        float alpha, float* sample, long lds, int* idx, long ldi, int ioff, float* logits, int M, int N,
                        hipStream_t st);
 
-void set_prior_head_form(int f);
 bool launch_prior_head(const float* x, long ldx, const float* gamma, const float* beta, float eps, int act, const float* W,
                        const float* b, const float* uni, float alpha, float* sample, long lds, int* idx, long ldi, int ioff,
                        int M, int K, int N, hipStream_t st);
@@ -835,7 +834,6 @@ void register_ext(pybind11::module& m) {
         pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("eps"), pybind11::arg("act"), pybind11::arg("Wh"),
         pybind11::arg("bh"), pybind11::arg("uniform"), pybind11::arg("alpha"), pybind11::arg("sample"), pybind11::arg("idx"),
         pybind11::arg("ioff"), pybind11::arg("logits") = pybind11::none());
-  m.def("set_prior_head_form", [](int64_t f) { set_prior_head_form((int)f); });
   m.def("prior_head", &prior_head, pybind11::arg("x"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("eps"),
         pybind11::arg("act"), pybind11::arg("W"), pybind11::arg("b"), pybind11::arg("uniform"), pybind11::arg("alpha"),
         pybind11::arg("sample"), pybind11::arg("idx"), pybind11::arg("ioff"));

@@ -159,129 +159,8 @@ __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
   }
 }
 
-// K-split form: the per-workgroup chain (stage -> LayerNorm -> W stream -> sample) is latency-bound (profiles/
-// r5_prior_head_tiles.md: M = 256 runs as long as M = 1024), so each categorical's K range is split over two waves,
-// halving the serial W-stream batches per wave; the upper half parks its accumulators in LDS (over the dead row
-// tile) and the lower half adds them in a fixed order and samples.  Workgroup = 16 rows x 4 categoricals (8 waves),
-// grid (M / 16, N / 128): 512 workgroups at M = 1024, two per CU.
-template <int KV>
-__global__ void __launch_bounds__(NT) prior_head_ks_kernel(HP p) {
-  extern __shared__ float sm[];
-  const int lda = p.K + 4;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = lane & 15, g = lane >> 4;
-  const int cw = w & 3, kh = w >> 2;
-  const int r0 = blockIdx.x * 16;
-  const int nrow = min(16, p.M - r0);
-  const int G = p.N / CL;
-  const int gg = blockIdx.y * 4 + cw;
-  const int n0 = gg * CL;
-  constexpr int NCH = 4 * KV;          // 16-wide K chunks of the whole row
-  constexpr int NH = NCH / 2;          // this wave's chunks
-  constexpr int UKS = NH < UK ? NH : UK;
-  static_assert(NH % UKS == 0, "K chunks per batch");
-  const int kc0 = kh * NH;             // first chunk of this wave's half
-  const float* wr0 = p.W + (long)(n0 + i) * p.K + 4 * g + 16 * kc0;
-  const float* wr1 = wr0 + 16L * p.K;
-  f4 cb0[UKS], cb1[UKS];
-#pragma unroll
-  for (int q = 0; q < UKS; ++q) {
-    cb0[q] = *(const f4*)(wr0 + 16 * q);
-    cb1[q] = *(const f4*)(wr1 + 16 * q);
-  }
-  const float bb0 = p.b ? p.b[n0 + i] : 0.f, bb1 = p.b ? p.b[n0 + 16 + i] : 0.f;
-  const int c4 = p.K >> 2;
-  for (int e = threadIdx.x; e < 16 * c4; e += NT) {
-    const int r = e / c4, k = (e - r * c4) << 2;
-    *(f4*)(sm + r * lda + k) = r < nrow ? *(const f4*)(p.x + (long)(r0 + r) * p.ldx + k) : f4{0.f, 0.f, 0.f, 0.f};
-  }
-  __syncthreads();
-  for (int r = w; r < 16; r += NT / 64) {
-    float mu, rs;
-    scandev::wave_ln_act_row<KV>(sm + r * lda, p.K, p.eps, p.gamma, p.beta, p.act, mu, rs);
-  }
-  __syncthreads();
-  const float* arow = sm + i * lda + 4 * g + 16 * kc0;
-  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int c0 = 0; c0 < NH; c0 += UKS) {
-    f4 nb0[UKS], nb1[UKS];
-    const int cn = c0 + UKS < NH ? c0 + UKS : c0;
-#pragma unroll
-    for (int q = 0; q < UKS; ++q) {
-      nb0[q] = *(const f4*)(wr0 + 16 * (cn + q));
-      nb1[q] = *(const f4*)(wr1 + 16 * (cn + q));
-    }
-#pragma unroll
-    for (int q = 0; q < UKS; ++q) {
-      const f4 a = *(const f4*)(arow + 16 * (c0 + q));
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], cb0[q][0], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], cb1[q][0], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], cb0[q][1], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], cb1[q][1], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], cb0[q][2], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], cb1[q][2], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], cb0[q][3], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], cb1[q][3], acc1, 0, 0, 0);
-    }
-#pragma unroll
-    for (int q = 0; q < UKS; ++q) {
-      cb0[q] = nb0[q];
-      cb1[q] = nb1[q];
-    }
-  }
-  __syncthreads();  // every wave's A reads are done: the upper halves park their sums over the row tile
-  float* park = sm + cw * 512 + lane * 8;
-  if (kh == 1) {
-    *(f4*)park = acc0;
-    *(f4*)(park + 4) = acc1;
-  }
-  __syncthreads();
-  if (kh == 1) return;
-  acc0 += *(const f4*)park;
-  acc1 += *(const f4*)(park + 4);
-  const float inv = 1.f / CL;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = 4 * g + r;
-    const float l0 = acc0[r] + bb0, l1 = acc1[r] + bb1;
-    float m0 = l0, m1 = l1;
-    if (p.alpha > 0.f) {
-      const float mx = row16_max(fmaxf(l0, l1));
-      const float e0 = __expf(l0 - mx), e1 = __expf(l1 - mx);
-      const float s = row16_sum(e0 + e1);
-      float q0 = (1.f - p.alpha) * (e0 / s) + p.alpha * inv;
-      float q1 = (1.f - p.alpha) * (e1 / s) + p.alpha * inv;
-      q0 = fminf(fmaxf(q0, FEPS), 1.f - FEPS);
-      q1 = fminf(fmaxf(q1, FEPS), 1.f - FEPS);
-      m0 = logf(q0);
-      m1 = logf(q1);
-    }
-    const float mx2 = row16_max(fmaxf(m0, m1));
-    const float e0 = __expf(m0 - mx2), e1 = __expf(m1 - mx2);
-    const float s2 = row16_sum(e0 + e1);
-    const float cdf0 = row16_scan(e0 / s2);
-    const float cdf1 = row16_last(cdf0) + row16_scan(e1 / s2);
-    const float cmax = row16_last(cdf1);
-    const float u = row < nrow ? p.uni[(long)(r0 + row) * G + gg] : 0.f;
-    const float thr = u * cmax;
-    int pick = (int)row16_sum((cdf0 < thr ? 1.f : 0.f) + (cdf1 < thr ? 1.f : 0.f));
-    if (pick > CL - 1) pick = CL - 1;
-    if (row < nrow) {
-      float* srow = p.sample + (long)(r0 + row) * p.lds + n0;
-      srow[i] = i == pick ? 1.f : 0.f;
-      srow[16 + i] = 16 + i == pick ? 1.f : 0.f;
-      if (p.idx != nullptr && i == 0) p.idx[(long)(r0 + row) * p.ldi + gg] = p.ioff + n0 + pick;
-    }
-  }
-}
-
 }  // namespace phead
 }  // namespace srl
-
-// 0: 16 rows x 8 categoricals per workgroup (round 4), 1: the K-split form (prior_head_ks_kernel)
-static int g_prior_head_form = 0;
-void set_prior_head_form(int f) { g_prior_head_form = f; }
 
 // false: shape not covered (caller runs the three-launch path)
 bool launch_prior_head(const float* x, long ldx, const float* gamma, const float* beta, float eps, int act, const float* W,
@@ -300,21 +179,9 @@ bool launch_prior_head(const float* x, long ldx, const float* gamma, const float
                               16 * 516 * 4);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prior_head_kernel<16>), hipFuncAttributeMaxDynamicSharedMemorySize,
                               16 * 1028 * 4);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(prior_head_ks_kernel<16>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 16 * 1028 * 4);
     return true;
   }();
   (void)lds_set;
-  if (g_prior_head_form == 1 && N % 128 == 0) {
-    const dim3 g2((M + 15) / 16, N / 128);
-    if (K == 256)
-      hipLaunchKernelGGL(prior_head_ks_kernel<4>, g2, dim3(NT), shm, st, p);
-    else if (K == 512)
-      hipLaunchKernelGGL(prior_head_ks_kernel<8>, g2, dim3(NT), shm, st, p);
-    else
-      hipLaunchKernelGGL(prior_head_ks_kernel<16>, g2, dim3(NT), shm, st, p);
-    return true;
-  }
   if (K == 256)
     hipLaunchKernelGGL(prior_head_kernel<4>, grid, dim3(NT), shm, st, p);
   else if (K == 512)

@@ -22,24 +22,12 @@ def _ref_cdf(x, gamma, beta, eps, W, b, alpha, C=32):
     return p.cumsum(-1)
 
 
-@pytest.mark.parametrize("form", [0, 1])
 @pytest.mark.parametrize("M,K,N,strided,bias", [(1024, 512, 1024, True, True), (40, 512, 256, False, True),
                                                 (64, 1024, 512, True, False), (16, 256, 1024, False, True)])
-def test_prior_head_matches_fp64(M, K, N, strided, bias, form):
+def test_prior_head_matches_fp64(M, K, N, strided, bias):
     from sheeprl_prey_amd import ops
 
     C = ops._ext()
-    C.set_prior_head_form(form)  # 0: 16 rows x 8 categoricals; 1: the K-split form
-    try:
-        _check_prior_head(C, ops, M, K, N, strided, bias)
-    finally:
-        C.set_prior_head_form(DEFAULT_FORM)
-
-
-DEFAULT_FORM = 0
-
-
-def _check_prior_head(C, ops, M, K, N, strided, bias):
     torch.manual_seed(0)
     dev = "cuda"
     G = N // 32
