@@ -133,14 +133,19 @@ class EncoderConvFn(torch.autograd.Function):
         act, eps = meta["act"], meta["eps"]
         ws, gs, bs = params[:L], params[L:2 * L], params[2 * L:3 * L]
         q = C.conv_to_nhwc4(x.contiguous(), float(meta.get("scale", 1.0)))
+        # every weight pack of the step in ONE launch: the forward's DOWN forms and (with grad) the backward's UP forms
+        grad = any(ctx.needs_input_grad)
+        jobs = [(ws[i], 0, q.shape[3] if i == 0 else ws[i].shape[1]) for i in range(L)]
+        if grad:
+            jobs += [(ws[i], 1, ws[i].shape[1]) for i in range(1, L)]
+        packs = C.conv_pack_many([j[0] for j in jobs], [j[1] for j in jobs], [int(j[2]) for j in jobs])
         saved = []
         for i in range(L):
-            wp = C.conv_pack_down(ws[i], q.shape[3])
-            z, y, mean, rstd = C.conv_gemm(0, q, wp, ws[i].shape[0], 0, gs[i], bs[i], eps[i], act[i], i == L - 1,
+            z, y, mean, rstd = C.conv_gemm(0, q, packs[i], ws[i].shape[0], 0, gs[i], bs[i], eps[i], act[i], i == L - 1,
                                            None, None, None, None, None, None, 0.0, 0)
             saved += [q, z, mean, rstd]
             q = y
-        ctx.save_for_backward(*saved, *params)
+        ctx.save_for_backward(*saved, *params, *packs[L:])
         ctx.meta, ctx.L, ctx.in_ch = meta, L, x.shape[1]
         return q
 
@@ -150,7 +155,8 @@ class EncoderConvFn(torch.autograd.Function):
         L, meta = ctx.L, ctx.meta
         sv = ctx.saved_tensors
         acts = sv[:4 * L]
-        params = sv[4 * L:]
+        params = sv[4 * L:4 * L + 3 * L]
+        up_packs = sv[4 * L + 3 * L:]  # UP forms of layers 1..L-1 (made by the forward's one pack launch)
         ws, gs, bs = params[:L], params[L:2 * L], params[2 * L:3 * L]
         act = meta["act"]
         dgb = torch.zeros(2 * sum(int(g.numel()) for g in gs), device=dy.device, dtype=dy.dtype)
@@ -168,7 +174,7 @@ class EncoderConvFn(torch.autograd.Function):
             cin = ws[i].shape[1]
             dws[i] = C.conv_wgrad(dz, q, cin)
             if i > 0:
-                wp = C.conv_pack_up(ws[i], cin)
+                wp = up_packs[i - 1]
                 _, zp, mp, rp = acts[4 * (i - 1):4 * i]
                 dz = C.conv_gemm(1, dz, wp, cin, 1, gs[i - 1], bs[i - 1], 0.0, act[i - 1], False, zp, mp, rp,
                                  dgs[i - 1], dbs[i - 1], None, 0.0, 0)[0]
@@ -219,17 +225,23 @@ class DecoderConvFn(torch.autograd.Function):
         N = h.shape[0]
         c0 = ws[0].shape[0]
         p = h.reshape(N, c0, 4, 4).permute(0, 2, 3, 1).contiguous()
+        # every weight pack of the step in ONE launch: the forward's UP forms and (with grad) the backward's DOWN forms
+        # (the last layer's against the 4-channel NHWC image gradient)
+        grad = any(ctx.needs_input_grad)
+        jobs = [(ws[i], 1, ws[i].shape[1]) for i in range(L)]
+        if grad:
+            jobs += [(ws[i], 0, ws[i].shape[1]) for i in range(L)] + [(ws[L], 0, 4)]
+        packs = C.conv_pack_many([j[0] for j in jobs], [j[1] for j in jobs], [int(j[2]) for j in jobs])
         saved = []
         for i in range(L):
             cout = ws[i].shape[1]
-            wp = C.conv_pack_up(ws[i], cout)
-            z, y, mean, rstd = C.conv_gemm(1, p, wp, cout, 0, gs[i], bs[i], eps[i], act[i], False,
+            z, y, mean, rstd = C.conv_gemm(1, p, packs[i], cout, 0, gs[i], bs[i], eps[i], act[i], False,
                                            None, None, None, None, None, None, 0.0, 0)
             saved += [p, z, mean, rstd]
             p = y
         out = C.conv_up_small(p, ws[L], bias_last, float(meta["c0"]))
         saved.append(p)
-        ctx.save_for_backward(*saved, *params)
+        ctx.save_for_backward(*saved, *params, *packs[L:])
         ctx.meta, ctx.L = meta, L
         ctx.wparams = params[:L + 1]  # the conv weights (leaves) a deferred weight gradient is assigned to
         return out
@@ -240,7 +252,8 @@ class DecoderConvFn(torch.autograd.Function):
         L, meta = ctx.L, ctx.meta
         sv = ctx.saved_tensors
         acts, p_last = sv[:4 * L], sv[4 * L]
-        params = sv[4 * L + 1:]
+        params = sv[4 * L + 1:4 * L + 1 + 3 * L + 2]
+        down_packs = sv[4 * L + 1 + 3 * L + 2:]  # DOWN forms of layers 0..L-1, then the last layer's (the forward's pack launch)
         ws = params[:L + 1]
         gs, bs = params[L + 1:2 * L + 1], params[2 * L + 1:3 * L + 1]
         act = meta["act"]
@@ -259,7 +272,8 @@ class DecoderConvFn(torch.autograd.Function):
         # the weight gradients leave the critical path (data gradients -> scan backward -> encoder): inside the
         # world-model backward they are queued and run beside the scan backward (ops/sidestream.py)
         dws[L] = _wgrad(C, p_last, q, cout_last, ctx.wparams[L])
-        wp = C.conv_pack_down(ws[L], q.shape[3])
+        assert q.shape[3] == 4, q.shape
+        wp = down_packs[L]
         _, zp, mp, rp = acts[4 * (L - 1):4 * L]
         dz = C.conv_gemm(0, q, wp, ws[L].shape[0], 1, gs[L - 1], bs[L - 1], 0.0, act[L - 1], False, zp, mp, rp,
                          dgs[L - 1], dbs[L - 1], None, 0.0, 0)[0]
@@ -268,7 +282,7 @@ class DecoderConvFn(torch.autograd.Function):
             p = acts[4 * i]
             cout = ws[i].shape[1]
             dws[i] = _wgrad(C, p, dz, cout, ctx.wparams[i])
-            wp = C.conv_pack_down(ws[i], cout)
+            wp = down_packs[i]
             cin = ws[i].shape[0]
             if i > 0:
                 _, zp, mp, rp = acts[4 * (i - 1):4 * i]

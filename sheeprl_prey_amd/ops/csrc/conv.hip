@@ -757,6 +757,32 @@ __global__ void pack_up_kernel(const float* __restrict__ w, float* __restrict__ 
   out[idx] = b < B ? w[((size_t)a * B + b) * 16 + kh * 4 + kw] : 0.f;
 }
 
+// Every weight pack of a conv stack in ONE launch (the forward's and the backward's forms of every layer: they depend
+// only on the weights, which are fixed for the whole step): job j = blockIdx.y, kind 0 = DOWN, 1 = UP (as above).
+constexpr int MAX_PACK_JOBS = 16;
+struct PackJobs {
+  const float* w[MAX_PACK_JOBS];
+  float* out[MAX_PACK_JOBS];
+  int A[MAX_PACK_JOBS], B[MAX_PACK_JOBS], Bp[MAX_PACK_JOBS], kind[MAX_PACK_JOBS];
+};
+__global__ void multi_pack_kernel(PackJobs jobs) {
+  const int j = blockIdx.y;
+  const int A = jobs.A[j], B = jobs.B[j], Bp = jobs.Bp[j];
+  const float* __restrict__ w = jobs.w[j];
+  float* __restrict__ out = jobs.out[j];
+  const int tot = A * 16 * Bp;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += gridDim.x * blockDim.x) {
+    if (jobs.kind[j] == 0) {
+      const int a = idx / (16 * Bp), rem = idx - a * 16 * Bp, tap = rem / Bp, b = rem - tap * Bp;
+      out[idx] = b < B ? w[((size_t)a * B + b) * 16 + tap] : 0.f;
+    } else {
+      const int a = idx % A, t = (idx / A) & 3, b = (idx / (4 * A)) % Bp, cls = idx / (4 * A * Bp);
+      const int kh = 1 - (cls >> 1) + 2 * (t >> 1), kw = 1 - (cls & 1) + 2 * (t & 1);
+      out[idx] = b < B ? w[((size_t)a * B + b) * 16 + kh * 4 + kw] : 0.f;
+    }
+  }
+}
+
 // NCHW (uint8 or f32) with C <= 4 channels -> NHWC4 f32, scaled; channel C..3 = 0
 template <typename T>
 __global__ void to_nhwc4_kernel(const T* __restrict__ x, f4* __restrict__ out, int N, int C, int HW, float scale) {
@@ -1259,6 +1285,25 @@ bool launch_conv_wgrad(const float* P, const float* Q, float* slab, float* dw, i
 void launch_pack_down(const float* w, float* out, int A, int B, int Bp, hipStream_t st) {
   const int tot = A * 16 * Bp;
   hipLaunchKernelGGL(pack_down_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, w, out, A, B, Bp);
+}
+
+bool launch_multi_pack(const float* const* w, float* const* out, const int* A, const int* B, const int* Bp, const int* kind,
+                       int n, hipStream_t st) {
+  if (n < 1 || n > MAX_PACK_JOBS) return false;
+  PackJobs jobs{};
+  int mx = 0;
+  for (int j = 0; j < n; ++j) {
+    jobs.w[j] = w[j];
+    jobs.out[j] = out[j];
+    jobs.A[j] = A[j];
+    jobs.B[j] = B[j];
+    jobs.Bp[j] = Bp[j];
+    jobs.kind[j] = kind[j];
+    mx = std::max(mx, A[j] * 16 * Bp[j]);
+  }
+  const int bx = std::min((mx + 255) / 256, 512);
+  hipLaunchKernelGGL(multi_pack_kernel, dim3(bx, n), dim3(256), 0, st, jobs);
+  return true;
 }
 
 void launch_pack_up(const float* w, float* out, int A, int B, int Bp, hipStream_t st) {

@@ -16,6 +16,7 @@ void conv_wgrad_plan(int, int, int, int, int, int*, int*);
 bool launch_conv_wgrad(const float*, const float*, float*, float*, int, int, int, int, int, int, hipStream_t);
 void launch_pack_down(const float*, float*, int, int, int, hipStream_t);
 void launch_pack_up(const float*, float*, int, int, int, hipStream_t);
+bool launch_multi_pack(const float* const*, float* const*, const int*, const int*, const int*, const int*, int, hipStream_t);
 void launch_to_nhwc4(const void*, bool, float*, int, int, int, float, hipStream_t);
 bool launch_ln_bwd_flat(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
                         float*, int, int, int, int, float*, int, hipStream_t);
@@ -93,6 +94,34 @@ torch::Tensor conv_pack_up(torch::Tensor w, int64_t Bp) {
   auto out = torch::empty({4, Bp, 4, w.size(0)}, w.options());
   launch_pack_up(w.data_ptr<float>(), out.data_ptr<float>(), w.size(0), w.size(1), Bp, stream());
   return out;
+}
+
+// Every pack of a stack in one launch: jobs (w [A,B,4,4], kind 0 = DOWN / 1 = UP, Bp) -> the packed tensors, in order
+std::vector<torch::Tensor> conv_pack_many(std::vector<torch::Tensor> ws, std::vector<int64_t> kinds, std::vector<int64_t> bps) {
+  const size_t n = ws.size();
+  TORCH_CHECK(n >= 1 && n <= 16 && kinds.size() == n && bps.size() == n, "pack_many: 1..16 jobs");
+  std::vector<torch::Tensor> outs;
+  std::vector<const float*> wp(n);
+  std::vector<float*> op(n);
+  std::vector<int> A(n), B(n), Bp(n), K(n);
+  for (size_t j = 0; j < n; ++j) {
+    auto& w = ws[j];
+    chk(w, "w");
+    TORCH_CHECK(w.dim() == 4 && w.size(2) == 4 && w.size(3) == 4, "pack_many: weight must be [A,B,4,4]");
+    TORCH_CHECK(bps[j] >= w.size(1) && (kinds[j] == 1 || bps[j] % 4 == 0), "pack_many: bad padding");
+    TORCH_CHECK(kinds[j] == 0 || kinds[j] == 1, "pack_many: kind 0 (DOWN) or 1 (UP)");
+    outs.push_back(kinds[j] == 0 ? torch::empty({w.size(0), 16, bps[j]}, w.options())
+                                 : torch::empty({4, bps[j], 4, w.size(0)}, w.options()));
+    wp[j] = w.data_ptr<float>();
+    op[j] = outs.back().data_ptr<float>();
+    A[j] = (int)w.size(0);
+    B[j] = (int)w.size(1);
+    Bp[j] = (int)bps[j];
+    K[j] = (int)kinds[j];
+  }
+  TORCH_CHECK(launch_multi_pack(wp.data(), op.data(), A.data(), B.data(), Bp.data(), K.data(), (int)n, stream()),
+              "pack_many: launch");
+  return outs;
 }
 
 // DOWN: Q NHWC [N, 2SH, 2SW, Cb], Wp [Nc, 16, Cb] -> outputs on [N, SH, SW, Nc]
@@ -299,6 +328,7 @@ torch::Tensor conv_small_encoder(torch::Tensor x, std::vector<torch::Tensor> ws,
 void register_conv(pybind11::module& m) {
   m.def("conv_pack_down", &conv_pack_down);
   m.def("conv_pack_up", &conv_pack_up);
+  m.def("conv_pack_many", &conv_pack_many);
   m.def("conv_gemm", &conv_gemm);
   m.def("conv_wgrad", &conv_wgrad, pybind11::arg("P"), pybind11::arg("Q"), pybind11::arg("Cb"), pybind11::arg("out") = pybind11::none());
   m.def("conv_to_nhwc4", &conv_to_nhwc4);

@@ -72,7 +72,7 @@ __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
     const float* __restrict__ beta, float eps, int act, int ln, float* __restrict__ z_out, int ldz,
     float* __restrict__ y_out, int ldo, float* __restrict__ mean_out, float* __restrict__ rstd_out, int M, int N,
     int* __restrict__ err, const float* __restrict__ xa, int ldxa, int nA, const float* __restrict__ Wa) {
-  static_assert(WPR == 1 || WPR == 2, "onehot_gather_ln: 1 or 2 waves per row");
+  static_assert(WPR == 1 || WPR == 2 || WPR == 4, "onehot_gather_ln: 1, 2 or 4 waves per row");
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, part = wave % WPR;
   const int r = blockIdx.x * (4 / WPR) + wave / WPR;
@@ -139,6 +139,10 @@ __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
       if (lane == 0) red[0][wave] = s;
       __syncthreads();
       s = red[0][wave & ~1] + red[0][wave | 1];
+    } else if (WPR == 4) {
+      if (lane == 0) red[0][wave] = s;
+      __syncthreads();
+      s = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
     }
     mu = s / N;
     float q = 0.f;
@@ -154,6 +158,10 @@ __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
       if (lane == 0) red[1][wave] = q;
       __syncthreads();
       q = red[1][wave & ~1] + red[1][wave | 1];
+    } else if (WPR == 4) {
+      if (lane == 0) red[1][wave] = q;
+      __syncthreads();
+      q = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
     }
     rs = rsqrtf(q / N + eps);
     if (live && lane == 0 && part == 0) {
@@ -183,6 +191,11 @@ bool launch_onehot_gather_ln(const float* Y, int ldy, const int* idx, int ldi, i
   const dim3 block(256);
   if (nv == 2 && M <= 4096) {  // latency-bound rollout sizes: two waves per 512-wide row
     hipLaunchKernelGGL((srl::onehot::onehot_gather_ln_kernel<1, 2>), dim3((M + 1) / 2), block, 0, st, Y, ldy, idx, ldi, G, off,
+                       T, K, bias, gamma, beta, eps, act, ln, z_out, ldz, y_out, ldo, mean, rstd, M, N, err, xa, ldxa, nA, Wa);
+    return true;
+  }
+  if (nv == 4 && M <= 16384) {  // 1024-wide rows (exp=dreamer_v3_prey, dense 1024): four waves per row, 2 L2 round trips
+    hipLaunchKernelGGL((srl::onehot::onehot_gather_ln_kernel<1, 4>), dim3(M), block, 0, st, Y, ldy, idx, ldi, G, off,
                        T, K, bias, gamma, beta, eps, act, ln, z_out, ldz, y_out, ldo, mean, rstd, M, N, err, xa, ldxa, nA, Wa);
     return true;
   }

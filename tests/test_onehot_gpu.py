@@ -12,7 +12,7 @@ def _onehot(M, G, C, gen):
     return F.one_hot(k, C).float().view(M, G * C), k
 
 
-@pytest.mark.parametrize("N,Kd,ln,bias", [(512, 512, True, False), (4096, 512, False, True), (1024, 96, True, True),
+@pytest.mark.parametrize("N,Kd,ln,bias", [(512, 512, True, False), (4096, 512, False, True), (1024, 96, True, True), (1000, 64, True, True),
                                           (256, 0, True, False)])
 def test_gather_first_layer_matches_dense(N, Kd, ln, bias):
     from sheeprl_prey_amd.ops import onehot as oh
