@@ -28,6 +28,7 @@ actor forward).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -126,6 +127,11 @@ class ContinuousRollout:
         else:
             self.tr_pre = post.new_empty(horizon, M, hid)
         self.tr_y = post.new_empty(horizon, M, hid)
+        # transition LayerNorm + act + output Linear + unimix sample as ONE launch (prior_head.hip) that also writes what
+        # the backward reads (the pre-unimix logits, the LayerNorm row statistics): 3 launches -> 1 per step
+        self.phead = (self.merge and getattr(rssm, "_prior_head_ok", True) and self.disc == 32 and S % 256 == 0
+                      and hid in (256, 512, 1024) and isinstance(self.tr2, nn.Linear)
+                      and os.environ.get("SRL_CONT_PHEAD", "1") != "0")
         self.tr_mean = post.new_empty(horizon, M)
         self.tr_rstd = post.new_empty(horizon, M)
         self.logits = post.new_empty(horizon, M, S)
@@ -186,6 +192,12 @@ class ContinuousRollout:
                 C.ln_gru_into(gx, buf[t, :, S:S + Hd], gln.weight, gln.bias, float(gln.eps), buf[t + 1, :, S:S + Hd],
                               mean=self.g_mean[t], rstd=self.g_rstd[t], x2=self.hm[t][:, hidm + Na:], write_sum=True)
                 self._hmm(buf[t + 1, :, S:S + Hd], self.hm[t + 1])
+                if self.phead and C.prior_head(self.hm[t + 1][:, :hid], tln.weight, tln.bias, float(tln.eps),
+                                               ops._act_code(tln.act), self.tr2.weight, self.tr2.bias, self.u_prior[t],
+                                               float(self.rssm.unimix), buf[t + 1, :, :S], self.IDX[t + 1], 0,
+                                               logits_out=self.logits[t], mean_out=self.tr_mean[t],
+                                               rstd_out=self.tr_rstd[t]):
+                    continue
                 C.ln_act_fwd_into(self.hm[t + 1], self.hm.shape[-1], self.tr_y[t], hid, tln.weight, tln.bias,
                                   self.tr_mean[t], self.tr_rstd[t], M, hid, 1, float(tln.eps), ops._act_code(tln.act))
             else:

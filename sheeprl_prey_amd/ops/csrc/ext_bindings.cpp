@@ -77,7 +77,8 @@ bool launch_actor_tail(const float* pre, long ldp, float* y, long ldy, const flo
 
 bool launch_prior_head(const float* x, long ldx, const float* gamma, const float* beta, float eps, int act, const float* W,
                        const float* b, const float* uni, float alpha, float* sample, long lds, int* idx, long ldi, int ioff,
-                       int M, int K, int N, hipStream_t st);
+                       int M, int K, int N, hipStream_t st, float* logits = nullptr, long ldl = 0,
+                       float* mean_out = nullptr, float* rstd_out = nullptr);
 
 bool launch_seq_sample(const void* const* src, void* const* dst, const long* row_bytes, int nk, int n_envs, long cap, int B,
                        int L, long n1, long start2, long n2, unsigned long long seed, unsigned long long counter,
@@ -734,7 +735,8 @@ bool actor_tail(torch::Tensor pre, torch::Tensor y, c10::optional<torch::Tensor>
 // uniform [M * N / 32].  false: shape not covered.
 bool prior_head(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, double eps, int64_t act, torch::Tensor W,
                 c10::optional<torch::Tensor> b, torch::Tensor uniform, double alpha, torch::Tensor sample,
-                c10::optional<torch::Tensor> idx, int64_t ioff) {
+                c10::optional<torch::Tensor> idx, int64_t ioff, c10::optional<torch::Tensor> logits_out,
+                c10::optional<torch::Tensor> mean_out, c10::optional<torch::Tensor> rstd_out) {
   const int64_t M = x.size(0), K = x.size(1), N = W.size(0);
   rowview(x, "x", M, K, torch::kFloat32);
   rowview(sample, "sample", M, N, torch::kFloat32);
@@ -752,9 +754,23 @@ bool prior_head(torch::Tensor x, torch::Tensor gamma, torch::Tensor beta, double
     ip = idx->data_ptr<int>();
     ldi = idx->stride(0);
   }
+  float* lp = nullptr;
+  int64_t ldl = 0;
+  if (logits_out.has_value() && logits_out->defined()) {
+    rowview(*logits_out, "logits_out", M, N, torch::kFloat32);
+    lp = logits_out->data_ptr<float>();
+    ldl = logits_out->stride(0);
+  }
+  float* mp = nullptr;
+  float* rp = nullptr;
+  if (mean_out.has_value() && mean_out->defined()) {
+    TORCH_CHECK(rstd_out.has_value() && rstd_out->defined(), "prior_head: mean_out needs rstd_out");
+    mp = const_cast<float*>(optf(*mean_out, "mean_out", M));
+    rp = const_cast<float*>(optf(*rstd_out, "rstd_out", M));
+  }
   return launch_prior_head(x.data_ptr<float>(), x.stride(0), gp, bp, (float)eps, (int)act, W.data_ptr<float>(), hp, up,
                            (float)alpha, sample.data_ptr<float>(), sample.stride(0), ip, ldi, (int)ioff, (int)M, (int)K,
-                           (int)N, stream());
+                           (int)N, stream(), lp, ldl, mp, rp);
 }
 
 // Fused replay sequence sample into preallocated [L, B, ...] outputs (gather.hip seq_sample_kernel): srcs are
@@ -836,7 +852,8 @@ void register_ext(pybind11::module& m) {
         pybind11::arg("ioff"), pybind11::arg("logits") = pybind11::none());
   m.def("prior_head", &prior_head, pybind11::arg("x"), pybind11::arg("gamma"), pybind11::arg("beta"), pybind11::arg("eps"),
         pybind11::arg("act"), pybind11::arg("W"), pybind11::arg("b"), pybind11::arg("uniform"), pybind11::arg("alpha"),
-        pybind11::arg("sample"), pybind11::arg("idx"), pybind11::arg("ioff"));
+        pybind11::arg("sample"), pybind11::arg("idx"), pybind11::arg("ioff"), pybind11::arg("logits_out") = pybind11::none(),
+        pybind11::arg("mean_out") = pybind11::none(), pybind11::arg("rstd_out") = pybind11::none());
   m.def("wgrad", &wgrad, pybind11::arg("dz"), pybind11::arg("x"), pybind11::arg("idx"), pybind11::arg("G"), pybind11::arg("C"),
         pybind11::arg("off"), pybind11::arg("dW"), pybind11::arg("db"), pybind11::arg("accumulate") = false);
   m.def("onehot_gather_ln", &onehot_gather_ln, pybind11::arg("Y"), pybind11::arg("idx"), pybind11::arg("G"), pybind11::arg("off"),

@@ -45,6 +45,11 @@ struct HP {
   long ldi;
   int ioff, M, K, N, act;
   float eps, alpha;
+  // optional saved forward state for a backward through the head (continuous imagination, imagine_cont.py):
+  float* logits;     // [M, >= N] row-strided pre-unimix logits, or null
+  long ldl;
+  float* mean_out;   // [M] LayerNorm row statistics of x, or null
+  float* rstd_out;
 };
 
 // 16-lane (DPP row) reductions / scan: no LDS-crossbar shuffles (common.h row16_*); the row's last lane by readlanes
@@ -85,6 +90,10 @@ __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
   for (int r = w; r < 16; r += NT / 64) {
     float mu, rs;
     scandev::wave_ln_act_row<KV>(sm + r * lda, p.K, p.eps, p.gamma, p.beta, p.act, mu, rs);
+    if (p.mean_out != nullptr && blockIdx.y == 0 && lane == 0 && r < nrow) {
+      p.mean_out[r0 + r] = mu;
+      p.rstd_out[r0 + r] = rs;
+    }
   }
   __syncthreads();
   // logits tile [16 rows x 32 classes] of this wave's categorical.  K = 64 * KV exactly (compile-time trip count,
@@ -128,6 +137,11 @@ __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
   for (int r = 0; r < 4; ++r) {
     const int row = 4 * g + r;
     const float l0 = acc0[r] + bb0, l1 = acc1[r] + bb1;
+    if (p.logits != nullptr && row < nrow) {
+      float* lrow = p.logits + (long)(r0 + row) * p.ldl + n0;
+      lrow[i] = l0;
+      lrow[16 + i] = l1;
+    }
     float m0 = l0, m1 = l1;
     if (p.alpha > 0.f) {
       const float mx = row16_max(fmaxf(l0, l1));
@@ -165,11 +179,12 @@ __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
 // false: shape not covered (caller runs the three-launch path)
 bool launch_prior_head(const float* x, long ldx, const float* gamma, const float* beta, float eps, int act, const float* W,
                        const float* b, const float* uni, float alpha, float* sample, long lds, int* idx, long ldi, int ioff,
-                       int M, int K, int N, hipStream_t st) {
+                       int M, int K, int N, hipStream_t st, float* logits, long ldl, float* mean_out, float* rstd_out) {
   using namespace srl::phead;
   if (M <= 0 || (K != 256 && K != 512 && K != 1024) || N % 256 != 0 || ldx % 4 != 0 || !gamma || !beta) return false;
   if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(W)) & 15) return false;
-  HP p{x, ldx, gamma, beta, W, b, uni, sample, lds, idx, ldi, ioff, M, K, N, act, eps, alpha};
+  if ((mean_out == nullptr) != (rstd_out == nullptr)) return false;
+  HP p{x, ldx, gamma, beta, W, b, uni, sample, lds, idx, ldi, ioff, M, K, N, act, eps, alpha, logits, ldl, mean_out, rstd_out};
   const dim3 grid((M + 15) / 16, N / 256);
   const size_t shm = (size_t)16 * (K + 4) * sizeof(float);
   static const bool lds_set = [] {  // K = 1024 needs 65.8 KB of the 160 KB

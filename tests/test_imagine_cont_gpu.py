@@ -6,7 +6,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _models(seed=0, horizon=5):
+def _models(seed=0, horizon=5, tr_hidden=64):
     from sheeprl_prey_amd.algos.dreamer_v3.agent import build_models
     from sheeprl_prey_amd.config.compose import compose
     from sheeprl_prey_amd.envs import spaces
@@ -17,7 +17,7 @@ def _models(seed=0, horizon=5):
         "exp=dreamer_v3", "env=dummy", "cnn_keys.encoder=[rgb]", "cnn_keys.decoder=[rgb]", "algo.dense_units=64",
         "algo.mlp_layers=2", "algo.world_model.encoder.cnn_channels_multiplier=8",
         "algo.world_model.recurrent_model.recurrent_state_size=64", "algo.world_model.representation_model.hidden_size=64",
-        "algo.world_model.transition_model.hidden_size=64", f"algo.horizon={horizon}", "fabric.accelerator=cuda",
+        f"algo.world_model.transition_model.hidden_size={tr_hidden}", f"algo.horizon={horizon}", "fabric.accelerator=cuda",
     ]))
     torch.manual_seed(seed)
     runner = Runner(**dict(cfg.fabric))
@@ -52,10 +52,11 @@ def _eager(rssm, actor, post, h, roll):
     return torch.stack(trajs), torch.stack(acts), torch.stack(pres)
 
 
-def test_continuous_rollout_matches_eager_forward_and_backward():
+@pytest.mark.parametrize("tr_hidden", [64, 256])  # 256: the transition head runs as the one-launch prior head
+def test_continuous_rollout_matches_eager_forward_and_backward(tr_hidden):
     from sheeprl_prey_amd.algos.dreamer_v3 import imagine_cont
 
-    wm, actor = _models()
+    wm, actor = _models(tr_hidden=tr_hidden)
     rssm = wm.rssm
     assert imagine_cont.supported(rssm, actor)
     for p in wm.parameters():
@@ -65,6 +66,7 @@ def test_continuous_rollout_matches_eager_forward_and_backward():
     post = torch.nn.functional.one_hot(torch.randint(0, 32, (M, 32), device="cuda", generator=g), 32).float().view(M, S)
     h = torch.randn(M, Hd, device="cuda", generator=g)
     traj, acts, pre, roll = imagine_cont.imagine_continuous(rssm, actor, post, h, 5)
+    assert roll.phead == (tr_hidden == 256)
     e_traj, e_acts, e_pre = _eager(rssm, actor, post, h, roll)
     torch.cuda.synchronize()
     # the one-hot priors sampled from the same uniforms: identical hot columns every step
