@@ -681,15 +681,78 @@ class Actor(nn.Module):
 
     def sample_actions(self, state: Tensor, is_training: bool = True) -> Tuple[Tensor, ...]:
         """The actions of ``forward`` without building the distributions (discrete: their logits normalisation
-        is ~10 kernels per env step the player never reads)."""
+        is ~10 kernels per env step the player never reads; truncated-normal: the last LayerNorm, the head Linear and
+        the draw are ONE kernel instead of ~16 small ones)."""
         if self.is_continuous:
-            return self.forward(state, is_training)[0]
+            fast = self._tn_sample(state) if is_training else None
+            return (fast,) if fast is not None else self.forward(state, is_training)[0]
+        fast = self._tail_sample(state) if is_training else None
+        if fast is not None:
+            return (fast,)
         out = self.model(state)
         return tuple(ops.unimix_sample(head(out), head.out_features, self._unimix, sample=is_training)[1]
                      for head in self.mlp_heads)
 
     def _uniform_mix(self, logits: Tensor) -> Tensor:
         return ops.reference.unimix_logits(logits, logits.shape[-1], self._unimix)
+
+    @torch.no_grad()
+    def _tail_sample(self, state: Tensor) -> Optional[Tensor]:
+        """One-hot action draw of the player (one discrete head, no grad): the trunk up to its last pre-activation,
+        then its LayerNorm + act, the head Linear and the unimix draw in one launch (``actor_tail.hip``, the
+        imagination rollout's kernel); None when it does not apply."""
+        from sheeprl_prey_amd.ops.mlp_trunk import trunk_layers
+
+        if (len(self.mlp_heads) != 1 or not state.is_cuda or not ops.fused_enabled() or getattr(self, "_srl_autocast", False)
+                or not RSSM._actor_tail_ok):
+            return None
+        layers = trunk_layers(self.model)
+        if layers is None:
+            return None
+        x = state.reshape(-1, state.shape[-1])
+        for lin, ln in layers[:-1]:
+            x = ln(lin(x))
+        lin, ln = layers[-1]
+        z = lin(x)
+        head = self.mlp_heads[0]
+        M, N, A = z.shape[0], z.shape[1], head.out_features
+        u = torch.rand(M, device=z.device)
+        y, mean, rstd, out = z.new_empty(M, N), z.new_empty(M), z.new_empty(M), z.new_empty(M, A)
+        if not ops._ext().actor_tail(z, y, ln.weight, ln.bias, mean, rstd, float(ln.eps), ops._act_code(ln.act), head.weight,
+                                     head.bias, u, float(self._unimix), out, None, 0, None):
+            return None
+        return out.view(*state.shape[:-1], A)
+
+    @torch.no_grad()
+    def _tn_sample(self, state: Tensor) -> Optional[Tensor]:
+        """Truncated-normal action draw of the player (no grad): the trunk up to its last pre-activation, then its
+        LayerNorm + act, the head Linear and the inverse-CDF draw in one launch (``truncnorm.hip``
+        head_linear_sample_fwd, the imagination rollout's kernel); None when it does not apply."""
+        from sheeprl_prey_amd.ops.mlp_trunk import trunk_layers
+
+        if (self.distribution != "trunc_normal" or len(self.mlp_heads) != 1 or not state.is_cuda
+                or not ops.fused_enabled() or getattr(self, "_srl_autocast", False)):
+            return None
+        layers = trunk_layers(self.model)
+        if layers is None:
+            return None
+        x = state.reshape(-1, state.shape[-1])
+        for lin, ln in layers[:-1]:
+            x = ln(lin(x))
+        lin, ln = layers[-1]
+        z = lin(x)
+        head = self.mlp_heads[0]
+        M, K, A = z.shape[0], z.shape[1], head.out_features // 2
+        eps = float(torch.finfo(torch.float32).eps)
+        u = torch.empty(M, A, device=z.device).uniform_(eps, 1.0 - eps)
+        pre, loc, scale = z.new_empty(M, 2 * A), z.new_empty(M, A), z.new_empty(M, A)
+        out, y, mean, rstd = z.new_empty(M, A), z.new_empty(M, K), z.new_empty(M), z.new_empty(M)
+        if not ops._ext().tn_head_linear_sample_fwd(z, head.weight, head.bias, u, float(self.init_std), float(self.min_std),
+                                                     -1.0, 1.0, pre, loc, scale, out, ln_w=ln.weight, ln_b=ln.bias,
+                                                     ln_eps=float(ln.eps), act=ops._act_code(ln.act), y_out=y, mean=mean,
+                                                     rstd=rstd):
+            return None
+        return out.view(*state.shape[:-1], A)
 
 
 class MinedojoActor(Actor):

@@ -40,3 +40,24 @@ def test_actor_tail_matches_unfused(M, N, A, sample):
     assert torch.equal(idx[:, 1:], ridx)
     assert torch.all(out[:, A:] == 0)
     assert torch.equal(out[:, :A].sum(1), torch.ones(M, device="cuda"))
+
+
+def test_player_tail_draw_matches_eager():
+    """The discrete player's fused draw (Actor._tail_sample: last LayerNorm + head + unimix sample in one launch)
+    against the eager trunk + head + unimix sampler fed the same uniforms."""
+    from sheeprl_prey_amd import ops
+    from tests.test_dreamer_gpu import _build
+
+    actor = _build(graphs=False).actor
+    M = 9
+    state = torch.randn(1, M, actor.model.model[0].in_features, device="cuda")
+    torch.manual_seed(3)
+    a = actor._tail_sample(state)
+    assert a is not None and a.shape == (1, M, 5)
+    torch.manual_seed(3)
+    u = torch.rand(M, device="cuda")
+    with torch.no_grad():
+        logits = actor.mlp_heads[0](actor.model(state.view(M, -1)))
+        ref = ops.unimix_sample(logits, 5, actor._unimix, sample=True, uniform=u)[1]
+    assert torch.equal(a.view(M, 5).sum(-1), torch.ones(M, device="cuda"))
+    assert torch.equal(a.view(M, 5), ref)

@@ -135,3 +135,24 @@ def test_dv3_continuous_step_fast_rollout_runs():
             assert float(out["Loss/policy_loss"]) == float(out["Loss/policy_loss"])
     assert tr.graphed.graph is not None
     assert losses[-1] < losses[0], losses
+
+
+def test_player_truncnorm_draw_matches_eager():
+    """The continuous player's fused draw (Actor._tn_sample: last LayerNorm + head + inverse-CDF sample in one launch)
+    against the eager head + TruncatedNormal with the same uniforms."""
+    from sheeprl_prey_amd import ops
+
+    wm, actor = _models(seed=2)
+    M = 7
+    state = torch.randn(1, M, actor.model.model[0].in_features, device="cuda")
+    torch.manual_seed(5)
+    a = actor._tn_sample(state)
+    assert a is not None and a.shape == (1, M, 3)
+    torch.manual_seed(5)
+    eps = float(torch.finfo(torch.float32).eps)
+    u = torch.empty(M, 3, device="cuda").uniform_(eps, 1.0 - eps)
+    with torch.no_grad():
+        d = actor._continuous_dist(actor.mlp_heads[0](actor.model(state.view(M, -1)))).base_dist
+        ref = ops.truncnorm_rsample(d.loc, d.scale, d.loc.new_full((), -1.0), d.loc.new_full((), 1.0), u)
+    torch.testing.assert_close(a.view(M, 3), ref, rtol=1e-4, atol=1e-5)
+    assert float(a.abs().max()) <= 1.0
