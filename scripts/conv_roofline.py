@@ -18,19 +18,21 @@ import sys
 
 PEAK_TF = 157.3
 N = 1024
+MULT = 32  # --mult: the channel multiplier (32 = Atari-100k, 96 = XL)
 
 
 def layer_flops():
     """FLOPs of every conv GEMM of the stack (k4 s2 p1; 2 * M * N * K)."""
     out = {}
-    enc = [(3, 32, 32), (32, 64, 16), (64, 128, 8), (128, 256, 4)]  # (cin, cout, output side)
+    m = MULT
+    enc = [(3, m, 32), (m, 2 * m, 16), (2 * m, 4 * m, 8), (4 * m, 8 * m, 4)]  # (cin, cout, output side)
     for i, (ci, co, s) in enumerate(enc):
         cip = max(ci, 4)
         out[f"E{i + 1} fwd"] = 2 * N * s * s * co * cip * 16
         out[f"E{i + 1} wgrad"] = out[f"E{i + 1} fwd"]
         if i > 0:
             out[f"E{i + 1} dgrad"] = 2 * N * s * s * co * ci * 16
-    dec = [(256, 128, 8), (128, 64, 16), (64, 32, 32), (32, 3, 64)]
+    dec = [(8 * m, 4 * m, 8), (4 * m, 2 * m, 16), (2 * m, m, 32), (m, 3, 64)]
     for i, (ci, co, s) in enumerate(dec):
         out[f"D{i + 1} fwd"] = 2 * N * s * s * co * ci * 4  # UP: K = 4 taps x Ca per parity class
         out[f"D{i + 1} wgrad"] = out[f"D{i + 1} fwd"]
@@ -45,8 +47,8 @@ def run(iters: int) -> None:
     from sheeprl_prey_amd.algos.dreamer_v3.agent import CNNDecoder, CNNEncoder
 
     torch.manual_seed(0)
-    enc = CNNEncoder(["rgb"], [3], (64, 64), 32).cuda()
-    dec = CNNDecoder(["rgb"], [3], 32, 1536, enc.output_dim, (64, 64)).cuda()
+    enc = CNNEncoder(["rgb"], [3], (64, 64), MULT).cuda()
+    dec = CNNDecoder(["rgb"], [3], MULT, 1536, enc.output_dim, (64, 64)).cuda()
     x = torch.randint(0, 255, (N, 3, 64, 64), dtype=torch.uint8, device="cuda")
     lat = torch.randn(N, 1536, device="cuda", requires_grad=True)
     g_e = torch.randn(N, enc.output_dim, device="cuda")
@@ -124,7 +126,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--csv", default=None)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--mult", type=int, default=32)
     a = ap.parse_args()
+    MULT = a.mult
     if a.csv:
         report(a.csv, a.iters)
     else:
