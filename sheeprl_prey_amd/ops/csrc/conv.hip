@@ -1301,7 +1301,9 @@ bool launch_multi_pack(const float* const* w, float* const* out, const int* A, c
     jobs.kind[j] = kind[j];
     mx = std::max(mx, A[j] * 16 * Bp[j]);
   }
-  const int bx = std::min((mx + 255) / 256, 512);
+  // one thread per packed element of the largest job (the XL weights reach 4.7 M elements: a capped grid walking them
+  // in a stride loop measured 140 us per launch), capped only at 16384 workgroups per job
+  const int bx = std::min((mx + 255) / 256, 16384);
   hipLaunchKernelGGL(multi_pack_kernel, dim3(bx, n), dim3(256), 0, st, jobs);
   return true;
 }
