@@ -36,7 +36,8 @@ def quiesce_for_capture(settle_s: float = 0.25) -> None:
 
     import torch.distributed as dist
 
-    torch.cuda.synchronize()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     if dist.is_available() and dist.is_initialized():
         time.sleep(settle_s)
 

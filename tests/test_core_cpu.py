@@ -457,3 +457,41 @@ def test_reduce_workspace_is_gpu_only():
     from sheeprl_prey_amd import ops
 
     assert ops.init_reduce_workspace("cpu") is False
+
+
+def test_heartbeat_startup_grace_scales_with_the_step_timeout():
+    """The start-up grace defaults to a multiple of the step timeout (a short step timeout keeps a short start-up
+    limit); an explicit grace wins."""
+    from sheeprl_prey_amd.parallel.collectives import Heartbeat
+
+    h = Heartbeat(0.0)  # disabled: no thread, the limits are still computed
+    assert h.startup_grace_s == 0.0
+    h = Heartbeat(30.0)
+    try:
+        assert h.startup_grace_s == 120.0
+    finally:
+        h.stop()
+    h = Heartbeat(30.0, startup_grace_s=10.0)
+    try:
+        assert h.startup_grace_s == 10.0
+    finally:
+        h.stop()
+
+
+def test_phased_step_eager_replay_api():
+    """On the CPU a PhasedStep runs eagerly: no captured inputs to draw into, replay() is a no-op, the phases and
+    collectives run in order."""
+    from sheeprl_prey_amd.parallel.graphs import PhasedStep, quiesce_for_capture
+
+    class R:
+        device = torch.device("cpu")
+        world_size = 1
+
+    order = []
+    ps = PhasedStep(R(), [lambda d: order.append("a"), lambda d: order.append("b") or {"x": d["x"] + 1}],
+                    [lambda dry=False: order.append("c")])
+    assert ps.mode == "eager" and not ps.enabled
+    assert ps.captured_inputs() is None and ps.replay() is None
+    out = ps({"x": torch.zeros(2)})
+    assert order == ["a", "c", "b"] and torch.equal(out["x"], torch.ones(2))
+    quiesce_for_capture()  # no device, no process group: returns at once
