@@ -24,6 +24,7 @@
 #include "common.h"
 #include "conv.h"
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 
@@ -1077,9 +1078,27 @@ static void dispatch_epi(const LA& la, const Dense<BN, 64 * WM * WN>& lb, const 
 //   512 / 768   64 x C, 1 x 8 waves (TM 2, TN 2 / 3; 512 threads keep the B-tile prefetch at 8 / 12
 //               float4 per thread; LDS 83 / 120 KB)
 //   1024        32 x C, 1 x 8 waves (TM 1, TN 4: no register spill; LDS 152 KB)
+// 32-channel tile variants (SRL_CONV_T32, A/B): 0 = 256 x 32 on 4 waves, 1 = 128 x 32 on 2 waves, 2 = 256 x 32 on
+// 2 waves (TM 4: each B fragment feeds four 32-row MFMA tiles), 3 = 128 x 32 on 4 waves (TM 1)
+static int conv_t32() {
+  static const int v = [] {
+    const char* e = getenv("SRL_CONV_T32");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+#define CONV_T32(X, ...)                                                                           \
+  do {                                                                                              \
+    switch (conv_t32()) {                                                                           \
+      case 1: X<128, 32, 2, 1>(__VA_ARGS__); break;                                                 \
+      case 2: X<256, 32, 2, 1>(__VA_ARGS__); break;                                                 \
+      case 3: X<128, 32, 4, 1>(__VA_ARGS__); break;                                                 \
+      default: X<256, 32, 4, 1>(__VA_ARGS__); break;                                                \
+    }                                                                                               \
+  } while (0)
 #define CONV_TILES(X, ...)                                                                         \
   switch (Nc) {                                                                                     \
-    case 32: X<256, 32, 4, 1>(__VA_ARGS__); return true;                                            \
+    case 32: CONV_T32(X, __VA_ARGS__); return true;                                                 \
     case 64: X<128, 64, 2, 2>(__VA_ARGS__); return true;                                            \
     case 96: X<128, 96, 4, 1>(__VA_ARGS__); return true;                                            \
     case 128: X<128, 128, 2, 2>(__VA_ARGS__); return true;                                          \
