@@ -1078,18 +1078,20 @@ static void dispatch_epi(const LA& la, const Dense<BN, 64 * WM * WN>& lb, const 
 //   512 / 768   64 x C, 1 x 8 waves (TM 2, TN 2 / 3; 512 threads keep the B-tile prefetch at 8 / 12
 //               float4 per thread; LDS 83 / 120 KB)
 //   1024        32 x C, 1 x 8 waves (TM 1, TN 4: no register spill; LDS 152 KB)
-// 32-channel tile variants (SRL_CONV_T32, A/B): 0 = 256 x 32 on 4 waves, 1 = 128 x 32 on 2 waves, 2 = 256 x 32 on
-// 2 waves (TM 4: each B fragment feeds four 32-row MFMA tiles), 3 = 128 x 32 on 4 waves (TM 1)
-static int conv_t32() {
+// 32-channel tile variants: 0 = 256 x 32 on 4 waves, 1 = 128 x 32 on 2 waves, 2 = 256 x 32 on 2 waves (TM 4), 3 = 128 x
+// 32 on 4 waves (TM 1).  Default (SRL_CONV_T32 unset = -1): 3 for the forward LayerNorm+act epilogue, 0 otherwise -
+// per-launch medians at the Atari-100k shapes (profiles/r6_conv_t32.md): E1 fwd 83.5 -> 80.0 us, D3 fwd 211.6 -> 193.6
+// us with 3; the LayerNorm-backward epilogues (D4 dgrad 134 vs 222 us, E2 dgrad 243 vs 245 us) keep 0
+static int conv_t32(int mode) {
   static const int v = [] {
     const char* e = getenv("SRL_CONV_T32");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : -1;
   }();
-  return v;
+  return v >= 0 ? v : (mode == 0 ? 3 : 0);
 }
 #define CONV_T32(X, ...)                                                                           \
   do {                                                                                              \
-    switch (conv_t32()) {                                                                           \
+    switch (conv_t32(e.mode)) {                                                                     \
       case 1: X<128, 32, 2, 1>(__VA_ARGS__); break;                                                 \
       case 2: X<256, 32, 2, 1>(__VA_ARGS__); break;                                                 \
       case 3: X<128, 32, 4, 1>(__VA_ARGS__); break;                                                 \
