@@ -14,6 +14,8 @@ struct EpiLNActP {  // z = acc, y = act(LN_c(z)), per-pixel mean/rstd
 struct EpiLNBwdP {  // acc = dy; dz = LN/act backward; dgamma/dbeta += column sums
   const float *z, *mean, *rstd, *gamma, *beta;
   float *dz, *dgamma, *dbeta;
+  float* part;    // [part_rows][2 * Nc] per-workgroup column sums (fixed-order reduce, no atomics); null -> atomics
+  int part_rows;  // capacity of part in workgroups
   int act, M;
 };
 struct EpiPlainP {  // out = acc + bias + c0

@@ -524,6 +524,8 @@ struct EpiLNBwd : EpiLNBwdP {  // acc = dy (grad of y = act(LN(z))); dz = d/dz; 
         }
       }
       __syncthreads();
+      // one row of 2 * BN column sums per workgroup (reduced later in a fixed order), or float atomics
+      float* prow = part ? part + (size_t)(blockIdx.x + gridDim.x * blockIdx.z) * 2 * BN : nullptr;
       for (int c = threadIdx.x; c < BN; c += NTH) {
         float sg = 0.f, sb = 0.f;
 #pragma unroll
@@ -531,8 +533,13 @@ struct EpiLNBwd : EpiLNBwdP {  // acc = dy (grad of y = act(LN(z))); dz = d/dz; 
           sg += lds[q * BN + c];
           sb += lds[NW * BN + q * BN + c];
         }
-        if (dgamma) atomicAdd(dgamma + c, sg);
-        if (dbeta) atomicAdd(dbeta + c, sb);
+        if (prow) {
+          prow[c] = sg;
+          prow[BN + c] = sb;
+        } else {
+          if (dgamma) atomicAdd(dgamma + c, sg);
+          if (dbeta) atomicAdd(dbeta + c, sb);
+        }
       }
     }
   }
@@ -920,22 +927,26 @@ __global__ __launch_bounds__(256) void ln_bwd_img_kernel(const float* __restrict
   }
 }
 
-// out[j] += sum_b part[b][j] (j < W) in a fixed order: 64 columns x 16 row groups per workgroup (each thread's rows
-// b = grp, grp + 16, ... summed in 4 independent chains so their loads are in flight together), LDS combine in order.
-__global__ __launch_bounds__(1024) void ln_part_reduce_kernel(const float* __restrict__ part, int nb, int W,
-                                                              float* __restrict__ out0, float* __restrict__ out1, int C) {
+// Sum of the rows [blockIdx.y * rpb, min(nb, (blockIdx.y + 1) * rpb)) of part[nb][W] in a fixed order: 64 columns x
+// 16 row groups per workgroup (each thread's rows lo + grp, lo + grp + 16, ... summed in 4 independent chains so their
+// loads are in flight together), LDS combine in order.  stage != null: stage[blockIdx.y][col] = sum (first pass of a
+// two-pass reduction of a tall part); else out0[col] += sum (col < C), out1[col - C] += sum (C <= col < W).
+__global__ __launch_bounds__(1024) void ln_part_reduce_kernel(const float* __restrict__ part, int nb, int W, int rpb,
+                                                              float* __restrict__ stage, float* __restrict__ out0,
+                                                              float* __restrict__ out1, int C) {
   __shared__ float red[16][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6, col = blockIdx.x * 64 + cl;
+  const int lo = blockIdx.y * rpb, hi = min(nb, lo + rpb);
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (col < W) {
-    int b = grp;
-    for (; b + 48 < nb; b += 64) {
+    int b = lo + grp;
+    for (; b + 48 < hi; b += 64) {
       s0 += part[(size_t)b * W + col];
       s1 += part[(size_t)(b + 16) * W + col];
       s2 += part[(size_t)(b + 32) * W + col];
       s3 += part[(size_t)(b + 48) * W + col];
     }
-    for (; b < nb; b += 16) s0 += part[(size_t)b * W + col];
+    for (; b < hi; b += 16) s0 += part[(size_t)b * W + col];
   }
   red[grp][cl] = (s0 + s1) + (s2 + s3);
   __syncthreads();
@@ -943,11 +954,34 @@ __global__ __launch_bounds__(1024) void ln_part_reduce_kernel(const float* __res
     float v = 0.f;
 #pragma unroll
     for (int g = 0; g < 16; ++g) v += red[g][cl];
-    if (col < C) {
+    if (stage) {
+      stage[(size_t)blockIdx.y * W + col] = v;
+    } else if (col < C) {
       if (out0) out0[col] += v;
     } else if (out1) {
       out1[col - C] += v;
     }
+  }
+}
+
+// rows of part summed per workgroup in the first pass of a two-pass reduction; a part buffer of nb rows needs
+// part_stage_rows(nb) more rows behind it for the first pass's output
+constexpr int PART_RPB = 64;
+inline int part_stage_rows(int nb) { return (nb + PART_RPB - 1) / PART_RPB; }
+
+// dgamma (columns < C) / dbeta (columns C..W) += column sums of part[nb][W]; part has part_stage_rows(nb) spare rows
+// behind its nb rows when stage_ok (tall parts: a 64-rows-per-workgroup first pass spreads the loads over the chip)
+static void launch_part_reduce(float* part, int nb, int W, float* out0, float* out1, int C, bool stage_ok, hipStream_t st) {
+  const int cb = (W + 63) / 64;
+  if (stage_ok && nb > 2 * PART_RPB) {
+    const int g = part_stage_rows(nb);
+    float* stage = part + (size_t)nb * W;
+    hipLaunchKernelGGL(ln_part_reduce_kernel, dim3(cb, g), dim3(1024), 0, st, part, nb, W, PART_RPB, stage, out0, out1, C);
+    hipLaunchKernelGGL(ln_part_reduce_kernel, dim3(cb, 1), dim3(1024), 0, st, stage, g, W, g, (float*)nullptr, out0,
+                       out1, C);
+  } else {
+    hipLaunchKernelGGL(ln_part_reduce_kernel, dim3(cb, 1), dim3(1024), 0, st, part, nb, W, nb, (float*)nullptr, out0,
+                       out1, C);
   }
 }
 
@@ -1061,7 +1095,11 @@ static void dispatch_epi(const LA& la, const Dense<BN, 64 * WM * WN>& lb, const 
   } else if (e.mode == 1) {
     EpiLNBwd ep;
     static_cast<EpiLNBwdP&>(ep) = e.lb;
+    const int nblk = mtiles * ncls;
+    const bool sums = ep.dgamma || ep.dbeta;
+    if (!sums || nblk > ep.part_rows) ep.part = nullptr;
     launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNBwd, RM>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
+    if (ep.part) launch_part_reduce(ep.part, nblk, 2 * BN, ep.dgamma, ep.dbeta, BN, true, st);
   } else {
     EpiPlain ep;
     static_cast<EpiPlainP&>(ep) = e.pl;
@@ -1112,6 +1150,23 @@ static int conv_t32(int mode) {
     case 1024: X<32, 1024, 1, 8>(__VA_ARGS__); return true;                                         \
     default: return false;                                                                          \
   }
+
+// rows to allocate for a dgamma / dbeta partial buffer of nb workgroup rows (+ the two-pass reduction's stage rows)
+int conv_part_alloc_rows(int nb) { return nb + part_stage_rows(nb); }
+
+// rows (BM) of the workgroup tile CONV_TILES picks for Nc output channels and epilogue mode (0 if unsupported)
+int conv_tile_rows(int Nc, int mode) {
+  switch (Nc) {
+    case 32: {
+      const int v = conv_t32(mode);
+      return (v == 1 || v == 3) ? 128 : 256;
+    }
+    case 64: case 96: case 128: case 192: return 128;
+    case 256: case 384: case 512: case 768: return 64;
+    case 1024: return 32;
+    default: return 0;
+  }
+}
 
 bool conv_channels_supported(int Nc) {
   switch (Nc) {
@@ -1377,8 +1432,7 @@ bool launch_ln_bwd_flat(const float* dy, const float* z, const float* mean, cons
       default: SRL_LNBI(16); break;
     }
 #undef SRL_LNBI
-    if (dgamma || dbeta)
-      hipLaunchKernelGGL(ln_part_reduce_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, part, nb, 2 * C, dgamma, dbeta, C);
+    if (dgamma || dbeta) launch_part_reduce(part, nb, 2 * C, dgamma, dbeta, C, true, st);
     return true;
   }
   const int rpb = 64;

@@ -23,6 +23,8 @@ bool launch_ln_bwd_flat(const float*, const float*, const float*, const float*, 
 bool launch_up_small(const float*, const float*, const float*, float, float*, int, int, int, int, int, hipStream_t);
 void set_up_last_form(int);
 bool conv_channels_supported(int);
+int conv_tile_rows(int, int);
+int conv_part_alloc_rows(int);
 
 namespace {
 
@@ -180,6 +182,13 @@ std::vector<torch::Tensor> conv_gemm(int64_t kind, torch::Tensor src, torch::Ten
     e.lb.dz = dz.data_ptr<float>();
     e.lb.dgamma = optw(dgamma);
     e.lb.dbeta = optw(dbeta);
+    if (e.lb.dgamma || e.lb.dbeta) {
+      // per-workgroup column sums, summed in a fixed order after the GEMM (deterministic dgamma / dbeta)
+      const int64_t rows = (M + conv_tile_rows((int)Nc, 1) - 1) / conv_tile_rows((int)Nc, 1) * (down ? 1 : 4);
+      auto part = torch::empty({conv_part_alloc_rows((int)rows), 2 * Nc}, opts);
+      e.lb.part = part.data_ptr<float>();
+      e.lb.part_rows = (int)rows;  // freed on return: stream-ordered reuse by the caching allocator is safe
+    }
     outs = {dz};
   } else {
     TORCH_CHECK(Nreal >= 1 && Nreal <= Nc, "conv PLAIN: bad Nreal");
@@ -248,7 +257,7 @@ torch::Tensor conv_ln_bwd_flat(torch::Tensor dy, torch::Tensor z, torch::Tensor 
   auto dz = torch::empty_like(z);
   // per-workgroup dgamma / dbeta partials of the image-tiled kernel (one image per workgroup up to 1024), reduced in a fixed order
   const int64_t nblk = std::min<int64_t>(N, 1024);
-  auto part = torch::empty({nblk, 2 * C}, z.options());
+  auto part = torch::empty({conv_part_alloc_rows((int)nblk), 2 * C}, z.options());
   bool ok = launch_ln_bwd_flat(dy.data_ptr<float>(), z.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                                optp(gamma), optp(beta), dz.data_ptr<float>(), optw(dgamma), optw(dbeta), N * HW, C, HW,
                                (int)act, part.data_ptr<float>(), (int)nblk, stream());

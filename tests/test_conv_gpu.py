@@ -169,3 +169,19 @@ def test_ln_bwd_flat_matches_autograd_and_is_deterministic(n, hw, c):
     torch.testing.assert_close(outs[0][1].double(), g64.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(outs[0][2].double(), b64.grad, rtol=1e-4, atol=1e-3)
     assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
+
+
+def test_stack_grads_are_bitwise_reproducible(monkeypatch):
+    """The fused stacks' LayerNorm-backward GEMM epilogues write per-workgroup column sums that a fixed-order kernel
+    reduces (no float atomics): two identical fwd+bwd passes give bitwise-equal gradients of every parameter."""
+    monkeypatch.setattr(conv_ops, "MIN_FRAMES", 1)
+    enc, dec = _encoder_decoder(32, 64, 3)
+    torch.manual_seed(1)
+    x = torch.rand(66, 3, 64, 64, device=DEV)
+    lat = torch.randn(66, 96, device=DEV)
+    g_e = torch.randn(66, enc.output_dim, device=DEV)
+    g_d = torch.randn(66, 3, 64, 64, device=DEV)
+    runs = [_run(enc, dec, x, lat, g_e, g_d, True) for _ in range(2)]
+    diff = [k for k in runs[0][3] if not torch.equal(runs[0][3][k], runs[1][3][k])]
+    assert not diff, f"gradients differ run to run: {diff}"
+    assert torch.equal(runs[0][2], runs[1][2])
