@@ -265,8 +265,8 @@ class DecoderConvFn(torch.autograd.Function):
             o += g.numel()
             dbs.append(dgb[o:o + g.numel()])
             o += g.numel()
-        q = C.conv_to_nhwc4(dout, 1.0)
-        dbias = dout.sum(dim=(0, 2, 3))
+        # NHWC4 form of the image gradient and the last layer's bias gradient in one pass over it
+        q, dbias = C.conv_to_nhwc4_sum(dout)
         dws: List[Optional[Tensor]] = [None] * (L + 1)
         cout_last = ws[L].shape[1]
         # the weight gradients leave the critical path (data gradients -> scan backward -> encoder): inside the

@@ -802,6 +802,32 @@ __global__ void to_nhwc4_kernel(const T* __restrict__ x, f4* __restrict__ out, i
   out[idx] = f4{v[0], v[1], v[2], v[3]};
 }
 
+// to_nhwc4 of an f32 NCHW tensor (the image gradient entering the decoder backward) that also sums each channel over
+// the block's pixels: part[block][c] (c < C), summed over the blocks in a fixed order by ln_part_reduce_kernel - the
+// last layer's bias gradient without a second pass over the 50 MB gradient
+__global__ __launch_bounds__(256) void to_nhwc4_sum_kernel(const float* __restrict__ x, f4* __restrict__ out, int N, int C,
+                                                           int HW, float* __restrict__ part) {
+  __shared__ float red[4][4];
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (idx < N * HW) {
+    const int n = idx / HW, hw = idx - n * HW;
+    for (int c = 0; c < C; ++c) v[c] = x[((size_t)n * C + c) * HW + hw];
+    out[idx] = f4{v[0], v[1], v[2], v[3]};
+  }
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float s = wave_sum_dpp(v[c]);
+    if ((threadIdx.x & 63) == 0) red[w][c] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < C) {
+    const int c = threadIdx.x;
+    part[(size_t)blockIdx.x * C + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+  }
+}
+
 // Row LayerNorm+act backward with dy in NCHW-flat order (the encoder's last stage feeds the flat
 // embedding); z NHWC [M][C]; one wave per pixel row, channel c = lane + 64 e (e < CPL, c < C); column
 // partials per block, one atomic per channel per block.
@@ -930,10 +956,11 @@ __global__ __launch_bounds__(256) void ln_bwd_img_kernel(const float* __restrict
 // Sum of the rows [blockIdx.y * rpb, min(nb, (blockIdx.y + 1) * rpb)) of part[nb][W] in a fixed order: 64 columns x
 // 16 row groups per workgroup (each thread's rows lo + grp, lo + grp + 16, ... summed in 4 independent chains so their
 // loads are in flight together), LDS combine in order.  stage != null: stage[blockIdx.y][col] = sum (first pass of a
-// two-pass reduction of a tall part); else out0[col] += sum (col < C), out1[col - C] += sum (C <= col < W).
+// two-pass reduction of a tall part); else out0[col] += sum (col < C), out1[col - C] += sum (C <= col < W) (= with
+// assign).
 __global__ __launch_bounds__(1024) void ln_part_reduce_kernel(const float* __restrict__ part, int nb, int W, int rpb,
                                                               float* __restrict__ stage, float* __restrict__ out0,
-                                                              float* __restrict__ out1, int C) {
+                                                              float* __restrict__ out1, int C, int assign) {
   __shared__ float red[16][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6, col = blockIdx.x * 64 + cl;
   const int lo = blockIdx.y * rpb, hi = min(nb, lo + rpb);
@@ -957,9 +984,9 @@ __global__ __launch_bounds__(1024) void ln_part_reduce_kernel(const float* __res
     if (stage) {
       stage[(size_t)blockIdx.y * W + col] = v;
     } else if (col < C) {
-      if (out0) out0[col] += v;
+      if (out0) out0[col] = assign ? v : out0[col] + v;
     } else if (out1) {
-      out1[col - C] += v;
+      out1[col - C] = assign ? v : out1[col - C] + v;
     }
   }
 }
@@ -971,17 +998,19 @@ inline int part_stage_rows(int nb) { return (nb + PART_RPB - 1) / PART_RPB; }
 
 // dgamma (columns < C) / dbeta (columns C..W) += column sums of part[nb][W]; part has part_stage_rows(nb) spare rows
 // behind its nb rows when stage_ok (tall parts: a 64-rows-per-workgroup first pass spreads the loads over the chip)
-static void launch_part_reduce(float* part, int nb, int W, float* out0, float* out1, int C, bool stage_ok, hipStream_t st) {
-  const int cb = (W + 63) / 64;
+static void launch_part_reduce(float* part, int nb, int W, float* out0, float* out1, int C, bool stage_ok, hipStream_t st,
+                               bool assign = false) {
+  const int cb = (W + 63) / 64, as = assign ? 1 : 0;
   if (stage_ok && nb > 2 * PART_RPB) {
     const int g = part_stage_rows(nb);
     float* stage = part + (size_t)nb * W;
-    hipLaunchKernelGGL(ln_part_reduce_kernel, dim3(cb, g), dim3(1024), 0, st, part, nb, W, PART_RPB, stage, out0, out1, C);
+    hipLaunchKernelGGL(ln_part_reduce_kernel, dim3(cb, g), dim3(1024), 0, st, part, nb, W, PART_RPB, stage, out0, out1, C,
+                       0);
     hipLaunchKernelGGL(ln_part_reduce_kernel, dim3(cb, 1), dim3(1024), 0, st, stage, g, W, g, (float*)nullptr, out0,
-                       out1, C);
+                       out1, C, as);
   } else {
     hipLaunchKernelGGL(ln_part_reduce_kernel, dim3(cb, 1), dim3(1024), 0, st, part, nb, W, nb, (float*)nullptr, out0,
-                       out1, C);
+                       out1, C, as);
   }
 }
 
@@ -1387,6 +1416,13 @@ bool launch_multi_pack(const float* const* w, float* const* out, const int* A, c
 void launch_pack_up(const float* w, float* out, int A, int B, int Bp, hipStream_t st) {
   const int tot = 16 * Bp * A;
   hipLaunchKernelGGL(pack_up_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, w, out, A, B, Bp);
+}
+
+// NCHW f32 -> NHWC4 + per-channel sums over (N, H, W) into csum[C] (assigned); part: conv_part_alloc_rows(blocks) x C
+void launch_to_nhwc4_sum(const float* x, float* out, int N, int C, int HW, float* csum, float* part, hipStream_t st) {
+  const int nb = (N * HW + 255) / 256;
+  hipLaunchKernelGGL(to_nhwc4_sum_kernel, dim3(nb), dim3(256), 0, st, x, (f4*)out, N, C, HW, part);
+  launch_part_reduce(part, nb, C, csum, nullptr, C, true, st, true);
 }
 
 void launch_to_nhwc4(const void* x, bool u8, float* out, int N, int C, int HW, float scale, hipStream_t st) {

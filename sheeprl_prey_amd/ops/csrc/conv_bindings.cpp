@@ -18,6 +18,7 @@ void launch_pack_down(const float*, float*, int, int, int, hipStream_t);
 void launch_pack_up(const float*, float*, int, int, int, hipStream_t);
 bool launch_multi_pack(const float* const*, float* const*, const int*, const int*, const int*, const int*, int, hipStream_t);
 void launch_to_nhwc4(const void*, bool, float*, int, int, int, float, hipStream_t);
+void launch_to_nhwc4_sum(const float*, float*, int, int, int, float*, float*, hipStream_t);
 bool launch_ln_bwd_flat(const float*, const float*, const float*, const float*, const float*, const float*, float*, float*,
                         float*, int, int, int, int, float*, int, hipStream_t);
 bool launch_up_small(const float*, const float*, const float*, float, float*, int, int, int, int, int, hipStream_t);
@@ -244,6 +245,21 @@ torch::Tensor conv_to_nhwc4(torch::Tensor x, double scale) {
   return out;
 }
 
+// f32 NCHW [N, C<=4, H, W] -> (NHWC4 [N, H, W, 4], per-channel sum [C]) in one pass over x (+ a fixed-order reduce)
+std::vector<torch::Tensor> conv_to_nhwc4_sum(torch::Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.size(1) <= 4 && x.is_contiguous() && x.scalar_type() == torch::kFloat32,
+              "to_nhwc4_sum: contiguous f32 NCHW with <= 4 channels");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 31), "to_nhwc4_sum: too large");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  auto out = torch::empty({N, x.size(2), x.size(3), 4}, x.options());
+  auto csum = torch::empty({C}, x.options());
+  const int nb = (int)((N * HW + 255) / 256);
+  auto part = torch::empty({conv_part_alloc_rows(nb), C}, x.options());
+  launch_to_nhwc4_sum(x.data_ptr<float>(), out.data_ptr<float>(), N, C, HW, csum.data_ptr<float>(), part.data_ptr<float>(),
+                      stream());
+  return {out, csum};
+}
+
 // row LN+act backward, dy NCHW-flat [N, C*HW], z NHWC [N, HW, C]
 torch::Tensor conv_ln_bwd_flat(torch::Tensor dy, torch::Tensor z, torch::Tensor mean, torch::Tensor rstd,
                                c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, int64_t act,
@@ -341,6 +357,7 @@ void register_conv(pybind11::module& m) {
   m.def("conv_gemm", &conv_gemm);
   m.def("conv_wgrad", &conv_wgrad, pybind11::arg("P"), pybind11::arg("Q"), pybind11::arg("Cb"), pybind11::arg("out") = pybind11::none());
   m.def("conv_to_nhwc4", &conv_to_nhwc4);
+  m.def("conv_to_nhwc4_sum", &conv_to_nhwc4_sum);
   m.def("conv_ln_bwd_flat", &conv_ln_bwd_flat);
   m.def("conv_up_small", &conv_up_small);
   m.def("set_up_last_form", &set_up_last_form);  // 0 = MFMA final ConvT (default), 1 = VALU (A/B, tests)
