@@ -169,6 +169,7 @@ class EncoderConvFn(torch.autograd.Function):
         q, z, mean, rstd = acts[4 * (L - 1):4 * L]
         dz = C.conv_ln_bwd_flat(dy.contiguous(), z, mean, rstd, gs[-1], bs[-1], act[-1], dgs[-1], dbs[-1])
         dws: List[Optional[Tensor]] = [None] * L
+        parts: List[Tensor] = []  # the LayerNorm-backward convs' dgamma / dbeta partials, reduced together at the end
         for i in range(L - 1, -1, -1):
             q = acts[4 * i]
             cin = ws[i].shape[1]
@@ -176,8 +177,10 @@ class EncoderConvFn(torch.autograd.Function):
             if i > 0:
                 wp = up_packs[i - 1]
                 _, zp, mp, rp = acts[4 * (i - 1):4 * i]
-                dz = C.conv_gemm(1, dz, wp, cin, 1, gs[i - 1], bs[i - 1], 0.0, act[i - 1], False, zp, mp, rp,
-                                 dgs[i - 1], dbs[i - 1], None, 0.0, 0)[0]
+                dz, part = C.conv_gemm_lnbwd_part(1, dz, wp, cin, gs[i - 1], bs[i - 1], act[i - 1], zp, mp, rp)
+                parts.append(part)
+        if parts:  # layers L-2 .. 0, one pair of launches for all of them (assigned: the buffer's other slices)
+            C.conv_part_reduce_many(parts, dgs[L - 2::-1], dbs[L - 2::-1], True)
         return (None, None, *dws, *[d.view_as(g) for d, g in zip(dgs, gs)], *[d.view_as(b) for d, b in zip(dbs, bs)])
 
 
@@ -258,7 +261,8 @@ class DecoderConvFn(torch.autograd.Function):
         gs, bs = params[L + 1:2 * L + 1], params[2 * L + 1:3 * L + 1]
         act = meta["act"]
         dout = dout.contiguous()
-        dgb = torch.zeros(2 * sum(int(g.numel()) for g in gs), device=dout.device, dtype=dout.dtype)
+        # every slice is assigned by the deferred partial reduction below (no zero fill)
+        dgb = torch.empty(2 * sum(int(g.numel()) for g in gs), device=dout.device, dtype=dout.dtype)
         dgs, dbs, o = [], [], 0
         for g in gs:
             dgs.append(dgb[o:o + g.numel()])
@@ -275,8 +279,8 @@ class DecoderConvFn(torch.autograd.Function):
         assert q.shape[3] == 4, q.shape
         wp = down_packs[L]
         _, zp, mp, rp = acts[4 * (L - 1):4 * L]
-        dz = C.conv_gemm(0, q, wp, ws[L].shape[0], 1, gs[L - 1], bs[L - 1], 0.0, act[L - 1], False, zp, mp, rp,
-                         dgs[L - 1], dbs[L - 1], None, 0.0, 0)[0]
+        dz, part = C.conv_gemm_lnbwd_part(0, q, wp, ws[L].shape[0], gs[L - 1], bs[L - 1], act[L - 1], zp, mp, rp)
+        parts = [part]  # the LayerNorm-backward convs' dgamma / dbeta partials, reduced together at the end
         dh = None
         for i in range(L - 1, -1, -1):
             p = acts[4 * i]
@@ -286,11 +290,12 @@ class DecoderConvFn(torch.autograd.Function):
             cin = ws[i].shape[0]
             if i > 0:
                 _, zp, mp, rp = acts[4 * (i - 1):4 * i]
-                dz = C.conv_gemm(0, dz, wp, cin, 1, gs[i - 1], bs[i - 1], 0.0, act[i - 1], False, zp, mp, rp,
-                                 dgs[i - 1], dbs[i - 1], None, 0.0, 0)[0]
+                dz, part = C.conv_gemm_lnbwd_part(0, dz, wp, cin, gs[i - 1], bs[i - 1], act[i - 1], zp, mp, rp)
+                parts.append(part)
             else:
                 dh = C.conv_gemm(0, dz, wp, cin, 2, None, None, 0.0, 0, True, None, None, None, None, None, None,
                                  0.0, cin)[0]
+        C.conv_part_reduce_many(parts, dgs[::-1], dbs[::-1], True)  # layers L-1 .. 0
         dh = dh.reshape(dh.shape[0], -1)
         return (dh, None, *dws, *[d.view_as(g) for d, g in zip(dgs, gs)], *[d.view_as(b) for d, b in zip(dbs, bs)],
                 dbias)

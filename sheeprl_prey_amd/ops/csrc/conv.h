@@ -16,6 +16,7 @@ struct EpiLNBwdP {  // acc = dy; dz = LN/act backward; dgamma/dbeta += column su
   float *dz, *dgamma, *dbeta;
   float* part;    // [part_rows][2 * Nc] per-workgroup column sums (fixed-order reduce, no atomics); null -> atomics
   int part_rows;  // capacity of part in workgroups
+  int defer;      // 1: leave part for a later conv_part_reduce_many (dgamma / dbeta unused)
   int act, M;
 };
 struct EpiPlainP {  // out = acc + bias + c0

@@ -506,7 +506,7 @@ struct EpiLNBwd : EpiLNBwdP {  // acc = dy (grad of y = act(LN(z))); dz = d/dz; 
         }
       }
     }
-    if (dgamma || dbeta) {
+    if (part || dgamma || dbeta) {
       // rows of a wave pass share columns: fold the RPW row groups, then the NW waves through LDS
 #pragma unroll
       for (int e = 0; e < CPL; ++e)
@@ -953,17 +953,12 @@ __global__ __launch_bounds__(256) void ln_bwd_img_kernel(const float* __restrict
   }
 }
 
-// Sum of the rows [blockIdx.y * rpb, min(nb, (blockIdx.y + 1) * rpb)) of part[nb][W] in a fixed order: 64 columns x
-// 16 row groups per workgroup (each thread's rows lo + grp, lo + grp + 16, ... summed in 4 independent chains so their
-// loads are in flight together), LDS combine in order.  stage != null: stage[blockIdx.y][col] = sum (first pass of a
-// two-pass reduction of a tall part); else out0[col] += sum (col < C), out1[col - C] += sum (C <= col < W) (= with
-// assign).
-__global__ __launch_bounds__(1024) void ln_part_reduce_kernel(const float* __restrict__ part, int nb, int W, int rpb,
-                                                              float* __restrict__ stage, float* __restrict__ out0,
-                                                              float* __restrict__ out1, int C, int assign) {
-  __shared__ float red[16][64];
-  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6, col = blockIdx.x * 64 + cl;
-  const int lo = blockIdx.y * rpb, hi = min(nb, lo + rpb);
+// Sum of the rows [lo, hi) of column col of part[.][W] in a fixed order: 64 columns x 16 row groups per workgroup
+// (each thread's rows lo + grp, lo + grp + 16, ... summed in 4 independent chains so their loads are in flight
+// together), LDS combine in order; the result is valid on the threads of row group 0.
+__device__ __forceinline__ float part_block_sum(const float* __restrict__ part, int lo, int hi, int W, int col,
+                                                float (*red)[64]) {
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (col < W) {
     int b = lo + grp;
@@ -977,10 +972,25 @@ __global__ __launch_bounds__(1024) void ln_part_reduce_kernel(const float* __res
   }
   red[grp][cl] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (grp == 0 && col < W) {
-    float v = 0.f;
+  float v = 0.f;
+  if (grp == 0) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) v += red[g][cl];
+  }
+  return v;
+}
+
+// Rows [blockIdx.y * rpb, min(nb, (blockIdx.y + 1) * rpb)) of part[nb][W] summed (part_block_sum).  stage != null:
+// stage[blockIdx.y][col] = sum (first pass of a two-pass reduction of a tall part); else out0[col] += sum (col < C),
+// out1[col - C] += sum (C <= col < W) (= with assign).
+__global__ __launch_bounds__(1024) void ln_part_reduce_kernel(const float* __restrict__ part, int nb, int W, int rpb,
+                                                              float* __restrict__ stage, float* __restrict__ out0,
+                                                              float* __restrict__ out1, int C, int assign) {
+  __shared__ float red[16][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lo = blockIdx.y * rpb, hi = min(nb, lo + rpb);
+  const float v = part_block_sum(part, lo, hi, W, col, red);
+  if (threadIdx.x < 64 && col < W) {
     if (stage) {
       stage[(size_t)blockIdx.y * W + col] = v;
     } else if (col < C) {
@@ -1126,9 +1136,9 @@ static void dispatch_epi(const LA& la, const Dense<BN, 64 * WM * WN>& lb, const 
     static_cast<EpiLNBwdP&>(ep) = e.lb;
     const int nblk = mtiles * ncls;
     const bool sums = ep.dgamma || ep.dbeta;
-    if (!sums || nblk > ep.part_rows) ep.part = nullptr;
+    if (!(sums || ep.defer) || nblk > ep.part_rows) ep.part = nullptr;
     launch(igemm_kernel<BM, BN, WM, WN, LA, Dense<BN, 64 * WM * WN>, EpiLNBwd, RM>, grid, block, st, la, lb, ep, rm, K, ncls, remap);
-    if (ep.part) launch_part_reduce(ep.part, nblk, 2 * BN, ep.dgamma, ep.dbeta, BN, true, st);
+    if (ep.part && !ep.defer) launch_part_reduce(ep.part, nblk, 2 * BN, ep.dgamma, ep.dbeta, BN, true, st);
   } else {
     EpiPlain ep;
     static_cast<EpiPlainP&>(ep) = e.pl;
@@ -1416,6 +1426,72 @@ bool launch_multi_pack(const float* const* w, float* const* out, const int* A, c
 void launch_pack_up(const float* w, float* out, int A, int B, int Bp, hipStream_t st) {
   const int tot = 16 * Bp * A;
   hipLaunchKernelGGL(pack_up_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, w, out, A, B, Bp);
+}
+
+// Every deferred dgamma / dbeta partial of a stack's backward in two launches (instead of two per layer): pass 0 sums
+// 64-row groups of every job's part into its stage rows, pass 1 sums the stage rows into the outputs.  Same fixed
+// order as launch_part_reduce.
+constexpr int MAX_PR_JOBS = 16;
+struct PRJobs {
+  const float* part[MAX_PR_JOBS];
+  float* stage[MAX_PR_JOBS];
+  float* out0[MAX_PR_JOBS];
+  float* out1[MAX_PR_JOBS];
+  int nb[MAX_PR_JOBS], W[MAX_PR_JOBS], C[MAX_PR_JOBS], g[MAX_PR_JOBS];
+  int off[MAX_PR_JOBS + 1];  // first workgroup of each job in this pass
+  int n, assign;
+};
+
+__global__ __launch_bounds__(1024) void part_reduce_many_kernel(PRJobs J, int pass) {
+  __shared__ float red[16][64];
+  int j = 0;
+  while (j + 1 < J.n && (int)blockIdx.x >= J.off[j + 1]) ++j;  // workgroup-uniform
+  const int local = blockIdx.x - J.off[j], W = J.W[j], cb = (W + 63) / 64;
+  const int cbi = local % cb, gi = local / cb;
+  const int col = cbi * 64 + (threadIdx.x & 63);
+  const float v = pass == 0 ? part_block_sum(J.part[j], gi * PART_RPB, min(J.nb[j], (gi + 1) * PART_RPB), W, col, red)
+                            : part_block_sum(J.stage[j], 0, J.g[j], W, col, red);
+  if (threadIdx.x < 64 && col < W) {
+    if (pass == 0) {
+      J.stage[j][(size_t)gi * W + col] = v;
+    } else {
+      const int C = J.C[j];
+      float* o = col < C ? J.out0[j] : J.out1[j];
+      const int c = col < C ? col : col - C;
+      if (o) o[c] = J.assign ? v : o[c] + v;
+    }
+  }
+}
+
+// stage: sum over jobs of part_stage_rows(nb) * W floats
+bool launch_part_reduce_many(const float* const* parts, const int* nbs, const int* Ws, float* const* out0,
+                             float* const* out1, const int* Cs, int n, float* stage, bool assign, hipStream_t st) {
+  if (n < 1 || n > MAX_PR_JOBS) return false;
+  PRJobs J{};
+  J.n = n;
+  J.assign = assign ? 1 : 0;
+  size_t so = 0;
+  for (int j = 0; j < n; ++j) {
+    J.part[j] = parts[j];
+    J.nb[j] = nbs[j];
+    J.W[j] = Ws[j];
+    J.C[j] = Cs[j];
+    J.out0[j] = out0[j];
+    J.out1[j] = out1[j];
+    J.g[j] = part_stage_rows(nbs[j]);
+    J.stage[j] = stage + so;
+    so += (size_t)J.g[j] * Ws[j];
+  }
+  for (int pass = 0; pass < 2; ++pass) {
+    int tot = 0;
+    for (int j = 0; j < n; ++j) {
+      J.off[j] = tot;
+      tot += (Ws[j] + 63) / 64 * (pass == 0 ? J.g[j] : 1);
+    }
+    J.off[n] = tot;
+    hipLaunchKernelGGL(part_reduce_many_kernel, dim3(tot), dim3(1024), 0, st, J, pass);
+  }
+  return true;
 }
 
 // NCHW f32 -> NHWC4 + per-channel sums over (N, H, W) into csum[C] (assigned); part: conv_part_alloc_rows(blocks) x C

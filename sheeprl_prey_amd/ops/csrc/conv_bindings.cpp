@@ -26,6 +26,8 @@ void set_up_last_form(int);
 bool conv_channels_supported(int);
 int conv_tile_rows(int, int);
 int conv_part_alloc_rows(int);
+bool launch_part_reduce_many(const float* const*, const int*, const int*, float* const*, float* const*, const int*, int,
+                             float*, bool, hipStream_t);
 
 namespace {
 
@@ -131,12 +133,12 @@ std::vector<torch::Tensor> conv_pack_many(std::vector<torch::Tensor> ws, std::ve
 // mode 0: LN_ACT -> (z, y, mean, rstd); y_nchw: y as [N, Nc*SH*SW] (C,H,W order)
 // mode 1: LN_BWD (ln_z/ln_mean/ln_rstd of the output layer, dgamma/dbeta accumulated) -> (dz)
 // mode 2: PLAIN (bias, c0, Nreal, nchw) -> (out)
-std::vector<torch::Tensor> conv_gemm(int64_t kind, torch::Tensor src, torch::Tensor Wp, int64_t Nc, int64_t mode,
-                                     c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, double eps,
-                                     int64_t act, bool out_nchw, c10::optional<torch::Tensor> ln_z,
-                                     c10::optional<torch::Tensor> ln_mean, c10::optional<torch::Tensor> ln_rstd,
-                                     c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta,
-                                     c10::optional<torch::Tensor> bias, double c0, int64_t Nreal) {
+static std::vector<torch::Tensor> conv_gemm_impl(int64_t kind, torch::Tensor src, torch::Tensor Wp, int64_t Nc, int64_t mode,
+                                                 c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta,
+                                                 double eps, int64_t act, bool out_nchw, c10::optional<torch::Tensor> ln_z,
+                                                 c10::optional<torch::Tensor> ln_mean, c10::optional<torch::Tensor> ln_rstd,
+                                                 c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta,
+                                                 c10::optional<torch::Tensor> bias, double c0, int64_t Nreal, bool defer) {
   chk_nhwc(src, "conv input");
   chk(Wp, "packed weight");
   const bool down = kind == 0;
@@ -181,16 +183,23 @@ std::vector<torch::Tensor> conv_gemm(int64_t kind, torch::Tensor src, torch::Ten
     e.lb.mean = optp(ln_mean);
     e.lb.rstd = optp(ln_rstd);
     e.lb.dz = dz.data_ptr<float>();
-    e.lb.dgamma = optw(dgamma);
-    e.lb.dbeta = optw(dbeta);
-    if (e.lb.dgamma || e.lb.dbeta) {
-      // per-workgroup column sums, summed in a fixed order after the GEMM (deterministic dgamma / dbeta)
-      const int64_t rows = (M + conv_tile_rows((int)Nc, 1) - 1) / conv_tile_rows((int)Nc, 1) * (down ? 1 : 4);
+    e.lb.dgamma = defer ? nullptr : optw(dgamma);
+    e.lb.dbeta = defer ? nullptr : optw(dbeta);
+    // per-workgroup column sums (one row per workgroup of the launch), summed in a fixed order after the GEMM -
+    // right behind it, or (defer) by the caller's conv_part_reduce_many with the other layers' (deterministic)
+    const int64_t rows = (M + conv_tile_rows((int)Nc, 1) - 1) / conv_tile_rows((int)Nc, 1) * (down ? 1 : 4);
+    outs = {dz};
+    if (defer) {
+      auto part = torch::empty({rows, 2 * Nc}, opts);
+      e.lb.part = part.data_ptr<float>();
+      e.lb.part_rows = (int)rows;
+      e.lb.defer = 1;
+      outs.push_back(part);
+    } else if (e.lb.dgamma || e.lb.dbeta) {
       auto part = torch::empty({conv_part_alloc_rows((int)rows), 2 * Nc}, opts);
       e.lb.part = part.data_ptr<float>();
       e.lb.part_rows = (int)rows;  // freed on return: stream-ordered reuse by the caching allocator is safe
     }
-    outs = {dz};
   } else {
     TORCH_CHECK(Nreal >= 1 && Nreal <= Nc, "conv PLAIN: bad Nreal");
     auto out = out_nchw ? torch::empty({N, Nreal, OH, OW}, opts) : torch::empty({N, OH, OW, Nreal}, opts);
@@ -206,6 +215,55 @@ std::vector<torch::Tensor> conv_gemm(int64_t kind, torch::Tensor src, torch::Ten
                  : launch_conv_up(src.data_ptr<float>(), Wp.data_ptr<float>(), N, H, W, C, Nc, e, stream());
   TORCH_CHECK(ok, "conv: unsupported configuration");
   return outs;
+}
+
+std::vector<torch::Tensor> conv_gemm(int64_t kind, torch::Tensor src, torch::Tensor Wp, int64_t Nc, int64_t mode,
+                                     c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta, double eps,
+                                     int64_t act, bool out_nchw, c10::optional<torch::Tensor> ln_z,
+                                     c10::optional<torch::Tensor> ln_mean, c10::optional<torch::Tensor> ln_rstd,
+                                     c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta,
+                                     c10::optional<torch::Tensor> bias, double c0, int64_t Nreal) {
+  return conv_gemm_impl(kind, src, Wp, Nc, mode, gamma, beta, eps, act, out_nchw, ln_z, ln_mean, ln_rstd, dgamma, dbeta,
+                        bias, c0, Nreal, false);
+}
+
+// LN_BWD conv whose dgamma / dbeta partials are left for conv_part_reduce_many -> (dz, part [workgroups, 2 Nc])
+std::vector<torch::Tensor> conv_gemm_lnbwd_part(int64_t kind, torch::Tensor src, torch::Tensor Wp, int64_t Nc,
+                                                c10::optional<torch::Tensor> gamma, c10::optional<torch::Tensor> beta,
+                                                int64_t act, torch::Tensor ln_z, torch::Tensor ln_mean, torch::Tensor ln_rstd) {
+  return conv_gemm_impl(kind, src, Wp, Nc, 1, gamma, beta, 0.0, act, false, ln_z, ln_mean, ln_rstd, c10::nullopt,
+                        c10::nullopt, c10::nullopt, 0.0, 0, true);
+}
+
+// out0[j] (=|+=) column sums of parts[j][:, :C], out1[j] of parts[j][:, C:] (C = W / 2): every deferred partial of a
+// stack's backward in two launches
+void conv_part_reduce_many(std::vector<torch::Tensor> parts, std::vector<torch::Tensor> out0, std::vector<torch::Tensor> out1,
+                           bool assign) {
+  const size_t n = parts.size();
+  TORCH_CHECK(n >= 1 && n <= 16 && out0.size() == n && out1.size() == n, "part_reduce_many: 1..16 jobs");
+  std::vector<const float*> pp(n);
+  std::vector<float*> o0(n), o1(n);
+  std::vector<int> nb(n), W(n), C(n);
+  int64_t stage = 0;
+  for (size_t j = 0; j < n; ++j) {
+    chk(parts[j], "part");
+    chk(out0[j], "out0");
+    chk(out1[j], "out1");
+    TORCH_CHECK(parts[j].dim() == 2 && parts[j].size(1) % 2 == 0, "part_reduce_many: part [rows, 2C]");
+    const int64_t c = parts[j].size(1) / 2;
+    TORCH_CHECK(out0[j].numel() == c && out1[j].numel() == c, "part_reduce_many: outputs must have C elements");
+    pp[j] = parts[j].data_ptr<float>();
+    o0[j] = out0[j].data_ptr<float>();
+    o1[j] = out1[j].data_ptr<float>();
+    nb[j] = (int)parts[j].size(0);
+    W[j] = (int)(2 * c);
+    C[j] = (int)c;
+    stage += (int64_t)(conv_part_alloc_rows(nb[j]) - nb[j]) * W[j];
+  }
+  auto st = torch::empty({std::max<int64_t>(stage, 1)}, parts[0].options());
+  TORCH_CHECK(launch_part_reduce_many(pp.data(), nb.data(), W.data(), o0.data(), o1.data(), C.data(), (int)n,
+                                      st.data_ptr<float>(), assign, stream()),
+              "part_reduce_many: launch");
 }
 
 // dW[a][b][4][4] = sum_m P[m][a] Q[gather(m, tap)][b]; P NHWC small grid [N,SH,SW,Ca], Q NHWC large [N,2SH,2SW,Cbp]
@@ -358,6 +416,8 @@ void register_conv(pybind11::module& m) {
   m.def("conv_wgrad", &conv_wgrad, pybind11::arg("P"), pybind11::arg("Q"), pybind11::arg("Cb"), pybind11::arg("out") = pybind11::none());
   m.def("conv_to_nhwc4", &conv_to_nhwc4);
   m.def("conv_to_nhwc4_sum", &conv_to_nhwc4_sum);
+  m.def("conv_gemm_lnbwd_part", &conv_gemm_lnbwd_part);
+  m.def("conv_part_reduce_many", &conv_part_reduce_many);
   m.def("conv_ln_bwd_flat", &conv_ln_bwd_flat);
   m.def("conv_up_small", &conv_up_small);
   m.def("set_up_last_form", &set_up_last_form);  // 0 = MFMA final ConvT (default), 1 = VALU (A/B, tests)
