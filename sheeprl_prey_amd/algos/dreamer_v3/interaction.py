@@ -15,9 +15,10 @@ uses the trained weights, as there; the gradient steps are launched BEFORE the e
 env step overlaps them.  Divergence: the reset rows (final obs, ``done=1``) of episodes that end at
 this env step are added after this step's gradient launch, so they reach training one step later
 than in the reference (a sequence sample covers the newest row with probability ~ B*L / buffer
-length).  ``algo.interaction_serial_order=True`` keeps the reference's order exactly: the gradient steps run after
-the env step and the reset rows, and the GPU idles while the CPU steps the env (the pipelined default measured
-+1.6 % on the Atari-100k bench, three alternating pairs, ``profiles/r6_interaction_drain.md``).
+length).  ``algo.interaction_serial_order=True`` (the default since round 5) keeps the reference's order exactly: the
+gradient steps run after the env step and the reset rows, and the GPU idles while the CPU steps the env; the
+pipelined opt-in measured +1.6 % on the Atari-100k bench in round 6 (three alternating pairs,
+``profiles/r6_interaction_drain.md``; round 5: no difference, ``profiles/r5_serial_order.md``).
 
 ``last_train_host_s`` is the host time spent inside ``train_fn`` during the last ``step``; callers
 timing the env interaction subtract it (the reference times interaction and training separately,
@@ -55,7 +56,7 @@ class InteractionLoop:
         self.row_keys = self.obs_keys + ["rewards", "dones", "is_first"]
         self.pipelined = self.device.type == "cuda"
         # reference effect order (act, add, env step, add reset rows, train) instead of training before the env step
-        self.serial_order = bool(cfg.algo.get("interaction_serial_order", False))
+        self.serial_order = bool(cfg.algo.get("interaction_serial_order", True))
         self.step_data = TensorDict({}, batch_size=[self.ne], device="cpu")
         self._slot = 0
         self._ring: List[Dict[str, torch.Tensor]] = []
