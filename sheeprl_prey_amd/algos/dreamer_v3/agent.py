@@ -36,7 +36,6 @@ from sheeprl_prey_amd.utils.distribution import (
     TruncatedNormal,
 )
 from sheeprl_prey_amd.utils.model import LayerNormChannelLast, ModuleType, cnn_forward
-from sheeprl_prey_amd.utils.utils import symlog
 
 
 def _act(name):
@@ -148,7 +147,10 @@ class MLPEncoder(nn.Module):
         self.symlog_inputs = symlog_inputs
 
     def forward(self, obs: Dict[str, Tensor]) -> Tensor:
-        x = torch.cat([symlog(obs[k]) if self.symlog_inputs else obs[k] for k in self.keys], -1)
+        if self.symlog_inputs:
+            x = ops.symlog_cat([obs[k] for k in self.keys])  # one launch on GPU (sign / abs / log1p / mul + cat in torch)
+        else:
+            x = torch.cat([obs[k] for k in self.keys], -1)
         return self.model(x)
 
 

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import importlib
 import os
-from typing import Optional, Tuple
+from typing import Optional, Sequence, Tuple
 
 import torch
 from torch import Tensor
@@ -951,6 +951,18 @@ def obs_mse(rec: Tensor, target: Tensor, scale: float = 1.0, symlog: bool = Fals
         d = torch.where(d < 1e-8, torch.zeros_like(d), d)
         return d.sum(dim=dims)
     return ((rec - tgt) ** 2).sum(dim=dims)
+
+
+def symlog_cat(xs: Sequence[Tensor]) -> Tensor:
+    """``cat([symlog(x) for x in xs], -1)`` (the DreamerV3 vector encoder's input, reference
+    ``dreamer_v3/agent.py`` MLPEncoder): one launch on GPU for inputs that need no gradient; eager torch otherwise."""
+    xs = list(xs)
+    if (xs and len(xs) <= 8 and _native(xs[0]) and all(x.dtype == torch.float32 and x.is_cuda and not x.requires_grad
+                                                        for x in xs)):
+        return _ext().symlog_cat([x.contiguous() for x in xs])
+    from sheeprl_prey_amd.utils.utils import symlog
+
+    return torch.cat([symlog(x) for x in xs], -1)
 
 
 def imag_discount(continue_logits: Tensor, dones: Tensor, gamma: float, skip_first: bool = False):

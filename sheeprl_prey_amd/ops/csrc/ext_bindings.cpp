@@ -38,6 +38,7 @@ void launch_wm_loss_bwd(const float* logit, const float* done, const float* g, i
                         float* d_obs, float* d_rew, float* d_logit, hipStream_t st);
 bool launch_ens_disagreement(const float* X, const float* W, const float* b, float* part, int n, int M, int O, int H,
                              hipStream_t st);
+bool launch_symlog_cat(const float* const* src, const int* d, int n, float* out, int rows, hipStream_t st);
 void launch_obs_mse_fwd(const float* rec, const void* tgt, bool u8, int rows, int n, float scale, int symlog, float* loss,
                         hipStream_t st);
 void launch_obs_mse_bwd(const float* rec, const void* tgt, bool u8, int rows, int n, float scale, int symlog, const float* g,
@@ -513,6 +514,31 @@ static void obs_check(const torch::Tensor& rec, const torch::Tensor& tgt, int64_
   TORCH_CHECK(rows > 0 && rec.numel() % rows == 0 && (rec.numel() / rows) % 4 == 0, "obs_mse: row length % 4");
 }
 
+// cat([symlog(x) for x in xs], -1) in one launch: xs contiguous float32 [..., d_j] with equal leading shapes
+torch::Tensor symlog_cat(std::vector<torch::Tensor> xs) {
+  TORCH_CHECK(!xs.empty() && xs.size() <= 8, "symlog_cat: 1..8 inputs");
+  std::vector<const float*> src;
+  std::vector<int> d;
+  const auto lead = xs[0].sizes().slice(0, xs[0].dim() - 1);
+  int64_t W = 0;
+  for (auto& x : xs) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kFloat32 && x.is_contiguous() && x.dim() >= 1,
+                "symlog_cat: contiguous float32 GPU inputs");
+    TORCH_CHECK(x.sizes().slice(0, x.dim() - 1) == lead, "symlog_cat: equal leading shapes");
+    src.push_back(x.data_ptr<float>());
+    d.push_back((int)x.size(-1));
+    W += x.size(-1);
+  }
+  std::vector<int64_t> shape(lead.begin(), lead.end());
+  shape.push_back(W);
+  auto out = torch::empty(shape, xs[0].options());
+  const int64_t rows = W > 0 ? out.numel() / W : 0;
+  TORCH_CHECK(rows * W < (int64_t(1) << 31), "symlog_cat: too large");
+  if (rows > 0) TORCH_CHECK(launch_symlog_cat(src.data(), d.data(), (int)xs.size(), out.data_ptr<float>(), (int)rows, stream()),
+                            "symlog_cat: launch");
+  return out;
+}
+
 torch::Tensor obs_mse_fwd(torch::Tensor rec, torch::Tensor tgt, int64_t rows, double scale, int64_t symlog) {
   obs_check(rec, tgt, rows);
   auto loss = torch::empty({rows}, rec.options());
@@ -871,6 +897,7 @@ void register_ext(pybind11::module& m) {
   m.def("ens_disagreement", &ens_disagreement);
   m.def("wm_loss_fwd", &wm_loss_fwd);
   m.def("wm_loss_bwd", &wm_loss_bwd);
+  m.def("symlog_cat", &symlog_cat);
   m.def("obs_mse_fwd", &obs_mse_fwd);
   m.def("obs_mse_bwd", &obs_mse_bwd);
   m.def("sac_twin_q_target", &sac_twin_q_target);

@@ -77,6 +77,42 @@ __global__ __launch_bounds__(NTH) void obs_mse_bwd_kernel(const float* __restric
 }  // namespace obsloss
 }  // namespace srl
 
+// Vector-observation encoder input (reference dreamer_v3/agent.py MLPEncoder: cat of symlog(obs[k]) over the keys):
+// the symlog of up to 8 row-major [rows, d_j] inputs written side by side into out [rows, sum d_j] in one pass
+// (torch: sign, abs, log1p, mul per key + the concatenation copy).
+struct SymlogCat {
+  const float* src[8];
+  int d[8];
+  int off[9];
+  int n;
+};
+__global__ __launch_bounds__(256) void symlog_cat_kernel(SymlogCat s, float* __restrict__ out, int rows, int W) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)rows * W) return;
+  const int r = (int)(i / W), c = (int)(i - (long)r * W);
+  int j = 0;
+  while (j + 1 < s.n && c >= s.off[j + 1]) ++j;
+  const float v = s.src[j][(long)r * s.d[j] + (c - s.off[j])];
+  out[i] = copysignf(log1pf(fabsf(v)), v);
+}
+
+bool launch_symlog_cat(const float* const* src, const int* d, int n, float* out, int rows, hipStream_t st) {
+  if (n < 1 || n > 8 || rows < 1) return false;
+  SymlogCat s{};
+  s.n = n;
+  int W = 0;
+  for (int j = 0; j < n; ++j) {
+    s.src[j] = src[j];
+    s.d[j] = d[j];
+    s.off[j] = W;
+    W += d[j];
+  }
+  s.off[n] = W;
+  const long tot = (long)rows * W;
+  hipLaunchKernelGGL(symlog_cat_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, s, out, rows, W);
+  return true;
+}
+
 void launch_obs_mse_fwd(const float* rec, const void* tgt, bool u8, int rows, int n, float scale, int symlog, float* loss,
                         hipStream_t st) {
   if (u8)
