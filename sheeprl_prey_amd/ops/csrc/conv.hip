@@ -1665,9 +1665,11 @@ __global__ __launch_bounds__(256) void up_small2_kernel(const float* __restrict_
 // so N = 48 for RGB fills three 16-wide MFMA tiles exactly (the output-centric form would pad N = CO to 16),
 // and no K entry is a structural zero.  A workgroup owns a 16 x 16 small-pixel tile of one image: it stages the
 // 18 x 18 halo window (32 channels per pass) in LDS, runs the window's 21 x CO 16x16 tiles on
-// v_mfma_f32_16x16x4_f32 (B fragments - the packed weights - held in registers for the whole pass), parks C in
-// LDS over the dead window, and each thread then sums the 4 (tap, neighbour) contributions of each of its 2 x 2
-// x CO output pixels (col2im) and writes the NCHW image rows as float2.
+// v_mfma_f32_16x16x4_f32 (B fragments - the packed weights - held in registers for the whole pass).  The columns
+// are channel-major (col = 16 co + tap), so MFMA column tile t is output channel t: each channel's C is parked in
+// LDS over the dead window on its own (22 KB, not the whole 64 KB C: three workgroups fit a CU instead of two), and
+// each thread sums the 4 (tap, neighbour) contributions of each of its 2 x 2 output pixels (col2im) and writes the
+// NCHW image rows as float2.
 template <int CO>
 __global__ __launch_bounds__(256) void up_last_mfma_kernel(const float* __restrict__ P, const float* __restrict__ W,
                                                            const float* __restrict__ bias, float c0, float* __restrict__ out,
@@ -1676,7 +1678,7 @@ __global__ __launch_bounds__(256) void up_last_mfma_kernel(const float* __restri
   constexpr int T = 16, TH = T + 2, NPIX = TH * TH;  // 324 window pixels
   constexpr int MT = (NPIX + 15) / 16;               // 21 M tiles
   constexpr int MPW = (MT + 3) / 4;                  // M tiles per wave
-  constexpr int LDA = 36, LDC = 16 * CO + 1;
+  constexpr int LDA = 36, LDC = 17;                  // C of ONE output channel: [pixel][16 taps] (+1 pad)
   constexpr int LDS_A = MT * 16 * LDA, LDS_C = MT * 16 * LDC;
   __shared__ float sm[LDS_A > LDS_C ? LDS_A : LDS_C];
   const int tiles_x = SW / T;
@@ -1698,17 +1700,14 @@ __global__ __launch_bounds__(256) void up_last_mfma_kernel(const float* __restri
       }
       *(f4*)(sm + r * LDA + q4) = v;
     }
-    // B fragments: lane (i, g) of MFMA j in K chunk c holds B[k = a0 + 16c + 4g + j][col = 16t + i], col = tap * CO + co
+    // B fragments: lane (i, g) of MFMA j in K chunk c holds B[k = a0 + 16c + 4g + j][col = 16t + i]: channel t, tap i
     float b[2][CO][4];
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int t = 0; t < CO; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = 16 * t + i, tap = col / CO, co = col - tap * CO;
-          b[c][t][j] = W[((size_t)(a0 + 16 * c + 4 * g + j) * CO + co) * 16 + tap];
-        }
+        for (int j = 0; j < 4; ++j) b[c][t][j] = W[((size_t)(a0 + 16 * c + 4 * g + j) * CO + t) * 16 + i];
     __syncthreads();
 #pragma unroll
     for (int m = 0; m < MPW; ++m) {
@@ -1726,24 +1725,22 @@ __global__ __launch_bounds__(256) void up_last_mfma_kernel(const float* __restri
       }
     }
   }
-  __syncthreads();  // every wave's A reads are done: C overwrites the window
-#pragma unroll
-  for (int m = 0; m < MPW; ++m) {
-    const int mt = w + 4 * m;
-    if (mt < MT) {
-#pragma unroll
-      for (int t = 0; t < CO; ++t)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) sm[(mt * 16 + 4 * g + e) * LDC + 16 * t + i] = acc[m][t][e];
-    }
-  }
-  __syncthreads();
-  // col2im: thread = small pixel (u, v); output (2u + cy, 2v + cx) sums taps (1 - cy + 2th, 1 - cx + 2tw) of the
-  // small pixels (u + cy - th, v + cx - tw), th, tw in {0, 1}
+  // col2im per output channel: thread = small pixel (u, v); output (2u + cy, 2v + cx) sums taps (1 - cy + 2th,
+  // 1 - cx + 2tw) of the small pixels (u + cy - th, v + cx - tw), th, tw in {0, 1}
   const int u = threadIdx.x >> 4, v = threadIdx.x & 15;
   const int LH = 2 * SH, LW = 2 * SW;
 #pragma unroll
   for (int co = 0; co < CO; ++co) {
+    __syncthreads();  // every wave's A reads (co = 0) / the previous channel's col2im reads are done
+#pragma unroll
+    for (int m = 0; m < MPW; ++m) {
+      const int mt = w + 4 * m;
+      if (mt < MT) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sm[(mt * 16 + 4 * g + e) * LDC + i] = acc[m][co][e];
+      }
+    }
+    __syncthreads();
     const float bb = (bias ? bias[co] : 0.f) + c0;
 #pragma unroll
     for (int cy = 0; cy < 2; ++cy) {
@@ -1757,7 +1754,7 @@ __global__ __launch_bounds__(256) void up_last_mfma_kernel(const float* __restri
           for (int tw = 0; tw < 2; ++tw) {
             const int r = (u + cy - th + 1) * TH + (v + cx - tw + 1);
             const int tap = (1 - cy + 2 * th) * 4 + (1 - cx + 2 * tw);
-            s += sm[r * LDC + tap * CO + co];
+            s += sm[r * LDC + tap];
           }
         o[cx] = s;
       }
