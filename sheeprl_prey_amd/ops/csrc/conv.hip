@@ -575,8 +575,14 @@ struct EpiPlain : EpiPlainP {  // out = acc + bias[c] + c0 for c < Nreal; NHWC (
 // Tile BM x BN, WM x WN waves of (TM*32) x (TN*32); 64*WM*WN threads; one LDS stage + register
 // prefetch of the next stage (a double-buffered form with one barrier per stage measured no gain:
 // profiles/r4_conv_ab.md, profiles/r4_conv_db_wide.md; removed).
+// Waves per SIMD the register allocation targets: 3 for the 4-wave 32 / 64 / 128-column tiles (<= 168 VGPRs, no
+// spill: three workgroups per CU overlap one another's prologue / epilogue; Atari-100k stack -1 %), the compiler's
+// default (2) elsewhere - the 96 / 192 / 384-column XL tiles miss the target and slow down 2-40 % when forced.
+constexpr int igemm_min_waves(int BN, int WM, int WN) { return (WM * WN == 4 && (BN == 32 || BN == 64 || BN == 128)) ? 3 : 1; }
+
 template <int BM, int BN, int WM, int WN, class LA, class LB, class EP, class RM>
-__global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep, RM rm, int K, int ncls, int remap) {
+__global__ __launch_bounds__(64 * WM * WN, igemm_min_waves(BN, WM, WN)) void igemm_kernel(LA la, LB lb, EP ep, RM rm, int K,
+                                                                                         int ncls, int remap) {
   constexpr int NTH = 64 * WM * WN, TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(TM >= 1 && TN >= 1 && TM * WM * 32 == BM && TN * WN * 32 == BN, "bad tile");
   constexpr int LDS_MAIN = (BM + BN) * LDK;
@@ -647,8 +653,9 @@ __global__ __launch_bounds__(64 * WM* WN) void igemm_kernel(LA la, LB lb, EP ep,
 }
 
 // WGRAD: rows a (Ca), cols (tap,b) (16 Cb), K = pixel range of split blockIdx.z; writes the partial slab.
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(64 * WM* WN) void wgrad_kernel(WgP<BM, 64 * WM * WN> la, WgQ<BN, 64 * WM * WN> lb,
+// MINW: waves per SIMD targeted by the register allocation (3 = the short-K form, see wgrad_cfg)
+template <int BM, int BN, int WM, int WN, int MINW = 1>
+__global__ __launch_bounds__(64 * WM * WN, MINW) void wgrad_kernel(WgP<BM, 64 * WM * WN> la, WgQ<BN, 64 * WM * WN> lb,
                                                               float* slab, int ldn, int Mrows, int kper, int remap) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   __shared__ float lds[(BM + BN) * LDK];
@@ -1284,6 +1291,14 @@ static void wgrad_cfg(const float* P, const float* Q, float* slab, int S, int kp
   dim3 grid(Ca / BM, 16 * Cbp / BN, S);
   // XCD-ordered splits (profiles/r4_wgrad_remap_{on,off}.txt: Atari layers 1.165 -> 1.126 ms)
   const int remap = (grid.x * grid.y * grid.z) % 8 == 0;
+  // few 128 x 128 tiles (<= 32) with short K splits (<= 2048 pixels: the Atari-100k layers) as 3 waves per SIMD
+  // (<= 168 VGPRs, no spill: 148-152 vs 155-157 us per launch); the XL layers (72-288 tiles) keep 2 (3 measured +3.4 %)
+  if constexpr (BM == 128 && BN == 128 && WM * WN == 4) {
+    if (kper <= 2048 && grid.x * grid.y <= 32) {
+      hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, 3>), grid, dim3(NTH), 0, st, la, lb, slab, 16 * Cbp, Ca, kper, remap);
+      return;
+    }
+  }
   hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN>), grid, dim3(NTH), 0, st, la, lb, slab, 16 * Cbp, Ca, kper, remap);
 }
 
