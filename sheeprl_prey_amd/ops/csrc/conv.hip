@@ -17,7 +17,8 @@
 //
 // Epilogues fuse the channel LayerNorm: the workgroup tile spans the whole channel row (N <= 256), so
 //   LN_ACT : z = acc; y = act(LN(z)) (+ per-pixel mean/rstd)        (forward of conv -> LN -> act)
-//   LN_BWD : acc = dy of the NEXT-lower layer's output; dz = LN/act backward, dgamma/dbeta atomics
+//   LN_BWD : acc = dy of the NEXT-lower layer's output; dz = LN/act backward, dgamma/dbeta as per-workgroup
+//            column-sum rows reduced in a fixed order afterwards (deterministic; float atomics only without a buffer)
 //   PLAIN  : out = acc + bias + c0, NHWC or NCHW (for the 3-channel image / the flat Linear seam)
 // Spatial sizes are powers of two; channel counts are multiples of 32 up to 1024 (the 4-channel image
 // side: a power of two below 32); all host-checked.
