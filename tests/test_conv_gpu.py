@@ -185,3 +185,15 @@ def test_stack_grads_are_bitwise_reproducible(monkeypatch):
     diff = [k for k in runs[0][3] if not torch.equal(runs[0][3][k], runs[1][3][k])]
     assert not diff, f"gradients differ run to run: {diff}"
     assert torch.equal(runs[0][2], runs[1][2])
+
+
+@pytest.mark.parametrize("n,c,hw", [(5, 3, 64), (3, 1, 64), (2, 3, 6), (4, 4, 16)])
+def test_to_nhwc4_uint8_matches_permute(n, c, hw):
+    """The encoder input conversion: uint8 NCHW frames -> NHWC4 f32 scaled by 1/255 (channels past C zero); the
+    4-pixel form (HW % 4 == 0) and the per-pixel form (HW = 36)."""
+    C = ops._ext()
+    x = torch.randint(0, 256, (n, c, hw, hw), dtype=torch.uint8, device=DEV)
+    out = C.conv_to_nhwc4(x, 1.0 / 255.0)
+    ref = torch.zeros(n, hw, hw, 4, device=DEV)
+    ref[..., :c] = x.permute(0, 2, 3, 1).float() * (1.0 / 255.0)
+    torch.testing.assert_close(out, ref, rtol=0, atol=1e-7)
