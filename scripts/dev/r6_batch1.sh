@@ -2,7 +2,7 @@
 # Round-6 measurement batch: kernel tests of the changed ops, prey step time, the default bench x2, the player-gap probe,
 # the continuous bench + trace.  Every GPU step has its own time limit; a failed test step stops the batch.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_onehot_gpu.py tests/test_conv_gpu.py tests/test_prior_head_gpu.py tests/test_dreamer_gpu.py tests/test_dv3_step_oracle_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/b1_tests.log 2>&1 || { tail -30 gpurun_out/b1_tests.log; exit 1; }

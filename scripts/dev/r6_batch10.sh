@@ -2,7 +2,7 @@
 # Round-6 batch 10: wm-phase time (hipEvents, --phase-times) with the deferred weight-gradient branch enqueued after
 # (default) vs before the persistent scan backward
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 for i in 1 2; do

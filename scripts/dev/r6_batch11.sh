@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 batch 11: reference (serial) vs pipelined order of effects in the interaction step, 3 alternating pairs
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 for i in 1 2 3; do

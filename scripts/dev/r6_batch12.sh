@@ -2,7 +2,7 @@
 # Round-6 batch 12: one-launch prior head (default) vs LayerNorm + library GEMM + sampler (SRL_PRIOR_HEAD=0) in the
 # imagination rollout: bench pairs + imagine-phase time
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 for i in 1 2; do

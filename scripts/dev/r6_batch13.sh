@@ -2,7 +2,7 @@
 # Round-6 batch 13: the 512 x 512 head weight gradients over 16k imagined rows through the split-K kernel (tiles <= 32,
 # default) vs the library GEMM + column sum (SRL_WGRAD_MAX_TILES=15): bench pairs + actor / critic phase times
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 for i in 1 2; do

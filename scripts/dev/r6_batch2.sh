@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 measurement batch 2: the player-gap probe, the continuous bench + kernel trace (with a one-step dump).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python scripts/player_after_train.py > gpurun_out/b2_player.log 2>&1; grep player gpurun_out/b2_player.log || tail -5 gpurun_out/b2_player.log

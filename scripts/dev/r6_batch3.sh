@@ -2,7 +2,7 @@
 # Round-6 batch 3: fused player draws (discrete tail / truncated-normal head) - tests, the benches, the player probe,
 # and the ATen small-op call sites of one eager step (SRL_PROFILE_SITES).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_actor_tail_gpu.py tests/test_imagine_cont_gpu.py tests/test_dreamer_gpu.py tests/test_algos_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/b3_tests.log 2>&1 || { tail -30 gpurun_out/b3_tests.log; exit 1; }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 batch 4: XL conv roofline, XL bench, XL kernel trace.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 MULT=96 bash scripts/conv_roofline.sh > gpurun_out/b4_roof.txt 2>&1; cp gpurun_out/conv_roofline.md gpurun_out/b4_conv_roofline_xl.md; tail -3 gpurun_out/b4_roof.txt

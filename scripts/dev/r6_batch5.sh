@@ -2,7 +2,7 @@
 # Round-6 batch 5: 32-channel conv tile variants (SRL_CONV_T32 = 0..3): correctness (conv stack tests) and the
 # per-launch roofline of each, then the bench with each.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 for v in 1 2 3; do

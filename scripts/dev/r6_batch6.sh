@@ -2,7 +2,7 @@
 # Round-6 batch 6: host-side breakdown of the interaction step (SRL_HOST_TIMES) for the Atari and the continuous bench,
 # serial (reference) vs pipelined effect order, and a one-step kernel dump of the continuous bench at HEAD.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 for so in True False; do

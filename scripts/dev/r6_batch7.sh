@@ -2,7 +2,7 @@
 # Round-6 batch 7: drain the gradient step before enqueuing the player (SRL_DRAIN_BEFORE_PLAYER=1, default) vs not (0):
 # Atari and continuous benches alternating, then a one-step kernel dump of the continuous bench with the drain.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 for i in 1 2; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 batch 8: runtime knobs vs the player bursts after the gradient step (continuous bench, then Atari)
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 run() {  # tag env...

@@ -2,7 +2,7 @@
 # Round-6 batch 9: the deferred weight-gradient branch enqueued before vs after the persistent scan backward, with
 # head delays (bench; the scan-health check at the end of bench.py fails the run if the scan was starved)
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 run() {  # tag env...

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 final numbers of the secondary benches at HEAD (one run each)
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export PYTHONPATH=. TMPDIR=/tmp
 mkdir -p gpurun_out
 run() {  # tag args...
