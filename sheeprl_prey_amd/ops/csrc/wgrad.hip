@@ -543,8 +543,20 @@ __global__ void __launch_bounds__(256) reduce_kernel(const float* __restrict__ p
   if ((K & 3) == 0 && (ldo & 3) == 0 && (coff & 3) == 0) {
     const long i4 = i * 4;
     if (i4 >= total) return;
+    // the S chunk partials summed in chunk order (deterministic); 8 loads issued before their adds so the chunk loads
+    // are in flight together (the one-at-a-time loop waited a full memory latency per chunk: 19.5 us at 32 x 512 x 512)
     float4 a = reinterpret_cast<const float4*>(part + i4)[0];
-    for (int s = 1; s < S; ++s) {
+    int s = 1;
+    for (; s + 8 <= S; s += 8) {
+      float4 b[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b[j] = reinterpret_cast<const float4*>(part + (long)(s + j) * total + i4)[0];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a.x += b[j].x; a.y += b[j].y; a.z += b[j].z; a.w += b[j].w;
+      }
+    }
+    for (; s < S; ++s) {
       const float4 b = reinterpret_cast<const float4*>(part + (long)s * total + i4)[0];
       a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
     }
@@ -559,7 +571,15 @@ __global__ void __launch_bounds__(256) reduce_kernel(const float* __restrict__ p
   }
   if (i >= total) return;
   float a = part[i];
-  for (int s = 1; s < S; ++s) a += part[(long)s * total + i];
+  int s = 1;
+  for (; s + 8 <= S; s += 8) {
+    float b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) b[j] = part[(long)(s + j) * total + i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a += b[j];
+  }
+  for (; s < S; ++s) a += part[(long)s * total + i];
   const long n = i / K, k = i - n * K;
   float* o = out + n * ldo + coff + k;
   *o = accumulate ? *o + a : a;
