@@ -739,8 +739,17 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   if (idx < tot) {
     const f4* src = (const f4*)(slab + idx);
     const size_t stride = (size_t)tot / 4;
-#pragma unroll 4
-    for (int k = grp; k < S; k += 16) acc += src[k * stride];
+    // splits summed in split order; 8 loads issued before their adds (the single-tile layers run S = 1024
+    // splits through 32 workgroups: 64 splits per thread, one memory latency per batch instead of per load)
+    int k = grp;
+    for (; k + 7 * 16 < S; k += 8 * 16) {
+      f4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(k + 16 * u) * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; k < S; k += 16) acc += src[(size_t)k * stride];
   }
   part[grp][col] = acc;
   __syncthreads();
