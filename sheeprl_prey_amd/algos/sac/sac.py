@@ -425,8 +425,12 @@ def run_sac_family(runner, cfg: Dict[str, Any], variant: str = "sac"):
     obs_dim = int(sum(int(np.prod(obs_space[k].shape)) for k in cfg.mlp_keys.encoder))
 
     droq = variant == "droq"
-    agent = build_agent(runner, cfg, obs_dim, action_space, state["agent"] if state else None,
-                        dropout=float(cfg.algo.critic.get("dropout", 0.0)) if droq else 0.0, layer_norm=droq)
+    if droq:
+        from sheeprl_prey_amd.algos.droq.agent import build_agent as build_droq_agent
+
+        agent = build_droq_agent(runner, cfg, obs_dim, action_space, state["agent"] if state else None)
+    else:
+        agent = build_agent(runner, cfg, obs_dim, action_space, state["agent"] if state else None)
     qf_optimizer = build_optimizer(cfg.algo.critic.optimizer, agent.critic.parameters())
     actor_optimizer = build_optimizer(cfg.algo.actor.optimizer, agent.actor.parameters())
     alpha_optimizer = build_optimizer(cfg.algo.alpha.optimizer, [agent.log_alpha])
