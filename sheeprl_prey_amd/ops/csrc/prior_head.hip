@@ -59,6 +59,32 @@ __device__ __forceinline__ float row16_last(float v) {
   return r == 0 ? a : (r == 1 ? b : (r == 2 ? c : d));
 }
 
+// LayerNorm + act of one LDS row of K = 64 KV with this lane's gamma / beta columns (s + 64 m) already in registers
+// (scan_dev.h wave_ln_act_row reads them from global memory after the row reductions: one more memory latency per
+// row on the kernel's serial prologue); same arithmetic
+template <int KV, int ACTC>
+__device__ __forceinline__ void ln_act_row_regs(float* r, int N, float eps, const float (&gm)[KV], const float (&bt)[KV],
+                                                int act, float& mu, float& rs) {
+  const int s = threadIdx.x & 63;  // N = 64 KV (runtime value: the same division as wave_ln_act_row)
+  float v[KV];
+  float a = 0.f;
+#pragma unroll
+  for (int m = 0; m < KV; ++m) {
+    v[m] = r[s + 64 * m];
+    a += v[m];
+  }
+  mu = wave_sum_dpp(a) / N;
+  float q = 0.f;
+#pragma unroll
+  for (int m = 0; m < KV; ++m) {
+    const float d = v[m] - mu;
+    q += d * d;
+  }
+  rs = rsqrtf(wave_sum_dpp(q) / N + eps);
+#pragma unroll
+  for (int m = 0; m < KV; ++m) r[s + 64 * m] = scandev::f_act_c<ACTC>((v[m] - mu) * rs * gm[m] + bt[m], act);
+}
+
 template <int KV>
 __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
   extern __shared__ float sm[];
@@ -80,16 +106,37 @@ __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
     cb1[q] = *(const f4*)(wr1 + 16 * q);
   }
   const float bb0 = p.b ? p.b[n0 + i] : 0.f, bb1 = p.b ? p.b[n0 + 16 + i] : 0.f;
-  // 16 x K row tile -> LDS (rows past M zero), then LayerNorm + act in place (two rows per wave)
-  const int c4 = p.K >> 2;
-  for (int e = threadIdx.x; e < 16 * c4; e += NT) {
-    const int r = e / c4, k = (e - r * c4) << 2;
-    *(f4*)(sm + r * lda + k) = r < nrow ? *(const f4*)(p.x + (long)(r0 + r) * p.ldx + k) : f4{0.f, 0.f, 0.f, 0.f};
+  // everything else the prologue and the sampler read from global memory is requested here too, so the serial
+  // part of the kernel (stage -> LayerNorm -> K loop -> sample) waits on one memory latency, not one per use:
+  // the LN parameters of this lane's columns and the uniforms of this lane's four (row, categorical) draws
+  float gm[KV], bt[KV];
+#pragma unroll
+  for (int m = 0; m < KV; ++m) {
+    gm[m] = p.gamma[lane + 64 * m];
+    bt[m] = p.beta[lane + 64 * m];
+  }
+  float un[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) un[r] = 4 * g + r < nrow ? p.uni[(long)(r0 + 4 * g + r) * G + gg] : 0.f;
+  // 16 x K row tile -> LDS (rows past M zero; all of a thread's loads in flight together), then LayerNorm + act in
+  // place (two rows per wave)
+  constexpr int C4 = 16 * KV, PER = 16 * C4 / NT;  // K / 4 float4 per row; float4 per thread
+  static_assert(PER * NT == 16 * C4, "row tile per thread");
+  f4 xv[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = threadIdx.x + j * NT, r = e / C4, k = (e - r * C4) << 2;
+    xv[j] = r < nrow ? *(const f4*)(p.x + (long)(r0 + r) * p.ldx + k) : f4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = threadIdx.x + j * NT, r = e / C4, k = (e - r * C4) << 2;
+    *(f4*)(sm + r * lda + k) = xv[j];
   }
   __syncthreads();
   for (int r = w; r < 16; r += NT / 64) {
     float mu, rs;
-    scandev::wave_ln_act_row<KV>(sm + r * lda, p.K, p.eps, p.gamma, p.beta, p.act, mu, rs);
+    SRL_ACT_SPECIALIZE(p.act, (ln_act_row_regs<KV, ACTC>(sm + r * lda, p.K, p.eps, gm, bt, p.act, mu, rs)));
     if (p.mean_out != nullptr && blockIdx.y == 0 && lane == 0 && r < nrow) {
       p.mean_out[r0 + r] = mu;
       p.rstd_out[r0 + r] = rs;
@@ -160,8 +207,7 @@ __global__ void __launch_bounds__(NT) prior_head_kernel(HP p) {
     const float cdf0 = row16_scan(e0 / s2);
     const float cdf1 = row16_last(cdf0) + row16_scan(e1 / s2);
     const float cmax = row16_last(cdf1);
-    const float u = row < nrow ? p.uni[(long)(r0 + row) * G + gg] : 0.f;
-    const float thr = u * cmax;
+    const float thr = un[r] * cmax;
     int pick = (int)row16_sum((cdf0 < thr ? 1.f : 0.f) + (cdf1 < thr ? 1.f : 0.f));
     if (pick > CL - 1) pick = CL - 1;
     if (row < nrow) {
