@@ -51,6 +51,17 @@ __global__ void __launch_bounds__(256) tail_kernel(TP p) {
 #pragma unroll
     for (int k = 0; k < NV4; ++k) wv[a][k] = wr[min(lane + 64 * k, N4 - 1)];
   }
+  // the LayerNorm parameters, this lane's head bias and the row's uniform: requested here too, so the row statistics,
+  // the head and the draw below wait on no further memory latency
+  float4 gv[NV4], bv4[NV4];
+#pragma unroll
+  for (int k = 0; k < NV4; ++k) {
+    const int i4 = min(lane + 64 * k, N4 - 1);
+    gv[k] = p.gamma ? reinterpret_cast<const float4*>(p.gamma)[i4] : make_float4(1.f, 1.f, 1.f, 1.f);
+    bv4[k] = p.beta ? reinterpret_cast<const float4*>(p.beta)[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float bhl = (p.bh && lane < p.A) ? p.bh[lane] : 0.f;
+  const float ur = p.uniform != nullptr ? p.uniform[r] : 0.f;
   const float4* xr = reinterpret_cast<const float4*>(p.pre + (long)r * p.ldp);
   float4 v[NV4];
   float s = 0.f;
@@ -75,8 +86,7 @@ __global__ void __launch_bounds__(256) tail_kernel(TP p) {
   for (int k = 0; k < NV4; ++k) {
     const int i4 = lane + 64 * k;
     if (i4 < N4) {
-      const float4 g = p.gamma ? reinterpret_cast<const float4*>(p.gamma)[i4] : make_float4(1.f, 1.f, 1.f, 1.f);
-      const float4 b = p.beta ? reinterpret_cast<const float4*>(p.beta)[i4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 g = gv[k], b = bv4[k];
       float4 o;
       o.x = act_fwd_c<ACTC>((v[k].x - mu) * rs * g.x + b.x, p.act);
       o.y = act_fwd_c<ACTC>((v[k].y - mu) * rs * g.y + b.y, p.act);
@@ -103,7 +113,7 @@ __global__ void __launch_bounds__(256) tail_kernel(TP p) {
           d += (v[k].x * w.x + v[k].y * w.y) + (v[k].z * w.z + v[k].w * w.w);
         }
       }
-      const float l = wave_sum_dpp(d) + (p.bh ? p.bh[a] : 0.f);
+      const float l = wave_sum_dpp(d) + bhl;  // lane a: + bh[a]
       if (lane == a) la = l;
     }
   }
@@ -128,7 +138,7 @@ __global__ void __launch_bounds__(256) tail_kernel(TP p) {
   int pick;
   if (p.uniform != nullptr) {
     const float cdf = row16_scan(pr);
-    const float u = p.uniform[r];
+    const float u = ur;
     const float cmax = seg_max_f(cdf, W);
     const float below = (valid && cdf < u * cmax) ? 1.f : 0.f;
     pick = (int)seg_sum_f(below, W);

@@ -20,9 +20,27 @@ __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* x, const f
                                                          int ldo, const float* __restrict__ x2, int ldx2, float* xsum) {
   __shared__ float red[4];
   const int T = 256, N = 3 * H;
+  // LayerNorm parameters (and, per row, h) requested before the row loads: used after the two block reductions,
+  // they no longer add a memory latency there
+  float gm[3][MAXH], bt[3][MAXH];
+#pragma unroll
+  for (int k = 0; k < MAXH; ++k) {
+    const int j = threadIdx.x + k * T;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      gm[g][k] = j < H ? gamma[g * H + j] : 0.f;
+      bt[g][k] = j < H ? beta[g * H + j] : 0.f;
+    }
+  }
   for (int row = blockIdx.x; row < M; row += gridDim.x) {
     const float* xr = x + (int64_t)row * N;
     const float* x2r = x2 ? x2 + (int64_t)row * ldx2 : nullptr;  // optional second GEMM part (row-strided)
+    float hp[MAXH];
+#pragma unroll
+    for (int k = 0; k < MAXH; ++k) {
+      const int j = threadIdx.x + k * T;
+      hp[k] = j < H ? h[(int64_t)row * ldh + j] : 0.f;
+    }
     float v[3][MAXH];
     float s = 0.f;
 #pragma unroll
@@ -51,14 +69,13 @@ __global__ void __launch_bounds__(256) ln_gru_fwd_kernel(const float* x, const f
     for (int k = 0; k < MAXH; ++k) {
       int j = threadIdx.x + k * T;
       if (j < H) {
-        float zr = (v[0][k] - mu) * rs * gamma[j] + beta[j];
-        float zc = (v[1][k] - mu) * rs * gamma[H + j] + beta[H + j];
-        float zu = (v[2][k] - mu) * rs * gamma[2 * H + j] + beta[2 * H + j];
+        float zr = (v[0][k] - mu) * rs * gm[0][k] + bt[0][k];
+        float zc = (v[1][k] - mu) * rs * gm[1][k] + bt[1][k];
+        float zu = (v[2][k] - mu) * rs * gm[2][k] + bt[2][k];
         float r = sigmoidf_(zr);
         float c = tanhf(r * zc);
         float u = sigmoidf_(zu - 1.f);
-        float hp = h[(int64_t)row * ldh + j];
-        hn[(int64_t)row * ldo + j] = u * c + (1.f - u) * hp;
+        hn[(int64_t)row * ldo + j] = u * c + (1.f - u) * hp[k];
       }
     }
     if (threadIdx.x == 0) {

@@ -41,19 +41,16 @@ __global__ void __launch_bounds__(256) onehot_index_kernel(const float* __restri
 }
 
 // y = act(LN(acc)) for one wave's float4 columns c4 + lane + 64 v (ACTC: common.h SRL_ACT_SPECIALIZE)
+// (gp / bp: this lane's LayerNorm parameters, loaded in the kernel prologue)
 template <int NV4, int ACTC>
 __device__ __forceinline__ void store_rows(const f4 (&acc)[NV4], int c4, int lane, int N4, int ln, float mu, float rs,
-                                           const float* gamma, const float* beta, int act, float* yrow) {
+                                           const f4 (&gp)[NV4], const f4 (&bp)[NV4], int act, float* yrow) {
 #pragma unroll
   for (int v = 0; v < NV4; ++v) {
     const int i4 = c4 + lane + 64 * v;
     if (i4 < N4) {
       f4 o = acc[v];
-      if (ln) {
-        const f4 g = gamma ? reinterpret_cast<const f4*>(gamma)[i4] : f4{1.f, 1.f, 1.f, 1.f};
-        const f4 b = beta ? reinterpret_cast<const f4*>(beta)[i4] : zero4();
-        o = (o - mu) * rs * g + b;
-      }
+      if (ln) o = (o - mu) * rs * gp[v] + bp[v];
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = act_fwd_c<ACTC>(o[e], act);
       reinterpret_cast<f4*>(yrow)[i4] = o;
@@ -78,10 +75,15 @@ __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
   const int r = blockIdx.x * (4 / WPR) + wave / WPR;
   const bool live = r < M;  // (no early return: the WPR = 2 row reduction joins the block)
   const int N4 = N >> 2, c4 = part * 64 * NV4;
-  f4 acc[NV4];
+  f4 acc[NV4], gp[NV4], bp[NV4];
 #pragma unroll
   for (int v = 0; v < NV4; ++v) {
     const int i4 = c4 + lane + 64 * v;
+    // the LayerNorm parameters are requested with the first loads: used only after the gathers and the row
+    // reductions, they no longer add a memory latency at the end of the kernel
+    const bool pv = ln && live && i4 < N4;
+    gp[v] = (pv && gamma) ? reinterpret_cast<const f4*>(gamma)[i4] : f4{1.f, 1.f, 1.f, 1.f};
+    bp[v] = (pv && beta) ? reinterpret_cast<const f4*>(beta)[i4] : zero4();
     acc[v] = (live && Y != nullptr && i4 < N4) ? reinterpret_cast<const f4*>(Y + (int64_t)r * ldy)[i4] : zero4();
     if (live && bias != nullptr && i4 < N4) acc[v] += reinterpret_cast<const f4*>(bias)[i4];
   }
@@ -170,7 +172,7 @@ __global__ void __launch_bounds__(256) onehot_gather_ln_kernel(
     }
   }
   if (!live) return;
-  SRL_ACT_SPECIALIZE(act, store_rows<NV4, ACTC>(acc, c4, lane, N4, ln, mu, rs, gamma, beta, act, y_out + (int64_t)r * ldo));
+  SRL_ACT_SPECIALIZE(act, store_rows<NV4, ACTC>(acc, c4, lane, N4, ln, mu, rs, gp, bp, act, y_out + (int64_t)r * ldo));
 }
 
 }  // namespace onehot
