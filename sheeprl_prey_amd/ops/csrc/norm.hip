@@ -524,8 +524,33 @@ __global__ void __launch_bounds__(256) colsum_t_kernel(const float* __restrict__
   const int j0 = (int)((int64_t)Rg * s / S), j1 = (int)((int64_t)Rg * (s + 1) / S);
   float a = 0.f, b = 0.f;
   if (n < N) {
-#pragma unroll 4
-    for (int j = j0 + slice; j < j1; j += 4) {
+    // rows summed in row order; 8 rows' loads issued before their adds (one memory latency per 8 rows, not per 2)
+    int j = j0 + slice;
+    if (pb) {
+      for (; j + 7 * 4 < j1; j += 8 * 4) {
+        float va[8], vb[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int64_t p = (int64_t)g + (int64_t)G * (j + 4 * u);
+          va[u] = pa[p * ld + n];
+          vb[u] = pb[p * ld + n];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          a += va[u];
+          b += vb[u];
+        }
+      }
+    } else {
+      for (; j + 7 * 4 < j1; j += 8 * 4) {
+        float va[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) va[u] = pa[((int64_t)g + (int64_t)G * (j + 4 * u)) * ld + n];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += va[u];
+      }
+    }
+    for (; j < j1; j += 4) {
       const int64_t p = (int64_t)g + (int64_t)G * j;
       a += pa[p * ld + n];
       if (pb) b += pb[p * ld + n];
@@ -558,10 +583,24 @@ __global__ void __launch_bounds__(256) colsum_t_kernel(const float* __restrict__
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only: every read below is sc1
   a = 0.f;
   b = 0.f;
-  if (n < N) {
-    for (int q = slice; q < S; q += 4) {
-      a += __hip_atomic_load(ws + ((int64_t)q * G + g) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (pb) b += __hip_atomic_load(ws + plane + ((int64_t)q * G + g) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (n < N) {  // the S partials summed in order, 8 requested before their adds
+    for (int q0 = slice; q0 < S; q0 += 8 * 4) {
+      float va[8], vb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = q0 + 4 * u;
+        va[u] = q < S ? __hip_atomic_load(ws + ((int64_t)q * G + g) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+        vb[u] = (q < S && pb)
+                    ? __hip_atomic_load(ws + plane + ((int64_t)q * G + g) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (q0 + 4 * u < S) {
+          a += va[u];
+          b += vb[u];
+        }
+      }
     }
   }
   __syncthreads();  // every wave has read its ta / tb out of sa / sb
