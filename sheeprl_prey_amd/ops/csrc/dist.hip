@@ -412,6 +412,12 @@ __global__ void __launch_bounds__(256) twohot_nll_bwd_kernel(const float* __rest
 }
 
 // out[r] = symexp(sum_k softmax(l)_k * bins_k); also stores s = sum p*b for the backward
+// wave max through DPP row reductions + readlanes (max is exact, so the result equals wave_max's)
+__device__ __forceinline__ float wave_max_exact(float v) {
+  v = row16_max(v);
+  return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
+}
+
 template <int MAXK>
 __global__ void __launch_bounds__(256) twohot_mean_fwd_kernel(const float* __restrict__ logits,
                                                               const float* __restrict__ bins, float* __restrict__ out,
@@ -420,15 +426,16 @@ __global__ void __launch_bounds__(256) twohot_mean_fwd_kernel(const float* __res
   const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (r >= R) return;
   const float* lr = logits + (int64_t)r * K;
-  float lv[MAXK];
+  float lv[MAXK], bv[MAXK];  // (the bins requested with the row: no second memory latency after the max)
   float mx = -INFINITY;
 #pragma unroll
   for (int i = 0; i < MAXK; ++i) {
     int k = lane + 64 * i;
     lv[i] = k < K ? lr[k] : -INFINITY;
+    bv[i] = k < K ? bins[k] : 0.f;
     mx = fmaxf(mx, lv[i]);
   }
-  mx = wave_max(mx);
+  mx = wave_max_exact(mx);
   float se = 0.f, sb = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXK; ++i) {
@@ -436,7 +443,7 @@ __global__ void __launch_bounds__(256) twohot_mean_fwd_kernel(const float* __res
     if (k < K) {
       float e = __expf(lv[i] - mx);
       se += e;
-      sb += e * bins[k];
+      sb += e * bv[i];
     }
   }
   se = wave_sum(se);
@@ -457,26 +464,27 @@ __global__ void __launch_bounds__(256) twohot_mean_bwd_kernel(const float* __res
   const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (r >= R) return;
   const float* lr = logits + (int64_t)r * K;
-  float lv[MAXK];
+  float lv[MAXK], bv[MAXK];
   float mx = -INFINITY;
+  const float s = s_in[r], go = gout[r];  // requested with the row (used after the reductions)
 #pragma unroll
   for (int i = 0; i < MAXK; ++i) {
     int k = lane + 64 * i;
     lv[i] = k < K ? lr[k] : -INFINITY;
+    bv[i] = k < K ? bins[k] : 0.f;
     mx = fmaxf(mx, lv[i]);
   }
-  mx = wave_max(mx);
+  mx = wave_max_exact(mx);
   float se = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXK; ++i) se += (lane + 64 * i < K) ? __expf(lv[i] - mx) : 0.f;
   se = wave_sum(se);
-  const float s = s_in[r];
-  const float g = gout[r] * __expf(fabsf(s));
+  const float g = go * __expf(fabsf(s));
   float* dr = dlogits + (int64_t)r * K;
 #pragma unroll
   for (int i = 0; i < MAXK; ++i) {
     int k = lane + 64 * i;
-    if (k < K) dr[k] = g * (__expf(lv[i] - mx) / se) * (bins[k] - s);
+    if (k < K) dr[k] = g * (__expf(lv[i] - mx) / se) * (bv[i] - s);
   }
 }
 
