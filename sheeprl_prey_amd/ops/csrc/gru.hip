@@ -230,9 +230,43 @@ __global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict
   for (int k = 0; k < MAXH; ++k)
 #pragma unroll
     for (int g = 0; g < 3; ++g) ag[g][k] = ab[g][k] = 0.f;
-  for (int row = blockIdx.x; row < M; row += gridDim.x) {
+  // row-invariant LN parameters hoisted; the next row's inputs are requested before this row's math (a block walks
+  // M / grid rows: at M = 15360 one memory latency per row was the kernel's time)
+  float gm[3][MAXH], bt[3][MAXH];
+#pragma unroll
+  for (int k = 0; k < MAXH; ++k) {
+    const int j = threadIdx.x + k * T;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+      gm[g][k] = j < H ? gamma[g * H + j] : 0.f;
+      bt[g][k] = j < H ? beta[g * H + j] : 0.f;
+    }
+  }
+  struct RowIn {
+    float x[3][MAXH], h[MAXH], go[MAXH], ad[MAXH], mu, rs;
+  };
+  auto load = [&](int row, RowIn& in) {
     const float* xr = x + (int64_t)row * N;
-    const float mu = mean[row], rs = rstd[row];
+    in.mu = mean[row];
+    in.rs = rstd[row];
+#pragma unroll
+    for (int k = 0; k < MAXH; ++k) {
+      const int j = threadIdx.x + k * T;
+      const bool ok = j < H;
+#pragma unroll
+      for (int g = 0; g < 3; ++g) in.x[g][k] = ok ? xr[g * H + j] : 0.f;
+      in.h[k] = ok ? h[(int64_t)row * ldh + j] : 0.f;
+      in.go[k] = ok ? dhn[(int64_t)row * H + j] : 0.f;
+      in.ad[k] = (ok && dadd) ? dadd[(int64_t)row * ldadd + j] : 0.f;
+    }
+  };
+  constexpr bool PF = MAXH <= 4;  // (wider rows: no second row of registers, one row at a time as before)
+  RowIn cur, nxt;
+  if (PF && blockIdx.x < M) load(blockIdx.x, cur);
+  for (int row = blockIdx.x; row < M; row += gridDim.x) {
+    if (!PF) load(row, cur);
+    if (PF && row + (int)gridDim.x < M) load(row + gridDim.x, nxt);
+    const float mu = cur.mu, rs = cur.rs;
     float xh[3][MAXH], dxh[3][MAXH];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -241,15 +275,15 @@ __global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict
 #pragma unroll
       for (int g = 0; g < 3; ++g) xh[g][k] = dxh[g][k] = 0.f;
       if (j < H) {
-        float hr = (xr[j] - mu) * rs, hc = (xr[H + j] - mu) * rs, hu = (xr[2 * H + j] - mu) * rs;
-        float gr = gamma[j], gc = gamma[H + j], gu = gamma[2 * H + j];
-        float zr = hr * gr + beta[j], zc = hc * gc + beta[H + j], zu = hu * gu + beta[2 * H + j];
+        float hr = (cur.x[0][k] - mu) * rs, hc = (cur.x[1][k] - mu) * rs, hu = (cur.x[2][k] - mu) * rs;
+        float gr = gm[0][k], gc = gm[1][k], gu = gm[2][k];
+        float zr = hr * gr + bt[0][k], zc = hc * gc + bt[1][k], zu = hu * gu + bt[2][k];
         float r = sigmoidf_(zr);
         float c = tanhf(r * zc);
         float u = sigmoidf_(zu - 1.f);
-        float hp = h[(int64_t)row * ldh + j];
-        float g_out = dhn[(int64_t)row * H + j];
-        dh[(int64_t)row * H + j] = g_out * (1.f - u) + (dadd ? dadd[(int64_t)row * ldadd + j] : 0.f);
+        float hp = cur.h[k];
+        float g_out = cur.go[k];
+        dh[(int64_t)row * H + j] = g_out * (1.f - u) + (dadd ? cur.ad[k] : 0.f);
         float du = g_out * (c - hp);
         float dc = g_out * u;
         float dzu = du * u * (1.f - u);
@@ -279,6 +313,7 @@ __global__ void __launch_bounds__(256) ln_gru_bwd_kernel(const float* __restrict
         for (int g = 0; g < 3; ++g) dxr[g * H + j] = rs * (dxh[g][k] - m1 - xh[g][k] * m2);
       }
     }
+    if (PF) cur = nxt;
   }
 #pragma unroll
   for (int k = 0; k < MAXH; ++k) {
