@@ -143,10 +143,33 @@ __global__ void __launch_bounds__(256) head_linear_sample_fwd(const float* __res
   const int K = 64 * KM, NA = 2 * A;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = blockIdx.x * 4 + wave;  // one row per wave: M / 4 workgroups
-  float v[KM];
+  float v[KM], gv[KM], bv[KM];
 #pragma unroll
   for (int m = 0; m < KM; ++m) v[m] = r < M ? y[(int64_t)r * ldy + lane + 64 * m] : 0.f;  // in flight under the staging
-  for (int i = threadIdx.x; i < NA * K; i += 256) ws[i] = W[i];
+  // everything read after a reduction is requested now: the LN parameters, this lane's head bias, its uniform
+#pragma unroll
+  for (int m = 0; m < KM; ++m) {
+    gv[m] = lng != nullptr ? lng[lane + 64 * m] : 0.f;
+    bv[m] = lng != nullptr ? lnb[lane + 64 * m] : 0.f;
+  }
+  const float bl = (b != nullptr && lane < NA) ? b[lane] : 0.f;
+  const float ul = (r < M && lane < A) ? u[r * A + lane] : 0.f;
+  {  // head weights -> LDS, 8 loads in flight per thread before their stores
+    const int n = NA * K;
+    for (int base = 0; base < n; base += 8 * 256) {
+      float t[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int i = base + q * 256 + threadIdx.x;
+        t[q] = i < n ? W[i] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int i = base + q * 256 + threadIdx.x;
+        if (i < n) ws[i] = t[q];
+      }
+    }
+  }
   if (lng != nullptr && r < M) {
     // y holds the trunk's last pre-activation: its LayerNorm + activation first (the row is in registers), the
     // normalised row and its statistics written out for the trunk backward
@@ -161,7 +184,7 @@ __global__ void __launch_bounds__(256) head_linear_sample_fwd(const float* __res
 #pragma unroll
     for (int m = 0; m < KM; ++m) {
       const int k = lane + 64 * m;
-      v[m] = act_fwd((v[m] - mu) * rs * lng[k] + lnb[k], act);
+      v[m] = act_fwd((v[m] - mu) * rs * gv[m] + bv[m], act);
       yo[(int64_t)r * ldyo + k] = v[m];
     }
     if (lane == 0) {
@@ -177,8 +200,8 @@ __global__ void __launch_bounds__(256) head_linear_sample_fwd(const float* __res
       float s = 0.f;
 #pragma unroll
       for (int m = 0; m < KM; ++m) s += v[m] * ws[j * K + lane + 64 * m];
-      s = wave_sum_dpp(s) + (b ? b[j] : 0.f);
-      if (lane == j) mine = s;
+      s = wave_sum_dpp(s);
+      if (lane == j) mine = s + (b ? bl : 0.f);  // lane j: + b[j]
     }
     if (lane < NA) pre[(int64_t)r * NA + lane] = mine;
     const float ps = __shfl(mine, lane + A, 64);  // the log-std column of action `lane`
@@ -188,7 +211,7 @@ __global__ void __launch_bounds__(256) head_linear_sample_fwd(const float* __res
       const float sg = 1.f / (1.f + __expf(-0.5f * (ps + init_std)));
       const float sc = 2.f * sg + min_std;
       const Trunc t = bounds(l, sc, lo, hi);
-      const float xi = cdf(t.alpha) + u[i] * t.Z;
+      const float xi = cdf(t.alpha) + ul * t.Z;
       loc_out[i] = l;
       scale_out[i] = sc;
       x[(int64_t)r * ldx + lane] = l + sc * (SQRT_2 * erfinvf(2.f * xi - 1.f));
